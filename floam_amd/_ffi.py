@@ -1,0 +1,118 @@
+"""ctypes binding of libfloam_amd.so (the C ABI in include/floam_c.h).
+
+The product path has no CPU fallback: if the HIP library is missing, or no gfx950 device is present, every call
+raises ``FloamError`` loudly.  Loading the library itself needs no GPU (symbol checks run in CPU-only CI).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libfloam_amd.so")
+
+# floam_status (include/floam_c.h)
+OK = 0
+ERR_INVALID_ARGUMENT = 1
+ERR_DEVICE = 2
+ERR_OUT_OF_MEMORY = 3
+ERR_UNSUPPORTED = 4
+ERR_COMM = 5
+WARN_MAP_TOO_SMALL = 100
+WARN_FEW_CORRESPONDENCES = 101
+
+STATUS_NAMES = {0: "OK", 1: "ERR_INVALID_ARGUMENT", 2: "ERR_DEVICE", 3: "ERR_OUT_OF_MEMORY", 4: "ERR_UNSUPPORTED",
+                5: "ERR_COMM", 100: "WARN_MAP_TOO_SMALL", 101: "WARN_FEW_CORRESPONDENCES"}
+
+# every entry point include/floam_c.h declares (checked by tests/test_abi.py)
+EXPORTS = [
+    "floam_cloud_create", "floam_cloud_destroy", "floam_cloud_upload", "floam_cloud_download", "floam_cloud_size",
+    "floam_cloud_clear", "floam_cloud_copy", "floam_cloud_device_ptr",
+    "floam_lp_create", "floam_lp_destroy", "floam_lp_feature_extraction",
+    "floam_odom_create", "floam_odom_destroy", "floam_odom_init_map", "floam_odom_update_selector",
+    "floam_odom_update", "floam_odom_get_pose", "floam_odom_get_last_pose", "floam_odom_get_velocity",
+    "floam_odom_get_map", "floam_odom_get_map_sizes", "floam_odom_download_maps", "floam_odom_get_stats",
+    "floam_comm_unique_id", "floam_odom_set_shard",
+    "floam_last_error", "floam_version", "floam_reset_process_state", "floam_device_synchronize",
+    "floam_profile_enable", "floam_profile_read", "floam_profile_reset",
+]
+
+
+class FloamError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"{STATUS_NAMES.get(status, status)}: {msg}")
+        self.status = status
+
+
+class LidarParams(C.Structure):
+    _fields_ = [("num_lines", C.c_int), ("scan_period", C.c_double), ("vertical_angle", C.c_double),
+                ("max_distance", C.c_double), ("min_distance", C.c_double)]
+
+
+class OdomStats(C.Structure):
+    _fields_ = [("optimization_count", C.c_int), ("solves", C.c_int), ("edge_queries", C.c_int),
+                ("surf_queries", C.c_int), ("edge_correspondences", C.c_int), ("surf_correspondences", C.c_int),
+                ("lm_iterations", C.c_int), ("map_updated", C.c_int), ("corner_map", C.c_size_t),
+                ("surf_map", C.c_size_t), ("final_cost", C.c_double)]
+
+
+class KernelTiming(C.Structure):
+    _fields_ = [("name", C.c_char * 32), ("launches", C.c_longlong), ("total_ms", C.c_double),
+                ("algorithmic_bytes", C.c_double)]
+
+
+_LIB = None
+
+
+def load(path: str | None = None):
+    """Load libfloam_amd.so (raises FileNotFoundError if it has not been built)."""
+    global _LIB
+    if _LIB is not None and path is None:
+        return _LIB
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise FileNotFoundError(f"{p} not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                                "or `make -C floam_amd/csrc`")
+    L = C.CDLL(p)
+    vp, sz, i32, dbl = C.c_void_p, C.c_size_t, C.c_int, C.c_double
+    pp = C.POINTER(C.c_void_p)
+    szp = C.POINTER(C.c_size_t)
+    dp = C.POINTER(C.c_double)
+    sig = {
+        "floam_cloud_create": [i32, sz, pp], "floam_cloud_destroy": [vp],
+        "floam_cloud_upload": [vp, vp, sz, sz], "floam_cloud_download": [vp, vp, sz, szp],
+        "floam_cloud_size": [vp, szp], "floam_cloud_clear": [vp], "floam_cloud_copy": [vp, vp],
+        "floam_lp_create": [C.POINTER(LidarParams), i32, pp], "floam_lp_destroy": [vp],
+        "floam_lp_feature_extraction": [vp, vp, vp, vp],
+        "floam_odom_create": [C.POINTER(LidarParams), dbl, C.c_char_p, i32, pp], "floam_odom_destroy": [vp],
+        "floam_odom_init_map": [vp, vp, vp], "floam_odom_update_selector": [vp, vp, vp, i32],
+        "floam_odom_update": [vp, vp, vp, i32], "floam_odom_get_pose": [vp, dp, dp],
+        "floam_odom_get_last_pose": [vp, dp, dp], "floam_odom_get_velocity": [vp, dp],
+        "floam_odom_get_map": [vp, vp], "floam_odom_get_map_sizes": [vp, szp, szp],
+        "floam_odom_download_maps": [vp, vp, sz, vp, sz], "floam_odom_get_stats": [vp, C.POINTER(OdomStats)],
+        "floam_comm_unique_id": [vp], "floam_odom_set_shard": [vp, i32, i32, vp],
+        "floam_device_synchronize": [i32], "floam_profile_enable": [i32, i32],
+        "floam_profile_read": [i32, C.POINTER(KernelTiming), i32, C.POINTER(C.c_int)], "floam_profile_reset": [i32],
+    }
+    for name, args in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = C.c_int
+    L.floam_cloud_device_ptr.argtypes = [vp]
+    L.floam_cloud_device_ptr.restype = vp
+    L.floam_last_error.argtypes = []
+    L.floam_last_error.restype = C.c_char_p
+    L.floam_version.argtypes = []
+    L.floam_version.restype = C.c_char_p
+    L.floam_reset_process_state.argtypes = []
+    L.floam_reset_process_state.restype = None
+    if path is None:
+        _LIB = L
+    return L
+
+
+def check(status: int, allow_warnings: bool = True) -> int:
+    if status == OK or (allow_warnings and status >= 100):
+        return status
+    msg = load().floam_last_error()
+    raise FloamError(status, msg.decode() if msg else "")

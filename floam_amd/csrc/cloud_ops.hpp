@@ -1,0 +1,63 @@
+#pragma once
+#include "floam_common.hpp"
+
+namespace floam {
+
+// pointAssociateToMap (src/odomEstimationClass.cpp:126-135): Eigen q*v (_transformVector) + t in double, float
+// store.  pose = {qx, qy, qz, qw, tx, ty, tz} (include/odomEstimationClass.h:90-92).
+__device__ __forceinline__ void associate_to_map(const double* __restrict__ pose, float x, float y, float z,
+                                                 float& ox, float& oy, float& oz) {
+  const double qx = pose[0], qy = pose[1], qz = pose[2], qw = pose[3];
+  const double vx = x, vy = y, vz = z;
+  double ux = qy * vz - qz * vy, uy = qz * vx - qx * vz, uz = qx * vy - qy * vx;
+  ux = ux + ux; uy = uy + uy; uz = uz + uz;
+  const double ax = vx + qw * ux, ay = vy + qw * uy, az = vz + qw * uz;
+  const double cx = qy * uz - qz * uy, cy = qz * ux - qx * uz, cz = qx * uy - qy * ux;
+  ox = (float)((ax + cx) + pose[4]);
+  oy = (float)((ay + cy) + pose[5]);
+  oz = (float)((az + cz) + pose[6]);
+}
+
+struct SortScratch {
+  DevBuf<uint32_t> k0, k1;
+  DevBuf<int> v0, v1, flags, pos;
+  DevBuf<char> temp;
+  size_t temp_bytes = 0;
+  void reserve(int n);
+};
+
+struct VoxelScratch {
+  SortScratch s;
+  DevBuf<int> mm;     // 6 ordered-int min/max + mode flag
+};
+
+// out = pcl::VoxelGrid(in[0, *d_n)) with cubic leaf (PCL 1.8.1 semantics, stable within-voxel order).
+// n_ub: host upper bound on *d_n.  Writes *d_out_count.  out must hold n_ub points.
+void voxel_launch(VoxelScratch& sc, const PointRec* in, const int* d_n, int n_ub, float leaf, PointRec* out,
+                  int* d_out_count, hipStream_t st);
+
+// out = pcl::CropBox([old[0,*d_old) ; associate(pose, neu[0,*d_new))], t +- 100) — the map half of
+// addPointsToMap (src/odomEstimationClass.cpp:253-287).  out must hold old_ub + new_ub points.
+void crop_concat_launch(SortScratch& sc, const PointRec* old, const int* d_old, int old_ub, const PointRec* neu,
+                        const int* d_new, int new_ub, const double* d_pose, PointRec* out, int* d_out_count,
+                        hipStream_t st);
+
+// dmapping::CompensateVelocity (src/dataHandler.cpp:82-92), in place
+void compensate_velocity_launch(PointRec* pts, const int* d_n, int n_ub, double vx, double vy, double vz,
+                                hipStream_t st);
+
+// dst[*d_dst_count + i] = src[i] for i < *d_src_count, then *d_dst_count += *d_src_count.
+// xyzi: VelToIntensityCopy semantics (src/odomEstimationClass.cpp:308-318): keep x, y, z, intensity only.
+void append_launch(PointRec* dst, int* d_dst_count, const PointRec* src, const int* d_src_count, int src_ub,
+                   bool xyzi, hipStream_t st);
+
+// ordered-int min/max of x,y,z into d_mm[0..5] (min x,y,z, max x,y,z)
+void minmax_launch(const PointRec* in, const int* d_n, int n_ub, int* d_mm, hipStream_t st);
+
+__device__ __forceinline__ int f2ord(float f) {
+  const int i = __float_as_int(f);
+  return i >= 0 ? i : i ^ 0x7FFFFFFF;
+}
+__device__ __forceinline__ float ord2f(int i) { return __int_as_float(i >= 0 ? i : i ^ 0x7FFFFFFF); }
+
+}  // namespace floam

@@ -1,0 +1,394 @@
+// Feature extraction on gfx950: LaserProcessingClass::featureExtraction (src/laserProcessingClass.cpp:72-231).
+//
+// Kernels (one scan, P points, R rings):
+//   fe_keys    grid over P     range filter + ring key + per-ring histogram            reads 32 B/pt
+//   fe_bucket  one WG / ring   stable bucketing by ring (order-preserving scan)       ring-major float4 xyz + index
+//   fe_sector  one WG / sector curvature stencil, LDS bitonic sort, greedy edge pick, surf compaction
+//   fe_output  one WG / sector gather the 32-B records of edges / surfs to their ring-major, sector-major slots
+// Arithmetic follows the reference bit for bit: float stencil sums in source order, double squares, no FMA
+// contraction (built with -ffp-contract=off).  Sorting is by (value, ring index), which equals the reference's
+// unstable std::sort whenever a sector has no tied curvature values (SURVEY.md §7 "Hard parts").
+#include "floam_common.hpp"
+#include "fe.hpp"
+
+namespace floam {
+
+namespace {
+
+constexpr int kBucketThreads = 1024;
+constexpr int kSectorThreads = 256;
+constexpr int kMaxEdgesPerSector = 20;
+
+__device__ __forceinline__ PointRec make_out(const PointRec& p) {
+  PointRec o;
+  o.x = p.x; o.y = p.y; o.z = p.z; o.pad0 = 1.0f;
+  o.intensity = p.intensity;
+  o.ring = p.ring; o.pad1 = 0;
+  o.time = p.time; o.pad2 = 0.0f;
+  return o;
+}
+
+// RingExtractionVelodyne (src/laserProcessingClass.cpp:11-22): float x*x+y*y, float sqrt, double compare.
+__global__ void fe_keys(const PointRec* __restrict__ in, int n, int num_lines, double min_d, double max_d,
+                        uint16_t* __restrict__ keys, int n_keys_padded, int* __restrict__ ring_count,
+                        int* __restrict__ status) {
+  extern __shared__ int hist[];
+  for (int r = threadIdx.x; r < num_lines; r += blockDim.x) hist[r] = 0;
+  __syncthreads();
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const float2 xy = *reinterpret_cast<const float2*>(&in[i].x);
+    const uint16_t ring = in[i].ring;
+    const float d2 = xy.x * xy.x + xy.y * xy.y;
+    const double d = (double)sqrtf(d2);
+    bool keep = !(d < min_d || d > max_d);
+    if (keep && ring >= num_lines) {   // reference: vector index out of bounds (UB)
+      atomicOr(status, FE_STATUS_BAD_RING);
+      keep = false;
+    }
+    keys[i] = keep ? ring : (uint16_t)0xFFFF;
+    if (keep) atomicAdd(&hist[ring], 1);
+  } else if (i < n_keys_padded) {
+    keys[i] = 0xFFFF;
+  }
+  __syncthreads();
+  for (int r = threadIdx.x; r < num_lines; r += blockDim.x)
+    if (hist[r]) atomicAdd(&ring_count[r], hist[r]);
+}
+
+__device__ __forceinline__ int block_exclusive_scan_1024(int v, int* smem /* >= 32 ints */, int* total) {
+  // wave-level inclusive scan then cross-wave scan; blockDim.x <= 1024, wave = 64
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) smem[wid] = x;
+  __syncthreads();
+  const int nw = (blockDim.x + 63) >> 6;
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int w = 0; w < nw; ++w) {
+      const int t = smem[w];
+      smem[w] = acc;
+      acc += t;
+    }
+    smem[32] = acc;
+  }
+  __syncthreads();
+  const int excl = smem[wid] + x - v;
+  *total = smem[32];
+  __syncthreads();
+  return excl;
+}
+
+__device__ __forceinline__ int ring_offset(const int* ring_count, int r) {
+  int off = 0;
+  for (int k = 0; k < r; ++k) off += ring_count[k];
+  return off;
+}
+
+// Stable ring bucketing: WG r scans the whole key array once to count, once to emit, in input order.
+__global__ __launch_bounds__(kBucketThreads) void fe_bucket(const PointRec* __restrict__ in, int n_padded,
+                                                            const uint16_t* __restrict__ keys,
+                                                            const int* __restrict__ ring_count,
+                                                            int* __restrict__ ring_idx, float4* __restrict__ ring_xyz) {
+  __shared__ int smem[33];
+  __shared__ int s_off;
+  const int r = blockIdx.x;
+  if (threadIdx.x == 0) s_off = ring_offset(ring_count, r);
+  __syncthreads();
+  const int off = s_off;
+  // contiguous segment of 8-key groups per thread
+  const int groups = n_padded >> 3;
+  const int per = (groups + blockDim.x - 1) / blockDim.x;
+  const int g0 = threadIdx.x * per;
+  const int g1 = min(groups, g0 + per);
+  const uint4* k4 = reinterpret_cast<const uint4*>(keys);
+  int c = 0;
+  for (int g = g0; g < g1; ++g) {
+    const uint4 v = k4[g];
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      c += ((w[h] & 0xFFFFu) == (uint32_t)r);
+      c += ((w[h] >> 16) == (uint32_t)r);
+    }
+  }
+  int total;
+  int pos = off + block_exclusive_scan_1024(c, smem, &total);
+  for (int g = g0; g < g1; ++g) {
+    const uint4 v = k4[g];
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int h = 0; h < 8; ++h) {
+      const uint32_t key = (h & 1) ? (w[h >> 1] >> 16) : (w[h >> 1] & 0xFFFFu);
+      if (key == (uint32_t)r) {
+        const int i = g * 8 + h;
+        ring_idx[pos] = i;
+        const PointRec p = in[i];
+        ring_xyz[pos] = make_float4(p.x, p.y, p.z, 0.0f);
+        ++pos;
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void sector_range(int n_r, int s, int& a, int& b) {
+  // src/laserProcessingClass.cpp:103-110: T = n - 10, L = T / 6, [L*s, L*(s+1) - 1), last: [5L, T - 1)
+  const int T = n_r - 10;
+  const int L = T / 6;
+  a = L * s;
+  b = (s == 5) ? T - 1 : L * (s + 1) - 1;
+}
+
+template <int MAXSEC>
+__global__ __launch_bounds__(kSectorThreads) void fe_sector(const int* __restrict__ ring_count,
+                                                            const float4* __restrict__ ring_xyz,
+                                                            int* __restrict__ sec_edge_cnt, int* __restrict__ sec_edge_pos,
+                                                            int* __restrict__ sec_surf_cnt, int* __restrict__ surf_pos,
+                                                            int* __restrict__ status) {
+  constexpr int kPts = MAXSEC + 10;
+  __shared__ unsigned long long s_key[MAXSEC];
+  __shared__ uint16_t s_id[MAXSEC];      // ring index - a - 5 (the curvature entry offset)
+  __shared__ float s_x[kPts], s_y[kPts], s_z[kPts];
+  __shared__ uint8_t s_picked[kPts];
+  __shared__ int s_edges[kMaxEdgesPerSector];
+  __shared__ int s_nedge;
+  __shared__ int smem[33];
+  __shared__ int s_off;
+
+  const int r = blockIdx.x / 6, s = blockIdx.x % 6;
+  const int sec = blockIdx.x;
+  const int n_r = ring_count[r];
+  if (n_r < 131) {                                    // :89
+    if (threadIdx.x == 0) { sec_edge_cnt[sec] = 0; sec_surf_cnt[sec] = 0; }
+    return;
+  }
+  int a, b;
+  sector_range(n_r, s, a, b);
+  const int m = b - a;
+  if (m > MAXSEC) {
+    if (threadIdx.x == 0) {
+      atomicOr(status, FE_STATUS_SECTOR_TOO_LONG);
+      sec_edge_cnt[sec] = 0;
+      sec_surf_cnt[sec] = 0;
+    }
+    return;
+  }
+  if (threadIdx.x == 0) s_off = ring_offset(ring_count, r);
+  __syncthreads();
+  const int off = s_off;
+  // stage ring points [a, b + 10) (= ids a..b+9: stencils of entries a..b-1 and all suppression neighbours)
+  const int npts = m + 10;
+  for (int k = threadIdx.x; k < npts; k += blockDim.x) {
+    const float4 p = ring_xyz[off + a + k];
+    s_x[k] = p.x; s_y[k] = p.y; s_z[k] = p.z;
+    s_picked[k] = 0;
+  }
+  __syncthreads();
+  // curvature (src/laserProcessingClass.cpp:95-101), entry e = a + k, point j = e + 5 -> local k + 5
+  int P2 = 1;
+  while (P2 < m) P2 <<= 1;
+  for (int k = threadIdx.x; k < P2; k += blockDim.x) {
+    if (k < m) {
+      const int c = k + 5;
+      const float fx = s_x[c - 5] + s_x[c - 4] + s_x[c - 3] + s_x[c - 2] + s_x[c - 1] - 10 * s_x[c] + s_x[c + 1] +
+                       s_x[c + 2] + s_x[c + 3] + s_x[c + 4] + s_x[c + 5];
+      const float fy = s_y[c - 5] + s_y[c - 4] + s_y[c - 3] + s_y[c - 2] + s_y[c - 1] - 10 * s_y[c] + s_y[c + 1] +
+                       s_y[c + 2] + s_y[c + 3] + s_y[c + 4] + s_y[c + 5];
+      const float fz = s_z[c - 5] + s_z[c - 4] + s_z[c - 3] + s_z[c - 2] + s_z[c - 1] - 10 * s_z[c] + s_z[c + 1] +
+                       s_z[c + 2] + s_z[c + 3] + s_z[c + 4] + s_z[c + 5];
+      const double dX = fx, dY = fy, dZ = fz;
+      const double v = dX * dX + dY * dY + dZ * dZ;
+      s_key[k] = (unsigned long long)__double_as_longlong(v);   // v >= +0: bit pattern is order-preserving
+      s_id[k] = (uint16_t)k;
+    } else {
+      s_key[k] = ~0ull;
+      s_id[k] = 0xFFFF;
+    }
+  }
+  __syncthreads();
+  // bitonic sort ascending by (key, id)
+  for (int size = 2; size <= P2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = threadIdx.x; t < (P2 >> 1); t += blockDim.x) {
+        const int lo = 2 * t - (t & (stride - 1));
+        const int hi = lo + stride;
+        const bool up = ((lo & size) == 0);
+        const unsigned long long ka = s_key[lo], kb = s_key[hi];
+        const uint16_t ia = s_id[lo], ib = s_id[hi];
+        const bool gt = (ka > kb) || (ka == kb && ia > ib);
+        if (gt == up) {
+          s_key[lo] = kb; s_key[hi] = ka;
+          s_id[lo] = ib; s_id[hi] = ia;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // greedy edge pick (src/laserProcessingClass.cpp:129-170), one lane, LDS only
+  if (threadIdx.x == 0) {
+    int picked_num = 0, nedge = 0;
+    for (int i = m - 1; i >= 0; --i) {
+      const int ind = s_id[i] + 5;                      // local point index
+      if (s_picked[ind]) continue;
+      if (__longlong_as_double((long long)s_key[i]) <= 0.1) break;
+      ++picked_num;
+      s_picked[ind] = 1;
+      if (picked_num <= kMaxEdgesPerSector) {
+        s_edges[nedge++] = ind;
+      } else {
+        break;
+      }
+      for (int k = 1; k <= 5; ++k) {
+        const double dX = s_x[ind + k] - s_x[ind + k - 1];
+        const double dY = s_y[ind + k] - s_y[ind + k - 1];
+        const double dZ = s_z[ind + k] - s_z[ind + k - 1];
+        if (dX * dX + dY * dY + dZ * dZ > 0.05) break;
+        s_picked[ind + k] = 1;
+      }
+      for (int k = -1; k >= -5; --k) {
+        const double dX = s_x[ind + k] - s_x[ind + k + 1];
+        const double dY = s_y[ind + k] - s_y[ind + k + 1];
+        const double dZ = s_z[ind + k] - s_z[ind + k + 1];
+        if (dX * dX + dY * dY + dZ * dZ > 0.05) break;
+        s_picked[ind + k] = 1;
+      }
+    }
+    s_nedge = nedge;
+  }
+  __syncthreads();
+  const int nedge = s_nedge;
+  if (threadIdx.x < nedge) sec_edge_pos[sec * kMaxEdgesPerSector + threadIdx.x] = off + a + s_edges[threadIdx.x];
+  // surf = unpicked entries in ascending order (src/laserProcessingClass.cpp:220-227): contiguous chunk per thread
+  const int per = (m + blockDim.x - 1) / blockDim.x;
+  const int i0 = threadIdx.x * per, i1 = min(m, i0 + per);
+  int c = 0;
+  for (int i = i0; i < i1; ++i) c += !s_picked[s_id[i] + 5];
+  int total;
+  int pos = block_exclusive_scan_1024(c, smem, &total);
+  for (int i = i0; i < i1; ++i) {
+    const int ind = s_id[i] + 5;
+    if (!s_picked[ind]) surf_pos[off + a + pos++] = off + a + ind;
+  }
+  if (threadIdx.x == 0) {
+    sec_edge_cnt[sec] = nedge;
+    sec_surf_cnt[sec] = total;
+  }
+}
+
+__global__ __launch_bounds__(kSectorThreads) void fe_output(const PointRec* __restrict__ in,
+                                                            const int* __restrict__ ring_count,
+                                                            const int* __restrict__ ring_idx,
+                                                            const int* __restrict__ sec_edge_cnt,
+                                                            const int* __restrict__ sec_edge_pos,
+                                                            const int* __restrict__ sec_surf_cnt,
+                                                            const int* __restrict__ surf_pos,
+                                                            PointRec* __restrict__ edge_out, const int* __restrict__ edge_count,
+                                                            PointRec* __restrict__ surf_out, const int* __restrict__ surf_count) {
+  __shared__ int red[2][kSectorThreads / 64];
+  __shared__ int s_off;
+  const int sec = blockIdx.x;
+  const int r = sec / 6, s = sec % 6;
+  int pe = 0, ps = 0;
+  for (int k = threadIdx.x; k < sec; k += blockDim.x) {
+    pe += sec_edge_cnt[k];
+    ps += sec_surf_cnt[k];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    pe += __shfl_down(pe, o, 64);
+    ps += __shfl_down(ps, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = pe;
+    red[1][threadIdx.x >> 6] = ps;
+  }
+  if (threadIdx.x == 0) s_off = ring_offset(ring_count, r);
+  __syncthreads();
+  int edge_prefix = 0, surf_prefix = 0;
+  for (int w = 0; w < kSectorThreads / 64; ++w) {
+    edge_prefix += red[0][w];
+    surf_prefix += red[1][w];
+  }
+  const int ne = sec_edge_cnt[sec], ns = sec_surf_cnt[sec];
+  const int be = edge_count[0] + edge_prefix, bs = surf_count[0] + surf_prefix;
+  if ((int)threadIdx.x < ne) edge_out[be + threadIdx.x] = make_out(in[ring_idx[sec_edge_pos[sec * kMaxEdgesPerSector + threadIdx.x]]]);
+  if (ns > 0) {
+    int a, b;
+    sector_range(ring_count[r], s, a, b);
+    const int base = s_off + a;
+    for (int k = threadIdx.x; k < ns; k += blockDim.x) surf_out[bs + k] = make_out(in[ring_idx[surf_pos[base + k]]]);
+  }
+}
+
+__global__ void fe_commit(int n_sectors, const int* __restrict__ sec_edge_cnt, const int* __restrict__ sec_surf_cnt,
+                          int* __restrict__ edge_count, int* __restrict__ surf_count) {
+  __shared__ int red[2][4];
+  int pe = 0, ps = 0;
+  for (int k = threadIdx.x; k < n_sectors; k += blockDim.x) {
+    pe += sec_edge_cnt[k];
+    ps += sec_surf_cnt[k];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    pe += __shfl_down(pe, o, 64);
+    ps += __shfl_down(ps, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = pe;
+    red[1][threadIdx.x >> 6] = ps;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int te = 0, ts = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) { te += red[0][w]; ts += red[1][w]; }
+    edge_count[0] += te;
+    surf_count[0] += ts;
+  }
+}
+
+}  // namespace
+
+void fe_launch(FeScratch& sc, const FeParams& prm, const PointRec* d_in, int n, PointRec* edge_out,
+               int* edge_count, PointRec* surf_out, int* surf_count, hipStream_t st) {
+  const int R = prm.num_lines;
+  const int n_pad = ((n + 8191) / 8192) * 8192;   // whole uint4 groups for every bucket thread
+  sc.keys.reserve(n_pad);
+  sc.ring_count.reserve(R);
+  sc.ring_idx.reserve(n + 16);
+  sc.ring_xyz.reserve(n + 16);
+  sc.sec_edge_cnt.reserve(6 * R);
+  sc.sec_surf_cnt.reserve(6 * R);
+  sc.sec_edge_pos.reserve(6 * R * kMaxEdgesPerSector);
+  sc.surf_pos.reserve(n + 16);
+  FLOAM_HIP(hipMemsetAsync(sc.ring_count.p, 0, sizeof(int) * R, st));
+  const int tb = 256;
+  hipLaunchKernelGGL(fe_keys, dim3(div_up(n_pad, tb)), dim3(tb), sizeof(int) * R, st, d_in, n, R, prm.min_distance,
+                     prm.max_distance, sc.keys.p, n_pad, sc.ring_count.p, sc.status);
+  FLOAM_LAUNCH_CHECK();
+  hipLaunchKernelGGL(fe_bucket, dim3(R), dim3(kBucketThreads), 0, st, d_in, n_pad, sc.keys.p, sc.ring_count.p,
+                     sc.ring_idx.p, sc.ring_xyz.p);
+  FLOAM_LAUNCH_CHECK();
+  // the longest possible sector is (max ring size - 10) / 6 + 5 <= n / 6 + 5
+  if (n / 6 + 8 <= 1024) {
+    hipLaunchKernelGGL(fe_sector<1024>, dim3(6 * R), dim3(kSectorThreads), 0, st, sc.ring_count.p, sc.ring_xyz.p,
+                       sc.sec_edge_cnt.p, sc.sec_edge_pos.p, sc.sec_surf_cnt.p, sc.surf_pos.p, sc.status);
+  } else {
+    hipLaunchKernelGGL(fe_sector<4096>, dim3(6 * R), dim3(kSectorThreads), 0, st, sc.ring_count.p, sc.ring_xyz.p,
+                       sc.sec_edge_cnt.p, sc.sec_edge_pos.p, sc.sec_surf_cnt.p, sc.surf_pos.p, sc.status);
+  }
+  FLOAM_LAUNCH_CHECK();
+  hipLaunchKernelGGL(fe_output, dim3(6 * R), dim3(kSectorThreads), 0, st, d_in, sc.ring_count.p, sc.ring_idx.p,
+                     sc.sec_edge_cnt.p, sc.sec_edge_pos.p, sc.sec_surf_cnt.p, sc.surf_pos.p, edge_out, edge_count,
+                     surf_out, surf_count);
+  FLOAM_LAUNCH_CHECK();
+  hipLaunchKernelGGL(fe_commit, dim3(1), dim3(256), 0, st, 6 * R, sc.sec_edge_cnt.p, sc.sec_surf_cnt.p, edge_count,
+                     surf_count);
+  FLOAM_LAUNCH_CHECK();
+}
+
+}  // namespace floam

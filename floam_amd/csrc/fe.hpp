@@ -1,0 +1,24 @@
+#pragma once
+#include "floam_common.hpp"
+
+namespace floam {
+
+enum : int { FE_STATUS_BAD_RING = 1, FE_STATUS_SECTOR_TOO_LONG = 2 };
+
+struct FeParams {
+  int num_lines;
+  double min_distance, max_distance;
+};
+
+struct FeScratch {
+  DevBuf<uint16_t> keys;
+  DevBuf<int> ring_count, ring_idx, sec_edge_cnt, sec_surf_cnt, sec_edge_pos, surf_pos;
+  DevBuf<float4> ring_xyz;
+  int* status = nullptr;   // device int, owned by the caller
+};
+
+// Appends edge/surf features of d_in[0, n) to edge_out/surf_out at their device counts (which are advanced).
+void fe_launch(FeScratch& sc, const FeParams& prm, const PointRec* d_in, int n, PointRec* edge_out, int* edge_count,
+               PointRec* surf_out, int* surf_count, hipStream_t st);
+
+}  // namespace floam

@@ -1,0 +1,96 @@
+// Shared host/device definitions of the MI355X-native FLOAM core (gfx950, CDNA4).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+
+#include "../../include/floam_c.h"
+
+namespace floam {
+
+// 32-B record == vel_point::PointXYZIRT (include/lidar.h:14-32) == floam_point.  AoS in HBM for I/O clouds so a
+// pcl::PointCloud's points.data() can be copied without repacking; 16-B aligned so one record is two dwordx4.
+struct alignas(16) PointRec {
+  float x, y, z, pad0;
+  float intensity;
+  uint16_t ring;
+  uint16_t pad1;
+  float time;
+  float pad2;
+};
+static_assert(sizeof(PointRec) == 32, "point record must be 32 B");
+static_assert(sizeof(PointRec) == sizeof(floam_point), "ABI");
+
+// Error carried to the C-ABI as a status + message.
+struct Error : std::runtime_error {
+  floam_status status;
+  Error(floam_status s, const std::string& m) : std::runtime_error(m), status(s) {}
+};
+
+#define FLOAM_HIP(call)                                                                                  \
+  do {                                                                                                   \
+    hipError_t _e = (call);                                                                              \
+    if (_e != hipSuccess)                                                                                \
+      throw ::floam::Error(_e == hipErrorOutOfMemory ? FLOAM_ERR_OUT_OF_MEMORY : FLOAM_ERR_DEVICE,      \
+                           std::string(#call) + ": " + hipGetErrorString(_e) + " @" + __FILE__ + ":" +   \
+                               std::to_string(__LINE__));                                                \
+  } while (0)
+
+#define FLOAM_LAUNCH_CHECK() FLOAM_HIP(hipGetLastError())
+
+inline unsigned div_up(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
+
+// ------------------------------------------------------------------------------------- device buffers
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t cap = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  // grow-only; contents are not preserved
+  void reserve(size_t n) {
+    if (n <= cap) return;
+    release();
+    size_t c = n < 1024 ? 1024 : n + n / 4;
+    FLOAM_HIP(hipMalloc(&p, c * sizeof(T)));
+    cap = c;
+  }
+};
+
+// Pinned host staging
+template <typename T>
+struct HostBuf {
+  T* p = nullptr;
+  size_t cap = 0;
+  ~HostBuf() {
+    if (p) (void)hipHostFree(p);
+  }
+  void reserve(size_t n) {
+    if (n <= cap) return;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    FLOAM_HIP(hipHostMalloc(&p, n * sizeof(T), hipHostMallocDefault));
+    cap = n;
+  }
+};
+
+}  // namespace floam
+
+// Device-resident cloud behind the opaque floam_cloud handle.
+struct floam_cloud {
+  int device = 0;
+  floam::DevBuf<floam::PointRec> pts;
+  floam::DevBuf<int> count;    // count.p[0] = number of points (device-resident)
+  size_t host_count = 0;       // last value the host knows (valid when host_count_valid)
+  bool host_count_valid = true;
+};

@@ -1,0 +1,814 @@
+// Host control of the MI355X-native FLOAM core + the C ABI (include/floam_c.h).
+//
+// floam_lp   = LaserProcessingClass   (include/laserProcessingClass.h:37-50)
+// floam_odom = OdomEstimationClass    (include/odomEstimationClass.h:52-126, src/odomEstimationClass.cpp)
+//
+// All device work of one device is issued on one HIP stream.  Per updatePointsToMap call the host issues a fixed
+// kernel sequence (downsample, [grid rebuild], optimization_count x {lm_init + correspondences, 5 x {LM evaluate,
+// LM control}}) and synchronises once, to read the pose back — the reference exposes `odom` to its caller after
+// every call (src/odomEstimationNode.cpp:242-244).  The keyframe decision and the map update follow on the host
+// / device respectively.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cctype>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "cloud_ops.hpp"
+#include "fe.hpp"
+#include "floam_common.hpp"
+#include "odom_kernels.hpp"
+#include "pose.hpp"
+
+namespace floam {
+
+// ----------------------------------------------------------------------------------------- device context
+struct PendingTiming {
+  std::string name;
+  hipEvent_t e0, e1;
+  double bytes;
+};
+
+struct DeviceCtx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool profile = false;
+  std::vector<PendingTiming> pending;
+  std::vector<hipEvent_t> free_events;
+  std::map<std::string, floam_kernel_timing> totals;
+
+  hipEvent_t get_event() {
+    if (!free_events.empty()) {
+      hipEvent_t e = free_events.back();
+      free_events.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    FLOAM_HIP(hipEventCreate(&e));
+    return e;
+  }
+  void drain() {
+    for (auto& p : pending) {
+      float ms = 0.f;
+      FLOAM_HIP(hipEventSynchronize(p.e1));
+      FLOAM_HIP(hipEventElapsedTime(&ms, p.e0, p.e1));
+      auto& t = totals[p.name];
+      std::strncpy(t.name, p.name.c_str(), sizeof(t.name) - 1);
+      t.launches += 1;
+      t.total_ms += ms;
+      t.algorithmic_bytes += p.bytes;
+      free_events.push_back(p.e0);
+      free_events.push_back(p.e1);
+    }
+    pending.clear();
+  }
+};
+
+static std::mutex g_ctx_mu;
+static std::map<int, std::unique_ptr<DeviceCtx>> g_ctx;
+
+static DeviceCtx& ctx_for(int device) {
+  std::lock_guard<std::mutex> lk(g_ctx_mu);
+  auto it = g_ctx.find(device);
+  if (it != g_ctx.end()) return *it->second;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+    throw Error(FLOAM_ERR_DEVICE, "no HIP device available (the floam_amd core needs an MI355X / gfx950 GPU)");
+  if (device < 0 || device >= n) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "device index out of range");
+  FLOAM_HIP(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  FLOAM_HIP(hipGetDeviceProperties(&prop, device));
+  if (std::string(prop.gcnArchName).rfind("gfx950", 0) != 0)
+    throw Error(FLOAM_ERR_DEVICE, std::string("device is ") + prop.gcnArchName + ", this build targets gfx950");
+  auto c = std::make_unique<DeviceCtx>();
+  c->device = device;
+  FLOAM_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  DeviceCtx& ref = *c;
+  g_ctx[device] = std::move(c);
+  return ref;
+}
+
+// Records HIP events around a launch sequence on the library stream when profiling is on.
+struct ProfScope {
+  DeviceCtx& c;
+  const char* name;
+  double bytes;
+  hipEvent_t e0 = nullptr;
+  ProfScope(DeviceCtx& ctx, const char* n, double b = 0.0) : c(ctx), name(n), bytes(b) {
+    if (c.profile) {
+      e0 = c.get_event();
+      FLOAM_HIP(hipEventRecord(e0, c.stream));
+    }
+  }
+  ~ProfScope() {
+    if (c.profile && e0) {
+      hipEvent_t e1 = c.get_event();
+      (void)hipEventRecord(e1, c.stream);
+      c.pending.push_back(PendingTiming{name, e0, e1, bytes});
+    }
+  }
+};
+
+// ----------------------------------------------------------------------------------------- cloud helpers
+static size_t cloud_count_sync(const floam_cloud* c) {
+  if (c->host_count_valid) return c->host_count;
+  DeviceCtx& ctx = ctx_for(c->device);
+  int v = 0;
+  FLOAM_HIP(hipMemcpyAsync(&v, c->count.p, sizeof(int), hipMemcpyDeviceToHost, ctx.stream));
+  FLOAM_HIP(hipStreamSynchronize(ctx.stream));
+  auto* mc = const_cast<floam_cloud*>(c);
+  mc->host_count = (size_t)v;
+  mc->host_count_valid = true;
+  return mc->host_count;
+}
+
+// grow keeping the first `keep` points (stream-ordered copy, then the old buffer is freed after a sync)
+static void cloud_reserve(floam_cloud* c, size_t n, size_t keep, hipStream_t st) {
+  if (n <= c->pts.cap) return;
+  const size_t cap = std::max<size_t>(n + n / 4, 1024);
+  PointRec* p = nullptr;
+  FLOAM_HIP(hipMalloc(&p, cap * sizeof(PointRec)));
+  if (keep && c->pts.p) {
+    FLOAM_HIP(hipMemcpyAsync(p, c->pts.p, keep * sizeof(PointRec), hipMemcpyDeviceToDevice, st));
+    FLOAM_HIP(hipStreamSynchronize(st));
+  }
+  if (c->pts.p) FLOAM_HIP(hipFree(c->pts.p));
+  c->pts.p = p;
+  c->pts.cap = cap;
+}
+
+static void cloud_init(floam_cloud* c, int device, size_t capacity) {
+  c->device = device;
+  c->count.reserve(1);
+  DeviceCtx& ctx = ctx_for(device);
+  FLOAM_HIP(hipMemsetAsync(c->count.p, 0, sizeof(int), ctx.stream));
+  c->host_count = 0;
+  c->host_count_valid = true;
+  if (capacity) cloud_reserve(c, capacity, 0, ctx.stream);
+}
+
+static bool g_keyframe_first = true;   // KeyFrameUpdate's function-static `first` (odomEstimationClass.cpp:323, Q6)
+
+}  // namespace floam
+
+using namespace floam;
+
+// ============================================================================================ handles
+struct floam_lp {
+  int device = 0;
+  FeParams prm{};
+  FeScratch sc;
+  DevBuf<int> status;
+  HostBuf<int> h_out;   // edge count, surf count, status
+};
+
+struct floam_odom {
+  int device = 0;
+  floam_lidar_params lp{};
+  double map_resolution = 0.4;
+  bool huber = false;
+  float leafE = 0.4f, leafS = 0.8f;
+  // local map (device) and host-known exact sizes (valid as of the last synchronisation)
+  floam_cloud mapE, mapS;
+  size_t mapE_n = 0, mapS_n = 0;
+  bool maps_exact = true;
+  // scratch
+  DevBuf<PointRec> dE, dS, tmp;
+  DevBuf<int> cnt;   // [0] dE count [1] dS count [2] tmp count
+  VoxelScratch vs;
+  GridScratch gsc;
+  Grid gE, gS;
+  bool grid_dirty = true;
+  CorrSet ce, cs;
+  DevBuf<double> partials, sums;
+  DevBuf<LMState> lm;
+  HostBuf<LMState> h_lm;
+  HostBuf<int> h_cnt;   // dE, dS, mapE, mapS
+  HostBuf<double> h_x;
+  // pose state (host, double)
+  Pose odom = pose_identity(), last_odom = pose_identity();
+  double parameters[7] = {0, 0, 0, 1, 0, 0, 0};
+  int optimization_count = 2;
+  std::vector<Pose> keyframes;
+  // sharding
+  int rank = 0, world = 1;
+  ncclComm_t comm = nullptr;
+  floam_odom_stats stats{};
+  floam_status last_warning = FLOAM_OK;
+};
+
+namespace {
+thread_local std::string t_err;
+
+floam_status fail(floam_status s, const std::string& m) {
+  t_err = m;
+  return s;
+}
+
+template <typename F>
+floam_status guarded(F&& f) {
+  try {
+    return f();
+  } catch (const Error& e) {
+    return fail(e.status, e.what());
+  } catch (const std::bad_alloc&) {
+    return fail(FLOAM_ERR_OUT_OF_MEMORY, "host allocation failed");
+  } catch (const std::exception& e) {
+    return fail(FLOAM_ERR_DEVICE, e.what());
+  }
+}
+
+void check_params(const floam_lidar_params* p) {
+  if (!p) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null lidar params");
+  if (p->num_lines <= 0 || p->num_lines > 4096) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "num_lines out of range");
+}
+
+// ------------------------------------------------------------------------------------- odometry internals
+void odom_set_params_from_odom(floam_odom* o) {
+  // q_w_curr = Quaterniond(odom.rotation()); t_w_curr = odom.translation() (odomEstimationClass.cpp:70-71)
+  double q[4];
+  mat_to_quat(o->odom.R, q);
+  for (int i = 0; i < 4; ++i) o->parameters[i] = q[i];
+  for (int i = 0; i < 3; ++i) o->parameters[4 + i] = o->odom.t[i];
+}
+
+bool keyframe_update(floam_odom* o, const Pose& pose) {   // KeyFrameUpdate (odomEstimationClass.cpp:320-343)
+  if (g_keyframe_first || o->keyframes.empty()) {
+    g_keyframe_first = false;
+    o->keyframes.push_back(pose);
+    return true;
+  }
+  const Pose delta = pose_mul(pose_inverse(o->keyframes.back()), pose);
+  const double dm = std::sqrt(delta.t[0] * delta.t[0] + delta.t[1] * delta.t[1] + delta.t[2] * delta.t[2]);
+  const double dr = rotation_angle(delta.R);
+  if (dm > 0.07 || dr > 2 * M_PI / 180.0) {
+    o->keyframes.push_back(pose);
+    if (o->keyframes.size() > 3) o->keyframes.erase(o->keyframes.begin());
+    return true;
+  }
+  return false;
+}
+
+void allreduce_sums(floam_odom* o, DeviceCtx& ctx) {
+  const ncclResult_t r =
+      ncclAllReduce(o->sums.p, o->sums.p, LM_NSUM, ncclDouble, ncclSum, o->comm, ctx.stream);
+  if (r != ncclSuccess) throw Error(FLOAM_ERR_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+}
+
+// updatePointsToMap (src/odomEstimationClass.cpp:52-124)
+void odom_update(floam_odom* o, const floam_cloud* edge, const floam_cloud* surf, int type) {
+  DeviceCtx& ctx = ctx_for(o->device);
+  hipStream_t st = ctx.stream;
+  FLOAM_HIP(hipSetDevice(o->device));
+  const int ne_ub = (int)cloud_count_sync(edge);
+  const int ns_ub = (int)cloud_count_sync(surf);
+
+  if (o->optimization_count > 2) o->optimization_count--;
+  const Pose pred = pose_mul(o->odom, pose_mul(pose_inverse(o->last_odom), o->odom));
+  o->last_odom = o->odom;   // Q2: the branch is taken for every update type
+  o->odom = pred;
+  odom_set_params_from_odom(o);
+
+  o->dE.reserve(std::max(ne_ub, 1));
+  o->dS.reserve(std::max(ns_ub, 1));
+  o->cnt.reserve(4);
+  {
+    ProfScope ps(ctx, "voxel_downsample");
+    // VelToIntensityCopy + downSamplingToMap (:53-54, :75, :137-142)
+    voxel_launch(o->vs, edge->pts.p, edge->count.p, ne_ub, o->leafE, o->dE.p, o->cnt.p + 0, st);
+    voxel_launch(o->vs, surf->pts.p, surf->count.p, ns_ub, o->leafS, o->dS.p, o->cnt.p + 1, st);
+  }
+  const int mE_ub = (int)o->mapE_n, mS_ub = (int)o->mapS_n;   // exact or upper bounds
+  if (o->grid_dirty) {
+    ProfScope ps(ctx, "grid_build");
+    grid_build_launch(o->gE, o->gsc, o->mapE.pts.p, o->mapE.count.p, std::max(mE_ub, 1), st);
+    grid_build_launch(o->gS, o->gsc, o->mapS.pts.p, o->mapS.count.p, std::max(mS_ub, 1), st);
+    o->grid_dirty = false;
+  }
+  o->lm.reserve(1);
+  o->h_lm.reserve(1);
+  o->h_cnt.reserve(4);
+  o->h_x.reserve(8);
+  std::memcpy(o->h_x.p, o->parameters, sizeof(double) * 7);
+  FLOAM_HIP(hipMemcpyAsync(o->lm.p->x, o->h_x.p, sizeof(double) * 7, hipMemcpyHostToDevice, st));
+  o->partials.reserve((size_t)LM_NSUM * 512);
+  o->sums.reserve(LM_NSUM);
+  const QuerySet qe{o->dE.p, o->cnt.p + 0, ne_ub};
+  const QuerySet qs{o->dS.p, o->cnt.p + 1, ns_ub};
+  const bool sharded = o->world > 1;
+  for (int it = 0; it < o->optimization_count; ++it) {
+    {
+      ProfScope ps(ctx, "knn_correspondences");
+      corr_launch(o->lm.p, qe, o->gE, o->mapE.count.p, qs, o->gS, o->mapS.count.p, o->ce, o->cs, o->rank, o->world,
+                  st);
+    }
+    // iteration zero + at most max_num_iterations = 4 candidates (odomEstimationClass.cpp:102)
+    for (int ev = 0; ev < 5; ++ev) {
+      int nblk;
+      {
+        ProfScope ps(ctx, "lm_evaluate");
+        nblk = lm_eval_launch(o->lm.p, o->ce, ne_ub, o->cs, ns_ub, o->huber, o->partials.p, st);
+      }
+      ProfScope ps(ctx, "lm_control");
+      if (sharded) {
+        lm_reduce_launch(o->partials.p, nblk, o->sums.p, st);
+        allreduce_sums(o, ctx);
+        lm_control_launch(o->lm.p, o->sums.p, 0, st);
+      } else {
+        lm_control_launch(o->lm.p, o->partials.p, nblk, st);
+      }
+    }
+  }
+  FLOAM_HIP(hipMemcpyAsync(o->h_lm.p, o->lm.p, sizeof(LMState), hipMemcpyDeviceToHost, st));
+  FLOAM_HIP(hipMemcpyAsync(o->h_cnt.p, o->cnt.p, sizeof(int) * 2, hipMemcpyDeviceToHost, st));
+  FLOAM_HIP(hipMemcpyAsync(o->h_cnt.p + 2, o->mapE.count.p, sizeof(int), hipMemcpyDeviceToHost, st));
+  FLOAM_HIP(hipMemcpyAsync(o->h_cnt.p + 3, o->mapS.count.p, sizeof(int), hipMemcpyDeviceToHost, st));
+  FLOAM_HIP(hipStreamSynchronize(st));
+  ctx.drain();
+  const LMState& L = *o->h_lm.p;
+  const int nEd = o->h_cnt.p[0], nSd = o->h_cnt.p[1];
+  o->mapE_n = (size_t)o->h_cnt.p[2];
+  o->mapS_n = (size_t)o->h_cnt.p[3];
+  o->mapE.host_count = o->mapE_n; o->mapE.host_count_valid = true;
+  o->mapS.host_count = o->mapS_n; o->mapS.host_count_valid = true;
+  o->last_warning = FLOAM_OK;
+  const bool gate = o->mapE_n > 10 && o->mapS_n > 50;   // (:77)
+  if (gate) {
+    std::memcpy(o->parameters, L.x, sizeof(double) * 7);
+    if (L.corr_edge < 20 || L.corr_surf < 20) o->last_warning = FLOAM_WARN_FEW_CORRESPONDENCES;
+  } else {
+    o->last_warning = FLOAM_WARN_MAP_TOO_SMALL;
+  }
+  // odom = Isometry(q_w_curr.toRotationMatrix(), t_w_curr) (:114-116)
+  o->odom.R = quat_to_mat(o->parameters);
+  for (int i = 0; i < 3; ++i) o->odom.t[i] = o->parameters[4 + i];
+  o->stats.optimization_count = o->optimization_count;
+  o->stats.solves = gate ? o->optimization_count : 0;
+  o->stats.edge_queries = nEd;
+  o->stats.surf_queries = nSd;
+  o->stats.edge_correspondences = gate ? L.corr_edge : 0;
+  o->stats.surf_correspondences = gate ? L.corr_surf : 0;
+  o->stats.lm_iterations = gate ? L.iteration : 0;
+  o->stats.final_cost = gate ? L.x_cost : 0.0;
+  o->stats.map_updated = 0;
+  if (type == FLOAM_VANILLA || type == FLOAM_REFINEMENT_AND_UPDATE) {
+    if (keyframe_update(o, o->odom)) {
+      // addPointsToMap (:253-294): device-side transform + append + CropBox + VoxelGrid of both maps, using the
+      // optimised pose, which is lm->x (== parameters) on the device.
+      ProfScope ps(ctx, "map_update");
+      if (!gate) {   // lm->x still holds the prediction we uploaded: identical to parameters
+      }
+      const int ubS = (int)o->mapS_n + nSd, ubE = (int)o->mapE_n + nEd;
+      const int ub = std::max(std::max(ubS, ubE), 1);
+      o->tmp.reserve(ub);
+      o->cnt.reserve(4);
+      cloud_reserve(&o->mapS, std::max(ubS, 1), o->mapS_n, st);
+      cloud_reserve(&o->mapE, std::max(ubE, 1), o->mapE_n, st);
+      crop_concat_launch(o->vs.s, o->mapS.pts.p, o->mapS.count.p, (int)o->mapS_n, o->dS.p, o->cnt.p + 1, nSd,
+                         o->lm.p->x, o->tmp.p, o->cnt.p + 2, st);
+      voxel_launch(o->vs, o->tmp.p, o->cnt.p + 2, std::max(ubS, 1), o->leafS, o->mapS.pts.p, o->mapS.count.p, st);
+      crop_concat_launch(o->vs.s, o->mapE.pts.p, o->mapE.count.p, (int)o->mapE_n, o->dE.p, o->cnt.p + 0, nEd,
+                         o->lm.p->x, o->tmp.p, o->cnt.p + 2, st);
+      voxel_launch(o->vs, o->tmp.p, o->cnt.p + 2, std::max(ubE, 1), o->leafE, o->mapE.pts.p, o->mapE.count.p, st);
+      o->mapS_n = (size_t)ubS;   // upper bounds until the next synchronisation
+      o->mapE_n = (size_t)ubE;
+      o->mapS.host_count_valid = false;
+      o->mapE.host_count_valid = false;
+      o->grid_dirty = true;
+      o->stats.map_updated = 1;
+    }
+  }
+}
+
+// CompensateVelocity (src/dataHandler.cpp:82-92) with GetVelocity (include/odomEstimationClass.h:78)
+void odom_velocity(const floam_odom* o, double v[3]) {
+  for (int i = 0; i < 3; ++i) v[i] = (o->odom.t[i] - o->last_odom.t[i]) / o->lp.scan_period;
+}
+
+}  // namespace
+
+// ============================================================================================ C ABI
+extern "C" {
+
+const char* floam_last_error(void) { return t_err.c_str(); }
+const char* floam_version(void) { return "floam_amd 0.1.0 (gfx950)"; }
+void floam_reset_process_state(void) { g_keyframe_first = true; }
+
+floam_status floam_device_synchronize(int device) {
+  return guarded([&] {
+    DeviceCtx& c = ctx_for(device);
+    FLOAM_HIP(hipStreamSynchronize(c.stream));
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_cloud_create(int device, size_t capacity, floam_cloud** out) {
+  return guarded([&] {
+    if (!out) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null out");
+    auto c = std::make_unique<floam_cloud>();
+    FLOAM_HIP(hipSetDevice(device));
+    cloud_init(c.get(), device, capacity);
+    *out = c.release();
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_cloud_destroy(floam_cloud* c) {
+  return guarded([&] {
+    if (c) {
+      DeviceCtx& ctx = ctx_for(c->device);
+      FLOAM_HIP(hipStreamSynchronize(ctx.stream));
+      delete c;
+    }
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_cloud_upload(floam_cloud* c, const void* host, size_t n, size_t stride) {
+  return guarded([&] {
+    if (!c || (!host && n)) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null cloud / points");
+    if (n > (size_t)INT32_MAX) throw Error(FLOAM_ERR_UNSUPPORTED, "cloud larger than 2^31 points");
+    if (stride < 28) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "stride must cover the PointXYZIRT fields");
+    DeviceCtx& ctx = ctx_for(c->device);
+    FLOAM_HIP(hipSetDevice(c->device));
+    FLOAM_HIP(hipStreamSynchronize(ctx.stream));
+    cloud_reserve(c, std::max<size_t>(n, 1), 0, ctx.stream);
+    if (stride == sizeof(PointRec)) {
+      FLOAM_HIP(hipMemcpyAsync(c->pts.p, host, n * sizeof(PointRec), hipMemcpyHostToDevice, ctx.stream));
+    } else {
+      std::vector<PointRec> tmp(n);
+      const char* b = static_cast<const char*>(host);
+      for (size_t i = 0; i < n; ++i) std::memcpy(&tmp[i], b + i * stride, 28);
+      FLOAM_HIP(hipMemcpyAsync(c->pts.p, tmp.data(), n * sizeof(PointRec), hipMemcpyHostToDevice, ctx.stream));
+      FLOAM_HIP(hipStreamSynchronize(ctx.stream));
+    }
+    const int cnt = (int)n;
+    FLOAM_HIP(hipMemcpyAsync(c->count.p, &cnt, sizeof(int), hipMemcpyHostToDevice, ctx.stream));
+    FLOAM_HIP(hipStreamSynchronize(ctx.stream));
+    c->host_count = n;
+    c->host_count_valid = true;
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_cloud_size(const floam_cloud* c, size_t* n) {
+  return guarded([&] {
+    if (!c || !n) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
+    *n = cloud_count_sync(c);
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_cloud_download(const floam_cloud* c, void* host, size_t capacity, size_t* n_out) {
+  return guarded([&] {
+    if (!c) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null cloud");
+    const size_t n = cloud_count_sync(c);
+    if (n_out) *n_out = n;
+    const size_t k = std::min(n, capacity);
+    if (k) {
+      if (!host) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null host buffer");
+      DeviceCtx& ctx = ctx_for(c->device);
+      FLOAM_HIP(hipMemcpyAsync(host, c->pts.p, k * sizeof(PointRec), hipMemcpyDeviceToHost, ctx.stream));
+      FLOAM_HIP(hipStreamSynchronize(ctx.stream));
+    }
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_cloud_clear(floam_cloud* c) {
+  return guarded([&] {
+    if (!c) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null cloud");
+    DeviceCtx& ctx = ctx_for(c->device);
+    FLOAM_HIP(hipMemsetAsync(c->count.p, 0, sizeof(int), ctx.stream));
+    c->host_count = 0;
+    c->host_count_valid = true;
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_cloud_copy(floam_cloud* dst, const floam_cloud* src) {
+  return guarded([&] {
+    if (!dst || !src) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null cloud");
+    if (dst->device != src->device) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "clouds on different devices");
+    DeviceCtx& ctx = ctx_for(dst->device);
+    const size_t n = cloud_count_sync(src);
+    cloud_reserve(dst, std::max<size_t>(n, 1), 0, ctx.stream);
+    if (n)
+      FLOAM_HIP(hipMemcpyAsync(dst->pts.p, src->pts.p, n * sizeof(PointRec), hipMemcpyDeviceToDevice, ctx.stream));
+    FLOAM_HIP(hipMemcpyAsync(dst->count.p, src->count.p, sizeof(int), hipMemcpyDeviceToDevice, ctx.stream));
+    dst->host_count = n;
+    dst->host_count_valid = true;
+    return FLOAM_OK;
+  });
+}
+
+void* floam_cloud_device_ptr(floam_cloud* c) { return c ? c->pts.p : nullptr; }
+
+// ------------------------------------------------------------------------------------------ laser processing
+floam_status floam_lp_create(const floam_lidar_params* p, int device, floam_lp** out) {
+  return guarded([&] {
+    check_params(p);
+    if (!out) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null out");
+    ctx_for(device);
+    FLOAM_HIP(hipSetDevice(device));
+    auto lp = std::make_unique<floam_lp>();
+    lp->device = device;
+    lp->prm.num_lines = p->num_lines;
+    lp->prm.min_distance = p->min_distance;
+    lp->prm.max_distance = p->max_distance;
+    lp->status.reserve(1);
+    lp->h_out.reserve(4);
+    lp->sc.status = lp->status.p;
+    *out = lp.release();
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_lp_destroy(floam_lp* lp) {
+  return guarded([&] {
+    if (lp) {
+      DeviceCtx& ctx = ctx_for(lp->device);
+      FLOAM_HIP(hipStreamSynchronize(ctx.stream));
+      delete lp;
+    }
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_lp_feature_extraction(floam_lp* lp, const floam_cloud* in, floam_cloud* edge, floam_cloud* surf) {
+  return guarded([&] {
+    if (!lp || !in || !edge || !surf) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
+    if (in->device != lp->device || edge->device != lp->device || surf->device != lp->device)
+      throw Error(FLOAM_ERR_INVALID_ARGUMENT, "clouds and handle on different devices");
+    if (edge == surf || in == edge || in == surf) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "clouds must be distinct");
+    DeviceCtx& ctx = ctx_for(lp->device);
+    hipStream_t st = ctx.stream;
+    FLOAM_HIP(hipSetDevice(lp->device));
+    const size_t n = cloud_count_sync(in);
+    const size_t ne0 = cloud_count_sync(edge), ns0 = cloud_count_sync(surf);
+    cloud_reserve(edge, ne0 + std::min(n, (size_t)lp->prm.num_lines * 6 * 20) + 1, ne0, st);
+    cloud_reserve(surf, ns0 + n + 1, ns0, st);
+    FLOAM_HIP(hipMemsetAsync(lp->status.p, 0, sizeof(int), st));
+    if (n > 0) {
+      ProfScope ps(ctx, "feature_extraction", 64.0 * (double)n);
+      fe_launch(lp->sc, lp->prm, in->pts.p, (int)n, edge->pts.p, edge->count.p, surf->pts.p, surf->count.p, st);
+    }
+    FLOAM_HIP(hipMemcpyAsync(lp->h_out.p + 0, edge->count.p, sizeof(int), hipMemcpyDeviceToHost, st));
+    FLOAM_HIP(hipMemcpyAsync(lp->h_out.p + 1, surf->count.p, sizeof(int), hipMemcpyDeviceToHost, st));
+    FLOAM_HIP(hipMemcpyAsync(lp->h_out.p + 2, lp->status.p, sizeof(int), hipMemcpyDeviceToHost, st));
+    FLOAM_HIP(hipStreamSynchronize(st));
+    ctx.drain();
+    edge->host_count = (size_t)lp->h_out.p[0];
+    edge->host_count_valid = true;
+    surf->host_count = (size_t)lp->h_out.p[1];
+    surf->host_count_valid = true;
+    const int status = lp->h_out.p[2];
+    if (status & FE_STATUS_SECTOR_TOO_LONG)
+      throw Error(FLOAM_ERR_UNSUPPORTED, "a ring sector exceeds 4096 points (ring longer than ~24k points)");
+    if (status & FE_STATUS_BAD_RING)
+      throw Error(FLOAM_ERR_INVALID_ARGUMENT, "point ring index >= num_lines (out of bounds in the reference)");
+    return FLOAM_OK;
+  });
+}
+
+// ------------------------------------------------------------------------------------------ odometry
+floam_status floam_odom_create(const floam_lidar_params* p, double map_resolution, const char* loss, int device,
+                               floam_odom** out) {
+  return guarded([&] {
+    check_params(p);
+    if (!out) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null out");
+    if (!(map_resolution > 0)) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "map_resolution must be > 0");
+    ctx_for(device);
+    FLOAM_HIP(hipSetDevice(device));
+    auto o = std::make_unique<floam_odom>();
+    o->device = device;
+    o->lp = *p;
+    o->map_resolution = map_resolution;
+    std::string l = loss ? loss : "";
+    std::transform(l.begin(), l.end(), l.begin(), [](unsigned char c) { return (char)std::tolower(c); });
+    o->huber = (l == "huber");   // any other string: no robust loss (Q3)
+    o->leafE = (float)map_resolution;          // downSizeFilterEdge.setLeafSize(r) (:13)
+    o->leafS = (float)(map_resolution * 2);    // downSizeFilterSurf.setLeafSize(2r) (:14)
+    cloud_init(&o->mapE, device, 1024);
+    cloud_init(&o->mapS, device, 1024);
+    o->cnt.reserve(4);
+    DeviceCtx& ctx = ctx_for(device);
+    FLOAM_HIP(hipMemsetAsync(o->cnt.p, 0, sizeof(int) * 4, ctx.stream));
+    o->lm.reserve(1);
+    FLOAM_HIP(hipMemsetAsync(o->lm.p, 0, sizeof(LMState), ctx.stream));
+    FLOAM_HIP(hipStreamSynchronize(ctx.stream));
+    *out = o.release();
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_odom_destroy(floam_odom* o) {
+  return guarded([&] {
+    if (o) {
+      DeviceCtx& ctx = ctx_for(o->device);
+      FLOAM_HIP(hipStreamSynchronize(ctx.stream));
+      if (o->comm) ncclCommDestroy(o->comm);
+      delete o;
+    }
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_odom_init_map(floam_odom* o, const floam_cloud* edge, const floam_cloud* surf) {
+  return guarded([&] {
+    if (!o || !edge || !surf) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
+    DeviceCtx& ctx = ctx_for(o->device);
+    hipStream_t st = ctx.stream;
+    const size_t ne = cloud_count_sync(edge), ns = cloud_count_sync(surf);
+    const size_t mE = cloud_count_sync(&o->mapE), mS = cloud_count_sync(&o->mapS);
+    cloud_reserve(&o->mapE, mE + ne + 1, mE, st);
+    cloud_reserve(&o->mapS, mS + ns + 1, mS, st);
+    append_launch(o->mapE.pts.p, o->mapE.count.p, edge->pts.p, edge->count.p, (int)ne, true, st);
+    append_launch(o->mapS.pts.p, o->mapS.count.p, surf->pts.p, surf->count.p, (int)ns, true, st);
+    o->mapE_n = mE + ne;
+    o->mapS_n = mS + ns;
+    o->mapE.host_count = o->mapE_n; o->mapE.host_count_valid = true;
+    o->mapS.host_count = o->mapS_n; o->mapS.host_count_valid = true;
+    o->grid_dirty = true;
+    o->optimization_count = 12;   // (:31)
+    FLOAM_HIP(hipStreamSynchronize(st));
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_odom_update(floam_odom* o, const floam_cloud* edge, const floam_cloud* surf, int type) {
+  return guarded([&] {
+    if (!o || !edge || !surf) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
+    if (type < 0 || type > 2) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "bad update type");
+    odom_update(o, edge, surf, type);
+    return o->last_warning;
+  });
+}
+
+floam_status floam_odom_update_selector(floam_odom* o, floam_cloud* edge, floam_cloud* surf, int deskew) {
+  return guarded([&] {
+    if (!o || !edge || !surf) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
+    if (!deskew) {
+      odom_update(o, edge, surf, FLOAM_VANILLA);
+      return o->last_warning;
+    }
+    odom_update(o, edge, edge, FLOAM_INITIAL_ITERATION);   // Q4: the edge cloud is passed as the surf input
+    const floam_status w1 = o->last_warning;
+    double v[3];
+    odom_velocity(o, v);
+    DeviceCtx& ctx = ctx_for(o->device);
+    {
+      ProfScope ps(ctx, "deskew");
+      compensate_velocity_launch(edge->pts.p, edge->count.p, (int)cloud_count_sync(edge), v[0], v[1], v[2], ctx.stream);
+      compensate_velocity_launch(surf->pts.p, surf->count.p, (int)cloud_count_sync(surf), v[0], v[1], v[2], ctx.stream);
+    }
+    odom_update(o, edge, surf, FLOAM_REFINEMENT_AND_UPDATE);
+    return o->last_warning != FLOAM_OK ? o->last_warning : w1;
+  });
+}
+
+floam_status floam_odom_get_pose(const floam_odom* o, double q[4], double t[3]) {
+  return guarded([&] {
+    if (!o || !q || !t) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
+    mat_to_quat(o->odom.R, q);
+    for (int i = 0; i < 3; ++i) t[i] = o->odom.t[i];
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_odom_get_last_pose(const floam_odom* o, double q[4], double t[3]) {
+  return guarded([&] {
+    if (!o || !q || !t) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
+    mat_to_quat(o->last_odom.R, q);
+    for (int i = 0; i < 3; ++i) t[i] = o->last_odom.t[i];
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_odom_get_velocity(const floam_odom* o, double v[3]) {
+  return guarded([&] {
+    if (!o || !v) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
+    odom_velocity(o, v);
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_odom_get_map_sizes(floam_odom* o, size_t* corner, size_t* surf) {
+  return guarded([&] {
+    if (!o) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
+    const size_t e = cloud_count_sync(&o->mapE), s = cloud_count_sync(&o->mapS);
+    o->mapE_n = e;
+    o->mapS_n = s;
+    if (corner) *corner = e;
+    if (surf) *surf = s;
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_odom_download_maps(floam_odom* o, void* corner, size_t ccap, void* surf, size_t scap) {
+  return guarded([&] {
+    if (!o) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
+    size_t n;
+    floam_status s = floam_cloud_download(&o->mapE, corner, ccap, &n);
+    if (s != FLOAM_OK) return s;
+    return floam_cloud_download(&o->mapS, surf, scap, &n);
+  });
+}
+
+floam_status floam_odom_get_map(floam_odom* o, floam_cloud* out) {
+  return guarded([&] {
+    if (!o || !out) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
+    DeviceCtx& ctx = ctx_for(o->device);
+    const size_t e = cloud_count_sync(&o->mapE), s = cloud_count_sync(&o->mapS), n0 = cloud_count_sync(out);
+    cloud_reserve(out, n0 + e + s + 1, n0, ctx.stream);
+    append_launch(out->pts.p, out->count.p, o->mapS.pts.p, o->mapS.count.p, (int)s, false, ctx.stream);
+    append_launch(out->pts.p, out->count.p, o->mapE.pts.p, o->mapE.count.p, (int)e, false, ctx.stream);
+    out->host_count = n0 + e + s;
+    out->host_count_valid = true;
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_odom_get_stats(const floam_odom* o, floam_odom_stats* s) {
+  return guarded([&] {
+    if (!o || !s) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
+    *s = o->stats;
+    s->corner_map = o->mapE_n;
+    s->surf_map = o->mapS_n;
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_comm_unique_id(void* id) {
+  return guarded([&] {
+    if (!id) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null id");
+    static_assert(sizeof(ncclUniqueId) == 128, "RCCL unique id is 128 bytes");
+    ncclUniqueId u;
+    const ncclResult_t r = ncclGetUniqueId(&u);
+    if (r != ncclSuccess) throw Error(FLOAM_ERR_COMM, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+    std::memcpy(id, &u, sizeof(u));
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_odom_set_shard(floam_odom* o, int rank, int world, const void* id) {
+  return guarded([&] {
+    if (!o || world < 1 || rank < 0 || rank >= world) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "bad rank / world");
+    if (o->comm) {
+      ncclCommDestroy(o->comm);
+      o->comm = nullptr;
+    }
+    o->rank = rank;
+    o->world = world;
+    if (world > 1) {
+      if (!id) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null unique id");
+      FLOAM_HIP(hipSetDevice(o->device));
+      ncclUniqueId u;
+      std::memcpy(&u, id, sizeof(u));
+      const ncclResult_t r = ncclCommInitRank(&o->comm, world, u, rank);
+      if (r != ncclSuccess) throw Error(FLOAM_ERR_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    }
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_profile_enable(int device, int enable) {
+  return guarded([&] {
+    DeviceCtx& c = ctx_for(device);
+    c.profile = enable != 0;
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_profile_reset(int device) {
+  return guarded([&] {
+    DeviceCtx& c = ctx_for(device);
+    FLOAM_HIP(hipStreamSynchronize(c.stream));
+    c.drain();
+    c.totals.clear();
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_profile_read(int device, floam_kernel_timing* out, int max_entries, int* n_out) {
+  return guarded([&] {
+    DeviceCtx& c = ctx_for(device);
+    FLOAM_HIP(hipStreamSynchronize(c.stream));
+    c.drain();
+    int k = 0;
+    for (auto& kv : c.totals) {
+      if (k < max_entries && out) out[k] = kv.second;
+      ++k;
+    }
+    if (n_out) *n_out = k;
+    return FLOAM_OK;
+  });
+}
+
+}  // extern "C"

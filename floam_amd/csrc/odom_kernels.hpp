@@ -1,0 +1,95 @@
+#pragma once
+#include "cloud_ops.hpp"
+#include "floam_common.hpp"
+
+namespace floam {
+
+// ----------------------------------------------------------------------------------------- hash grid
+// Map points bucketed into cubic cells (edge >= 1 m, power of two) over the map's bounding box, cell-sorted as
+// float4 {x, y, z, map index bits}; occupied cells in an open-addressing hash table key -> (start, count).
+// Exact replacement of the 5-NN KD-tree under the reference's sqd[4] < 1 gate: every map
+// point with float sq-distance < 1 lies within one cell of the query's cell along each axis.
+struct GridParams {
+  double ox, oy, oz;     // origin = floor(bbox min)
+  double c;              // cell edge (1, 2, 4, ... m)
+  int nx, ny, nz;
+  int shift;             // hash: (key * 0x9E3779B1) >> shift
+  unsigned mask;
+  int n;                 // map points
+};
+
+struct Grid {
+  DevBuf<GridParams> params;
+  DevBuf<float4> pts;      // cell-sorted
+  DevBuf<uint32_t> tkey;
+  DevBuf<int2> tval;       // (start, count)
+  int table_size = 0;
+  int shift = 0;
+};
+
+struct GridScratch {
+  SortScratch s;
+  DevBuf<int> mm;
+};
+
+void grid_build_launch(Grid& g, GridScratch& sc, const PointRec* map, const int* d_m, int m_ub, hipStream_t st);
+
+// ----------------------------------------------------------------------------------------- correspondences
+// Edge record (EdgeAnalyticCostFunction inputs): cp (sensor point), a, b.  Surf: cp, unit normal n, d.
+// SoA doubles, field f of slot i at base[f * cap + i]; valid[i] != 0 for accepted correspondences.
+enum { EDGE_FIELDS = 9, SURF_FIELDS = 7 };
+
+struct CorrSet {
+  DevBuf<double> rec;
+  DevBuf<uint8_t> valid;
+  int cap = 0;
+  void reserve(int n, int fields) {
+    if (n <= cap) return;
+    const int c = n < 1024 ? 1024 : n + n / 4;
+    rec.reserve((size_t)c * fields);
+    valid.reserve(c);
+    cap = (int)valid.cap;
+    rec.reserve((size_t)cap * fields);
+  }
+};
+
+// ----------------------------------------------------------------------------------------- LM state
+struct LMState {
+  double x[7];        // accepted parameters (qx, qy, qz, qw, tx, ty, tz)
+  double cand[7];     // candidate under evaluation
+  double x_cost;
+  double H[21];       // J^T J at x (unscaled, upper triangle row-major)
+  double g[6];        // J^T r at x
+  double scale[6];    // Jacobi scaling, fixed at iteration 0
+  double diag[6];     // LM diagonal (reused after a rejected / invalid step)
+  double radius, dfac, mcc, x_norm, gmax, initial_cost;
+  int phase;          // 0: evaluate x (iteration zero); 1: evaluate cand
+  int done;
+  int iteration;
+  int reuse;
+  int invalid;
+  int successful;
+  int n_res;
+  int corr_edge, corr_surf;   // accepted correspondences (this solve)
+  int pad;
+};
+
+enum { LM_NSUM = 29 };   // cost, H[21], g[6], count
+
+struct QuerySet {
+  const PointRec* pts;
+  const int* d_n;
+  int n_ub;
+};
+
+// lm_init + correspondence search for edge & surf queries, at the pose in st->x
+void corr_launch(LMState* d_st, const QuerySet& qe, const Grid& ge, const int* d_me, const QuerySet& qs,
+                 const Grid& gs, const int* d_ms, CorrSet& ce, CorrSet& cs, int rank, int world, hipStream_t st);
+// one LM evaluation (at x in phase 0, else at cand): block partial sums of (cost, J^T J, J^T r, count)
+int lm_eval_launch(const LMState* d_st, const CorrSet& ce, int ne_ub, const CorrSet& cs, int ns_ub, bool huber,
+                   double* partials, hipStream_t st);
+// reduce partials (nblk > 0) or read 29 pre-reduced sums (nblk == 0), then run the Ceres LM control step
+void lm_control_launch(LMState* d_st, const double* partials, int nblk, hipStream_t st);
+void lm_reduce_launch(const double* partials, int nblk, double* sums, hipStream_t st);
+
+}  // namespace floam

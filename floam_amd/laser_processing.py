@@ -1,0 +1,75 @@
+"""LaserProcessingClass — host mirror of include/laserProcessingClass.h:37-50 over the C ABI.
+
+Same method names, argument meaning and append semantics as the reference; clouds are ``DeviceCloud``s
+(device-resident 32-B PointXYZIRT records) instead of ``pcl::PointCloud<PointXYZIRT>::Ptr``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+from . import _ffi
+from .cloud import DeviceCloud
+
+
+@dataclass
+class LidarParams:
+    """lidar::Lidar (include/lidar.h:53-85): the fields the path reads."""
+    num_lines: int = 64
+    scan_period: float = 0.1
+    vertical_angle: float = 2.0
+    max_distance: float = 60.0
+    min_distance: float = 2.0
+
+    # setters of lidar::Lidar (src/lidar.cpp)
+    def setLines(self, n):
+        self.num_lines = int(n)
+
+    def setScanPeriod(self, p):
+        self.scan_period = float(p)
+
+    def setVerticalAngle(self, a):
+        self.vertical_angle = float(a)
+
+    def setMaxDistance(self, d):
+        self.max_distance = float(d)
+
+    def setMinDistance(self, d):
+        self.min_distance = float(d)
+
+    def to_c(self) -> _ffi.LidarParams:
+        return _ffi.LidarParams(self.num_lines, self.scan_period, self.vertical_angle, self.max_distance,
+                                self.min_distance)
+
+
+class LaserProcessingClass:
+    def __init__(self, device: int = 0):
+        self._L = _ffi.load()
+        self.device = device
+        self._h = None
+
+    def init(self, lidar_param: LidarParams) -> None:
+        """LaserProcessingClass::init (src/laserProcessingClass.cpp:6-10)."""
+        self.close()
+        h = C.c_void_p()
+        p = lidar_param.to_c()
+        _ffi.check(self._L.floam_lp_create(C.byref(p), self.device, C.byref(h)))
+        self._h = h
+
+    def featureExtraction(self, pc_in: DeviceCloud, pc_out_edge: DeviceCloud, pc_out_surf: DeviceCloud) -> None:
+        """LaserProcessingClass::featureExtraction (src/laserProcessingClass.cpp:72-118): appends edge / surf
+        features of pc_in to pc_out_edge / pc_out_surf (never clears them, like the reference)."""
+        if self._h is None:
+            raise _ffi.FloamError(_ffi.ERR_INVALID_ARGUMENT, "LaserProcessingClass.init() not called")
+        _ffi.check(self._L.floam_lp_feature_extraction(self._h, pc_in.handle, pc_out_edge.handle, pc_out_surf.handle))
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._L.floam_lp_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

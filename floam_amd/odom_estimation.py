@@ -1,0 +1,162 @@
+"""OdomEstimationClass — host mirror of include/odomEstimationClass.h:52-126 over the C ABI.
+
+Method names, argument meaning and update semantics follow the reference (src/odomEstimationClass.cpp); the
+public members ``odom``, ``laserCloudCornerMap`` and ``laserCloudSurfMap`` are properties that read the device
+state.  Clouds are ``DeviceCloud``s.  Non-fatal warnings (the reference's printf diagnostics) are kept in
+``last_status``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from enum import IntEnum
+
+import numpy as np
+
+from . import _ffi
+from .cloud import DeviceCloud
+from .laser_processing import LidarParams
+
+
+class UpdateType(IntEnum):   # include/odomEstimationClass.h:56
+    VANILLA = 0
+    INITIAL_ITERATION = 1
+    REFINEMENT_AND_UPDATE = 2
+
+
+def quat_to_matrix(q):
+    x, y, z, w = q
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                     [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                     [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
+
+
+class OdomEstimationClass:
+    VANILLA = UpdateType.VANILLA
+    INITIAL_ITERATION = UpdateType.INITIAL_ITERATION
+    REFINEMENT_AND_UPDATE = UpdateType.REFINEMENT_AND_UPDATE
+
+    def __init__(self, device: int = 0):
+        self._L = _ffi.load()
+        self.device = device
+        self._h = None
+        self.last_status = _ffi.OK
+
+    def init(self, lidar_param: LidarParams, map_resolution: float, loss_function: str) -> None:
+        """OdomEstimationClass::init (src/odomEstimationClass.cpp:7-26)."""
+        self.close()
+        h = C.c_void_p()
+        p = lidar_param.to_c()
+        _ffi.check(self._L.floam_odom_create(C.byref(p), float(map_resolution), loss_function.encode(), self.device,
+                                             C.byref(h)))
+        self._h = h
+        self.lidar_param = lidar_param
+
+    def _need(self):
+        if self._h is None:
+            raise _ffi.FloamError(_ffi.ERR_INVALID_ARGUMENT, "OdomEstimationClass.init() not called")
+        return self._h
+
+    def initMapWithPoints(self, edge_in: DeviceCloud, surf_in: DeviceCloud) -> None:
+        """src/odomEstimationClass.cpp:28-32"""
+        _ffi.check(self._L.floam_odom_init_map(self._need(), edge_in.handle, surf_in.handle))
+
+    def UpdatePointsToMapSelector(self, edge_in: DeviceCloud, surf_in: DeviceCloud, deskew: bool) -> int:
+        """src/odomEstimationClass.cpp:34-50 (deskew velocity-compensates the clouds in place, Q5)."""
+        self.last_status = _ffi.check(self._L.floam_odom_update_selector(self._need(), edge_in.handle,
+                                                                          surf_in.handle, int(bool(deskew))))
+        return self.last_status
+
+    def updatePointsToMap(self, edge_in: DeviceCloud, surf_in: DeviceCloud,
+                          update_type: UpdateType = UpdateType.VANILLA) -> int:
+        """src/odomEstimationClass.cpp:52-124"""
+        self.last_status = _ffi.check(self._L.floam_odom_update(self._need(), edge_in.handle, surf_in.handle,
+                                                                 int(update_type)))
+        return self.last_status
+
+    def getMap(self, laserCloudMap: DeviceCloud) -> None:
+        """src/odomEstimationClass.cpp:296-300 (appends surf map, then corner map)."""
+        _ffi.check(self._L.floam_odom_get_map(self._need(), laserCloudMap.handle))
+
+    def GetVelocity(self) -> np.ndarray:
+        """include/odomEstimationClass.h:78"""
+        v = np.zeros(3)
+        _ffi.check(self._L.floam_odom_get_velocity(self._need(), v.ctypes.data_as(C.POINTER(C.c_double))))
+        return v
+
+    def pose(self):
+        """(q_xyzw, t) of the public member `odom`."""
+        q, t = np.zeros(4), np.zeros(3)
+        _ffi.check(self._L.floam_odom_get_pose(self._need(), q.ctypes.data_as(C.POINTER(C.c_double)),
+                                               t.ctypes.data_as(C.POINTER(C.c_double))))
+        return q, t
+
+    def last_pose(self):
+        q, t = np.zeros(4), np.zeros(3)
+        _ffi.check(self._L.floam_odom_get_last_pose(self._need(), q.ctypes.data_as(C.POINTER(C.c_double)),
+                                                    t.ctypes.data_as(C.POINTER(C.c_double))))
+        return q, t
+
+    @property
+    def odom(self) -> np.ndarray:
+        """Eigen::Isometry3d odom as a 4x4 matrix."""
+        q, t = self.pose()
+        T = np.eye(4)
+        T[:3, :3] = quat_to_matrix(q)
+        T[:3, 3] = t
+        return T
+
+    def map_sizes(self):
+        a, b = C.c_size_t(), C.c_size_t()
+        _ffi.check(self._L.floam_odom_get_map_sizes(self._need(), C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+    def _maps(self):
+        from .synth import POINT_DTYPE
+        ne, ns = self.map_sizes()
+        e = np.zeros(ne, POINT_DTYPE)
+        s = np.zeros(ns, POINT_DTYPE)
+        _ffi.check(self._L.floam_odom_download_maps(self._need(), e.ctypes.data_as(C.c_void_p), ne,
+                                                    s.ctypes.data_as(C.c_void_p), ns))
+        return e, s
+
+    @property
+    def laserCloudCornerMap(self) -> np.ndarray:
+        return self._maps()[0]
+
+    @property
+    def laserCloudSurfMap(self) -> np.ndarray:
+        return self._maps()[1]
+
+    def stats(self) -> dict:
+        s = _ffi.OdomStats()
+        _ffi.check(self._L.floam_odom_get_stats(self._need(), C.byref(s)))
+        return {k: getattr(s, k) for k, _ in _ffi.OdomStats._fields_}
+
+    def set_shard(self, rank: int, world: int, unique_id: bytes | None) -> None:
+        """Shard the correspondence queries over `world` ranks (one RCCL all-reduce per LM evaluation)."""
+        buf = None
+        if unique_id is not None:
+            buf = C.create_string_buffer(bytes(unique_id), 128)
+        _ffi.check(self._L.floam_odom_set_shard(self._need(), rank, world, buf))
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._L.floam_odom_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def comm_unique_id() -> bytes:
+    buf = C.create_string_buffer(128)
+    _ffi.check(_ffi.load().floam_comm_unique_id(buf))
+    return buf.raw
+
+
+def reset_process_state() -> None:
+    """Reset KeyFrameUpdate's process-static `first` flag (src/odomEstimationClass.cpp:323, quirk Q6)."""
+    _ffi.load().floam_reset_process_state()

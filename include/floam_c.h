@@ -1,0 +1,156 @@
+/*
+ * floam_c.h — C ABI of the MI355X-native FLOAM scan-to-map odometry core (libfloam_amd.so).
+ *
+ * Drop-in boundary for the reference operator API (dan11003/floam).  Each entry point names the reference
+ * interface it replaces (file:line relative to the reference repo root).  Plain pointers and sizes only; no PCL,
+ * Eigen, ROS or torch types cross this boundary.  The C++ adapters that restore the reference's exact class
+ * signatures (LaserProcessingClass, OdomEstimationClass over pcl::PointCloud) are shown in INTEGRATION.md.
+ *
+ * Ownership: the caller owns host buffers.  floam_cloud / floam_lp / floam_odom handles own their device memory.
+ * Threading: a handle is used from one host thread at a time (the reference drives each class from one worker
+ * thread, src/odomEstimationNode.cpp:365, src/laserProcessingNode.cpp:212).  All handles on one device share
+ * one HIP stream, so work issued through different handles is ordered.
+ * Errors: every call returns floam_status; floam_last_error() gives a thread-local message.  Warnings
+ * (status >= 100) are non-fatal and mirror the reference's printf diagnostics; the pose is then left where the
+ * reference leaves it.
+ */
+#ifndef FLOAM_C_H
+#define FLOAM_C_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum floam_status {
+  FLOAM_OK = 0,
+  FLOAM_ERR_INVALID_ARGUMENT = 1,
+  FLOAM_ERR_DEVICE = 2,        /* HIP runtime / kernel launch failure, or no usable gfx950 device */
+  FLOAM_ERR_OUT_OF_MEMORY = 3,
+  FLOAM_ERR_UNSUPPORTED = 4,   /* input outside the kernels' envelope (e.g. a ring sector > 4096 points) */
+  FLOAM_ERR_COMM = 5,          /* RCCL failure in the sharded path */
+  /* non-fatal, same conditions as the reference's printf warnings */
+  FLOAM_WARN_MAP_TOO_SMALL = 100,       /* src/odomEstimationClass.cpp:112 "not enough points in map" */
+  FLOAM_WARN_FEW_CORRESPONDENCES = 101  /* src/odomEstimationClass.cpp:192-194, 247-249 (< 20 factors) */
+} floam_status;
+
+/* 32-byte point record, byte-compatible with vel_point::PointXYZIRT (include/lidar.h:14-32) and with
+ * pcl::PointXYZI (x,y,z,intensity at the same offsets); padding is written as pad0 = 1.0f, pad1 = pad2 = 0. */
+typedef struct floam_point {
+  float x, y, z, pad0;
+  float intensity;
+  uint16_t ring;
+  uint16_t pad1;
+  float time;
+  float pad2;
+} floam_point;
+
+/* lidar::Lidar (include/lidar.h:53-85): the fields the path reads. */
+typedef struct floam_lidar_params {
+  int num_lines;          /* /scan_line  -> N_SCANS (src/laserProcessingClass.cpp:78) */
+  double scan_period;     /* /scan_period (GetVelocity, include/odomEstimationClass.h:78) */
+  double vertical_angle;  /* /vertical_angle (not used on the path) */
+  double max_distance;    /* /max_dis (src/laserProcessingClass.cpp:15) */
+  double min_distance;    /* /min_dis */
+} floam_lidar_params;
+
+/* OdomEstimationClass::UpdateType (include/odomEstimationClass.h:56) */
+enum { FLOAM_VANILLA = 0, FLOAM_INITIAL_ITERATION = 1, FLOAM_REFINEMENT_AND_UPDATE = 2 };
+
+/* ------------------------------------------------------------------------------------------ device clouds */
+/* A device-resident point cloud (HBM), the stand-in for pcl::PointCloud<PointXYZIRT|PointXYZI>::Ptr.
+ * Its element count lives on the device; floam_cloud_size() synchronises to read it. */
+typedef struct floam_cloud floam_cloud;
+
+floam_status floam_cloud_create(int device, size_t capacity, floam_cloud** out);
+floam_status floam_cloud_destroy(floam_cloud* c);
+/* Replace the contents with n host points of `stride` bytes each (x,y,z,pad,intensity,ring,pad,time at the
+ * PointXYZIRT offsets; stride 32 = a pcl::PointCloud's points.data()).  Replaces pcl::fromROSMsg + copy. */
+floam_status floam_cloud_upload(floam_cloud* c, const void* host_points, size_t n, size_t stride);
+/* Copy up to `capacity` points to host (32-B records); *n_out = number of points in the cloud. Synchronises. */
+floam_status floam_cloud_download(const floam_cloud* c, void* host_points, size_t capacity, size_t* n_out);
+floam_status floam_cloud_size(const floam_cloud* c, size_t* n_out);
+floam_status floam_cloud_clear(floam_cloud* c);
+floam_status floam_cloud_copy(floam_cloud* dst, const floam_cloud* src);   /* device to device */
+void* floam_cloud_device_ptr(floam_cloud* c);                              /* 32-B records in HBM */
+
+/* ------------------------------------------------------------------------------- LaserProcessingClass */
+typedef struct floam_lp floam_lp;
+
+/* LaserProcessingClass() + init(lidar::Lidar) (include/laserProcessingClass.h:37-39) */
+floam_status floam_lp_create(const floam_lidar_params* p, int device, floam_lp** out);
+floam_status floam_lp_destroy(floam_lp* lp);
+/* featureExtraction(pc_in, pc_out_edge, pc_out_surf) (include/laserProcessingClass.h:40,
+ * src/laserProcessingClass.cpp:72-118).  Appends to edge/surf like the reference (never clears them). */
+floam_status floam_lp_feature_extraction(floam_lp* lp, const floam_cloud* in, floam_cloud* edge, floam_cloud* surf);
+
+/* -------------------------------------------------------------------------------- OdomEstimationClass */
+typedef struct floam_odom floam_odom;
+
+/* OdomEstimationClass() + init(lidar, map_resolution, loss_function) (include/odomEstimationClass.h:58-60,
+ * src/odomEstimationClass.cpp:7-26).  loss "huber" (any case) -> HuberLoss(0.1); anything else -> no loss (Q3). */
+floam_status floam_odom_create(const floam_lidar_params* p, double map_resolution, const char* loss_function,
+                               int device, floam_odom** out);
+floam_status floam_odom_destroy(floam_odom* o);
+/* initMapWithPoints(edge_in, surf_in) (src/odomEstimationClass.cpp:28-32): raw append, optimization_count = 12 */
+floam_status floam_odom_init_map(floam_odom* o, const floam_cloud* edge, const floam_cloud* surf);
+/* UpdatePointsToMapSelector(edge_in, surf_in, deskew) (src/odomEstimationClass.cpp:34-50).  With deskew the
+ * clouds are velocity-compensated IN PLACE, as the reference does (Q5). */
+floam_status floam_odom_update_selector(floam_odom* o, floam_cloud* edge, floam_cloud* surf, int deskew);
+/* updatePointsToMap(edge_in, surf_in, update_type) (src/odomEstimationClass.cpp:52-124) */
+floam_status floam_odom_update(floam_odom* o, const floam_cloud* edge, const floam_cloud* surf, int update_type);
+/* public member `odom` (include/odomEstimationClass.h:84): quaternion (x,y,z,w) + translation */
+floam_status floam_odom_get_pose(const floam_odom* o, double q_xyzw[4], double t[3]);
+floam_status floam_odom_get_last_pose(const floam_odom* o, double q_xyzw[4], double t[3]);
+/* GetVelocity() (include/odomEstimationClass.h:78) */
+floam_status floam_odom_get_velocity(const floam_odom* o, double v[3]);
+/* getMap(laserCloudMap) (src/odomEstimationClass.cpp:296-300): appends surf map then corner map */
+floam_status floam_odom_get_map(floam_odom* o, floam_cloud* out);
+/* public members laserCloudCornerMap / laserCloudSurfMap (include/odomEstimationClass.h:86-87) */
+floam_status floam_odom_get_map_sizes(floam_odom* o, size_t* corner, size_t* surf);
+floam_status floam_odom_download_maps(floam_odom* o, void* corner, size_t corner_cap, void* surf, size_t surf_cap);
+
+typedef struct floam_odom_stats {
+  int optimization_count;       /* value used by the last updatePointsToMap */
+  int solves;                   /* outer iterations (one ceres::Solve each) in the last call */
+  int edge_queries, surf_queries;       /* after VoxelGrid */
+  int edge_correspondences, surf_correspondences;   /* accepted factors in the last outer iteration */
+  int lm_iterations;            /* trust-region iterations of the last solve */
+  int map_updated;              /* KeyFrameUpdate() returned true */
+  size_t corner_map, surf_map;  /* map sizes after the call */
+  double final_cost;
+} floam_odom_stats;
+floam_status floam_odom_get_stats(const floam_odom* o, floam_odom_stats* s);
+
+/* Query sharding over ranks (one process per GPU): each rank runs the same calls on the same scans; the
+ * correspondence queries are split into `world` contiguous ranges and the normal equations (J^T J, J^T r, cost)
+ * are summed with one RCCL all-reduce per LM evaluation.  unique_id: 128 bytes from floam_comm_unique_id() on
+ * rank 0, broadcast by the caller (e.g. torch.distributed). */
+floam_status floam_comm_unique_id(void* unique_id_128);
+floam_status floam_odom_set_shard(floam_odom* o, int rank, int world, const void* unique_id_128);
+
+/* ------------------------------------------------------------------------------------------ misc */
+const char* floam_last_error(void);
+const char* floam_version(void);
+/* KeyFrameUpdate keeps a function-static `first` flag shared by every instance in the process
+ * (src/odomEstimationClass.cpp:323, quirk Q6); this resets it (tests/bench only). */
+void floam_reset_process_state(void);
+floam_status floam_device_synchronize(int device);
+
+/* Per-kernel timing with HIP events recorded on the library stream (bench.py's roofline leg). */
+typedef struct floam_kernel_timing {
+  char name[32];
+  long long launches;
+  double total_ms;
+  double algorithmic_bytes;   /* sum over launches of the algorithmic byte count */
+} floam_kernel_timing;
+floam_status floam_profile_enable(int device, int enable);
+floam_status floam_profile_read(int device, floam_kernel_timing* out, int max_entries, int* n_out);
+floam_status floam_profile_reset(int device);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FLOAM_C_H */

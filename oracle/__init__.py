@@ -1,0 +1,231 @@
+"""CPU ORACLE — test infrastructure only (tests/, __graft_entry__.smoke(), bench.py cpu_baseline leg).
+
+ctypes bindings over oracle/liboracle.so, the single-threaded C++ restatement of the FLOAM hot path
+(see oracle/oracle.hpp for the reference file:line map).  PARITY UNPINNED: the reference has no tests or
+fixtures and cannot be built here; the oracle is pinned by numpy/scipy cross-checks, known-answer tests and
+its own committed golden vectors (tests/golden/).
+
+Never imported by the product package ``floam_amd``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+c_double_p = C.POINTER(C.c_double)
+c_float_p = C.POINTER(C.c_float)
+c_int_p = C.POINTER(C.c_int)
+c_size_p = C.POINTER(C.c_size_t)
+
+
+def build(force: bool = False) -> str:
+    so = os.path.join(_HERE, "liboracle.so")
+    if force or not os.path.exists(so):
+        subprocess.run(["make", "-C", _HERE, "-s"], check=True)
+    return so
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        so = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(so):
+            build()
+        L = C.CDLL(so)
+        L.oracle_feature_extraction.argtypes = [C.c_int, C.c_double, C.c_double, C.c_void_p, C.c_size_t, C.c_int,
+                                                C.c_void_p, c_size_p, C.c_void_p, c_size_p, c_size_p]
+        L.oracle_feature_extraction.restype = C.c_int
+        L.oracle_voxel_grid.argtypes = [C.c_void_p, C.c_size_t, C.c_float, C.c_int, C.c_void_p, c_size_p]
+        L.oracle_voxel_grid.restype = C.c_int
+        L.oracle_crop_box.argtypes = [C.c_void_p, C.c_size_t, c_float_p, c_float_p, C.c_void_p, c_size_p]
+        L.oracle_crop_box.restype = C.c_int
+        L.oracle_knn.argtypes = [C.c_void_p, C.c_size_t, c_float_p, C.c_size_t, C.c_int, c_int_p, c_float_p]
+        L.oracle_eig_sym3.argtypes = [c_double_p, c_double_p, c_double_p]
+        L.oracle_plane_solve.argtypes = [c_double_p, c_double_p]
+        L.oracle_odom_create.argtypes = [C.c_int, C.c_double, C.c_double, C.c_double, C.c_double, C.c_char_p,
+                                         C.c_int]
+        L.oracle_odom_create.restype = C.c_void_p
+        for name in ("oracle_odom_destroy", "oracle_odom_clear_traces"):
+            getattr(L, name).argtypes = [C.c_void_p]
+        L.oracle_odom_init_map.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t]
+        L.oracle_odom_update_selector.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
+                                                  C.c_int]
+        L.oracle_odom_update.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_int]
+        L.oracle_odom_get_pose.argtypes = [C.c_void_p, c_double_p, c_double_p]
+        L.oracle_odom_get_last_pose.argtypes = [C.c_void_p, c_double_p, c_double_p]
+        L.oracle_odom_get_velocity.argtypes = [C.c_void_p, c_double_p]
+        L.oracle_odom_map_size.argtypes = [C.c_void_p, C.c_int]
+        L.oracle_odom_map_size.restype = C.c_size_t
+        L.oracle_odom_get_map.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
+        L.oracle_odom_optimization_count.argtypes = [C.c_void_p]
+        L.oracle_odom_optimization_count.restype = C.c_int
+        L.oracle_odom_num_traces.argtypes = [C.c_void_p]
+        L.oracle_odom_num_traces.restype = C.c_size_t
+        L.oracle_odom_get_trace.argtypes = [C.c_void_p, C.c_size_t, c_double_p]
+        L.oracle_reset_process_statics.argtypes = []
+        _LIB = L
+    return _LIB
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def _as_points(a: np.ndarray) -> np.ndarray:
+    from floam_amd.synth import POINT_DTYPE
+    a = np.ascontiguousarray(a)
+    assert a.dtype.itemsize == 32, a.dtype
+    return a.view(POINT_DTYPE) if a.dtype != POINT_DTYPE else a
+
+
+def feature_extraction(points: np.ndarray, num_lines: int, min_dis: float = 0.5, max_dis: float = 90.0,
+                       canonical: bool = False):
+    """LaserProcessingClass::featureExtraction (src/laserProcessingClass.cpp:72-118).
+    Returns (edge, surf, stats) with stats = (out_of_range_ring_points, sector_ties)."""
+    from floam_amd.synth import POINT_DTYPE
+    pts = _as_points(points)
+    n = pts.shape[0]
+    e = np.zeros(n, POINT_DTYPE)
+    s = np.zeros(n, POINT_DTYPE)
+    ne, ns = C.c_size_t(n), C.c_size_t(n)
+    st = (C.c_size_t * 2)()
+    rc = lib().oracle_feature_extraction(num_lines, min_dis, max_dis, _ptr(pts), n, int(canonical), _ptr(e),
+                                         C.byref(ne), _ptr(s), C.byref(ns), st)
+    assert rc == 0
+    return e[: ne.value].copy(), s[: ns.value].copy(), (st[0], st[1])
+
+
+def voxel_grid(points: np.ndarray, leaf: float, stable: bool = True) -> np.ndarray:
+    from floam_amd.synth import POINT_DTYPE
+    pts = _as_points(points)
+    n = pts.shape[0]
+    out = np.zeros(max(n, 1), POINT_DTYPE)
+    no = C.c_size_t(max(n, 1))
+    rc = lib().oracle_voxel_grid(_ptr(pts), n, C.c_float(leaf), int(stable), _ptr(out), C.byref(no))
+    assert rc == 0
+    return out[: no.value].copy()
+
+
+def crop_box(points: np.ndarray, mn, mx) -> np.ndarray:
+    from floam_amd.synth import POINT_DTYPE
+    pts = _as_points(points)
+    n = pts.shape[0]
+    out = np.zeros(max(n, 1), POINT_DTYPE)
+    no = C.c_size_t(max(n, 1))
+    a = (C.c_float * 3)(*mn)
+    b = (C.c_float * 3)(*mx)
+    rc = lib().oracle_crop_box(_ptr(pts), n, a, b, _ptr(out), C.byref(no))
+    assert rc == 0
+    return out[: no.value].copy()
+
+
+def knn(map_points: np.ndarray, queries: np.ndarray, k: int = 5):
+    """KdTreeFLANN nearestKSearch restated. queries: (n, 3) float32. Returns (idx (n,k) int32, sqd (n,k) f32)."""
+    mp = _as_points(map_points)
+    q = np.ascontiguousarray(queries, dtype=np.float32)
+    nq = q.shape[0]
+    idx = np.full((nq, k), -1, np.int32)
+    sqd = np.full((nq, k), np.inf, np.float32)
+    lib().oracle_knn(_ptr(mp), mp.shape[0], q.ctypes.data_as(c_float_p), nq, k, idx.ctypes.data_as(c_int_p),
+                     sqd.ctypes.data_as(c_float_p))
+    return idx, sqd
+
+
+def eig_sym3(a: np.ndarray):
+    a = np.ascontiguousarray(a, dtype=np.float64).reshape(9)
+    ev = np.zeros(3)
+    vec = np.zeros(9)
+    lib().oracle_eig_sym3(a.ctypes.data_as(c_double_p), ev.ctypes.data_as(c_double_p),
+                          vec.ctypes.data_as(c_double_p))
+    return ev, vec.reshape(3, 3).T   # columns = eigenvectors
+
+
+def plane_solve(a: np.ndarray) -> np.ndarray:
+    a = np.ascontiguousarray(a, dtype=np.float64).reshape(15)
+    x = np.zeros(3)
+    lib().oracle_plane_solve(a.ctypes.data_as(c_double_p), x.ctypes.data_as(c_double_p))
+    return x
+
+
+class Odometry:
+    """OdomEstimationClass restated (src/odomEstimationClass.cpp).  Poses are (q_xyzw, t)."""
+
+    VANILLA, INITIAL_ITERATION, REFINEMENT_AND_UPDATE = 0, 1, 2
+
+    def __init__(self, num_lines: int, scan_period: float = 0.1, min_dis: float = 0.5, max_dis: float = 90.0,
+                 map_resolution: float = 0.1, loss: str = "Cauchy", stable_voxel: bool = True):
+        self._L = lib()
+        self._h = self._L.oracle_odom_create(num_lines, scan_period, min_dis, max_dis, map_resolution,
+                                             loss.encode(), int(stable_voxel))
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            self._L.oracle_odom_destroy(h)
+            self._h = None
+
+    def init_map(self, edge: np.ndarray, surf: np.ndarray):
+        e, s = _as_points(edge), _as_points(surf)
+        self._L.oracle_odom_init_map(self._h, _ptr(e), e.shape[0], _ptr(s), s.shape[0])
+
+    def update_selector(self, edge: np.ndarray, surf: np.ndarray, deskew: bool = True):
+        """Mutates edge/surf in place when deskew (Q5)."""
+        assert edge.flags.c_contiguous and surf.flags.c_contiguous
+        self._L.oracle_odom_update_selector(self._h, _ptr(edge), edge.shape[0], _ptr(surf), surf.shape[0],
+                                            int(deskew))
+
+    def update(self, edge: np.ndarray, surf: np.ndarray, update_type: int = 0):
+        e, s = _as_points(edge), _as_points(surf)
+        self._L.oracle_odom_update(self._h, _ptr(e), e.shape[0], _ptr(s), s.shape[0], update_type)
+
+    def pose(self):
+        q, t = np.zeros(4), np.zeros(3)
+        self._L.oracle_odom_get_pose(self._h, q.ctypes.data_as(c_double_p), t.ctypes.data_as(c_double_p))
+        return q, t
+
+    def last_pose(self):
+        q, t = np.zeros(4), np.zeros(3)
+        self._L.oracle_odom_get_last_pose(self._h, q.ctypes.data_as(c_double_p), t.ctypes.data_as(c_double_p))
+        return q, t
+
+    def velocity(self):
+        v = np.zeros(3)
+        self._L.oracle_odom_get_velocity(self._h, v.ctypes.data_as(c_double_p))
+        return v
+
+    def map(self, which: int) -> np.ndarray:
+        from floam_amd.synth import POINT_DTYPE
+        n = self._L.oracle_odom_map_size(self._h, which)
+        out = np.zeros(n, POINT_DTYPE)
+        if n:
+            self._L.oracle_odom_get_map(self._h, which, _ptr(out))
+        return out
+
+    @property
+    def optimization_count(self) -> int:
+        return self._L.oracle_odom_optimization_count(self._h)
+
+    def traces(self):
+        n = self._L.oracle_odom_num_traces(self._h)
+        out = []
+        for i in range(n):
+            b = np.zeros(49)
+            self._L.oracle_odom_get_trace(self._h, i, b.ctypes.data_as(c_double_p))
+            out.append(dict(n_edge_queries=int(b[0]), n_surf_queries=int(b[1]), n_edge_corr=int(b[2]),
+                            n_surf_corr=int(b[3]), iterations=int(b[4]), successful=int(b[5]),
+                            initial_cost=b[6], final_cost=b[7], x_in=b[8:15].copy(), x_out=b[15:22].copy(),
+                            H0=b[22:43].copy(), g0=b[43:49].copy()))
+        return out
+
+    def clear_traces(self):
+        self._L.oracle_odom_clear_traces(self._h)
+
+
+def reset_process_statics():
+    lib().oracle_reset_process_statics()

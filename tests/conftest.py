@@ -1,0 +1,32 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU and the built libfloam_amd.so")
+    config.addinivalue_line("markers", "slow: multi-second CPU test")
+
+
+@pytest.fixture(scope="session")
+def oracle_lib():
+    import oracle
+    oracle.build()
+    return oracle
+
+
+@pytest.fixture(scope="session")
+def floam_gpu():
+    """The HIP product path.  GPU tests must never pass on a fallback: fail loudly if the library or device is
+    missing."""
+    import floam_amd
+    from floam_amd import _ffi
+    _ffi.load()   # raises if the .so is not built
+    c = floam_amd.DeviceCloud()   # raises FloamError(ERR_DEVICE) without a gfx950 device
+    c.close()
+    return floam_amd
