@@ -1,0 +1,247 @@
+#!/usr/bin/env python3
+"""Benchmark: scans/sec of the FLOAM scan-to-map odometry hot path on MI355X.
+
+One step = one scan through the reference's two operators, exactly as the nodes drive them:
+LaserProcessingClass::featureExtraction (src/laserProcessingNode.cpp:129) followed by
+OdomEstimationClass::UpdatePointsToMapSelector(edge, surf, deskew=true) (src/odomEstimationNode.cpp:228), with the
+launch-file defaults (launch/structor_odom.launch: map_resolution 0.1, deskew on, loss "Cauchy" -> no robust
+loss, min/max_dis 0.5/90).  The raw scans are resident in HBM before the timed region; the host reads the pose
+back after every update call like the node does.
+
+Workload (BASELINE.json configs[2], the headline): 64-ring HDL-64-style synthetic scans (~130k points), local map
+prefilled with 200k edge+surf points through initMapWithPoints, steady state (the warm-up covers the
+optimization_count 12 -> 2 ramp).
+
+--gpus N > 1 (launched by torch.distributed.run): every rank runs the same scan sequence and shards the
+correspondence queries; the normal equations are summed with one RCCL all-reduce per LM evaluation
+(SURVEY.md §8 e).  value = scans of the one sequence per second (strong scaling).  --mode replica runs N
+independent sequences instead (weak scaling).
+
+Prints ONE JSON line on rank 0 (contract in the task statement), with "roofline" for the dominant kernel
+(the surf correspondence kernel, HIP events on the library stream over the timed region) and "cpu_baseline"
+(the CPU oracle — the reference path restated, single-threaded — timed on this host on a bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (/opt/skills/guides/MI355X_MICROARCH.md: 8.0 TB/s)
+METRIC = "scans/sec scan-to-map odometry, 64-ring ~130k pts; pose RMSE vs reference"
+MAP_RES, LOSS, MIN_DIS, MAX_DIS, SCAN_PERIOD = 0.1, "Cauchy", 0.5, 90.0, 0.1
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def prefill_map(synth, oracle_fe, config, R, target):
+    """Edge/surf features of scan 0 (sensor frame == map frame) plus features of earlier scans on the ground-truth
+    trajectory, transformed into the map frame, until `target` points (the raw map initMapWithPoints receives)."""
+    e0, s0 = oracle_fe(synth.generate_scan(config, 0), R)
+    E, S = [synth.to_xyzi(e0)], [synth.to_xyzi(s0)]
+    n = e0.shape[0] + s0.shape[0]
+    k = -3
+    while n < target:
+        raw = synth.generate_scan(config, k)
+        e, s = oracle_fe(raw, R)
+        T = synth.gt_pose_matrix(k)
+        E.append(synth.to_xyzi(synth.transform_points(e, T)))
+        S.append(synth.to_xyzi(synth.transform_points(s, T)))
+        n += e.shape[0] + s.shape[0]
+        k -= 3
+    E, S = np.concatenate(E), np.concatenate(S)
+    extra = E.shape[0] + S.shape[0] - target
+    if target and extra > 0:   # trim the surf tail to hit the stated size exactly
+        S = S[: S.shape[0] - extra]
+    return E, S
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--config", default="c3")
+    ap.add_argument("--mode", choices=["shard", "replica"], default="shard")
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
+    ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--json-out", default="")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist   # control plane only (barrier, id broadcast, max-time); data: RCCL
+        dist.init_process_group(backend="gloo")
+
+    import floam_amd
+    import oracle
+    from floam_amd import _ffi, synth
+    from floam_amd.odom_estimation import comm_unique_id, reset_process_state
+
+    L = _ffi.load()
+    dev = local_rank
+    cfg = args.config
+    model = synth.lidar_model(cfg)
+    R = model.rings
+    target = synth.MAP_PREFILL.get(cfg, 0)
+
+    def oracle_fe(raw, R_):
+        e, s, _ = oracle.feature_extraction(raw, R_, MIN_DIS, MAX_DIS, canonical=True)
+        return e, s
+
+    t0 = time.time()
+    n_scans = args.warmup + args.steps
+    scan_offset = rank * 1000 if args.mode == "replica" else 0
+    raws = [synth.generate_scan(cfg, scan_offset + k) for k in range(1, n_scans + 1)]
+    mapE, mapS = prefill_map(synth, oracle_fe, cfg, R, target)
+    log(f"[rank {rank}] generated {n_scans} scans ({raws[0].shape[0]} pts) + map {mapE.shape[0]}+{mapS.shape[0]} "
+        f"in {time.time() - t0:.1f}s")
+
+    params = floam_amd.LidarParams(num_lines=R, scan_period=SCAN_PERIOD, vertical_angle=2.0, max_distance=MAX_DIS,
+                                   min_distance=MIN_DIS)
+    reset_process_state()
+    lp = floam_amd.LaserProcessingClass(device=dev)
+    lp.init(params)
+    odo = floam_amd.OdomEstimationClass(device=dev)
+    odo.init(params, MAP_RES, LOSS)
+    if world > 1 and args.mode == "shard":
+        uid = [comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        odo.set_shard(rank, world, uid[0])
+    d_raw = [floam_amd.DeviceCloud(r, device=dev) for r in raws]       # inputs resident in HBM
+    odo.initMapWithPoints(floam_amd.DeviceCloud(mapE, device=dev), floam_amd.DeviceCloud(mapS, device=dev))
+    d_edge, d_surf = floam_amd.DeviceCloud(device=dev), floam_amd.DeviceCloud(device=dev)
+
+    poses = []
+
+    def step(k):
+        d_edge.clear()
+        d_surf.clear()
+        lp.featureExtraction(d_raw[k], d_edge, d_surf)
+        odo.UpdatePointsToMapSelector(d_edge, d_surf, True)
+        poses.append(odo.pose())
+
+    def barrier_sync():
+        if dist is not None:
+            dist.barrier()
+        _ffi.check(L.floam_device_synchronize(dev))
+
+    for k in range(args.warmup):
+        step(k)
+    if not args.no_roofline:
+        _ffi.check(L.floam_profile_reset(dev))
+        _ffi.check(L.floam_profile_enable(dev, 1))   # FLOAM_PROF_KNN: events around the two kNN kernels only
+    barrier_sync()
+    t_start = time.perf_counter()
+    for k in range(args.warmup, n_scans):
+        step(k)
+    barrier_sync()
+    elapsed = time.perf_counter() - t_start
+    _ffi.check(L.floam_profile_enable(dev, 0))
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    stats = odo.stats()
+
+    roof = None
+    if not args.no_roofline:
+        arr = (_ffi.KernelTiming * 16)()
+        n = C.c_int()
+        _ffi.check(L.floam_profile_read(dev, arr, 16, C.byref(n)))
+        timings = {arr[i].name.decode(): arr[i] for i in range(min(n.value, 16))}
+        kt = timings.get("knn_surf")
+        if kt is not None and kt.launches > 0:
+            avg_ms = kt.total_ms / kt.launches
+            bytes_per = kt.algorithmic_bytes / kt.launches
+            ach = bytes_per / (avg_ms * 1e-3) / 1e9
+            roof = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
+                    "kernel": "corr_kernel<false> (surf kNN + plane geometry)", "avg_us": round(avg_ms * 1e3, 2),
+                    "launches": int(kt.launches), "algorithmic_bytes_per_launch": round(bytes_per)}
+            ke = timings.get("knn_edge")
+            if ke is not None and ke.launches:
+                roof["edge_kernel_avg_us"] = round(ke.total_ms / ke.launches * 1e3, 2)
+
+    cpu = None
+    pose_err = None
+    if rank == 0 and args.cpu_baseline_seconds > 0:
+        # the reference path restated (oracle), single-threaded, same scans from scan 1 and the same prefilled
+        # map; warm-up scans (optimization_count ramp) untimed, then steady-state scans for ~N seconds.
+        oracle.reset_process_statics()
+        ref = oracle.Odometry(R, SCAN_PERIOD, MIN_DIS, MAX_DIS, MAP_RES, LOSS, stable_voxel=True)
+        ref.init_map(mapE, mapS)
+        t_cpu, n_cpu, errs = 0.0, 0, []
+        for k in range(n_scans):
+            t1 = time.perf_counter()
+            e, s = oracle_fe(raws[k], R)
+            ref.update_selector(e, s, True)
+            dt = time.perf_counter() - t1
+            qr, tr = ref.pose()
+            qg, tg = poses[k]
+            errs.append((float(np.linalg.norm(tr - tg)), 2 * math.acos(min(1.0, abs(float(np.dot(qr, qg)))))))
+            if k >= min(args.warmup, 6):
+                t_cpu += dt
+                n_cpu += 1
+                if t_cpu >= args.cpu_baseline_seconds:
+                    break
+        if n_cpu:
+            cpu = {"value": round(n_cpu / t_cpu, 4), "unit": "scans/s", "cores": 1, "kind": "port",
+                   "sample": f"{cfg} scans {min(args.warmup, 6) + 1}..{min(args.warmup, 6) + n_cpu} (steady state) "
+                             f"of the same sequence, featureExtraction + UpdatePointsToMapSelector, oracle/ "
+                             f"single thread, {os.cpu_count()} host cores present"}
+        pose_err = {"scans_compared": len(errs), "max_dt_m": max(e[0] for e in errs),
+                    "max_drot_rad": max(e[1] for e in errs)}
+
+    if rank == 0:
+        gt_err = []
+        for k, (q, t) in enumerate(poses):
+            T = synth.gt_pose_matrix(scan_offset + k + 1)
+            gt_err.append(float(np.linalg.norm(T[:3, 3] - t)))
+        total_scans = args.steps * (world if args.mode == "replica" else 1)
+        value = total_scans / elapsed
+        out = {
+            "metric": METRIC, "value": round(value, 3), "unit": "scans/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,
+            "scaling": "weak" if args.mode == "replica" else "strong", "vs_baseline": None, "dtype": "fp32+fp64",
+            "data": "synthetic (seeded ring-lidar ray-cast scene, floam_amd/synth.py)",
+            "config": {"workload": f"{cfg}: {R}-ring synthetic scans ({raws[0].shape[0]} pts), map prefilled "
+                                   f"{target} pts, deskew on, loss {LOSS} (no robust loss, Q3), map_res {MAP_RES}",
+                       "rings": R, "points_per_scan": int(raws[0].shape[0]), "map_prefill": target,
+                       "parallelism": (f"query-shard x{world} (RCCL all-reduce of J^T J)" if args.mode == "shard"
+                                       else f"replica x{world}")},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "pose_vs_oracle": pose_err,
+            "pose_vs_ground_truth_rmse_m": round(math.sqrt(sum(e * e for e in gt_err) / len(gt_err)), 5),
+            "last_scan_stats": {k: (int(v) if isinstance(v, int) else v) for k, v in stats.items()},
+        }
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    odo.close()
+    lp.close()
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

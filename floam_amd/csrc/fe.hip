@@ -144,7 +144,9 @@ __device__ __forceinline__ void sector_range(int n_r, int s, int& a, int& b) {
   b = (s == 5) ? T - 1 : L * (s + 1) - 1;
 }
 
-template <int MAXSEC>
+// Sectors with MINSEC < m <= MAXSEC are processed; the small-LDS instantiation runs first and the large one only
+// picks up the (rare) longer sectors, so the common case keeps several workgroups per CU.
+template <int MINSEC, int MAXSEC, bool LAST>
 __global__ __launch_bounds__(kSectorThreads) void fe_sector(const int* __restrict__ ring_count,
                                                             const float4* __restrict__ ring_xyz,
                                                             int* __restrict__ sec_edge_cnt, int* __restrict__ sec_edge_pos,
@@ -164,14 +166,15 @@ __global__ __launch_bounds__(kSectorThreads) void fe_sector(const int* __restric
   const int sec = blockIdx.x;
   const int n_r = ring_count[r];
   if (n_r < 131) {                                    // :89
-    if (threadIdx.x == 0) { sec_edge_cnt[sec] = 0; sec_surf_cnt[sec] = 0; }
+    if (MINSEC == 0 && threadIdx.x == 0) { sec_edge_cnt[sec] = 0; sec_surf_cnt[sec] = 0; }
     return;
   }
   int a, b;
   sector_range(n_r, s, a, b);
   const int m = b - a;
+  if (m <= MINSEC) return;
   if (m > MAXSEC) {
-    if (threadIdx.x == 0) {
+    if (LAST && threadIdx.x == 0) {
       atomicOr(status, FE_STATUS_SECTOR_TOO_LONG);
       sec_edge_cnt[sec] = 0;
       sec_surf_cnt[sec] = 0;
@@ -325,8 +328,11 @@ __global__ __launch_bounds__(kSectorThreads) void fe_output(const PointRec* __re
   }
 }
 
+// Advances the output counts, publishes (edge count, surf count, status) for one D2H copy and re-zeroes the
+// per-call counters for the next call (so no memset nodes are needed).
 __global__ void fe_commit(int n_sectors, const int* __restrict__ sec_edge_cnt, const int* __restrict__ sec_surf_cnt,
-                          int* __restrict__ edge_count, int* __restrict__ surf_count) {
+                          int* __restrict__ edge_count, int* __restrict__ surf_count, int* __restrict__ ring_count,
+                          int num_lines, int* __restrict__ status, int* __restrict__ out3) {
   __shared__ int red[2][4];
   int pe = 0, ps = 0;
   for (int k = threadIdx.x; k < n_sectors; k += blockDim.x) {
@@ -348,7 +354,12 @@ __global__ void fe_commit(int n_sectors, const int* __restrict__ sec_edge_cnt, c
     for (int w = 0; w < (int)(blockDim.x >> 6); ++w) { te += red[0][w]; ts += red[1][w]; }
     edge_count[0] += te;
     surf_count[0] += ts;
+    out3[0] = edge_count[0];
+    out3[1] = surf_count[0];
+    out3[2] = *status;
+    *status = 0;
   }
+  for (int r = threadIdx.x; r < num_lines; r += blockDim.x) ring_count[r] = 0;
 }
 
 }  // namespace
@@ -358,14 +369,21 @@ void fe_launch(FeScratch& sc, const FeParams& prm, const PointRec* d_in, int n, 
   const int R = prm.num_lines;
   const int n_pad = ((n + 8191) / 8192) * 8192;   // whole uint4 groups for every bucket thread
   sc.keys.reserve(n_pad);
+  if (sc.ring_count.cap < (size_t)R) sc.zeroed = false;
   sc.ring_count.reserve(R);
+  sc.out3.reserve(4);
   sc.ring_idx.reserve(n + 16);
   sc.ring_xyz.reserve(n + 16);
   sc.sec_edge_cnt.reserve(6 * R);
   sc.sec_surf_cnt.reserve(6 * R);
   sc.sec_edge_pos.reserve(6 * R * kMaxEdgesPerSector);
   sc.surf_pos.reserve(n + 16);
-  FLOAM_HIP(hipMemsetAsync(sc.ring_count.p, 0, sizeof(int) * R, st));
+  if (!sc.zeroed || sc.zeroed_lines < R) {   // fe_commit re-zeroes the counters at the end of every call
+    FLOAM_HIP(hipMemsetAsync(sc.ring_count.p, 0, sizeof(int) * sc.ring_count.cap, st));
+    FLOAM_HIP(hipMemsetAsync(sc.status, 0, sizeof(int), st));
+    sc.zeroed = true;
+    sc.zeroed_lines = R;
+  }
   const int tb = 256;
   hipLaunchKernelGGL(fe_keys, dim3(div_up(n_pad, tb)), dim3(tb), sizeof(int) * R, st, d_in, n, R, prm.min_distance,
                      prm.max_distance, sc.keys.p, n_pad, sc.ring_count.p, sc.status);
@@ -373,13 +391,17 @@ void fe_launch(FeScratch& sc, const FeParams& prm, const PointRec* d_in, int n, 
   hipLaunchKernelGGL(fe_bucket, dim3(R), dim3(kBucketThreads), 0, st, d_in, n_pad, sc.keys.p, sc.ring_count.p,
                      sc.ring_idx.p, sc.ring_xyz.p);
   FLOAM_LAUNCH_CHECK();
-  // the longest possible sector is (max ring size - 10) / 6 + 5 <= n / 6 + 5
-  if (n / 6 + 8 <= 1024) {
-    hipLaunchKernelGGL(fe_sector<1024>, dim3(6 * R), dim3(kSectorThreads), 0, st, sc.ring_count.p, sc.ring_xyz.p,
-                       sc.sec_edge_cnt.p, sc.sec_edge_pos.p, sc.sec_surf_cnt.p, sc.surf_pos.p, sc.status);
+  // the longest possible sector is (max ring size - 10) / 6 <= n / 6: the 4096 pass is only needed beyond 1024
+  const bool big = n / 6 + 8 > 1024;
+  if (big) {
+    hipLaunchKernelGGL((fe_sector<0, 1024, false>), dim3(6 * R), dim3(kSectorThreads), 0, st, sc.ring_count.p,
+                       sc.ring_xyz.p, sc.sec_edge_cnt.p, sc.sec_edge_pos.p, sc.sec_surf_cnt.p, sc.surf_pos.p, sc.status);
+    FLOAM_LAUNCH_CHECK();
+    hipLaunchKernelGGL((fe_sector<1024, 4096, true>), dim3(6 * R), dim3(kSectorThreads), 0, st, sc.ring_count.p,
+                       sc.ring_xyz.p, sc.sec_edge_cnt.p, sc.sec_edge_pos.p, sc.sec_surf_cnt.p, sc.surf_pos.p, sc.status);
   } else {
-    hipLaunchKernelGGL(fe_sector<4096>, dim3(6 * R), dim3(kSectorThreads), 0, st, sc.ring_count.p, sc.ring_xyz.p,
-                       sc.sec_edge_cnt.p, sc.sec_edge_pos.p, sc.sec_surf_cnt.p, sc.surf_pos.p, sc.status);
+    hipLaunchKernelGGL((fe_sector<0, 1024, true>), dim3(6 * R), dim3(kSectorThreads), 0, st, sc.ring_count.p,
+                       sc.ring_xyz.p, sc.sec_edge_cnt.p, sc.sec_edge_pos.p, sc.sec_surf_cnt.p, sc.surf_pos.p, sc.status);
   }
   FLOAM_LAUNCH_CHECK();
   hipLaunchKernelGGL(fe_output, dim3(6 * R), dim3(kSectorThreads), 0, st, d_in, sc.ring_count.p, sc.ring_idx.p,
@@ -387,7 +409,7 @@ void fe_launch(FeScratch& sc, const FeParams& prm, const PointRec* d_in, int n, 
                      surf_out, surf_count);
   FLOAM_LAUNCH_CHECK();
   hipLaunchKernelGGL(fe_commit, dim3(1), dim3(256), 0, st, 6 * R, sc.sec_edge_cnt.p, sc.sec_surf_cnt.p, edge_count,
-                     surf_count);
+                     surf_count, sc.ring_count.p, R, sc.status, sc.out3.p);
   FLOAM_LAUNCH_CHECK();
 }
 

@@ -14,7 +14,10 @@ struct FeScratch {
   DevBuf<uint16_t> keys;
   DevBuf<int> ring_count, ring_idx, sec_edge_cnt, sec_surf_cnt, sec_edge_pos, surf_pos;
   DevBuf<float4> ring_xyz;
+  DevBuf<int> out3;        // edge count, surf count, status after the call (one D2H)
   int* status = nullptr;   // device int, owned by the caller
+  bool zeroed = false;
+  int zeroed_lines = 0;
 };
 
 // Appends edge/surf features of d_in[0, n) to edge_out/surf_out at their device counts (which are advanced).

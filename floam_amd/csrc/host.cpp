@@ -13,6 +13,8 @@
 
 #include <algorithm>
 #include <cctype>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -38,7 +40,7 @@ struct PendingTiming {
 struct DeviceCtx {
   int device = 0;
   hipStream_t stream = nullptr;
-  bool profile = false;
+  int profile = 0;   // bitmask of FLOAM_PROF_* categories
   std::vector<PendingTiming> pending;
   std::vector<hipEvent_t> free_events;
   std::map<std::string, floam_kernel_timing> totals;
@@ -100,14 +102,14 @@ struct ProfScope {
   const char* name;
   double bytes;
   hipEvent_t e0 = nullptr;
-  ProfScope(DeviceCtx& ctx, const char* n, double b = 0.0) : c(ctx), name(n), bytes(b) {
-    if (c.profile) {
+  ProfScope(DeviceCtx& ctx, const char* n, int category, double b = 0.0) : c(ctx), name(n), bytes(b) {
+    if (c.profile & category) {
       e0 = c.get_event();
       FLOAM_HIP(hipEventRecord(e0, c.stream));
     }
   }
   ~ProfScope() {
-    if (c.profile && e0) {
+    if (e0) {
       hipEvent_t e1 = c.get_event();
       (void)hipEventRecord(e1, c.stream);
       c.pending.push_back(PendingTiming{name, e0, e1, bytes});
@@ -187,10 +189,14 @@ struct floam_odom {
   bool grid_dirty = true;
   CorrSet ce, cs;
   DevBuf<double> partials, sums;
+  DevBuf<unsigned> step_counter;
+  DevBuf<unsigned long long> dbg_stamps;   // FLOAM_DEBUG_STAMPS=1: lm_step segment times (diagnostic)
   DevBuf<LMState> lm;
-  HostBuf<LMState> h_lm;
-  HostBuf<int> h_cnt;   // dE, dS, mapE, mapS
-  HostBuf<double> h_x;
+  DevBuf<UpdateStatus> ustat;
+  HostBuf<UpdateStatus> h_ustat;
+  DevBuf<unsigned long long> prof_bytes;
+  DevBuf<uint32_t> traffic_set;
+  bool prof_bytes_init = false;
   // pose state (host, double)
   Pose odom = pose_identity(), last_odom = pose_identity();
   double parameters[7] = {0, 0, 0, 1, 0, 0, 0};
@@ -279,62 +285,89 @@ void odom_update(floam_odom* o, const floam_cloud* edge, const floam_cloud* surf
   o->dS.reserve(std::max(ns_ub, 1));
   o->cnt.reserve(4);
   {
-    ProfScope ps(ctx, "voxel_downsample");
+    ProfScope ps(ctx, "voxel_downsample", FLOAM_PROF_CLOUD);
     // VelToIntensityCopy + downSamplingToMap (:53-54, :75, :137-142)
     voxel_launch(o->vs, edge->pts.p, edge->count.p, ne_ub, o->leafE, o->dE.p, o->cnt.p + 0, st);
     voxel_launch(o->vs, surf->pts.p, surf->count.p, ns_ub, o->leafS, o->dS.p, o->cnt.p + 1, st);
   }
   const int mE_ub = (int)o->mapE_n, mS_ub = (int)o->mapS_n;   // exact or upper bounds
   if (o->grid_dirty) {
-    ProfScope ps(ctx, "grid_build");
+    ProfScope ps(ctx, "grid_build", FLOAM_PROF_CLOUD);
     grid_build_launch(o->gE, o->gsc, o->mapE.pts.p, o->mapE.count.p, std::max(mE_ub, 1), st);
     grid_build_launch(o->gS, o->gsc, o->mapS.pts.p, o->mapS.count.p, std::max(mS_ub, 1), st);
     o->grid_dirty = false;
   }
   o->lm.reserve(1);
-  o->h_lm.reserve(1);
-  o->h_cnt.reserve(4);
-  o->h_x.reserve(8);
-  std::memcpy(o->h_x.p, o->parameters, sizeof(double) * 7);
-  FLOAM_HIP(hipMemcpyAsync(o->lm.p->x, o->h_x.p, sizeof(double) * 7, hipMemcpyHostToDevice, st));
   o->partials.reserve((size_t)LM_NSUM * 512);
+  if (!o->step_counter.p) {
+    o->step_counter.reserve(1);
+    FLOAM_HIP(hipMemsetAsync(o->step_counter.p, 0, sizeof(unsigned), st));
+    if (std::getenv("FLOAM_DEBUG_STAMPS")) {
+      o->dbg_stamps.reserve(8);
+      FLOAM_HIP(hipMemsetAsync(o->dbg_stamps.p, 0, sizeof(unsigned long long) * 8, st));
+    }
+  }
+  o->prof_bytes.reserve(2);
+  if (!o->prof_bytes_init) {
+    FLOAM_HIP(hipMemsetAsync(o->prof_bytes.p, 0, sizeof(unsigned long long) * 2, st));
+    o->prof_bytes_init = true;
+  }
   o->sums.reserve(LM_NSUM);
   const QuerySet qe{o->dE.p, o->cnt.p + 0, ne_ub};
   const QuerySet qs{o->dS.p, o->cnt.p + 1, ns_ub};
   const bool sharded = o->world > 1;
   for (int it = 0; it < o->optimization_count; ++it) {
+    lm_init_launch(o->lm.p, it == 0 ? o->parameters : nullptr, st);   // first solve starts at the prediction
     {
-      ProfScope ps(ctx, "knn_correspondences");
-      corr_launch(o->lm.p, qe, o->gE, o->mapE.count.p, qs, o->gS, o->mapS.count.p, o->ce, o->cs, o->rank, o->world,
-                  st);
+      ProfScope ps(ctx, "knn_edge", FLOAM_PROF_KNN);
+      corr_launch(true, o->lm.p, qe, o->gE, o->mapE.pts.p, o->mapE.count.p, o->mapS.count.p, o->ce, o->rank,
+                  o->world, st);
+    }
+    {
+      ProfScope ps(ctx, "knn_surf", FLOAM_PROF_KNN);
+      corr_launch(false, o->lm.p, qs, o->gS, o->mapS.pts.p, o->mapE.count.p, o->mapS.count.p, o->cs, o->rank,
+                  o->world, st);
+    }
+    if (ctx.profile & FLOAM_PROF_KNN) {   // untimed: algorithmic bytes of the two launches above
+      knn_traffic_launch(o->lm.p, qe, o->gE, o->ce, 8 * EDGE_FIELDS, o->rank, o->world, o->traffic_set,
+                         o->prof_bytes.p + 0, st);
+      knn_traffic_launch(o->lm.p, qs, o->gS, o->cs, 8 * SURF_FIELDS, o->rank, o->world, o->traffic_set,
+                         o->prof_bytes.p + 1, st);
     }
     // iteration zero + at most max_num_iterations = 4 candidates (odomEstimationClass.cpp:102)
     for (int ev = 0; ev < 5; ++ev) {
-      int nblk;
-      {
-        ProfScope ps(ctx, "lm_evaluate");
-        nblk = lm_eval_launch(o->lm.p, o->ce, ne_ub, o->cs, ns_ub, o->huber, o->partials.p, st);
-      }
-      ProfScope ps(ctx, "lm_control");
+      ProfScope ps(ctx, "lm_step", FLOAM_PROF_LM);
       if (sharded) {
+        const int nblk = lm_eval_launch(o->lm.p, o->ce, o->cnt.p + 0, ne_ub, o->cs, o->cnt.p + 1, ns_ub, o->huber,
+                                        o->partials.p, st);
         lm_reduce_launch(o->partials.p, nblk, o->sums.p, st);
         allreduce_sums(o, ctx);
         lm_control_launch(o->lm.p, o->sums.p, 0, st);
       } else {
-        lm_control_launch(o->lm.p, o->partials.p, nblk, st);
+        lm_step_launch(o->lm.p, o->ce, o->cnt.p + 0, ne_ub, o->cs, o->cnt.p + 1, ns_ub, o->huber, o->partials.p,
+                       o->step_counter.p, st, o->dbg_stamps.p);
       }
     }
   }
-  FLOAM_HIP(hipMemcpyAsync(o->h_lm.p, o->lm.p, sizeof(LMState), hipMemcpyDeviceToHost, st));
-  FLOAM_HIP(hipMemcpyAsync(o->h_cnt.p, o->cnt.p, sizeof(int) * 2, hipMemcpyDeviceToHost, st));
-  FLOAM_HIP(hipMemcpyAsync(o->h_cnt.p + 2, o->mapE.count.p, sizeof(int), hipMemcpyDeviceToHost, st));
-  FLOAM_HIP(hipMemcpyAsync(o->h_cnt.p + 3, o->mapS.count.p, sizeof(int), hipMemcpyDeviceToHost, st));
+  const bool prof_knn = (ctx.profile & FLOAM_PROF_KNN) != 0;
+  o->ustat.reserve(1);
+  o->h_ustat.reserve(1);
+  if (o->optimization_count <= 0) lm_init_launch(o->lm.p, o->parameters, st);
+  gather_status_launch(o->lm.p, o->cnt.p, o->mapE.count.p, o->mapS.count.p, prof_knn ? o->prof_bytes.p : nullptr,
+                       o->ustat.p, st);
+  FLOAM_HIP(hipMemcpyAsync(o->h_ustat.p, o->ustat.p, sizeof(UpdateStatus), hipMemcpyDeviceToHost, st));
+  if (prof_knn) FLOAM_HIP(hipMemsetAsync(o->prof_bytes.p, 0, sizeof(unsigned long long) * 2, st));
   FLOAM_HIP(hipStreamSynchronize(st));
   ctx.drain();
-  const LMState& L = *o->h_lm.p;
-  const int nEd = o->h_cnt.p[0], nSd = o->h_cnt.p[1];
-  o->mapE_n = (size_t)o->h_cnt.p[2];
-  o->mapS_n = (size_t)o->h_cnt.p[3];
+  if (prof_knn) {
+    ctx.totals["knn_edge"].algorithmic_bytes += (double)o->h_ustat.p->prof[0];
+    ctx.totals["knn_surf"].algorithmic_bytes += (double)o->h_ustat.p->prof[1];
+  }
+  const LMState& L = o->h_ustat.p->lm;
+  const int* hc = o->h_ustat.p->counts;
+  const int nEd = hc[0], nSd = hc[1];
+  o->mapE_n = (size_t)hc[2];
+  o->mapS_n = (size_t)hc[3];
   o->mapE.host_count = o->mapE_n; o->mapE.host_count_valid = true;
   o->mapS.host_count = o->mapS_n; o->mapS.host_count_valid = true;
   o->last_warning = FLOAM_OK;
@@ -361,7 +394,7 @@ void odom_update(floam_odom* o, const floam_cloud* edge, const floam_cloud* surf
     if (keyframe_update(o, o->odom)) {
       // addPointsToMap (:253-294): device-side transform + append + CropBox + VoxelGrid of both maps, using the
       // optimised pose, which is lm->x (== parameters) on the device.
-      ProfScope ps(ctx, "map_update");
+      ProfScope ps(ctx, "map_update", FLOAM_PROF_CLOUD);
       if (!gate) {   // lm->x still holds the prediction we uploaded: identical to parameters
       }
       const int ubS = (int)o->mapS_n + nSd, ubE = (int)o->mapE_n + nEd;
@@ -554,15 +587,18 @@ floam_status floam_lp_feature_extraction(floam_lp* lp, const floam_cloud* in, fl
     const size_t ne0 = cloud_count_sync(edge), ns0 = cloud_count_sync(surf);
     cloud_reserve(edge, ne0 + std::min(n, (size_t)lp->prm.num_lines * 6 * 20) + 1, ne0, st);
     cloud_reserve(surf, ns0 + n + 1, ns0, st);
-    FLOAM_HIP(hipMemsetAsync(lp->status.p, 0, sizeof(int), st));
     if (n > 0) {
-      ProfScope ps(ctx, "feature_extraction", 64.0 * (double)n);
+      ProfScope ps(ctx, "feature_extraction", FLOAM_PROF_FE, 64.0 * (double)n);
       fe_launch(lp->sc, lp->prm, in->pts.p, (int)n, edge->pts.p, edge->count.p, surf->pts.p, surf->count.p, st);
     }
-    FLOAM_HIP(hipMemcpyAsync(lp->h_out.p + 0, edge->count.p, sizeof(int), hipMemcpyDeviceToHost, st));
-    FLOAM_HIP(hipMemcpyAsync(lp->h_out.p + 1, surf->count.p, sizeof(int), hipMemcpyDeviceToHost, st));
-    FLOAM_HIP(hipMemcpyAsync(lp->h_out.p + 2, lp->status.p, sizeof(int), hipMemcpyDeviceToHost, st));
-    FLOAM_HIP(hipStreamSynchronize(st));
+    if (n > 0) {
+      FLOAM_HIP(hipMemcpyAsync(lp->h_out.p, lp->sc.out3.p, sizeof(int) * 3, hipMemcpyDeviceToHost, st));
+      FLOAM_HIP(hipStreamSynchronize(st));
+    } else {
+      lp->h_out.p[0] = (int)ne0;
+      lp->h_out.p[1] = (int)ns0;
+      lp->h_out.p[2] = 0;
+    }
     ctx.drain();
     edge->host_count = (size_t)lp->h_out.p[0];
     edge->host_count_valid = true;
@@ -613,6 +649,13 @@ floam_status floam_odom_destroy(floam_odom* o) {
     if (o) {
       DeviceCtx& ctx = ctx_for(o->device);
       FLOAM_HIP(hipStreamSynchronize(ctx.stream));
+      if (o->dbg_stamps.p) {
+        unsigned long long h[8];
+        FLOAM_HIP(hipMemcpy(h, o->dbg_stamps.p, sizeof(h), hipMemcpyDeviceToHost));
+        const double n = h[4] ? (double)h[4] : 1.0;
+        std::fprintf(stderr, "[floam stamps] lm_step x%llu: eval %.2f us, arrive %.2f us, reduce %.2f us, logic %.2f us\n",
+                     h[4], h[0] / n / 100.0, h[1] / n / 100.0, h[2] / n / 100.0, h[3] / n / 100.0);
+      }
       if (o->comm) ncclCommDestroy(o->comm);
       delete o;
     }
@@ -664,7 +707,7 @@ floam_status floam_odom_update_selector(floam_odom* o, floam_cloud* edge, floam_
     odom_velocity(o, v);
     DeviceCtx& ctx = ctx_for(o->device);
     {
-      ProfScope ps(ctx, "deskew");
+      ProfScope ps(ctx, "deskew", FLOAM_PROF_CLOUD);
       compensate_velocity_launch(edge->pts.p, edge->count.p, (int)cloud_count_sync(edge), v[0], v[1], v[2], ctx.stream);
       compensate_velocity_launch(surf->pts.p, surf->count.p, (int)cloud_count_sync(surf), v[0], v[1], v[2], ctx.stream);
     }
@@ -781,7 +824,7 @@ floam_status floam_odom_set_shard(floam_odom* o, int rank, int world, const void
 floam_status floam_profile_enable(int device, int enable) {
   return guarded([&] {
     DeviceCtx& c = ctx_for(device);
-    c.profile = enable != 0;
+    c.profile = enable;
     return FLOAM_OK;
   });
 }

@@ -16,6 +16,7 @@ namespace floam {
 namespace {
 constexpr int kTB = 256;
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
+constexpr unsigned kEvalBlocks = 128;   // LM evaluation grid (grid-stride over the device-resident slots)
 
 // ===================================================================================== hash grid build
 __global__ void grid_setup(const int* __restrict__ mm, const int* __restrict__ d_m, int shift, unsigned mask,
@@ -58,8 +59,10 @@ __device__ __forceinline__ int cell_of(double v, double o, double inv_c, int n) 
 
 __global__ __launch_bounds__(kTB) void grid_keys(const PointRec* __restrict__ map, const int* __restrict__ d_m, int m_ub,
                                                  const GridParams* __restrict__ gp, uint32_t* __restrict__ keys,
-                                                 int* __restrict__ vals) {
+                                                 int* __restrict__ vals, uint32_t* __restrict__ tkey, int tsize) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  // clear the hash table here (grid_fill inserts only after the sort), saving a memset node
+  for (int t = i; t < tsize; t += gridDim.x * blockDim.x) tkey[t] = kEmpty;
   if (i >= m_ub) return;
   uint32_t key = kEmpty;
   if (i < *d_m) {
@@ -103,9 +106,9 @@ __global__ __launch_bounds__(kTB) void grid_fill(const PointRec* __restrict__ ma
 }
 
 // ===================================================================================== geometry (fp64)
-// Eigen 3.3 SelfAdjointEigenSolver<Matrix3d>::compute restated for the device (same algorithm and operation
-// order as oracle/eigen_solvers.cpp: scaled lower triangle, closed-form 3x3 tridiagonalisation, implicit
-// Wilkinson-shift QR with Givens rotations, ascending selection sort).
+// Eigen 3.3 SelfAdjointEigenSolver<Matrix3d>::compute and ColPivHouseholderQR<Matrix<double,5,3>>::solve restated
+// for the device with the same algorithm and operation order as oracle/eigen_solvers.cpp.  Every array index is a
+// compile-time constant (templates / full unrolling) so the solvers stay in VGPRs instead of scratch.
 __device__ __forceinline__ double e_hypot(double x, double y) {
   const double ax = fabs(x), ay = fabs(y);
   double p, qp;
@@ -114,37 +117,105 @@ __device__ __forceinline__ double e_hypot(double x, double y) {
   return p * sqrt(1.0 + qp * qp);
 }
 
-__device__ void eig_sym3(const double A[3][3], double ev[3], double u_top[3]) {
-  double mat[3][3];
-  double scale = 0.0;
-  for (int r = 0; r < 3; ++r)
-    for (int c = 0; c <= r; ++c) {
-      mat[r][c] = A[r][c];
-      scale = fmax(scale, fabs(A[r][c]));
+// JacobiRotation<double>::makeGivens (real case)
+__device__ __forceinline__ void make_givens(double p, double q, double& c, double& s) {
+  if (q == 0.0) {
+    c = p < 0.0 ? -1.0 : 1.0;
+    s = 0.0;
+  } else if (p == 0.0) {
+    c = 0.0;
+    s = q < 0.0 ? 1.0 : -1.0;
+  } else if (fabs(p) > fabs(q)) {
+    const double t = q / p;
+    double u = sqrt(1.0 + t * t);
+    if (p < 0.0) u = -u;
+    c = 1.0 / u;
+    s = -t * c;
+  } else {
+    const double t = p / q;
+    double u = sqrt(1.0 + t * t);
+    if (q < 0.0) u = -u;
+    s = -1.0 / u;
+    c = -t * s;
+  }
+}
+
+// internal::tridiagonal_qr_step on rows/cols [S, E] of a 3x3 tridiagonal (Q column-major: Q[col][row])
+template <int S, int E>
+__device__ __forceinline__ void tridiag_qr_step(double (&d)[3], double (&e)[2], double (&Q)[3][3]) {
+  const double td = (d[E - 1] - d[E]) * 0.5;
+  const double ee = e[E - 1];
+  double mu = d[E];
+  if (td == 0.0) {
+    mu -= fabs(ee);
+  } else {
+    const double e2 = e[E - 1] * e[E - 1];
+    const double h = e_hypot(td, ee);
+    if (e2 == 0.0) mu -= (ee / (td + (td > 0.0 ? 1.0 : -1.0))) * (ee / h);
+    else mu -= e2 / (td + (td > 0.0 ? h : -h));
+  }
+  double x = d[S] - mu;
+  double z = e[S];
+#pragma unroll
+  for (int k = S; k < E; ++k) {
+    double c, s;
+    make_givens(x, z, c, s);
+    const double sdk = s * d[k] + c * e[k];
+    const double dkp1 = s * e[k] + c * d[k + 1];
+    d[k] = c * (c * d[k] - s * e[k]) - s * (c * e[k] - s * d[k + 1]);
+    d[k + 1] = s * sdk + c * dkp1;
+    e[k] = c * sdk - s * dkp1;
+    if (k > S) e[k - 1] = c * e[k - 1] - s * z;
+    x = e[k];
+    if (k < E - 1) {
+      z = -s * e[k + 1];
+      e[k + 1] = c * e[k + 1];
     }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const double xi = Q[k][i], yi = Q[k + 1][i];
+      Q[k][i] = c * xi - s * yi;
+      Q[k + 1][i] = s * xi + c * yi;
+    }
+  }
+}
+
+__device__ __forceinline__ void swap_d(double& a, double& b) {
+  const double t = a;
+  a = b;
+  b = t;
+}
+
+// eigenvalues ascending in ev; u_top = eigenvector of the largest eigenvalue
+__device__ void eig_sym3(const double (&A)[3][3], double (&ev)[3], double (&u_top)[3]) {
+  double m00 = A[0][0], m10 = A[1][0], m11 = A[1][1], m20 = A[2][0], m21 = A[2][1], m22 = A[2][2];
+  double scale = fabs(m00);
+  scale = fmax(scale, fabs(m10));
+  scale = fmax(scale, fabs(m11));
+  scale = fmax(scale, fabs(m20));
+  scale = fmax(scale, fabs(m21));
+  scale = fmax(scale, fabs(m22));
   if (scale == 0.0) scale = 1.0;
-  for (int r = 0; r < 3; ++r)
-    for (int c = 0; c <= r; ++c) mat[r][c] /= scale;
-  double diag[3], sub[2], Q[3][3];   // Q[col][row]
-  diag[0] = mat[0][0];
-  const double v1norm2 = mat[2][0] * mat[2][0];
+  m00 /= scale; m10 /= scale; m11 /= scale; m20 /= scale; m21 /= scale; m22 /= scale;
+  double d[3], e[2], Q[3][3];
+  d[0] = m00;
+  const double v1norm2 = m20 * m20;
   if (v1norm2 <= DBL_MIN) {
-    diag[1] = mat[1][1];
-    diag[2] = mat[2][2];
-    sub[0] = mat[1][0];
-    sub[1] = mat[2][1];
+    d[1] = m11; d[2] = m22; e[0] = m10; e[1] = m21;
+#pragma unroll
     for (int c = 0; c < 3; ++c)
+#pragma unroll
       for (int r = 0; r < 3; ++r) Q[c][r] = (c == r) ? 1.0 : 0.0;
   } else {
-    const double beta = sqrt(mat[1][0] * mat[1][0] + v1norm2);
+    const double beta = sqrt(m10 * m10 + v1norm2);
     const double invBeta = 1.0 / beta;
-    const double m01 = mat[1][0] * invBeta;
-    const double m02 = mat[2][0] * invBeta;
-    const double q = 2.0 * m01 * mat[2][1] + m02 * (mat[2][2] - mat[1][1]);
-    diag[1] = mat[1][1] + m02 * q;
-    diag[2] = mat[2][2] - m02 * q;
-    sub[0] = beta;
-    sub[1] = mat[2][1] - m01 * q;
+    const double m01 = m10 * invBeta;
+    const double m02 = m20 * invBeta;
+    const double q = 2.0 * m01 * m21 + m02 * (m22 - m11);
+    d[1] = m11 + m02 * q;
+    d[2] = m22 - m02 * q;
+    e[0] = beta;
+    e[1] = m21 - m01 * q;
     Q[0][0] = 1; Q[0][1] = 0; Q[0][2] = 0;
     Q[1][0] = 0; Q[1][1] = m01; Q[1][2] = m02;
     Q[2][0] = 0; Q[2][1] = m02; Q[2][2] = -m01;
@@ -152,198 +223,197 @@ __device__ void eig_sym3(const double A[3][3], double ev[3], double u_top[3]) {
   const double precision = 2.0 * DBL_EPSILON;
   int end = 2, start = 0, iter = 0;
   while (end > 0) {
-    for (int i = start; i < end; ++i)
-      if (fabs(sub[i]) <= (fabs(diag[i]) + fabs(diag[i + 1])) * precision || fabs(sub[i]) <= DBL_MIN) sub[i] = 0.0;
-    while (end > 0 && sub[end - 1] == 0.0) end--;
+    if (start <= 0 && 0 < end)
+      if (fabs(e[0]) <= (fabs(d[0]) + fabs(d[1])) * precision || fabs(e[0]) <= DBL_MIN) e[0] = 0.0;
+    if (start <= 1 && 1 < end)
+      if (fabs(e[1]) <= (fabs(d[1]) + fabs(d[2])) * precision || fabs(e[1]) <= DBL_MIN) e[1] = 0.0;
+    if (end == 2 && e[1] == 0.0) end = 1;
+    if (end == 1 && e[0] == 0.0) end = 0;
     if (end <= 0) break;
     if (++iter > 90) break;
-    start = end - 1;
-    while (start > 0 && sub[start - 1] != 0.0) start--;
-    // tridiagonal_qr_step
-    const double td = (diag[end - 1] - diag[end]) * 0.5;
-    const double e = sub[end - 1];
-    double mu = diag[end];
-    if (td == 0.0) {
-      mu -= fabs(e);
+    start = (end == 2 && e[0] != 0.0) ? 0 : end - 1;
+    if (end == 2) {
+      if (start == 0) tridiag_qr_step<0, 2>(d, e, Q);
+      else tridiag_qr_step<1, 2>(d, e, Q);
     } else {
-      const double e2 = sub[end - 1] * sub[end - 1];
-      const double h = e_hypot(td, e);
-      if (e2 == 0.0) mu -= (e / (td + (td > 0.0 ? 1.0 : -1.0))) * (e / h);
-      else mu -= e2 / (td + (td > 0.0 ? h : -h));
-    }
-    double x = diag[start] - mu;
-    double z = sub[start];
-    for (int k = start; k < end; ++k) {
-      double c, s;
-      if (z == 0.0) {
-        c = x < 0.0 ? -1.0 : 1.0;
-        s = 0.0;
-      } else if (x == 0.0) {
-        c = 0.0;
-        s = z < 0.0 ? 1.0 : -1.0;
-      } else if (fabs(x) > fabs(z)) {
-        const double t = z / x;
-        double uu = sqrt(1.0 + t * t);
-        if (x < 0.0) uu = -uu;
-        c = 1.0 / uu;
-        s = -t * c;
-      } else {
-        const double t = x / z;
-        double uu = sqrt(1.0 + t * t);
-        if (z < 0.0) uu = -uu;
-        s = -1.0 / uu;
-        c = -t * s;
-      }
-      const double sdk = s * diag[k] + c * sub[k];
-      const double dkp1 = s * sub[k] + c * diag[k + 1];
-      diag[k] = c * (c * diag[k] - s * sub[k]) - s * (c * sub[k] - s * diag[k + 1]);
-      diag[k + 1] = s * sdk + c * dkp1;
-      sub[k] = c * sdk - s * dkp1;
-      if (k > start) sub[k - 1] = c * sub[k - 1] - s * z;
-      x = sub[k];
-      if (k < end - 1) {
-        z = -s * sub[k + 1];
-        sub[k + 1] = c * sub[k + 1];
-      }
-      for (int i = 0; i < 3; ++i) {
-        const double xi = Q[k][i], yi = Q[k + 1][i];
-        Q[k][i] = c * xi - s * yi;
-        Q[k + 1][i] = s * xi + c * yi;
-      }
+      tridiag_qr_step<0, 1>(d, e, Q);
     }
   }
-  for (int i = 0; i < 2; ++i) {
-    int k = i;
-    for (int j = i + 1; j < 3; ++j)
-      if (diag[j] < diag[k]) k = j;
-    if (k != i) {
-      const double t = diag[i]; diag[i] = diag[k]; diag[k] = t;
-      for (int r = 0; r < 3; ++r) { const double q = Q[i][r]; Q[i][r] = Q[k][r]; Q[k][r] = q; }
-    }
+  // ascending selection sort (first minimum), swapping eigenvector columns
+  int k = 0;
+  if (d[1] < d[k]) k = 1;
+  if (d[2] < d[k]) k = 2;
+  if (k == 1) {
+    swap_d(d[0], d[1]);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) swap_d(Q[0][r], Q[1][r]);
+  } else if (k == 2) {
+    swap_d(d[0], d[2]);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) swap_d(Q[0][r], Q[2][r]);
   }
-  for (int i = 0; i < 3; ++i) ev[i] = diag[i] * scale;
+  if (d[2] < d[1]) {
+    swap_d(d[1], d[2]);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) swap_d(Q[1][r], Q[2][r]);
+  }
+  ev[0] = d[0] * scale; ev[1] = d[1] * scale; ev[2] = d[2] * scale;
   u_top[0] = Q[2][0]; u_top[1] = Q[2][1]; u_top[2] = Q[2][2];
 }
 
-// Eigen 3.3 ColPivHouseholderQR<Matrix<double,5,3>>::solve(-1) restated for the device.
-__device__ void householder(double* v, int len, double& tau, double& beta) {
+// Householder on column K of a column-major 5x3 (qr[col][row]): makeHouseholderInPlace + apply to columns > K
+template <int K>
+__device__ __forceinline__ void plane_hh(double (&qr)[3][5], double (&hc)[3]) {
   double tail = 0.0;
-  for (int i = 1; i < len; ++i) tail += v[i] * v[i];
-  const double c0 = v[0];
+#pragma unroll
+  for (int i = K + 1; i < 5; ++i) tail += qr[K][i] * qr[K][i];
+  const double c0 = qr[K][K];
+  double tau, beta;
   if (tail <= DBL_MIN) {
     tau = 0.0;
     beta = c0;
-    for (int i = 1; i < len; ++i) v[i] = 0.0;
+#pragma unroll
+    for (int i = K + 1; i < 5; ++i) qr[K][i] = 0.0;
   } else {
     beta = sqrt(c0 * c0 + tail);
     if (c0 >= 0.0) beta = -beta;
-    for (int i = 1; i < len; ++i) v[i] = v[i] / (c0 - beta);
+#pragma unroll
+    for (int i = K + 1; i < 5; ++i) qr[K][i] = qr[K][i] / (c0 - beta);
     tau = (beta - c0) / beta;
+  }
+  hc[K] = tau;
+  qr[K][K] = beta;
+  if (tau != 0.0) {
+#pragma unroll
+    for (int j = K + 1; j < 3; ++j) {
+      double tmp = 0.0;
+#pragma unroll
+      for (int r = K + 1; r < 5; ++r) tmp += qr[K][r] * qr[j][r];
+      tmp += qr[j][K];
+      qr[j][K] -= tau * tmp;
+#pragma unroll
+      for (int r = K + 1; r < 5; ++r) qr[j][r] -= tau * qr[K][r] * tmp;
+    }
   }
 }
 
-__device__ void plane_solve(const double A[5][3], double x[3]) {
+template <int K>
+__device__ __forceinline__ void plane_pivot_step(double (&qr)[3][5], double (&hc)[3], double (&nu)[3], double (&nd)[3],
+                                                 int (&tr)[3], int& nz, double threshold_helper) {
+  int big = K;
+#pragma unroll
+  for (int j = K + 1; j < 3; ++j)
+    if (nu[j] > nu[big == 0 ? 0 : (big == 1 ? 1 : 2)]) big = j;
+  double nb = nu[K];
+#pragma unroll
+  for (int j = K + 1; j < 3; ++j)
+    if (big == j) nb = nu[j];
+  if (nz == 3 && nb * nb < threshold_helper * (5 - K)) nz = K;
+  tr[K] = big;
+#pragma unroll
+  for (int j = K + 1; j < 3; ++j) {
+    if (big == j) {
+#pragma unroll
+      for (int r = 0; r < 5; ++r) swap_d(qr[K][r], qr[j][r]);
+      swap_d(nu[K], nu[j]);
+      swap_d(nd[K], nd[j]);
+    }
+  }
+  plane_hh<K>(qr, hc);
+  const double nrm_thr = sqrt(DBL_EPSILON);
+#pragma unroll
+  for (int j = K + 1; j < 3; ++j) {
+    if (nu[j] != 0.0) {
+      double temp = fabs(qr[j][K]) / nu[j];
+      temp = (1.0 + temp) * (1.0 - temp);
+      temp = temp < 0.0 ? 0.0 : temp;
+      const double ratio = nu[j] / nd[j];
+      const double temp2 = temp * ratio * ratio;
+      if (temp2 <= nrm_thr) {
+        double s = 0.0;
+#pragma unroll
+        for (int r = K + 1; r < 5; ++r) s += qr[j][r] * qr[j][r];
+        nd[j] = sqrt(s);
+        nu[j] = nd[j];
+      } else {
+        nu[j] *= sqrt(temp);
+      }
+    }
+  }
+}
+
+// least-squares plane n: min || A n + 1 || (odomEstimationClass.cpp:220), A = the 5 neighbours (rows)
+__device__ void plane_solve(const double (&A)[5][3], double (&x)[3]) {
   double qr[3][5];
+#pragma unroll
   for (int c = 0; c < 3; ++c)
+#pragma unroll
     for (int r = 0; r < 5; ++r) qr[c][r] = A[r][c];
-  double hc[3], nu[3], nd[3];
-  int tr[3], perm[3] = {0, 1, 2};
+  double hc[3] = {0.0, 0.0, 0.0}, nu[3], nd[3];
+  int tr[3] = {0, 1, 2};
+#pragma unroll
   for (int k = 0; k < 3; ++k) {
     double s = 0.0;
+#pragma unroll
     for (int r = 0; r < 5; ++r) s += qr[k][r] * qr[k][r];
     nd[k] = sqrt(s);
     nu[k] = nd[k];
   }
   const double maxn = fmax(nu[0], fmax(nu[1], nu[2]));
   const double threshold_helper = (maxn * DBL_EPSILON) * (maxn * DBL_EPSILON) / 5;
-  const double norm_downdate_threshold = sqrt(DBL_EPSILON);
   int nz = 3;
-  for (int k = 0; k < 3; ++k) {
-    int big = k;
-    for (int j = k + 1; j < 3; ++j)
-      if (nu[j] > nu[big]) big = j;
-    if (nz == 3 && nu[big] * nu[big] < threshold_helper * (5 - k)) nz = k;
-    tr[k] = big;
-    if (k != big) {
-      for (int r = 0; r < 5; ++r) { const double t = qr[k][r]; qr[k][r] = qr[big][r]; qr[big][r] = t; }
-      double t = nu[k]; nu[k] = nu[big]; nu[big] = t;
-      t = nd[k]; nd[k] = nd[big]; nd[big] = t;
-    }
-    double beta;
-    householder(&qr[k][k], 5 - k, hc[k], beta);
-    qr[k][k] = beta;
-    if (hc[k] != 0.0) {
-      for (int j = k + 1; j < 3; ++j) {
-        double tmp = 0.0;
-        for (int r = k + 1; r < 5; ++r) tmp += qr[k][r] * qr[j][r];
-        tmp += qr[j][k];
-        qr[j][k] -= hc[k] * tmp;
-        for (int r = k + 1; r < 5; ++r) qr[j][r] -= hc[k] * qr[k][r] * tmp;
+  plane_pivot_step<0>(qr, hc, nu, nd, tr, nz, threshold_helper);
+  plane_pivot_step<1>(qr, hc, nu, nd, tr, nz, threshold_helper);
+  plane_pivot_step<2>(qr, hc, nu, nd, tr, nz, threshold_helper);
+  // column permutation: perm = identity, then swap(perm[k], perm[tr[k]]) for k = 0..2
+  int perm[3] = {0, 1, 2};
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      if (j != k && tr[k] == j) {
+        const int t = perm[k];
+        perm[k] = perm[j];
+        perm[j] = t;
       }
-    }
-    for (int j = k + 1; j < 3; ++j) {
-      if (nu[j] != 0.0) {
-        double temp = fabs(qr[j][k]) / nu[j];
-        temp = (1.0 + temp) * (1.0 - temp);
-        temp = temp < 0.0 ? 0.0 : temp;
-        const double ratio = nu[j] / nd[j];
-        const double temp2 = temp * ratio * ratio;
-        if (temp2 <= norm_downdate_threshold) {
-          double s = 0.0;
-          for (int r = k + 1; r < 5; ++r) s += qr[j][r] * qr[j][r];
-          nd[j] = sqrt(s);
-          nu[j] = nd[j];
-        } else {
-          nu[j] *= sqrt(temp);
-        }
-      }
-    }
-  }
-  for (int k = 0; k < 3; ++k) {
-    const int t = perm[k]; perm[k] = perm[tr[k]]; perm[tr[k]] = t;
-  }
   x[0] = x[1] = x[2] = 0.0;
   if (nz == 0) return;
   double c[5] = {-1.0, -1.0, -1.0, -1.0, -1.0};
-  for (int k = 0; k < nz; ++k) {
-    if (hc[k] == 0.0) continue;
-    double tmp = c[k];
-    for (int r = k + 1; r < 5; ++r) tmp += qr[k][r] * c[r];
-    c[k] -= hc[k] * tmp;
-    for (int r = k + 1; r < 5; ++r) c[r] -= hc[k] * qr[k][r] * tmp;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    if (k < nz && hc[k] != 0.0) {
+      double tmp = c[k];
+#pragma unroll
+      for (int r = k + 1; r < 5; ++r) tmp += qr[k][r] * c[r];
+      c[k] -= hc[k] * tmp;
+#pragma unroll
+      for (int r = k + 1; r < 5; ++r) c[r] -= hc[k] * qr[k][r] * tmp;
+    }
   }
-  for (int i = nz - 1; i >= 0; --i) {
-    double s = c[i];
-    for (int j = i + 1; j < nz; ++j) s -= qr[j][i] * c[j];
-    c[i] = s / qr[i][i];
+#pragma unroll
+  for (int i = 2; i >= 0; --i) {
+    if (i < nz) {
+      double s = c[i];
+#pragma unroll
+      for (int j = i + 1; j < 3; ++j)
+        if (j < nz) s -= qr[j][i] * c[j];
+      c[i] = s / qr[i][i];
+    }
   }
-  double out[3] = {0.0, 0.0, 0.0};
-  for (int i = 0; i < nz; ++i) out[perm[i]] = c[i];
-  x[0] = out[0]; x[1] = out[1]; x[2] = out[2];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    if (i < nz) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+        if (perm[i] == j) x[j] = c[i];
+    }
 }
 
 // ===================================================================================== correspondence search
-struct Top5 {
-  float d[5];
-  int i[5];     // map index (tie-break, = FLANN index order)
-  int pos[5];   // position in the cell-sorted array (coordinates)
-  int cnt;
-};
-
-__device__ __forceinline__ void top5_insert(Top5& t, float d, int idx, int pos) {
-  // keep the 5 smallest (d, idx) in ascending order; ties broken by map index
-  if (!(d < t.d[4] || (d == t.d[4] && idx < t.i[4]))) return;
-  int k = 4;
-  while (k > 0 && (d < t.d[k - 1] || (d == t.d[k - 1] && idx < t.i[k - 1]))) {
-    t.d[k] = t.d[k - 1];
-    t.i[k] = t.i[k - 1];
-    t.pos[k] = t.pos[k - 1];
-    --k;
-  }
-  t.d[k] = d;
-  t.i[k] = idx;
-  t.pos[k] = pos;
-}
+// One query per group of kGroup lanes: the lanes stride the candidates of each stencil cell (coalesced 16-B
+// loads from the cell-sorted map), each keeps a sorted top-5 of 64-bit keys (float sq-distance bits << 32 | map
+// index: ascending distance, ties by map index), and a butterfly merge over the group gives the exact 5-NN.
+constexpr int kGroup = 16;
 
 __device__ __forceinline__ int2 grid_lookup(const uint32_t* __restrict__ tkey, const int2* __restrict__ tval,
                                             uint32_t key, int shift, unsigned mask) {
@@ -356,38 +426,40 @@ __device__ __forceinline__ int2 grid_lookup(const uint32_t* __restrict__ tkey, c
   }
 }
 
-// Exact fixed-radius 5-NN: every map point with float sqd < 1 (FLANN L2_Simple order: ((0+dx^2)+dy^2)+dz^2)
-// is visited; the 5 smallest are kept.  valid <=> at least 5 such points  <=>  KD-tree sqd[4] < 1.
-__device__ __forceinline__ void knn5(const GridParams& p, const float4* __restrict__ pts,
-                                     const uint32_t* __restrict__ tkey, const int2* __restrict__ tval, float qx,
-                                     float qy, float qz, Top5& t) {
-  for (int k = 0; k < 5; ++k) { t.d[k] = FLT_MAX; t.i[k] = INT_MAX; t.pos[k] = 0; }
-  t.cnt = 0;
-  const double inv = 1.0 / p.c;
-  // |p - q| < 1 along each axis => cell in [floor((q-o-1)/c), floor((q-o+1)/c)]  (exact: c is a power of two)
-  const int x0 = max(0, (int)floor(((double)qx - p.ox - 1.0) * inv)), x1 = min(p.nx - 1, (int)floor(((double)qx - p.ox + 1.0) * inv));
-  const int y0 = max(0, (int)floor(((double)qy - p.oy - 1.0) * inv)), y1 = min(p.ny - 1, (int)floor(((double)qy - p.oy + 1.0) * inv));
-  const int z0 = max(0, (int)floor(((double)qz - p.oz - 1.0) * inv)), z1 = min(p.nz - 1, (int)floor(((double)qz - p.oz + 1.0) * inv));
-  for (int cz = z0; cz <= z1; ++cz)
-    for (int cy = y0; cy <= y1; ++cy)
-      for (int cx = x0; cx <= x1; ++cx) {
-        const uint32_t key = (uint32_t)cx + (uint32_t)p.nx * ((uint32_t)cy + (uint32_t)p.ny * (uint32_t)cz);
-        const int2 se = grid_lookup(tkey, tval, key, p.shift, p.mask);
-        for (int j = se.x; j < se.x + se.y; ++j) {
-          const float4 m = pts[j];
-          float dd = 0.0f;
-          float df = qx - m.x;
-          dd += df * df;
-          df = qy - m.y;
-          dd += df * df;
-          df = qz - m.z;
-          dd += df * df;
-          if (dd < 1.0f) {
-            t.cnt++;
-            top5_insert(t, dd, __float_as_int(m.w), j);
-          }
-        }
-      }
+__device__ __forceinline__ void cswap(unsigned long long& a, unsigned long long& b) {
+  const unsigned long long lo = a < b ? a : b, hi = a < b ? b : a;
+  a = lo;
+  b = hi;
+}
+
+struct Top5 {
+  unsigned long long k[5];
+};
+
+__device__ __forceinline__ void top5_insert(Top5& t, unsigned long long key) {
+  if (key >= t.k[4]) return;
+  t.k[4] = key;
+  cswap(t.k[3], t.k[4]);
+  cswap(t.k[2], t.k[3]);
+  cswap(t.k[1], t.k[2]);
+  cswap(t.k[0], t.k[1]);
+}
+
+// 5 smallest of two ascending 5-lists: bitonic split min(a[i], b[4-i]), then a 5-input sorting network
+__device__ __forceinline__ void top5_merge(Top5& a, const Top5& b) {
+  unsigned long long m[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) m[i] = a.k[i] < b.k[4 - i] ? a.k[i] : b.k[4 - i];
+  cswap(m[0], m[1]); cswap(m[3], m[4]); cswap(m[2], m[4]); cswap(m[2], m[3]); cswap(m[0], m[3]);
+  cswap(m[0], m[2]); cswap(m[1], m[4]); cswap(m[1], m[3]); cswap(m[1], m[2]);
+#pragma unroll
+  for (int i = 0; i < 5; ++i) a.k[i] = m[i];
+}
+
+__device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v, int m) {
+  const int lo = __shfl_xor((int)(v & 0xFFFFFFFFull), m, kGroup);
+  const int hi = __shfl_xor((int)(v >> 32), m, kGroup);
+  return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
 }
 
 template <bool EDGE>
@@ -395,78 +467,190 @@ __global__ __launch_bounds__(kTB) void corr_kernel(LMState* __restrict__ st, con
                                                    const int* __restrict__ d_n, int n_ub,
                                                    const GridParams* __restrict__ gp, const float4* __restrict__ gpts,
                                                    const uint32_t* __restrict__ tkey, const int2* __restrict__ tval,
+                                                   const PointRec* __restrict__ map,
                                                    const int* __restrict__ d_me, const int* __restrict__ d_ms,
                                                    double* __restrict__ rec, uint8_t* __restrict__ valid, int cap,
                                                    int rank, int world) {
+  const int lane = threadIdx.x & (kGroup - 1);
+  const int n = min(*d_n, n_ub);
+  const int lo = (int)(((long long)n * rank) / world), hi = (int)(((long long)n * (rank + 1)) / world);
+  const bool gate = *d_me > 10 && *d_ms > 50;   // map-size gate (odomEstimationClass.cpp:77)
+  const int ngroups = (gridDim.x * blockDim.x) / kGroup;
+  // grid-stride over the queries the device holds (the host only knows an upper bound)
+  for (int i0 = 0; i0 < n; i0 += ngroups) {
+  const int i = i0 + (blockIdx.x * blockDim.x + threadIdx.x) / kGroup;   // query
+  bool ok = false;
+  if (i < n) {
+    if (i >= lo && i < hi && gate) {
+      const float4 pq = *reinterpret_cast<const float4*>(&q[i].x);
+      float wx, wy, wz;
+      associate_to_map(st->x, pq.x, pq.y, pq.z, wx, wy, wz);   // pointAssociateToMap (:126-135)
+      const GridParams p = *gp;
+      const double inv = 1.0 / p.c;
+      // |m - q| < 1 on every axis  =>  cell in [floor((q-o-1)/c), floor((q-o+1)/c)]  (c is a power of two)
+      const int x0 = max(0, (int)floor(((double)wx - p.ox - 1.0) * inv));
+      const int x1 = min(p.nx - 1, (int)floor(((double)wx - p.ox + 1.0) * inv));
+      const int y0 = max(0, (int)floor(((double)wy - p.oy - 1.0) * inv));
+      const int y1 = min(p.ny - 1, (int)floor(((double)wy - p.oy + 1.0) * inv));
+      const int z0 = max(0, (int)floor(((double)wz - p.oz - 1.0) * inv));
+      const int z1 = min(p.nz - 1, (int)floor(((double)wz - p.oz + 1.0) * inv));
+      const int nxr = max(0, x1 - x0 + 1), nyr = max(0, y1 - y0 + 1), nzr = max(0, z1 - z0 + 1);
+      const int ncell = nxr * nyr * nzr;   // <= 27
+      int2 se[2] = {make_int2(0, 0), make_int2(0, 0)};
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int c = lane + h * kGroup;
+        if (c < ncell) {
+          const int cx = x0 + c % nxr, cy = y0 + (c / nxr) % nyr, cz = z0 + c / (nxr * nyr);
+          const uint32_t key = (uint32_t)cx + (uint32_t)p.nx * ((uint32_t)cy + (uint32_t)p.ny * (uint32_t)cz);
+          se[h] = grid_lookup(tkey, tval, key, p.shift, p.mask);
+        }
+      }
+      Top5 t;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) t.k[k] = ~0ull;
+      int cnt = 0;
+      for (int c = 0; c < ncell; ++c) {
+        const int sx = __shfl(c < kGroup ? se[0].x : se[1].x, c & (kGroup - 1), kGroup);
+        const int sy = __shfl(c < kGroup ? se[0].y : se[1].y, c & (kGroup - 1), kGroup);
+        for (int j = sx + lane; j < sx + sy; j += kGroup) {
+          const float4 m = gpts[j];
+          float dd = 0.0f;   // flann::L2_Simple<float>: ((0 + dx*dx) + dy*dy) + dz*dz
+          float df = wx - m.x;
+          dd += df * df;
+          df = wy - m.y;
+          dd += df * df;
+          df = wz - m.z;
+          dd += df * df;
+          if (dd < 1.0f) {
+            ++cnt;
+            top5_insert(t, ((unsigned long long)__float_as_uint(dd) << 32) | (unsigned)__float_as_int(m.w));
+          }
+        }
+      }
+#pragma unroll
+      for (int m = kGroup / 2; m > 0; m >>= 1) {
+        Top5 o;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) o.k[k] = shfl_xor_u64(t.k[k], m);
+        top5_merge(t, o);
+        cnt += __shfl_xor(cnt, m, kGroup);
+      }
+      if (lane == 0 && cnt >= 5) {   // sqd[4] < 1 (:154, :210)
+        double P[5][3];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+          const float4 mp = *reinterpret_cast<const float4*>(&map[(int)(t.k[j] & 0xFFFFFFFFull)].x);
+          P[j][0] = mp.x; P[j][1] = mp.y; P[j][2] = mp.z;
+        }
+        const double cpx = pq.x, cpy = pq.y, cpz = pq.z;
+        if (EDGE) {
+          // addEdgeCostFactor geometry (odomEstimationClass.cpp:156-189)
+          double c[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+          for (int j = 0; j < 5; ++j) {
+            c[0] = c[0] + P[j][0]; c[1] = c[1] + P[j][1]; c[2] = c[2] + P[j][2];
+          }
+          c[0] = c[0] / 5.0; c[1] = c[1] / 5.0; c[2] = c[2] / 5.0;
+          double cov[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+#pragma unroll
+          for (int j = 0; j < 5; ++j) {
+            const double z[3] = {P[j][0] - c[0], P[j][1] - c[1], P[j][2] - c[2]};
+#pragma unroll
+            for (int a = 0; a < 3; ++a)
+#pragma unroll
+              for (int b = 0; b < 3; ++b) cov[a][b] = cov[a][b] + z[a] * z[b];
+          }
+          double ev[3], u[3];
+          eig_sym3(cov, ev, u);
+          if (ev[2] > 3 * ev[1]) {
+            ok = true;
+            rec[0 * cap + i] = cpx; rec[1 * cap + i] = cpy; rec[2 * cap + i] = cpz;
+            rec[3 * cap + i] = 0.1 * u[0] + c[0]; rec[4 * cap + i] = 0.1 * u[1] + c[1]; rec[5 * cap + i] = 0.1 * u[2] + c[2];
+            rec[6 * cap + i] = -0.1 * u[0] + c[0]; rec[7 * cap + i] = -0.1 * u[1] + c[1]; rec[8 * cap + i] = -0.1 * u[2] + c[2];
+          }
+        } else {
+          // addSurfCostFactor geometry (odomEstimationClass.cpp:208-243)
+          double nv[3];
+          plane_solve(P, nv);
+          const double z = nv[0] * nv[0] + nv[1] * nv[1] + nv[2] * nv[2];
+          const double d = 1 / sqrt(z);
+          if (z > 0.0) {
+            const double sz = sqrt(z);
+            nv[0] = nv[0] / sz; nv[1] = nv[1] / sz; nv[2] = nv[2] / sz;
+          }
+          bool planeValid = true;
+#pragma unroll
+          for (int j = 0; j < 5; ++j)
+            if (fabs(nv[0] * P[j][0] + nv[1] * P[j][1] + nv[2] * P[j][2] + d) > 0.2) planeValid = false;
+          if (planeValid) {
+            ok = true;
+            rec[0 * cap + i] = cpx; rec[1 * cap + i] = cpy; rec[2 * cap + i] = cpz;
+            rec[3 * cap + i] = nv[0]; rec[4 * cap + i] = nv[1]; rec[5 * cap + i] = nv[2];
+            rec[6 * cap + i] = d;
+          }
+        }
+      }
+    }
+    if (lane == 0) valid[i] = ok ? 1 : 0;
+  }
+  const unsigned long long b = __ballot(ok);
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd(EDGE ? &st->corr_edge : &st->corr_surf, __popcll(b));
+  }
+}
+
+// Algorithmic traffic of one correspondence launch (SURVEY.md §8 d): every occupied 1-m query cell streams its
+// 27-cell candidate set once (16 B per map point), every query is read once (16 B) and writes its valid flag
+// (1 B) and, if accepted, its record.  Runs untimed, after the kernel it describes, only when profiling.
+__global__ __launch_bounds__(kTB) void knn_traffic(const LMState* __restrict__ st, const PointRec* __restrict__ q,
+                                                   const int* __restrict__ d_n, int n_ub,
+                                                   const GridParams* __restrict__ gp, const uint32_t* __restrict__ tkey,
+                                                   const int2* __restrict__ tval, const uint8_t* __restrict__ valid,
+                                                   int rec_bytes, int rank, int world, uint32_t* __restrict__ set,
+                                                   unsigned set_mask, int set_shift,
+                                                   unsigned long long* __restrict__ out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_ub) return;
   const int n = *d_n;
   const int lo = (int)(((long long)n * rank) / world), hi = (int)(((long long)n * (rank + 1)) / world);
-  bool ok = false;
-  if (i >= lo && i < hi && *d_me > 10 && *d_ms > 50) {   // map-size gate (odomEstimationClass.cpp:77)
-    const PointRec pr = q[i];
-    float wx, wy, wz;
-    associate_to_map(st->x, pr.x, pr.y, pr.z, wx, wy, wz);
-    const GridParams p = *gp;
-    Top5 t;
-    knn5(p, gpts, tkey, tval, wx, wy, wz, t);
-    if (t.cnt >= 5) {
-      // the 5 neighbours in ascending distance order (Eigen::Vector3d of the map's float coordinates)
-      double P[5][3];
-      for (int j = 0; j < 5; ++j) {
-        const float4 mp = gpts[t.pos[j]];
-        P[j][0] = mp.x; P[j][1] = mp.y; P[j][2] = mp.z;
-      }
-      const double cpx = pr.x, cpy = pr.y, cpz = pr.z;
-      if (EDGE) {
-        // addEdgeCostFactor geometry (odomEstimationClass.cpp:156-189)
-        double c[3] = {0.0, 0.0, 0.0};
-        for (int j = 0; j < 5; ++j)
-          for (int d = 0; d < 3; ++d) c[d] = c[d] + P[j][d];
-        for (int d = 0; d < 3; ++d) c[d] = c[d] / 5.0;
-        double cov[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
-        for (int j = 0; j < 5; ++j) {
-          const double z[3] = {P[j][0] - c[0], P[j][1] - c[1], P[j][2] - c[2]};
-          for (int a = 0; a < 3; ++a)
-            for (int b = 0; b < 3; ++b) cov[a][b] = cov[a][b] + z[a] * z[b];
-        }
-        double ev[3], u[3];
-        eig_sym3(cov, ev, u);
-        if (ev[2] > 3 * ev[1]) {
-          ok = true;
-          rec[0 * cap + i] = cpx; rec[1 * cap + i] = cpy; rec[2 * cap + i] = cpz;
-          rec[3 * cap + i] = 0.1 * u[0] + c[0]; rec[4 * cap + i] = 0.1 * u[1] + c[1]; rec[5 * cap + i] = 0.1 * u[2] + c[2];
-          rec[6 * cap + i] = -0.1 * u[0] + c[0]; rec[7 * cap + i] = -0.1 * u[1] + c[1]; rec[8 * cap + i] = -0.1 * u[2] + c[2];
-        }
-      } else {
-        // addSurfCostFactor geometry (odomEstimationClass.cpp:208-243)
-        double nv[3];
-        plane_solve(P, nv);
-        const double z = nv[0] * nv[0] + nv[1] * nv[1] + nv[2] * nv[2];
-        const double d = 1 / sqrt(z);
-        if (z > 0.0) {
-          const double sz = sqrt(z);
-          nv[0] = nv[0] / sz; nv[1] = nv[1] / sz; nv[2] = nv[2] / sz;
-        }
-        bool planeValid = true;
-        for (int j = 0; j < 5; ++j)
-          if (fabs(nv[0] * P[j][0] + nv[1] * P[j][1] + nv[2] * P[j][2] + d) > 0.2) { planeValid = false; break; }
-        if (planeValid) {
-          ok = true;
-          rec[0 * cap + i] = cpx; rec[1 * cap + i] = cpy; rec[2 * cap + i] = cpz;
-          rec[3 * cap + i] = nv[0]; rec[4 * cap + i] = nv[1]; rec[5 * cap + i] = nv[2];
-          rec[6 * cap + i] = d;
-        }
-      }
-    }
+  if (i < lo || i >= hi) return;
+  const PointRec pr = q[i];
+  float wx, wy, wz;
+  associate_to_map(st->x, pr.x, pr.y, pr.z, wx, wy, wz);
+  const GridParams p = *gp;
+  const double inv = 1.0 / p.c;
+  const int cx = (int)floor(((double)wx - p.ox) * inv), cy = (int)floor(((double)wy - p.oy) * inv),
+            cz = (int)floor(((double)wz - p.oz) * inv);
+  unsigned long long bytes = 16ull + 1ull + (valid[i] ? (unsigned long long)rec_bytes : 0ull);
+  const uint32_t key = ((uint32_t)(cx + 2) & 0x7FFu) | (((uint32_t)(cy + 2) & 0x7FFu) << 11) |
+                       (((uint32_t)(cz + 2) & 0x3FFu) << 22);
+  uint32_t h = hash_slot(key, set_shift);
+  bool fresh = false;
+  for (;;) {
+    const uint32_t prev = atomicCAS(&set[h], kEmpty, key);
+    if (prev == kEmpty) { fresh = true; break; }
+    if (prev == key) break;
+    h = (h + 1) & set_mask;
   }
-  valid[i] = ok ? 1 : 0;
-  const unsigned long long b = __ballot(ok);
-  if ((threadIdx.x & 63) == 0 && b) atomicAdd(EDGE ? &st->corr_edge : &st->corr_surf, __popcll(b));
+  if (fresh) {
+    unsigned long long cand = 0;
+    for (int z = cz - 1; z <= cz + 1; ++z)
+      for (int y = cy - 1; y <= cy + 1; ++y)
+        for (int x = cx - 1; x <= cx + 1; ++x) {
+          if (x < 0 || y < 0 || z < 0 || x >= p.nx || y >= p.ny || z >= p.nz) continue;
+          const uint32_t k = (uint32_t)x + (uint32_t)p.nx * ((uint32_t)y + (uint32_t)p.ny * (uint32_t)z);
+          cand += (unsigned long long)grid_lookup(tkey, tval, k, p.shift, p.mask).y;
+        }
+    bytes += 16ull * cand;
+  }
+  atomicAdd(out, bytes);
 }
 
-__global__ void lm_init(LMState* st) {
+__global__ void lm_init(LMState* st, X7 x0) {
   if (threadIdx.x != 0) return;
+  if (x0.set)
+#pragma unroll
+    for (int k = 0; k < 7; ++k) st->x[k] = x0.v[k];
   st->phase = 0;
   st->done = 0;
   st->iteration = 0;
@@ -540,28 +724,29 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
-__global__ __launch_bounds__(kTB) void lm_eval(const LMState* __restrict__ st, const double* __restrict__ erec,
-                                               const uint8_t* __restrict__ evalid, int ecap, int ne_ub,
-                                               const double* __restrict__ srec, const uint8_t* __restrict__ svalid,
-                                               int scap, int ns_ub, int huber, double* __restrict__ partials) {
-  if (st->done) return;
+// Per-block partial sums (cost, J^T J upper, J^T r, count) of one LM evaluation over the device-resident
+// correspondence slots [0, *d_ne) and [0, *d_ns).  Evaluated at x (phase 0, iteration zero) or at the candidate.
+__device__ void eval_block(const LMState* __restrict__ st, const double* __restrict__ erec,
+                           const uint8_t* __restrict__ evalid, int ecap, int ne, const double* __restrict__ srec,
+                           const uint8_t* __restrict__ svalid, int scap, int ns, int huber, double* __restrict__ partials) {
   double x[7];
   const double* px = st->phase == 0 ? st->x : st->cand;
+#pragma unroll
   for (int k = 0; k < 7; ++k) x[k] = px[k];
   double acc[LM_NSUM];
 #pragma unroll
   for (int k = 0; k < LM_NSUM; ++k) acc[k] = 0.0;
-  const int total = ne_ub + ns_ub;
+  const int total = ne + ns;
   for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
     double J[6], r;
-    if (idx < ne_ub) {
+    if (idx < ne) {
       if (!evalid[idx]) continue;
       double f[9];
 #pragma unroll
       for (int k = 0; k < 9; ++k) f[k] = erec[k * ecap + idx];
       r = edge_residual(x, f, J);
     } else {
-      const int s = idx - ne_ub;
+      const int s = idx - ne;
       if (!svalid[s]) continue;
       double f[7];
 #pragma unroll
@@ -596,36 +781,51 @@ __global__ __launch_bounds__(kTB) void lm_eval(const LMState* __restrict__ st, c
     for (int a = 0; a < 6; ++a) acc[22 + a] += J[a] * r;
     acc[28] += 1.0;
   }
-  __shared__ double red[LM_NSUM][kTB / 64];
-  const int w = threadIdx.x >> 6;
+  // fixed-order block reduction through LDS: [component][thread] -> 8 strips of 32 per component -> 8 partials
+  __shared__ double red[LM_NSUM][kTB];
+  __shared__ double strip[LM_NSUM][8];
 #pragma unroll
-  for (int k = 0; k < LM_NSUM; ++k) {
-    const double v = wave_sum(acc[k]);
-    if ((threadIdx.x & 63) == 0) red[k][w] = v;
+  for (int k = 0; k < LM_NSUM; ++k) red[k][threadIdx.x] = acc[k];
+  __syncthreads();
+  if (threadIdx.x < LM_NSUM * 8) {
+    const int c = threadIdx.x >> 3, p = threadIdx.x & 7;
+    double v = 0.0;
+    for (int j = 0; j < kTB / 8; ++j) v += red[c][p * (kTB / 8) + j];
+    strip[c][p] = v;
   }
   __syncthreads();
   if (threadIdx.x < LM_NSUM) {
     double v = 0.0;
-    for (int k = 0; k < kTB / 64; ++k) v += red[threadIdx.x][k];
+    for (int p = 0; p < 8; ++p) v += strip[threadIdx.x][p];
     partials[threadIdx.x * gridDim.x + blockIdx.x] = v;
   }
 }
 
+__global__ __launch_bounds__(kTB) void lm_eval(const LMState* __restrict__ st, const double* __restrict__ erec,
+                                               const uint8_t* __restrict__ evalid, int ecap, const int* __restrict__ d_ne,
+                                               int ne_ub, const double* __restrict__ srec,
+                                               const uint8_t* __restrict__ svalid, int scap,
+                                               const int* __restrict__ d_ns, int ns_ub, int huber,
+                                               double* __restrict__ partials) {
+  if (st->done) return;
+  eval_block(st, erec, evalid, ecap, min(*d_ne, ne_ub), srec, svalid, scap, min(*d_ns, ns_ub), huber, partials);
+}
+
 __device__ void reduce_partials_block(const double* __restrict__ partials, int nblk, double* sums /* shared */) {
-  double acc[LM_NSUM];
-  for (int k = 0; k < LM_NSUM; ++k) acc[k] = 0.0;
-  for (int b = threadIdx.x; b < nblk; b += blockDim.x)
-    for (int k = 0; k < LM_NSUM; ++k) acc[k] += partials[k * nblk + b];
-  __shared__ double red[LM_NSUM][kTB / 64];
-  const int w = threadIdx.x >> 6;
-  for (int k = 0; k < LM_NSUM; ++k) {
-    const double v = wave_sum(acc[k]);
-    if ((threadIdx.x & 63) == 0) red[k][w] = v;
+  // component c = t / 8 sums its 8 block strips in order, then thread c sums the 8 strip totals (fixed order)
+  __shared__ double strip[LM_NSUM][8];
+  if (threadIdx.x < LM_NSUM * 8) {
+    const int c = threadIdx.x >> 3, p = threadIdx.x & 7;
+    const int per = (nblk + 7) / 8;
+    const int b0 = p * per, b1 = min(nblk, b0 + per);
+    double v = 0.0;
+    for (int bb = b0; bb < b1; ++bb) v += partials[c * nblk + bb];
+    strip[c][p] = v;
   }
   __syncthreads();
   if (threadIdx.x < LM_NSUM) {
     double v = 0.0;
-    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) v += red[threadIdx.x][k];
+    for (int p = 0; p < 8; ++p) v += strip[threadIdx.x][p];
     sums[threadIdx.x] = v;
   }
   __syncthreads();
@@ -658,11 +858,15 @@ __device__ void se3_plus(const double* x, const double* d, double* out) {
   } else {
     const double O[3][3] = {{0, -wz, wy}, {wz, 0, -wx}, {-wy, wx, 0}};
     double O2[3][3];
+#pragma unroll
     for (int i = 0; i < 3; ++i)
+#pragma unroll
       for (int j = 0; j < 3; ++j) O2[i][j] = O[i][0] * O[0][j] + O[i][1] * O[1][j] + O[i][2] * O[2][j];
     const double c1 = (1 - cos(theta)) / (theta * theta);
     const double c2 = (theta - sin(theta)) / pow(theta, 3.0);
+#pragma unroll
     for (int i = 0; i < 3; ++i)
+#pragma unroll
       for (int j = 0; j < 3; ++j) Jm[i][j] = ((i == j) ? 1.0 : 0.0) + c1 * O[i][j] + c2 * O2[i][j];
   }
   const double dtx = Jm[0][0] * d[3] + Jm[0][1] * d[4] + Jm[0][2] * d[5];
@@ -684,9 +888,11 @@ __device__ void se3_plus(const double* x, const double* d, double* out) {
 
 __device__ double grad_max_norm(const double* x, const double* g) {
   double ng[6], pr[7];
+#pragma unroll
   for (int k = 0; k < 6; ++k) ng[k] = -g[k];
   se3_plus(x, ng, pr);
   double m = 0.0;
+#pragma unroll
   for (int i = 0; i < 7; ++i) m = fmax(m, fabs(x[i] - pr[i]));
   return m;
 }
@@ -697,8 +903,11 @@ __device__ __forceinline__ int hidx(int a, int b) {   // upper-triangle row-majo
 
 // LevenbergMarquardtStrategy::ComputeStep in normal-equation form on the Jacobi-scaled system:
 // (Hs + diag(Hs)/radius) y = gs, step = -y; then TrustRegionMinimizer::ComputeTrustRegionStep's model cost change.
+// Runs on one lane; the 6x6 work lives in LDS with rolled loops (compact code: this path is latency-bound and
+// runs with a cold instruction cache every launch).
 __device__ bool compute_step(LMState* s) {
-  double Hs[6][6], gs[6];
+  __shared__ double Hs[6][6], L[6][6];
+  __shared__ double gs[6], y[6], step[6];
   for (int a = 0; a < 6; ++a) {
     gs[a] = s->scale[a] * s->g[a];
     for (int b = 0; b < 6; ++b) {
@@ -709,23 +918,18 @@ __device__ bool compute_step(LMState* s) {
   if (!s->reuse)
     for (int k = 0; k < 6; ++k) s->diag[k] = fmin(fmax(Hs[k][k], 1e-6), 1e32);
   s->reuse = 1;
-  double A[6][6];
-  for (int a = 0; a < 6; ++a)
-    for (int b = 0; b < 6; ++b) A[a][b] = Hs[a][b] + (a == b ? s->diag[a] / s->radius : 0.0);
-  // Cholesky A = L L^T
-  double L[6][6];
+  // Cholesky of A = Hs + diag / radius
   for (int j = 0; j < 6; ++j) {
-    double d = A[j][j];
+    double d = Hs[j][j] + s->diag[j] / s->radius;
     for (int k = 0; k < j; ++k) d -= L[j][k] * L[j][k];
     if (!(d > 0.0)) return false;
     L[j][j] = sqrt(d);
     for (int i = j + 1; i < 6; ++i) {
-      double v = A[i][j];
+      double v = Hs[i][j];
       for (int k = 0; k < j; ++k) v -= L[i][k] * L[j][k];
       L[i][j] = v / L[j][j];
     }
   }
-  double y[6];
   for (int i = 0; i < 6; ++i) {
     double v = gs[i];
     for (int k = 0; k < i; ++k) v -= L[i][k] * y[k];
@@ -736,7 +940,6 @@ __device__ bool compute_step(LMState* s) {
     for (int k = i + 1; k < 6; ++k) v -= L[k][i] * y[k];
     y[i] = v / L[i][i];
   }
-  double step[6];
   bool finite = true;
   for (int k = 0; k < 6; ++k) {
     step[k] = -y[k];
@@ -754,12 +957,14 @@ __device__ bool compute_step(LMState* s) {
   if (!(mcc > 0.0)) return false;
   s->mcc = mcc;
   double delta[6];
+#pragma unroll
   for (int k = 0; k < 6; ++k) delta[k] = step[k] * s->scale[k];
   se3_plus(s->x, delta, s->cand);
   return true;
 }
 
 __device__ void next_step(LMState* s) {
+#pragma unroll
   for (;;) {
     s->iteration++;
     if (compute_step(s)) {
@@ -777,6 +982,7 @@ __device__ void next_step(LMState* s) {
 
 __device__ double norm7(const double* a) {
   double v = 0.0;
+#pragma unroll
   for (int i = 0; i < 7; ++i) v += a[i] * a[i];
   return sqrt(v);
 }
@@ -787,9 +993,12 @@ __device__ void lm_logic(LMState* s, const double* sums) {
     if (s->n_res == 0) { s->done = 1; return; }   // no residual blocks: parameters untouched
     s->x_cost = sums[0];
     if (!isfinite(s->x_cost)) { s->done = 1; return; }
+#pragma unroll
     for (int k = 0; k < 21; ++k) s->H[k] = sums[1 + k];
+#pragma unroll
     for (int k = 0; k < 6; ++k) s->g[k] = sums[22 + k];
     s->initial_cost = s->x_cost;
+#pragma unroll
     for (int k = 0; k < 6; ++k) s->scale[k] = 1.0 / (1.0 + sqrt(s->H[hidx(k, k)]));
     s->x_norm = norm7(s->x);
     s->gmax = grad_max_norm(s->x, s->g);
@@ -807,6 +1016,7 @@ __device__ void lm_logic(LMState* s, const double* sums) {
   if (!isfinite(cand_cost)) cand_cost = DBL_MAX;
   // ParameterToleranceReached (candidate not applied)
   double sn = 0.0;
+#pragma unroll
   for (int i = 0; i < 7; ++i) sn += (s->x[i] - s->cand[i]) * (s->x[i] - s->cand[i]);
   sn = sqrt(sn);
   if (sn <= 1e-8 * (s->x_norm + 1e-8)) { s->done = 1; return; }
@@ -815,10 +1025,13 @@ __device__ void lm_logic(LMState* s, const double* sums) {
   const double rho = (s->x_cost - cand_cost) / s->mcc;
   bool success = false;
   if (rho > 1e-3) {
+#pragma unroll
     for (int i = 0; i < 7; ++i) s->x[i] = s->cand[i];
     s->x_norm = norm7(s->x);
     s->x_cost = cand_cost;
+#pragma unroll
     for (int k = 0; k < 21; ++k) s->H[k] = sums[1 + k];
+#pragma unroll
     for (int k = 0; k < 6; ++k) s->g[k] = sums[22 + k];
     s->gmax = grad_max_norm(s->x, s->g);
     const double t = 2.0 * rho - 1.0;
@@ -836,6 +1049,22 @@ __device__ void lm_logic(LMState* s, const double* sums) {
   next_step(s);
 }
 
+// The serial Ceres control step runs on an LDS copy of the LM state (global-memory round trips per field made
+// the single-lane logic latency-bound); all lanes stage it in and out.
+__device__ __forceinline__ void lm_logic_lds(LMState* __restrict__ st, const double* sums) {
+  __shared__ LMState sst;
+  constexpr int kWords = (int)(sizeof(LMState) / sizeof(unsigned));
+  static_assert(sizeof(LMState) % sizeof(unsigned) == 0, "LMState must be a whole number of dwords");
+  const unsigned* gsrc = reinterpret_cast<const unsigned*>(st);
+  unsigned* ldst = reinterpret_cast<unsigned*>(&sst);
+  for (int w = threadIdx.x; w < kWords; w += blockDim.x) ldst[w] = gsrc[w];
+  __syncthreads();
+  if (threadIdx.x == 0) lm_logic(&sst, sums);
+  __syncthreads();
+  unsigned* gdst = reinterpret_cast<unsigned*>(st);
+  for (int w = threadIdx.x; w < kWords; w += blockDim.x) gdst[w] = ldst[w];
+}
+
 __global__ __launch_bounds__(kTB) void lm_control(LMState* __restrict__ st, const double* __restrict__ partials, int nblk) {
   __shared__ double sums[LM_NSUM];
   if (st->done) return;
@@ -845,7 +1074,53 @@ __global__ __launch_bounds__(kTB) void lm_control(LMState* __restrict__ st, cons
     if (threadIdx.x < LM_NSUM) sums[threadIdx.x] = partials[threadIdx.x];
     __syncthreads();
   }
-  if (threadIdx.x == 0) lm_logic(st, sums);
+  lm_logic_lds(st, sums);
+}
+
+// One LM iteration in one launch (single-GPU path): every block evaluates its share, the last block to arrive
+// (device-scope counter) reduces the partials in fixed block order and runs the Ceres control step.  Hand-off per
+// MI355X_MICROARCH.md "Valid forms": plain stores -> s_waitcnt vmcnt(0) -> barrier -> lane-0 agent release ->
+// s_waitcnt -> atomic; the last block: agent acquire -> s_waitcnt -> barrier -> plain loads.
+__global__ __launch_bounds__(kTB) void lm_step(LMState* __restrict__ st, const double* __restrict__ erec,
+                                               const uint8_t* __restrict__ evalid, int ecap, const int* __restrict__ d_ne,
+                                               int ne_ub, const double* __restrict__ srec,
+                                               const uint8_t* __restrict__ svalid, int scap,
+                                               const int* __restrict__ d_ns, int ns_ub, int huber,
+                                               double* __restrict__ partials, unsigned* __restrict__ counter,
+                                               unsigned long long* __restrict__ dbg) {
+  if (st->done) return;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  eval_block(st, erec, evalid, ecap, min(*d_ne, ne_ub), srec, svalid, scap, min(*d_ns, ns_ub), huber, partials);
+  const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+  __shared__ int s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = atomicAdd(counter, 1u);
+    s_last = (prev == gridDim.x - 1);
+    if (s_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __shared__ double sums[LM_NSUM];
+  const unsigned long long t2 = __builtin_amdgcn_s_memrealtime();
+  reduce_partials_block(partials, gridDim.x, sums);
+  const unsigned long long t3 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) *counter = 0u;   // ready for the next launch (kernel boundary orders it)
+  lm_logic_lds(st, sums);
+  const unsigned long long t4 = __builtin_amdgcn_s_memrealtime();
+  if (dbg && threadIdx.x == 0) {   // diagnostic stamps (100 MHz): eval, arrive, reduce, logic
+    atomicAdd(&dbg[0], t1 - t0);
+    atomicAdd(&dbg[1], t2 - t1);
+    atomicAdd(&dbg[2], t3 - t2);
+    atomicAdd(&dbg[3], t4 - t3);
+    atomicAdd(&dbg[4], 1ull);
+  }
 }
 
 __global__ __launch_bounds__(kTB) void lm_reduce(const double* __restrict__ partials, int nblk, double* __restrict__ out) {
@@ -869,12 +1144,12 @@ void grid_build_launch(Grid& g, GridScratch& sc, const PointRec* map, const int*
   g.tval.reserve(tsize);
   g.table_size = tsize;
   g.shift = shift;
-  FLOAM_HIP(hipMemsetAsync(g.tkey.p, 0xFF, sizeof(uint32_t) * tsize, st));
   minmax_launch(map, d_m, ub, sc.mm.p, st);
   hipLaunchKernelGGL(grid_setup, dim3(1), dim3(64), 0, st, sc.mm.p, d_m, shift, (unsigned)(tsize - 1), g.params.p);
   FLOAM_LAUNCH_CHECK();
   const unsigned gb = div_up(ub, kTB);
-  hipLaunchKernelGGL(grid_keys, dim3(gb), dim3(kTB), 0, st, map, d_m, ub, g.params.p, sc.s.k0.p, sc.s.v0.p);
+  hipLaunchKernelGGL(grid_keys, dim3(gb), dim3(kTB), 0, st, map, d_m, ub, g.params.p, sc.s.k0.p, sc.s.v0.p, g.tkey.p,
+                     tsize);
   FLOAM_LAUNCH_CHECK();
   sort_pairs_u32(sc.s.temp.p, sc.s.temp_bytes, sc.s.k0.p, sc.s.k1.p, sc.s.v0.p, sc.s.v1.p, ub, 32, st);
   hipLaunchKernelGGL(grid_fill, dim3(gb), dim3(kTB), 0, st, map, d_m, sc.s.k1.p, sc.s.v1.p, g.params.p, g.pts.p,
@@ -882,34 +1157,86 @@ void grid_build_launch(Grid& g, GridScratch& sc, const PointRec* map, const int*
   FLOAM_LAUNCH_CHECK();
 }
 
-void corr_launch(LMState* d_st, const QuerySet& qe, const Grid& ge, const int* d_me, const QuerySet& qs,
-                 const Grid& gs, const int* d_ms, CorrSet& ce, CorrSet& cs, int rank, int world, hipStream_t st) {
-  hipLaunchKernelGGL(lm_init, dim3(1), dim3(64), 0, st, d_st);
-  FLOAM_LAUNCH_CHECK();
-  ce.reserve(std::max(qe.n_ub, 1), EDGE_FIELDS);
-  cs.reserve(std::max(qs.n_ub, 1), SURF_FIELDS);
-  if (qe.n_ub > 0) {
-    hipLaunchKernelGGL(corr_kernel<true>, dim3(div_up(qe.n_ub, kTB)), dim3(kTB), 0, st, d_st, qe.pts, qe.d_n,
-                       qe.n_ub, ge.params.p, ge.pts.p, ge.tkey.p, ge.tval.p, d_me, d_ms, ce.rec.p,
-                       ce.valid.p, ce.cap, rank, world);
-    FLOAM_LAUNCH_CHECK();
+void lm_init_launch(LMState* d_st, const double* x0, hipStream_t st) {
+  X7 x{};
+  if (x0) {
+    for (int k = 0; k < 7; ++k) x.v[k] = x0[k];
+    x.set = 1;
   }
-  if (qs.n_ub > 0) {
-    hipLaunchKernelGGL(corr_kernel<false>, dim3(div_up(qs.n_ub, kTB)), dim3(kTB), 0, st, d_st, qs.pts, qs.d_n,
-                       qs.n_ub, gs.params.p, gs.pts.p, gs.tkey.p, gs.tval.p, d_me, d_ms, cs.rec.p,
-                       cs.valid.p, cs.cap, rank, world);
-    FLOAM_LAUNCH_CHECK();
+  hipLaunchKernelGGL(lm_init, dim3(1), dim3(64), 0, st, d_st, x);
+  FLOAM_LAUNCH_CHECK();
+}
+
+// One D2H per update: LM state + query / map counts (+ profiling bytes) gathered into one block.
+__global__ void gather_status(const LMState* __restrict__ lm, const int* __restrict__ dcnt,
+                              const int* __restrict__ mapE_count, const int* __restrict__ mapS_count,
+                              const unsigned long long* __restrict__ prof, UpdateStatus* __restrict__ out) {
+  constexpr int kWords = (int)(sizeof(LMState) / sizeof(unsigned));
+  const unsigned* src = reinterpret_cast<const unsigned*>(lm);
+  unsigned* dst = reinterpret_cast<unsigned*>(&out->lm);
+  for (int w = threadIdx.x; w < kWords; w += blockDim.x) dst[w] = src[w];
+  if (threadIdx.x == 0) {
+    out->counts[0] = dcnt[0];
+    out->counts[1] = dcnt[1];
+    out->counts[2] = *mapE_count;
+    out->counts[3] = *mapS_count;
+    out->prof[0] = prof ? prof[0] : 0ull;
+    out->prof[1] = prof ? prof[1] : 0ull;
   }
 }
 
-int lm_eval_launch(const LMState* d_st, const CorrSet& ce, int ne_ub, const CorrSet& cs, int ns_ub, bool huber,
-                   double* partials, hipStream_t st) {
+void gather_status_launch(const LMState* lm, const int* dcnt, const int* mapE_count, const int* mapS_count,
+                          const unsigned long long* prof, UpdateStatus* out, hipStream_t st) {
+  hipLaunchKernelGGL(gather_status, dim3(1), dim3(256), 0, st, lm, dcnt, mapE_count, mapS_count, prof, out);
+  FLOAM_LAUNCH_CHECK();
+}
+
+void corr_launch(bool edge, LMState* d_st, const QuerySet& q, const Grid& g, const PointRec* map, const int* d_me,
+                 const int* d_ms, CorrSet& c, int rank, int world, hipStream_t st) {
+  c.reserve(std::max(q.n_ub, 1), edge ? EDGE_FIELDS : SURF_FIELDS);
+  if (q.n_ub <= 0) return;
+  const unsigned blocks = std::min(div_up((size_t)q.n_ub * kGroup, kTB), 2048u);
+  if (edge) {
+    hipLaunchKernelGGL(corr_kernel<true>, dim3(blocks), dim3(kTB), 0, st, d_st, q.pts, q.d_n, q.n_ub, g.params.p,
+                       g.pts.p, g.tkey.p, g.tval.p, map, d_me, d_ms, c.rec.p, c.valid.p, c.cap, rank, world);
+  } else {
+    hipLaunchKernelGGL(corr_kernel<false>, dim3(blocks), dim3(kTB), 0, st, d_st, q.pts, q.d_n, q.n_ub, g.params.p,
+                       g.pts.p, g.tkey.p, g.tval.p, map, d_me, d_ms, c.rec.p, c.valid.p, c.cap, rank, world);
+  }
+  FLOAM_LAUNCH_CHECK();
+}
+
+void knn_traffic_launch(const LMState* d_st, const QuerySet& q, const Grid& g, const CorrSet& c, int rec_bytes,
+                        int rank, int world, DevBuf<uint32_t>& set, unsigned long long* d_bytes, hipStream_t st) {
+  if (q.n_ub <= 0) return;
+  int size = 1024, shift = 22;
+  while (size < 2 * q.n_ub) { size <<= 1; --shift; }
+  set.reserve(size);
+  FLOAM_HIP(hipMemsetAsync(set.p, 0xFF, sizeof(uint32_t) * size, st));
+  hipLaunchKernelGGL(knn_traffic, dim3(div_up(q.n_ub, kTB)), dim3(kTB), 0, st, d_st, q.pts, q.d_n, q.n_ub,
+                     g.params.p, g.tkey.p, g.tval.p, c.valid.p, rec_bytes, rank, world, set.p, (unsigned)(size - 1),
+                     shift, d_bytes);
+  FLOAM_LAUNCH_CHECK();
+}
+
+int lm_eval_launch(const LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const CorrSet& cs,
+                   const int* d_ns, int ns_ub, bool huber, double* partials, hipStream_t st) {
   const int total = std::max(ne_ub + ns_ub, 1);
-  const int nblk = (int)std::min<unsigned>(div_up(total, kTB), 512u);
-  hipLaunchKernelGGL(lm_eval, dim3(nblk), dim3(kTB), 0, st, d_st, ce.rec.p, ce.valid.p, ce.cap, ne_ub, cs.rec.p,
-                     cs.valid.p, cs.cap, ns_ub, huber ? 1 : 0, partials);
+  const int nblk = (int)std::min<unsigned>(div_up(total, kTB), kEvalBlocks);
+  hipLaunchKernelGGL(lm_eval, dim3(nblk), dim3(kTB), 0, st, d_st, ce.rec.p, ce.valid.p, ce.cap, d_ne, ne_ub,
+                     cs.rec.p, cs.valid.p, cs.cap, d_ns, ns_ub, huber ? 1 : 0, partials);
   FLOAM_LAUNCH_CHECK();
   return nblk;
+}
+
+void lm_step_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const CorrSet& cs,
+                    const int* d_ns, int ns_ub, bool huber, double* partials, unsigned* counter, hipStream_t st,
+                    unsigned long long* dbg) {
+  const int total = std::max(ne_ub + ns_ub, 1);
+  const int nblk = (int)std::min<unsigned>(div_up(total, kTB), kEvalBlocks);
+  hipLaunchKernelGGL(lm_step, dim3(nblk), dim3(kTB), 0, st, d_st, ce.rec.p, ce.valid.p, ce.cap, d_ne, ne_ub,
+                     cs.rec.p, cs.valid.p, cs.cap, d_ns, ns_ub, huber ? 1 : 0, partials, counter, dbg);
+  FLOAM_LAUNCH_CHECK();
 }
 
 void lm_control_launch(LMState* d_st, const double* partials, int nblk, hipStream_t st) {

@@ -82,12 +82,33 @@ struct QuerySet {
   int n_ub;
 };
 
-// lm_init + correspondence search for edge & surf queries, at the pose in st->x
-void corr_launch(LMState* d_st, const QuerySet& qe, const Grid& ge, const int* d_me, const QuerySet& qs,
-                 const Grid& gs, const int* d_ms, CorrSet& ce, CorrSet& cs, int rank, int world, hipStream_t st);
+struct X7 {
+  double v[7];
+  int set;
+};
+// reset the per-solve LM state; x0 (7 doubles, by value) replaces x when non-null, else x is kept
+void lm_init_launch(LMState* d_st, const double* x0, hipStream_t st);
+
+struct UpdateStatus {
+  LMState lm;
+  int counts[4];                  // downsampled edge, surf; corner map, surf map
+  unsigned long long prof[2];     // algorithmic bytes of the kNN launches (profiling)
+};
+void gather_status_launch(const LMState* lm, const int* dcnt, const int* mapE_count, const int* mapS_count,
+                          const unsigned long long* prof, UpdateStatus* out, hipStream_t st);
+// correspondence search (kNN + line / plane geometry) for one query set at the pose in st->x
+void corr_launch(bool edge, LMState* d_st, const QuerySet& q, const Grid& g, const PointRec* map, const int* d_me,
+                 const int* d_ms, CorrSet& c, int rank, int world, hipStream_t st);
+// algorithmic bytes of the correspondence launch just issued (profiling only), accumulated into *d_bytes
+void knn_traffic_launch(const LMState* d_st, const QuerySet& q, const Grid& g, const CorrSet& c, int rec_bytes,
+                        int rank, int world, DevBuf<uint32_t>& set, unsigned long long* d_bytes, hipStream_t st);
 // one LM evaluation (at x in phase 0, else at cand): block partial sums of (cost, J^T J, J^T r, count)
-int lm_eval_launch(const LMState* d_st, const CorrSet& ce, int ne_ub, const CorrSet& cs, int ns_ub, bool huber,
-                   double* partials, hipStream_t st);
+int lm_eval_launch(const LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const CorrSet& cs,
+                   const int* d_ns, int ns_ub, bool huber, double* partials, hipStream_t st);
+// fused evaluation + control (single GPU): the last block reduces and runs the LM step; counter starts at 0
+void lm_step_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const CorrSet& cs,
+                    const int* d_ns, int ns_ub, bool huber, double* partials, unsigned* counter, hipStream_t st,
+                    unsigned long long* dbg = nullptr);
 // reduce partials (nblk > 0) or read 29 pre-reduced sums (nblk == 0), then run the Ceres LM control step
 void lm_control_launch(LMState* d_st, const double* partials, int nblk, hipStream_t st);
 void lm_reduce_launch(const double* partials, int nblk, double* sums, hipStream_t st);
