@@ -69,6 +69,11 @@ def lib():
         L.oracle_odom_num_traces.restype = C.c_size_t
         L.oracle_odom_get_trace.argtypes = [C.c_void_p, C.c_size_t, c_double_p]
         L.oracle_reset_process_statics.argtypes = []
+        L.oracle_edge_residual.argtypes = [c_double_p] * 5
+        L.oracle_edge_residual.restype = C.c_double
+        L.oracle_surf_residual.argtypes = [c_double_p, c_double_p, C.c_double, c_double_p, c_double_p]
+        L.oracle_surf_residual.restype = C.c_double
+        L.oracle_se3_plus.argtypes = [c_double_p] * 3
         _LIB = L
     return _LIB
 
@@ -229,3 +234,34 @@ class Odometry:
 
 def reset_process_statics():
     lib().oracle_reset_process_statics()
+
+
+def _dptr(a):
+    return a.ctypes.data_as(c_double_p)
+
+
+def edge_residual(cp, a, b, x):
+    """EdgeAnalyticCostFunction::Evaluate (src/lidarOptimization.cpp:12-43): (r, J over the 6 local params)."""
+    L = lib()
+    J = np.zeros(7)
+    v = [np.ascontiguousarray(t, dtype=np.float64) for t in (cp, a, b, x)]
+    r = L.oracle_edge_residual(_dptr(v[0]), _dptr(v[1]), _dptr(v[2]), _dptr(v[3]), _dptr(J))
+    return r, J[:6]
+
+
+def surf_residual(cp, n, d, x):
+    """SurfNormAnalyticCostFunction::Evaluate (src/lidarOptimization.cpp:51-74)."""
+    L = lib()
+    J = np.zeros(7)
+    v = [np.ascontiguousarray(t, dtype=np.float64) for t in (cp, n, x)]
+    r = L.oracle_surf_residual(_dptr(v[0]), _dptr(v[1]), float(d), _dptr(v[2]), _dptr(J))
+    return r, J[:6]
+
+
+def se3_plus(x, delta):
+    """PoseSE3Parameterization::Plus (src/lidarOptimization.cpp:77-92)."""
+    out = np.zeros(7)
+    xx = np.ascontiguousarray(x, dtype=np.float64)
+    dd = np.ascontiguousarray(delta, dtype=np.float64)
+    lib().oracle_se3_plus(_dptr(xx), _dptr(dd), _dptr(out))
+    return out

@@ -117,4 +117,12 @@ void oracle_odom_get_trace(void* h, size_t i, double* out /* 49 */) {
 void oracle_odom_clear_traces(void* h) { odom_clear_traces(static_cast<OdomState*>(h)); }
 void oracle_reset_process_statics() { reset_process_statics(); }
 
+double oracle_edge_residual(const double* cp, const double* a, const double* b, const double* x, double* J) {
+  return test_edge_eval(cp, a, b, x, J);
+}
+double oracle_surf_residual(const double* cp, const double* n, double d, const double* x, double* J) {
+  return test_surf_eval(cp, n, d, x, J);
+}
+void oracle_se3_plus(const double* x, const double* delta, double* out) { test_se3_plus(x, delta, out); }
+
 }  // extern "C"

@@ -320,6 +320,15 @@ SolveOut ceres_solve(const Problem& P, double* params) {
 
 }  // namespace
 
+// test hooks (capi.cpp): the cost functions and the manifold Plus, for Jacobian known-answer tests
+double test_edge_eval(const double cp[3], const double a[3], const double b[3], const double* x, double* J) {
+  return edge_eval(EdgeBlock{V3{cp[0], cp[1], cp[2]}, V3{a[0], a[1], a[2]}, V3{b[0], b[1], b[2]}}, x, J);
+}
+double test_surf_eval(const double cp[3], const double n[3], double d, const double* x, double* J) {
+  return surf_eval(SurfBlock{V3{cp[0], cp[1], cp[2]}, V3{n[0], n[1], n[2]}, d}, x, J);
+}
+void test_se3_plus(const double* x, const double* delta, double* out) { se3_plus(x, delta, out); }
+
 // ------------------------------------------------------------------------------------------ odometry state
 struct OdomState {
   LidarParams lp;

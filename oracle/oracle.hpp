@@ -113,5 +113,8 @@ const std::vector<SolveTrace>& odom_traces(const OdomState*);
 void odom_clear_traces(OdomState*);
 int odom_optimization_count(const OdomState*);
 void reset_process_statics();   // KeyFrameUpdate's function-static `first` (odomEstimationClass.cpp:323, Q6)
+double test_edge_eval(const double cp[3], const double a[3], const double b[3], const double* x, double* J);
+double test_surf_eval(const double cp[3], const double n[3], double d, const double* x, double* J);
+void test_se3_plus(const double* x, const double* delta, double* out);
 
 }  // namespace oracle
