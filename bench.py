@@ -93,7 +93,7 @@ def main():
     from floam_amd.odom_estimation import comm_unique_id, reset_process_state
 
     L = _ffi.load()
-    dev = local_rank
+    dev = int(os.environ.get("FLOAM_BENCH_DEVICE", local_rank))   # override: several ranks on one GPU (testing)
     cfg = args.config
     model = synth.lidar_model(cfg)
     R = model.rings
@@ -118,10 +118,22 @@ def main():
     lp.init(params)
     odo = floam_amd.OdomEstimationClass(device=dev)
     odo.init(params, MAP_RES, LOSS)
+    allreduce_impl = None
     if world > 1 and args.mode == "shard":
         uid = [comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
-        odo.set_shard(rank, world, uid[0])
+        try:
+            odo.set_shard(rank, world, uid[0])   # RCCL over xGMI
+            allreduce_impl = "rccl"
+        except floam_amd.FloamError as e:   # e.g. several ranks on one GPU: host all-reduce over gloo
+            log(f"[rank {rank}] RCCL unavailable ({e}); using the gloo host all-reduce")
+            import torch
+
+            def _allreduce(arr):
+                t = torch.from_numpy(arr)
+                dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            odo.set_shard_callback(rank, world, _allreduce)
+            allreduce_impl = "gloo-host"
     d_raw = [floam_amd.DeviceCloud(r, device=dev) for r in raws]       # inputs resident in HBM
     odo.initMapWithPoints(floam_amd.DeviceCloud(mapE, device=dev), floam_amd.DeviceCloud(mapS, device=dev))
     d_edge, d_surf = floam_amd.DeviceCloud(device=dev), floam_amd.DeviceCloud(device=dev)
@@ -223,8 +235,8 @@ def main():
             "config": {"workload": f"{cfg}: {R}-ring synthetic scans ({raws[0].shape[0]} pts), map prefilled "
                                    f"{target} pts, deskew on, loss {LOSS} (no robust loss, Q3), map_res {MAP_RES}",
                        "rings": R, "points_per_scan": int(raws[0].shape[0]), "map_prefill": target,
-                       "parallelism": (f"query-shard x{world} (RCCL all-reduce of J^T J)" if args.mode == "shard"
-                                       else f"replica x{world}")},
+                       "parallelism": (f"query-shard x{world} ({allreduce_impl or 'no'} all-reduce of J^T J)"
+                                       if args.mode == "shard" else f"replica x{world}")},
             "roofline": roof,
             "cpu_baseline": cpu,
             "pose_vs_oracle": pose_err,

@@ -32,7 +32,7 @@ EXPORTS = [
     "floam_odom_create", "floam_odom_destroy", "floam_odom_init_map", "floam_odom_update_selector",
     "floam_odom_update", "floam_odom_get_pose", "floam_odom_get_last_pose", "floam_odom_get_velocity",
     "floam_odom_get_map", "floam_odom_get_map_sizes", "floam_odom_download_maps", "floam_odom_get_stats",
-    "floam_comm_unique_id", "floam_odom_set_shard",
+    "floam_comm_unique_id", "floam_odom_set_shard", "floam_odom_set_shard_callback",
     "floam_last_error", "floam_version", "floam_reset_process_state", "floam_device_synchronize",
     "floam_profile_enable", "floam_profile_read", "floam_profile_reset",
 ]
@@ -54,6 +54,9 @@ class OdomStats(C.Structure):
                 ("surf_queries", C.c_int), ("edge_correspondences", C.c_int), ("surf_correspondences", C.c_int),
                 ("lm_iterations", C.c_int), ("map_updated", C.c_int), ("corner_map", C.c_size_t),
                 ("surf_map", C.c_size_t), ("final_cost", C.c_double)]
+
+
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.c_int, C.c_void_p)
 
 
 class KernelTiming(C.Structure):
@@ -91,6 +94,7 @@ def load(path: str | None = None):
         "floam_odom_get_map": [vp, vp], "floam_odom_get_map_sizes": [vp, szp, szp],
         "floam_odom_download_maps": [vp, vp, sz, vp, sz], "floam_odom_get_stats": [vp, C.POINTER(OdomStats)],
         "floam_comm_unique_id": [vp], "floam_odom_set_shard": [vp, i32, i32, vp],
+        "floam_odom_set_shard_callback": [vp, i32, i32, ALLREDUCE_FN, vp],
         "floam_device_synchronize": [i32], "floam_profile_enable": [i32, i32],
         "floam_profile_read": [i32, C.POINTER(KernelTiming), i32, C.POINTER(C.c_int)], "floam_profile_reset": [i32],
     }

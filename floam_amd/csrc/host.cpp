@@ -205,6 +205,9 @@ struct floam_odom {
   // sharding
   int rank = 0, world = 1;
   ncclComm_t comm = nullptr;
+  floam_allreduce_fn ar_fn = nullptr;   // host all-reduce (validation mode), used when comm is null
+  void* ar_user = nullptr;
+  HostBuf<double> h_sums;
   floam_odom_stats stats{};
   floam_status last_warning = FLOAM_OK;
 };
@@ -262,9 +265,18 @@ bool keyframe_update(floam_odom* o, const Pose& pose) {   // KeyFrameUpdate (odo
 }
 
 void allreduce_sums(floam_odom* o, DeviceCtx& ctx) {
-  const ncclResult_t r =
-      ncclAllReduce(o->sums.p, o->sums.p, LM_NSUM, ncclDouble, ncclSum, o->comm, ctx.stream);
-  if (r != ncclSuccess) throw Error(FLOAM_ERR_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+  if (o->comm) {
+    const ncclResult_t r = ncclAllReduce(o->sums.p, o->sums.p, LM_NSUM, ncclDouble, ncclSum, o->comm, ctx.stream);
+    if (r != ncclSuccess) throw Error(FLOAM_ERR_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+    return;
+  }
+  if (!o->ar_fn) throw Error(FLOAM_ERR_COMM, "sharded odometry without a communicator");
+  o->h_sums.reserve(LM_NSUM);
+  FLOAM_HIP(hipMemcpyAsync(o->h_sums.p, o->sums.p, sizeof(double) * LM_NSUM, hipMemcpyDeviceToHost, ctx.stream));
+  FLOAM_HIP(hipStreamSynchronize(ctx.stream));
+  if (o->ar_fn(o->h_sums.p, LM_NSUM, o->ar_user) != 0) throw Error(FLOAM_ERR_COMM, "host all-reduce callback failed");
+  FLOAM_HIP(hipMemcpyAsync(o->sums.p, o->h_sums.p, sizeof(double) * LM_NSUM, hipMemcpyHostToDevice, ctx.stream));
+  FLOAM_HIP(hipStreamSynchronize(ctx.stream));
 }
 
 // updatePointsToMap (src/odomEstimationClass.cpp:52-124)
@@ -807,6 +819,7 @@ floam_status floam_odom_set_shard(floam_odom* o, int rank, int world, const void
       ncclCommDestroy(o->comm);
       o->comm = nullptr;
     }
+    o->ar_fn = nullptr;
     o->rank = rank;
     o->world = world;
     if (world > 1) {
@@ -817,6 +830,22 @@ floam_status floam_odom_set_shard(floam_odom* o, int rank, int world, const void
       const ncclResult_t r = ncclCommInitRank(&o->comm, world, u, rank);
       if (r != ncclSuccess) throw Error(FLOAM_ERR_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
     }
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_odom_set_shard_callback(floam_odom* o, int rank, int world, floam_allreduce_fn fn, void* user) {
+  return guarded([&] {
+    if (!o || world < 1 || rank < 0 || rank >= world) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "bad rank / world");
+    if (world > 1 && !fn) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null all-reduce callback");
+    if (o->comm) {
+      ncclCommDestroy(o->comm);
+      o->comm = nullptr;
+    }
+    o->rank = rank;
+    o->world = world;
+    o->ar_fn = fn;
+    o->ar_user = user;
     return FLOAM_OK;
   });
 }

@@ -139,6 +139,19 @@ class OdomEstimationClass:
             buf = C.create_string_buffer(bytes(unique_id), 128)
         _ffi.check(self._L.floam_odom_set_shard(self._need(), rank, world, buf))
 
+    def set_shard_callback(self, rank: int, world: int, allreduce) -> None:
+        """Shard with a host all-reduce: ``allreduce(values: np.ndarray[float64])`` sums in place over ranks
+        (e.g. torch.distributed with gloo).  Validation mode for hosts where RCCL cannot run."""
+        def _cb(ptr, n, _user):
+            try:
+                arr = np.ctypeslib.as_array(ptr, shape=(n,))
+                allreduce(arr)
+                return 0
+            except Exception:   # reported as FLOAM_ERR_COMM by the library
+                return 1
+        self._ar_cb = _ffi.ALLREDUCE_FN(_cb)   # keep alive
+        _ffi.check(self._L.floam_odom_set_shard_callback(self._need(), rank, world, self._ar_cb, None))
+
     def close(self) -> None:
         if getattr(self, "_h", None):
             self._L.floam_odom_destroy(self._h)

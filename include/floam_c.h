@@ -130,6 +130,11 @@ floam_status floam_odom_get_stats(const floam_odom* o, floam_odom_stats* s);
  * rank 0, broadcast by the caller (e.g. torch.distributed). */
 floam_status floam_comm_unique_id(void* unique_id_128);
 floam_status floam_odom_set_shard(floam_odom* o, int rank, int world, const void* unique_id_128);
+/* Same sharding with a caller-supplied host all-reduce instead of RCCL (in-place sum of `count` doubles over all
+ * ranks, return 0 on success), e.g. torch.distributed/gloo.  Used to validate the sharded path when RCCL cannot
+ * run (several ranks on one GPU); synchronises once per LM evaluation. */
+typedef int (*floam_allreduce_fn)(double* values, int count, void* user);
+floam_status floam_odom_set_shard_callback(floam_odom* o, int rank, int world, floam_allreduce_fn fn, void* user);
 
 /* ------------------------------------------------------------------------------------------ misc */
 const char* floam_last_error(void);
