@@ -67,6 +67,20 @@ def prefill_map(synth, oracle_fe, config, R, target):
     return E, S
 
 
+def hbm_traffic(kernel_substr):
+    """HBM bytes per launch of the dominant kernel from the newest committed rocprofv3 PMC summary
+    (profiles/<tag>/hbm_traffic.json, written by tools/prof_summary.py from separate --pmc FETCH_SIZE / WRITE_SIZE
+    runs of this bench).  (None, None) when no profile is committed."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "hbm_traffic.json")))
+    for f in reversed(files):
+        d = json.load(open(f))
+        for name, v in d.get("kernels", {}).items():
+            if kernel_substr in name:
+                return round(v["total_bytes"]), os.path.relpath(f, ROOT)
+    return None, None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -113,34 +127,43 @@ def main():
 
     params = floam_amd.LidarParams(num_lines=R, scan_period=SCAN_PERIOD, vertical_angle=2.0, max_distance=MAX_DIS,
                                    min_distance=MIN_DIS)
-    reset_process_state()
-    lp = floam_amd.LaserProcessingClass(device=dev)
-    lp.init(params)
-    odo = floam_amd.OdomEstimationClass(device=dev)
-    odo.init(params, MAP_RES, LOSS)
-    allreduce_impl = None
-    if world > 1 and args.mode == "shard":
-        uid = [comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        try:
-            odo.set_shard(rank, world, uid[0])   # RCCL over xGMI
-            allreduce_impl = "rccl"
-        except floam_amd.FloamError as e:   # e.g. several ranks on one GPU: host all-reduce over gloo
-            log(f"[rank {rank}] RCCL unavailable ({e}); using the gloo host all-reduce")
-            import torch
-
-            def _allreduce(arr):
-                t = torch.from_numpy(arr)
-                dist.all_reduce(t, op=dist.ReduceOp.SUM)
-            odo.set_shard_callback(rank, world, _allreduce)
-            allreduce_impl = "gloo-host"
     d_raw = [floam_amd.DeviceCloud(r, device=dev) for r in raws]       # inputs resident in HBM
-    odo.initMapWithPoints(floam_amd.DeviceCloud(mapE, device=dev), floam_amd.DeviceCloud(mapS, device=dev))
+    d_mapE, d_mapS = floam_amd.DeviceCloud(mapE, device=dev), floam_amd.DeviceCloud(mapS, device=dev)
+    allreduce_impl = None
+    uid = None
+    if world > 1 and args.mode == "shard":
+        uid = [(comm_unique_id(), comm_unique_id()) if rank == 0 else None]   # timed run, byte-count replay
+        dist.broadcast_object_list(uid, src=0)
+    n_pipelines = 0
+
+    def make_pipeline():
+        nonlocal allreduce_impl, n_pipelines
+        reset_process_state()
+        lp = floam_amd.LaserProcessingClass(device=dev)
+        lp.init(params)
+        odo = floam_amd.OdomEstimationClass(device=dev)
+        odo.init(params, MAP_RES, LOSS)
+        if uid is not None:
+            try:
+                odo.set_shard(rank, world, uid[0][n_pipelines])   # RCCL over xGMI
+                allreduce_impl = "rccl"
+            except floam_amd.FloamError as e:   # e.g. several ranks on one GPU: host all-reduce over gloo
+                log(f"[rank {rank}] RCCL unavailable ({e}); using the gloo host all-reduce")
+                import torch
+
+                def _allreduce(arr):
+                    t = torch.from_numpy(arr)
+                    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+                odo.set_shard_callback(rank, world, _allreduce)
+                allreduce_impl = "gloo-host"
+        odo.initMapWithPoints(d_mapE, d_mapS)
+        n_pipelines += 1
+        return lp, odo
+
+    lp, odo = make_pipeline()
     d_edge, d_surf = floam_amd.DeviceCloud(device=dev), floam_amd.DeviceCloud(device=dev)
 
-    poses = []
-
-    def step(k):
+    def step(lp, odo, k, poses):
         d_edge.clear()
         d_surf.clear()
         lp.featureExtraction(d_raw[k], d_edge, d_surf)
@@ -152,15 +175,16 @@ def main():
             dist.barrier()
         _ffi.check(L.floam_device_synchronize(dev))
 
+    poses = []
     for k in range(args.warmup):
-        step(k)
+        step(lp, odo, k, poses)
     if not args.no_roofline:
         _ffi.check(L.floam_profile_reset(dev))
-        _ffi.check(L.floam_profile_enable(dev, 1))   # FLOAM_PROF_KNN: events around the two kNN kernels only
+        _ffi.check(L.floam_profile_enable(dev, 1))   # FLOAM_PROF_KNN: HIP events around the two kNN kernels only
     barrier_sync()
     t_start = time.perf_counter()
     for k in range(args.warmup, n_scans):
-        step(k)
+        step(lp, odo, k, poses)
     barrier_sync()
     elapsed = time.perf_counter() - t_start
     _ffi.check(L.floam_profile_enable(dev, 0))
@@ -171,24 +195,45 @@ def main():
         elapsed = float(t.item())
     stats = odo.stats()
 
-    roof = None
-    if not args.no_roofline:
+    def read_timings():
         arr = (_ffi.KernelTiming * 16)()
         n = C.c_int()
         _ffi.check(L.floam_profile_read(dev, arr, 16, C.byref(n)))
-        timings = {arr[i].name.decode(): arr[i] for i in range(min(n.value, 16))}
-        kt = timings.get("knn_surf")
-        if kt is not None and kt.launches > 0:
-            avg_ms = kt.total_ms / kt.launches
-            bytes_per = kt.algorithmic_bytes / kt.launches
+        return {arr[i].name.decode(): (arr[i].launches, arr[i].total_ms, arr[i].algorithmic_bytes)
+                for i in range(min(n.value, 16))}
+
+    roof = None
+    if not args.no_roofline:
+        timed = read_timings()
+        odo.close()
+        lp.close()
+        # Algorithmic bytes of the timed launches: an identical, untimed replay of the same sequence (the pipeline
+        # is deterministic) with the byte-counting kernel after each correspondence launch (FLOAM_PROF_KNN_BYTES).
+        lp, odo = make_pipeline()
+        replay = []
+        for k in range(args.warmup):
+            step(lp, odo, k, replay)
+        _ffi.check(L.floam_profile_reset(dev))
+        _ffi.check(L.floam_profile_enable(dev, 16))
+        for k in range(args.warmup, n_scans):
+            step(lp, odo, k, replay)
+        _ffi.check(L.floam_profile_enable(dev, 0))
+        counted = read_timings()
+        same = all(np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) for a, b in zip(poses, replay))
+        kt, kb = timed.get("knn_surf"), counted.get("knn_surf")
+        if kt is not None and kt[0] > 0 and kb is not None:
+            avg_ms = kt[1] / kt[0]
+            bytes_per = kb[2] / kt[0]
             ach = bytes_per / (avg_ms * 1e-3) / 1e9
+            traffic, traffic_src = hbm_traffic("corr_kernel<false>")
             roof = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
+                    "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": traffic_src,
                     "kernel": "corr_kernel<false> (surf kNN + plane geometry)", "avg_us": round(avg_ms * 1e3, 2),
-                    "launches": int(kt.launches), "algorithmic_bytes_per_launch": round(bytes_per)}
-            ke = timings.get("knn_edge")
-            if ke is not None and ke.launches:
-                roof["edge_kernel_avg_us"] = round(ke.total_ms / ke.launches * 1e3, 2)
+                    "launches": int(kt[0]), "algorithmic_bytes_per_launch": round(bytes_per),
+                    "replay_bitwise_identical": bool(same)}
+            ke = timed.get("knn_edge")
+            if ke is not None and ke[0]:
+                roof["edge_kernel_avg_us"] = round(ke[1] / ke[0] * 1e3, 2)
 
     cpu = None
     pose_err = None

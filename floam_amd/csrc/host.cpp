@@ -340,7 +340,7 @@ void odom_update(floam_odom* o, const floam_cloud* edge, const floam_cloud* surf
       corr_launch(false, o->lm.p, qs, o->gS, o->mapS.pts.p, o->mapE.count.p, o->mapS.count.p, o->cs, o->rank,
                   o->world, st);
     }
-    if (ctx.profile & FLOAM_PROF_KNN) {   // untimed: algorithmic bytes of the two launches above
+    if (ctx.profile & FLOAM_PROF_KNN_BYTES) {   // replay only: algorithmic bytes of the two launches above
       knn_traffic_launch(o->lm.p, qe, o->gE, o->ce, 8 * EDGE_FIELDS, o->rank, o->world, o->traffic_set,
                          o->prof_bytes.p + 0, st);
       knn_traffic_launch(o->lm.p, qs, o->gS, o->cs, 8 * SURF_FIELDS, o->rank, o->world, o->traffic_set,
@@ -361,7 +361,7 @@ void odom_update(floam_odom* o, const floam_cloud* edge, const floam_cloud* surf
       }
     }
   }
-  const bool prof_knn = (ctx.profile & FLOAM_PROF_KNN) != 0;
+  const bool prof_knn = (ctx.profile & FLOAM_PROF_KNN_BYTES) != 0;
   o->ustat.reserve(1);
   o->h_ustat.reserve(1);
   if (o->optimization_count <= 0) lm_init_launch(o->lm.p, o->parameters, st);

@@ -145,8 +145,11 @@ void floam_reset_process_state(void);
 floam_status floam_device_synchronize(int device);
 
 /* Per-kernel timing with HIP events recorded on the library stream (bench.py's roofline leg).
- * floam_profile_enable(device, mask): mask = OR of the categories below (0 disables). */
-enum { FLOAM_PROF_KNN = 1, FLOAM_PROF_LM = 2, FLOAM_PROF_CLOUD = 4, FLOAM_PROF_FE = 8, FLOAM_PROF_ALL = 0xFF };
+ * floam_profile_enable(device, mask): mask = OR of the categories below (0 disables).
+ * FLOAM_PROF_KNN_BYTES adds an extra (non-product) kernel after each correspondence launch that counts its
+ * algorithmic bytes; it is kept out of timed runs and used on an identical replay instead. */
+enum { FLOAM_PROF_KNN = 1, FLOAM_PROF_LM = 2, FLOAM_PROF_CLOUD = 4, FLOAM_PROF_FE = 8, FLOAM_PROF_KNN_BYTES = 16,
+       FLOAM_PROF_ALL = 0xEF };
 typedef struct floam_kernel_timing {
   char name[32];
   long long launches;
