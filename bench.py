@@ -220,20 +220,17 @@ def main():
         _ffi.check(L.floam_profile_enable(dev, 0))
         counted = read_timings()
         same = all(np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) for a, b in zip(poses, replay))
-        kt, kb = timed.get("knn_surf"), counted.get("knn_surf")
+        kt, kb = timed.get("knn"), counted.get("knn")
         if kt is not None and kt[0] > 0 and kb is not None:
             avg_ms = kt[1] / kt[0]
             bytes_per = kb[2] / kt[0]
             ach = bytes_per / (avg_ms * 1e-3) / 1e9
-            traffic, traffic_src = hbm_traffic("corr_kernel<false>")
+            traffic, traffic_src = hbm_traffic("corr_kernel(")
             roof = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": traffic_src,
-                    "kernel": "corr_kernel<false> (surf kNN + plane geometry)", "avg_us": round(avg_ms * 1e3, 2),
+                    "kernel": "corr_kernel (edge + surf kNN, line / plane geometry)", "avg_us": round(avg_ms * 1e3, 2),
                     "launches": int(kt[0]), "algorithmic_bytes_per_launch": round(bytes_per),
                     "replay_bitwise_identical": bool(same)}
-            ke = timed.get("knn_edge")
-            if ke is not None and ke[0]:
-                roof["edge_kernel_avg_us"] = round(ke[1] / ke[0] * 1e3, 2)
 
     cpu = None
     pose_err = None

@@ -315,8 +315,8 @@ void odom_update(floam_odom* o, const floam_cloud* edge, const floam_cloud* surf
     o->step_counter.reserve(1);
     FLOAM_HIP(hipMemsetAsync(o->step_counter.p, 0, sizeof(unsigned), st));
     if (std::getenv("FLOAM_DEBUG_STAMPS")) {
-      o->dbg_stamps.reserve(8);
-      FLOAM_HIP(hipMemsetAsync(o->dbg_stamps.p, 0, sizeof(unsigned long long) * 8, st));
+      o->dbg_stamps.reserve(32);
+      FLOAM_HIP(hipMemsetAsync(o->dbg_stamps.p, 0, sizeof(unsigned long long) * 32, st));
     }
   }
   o->prof_bytes.reserve(2);
@@ -331,14 +331,9 @@ void odom_update(floam_odom* o, const floam_cloud* edge, const floam_cloud* surf
   for (int it = 0; it < o->optimization_count; ++it) {
     lm_init_launch(o->lm.p, it == 0 ? o->parameters : nullptr, st);   // first solve starts at the prediction
     {
-      ProfScope ps(ctx, "knn_edge", FLOAM_PROF_KNN);
-      corr_launch(true, o->lm.p, qe, o->gE, o->mapE.pts.p, o->mapE.count.p, o->mapS.count.p, o->ce, o->rank,
-                  o->world, st);
-    }
-    {
-      ProfScope ps(ctx, "knn_surf", FLOAM_PROF_KNN);
-      corr_launch(false, o->lm.p, qs, o->gS, o->mapS.pts.p, o->mapE.count.p, o->mapS.count.p, o->cs, o->rank,
-                  o->world, st);
+      ProfScope ps(ctx, "knn", FLOAM_PROF_KNN);
+      corr_launch(o->lm.p, qe, o->gE, o->mapE.pts.p, o->ce, qs, o->gS, o->mapS.pts.p, o->cs, o->mapE.count.p,
+                  o->mapS.count.p, o->rank, o->world, st, o->dbg_stamps.p ? o->dbg_stamps.p + 8 : nullptr);
     }
     if (ctx.profile & FLOAM_PROF_KNN_BYTES) {   // replay only: algorithmic bytes of the two launches above
       knn_traffic_launch(o->lm.p, qe, o->gE, o->ce, 8 * EDGE_FIELDS, o->rank, o->world, o->traffic_set,
@@ -372,10 +367,12 @@ void odom_update(floam_odom* o, const floam_cloud* edge, const floam_cloud* surf
   FLOAM_HIP(hipStreamSynchronize(st));
   ctx.drain();
   if (prof_knn) {
-    ctx.totals["knn_edge"].algorithmic_bytes += (double)o->h_ustat.p->prof[0];
-    ctx.totals["knn_surf"].algorithmic_bytes += (double)o->h_ustat.p->prof[1];
+    floam_kernel_timing& t = ctx.totals["knn"];
+    std::strncpy(t.name, "knn", sizeof(t.name) - 1);
+    t.algorithmic_bytes += (double)o->h_ustat.p->prof[0] + (double)o->h_ustat.p->prof[1];
   }
   const LMState& L = o->h_ustat.p->lm;
+  if (L.n_res < 0) throw Error(FLOAM_ERR_DEVICE, "LM evaluation blocks did not arrive at the control block (timeout)");
   const int* hc = o->h_ustat.p->counts;
   const int nEd = hc[0], nSd = hc[1];
   o->mapE_n = (size_t)hc[2];
@@ -662,11 +659,19 @@ floam_status floam_odom_destroy(floam_odom* o) {
       DeviceCtx& ctx = ctx_for(o->device);
       FLOAM_HIP(hipStreamSynchronize(ctx.stream));
       if (o->dbg_stamps.p) {
-        unsigned long long h[8];
+        unsigned long long h[32];
         FLOAM_HIP(hipMemcpy(h, o->dbg_stamps.p, sizeof(h), hipMemcpyDeviceToHost));
         const double n = h[4] ? (double)h[4] : 1.0;
-        std::fprintf(stderr, "[floam stamps] lm_step x%llu: eval %.2f us, arrive %.2f us, reduce %.2f us, logic %.2f us\n",
-                     h[4], h[0] / n / 100.0, h[1] / n / 100.0, h[2] / n / 100.0, h[3] / n / 100.0);
+        std::fprintf(stderr, "[floam stamps] lm_step x%llu (control block): stage %.2f us, wait %.2f us, reduce %.2f us,"
+                   " control step %.2f us\n", h[4], h[0] / n / 100.0, h[1] / n / 100.0, h[2] / n / 100.0,
+                   h[3] / n / 100.0);
+        for (int set = 0; set < 2; ++set) {
+          const unsigned long long* c = h + 8 + 8 * set;
+          const double q = c[4] ? (double)c[4] : 1.0;
+          std::fprintf(stderr, "[floam stamps] knn %s: %llu queries, per query: lookup %.2f us, scan %.2f us, merge "
+                       "%.2f us, %.1f candidates\n", set ? "surf" : "edge", c[4],
+                       c[0] / q / 100.0, c[1] / q / 100.0, c[2] / q / 100.0, c[5] / q);
+        }
       }
       if (o->comm) ncclCommDestroy(o->comm);
       delete o;

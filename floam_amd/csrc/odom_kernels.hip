@@ -59,10 +59,10 @@ __device__ __forceinline__ int cell_of(double v, double o, double inv_c, int n) 
 
 __global__ __launch_bounds__(kTB) void grid_keys(const PointRec* __restrict__ map, const int* __restrict__ d_m, int m_ub,
                                                  const GridParams* __restrict__ gp, uint32_t* __restrict__ keys,
-                                                 int* __restrict__ vals, uint32_t* __restrict__ tkey, int tsize) {
+                                                 int* __restrict__ vals, int4* __restrict__ tab, int tsize) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   // clear the hash table here (grid_fill inserts only after the sort), saving a memset node
-  for (int t = i; t < tsize; t += gridDim.x * blockDim.x) tkey[t] = kEmpty;
+  for (int t = i; t < tsize; t += gridDim.x * blockDim.x) tab[t] = make_int4((int)kEmpty, 0, 0, 0);
   if (i >= m_ub) return;
   uint32_t key = kEmpty;
   if (i < *d_m) {
@@ -81,7 +81,7 @@ __device__ __forceinline__ uint32_t hash_slot(uint32_t key, int shift) { return 
 __global__ __launch_bounds__(kTB) void grid_fill(const PointRec* __restrict__ map, const int* __restrict__ d_m,
                                                  const uint32_t* __restrict__ keys, const int* __restrict__ vals,
                                                  const GridParams* __restrict__ gp, float4* __restrict__ pts,
-                                                 uint32_t* __restrict__ tkey, int2* __restrict__ tval) {
+                                                 int4* __restrict__ tab) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   const int m = *d_m;
   if (i >= m) return;
@@ -95,9 +95,10 @@ __global__ __launch_bounds__(kTB) void grid_fill(const PointRec* __restrict__ ma
     const GridParams p = *gp;
     uint32_t h = hash_slot(k, p.shift);
     for (;;) {
-      const uint32_t prev = atomicCAS(&tkey[h], kEmpty, k);
+      const uint32_t prev = atomicCAS(reinterpret_cast<uint32_t*>(&tab[h].x), kEmpty, k);
       if (prev == kEmpty) {
-        tval[h] = make_int2(i, e - i);
+        tab[h].y = i;
+        tab[h].z = e - i;
         break;
       }
       h = (h + 1) & p.mask;
@@ -410,18 +411,23 @@ __device__ void plane_solve(const double (&A)[5][3], double (&x)[3]) {
 }
 
 // ===================================================================================== correspondence search
-// One query per group of kGroup lanes: the lanes stride the candidates of each stencil cell (coalesced 16-B
-// loads from the cell-sorted map), each keeps a sorted top-5 of 64-bit keys (float sq-distance bits << 32 | map
-// index: ascending distance, ties by map index), and a butterfly merge over the group gives the exact 5-NN.
+// One query per group of kGroup lanes.  The group looks up the (<= 27) stencil cells of its query in parallel
+// (one 16-B hash probe per cell), scans their counts into an exclusive prefix held in LDS, and then walks the
+// FLATTENED candidate list: candidate t of the query lives in cell c with pre[c] <= t < pre[c+1], so the lanes
+// take t = lane, lane + 16, ... with a forward-only cursor and kUnroll independent 16-B loads in flight per lane
+// (coalesced within a cell, since cells are contiguous runs of the cell-sorted map).  Each lane keeps a sorted
+// top-5 of 64-bit keys (float sq-distance bits << 32 | map index: ascending distance, ties by map index) and a
+// butterfly merge over the group gives the exact 5-NN; lane 0 then runs the fp64 line / plane geometry.
 constexpr int kGroup = 16;
+constexpr int kGroupsPerBlock = kTB / kGroup;
+constexpr int kUnroll = 4;
 
-__device__ __forceinline__ int2 grid_lookup(const uint32_t* __restrict__ tkey, const int2* __restrict__ tval,
-                                            uint32_t key, int shift, unsigned mask) {
+__device__ __forceinline__ int2 grid_lookup(const int4* __restrict__ tab, uint32_t key, int shift, unsigned mask) {
   uint32_t h = hash_slot(key, shift);
   for (;;) {
-    const uint32_t k = tkey[h];
-    if (k == key) return tval[h];
-    if (k == kEmpty) return make_int2(0, 0);
+    const int4 e = tab[h];
+    if ((uint32_t)e.x == key) return make_int2(e.y, e.z);
+    if ((uint32_t)e.x == kEmpty) return make_int2(0, 0);
     h = (h + 1) & mask;
   }
 }
@@ -462,31 +468,58 @@ __device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v,
   return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
 }
 
-template <bool EDGE>
-__global__ __launch_bounds__(kTB) void corr_kernel(LMState* __restrict__ st, const PointRec* __restrict__ q,
-                                                   const int* __restrict__ d_n, int n_ub,
-                                                   const GridParams* __restrict__ gp, const float4* __restrict__ gpts,
-                                                   const uint32_t* __restrict__ tkey, const int2* __restrict__ tval,
-                                                   const PointRec* __restrict__ map,
-                                                   const int* __restrict__ d_me, const int* __restrict__ d_ms,
-                                                   double* __restrict__ rec, uint8_t* __restrict__ valid, int cap,
-                                                   int rank, int world) {
-  const int lane = threadIdx.x & (kGroup - 1);
-  const int n = min(*d_n, n_ub);
+__device__ __forceinline__ int group_incl_scan(int v, int lane) {
+#pragma unroll
+  for (int o = 1; o < kGroup; o <<= 1) {
+    const int u = __shfl_up(v, o, kGroup);
+    if (lane >= o) v += u;
+  }
+  return v;
+}
+
+// LDS written by some lanes of a wave and read by others of the same wave: DS ops of one wave execute in order,
+// so only the compiler has to be kept from reordering.
+__device__ __forceinline__ void wave_lds_order() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+struct CorrArgs {
+  const PointRec* q;       // downsampled scan points (sensor frame)
+  const int* d_n;          // device count
+  int n_ub;
+  const GridParams* gp;
+  const float4* gpts;
+  const int4* tab;
+  const PointRec* map;
+  double* rec;
+  uint8_t* valid;
+  int* nn;
+  int cap;
+  unsigned long long* dbg;   // FLOAM_DEBUG_STAMPS: per-phase latency sums (diagnostic, normally null)
+};
+
+// Pass 1: exact 5-NN of every query (no fp64 geometry here, so the kernel stays small and at high occupancy).
+__device__ __forceinline__ void knn_group(const LMState* __restrict__ st, const CorrArgs& A, int gid, int ngroups,
+                                          int lane, bool gate, int rank, int world, int* __restrict__ s_pre,
+                                          int* __restrict__ s_start) {
+  const int n = min(*A.d_n, A.n_ub);
   const int lo = (int)(((long long)n * rank) / world), hi = (int)(((long long)n * (rank + 1)) / world);
-  const bool gate = *d_me > 10 && *d_ms > 50;   // map-size gate (odomEstimationClass.cpp:77)
-  const int ngroups = (gridDim.x * blockDim.x) / kGroup;
+  const GridParams p = *A.gp;
+  const double inv = 1.0 / p.c;
+  unsigned long long dsum[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long ts = 0;
   // grid-stride over the queries the device holds (the host only knows an upper bound)
   for (int i0 = 0; i0 < n; i0 += ngroups) {
-  const int i = i0 + (blockIdx.x * blockDim.x + threadIdx.x) / kGroup;   // query
-  bool ok = false;
-  if (i < n) {
+    const int i = i0 + gid;   // query
+    if (i >= n) break;
+    bool ok = false;
     if (i >= lo && i < hi && gate) {
-      const float4 pq = *reinterpret_cast<const float4*>(&q[i].x);
+      if (A.dbg) ts = __builtin_amdgcn_s_memrealtime();
+      const float4 pq = *reinterpret_cast<const float4*>(&A.q[i].x);
       float wx, wy, wz;
       associate_to_map(st->x, pq.x, pq.y, pq.z, wx, wy, wz);   // pointAssociateToMap (:126-135)
-      const GridParams p = *gp;
-      const double inv = 1.0 / p.c;
       // |m - q| < 1 on every axis  =>  cell in [floor((q-o-1)/c), floor((q-o+1)/c)]  (c is a power of two)
       const int x0 = max(0, (int)floor(((double)wx - p.ox - 1.0) * inv));
       const int x1 = min(p.nx - 1, (int)floor(((double)wx - p.ox + 1.0) * inv));
@@ -503,100 +536,193 @@ __global__ __launch_bounds__(kTB) void corr_kernel(LMState* __restrict__ st, con
         if (c < ncell) {
           const int cx = x0 + c % nxr, cy = y0 + (c / nxr) % nyr, cz = z0 + c / (nxr * nyr);
           const uint32_t key = (uint32_t)cx + (uint32_t)p.nx * ((uint32_t)cy + (uint32_t)p.ny * (uint32_t)cz);
-          se[h] = grid_lookup(tkey, tval, key, p.shift, p.mask);
+          se[h] = grid_lookup(A.tab, key, p.shift, p.mask);
         }
       }
+      if (A.dbg) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+        dsum[0] += t - ts;
+        ts = t;
+      }
+      // exclusive prefix of the candidate counts over the cells, in cell order, into this group's LDS slot
+      const int p0 = group_incl_scan(se[0].y, lane);
+      const int tot0 = __shfl(p0, kGroup - 1, kGroup);
+      const int p1 = group_incl_scan(se[1].y, lane);
+      const int tot = tot0 + __shfl(p1, kGroup - 1, kGroup);
+      s_pre[lane] = p0 - se[0].y;
+      s_start[lane] = se[0].x;
+      if (lane + kGroup < 27) {
+        s_pre[lane + kGroup] = tot0 + p1 - se[1].y;
+        s_start[lane + kGroup] = se[1].x;
+      }
+      if (lane == 0) s_pre[27] = tot;
+      wave_lds_order();
       Top5 t;
 #pragma unroll
       for (int k = 0; k < 5; ++k) t.k[k] = ~0ull;
       int cnt = 0;
-      for (int c = 0; c < ncell; ++c) {
-        const int sx = __shfl(c < kGroup ? se[0].x : se[1].x, c & (kGroup - 1), kGroup);
-        const int sy = __shfl(c < kGroup ? se[0].y : se[1].y, c & (kGroup - 1), kGroup);
-        for (int j = sx + lane; j < sx + sy; j += kGroup) {
-          const float4 m = gpts[j];
+      int c = 0, c_lo = 0, c_hi = s_pre[1], c_start = s_start[0];   // cursor: cell c spans [c_lo, c_hi)
+      for (int tb = 0; tb < tot; tb += kGroup * kUnroll) {
+        float4 m[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+          const int tt = tb + u * kGroup + lane;
+          if (tt < tot) {
+            while (tt >= c_hi) {
+              ++c;
+              c_lo = c_hi;
+              c_hi = s_pre[c + 1];
+              c_start = s_start[c];
+            }
+            m[u] = A.gpts[c_start + (tt - c_lo)];
+          } else {
+            m[u] = make_float4(1e30f, 1e30f, 1e30f, 0.0f);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
           float dd = 0.0f;   // flann::L2_Simple<float>: ((0 + dx*dx) + dy*dy) + dz*dz
-          float df = wx - m.x;
+          float df = wx - m[u].x;
           dd += df * df;
-          df = wy - m.y;
+          df = wy - m[u].y;
           dd += df * df;
-          df = wz - m.z;
+          df = wz - m[u].z;
           dd += df * df;
           if (dd < 1.0f) {
             ++cnt;
-            top5_insert(t, ((unsigned long long)__float_as_uint(dd) << 32) | (unsigned)__float_as_int(m.w));
+            top5_insert(t, ((unsigned long long)__float_as_uint(dd) << 32) | (unsigned)__float_as_int(m[u].w));
           }
         }
       }
+      if (A.dbg) {
+        const unsigned long long tn = __builtin_amdgcn_s_memrealtime();
+        dsum[1] += tn - ts;
+        ts = tn;
+        dsum[5] += (unsigned long long)tot;
+      }
 #pragma unroll
-      for (int m = kGroup / 2; m > 0; m >>= 1) {
+      for (int mm = kGroup / 2; mm > 0; mm >>= 1) {
         Top5 o;
 #pragma unroll
-        for (int k = 0; k < 5; ++k) o.k[k] = shfl_xor_u64(t.k[k], m);
+        for (int k = 0; k < 5; ++k) o.k[k] = shfl_xor_u64(t.k[k], mm);
         top5_merge(t, o);
-        cnt += __shfl_xor(cnt, m, kGroup);
+        cnt += __shfl_xor(cnt, mm, kGroup);
       }
-      if (lane == 0 && cnt >= 5) {   // sqd[4] < 1 (:154, :210)
-        double P[5][3];
+      wave_lds_order();   // this group's LDS slot is rewritten by its next query
+      ok = cnt >= 5;      // sqd[4] < 1 (:154, :210)
+      if (ok && lane < 5) {
+        unsigned long long kk = t.k[0];
 #pragma unroll
-        for (int j = 0; j < 5; ++j) {
-          const float4 mp = *reinterpret_cast<const float4*>(&map[(int)(t.k[j] & 0xFFFFFFFFull)].x);
-          P[j][0] = mp.x; P[j][1] = mp.y; P[j][2] = mp.z;
-        }
-        const double cpx = pq.x, cpy = pq.y, cpz = pq.z;
-        if (EDGE) {
-          // addEdgeCostFactor geometry (odomEstimationClass.cpp:156-189)
-          double c[3] = {0.0, 0.0, 0.0};
-#pragma unroll
-          for (int j = 0; j < 5; ++j) {
-            c[0] = c[0] + P[j][0]; c[1] = c[1] + P[j][1]; c[2] = c[2] + P[j][2];
-          }
-          c[0] = c[0] / 5.0; c[1] = c[1] / 5.0; c[2] = c[2] / 5.0;
-          double cov[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
-#pragma unroll
-          for (int j = 0; j < 5; ++j) {
-            const double z[3] = {P[j][0] - c[0], P[j][1] - c[1], P[j][2] - c[2]};
-#pragma unroll
-            for (int a = 0; a < 3; ++a)
-#pragma unroll
-              for (int b = 0; b < 3; ++b) cov[a][b] = cov[a][b] + z[a] * z[b];
-          }
-          double ev[3], u[3];
-          eig_sym3(cov, ev, u);
-          if (ev[2] > 3 * ev[1]) {
-            ok = true;
-            rec[0 * cap + i] = cpx; rec[1 * cap + i] = cpy; rec[2 * cap + i] = cpz;
-            rec[3 * cap + i] = 0.1 * u[0] + c[0]; rec[4 * cap + i] = 0.1 * u[1] + c[1]; rec[5 * cap + i] = 0.1 * u[2] + c[2];
-            rec[6 * cap + i] = -0.1 * u[0] + c[0]; rec[7 * cap + i] = -0.1 * u[1] + c[1]; rec[8 * cap + i] = -0.1 * u[2] + c[2];
-          }
-        } else {
-          // addSurfCostFactor geometry (odomEstimationClass.cpp:208-243)
-          double nv[3];
-          plane_solve(P, nv);
-          const double z = nv[0] * nv[0] + nv[1] * nv[1] + nv[2] * nv[2];
-          const double d = 1 / sqrt(z);
-          if (z > 0.0) {
-            const double sz = sqrt(z);
-            nv[0] = nv[0] / sz; nv[1] = nv[1] / sz; nv[2] = nv[2] / sz;
-          }
-          bool planeValid = true;
-#pragma unroll
-          for (int j = 0; j < 5; ++j)
-            if (fabs(nv[0] * P[j][0] + nv[1] * P[j][1] + nv[2] * P[j][2] + d) > 0.2) planeValid = false;
-          if (planeValid) {
-            ok = true;
-            rec[0 * cap + i] = cpx; rec[1 * cap + i] = cpy; rec[2 * cap + i] = cpz;
-            rec[3 * cap + i] = nv[0]; rec[4 * cap + i] = nv[1]; rec[5 * cap + i] = nv[2];
-            rec[6 * cap + i] = d;
-          }
-        }
+        for (int k = 1; k < 5; ++k)
+          if (lane == k) kk = t.k[k];
+        A.nn[lane * A.cap + i] = (int)(kk & 0xFFFFFFFFull);
+      }
+      if (A.dbg) {
+        const unsigned long long tn = __builtin_amdgcn_s_memrealtime();
+        dsum[2] += tn - ts;
+        dsum[4] += 1;
       }
     }
-    if (lane == 0) valid[i] = ok ? 1 : 0;
+    if (lane == 0) A.valid[i] = ok ? 1 : 0;
+  }
+  if (A.dbg && lane == 0 && dsum[4])
+#pragma unroll
+    for (int k = 0; k < 6; ++k) atomicAdd(&A.dbg[k], dsum[k]);
+}
+
+// Edge and surf kNN in one launch: blocks [0, nbE) run edge groups, the others surf groups.
+__global__ __launch_bounds__(kTB) void knn_kernel(const LMState* __restrict__ st, CorrArgs E, CorrArgs S, int nbE,
+                                                  const int* __restrict__ d_me, const int* __restrict__ d_ms,
+                                                  int rank, int world) {
+  __shared__ int s_pre[kGroupsPerBlock][28];
+  __shared__ int s_start[kGroupsPerBlock][27];
+  const int lane = threadIdx.x & (kGroup - 1);
+  const int g = threadIdx.x / kGroup;
+  const bool gate = *d_me > 10 && *d_ms > 50;   // map-size gate (odomEstimationClass.cpp:77)
+  if ((int)blockIdx.x < nbE)
+    knn_group(st, E, (blockIdx.x * blockDim.x + threadIdx.x) / kGroup, nbE * kGroupsPerBlock, lane, gate, rank,
+              world, s_pre[g], s_start[g]);
+  else
+    knn_group(st, S, ((blockIdx.x - nbE) * blockDim.x + threadIdx.x) / kGroup, (gridDim.x - nbE) * kGroupsPerBlock,
+              lane, gate, rank, world, s_pre[g], s_start[g]);
+}
+
+// Pass 2: fp64 line / plane geometry, one query per lane (all 64 lanes busy).
+template <bool EDGE>
+__device__ __forceinline__ void geom_query(LMState* __restrict__ st, const CorrArgs& A, int i) {
+  const int n = min(*A.d_n, A.n_ub);
+  bool ok = false;
+  if (i < n && A.valid[i]) {
+    double P[5][3];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      const float4 mp = *reinterpret_cast<const float4*>(&A.map[A.nn[j * A.cap + i]].x);
+      P[j][0] = mp.x; P[j][1] = mp.y; P[j][2] = mp.z;
+    }
+    const float4 pq = *reinterpret_cast<const float4*>(&A.q[i].x);
+    const double cpx = pq.x, cpy = pq.y, cpz = pq.z;
+    double* rec = A.rec;
+    const int cap = A.cap;
+    if (EDGE) {
+      // addEdgeCostFactor geometry (odomEstimationClass.cpp:156-189)
+      double cc[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        cc[0] = cc[0] + P[j][0]; cc[1] = cc[1] + P[j][1]; cc[2] = cc[2] + P[j][2];
+      }
+      cc[0] = cc[0] / 5.0; cc[1] = cc[1] / 5.0; cc[2] = cc[2] / 5.0;
+      double cov[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        const double z[3] = {P[j][0] - cc[0], P[j][1] - cc[1], P[j][2] - cc[2]};
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+#pragma unroll
+          for (int b = 0; b < 3; ++b) cov[a][b] = cov[a][b] + z[a] * z[b];
+      }
+      double ev[3], u[3];
+      eig_sym3(cov, ev, u);
+      if (ev[2] > 3 * ev[1]) {
+        ok = true;
+        rec[0 * cap + i] = cpx; rec[1 * cap + i] = cpy; rec[2 * cap + i] = cpz;
+        rec[3 * cap + i] = 0.1 * u[0] + cc[0]; rec[4 * cap + i] = 0.1 * u[1] + cc[1];
+        rec[5 * cap + i] = 0.1 * u[2] + cc[2];
+        rec[6 * cap + i] = -0.1 * u[0] + cc[0]; rec[7 * cap + i] = -0.1 * u[1] + cc[1];
+        rec[8 * cap + i] = -0.1 * u[2] + cc[2];
+      }
+    } else {
+      // addSurfCostFactor geometry (odomEstimationClass.cpp:208-243)
+      double nv[3];
+      plane_solve(P, nv);
+      const double z = nv[0] * nv[0] + nv[1] * nv[1] + nv[2] * nv[2];
+      const double d = 1 / sqrt(z);
+      if (z > 0.0) {
+        const double sz = sqrt(z);
+        nv[0] = nv[0] / sz; nv[1] = nv[1] / sz; nv[2] = nv[2] / sz;
+      }
+      bool planeValid = true;
+#pragma unroll
+      for (int j = 0; j < 5; ++j)
+        if (fabs(nv[0] * P[j][0] + nv[1] * P[j][1] + nv[2] * P[j][2] + d) > 0.2) planeValid = false;
+      if (planeValid) {
+        ok = true;
+        rec[0 * cap + i] = cpx; rec[1 * cap + i] = cpy; rec[2 * cap + i] = cpz;
+        rec[3 * cap + i] = nv[0]; rec[4 * cap + i] = nv[1]; rec[5 * cap + i] = nv[2];
+        rec[6 * cap + i] = d;
+      }
+    }
+    A.valid[i] = ok ? 1 : 0;
   }
   const unsigned long long b = __ballot(ok);
   if ((threadIdx.x & 63) == 0 && b) atomicAdd(EDGE ? &st->corr_edge : &st->corr_surf, __popcll(b));
-  }
+}
+
+__global__ __launch_bounds__(kTB) void geom_kernel(LMState* __restrict__ st, CorrArgs E, CorrArgs S, int nbE) {
+  if ((int)blockIdx.x < nbE)
+    geom_query<true>(st, E, blockIdx.x * blockDim.x + threadIdx.x);
+  else
+    geom_query<false>(st, S, (blockIdx.x - nbE) * blockDim.x + threadIdx.x);
 }
 
 // Algorithmic traffic of one correspondence launch (SURVEY.md §8 d): every occupied 1-m query cell streams its
@@ -604,8 +730,8 @@ __global__ __launch_bounds__(kTB) void corr_kernel(LMState* __restrict__ st, con
 // (1 B) and, if accepted, its record.  Runs untimed, after the kernel it describes, only when profiling.
 __global__ __launch_bounds__(kTB) void knn_traffic(const LMState* __restrict__ st, const PointRec* __restrict__ q,
                                                    const int* __restrict__ d_n, int n_ub,
-                                                   const GridParams* __restrict__ gp, const uint32_t* __restrict__ tkey,
-                                                   const int2* __restrict__ tval, const uint8_t* __restrict__ valid,
+                                                   const GridParams* __restrict__ gp, const int4* __restrict__ tab,
+                                                   const uint8_t* __restrict__ valid,
                                                    int rec_bytes, int rank, int world, uint32_t* __restrict__ set,
                                                    unsigned set_mask, int set_shift,
                                                    unsigned long long* __restrict__ out) {
@@ -639,7 +765,7 @@ __global__ __launch_bounds__(kTB) void knn_traffic(const LMState* __restrict__ s
         for (int x = cx - 1; x <= cx + 1; ++x) {
           if (x < 0 || y < 0 || z < 0 || x >= p.nx || y >= p.ny || z >= p.nz) continue;
           const uint32_t k = (uint32_t)x + (uint32_t)p.nx * ((uint32_t)y + (uint32_t)p.ny * (uint32_t)z);
-          cand += (unsigned long long)grid_lookup(tkey, tval, k, p.shift, p.mask).y;
+          cand += (unsigned long long)grid_lookup(tab, k, p.shift, p.mask).y;
         }
     bytes += 16ull * cand;
   }
@@ -728,16 +854,21 @@ __device__ __forceinline__ double wave_sum(double v) {
 // correspondence slots [0, *d_ne) and [0, *d_ns).  Evaluated at x (phase 0, iteration zero) or at the candidate.
 __device__ void eval_block(const LMState* __restrict__ st, const double* __restrict__ erec,
                            const uint8_t* __restrict__ evalid, int ecap, int ne, const double* __restrict__ srec,
-                           const uint8_t* __restrict__ svalid, int scap, int ns, int huber, double* __restrict__ partials) {
-  double x[7];
-  const double* px = st->phase == 0 ? st->x : st->cand;
+                           const uint8_t* __restrict__ svalid, int scap, int ns, int huber, double* __restrict__ partials,
+                           int blk, int nblk) {
+  // x and cand are adjacent in LMState: load both with the phase in one round trip, then select
+  double xa[7], xc[7];
 #pragma unroll
-  for (int k = 0; k < 7; ++k) x[k] = px[k];
+  for (int k = 0; k < 7; ++k) { xa[k] = st->x[k]; xc[k] = st->cand[k]; }
+  const bool at_x = st->phase == 0;
+  double x[7];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) x[k] = at_x ? xa[k] : xc[k];
   double acc[LM_NSUM];
 #pragma unroll
   for (int k = 0; k < LM_NSUM; ++k) acc[k] = 0.0;
   const int total = ne + ns;
-  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+  for (int idx = blk * blockDim.x + threadIdx.x; idx < total; idx += nblk * blockDim.x) {
     double J[6], r;
     if (idx < ne) {
       if (!evalid[idx]) continue;
@@ -797,7 +928,7 @@ __device__ void eval_block(const LMState* __restrict__ st, const double* __restr
   if (threadIdx.x < LM_NSUM) {
     double v = 0.0;
     for (int p = 0; p < 8; ++p) v += strip[threadIdx.x][p];
-    partials[threadIdx.x * gridDim.x + blockIdx.x] = v;
+    partials[threadIdx.x * nblk + blk] = v;
   }
 }
 
@@ -808,7 +939,8 @@ __global__ __launch_bounds__(kTB) void lm_eval(const LMState* __restrict__ st, c
                                                const int* __restrict__ d_ns, int ns_ub, int huber,
                                                double* __restrict__ partials) {
   if (st->done) return;
-  eval_block(st, erec, evalid, ecap, min(*d_ne, ne_ub), srec, svalid, scap, min(*d_ns, ns_ub), huber, partials);
+  eval_block(st, erec, evalid, ecap, min(*d_ne, ne_ub), srec, svalid, scap, min(*d_ns, ns_ub), huber, partials,
+             blockIdx.x, gridDim.x);
 }
 
 __device__ void reduce_partials_block(const double* __restrict__ partials, int nblk, double* sums /* shared */) {
@@ -832,22 +964,33 @@ __device__ void reduce_partials_block(const double* __restrict__ partials, int n
 }
 
 // ===================================================================================== LM control (Ceres 1.13)
-// PoseSE3Parameterization::Plus + getTransformFromSe3 (src/lidarOptimization.cpp:77-140)
-__device__ void se3_plus(const double* x, const double* d, double* out) {
+// The control step is serial fp64 code, so its cost is its dependent instruction count (every fp64 VALU op is at
+// least 4 cycles for a wave).  It runs on one wave whose 64 lanes all hold the same LM state in registers (the
+// uniform part costs the same on 64 lanes as on one); the two SE(3) exponentials of a step — the candidate
+// x [+] delta and the gradient projection x [+] -g of the gradient-norm test — run side by side in lanes 0 and 1 of
+// the same instruction stream; the 6x6 Cholesky divides by each pivot once (reciprocals).  Loops are fully unrolled
+// with constant indices so nothing leaves registers.
+
+// PoseSE3Parameterization::Plus + getTransformFromSe3 (src/lidarOptimization.cpp:77-140).  theta^3 is formed by
+// multiplication where the reference calls pow(theta, 3) (<= 1 ulp apart).
+__device__ __forceinline__ void se3_plus(const double (&x)[7], const double (&d)[6], double (&out)[7]) {
   const double wx = d[0], wy = d[1], wz = d[2];
   const double theta = sqrt(wx * wx + wy * wy + wz * wz);
   const double half = 0.5 * theta;
-  const double real_factor = cos(half);
+  double sh, ch;
+  sincos(half, &sh, &ch);
+  const double real_factor = ch;
   double imag;
-  if (theta < 1e-10) {
+  const bool small = theta < 1e-10;
+  if (small) {
     const double t2 = theta * theta, t4 = t2 * t2;
     imag = 0.5 - 0.0208333 * t2 + 0.000260417 * t4;
   } else {
-    imag = sin(half) / theta;
+    imag = sh / theta;
   }
   const double dq[4] = {imag * wx, imag * wy, imag * wz, real_factor};   // x, y, z, w
   double Jm[3][3];
-  if (theta < 1e-10) {
+  if (small) {
     const double tx = 2 * dq[0], ty = 2 * dq[1], tz = 2 * dq[2];
     const double twx = tx * dq[3], twy = ty * dq[3], twz = tz * dq[3];
     const double txx = tx * dq[0], txy = ty * dq[0], txz = tz * dq[0];
@@ -862,8 +1005,10 @@ __device__ void se3_plus(const double* x, const double* d, double* out) {
     for (int i = 0; i < 3; ++i)
 #pragma unroll
       for (int j = 0; j < 3; ++j) O2[i][j] = O[i][0] * O[0][j] + O[i][1] * O[1][j] + O[i][2] * O[2][j];
-    const double c1 = (1 - cos(theta)) / (theta * theta);
-    const double c2 = (theta - sin(theta)) / pow(theta, 3.0);
+    double st, ct;
+    sincos(theta, &st, &ct);
+    const double c1 = (1 - ct) / (theta * theta);
+    const double c2 = (theta - st) / (theta * theta * theta);
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -886,130 +1031,156 @@ __device__ void se3_plus(const double* x, const double* d, double* out) {
   out[6] = tz + dtz;
 }
 
-__device__ double grad_max_norm(const double* x, const double* g) {
-  double ng[6], pr[7];
-#pragma unroll
-  for (int k = 0; k < 6; ++k) ng[k] = -g[k];
-  se3_plus(x, ng, pr);
-  double m = 0.0;
-#pragma unroll
-  for (int i = 0; i < 7; ++i) m = fmax(m, fabs(x[i] - pr[i]));
-  return m;
-}
-
-__device__ __forceinline__ int hidx(int a, int b) {   // upper-triangle row-major index, a <= b
+__host__ __device__ constexpr int hidx(int a, int b) {   // upper-triangle row-major index, a <= b
   return a * 6 - a * (a - 1) / 2 + (b - a);
 }
 
 // LevenbergMarquardtStrategy::ComputeStep in normal-equation form on the Jacobi-scaled system:
 // (Hs + diag(Hs)/radius) y = gs, step = -y; then TrustRegionMinimizer::ComputeTrustRegionStep's model cost change.
-// Runs on one lane; the 6x6 work lives in LDS with rolled loops (compact code: this path is latency-bound and
-// runs with a cold instruction cache every launch).
-__device__ bool compute_step(LMState* s) {
-  __shared__ double Hs[6][6], L[6][6];
-  __shared__ double gs[6], y[6], step[6];
+// (The oracle solves the equivalent [J; sqrt(D/radius)] least-squares problem by Householder QR like Ceres'
+// DENSE_QR; the two agree to ~cond * eps.)  Returns false for an invalid step; delta = scaled step.
+__device__ __forceinline__ bool solve_step(LMState& s, double (&delta)[6]) {
+  double Hs[6][6], gs[6];
+#pragma unroll
   for (int a = 0; a < 6; ++a) {
-    gs[a] = s->scale[a] * s->g[a];
-    for (int b = 0; b < 6; ++b) {
-      const int i = a <= b ? hidx(a, b) : hidx(b, a);
-      Hs[a][b] = s->scale[a] * s->H[i] * s->scale[b];
-    }
+    gs[a] = s.scale[a] * s.g[a];
+#pragma unroll
+    for (int b = 0; b < 6; ++b) Hs[a][b] = s.scale[a] * s.H[a <= b ? hidx(a, b) : hidx(b, a)] * s.scale[b];
   }
-  if (!s->reuse)
-    for (int k = 0; k < 6; ++k) s->diag[k] = fmin(fmax(Hs[k][k], 1e-6), 1e32);
-  s->reuse = 1;
-  // Cholesky of A = Hs + diag / radius
+  if (!s.reuse) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) s.diag[k] = fmin(fmax(Hs[k][k], 1e-6), 1e32);
+  }
+  s.reuse = 1;
+  // Cholesky of A = Hs + diag / radius, with one reciprocal per pivot
+  const double inv_radius = 1.0 / s.radius;
+  double L[6][6], rd[6];
+  bool pd = true;
+#pragma unroll
   for (int j = 0; j < 6; ++j) {
-    double d = Hs[j][j] + s->diag[j] / s->radius;
+    double d = Hs[j][j] + s.diag[j] * inv_radius;
+#pragma unroll
     for (int k = 0; k < j; ++k) d -= L[j][k] * L[j][k];
-    if (!(d > 0.0)) return false;
+    pd = pd && (d > 0.0);
     L[j][j] = sqrt(d);
+    rd[j] = 1.0 / L[j][j];
+#pragma unroll
     for (int i = j + 1; i < 6; ++i) {
       double v = Hs[i][j];
+#pragma unroll
       for (int k = 0; k < j; ++k) v -= L[i][k] * L[j][k];
-      L[i][j] = v / L[j][j];
+      L[i][j] = v * rd[j];
     }
   }
+  if (!pd) return false;
+  double y[6];
+#pragma unroll
   for (int i = 0; i < 6; ++i) {
     double v = gs[i];
+#pragma unroll
     for (int k = 0; k < i; ++k) v -= L[i][k] * y[k];
-    y[i] = v / L[i][i];
+    y[i] = v * rd[i];
   }
+#pragma unroll
   for (int i = 5; i >= 0; --i) {
     double v = y[i];
+#pragma unroll
     for (int k = i + 1; k < 6; ++k) v -= L[k][i] * y[k];
-    y[i] = v / L[i][i];
+    y[i] = v * rd[i];
   }
+  double step[6];
   bool finite = true;
+#pragma unroll
   for (int k = 0; k < 6; ++k) {
     step[k] = -y[k];
     finite = finite && isfinite(step[k]);
   }
   if (!finite) return false;
   double sg = 0.0, sHs = 0.0;
+#pragma unroll
   for (int a = 0; a < 6; ++a) {
     sg += step[a] * gs[a];
     double hv = 0.0;
+#pragma unroll
     for (int b = 0; b < 6; ++b) hv += Hs[a][b] * step[b];
     sHs += step[a] * hv;
   }
   const double mcc = -(sg + 0.5 * sHs);
   if (!(mcc > 0.0)) return false;
-  s->mcc = mcc;
-  double delta[6];
+  s.mcc = mcc;
 #pragma unroll
-  for (int k = 0; k < 6; ++k) delta[k] = step[k] * s->scale[k];
-  se3_plus(s->x, delta, s->cand);
+  for (int k = 0; k < 6; ++k) delta[k] = step[k] * s.scale[k];
   return true;
 }
 
-__device__ void next_step(LMState* s) {
-#pragma unroll
+__device__ __forceinline__ double bcast(double v, int src) { return __shfl(v, src, 64); }
+
+// NextStep with the gradient-norm test folded in: ComputeTrustRegionStep (+ HandleInvalidStep retries) and, when
+// check_gmax, the projected-gradient max norm at x (lane 1) computed alongside the candidate (lane 0).  If the
+// gradient test ends the solve the step is discarded, as in the sequential order (test first, then step).
+__device__ __forceinline__ void next_step_wave(LMState& s, bool check_gmax, int lane) {
   for (;;) {
-    s->iteration++;
-    if (compute_step(s)) {
-      s->invalid = 0;
+    double delta[6];
+    const bool valid = solve_step(s, delta);
+    double d[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) d[k] = lane == 1 ? -s.g[k] : (valid ? delta[k] : 0.0);
+    double out[7];
+    se3_plus(s.x, d, out);
+    if (check_gmax) {
+      double m = 0.0;
+#pragma unroll
+      for (int i = 0; i < 7; ++i) m = fmax(m, fabs(s.x[i] - bcast(out[i], 1)));
+      s.gmax = m;
+      check_gmax = false;
+      if (s.gmax <= 1e-10) { s.done = 1; return; }   // (phase 0: before any step; phase 1: success && gmax)
+    }
+    s.iteration++;
+    if (valid) {
+#pragma unroll
+      for (int i = 0; i < 7; ++i) s.cand[i] = bcast(out[i], 0);
+      s.invalid = 0;
       return;   // candidate pending evaluation
     }
     // HandleInvalidStep -> StepIsInvalid -> StepRejected(0)
-    if (++s->invalid >= 5) { s->done = 1; return; }
-    s->radius /= s->dfac;
-    s->dfac *= 2.0;
-    s->reuse = 1;
-    if (s->iteration >= 4 || s->radius < 1e-32) { s->done = 1; return; }
+    if (++s.invalid >= 5) { s.done = 1; return; }
+    s.radius /= s.dfac;
+    s.dfac *= 2.0;
+    s.reuse = 1;
+    if (s.iteration >= 4 || s.radius < 1e-32) { s.done = 1; return; }
   }
 }
 
-__device__ double norm7(const double* a) {
+__device__ __forceinline__ double norm7(const double (&a)[7]) {
   double v = 0.0;
 #pragma unroll
   for (int i = 0; i < 7; ++i) v += a[i] * a[i];
   return sqrt(v);
 }
 
-__device__ void lm_logic(LMState* s, const double* sums) {
-  if (s->phase == 0) {   // IterationZero
-    s->n_res = (int)sums[28];
-    if (s->n_res == 0) { s->done = 1; return; }   // no residual blocks: parameters untouched
-    s->x_cost = sums[0];
-    if (!isfinite(s->x_cost)) { s->done = 1; return; }
+// One Ceres control step after an evaluation (sums = cost, J^T J, J^T r, count at x in phase 0, else at cand).
+// Called by all 64 lanes of one wave with identical s and sums; every lane ends with the same s.
+__device__ __forceinline__ void lm_logic(LMState& s, const double (&sums)[LM_NSUM], int lane) {
+  if (s.phase == 0) {   // IterationZero
+    s.n_res = (int)sums[28];
+    if (s.n_res == 0) { s.done = 1; return; }   // no residual blocks: parameters untouched
+    s.x_cost = sums[0];
+    if (!isfinite(s.x_cost)) { s.done = 1; return; }
 #pragma unroll
-    for (int k = 0; k < 21; ++k) s->H[k] = sums[1 + k];
+    for (int k = 0; k < 21; ++k) s.H[k] = sums[1 + k];
 #pragma unroll
-    for (int k = 0; k < 6; ++k) s->g[k] = sums[22 + k];
-    s->initial_cost = s->x_cost;
+    for (int k = 0; k < 6; ++k) s.g[k] = sums[22 + k];
+    s.initial_cost = s.x_cost;
 #pragma unroll
-    for (int k = 0; k < 6; ++k) s->scale[k] = 1.0 / (1.0 + sqrt(s->H[hidx(k, k)]));
-    s->x_norm = norm7(s->x);
-    s->gmax = grad_max_norm(s->x, s->g);
-    s->radius = 1e4;
-    s->dfac = 2.0;
-    s->reuse = 0;
-    s->invalid = 0;
-    s->iteration = 0;
-    s->phase = 1;
-    if (s->gmax <= 1e-10) { s->done = 1; return; }
-    next_step(s);
+    for (int k = 0; k < 6; ++k) s.scale[k] = 1.0 / (1.0 + sqrt(s.H[hidx(k, k)]));
+    s.x_norm = norm7(s.x);
+    s.radius = 1e4;
+    s.dfac = 2.0;
+    s.reuse = 0;
+    s.invalid = 0;
+    s.iteration = 0;
+    s.phase = 1;
+    next_step_wave(s, true, lane);
     return;
   }
   double cand_cost = sums[0];
@@ -1017,40 +1188,48 @@ __device__ void lm_logic(LMState* s, const double* sums) {
   // ParameterToleranceReached (candidate not applied)
   double sn = 0.0;
 #pragma unroll
-  for (int i = 0; i < 7; ++i) sn += (s->x[i] - s->cand[i]) * (s->x[i] - s->cand[i]);
+  for (int i = 0; i < 7; ++i) sn += (s.x[i] - s.cand[i]) * (s.x[i] - s.cand[i]);
   sn = sqrt(sn);
-  if (sn <= 1e-8 * (s->x_norm + 1e-8)) { s->done = 1; return; }
+  if (sn <= 1e-8 * (s.x_norm + 1e-8)) { s.done = 1; return; }
   // FunctionToleranceReached
-  if (fabs(s->x_cost - cand_cost) <= 1e-6 * s->x_cost) { s->done = 1; return; }
-  const double rho = (s->x_cost - cand_cost) / s->mcc;
+  if (fabs(s.x_cost - cand_cost) <= 1e-6 * s.x_cost) { s.done = 1; return; }
+  const double rho = (s.x_cost - cand_cost) / s.mcc;
   bool success = false;
   if (rho > 1e-3) {
 #pragma unroll
-    for (int i = 0; i < 7; ++i) s->x[i] = s->cand[i];
-    s->x_norm = norm7(s->x);
-    s->x_cost = cand_cost;
+    for (int i = 0; i < 7; ++i) s.x[i] = s.cand[i];
+    s.x_norm = norm7(s.x);
+    s.x_cost = cand_cost;
 #pragma unroll
-    for (int k = 0; k < 21; ++k) s->H[k] = sums[1 + k];
+    for (int k = 0; k < 21; ++k) s.H[k] = sums[1 + k];
 #pragma unroll
-    for (int k = 0; k < 6; ++k) s->g[k] = sums[22 + k];
-    s->gmax = grad_max_norm(s->x, s->g);
+    for (int k = 0; k < 6; ++k) s.g[k] = sums[22 + k];
     const double t = 2.0 * rho - 1.0;
-    s->radius = fmin(1e16, s->radius / fmax(1.0 / 3.0, 1.0 - t * t * t));
-    s->dfac = 2.0;
-    s->reuse = 0;
-    s->successful++;
+    s.radius = fmin(1e16, s.radius / fmax(1.0 / 3.0, 1.0 - t * t * t));
+    s.dfac = 2.0;
+    s.reuse = 0;
+    s.successful++;
     success = true;
   } else {
-    s->radius /= s->dfac;
-    s->dfac *= 2.0;
-    s->reuse = 1;
+    s.radius /= s.dfac;
+    s.dfac *= 2.0;
+    s.reuse = 1;
   }
-  if (s->iteration >= 4 || s->radius < 1e-32 || (success && s->gmax <= 1e-10)) { s->done = 1; return; }
-  next_step(s);
+  if (s.iteration >= 4 || s.radius < 1e-32) { s.done = 1; return; }
+  next_step_wave(s, success, lane);
 }
 
-// The serial Ceres control step runs on an LDS copy of the LM state (global-memory round trips per field made
-// the single-lane logic latency-bound); all lanes stage it in and out.
+// Wave 0 of the block runs the control step in place on the LM state staged in LDS (sst): all 64 lanes read the
+// same fields (LDS broadcast) and store identical values, so the state never has to fit in registers.
+__device__ __forceinline__ void lm_logic_wave0(LMState& sst, const double* sums_lds) {
+  if (threadIdx.x < 64) {
+    double sm[LM_NSUM];
+#pragma unroll
+    for (int k = 0; k < LM_NSUM; ++k) sm[k] = sums_lds[k];
+    lm_logic(sst, sm, (int)threadIdx.x);
+  }
+}
+
 __device__ __forceinline__ void lm_logic_lds(LMState* __restrict__ st, const double* sums) {
   __shared__ LMState sst;
   constexpr int kWords = (int)(sizeof(LMState) / sizeof(unsigned));
@@ -1059,7 +1238,7 @@ __device__ __forceinline__ void lm_logic_lds(LMState* __restrict__ st, const dou
   unsigned* ldst = reinterpret_cast<unsigned*>(&sst);
   for (int w = threadIdx.x; w < kWords; w += blockDim.x) ldst[w] = gsrc[w];
   __syncthreads();
-  if (threadIdx.x == 0) lm_logic(&sst, sums);
+  lm_logic_wave0(sst, sums);
   __syncthreads();
   unsigned* gdst = reinterpret_cast<unsigned*>(st);
   for (int w = threadIdx.x; w < kWords; w += blockDim.x) gdst[w] = ldst[w];
@@ -1077,10 +1256,11 @@ __global__ __launch_bounds__(kTB) void lm_control(LMState* __restrict__ st, cons
   lm_logic_lds(st, sums);
 }
 
-// One LM iteration in one launch (single-GPU path): every block evaluates its share, the last block to arrive
-// (device-scope counter) reduces the partials in fixed block order and runs the Ceres control step.  Hand-off per
-// MI355X_MICROARCH.md "Valid forms": plain stores -> s_waitcnt vmcnt(0) -> barrier -> lane-0 agent release ->
-// s_waitcnt -> atomic; the last block: agent acquire -> s_waitcnt -> barrier -> plain loads.
+// One LM iteration in one launch (single-GPU path).  Block 0 is the control block; blocks 1..nblk evaluate.
+// Block 0 stages the LM state while the others evaluate, waits for them (bounded spin on a device-scope arrival
+// counter), reduces the partials in fixed block order and runs the control step on its first wave.
+// Hand-off per MI355X_MICROARCH.md "Valid forms": plain stores -> s_waitcnt vmcnt(0) -> barrier -> lane-0 agent
+// release -> s_waitcnt -> atomic; block 0: poll (agent-scope atomic load) -> agent acquire -> barrier -> plain loads.
 __global__ __launch_bounds__(kTB) void lm_step(LMState* __restrict__ st, const double* __restrict__ erec,
                                                const uint8_t* __restrict__ evalid, int ecap, const int* __restrict__ d_ne,
                                                int ne_ub, const double* __restrict__ srec,
@@ -1088,33 +1268,71 @@ __global__ __launch_bounds__(kTB) void lm_step(LMState* __restrict__ st, const d
                                                const int* __restrict__ d_ns, int ns_ub, int huber,
                                                double* __restrict__ partials, unsigned* __restrict__ counter,
                                                unsigned long long* __restrict__ dbg) {
-  if (st->done) return;
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  eval_block(st, erec, evalid, ecap, min(*d_ne, ne_ub), srec, svalid, scap, min(*d_ns, ns_ub), huber, partials);
-  const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
-  __shared__ int s_last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  const int nblk = (int)gridDim.x - 1;
+  if (blockIdx.x > 0) {
+    if (st->done) return;
+    eval_block(st, erec, evalid, ecap, min(*d_ne, ne_ub), srec, svalid, scap, min(*d_ns, ns_ub), huber, partials,
+               blockIdx.x - 1, nblk);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned prev = atomicAdd(counter, 1u);
-    s_last = (prev == gridDim.x - 1);
-    if (s_last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      atomicAdd(counter, 1u);
     }
+    return;
+  }
+  __shared__ LMState sst;
+  __shared__ double sums[LM_NSUM];
+  __shared__ int s_timeout;
+  constexpr int kWords = (int)(sizeof(LMState) / sizeof(unsigned));
+  static_assert(sizeof(LMState) % sizeof(unsigned) == 0, "LMState must be a whole number of dwords");
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  {
+    const unsigned* gsrc = reinterpret_cast<const unsigned*>(st);
+    unsigned* ldst = reinterpret_cast<unsigned*>(&sst);
+    for (int w = threadIdx.x; w < kWords; w += blockDim.x) ldst[w] = gsrc[w];
   }
   __syncthreads();
-  if (!s_last) return;
-  __shared__ double sums[LM_NSUM];
-  const unsigned long long t2 = __builtin_amdgcn_s_memrealtime();
-  reduce_partials_block(partials, gridDim.x, sums);
-  const unsigned long long t3 = __builtin_amdgcn_s_memrealtime();
+  if (sst.done) return;
+  unsigned long long t1 = 0, t2 = 0, t3 = 0;
+  if (threadIdx.x == 0) {
+    t1 = __builtin_amdgcn_s_memrealtime();
+    int timeout = 1;   // bounded wait (~1 s)
+    for (long long it = 0; it < (1ll << 24); ++it) {
+      if (__hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)nblk) {
+        timeout = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    s_timeout = timeout;
+    t2 = __builtin_amdgcn_s_memrealtime();
+  }
+  __syncthreads();
+  if (s_timeout) {   // never expected: give up on this solve instead of hanging the device
+    if (threadIdx.x == 0) {
+      st->done = 1;
+      st->n_res = -1;
+      *counter = 0u;
+    }
+    return;
+  }
+  reduce_partials_block(partials, nblk, sums);
+  t3 = __builtin_amdgcn_s_memrealtime();
   if (threadIdx.x == 0) *counter = 0u;   // ready for the next launch (kernel boundary orders it)
-  lm_logic_lds(st, sums);
-  const unsigned long long t4 = __builtin_amdgcn_s_memrealtime();
-  if (dbg && threadIdx.x == 0) {   // diagnostic stamps (100 MHz): eval, arrive, reduce, logic
+  lm_logic_wave0(sst, sums);
+  __syncthreads();
+  {
+    unsigned* gdst = reinterpret_cast<unsigned*>(st);
+    const unsigned* lsrc = reinterpret_cast<const unsigned*>(&sst);
+    for (int w = threadIdx.x; w < kWords; w += blockDim.x) gdst[w] = lsrc[w];
+  }
+  if (dbg && threadIdx.x == 0) {   // diagnostic stamps (100 MHz): stage, wait, reduce, control step + store
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    const unsigned long long t4 = __builtin_amdgcn_s_memrealtime();
     atomicAdd(&dbg[0], t1 - t0);
     atomicAdd(&dbg[1], t2 - t1);
     atomicAdd(&dbg[2], t3 - t2);
@@ -1140,20 +1358,19 @@ void grid_build_launch(Grid& g, GridScratch& sc, const PointRec* map, const int*
   g.pts.reserve(ub);
   int tsize = 1024, shift = 32 - 10;
   while (tsize < 2 * ub) { tsize <<= 1; --shift; }
-  g.tkey.reserve(tsize);
-  g.tval.reserve(tsize);
+  g.tab.reserve(tsize);
   g.table_size = tsize;
   g.shift = shift;
   minmax_launch(map, d_m, ub, sc.mm.p, st);
   hipLaunchKernelGGL(grid_setup, dim3(1), dim3(64), 0, st, sc.mm.p, d_m, shift, (unsigned)(tsize - 1), g.params.p);
   FLOAM_LAUNCH_CHECK();
   const unsigned gb = div_up(ub, kTB);
-  hipLaunchKernelGGL(grid_keys, dim3(gb), dim3(kTB), 0, st, map, d_m, ub, g.params.p, sc.s.k0.p, sc.s.v0.p, g.tkey.p,
+  hipLaunchKernelGGL(grid_keys, dim3(gb), dim3(kTB), 0, st, map, d_m, ub, g.params.p, sc.s.k0.p, sc.s.v0.p, g.tab.p,
                      tsize);
   FLOAM_LAUNCH_CHECK();
   sort_pairs_u32(sc.s.temp.p, sc.s.temp_bytes, sc.s.k0.p, sc.s.k1.p, sc.s.v0.p, sc.s.v1.p, ub, 32, st);
   hipLaunchKernelGGL(grid_fill, dim3(gb), dim3(kTB), 0, st, map, d_m, sc.s.k1.p, sc.s.v1.p, g.params.p, g.pts.p,
-                     g.tkey.p, g.tval.p);
+                     g.tab.p);
   FLOAM_LAUNCH_CHECK();
 }
 
@@ -1191,18 +1408,22 @@ void gather_status_launch(const LMState* lm, const int* dcnt, const int* mapE_co
   FLOAM_LAUNCH_CHECK();
 }
 
-void corr_launch(bool edge, LMState* d_st, const QuerySet& q, const Grid& g, const PointRec* map, const int* d_me,
-                 const int* d_ms, CorrSet& c, int rank, int world, hipStream_t st) {
-  c.reserve(std::max(q.n_ub, 1), edge ? EDGE_FIELDS : SURF_FIELDS);
-  if (q.n_ub <= 0) return;
-  const unsigned blocks = std::min(div_up((size_t)q.n_ub * kGroup, kTB), 2048u);
-  if (edge) {
-    hipLaunchKernelGGL(corr_kernel<true>, dim3(blocks), dim3(kTB), 0, st, d_st, q.pts, q.d_n, q.n_ub, g.params.p,
-                       g.pts.p, g.tkey.p, g.tval.p, map, d_me, d_ms, c.rec.p, c.valid.p, c.cap, rank, world);
-  } else {
-    hipLaunchKernelGGL(corr_kernel<false>, dim3(blocks), dim3(kTB), 0, st, d_st, q.pts, q.d_n, q.n_ub, g.params.p,
-                       g.pts.p, g.tkey.p, g.tval.p, map, d_me, d_ms, c.rec.p, c.valid.p, c.cap, rank, world);
-  }
+void corr_launch(LMState* d_st, const QuerySet& qe, const Grid& ge, const PointRec* mapE, CorrSet& ce,
+                 const QuerySet& qs, const Grid& gs, const PointRec* mapS, CorrSet& cs, const int* d_me,
+                 const int* d_ms, int rank, int world, hipStream_t st, unsigned long long* dbg) {
+  ce.reserve(std::max(qe.n_ub, 1), EDGE_FIELDS);
+  cs.reserve(std::max(qs.n_ub, 1), SURF_FIELDS);
+  if (qe.n_ub <= 0 && qs.n_ub <= 0) return;
+  const CorrArgs E{qe.pts, qe.d_n, qe.n_ub, ge.params.p, ge.pts.p, ge.tab.p, mapE, ce.rec.p, ce.valid.p, ce.nn.p,
+                   ce.cap, dbg};
+  const CorrArgs S{qs.pts, qs.d_n, qs.n_ub, gs.params.p, gs.pts.p, gs.tab.p, mapS, cs.rec.p, cs.valid.p, cs.nn.p,
+                   cs.cap, dbg ? dbg + 8 : nullptr};
+  const unsigned nbE = std::min(div_up((size_t)std::max(qe.n_ub, 1) * kGroup, kTB), 2048u);
+  const unsigned nbS = std::min(div_up((size_t)std::max(qs.n_ub, 1) * kGroup, kTB), 4096u);
+  hipLaunchKernelGGL(knn_kernel, dim3(nbE + nbS), dim3(kTB), 0, st, d_st, E, S, (int)nbE, d_me, d_ms, rank, world);
+  FLOAM_LAUNCH_CHECK();
+  const unsigned gE = div_up(std::max(qe.n_ub, 1), kTB), gS = div_up(std::max(qs.n_ub, 1), kTB);
+  hipLaunchKernelGGL(geom_kernel, dim3(gE + gS), dim3(kTB), 0, st, d_st, E, S, (int)gE);
   FLOAM_LAUNCH_CHECK();
 }
 
@@ -1214,7 +1435,7 @@ void knn_traffic_launch(const LMState* d_st, const QuerySet& q, const Grid& g, c
   set.reserve(size);
   FLOAM_HIP(hipMemsetAsync(set.p, 0xFF, sizeof(uint32_t) * size, st));
   hipLaunchKernelGGL(knn_traffic, dim3(div_up(q.n_ub, kTB)), dim3(kTB), 0, st, d_st, q.pts, q.d_n, q.n_ub,
-                     g.params.p, g.tkey.p, g.tval.p, c.valid.p, rec_bytes, rank, world, set.p, (unsigned)(size - 1),
+                     g.params.p, g.tab.p, c.valid.p, rec_bytes, rank, world, set.p, (unsigned)(size - 1),
                      shift, d_bytes);
   FLOAM_LAUNCH_CHECK();
 }
@@ -1234,7 +1455,7 @@ void lm_step_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub
                     unsigned long long* dbg) {
   const int total = std::max(ne_ub + ns_ub, 1);
   const int nblk = (int)std::min<unsigned>(div_up(total, kTB), kEvalBlocks);
-  hipLaunchKernelGGL(lm_step, dim3(nblk), dim3(kTB), 0, st, d_st, ce.rec.p, ce.valid.p, ce.cap, d_ne, ne_ub,
+  hipLaunchKernelGGL(lm_step, dim3(nblk + 1), dim3(kTB), 0, st, d_st, ce.rec.p, ce.valid.p, ce.cap, d_ne, ne_ub,
                      cs.rec.p, cs.valid.p, cs.cap, d_ns, ns_ub, huber ? 1 : 0, partials, counter, dbg);
   FLOAM_LAUNCH_CHECK();
 }

@@ -21,8 +21,7 @@ struct GridParams {
 struct Grid {
   DevBuf<GridParams> params;
   DevBuf<float4> pts;      // cell-sorted
-  DevBuf<uint32_t> tkey;
-  DevBuf<int2> tval;       // (start, count)
+  DevBuf<int4> tab;        // open addressing: {cell key, start, count, 0}; key 0xFFFFFFFF = empty (one 16-B probe)
   int table_size = 0;
   int shift = 0;
 };
@@ -41,15 +40,16 @@ enum { EDGE_FIELDS = 9, SURF_FIELDS = 7 };
 
 struct CorrSet {
   DevBuf<double> rec;
-  DevBuf<uint8_t> valid;
+  DevBuf<uint8_t> valid;   // after the kNN pass: 5 neighbours within sqd < 1; after geometry: record accepted
+  DevBuf<int> nn;          // the 5 nearest map indices of each query, nn[k * cap + i]
   int cap = 0;
   void reserve(int n, int fields) {
     if (n <= cap) return;
     const int c = n < 1024 ? 1024 : n + n / 4;
-    rec.reserve((size_t)c * fields);
     valid.reserve(c);
     cap = (int)valid.cap;
     rec.reserve((size_t)cap * fields);
+    nn.reserve((size_t)cap * 5);
   }
 };
 
@@ -96,9 +96,11 @@ struct UpdateStatus {
 };
 void gather_status_launch(const LMState* lm, const int* dcnt, const int* mapE_count, const int* mapS_count,
                           const unsigned long long* prof, UpdateStatus* out, hipStream_t st);
-// correspondence search (kNN + line / plane geometry) for one query set at the pose in st->x
-void corr_launch(bool edge, LMState* d_st, const QuerySet& q, const Grid& g, const PointRec* map, const int* d_me,
-                 const int* d_ms, CorrSet& c, int rank, int world, hipStream_t st);
+// correspondence search (kNN + line / plane geometry) for the edge and the surf query sets at the pose in st->x,
+// one launch: blocks [0, nbE) take edge queries against the corner map, the rest surf queries against the surf map
+void corr_launch(LMState* d_st, const QuerySet& qe, const Grid& ge, const PointRec* mapE, CorrSet& ce,
+                 const QuerySet& qs, const Grid& gs, const PointRec* mapS, CorrSet& cs, const int* d_me,
+                 const int* d_ms, int rank, int world, hipStream_t st, unsigned long long* dbg = nullptr);
 // algorithmic bytes of the correspondence launch just issued (profiling only), accumulated into *d_bytes
 void knn_traffic_launch(const LMState* d_st, const QuerySet& q, const Grid& g, const CorrSet& c, int rec_bytes,
                         int rank, int world, DevBuf<uint32_t>& set, unsigned long long* d_bytes, hipStream_t st);
