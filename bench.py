@@ -90,6 +90,8 @@ def main():
     ap.add_argument("--mode", choices=["shard", "replica"], default="shard")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--knn-detail", action="store_true", help="also time the search and geometry launches separately "
+                    "(extra events inside the timed region)")
     ap.add_argument("--json-out", default="")
     args = ap.parse_args()
 
@@ -180,7 +182,8 @@ def main():
         step(lp, odo, k, poses)
     if not args.no_roofline:
         _ffi.check(L.floam_profile_reset(dev))
-        _ffi.check(L.floam_profile_enable(dev, 1))   # FLOAM_PROF_KNN: HIP events around the two kNN kernels only
+        # FLOAM_PROF_KNN: HIP events around the correspondence pass only (+ FLOAM_PROF_KNN_DETAIL: per launch)
+        _ffi.check(L.floam_profile_enable(dev, 1 | (32 if args.knn_detail else 0)))
     barrier_sync()
     t_start = time.perf_counter()
     for k in range(args.warmup, n_scans):
@@ -231,6 +234,10 @@ def main():
                     "kernel": "corr_kernel (edge + surf kNN, line / plane geometry)", "avg_us": round(avg_ms * 1e3, 2),
                     "launches": int(kt[0]), "algorithmic_bytes_per_launch": round(bytes_per),
                     "replay_bitwise_identical": bool(same)}
+            for sub in ("knn_search", "knn_geometry"):
+                ks = timed.get(sub)
+                if ks is not None and ks[0]:
+                    roof[sub + "_avg_us"] = round(ks[1] / ks[0] * 1e3, 2)
 
     cpu = None
     pose_err = None

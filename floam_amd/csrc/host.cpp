@@ -331,9 +331,14 @@ void odom_update(floam_odom* o, const floam_cloud* edge, const floam_cloud* surf
   for (int it = 0; it < o->optimization_count; ++it) {
     lm_init_launch(o->lm.p, it == 0 ? o->parameters : nullptr, st);   // first solve starts at the prediction
     {
-      ProfScope ps(ctx, "knn", FLOAM_PROF_KNN);
-      corr_launch(o->lm.p, qe, o->gE, o->mapE.pts.p, o->ce, qs, o->gS, o->mapS.pts.p, o->cs, o->mapE.count.p,
-                  o->mapS.count.p, o->rank, o->world, st, o->dbg_stamps.p ? o->dbg_stamps.p + 8 : nullptr);
+      ProfScope ps(ctx, "knn", FLOAM_PROF_KNN);   // the correspondence pass: search + geometry
+      {
+        ProfScope ps1(ctx, "knn_search", FLOAM_PROF_KNN_DETAIL);
+        knn_launch(o->lm.p, qe, o->gE, o->mapE.pts.p, o->ce, qs, o->gS, o->mapS.pts.p, o->cs, o->mapE.count.p,
+                   o->mapS.count.p, o->rank, o->world, st, o->dbg_stamps.p ? o->dbg_stamps.p + 8 : nullptr);
+      }
+      ProfScope ps2(ctx, "knn_geometry", FLOAM_PROF_KNN_DETAIL);
+      geom_launch(o->lm.p, qe, o->gE, o->mapE.pts.p, o->ce, qs, o->gS, o->mapS.pts.p, o->cs, st);
     }
     if (ctx.profile & FLOAM_PROF_KNN_BYTES) {   // replay only: algorithmic bytes of the two launches above
       knn_traffic_launch(o->lm.p, qe, o->gE, o->ce, 8 * EDGE_FIELDS, o->rank, o->world, o->traffic_set,
@@ -668,9 +673,9 @@ floam_status floam_odom_destroy(floam_odom* o) {
         for (int set = 0; set < 2; ++set) {
           const unsigned long long* c = h + 8 + 8 * set;
           const double q = c[4] ? (double)c[4] : 1.0;
-          std::fprintf(stderr, "[floam stamps] knn %s: %llu queries, per query: lookup %.2f us, scan %.2f us, merge "
-                       "%.2f us, %.1f candidates\n", set ? "surf" : "edge", c[4],
-                       c[0] / q / 100.0, c[1] / q / 100.0, c[2] / q / 100.0, c[5] / q);
+          std::fprintf(stderr, "[floam stamps] knn %s: %llu queries, per query: 3x3x3 block %.2f us; %llu full-box "
+                       "fallbacks, %.2f us each\n", set ? "surf" : "edge", c[4], c[0] / q / 100.0, c[2],
+                       c[1] / (c[2] ? (double)c[2] : 1.0) / 100.0);
         }
       }
       if (o->comm) ncclCommDestroy(o->comm);

@@ -6,6 +6,7 @@
 // SE3 Plus).  Ceres 1.13 TrustRegionMinimizer + LevenbergMarquardtStrategy semantics are restated in lm_control
 // (see SURVEY.md §8 a-12 and oracle/odom.cpp for the CPU restatement).
 #include <cfloat>
+#include <cstdlib>
 #include <climits>
 
 #include "odom_kernels.hpp"
@@ -17,6 +18,9 @@ namespace {
 constexpr int kTB = 256;
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 constexpr unsigned kEvalBlocks = 128;   // LM evaluation grid (grid-stride over the device-resident slots)
+// Hash-grid cell edge (m).  Half the 1-m search radius: the 3x3x3 block around the query's cell covers every point
+// closer than one cell edge, so the 5-NN search usually ends there (see knn_group).
+constexpr double kBaseCell = 0.5;
 
 // ===================================================================================== hash grid build
 __global__ void grid_setup(const int* __restrict__ mm, const int* __restrict__ d_m, int shift, unsigned mask,
@@ -29,8 +33,9 @@ __global__ void grid_setup(const int* __restrict__ mm, const int* __restrict__ d
   p.n = m;
   if (m <= 0) {
     p.ox = p.oy = p.oz = 0.0;
-    p.c = 1.0;
+    p.c = kBaseCell;
     p.nx = p.ny = p.nz = 1;
+    p.cnx = p.cny = p.cnz = 1;
     *gp = p;
     return;
   }
@@ -39,16 +44,18 @@ __global__ void grid_setup(const int* __restrict__ mm, const int* __restrict__ d
     o[d] = floor((double)ord2f(mm[d]));
     mx[d] = (double)ord2f(mm[3 + d]);
   }
-  double c = 1.0;
+  double c = kBaseCell;
   int n[3];
   for (;;) {
     for (int d = 0; d < 3; ++d) n[d] = (int)floor((mx[d] - o[d]) / c) + 1;
-    if ((double)n[0] * (double)n[1] * (double)n[2] < 2147483000.0) break;
+    const double coarse = (double)((n[0] + 1) / 2) * (double)((n[1] + 1) / 2) * (double)((n[2] + 1) / 2);
+    if (coarse < 536870000.0) break;   // (coarse key << 3 | sub-cell) fits 32 bits, fine keys < 2^31
     c *= 2.0;
   }
   p.ox = o[0]; p.oy = o[1]; p.oz = o[2];
   p.c = c;
   p.nx = n[0]; p.ny = n[1]; p.nz = n[2];
+  p.cnx = (n[0] + 1) / 2; p.cny = (n[1] + 1) / 2; p.cnz = (n[2] + 1) / 2;
   *gp = p;
 }
 
@@ -57,20 +64,32 @@ __device__ __forceinline__ int cell_of(double v, double o, double inv_c, int n) 
   return c < 0 ? 0 : (c >= n ? n - 1 : c);
 }
 
+__device__ __forceinline__ uint32_t fine_key(const GridParams& p, int fx, int fy, int fz) {
+  return (uint32_t)fx + (uint32_t)p.nx * ((uint32_t)fy + (uint32_t)p.ny * (uint32_t)fz);
+}
+__device__ __forceinline__ uint32_t coarse_key(const GridParams& p, int cx, int cy, int cz) {
+  return (uint32_t)cx + (uint32_t)p.cnx * ((uint32_t)cy + (uint32_t)p.cny * (uint32_t)cz);
+}
+
+// sort key = coarse cell key << 3 | fine sub-cell (x bit 0, y bit 1, z bit 2)
 __global__ __launch_bounds__(kTB) void grid_keys(const PointRec* __restrict__ map, const int* __restrict__ d_m, int m_ub,
                                                  const GridParams* __restrict__ gp, uint32_t* __restrict__ keys,
-                                                 int* __restrict__ vals, int4* __restrict__ tab, int tsize) {
+                                                 int* __restrict__ vals, int4* __restrict__ tab,
+                                                 int4* __restrict__ ctab, int tsize) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  // clear the hash table here (grid_fill inserts only after the sort), saving a memset node
-  for (int t = i; t < tsize; t += gridDim.x * blockDim.x) tab[t] = make_int4((int)kEmpty, 0, 0, 0);
+  // clear the hash tables here (grid_fill inserts only after the sort), saving memset nodes
+  for (int t = i; t < tsize; t += gridDim.x * blockDim.x) {
+    tab[t] = make_int4((int)kEmpty, 0, 0, 0);
+    ctab[t] = make_int4((int)kEmpty, 0, 0, 0);
+  }
   if (i >= m_ub) return;
   uint32_t key = kEmpty;
   if (i < *d_m) {
     const GridParams p = *gp;
     const double inv = 1.0 / p.c;
     const float4 q = *reinterpret_cast<const float4*>(&map[i].x);
-    const int cx = cell_of(q.x, p.ox, inv, p.nx), cy = cell_of(q.y, p.oy, inv, p.ny), cz = cell_of(q.z, p.oz, inv, p.nz);
-    key = (uint32_t)cx + (uint32_t)p.nx * ((uint32_t)cy + (uint32_t)p.ny * (uint32_t)cz);
+    const int fx = cell_of(q.x, p.ox, inv, p.nx), fy = cell_of(q.y, p.oy, inv, p.ny), fz = cell_of(q.z, p.oz, inv, p.nz);
+    key = (coarse_key(p, fx >> 1, fy >> 1, fz >> 1) << 3) | (uint32_t)((fx & 1) | ((fy & 1) << 1) | ((fz & 1) << 2));
   }
   keys[i] = key;
   vals[i] = i;
@@ -78,10 +97,33 @@ __global__ __launch_bounds__(kTB) void grid_keys(const PointRec* __restrict__ ma
 
 __device__ __forceinline__ uint32_t hash_slot(uint32_t key, int shift) { return (key * 0x9E3779B1u) >> shift; }
 
+__device__ __forceinline__ int table_insert(int4* __restrict__ tab, uint32_t key, int start, int shift, unsigned mask) {
+  uint32_t h = hash_slot(key, shift);
+  for (;;) {
+    const uint32_t prev = atomicCAS(reinterpret_cast<uint32_t*>(&tab[h].x), kEmpty, key);
+    if (prev == kEmpty) {
+      tab[h].y = start;
+      return (int)h;
+    }
+    h = (h + 1) & mask;
+  }
+}
+
+__device__ __forceinline__ int table_find(const int4* __restrict__ tab, uint32_t key, int shift, unsigned mask) {
+  uint32_t h = hash_slot(key, shift);
+  for (;;) {
+    const uint32_t k = (uint32_t)tab[h].x;
+    if (k == key) return (int)h;
+    if (k == kEmpty) return -1;
+    h = (h + 1) & mask;
+  }
+}
+
+// cell-sorted copy of the map + the run heads of every fine and coarse cell inserted with their start
 __global__ __launch_bounds__(kTB) void grid_fill(const PointRec* __restrict__ map, const int* __restrict__ d_m,
                                                  const uint32_t* __restrict__ keys, const int* __restrict__ vals,
                                                  const GridParams* __restrict__ gp, float4* __restrict__ pts,
-                                                 int4* __restrict__ tab) {
+                                                 int4* __restrict__ tab, int4* __restrict__ ctab) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   const int m = *d_m;
   if (i >= m) return;
@@ -89,20 +131,38 @@ __global__ __launch_bounds__(kTB) void grid_fill(const PointRec* __restrict__ ma
   const float4 q = *reinterpret_cast<const float4*>(&map[j].x);
   pts[i] = make_float4(q.x, q.y, q.z, __int_as_float(j));
   const uint32_t k = keys[i];
-  if (i == 0 || keys[i - 1] != k) {
-    int e = i + 1;
-    while (e < m && keys[e] == k) ++e;
+  const uint32_t kp = i > 0 ? keys[i - 1] : kEmpty;
+  if (i == 0 || kp != k) {
     const GridParams p = *gp;
-    uint32_t h = hash_slot(k, p.shift);
-    for (;;) {
-      const uint32_t prev = atomicCAS(reinterpret_cast<uint32_t*>(&tab[h].x), kEmpty, k);
-      if (prev == kEmpty) {
-        tab[h].y = i;
-        tab[h].z = e - i;
-        break;
-      }
-      h = (h + 1) & p.mask;
-    }
+    const uint32_t ck = k >> 3, sub = k & 7u;
+    const int cx = (int)(ck % (uint32_t)p.cnx), cy = (int)((ck / (uint32_t)p.cnx) % (uint32_t)p.cny),
+              cz = (int)(ck / ((uint32_t)p.cnx * (uint32_t)p.cny));
+    table_insert(tab, fine_key(p, 2 * cx + (int)(sub & 1u), 2 * cy + (int)((sub >> 1) & 1u), 2 * cz + (int)(sub >> 2)),
+                 i, p.shift, p.mask);
+    if (i == 0 || (kp >> 3) != ck) table_insert(ctab, ck, i, p.shift, p.mask);
+  }
+}
+
+// run tails complete the counts (the heads' inserts are visible after the kernel boundary)
+__global__ __launch_bounds__(kTB) void grid_counts(const int* __restrict__ d_m, const uint32_t* __restrict__ keys,
+                                                   const GridParams* __restrict__ gp, int4* __restrict__ tab,
+                                                   int4* __restrict__ ctab) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int m = *d_m;
+  if (i >= m) return;
+  const uint32_t k = keys[i];
+  const uint32_t kn = i + 1 < m ? keys[i + 1] : kEmpty;
+  if (i + 1 < m && kn == k) return;
+  const GridParams p = *gp;
+  const uint32_t ck = k >> 3, sub = k & 7u;
+  const int cx = (int)(ck % (uint32_t)p.cnx), cy = (int)((ck / (uint32_t)p.cnx) % (uint32_t)p.cny),
+            cz = (int)(ck / ((uint32_t)p.cnx * (uint32_t)p.cny));
+  const int h = table_find(tab, fine_key(p, 2 * cx + (int)(sub & 1u), 2 * cy + (int)((sub >> 1) & 1u),
+                                         2 * cz + (int)(sub >> 2)), p.shift, p.mask);
+  if (h >= 0) tab[h].z = i + 1 - tab[h].y;
+  if (i + 1 >= m || (kn >> 3) != ck) {
+    const int hc = table_find(ctab, ck, p.shift, p.mask);
+    if (hc >= 0) ctab[hc].z = i + 1 - ctab[hc].y;
   }
 }
 
@@ -418,9 +478,8 @@ __device__ void plane_solve(const double (&A)[5][3], double (&x)[3]) {
 // (coalesced within a cell, since cells are contiguous runs of the cell-sorted map).  Each lane keeps a sorted
 // top-5 of 64-bit keys (float sq-distance bits << 32 | map index: ascending distance, ties by map index) and a
 // butterfly merge over the group gives the exact 5-NN; lane 0 then runs the fp64 line / plane geometry.
-constexpr int kGroup = 16;
-constexpr int kGroupsPerBlock = kTB / kGroup;
-constexpr int kUnroll = 4;
+constexpr int kGroupDefault = 16;   // lanes per query (template parameter G below)
+constexpr int kUnrollDefault = 4;   // candidate loads in flight per lane (U)
 
 __device__ __forceinline__ int2 grid_lookup(const int4* __restrict__ tab, uint32_t key, int shift, unsigned mask) {
   uint32_t h = hash_slot(key, shift);
@@ -462,16 +521,18 @@ __device__ __forceinline__ void top5_merge(Top5& a, const Top5& b) {
   for (int i = 0; i < 5; ++i) a.k[i] = m[i];
 }
 
+template <int G>
 __device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v, int m) {
-  const int lo = __shfl_xor((int)(v & 0xFFFFFFFFull), m, kGroup);
-  const int hi = __shfl_xor((int)(v >> 32), m, kGroup);
+  const int lo = __shfl_xor((int)(v & 0xFFFFFFFFull), m, G);
+  const int hi = __shfl_xor((int)(v >> 32), m, G);
   return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
 }
 
+template <int G>
 __device__ __forceinline__ int group_incl_scan(int v, int lane) {
 #pragma unroll
-  for (int o = 1; o < kGroup; o <<= 1) {
-    const int u = __shfl_up(v, o, kGroup);
+  for (int o = 1; o < G; o <<= 1) {
+    const int u = __shfl_up(v, o, G);
     if (lane >= o) v += u;
   }
   return v;
@@ -491,140 +552,200 @@ struct CorrArgs {
   int n_ub;
   const GridParams* gp;
   const float4* gpts;
-  const int4* tab;
-  const PointRec* map;
+  const int4* tab;         // fine cells
+  const int4* ctab;        // coarse cells
   double* rec;
   uint8_t* valid;
-  int* nn;
+  float* nnxyz;
   int cap;
   unsigned long long* dbg;   // FLOAM_DEBUG_STAMPS: per-phase latency sums (diagnostic, normally null)
 };
 
+// Scan a block of up to 3 x 3 x 3 cells of one table into the lane-local top-5 (keys: float sq-distance bits << 32
+// | position in the cell-sorted array, so ties go to the lower position).  Lane l looks up a contiguous run of the
+// block's cells (all first probes issued before any is waited on), the group scans the counts into an exclusive
+// prefix in LDS (cell order), and the lanes walk the flattened candidate list t = lane, lane + G, ... with a forward
+// cursor and U independent 16-B loads in flight (coalesced within a cell).
+constexpr int kMaxStencil = 27;
+
+template <int G, int U, bool COARSE>
+__device__ __forceinline__ void stencil_scan(const CorrArgs& A, const GridParams& p, int x0, int x1, int y0, int y1,
+                                             int z0, int z1, float wx, float wy, float wz, int lane,
+                                             int* __restrict__ s_pre, int* __restrict__ s_start, Top5& t, int& cnt) {
+  constexpr int P = (kMaxStencil + G - 1) / G;   // cells per lane
+  const int4* __restrict__ tab = COARSE ? A.ctab : A.tab;
+  const int nxr = max(0, x1 - x0 + 1), nyr = max(0, y1 - y0 + 1), nzr = max(0, z1 - z0 + 1);
+  const int ncell = nxr * nyr * nzr;
+  const int per = (ncell + G - 1) / G;
+  const int cb = min(ncell, lane * per), ce = min(ncell, cb + per);
+  uint32_t key[P];
+  uint32_t slot[P];
+  int4 e[P];
+#pragma unroll
+  for (int j = 0; j < P; ++j) {
+    const int c = cb + j;
+    key[j] = kEmpty;
+    e[j] = make_int4((int)kEmpty, 0, 0, 0);
+    if (c < ce) {
+      const int cx = x0 + c % nxr, cy = y0 + (c / nxr) % nyr, cz = z0 + c / (nxr * nyr);
+      key[j] = COARSE ? coarse_key(p, cx, cy, cz) : fine_key(p, cx, cy, cz);
+      slot[j] = hash_slot(key[j], p.shift);
+      e[j] = tab[slot[j]];
+    }
+  }
+  int local = 0;
+#pragma unroll
+  for (int j = 0; j < P; ++j) {
+    const int c = cb + j;
+    if (c < ce) {
+      while ((uint32_t)e[j].x != key[j] && (uint32_t)e[j].x != kEmpty) {   // collision chain (rare)
+        slot[j] = (slot[j] + 1) & p.mask;
+        e[j] = tab[slot[j]];
+      }
+      const int start = (uint32_t)e[j].x == key[j] ? e[j].y : 0;
+      const int count = (uint32_t)e[j].x == key[j] ? e[j].z : 0;
+      s_start[c] = start;
+      s_pre[c] = local;
+      local += count;
+    }
+  }
+  const int incl = group_incl_scan<G>(local, lane);
+  const int excl = incl - local;
+#pragma unroll
+  for (int j = 0; j < P; ++j)
+    if (cb + j < ce) s_pre[cb + j] += excl;
+  const int tot = __shfl(incl, G - 1, G);
+  if (lane == 0) s_pre[ncell] = tot;
+  wave_lds_order();
+  int c = 0, c_lo = 0, c_hi = ncell ? s_pre[1] : 0, c_start = ncell ? s_start[0] : 0;   // cell c = [c_lo, c_hi)
+  for (int tb = 0; tb < tot; tb += G * U) {
+    float4 m[U];
+    int pos[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int tt = tb + u * G + lane;
+      pos[u] = 0;
+      if (tt < tot) {
+        while (tt >= c_hi) {
+          ++c;
+          c_lo = c_hi;
+          c_hi = s_pre[c + 1];
+          c_start = s_start[c];
+        }
+        pos[u] = c_start + (tt - c_lo);
+        m[u] = A.gpts[pos[u]];
+      } else {
+        m[u] = make_float4(1e30f, 1e30f, 1e30f, 0.0f);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float dd = 0.0f;   // flann::L2_Simple<float>: ((0 + dx*dx) + dy*dy) + dz*dz
+      float df = wx - m[u].x;
+      dd += df * df;
+      df = wy - m[u].y;
+      dd += df * df;
+      df = wz - m[u].z;
+      dd += df * df;
+      if (dd < 1.0f) {
+        ++cnt;
+        top5_insert(t, ((unsigned long long)__float_as_uint(dd) << 32) | (unsigned)pos[u]);
+      }
+    }
+  }
+  wave_lds_order();   // the group's LDS slot is rewritten by its next scan
+}
+
+// group-wide top-5 (every lane ends with the merged list) and count
+template <int G>
+__device__ __forceinline__ void group_merge(Top5& t, int& cnt) {
+#pragma unroll
+  for (int mm = G / 2; mm > 0; mm >>= 1) {
+    Top5 o;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) o.k[k] = shfl_xor_u64<G>(t.k[k], mm);
+    top5_merge(t, o);
+    cnt += __shfl_xor(cnt, mm, G);
+  }
+}
+
 // Pass 1: exact 5-NN of every query (no fp64 geometry here, so the kernel stays small and at high occupancy).
+// The reference keeps a correspondence iff the 5th-nearest float sq-distance is < 1 (:154, :210), so only map
+// points within 1 m matter.  Stage 1 scans the 3x3x3 FINE cells (edge c = 0.5 m) around the query's cell: every
+// point outside that block is at least c away along some axis, so its float sq-distance is >= c*c (exact: the cell
+// bounds are exact and fl(dx) >= c by monotone rounding); if 5 points with sq-distance < c*c were found they are
+// the exact 5-NN.  Otherwise stage 2 scans the COARSE cells (edge 2c = 1 m) spanning [q-1, q+1] on every axis
+// (<= 3x3x3), which contain every point within 1 m.  Ties at equal float distance go to the lower grid position
+// (FLANN's own order depends on its tree traversal; tie-free data is identical).
+// Output: valid bit 0 = 5 neighbours within sqd < 1 (their coordinates in nnxyz), bit 1 = stage 2 was needed.
+template <int G, int U>
 __device__ __forceinline__ void knn_group(const LMState* __restrict__ st, const CorrArgs& A, int gid, int ngroups,
                                           int lane, bool gate, int rank, int world, int* __restrict__ s_pre,
                                           int* __restrict__ s_start) {
   const int n = min(*A.d_n, A.n_ub);
   const int lo = (int)(((long long)n * rank) / world), hi = (int)(((long long)n * (rank + 1)) / world);
   const GridParams p = *A.gp;
-  const double inv = 1.0 / p.c;
+  const double inv = 1.0 / p.c, cinv = 0.5 / p.c;
+  const float cc2 = (float)(p.c * p.c);
   unsigned long long dsum[6] = {0, 0, 0, 0, 0, 0};
   unsigned long long ts = 0;
   // grid-stride over the queries the device holds (the host only knows an upper bound)
   for (int i0 = 0; i0 < n; i0 += ngroups) {
     const int i = i0 + gid;   // query
     if (i >= n) break;
-    bool ok = false;
+    int flags = 0;
     if (i >= lo && i < hi && gate) {
       if (A.dbg) ts = __builtin_amdgcn_s_memrealtime();
       const float4 pq = *reinterpret_cast<const float4*>(&A.q[i].x);
       float wx, wy, wz;
       associate_to_map(st->x, pq.x, pq.y, pq.z, wx, wy, wz);   // pointAssociateToMap (:126-135)
-      // |m - q| < 1 on every axis  =>  cell in [floor((q-o-1)/c), floor((q-o+1)/c)]  (c is a power of two)
-      const int x0 = max(0, (int)floor(((double)wx - p.ox - 1.0) * inv));
-      const int x1 = min(p.nx - 1, (int)floor(((double)wx - p.ox + 1.0) * inv));
-      const int y0 = max(0, (int)floor(((double)wy - p.oy - 1.0) * inv));
-      const int y1 = min(p.ny - 1, (int)floor(((double)wy - p.oy + 1.0) * inv));
-      const int z0 = max(0, (int)floor(((double)wz - p.oz - 1.0) * inv));
-      const int z1 = min(p.nz - 1, (int)floor(((double)wz - p.oz + 1.0) * inv));
-      const int nxr = max(0, x1 - x0 + 1), nyr = max(0, y1 - y0 + 1), nzr = max(0, z1 - z0 + 1);
-      const int ncell = nxr * nyr * nzr;   // <= 27
-      int2 se[2] = {make_int2(0, 0), make_int2(0, 0)};
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int c = lane + h * kGroup;
-        if (c < ncell) {
-          const int cx = x0 + c % nxr, cy = y0 + (c / nxr) % nyr, cz = z0 + c / (nxr * nyr);
-          const uint32_t key = (uint32_t)cx + (uint32_t)p.nx * ((uint32_t)cy + (uint32_t)p.ny * (uint32_t)cz);
-          se[h] = grid_lookup(A.tab, key, p.shift, p.mask);
-        }
-      }
-      if (A.dbg) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned long long t = __builtin_amdgcn_s_memrealtime();
-        dsum[0] += t - ts;
-        ts = t;
-      }
-      // exclusive prefix of the candidate counts over the cells, in cell order, into this group's LDS slot
-      const int p0 = group_incl_scan(se[0].y, lane);
-      const int tot0 = __shfl(p0, kGroup - 1, kGroup);
-      const int p1 = group_incl_scan(se[1].y, lane);
-      const int tot = tot0 + __shfl(p1, kGroup - 1, kGroup);
-      s_pre[lane] = p0 - se[0].y;
-      s_start[lane] = se[0].x;
-      if (lane + kGroup < 27) {
-        s_pre[lane + kGroup] = tot0 + p1 - se[1].y;
-        s_start[lane + kGroup] = se[1].x;
-      }
-      if (lane == 0) s_pre[27] = tot;
-      wave_lds_order();
+      const double rx = (double)wx - p.ox, ry = (double)wy - p.oy, rz = (double)wz - p.oz;   // exact
+      const int qx = (int)floor(rx * inv), qy = (int)floor(ry * inv), qz = (int)floor(rz * inv);
       Top5 t;
 #pragma unroll
       for (int k = 0; k < 5; ++k) t.k[k] = ~0ull;
       int cnt = 0;
-      int c = 0, c_lo = 0, c_hi = s_pre[1], c_start = s_start[0];   // cursor: cell c spans [c_lo, c_hi)
-      for (int tb = 0; tb < tot; tb += kGroup * kUnroll) {
-        float4 m[kUnroll];
-#pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
-          const int tt = tb + u * kGroup + lane;
-          if (tt < tot) {
-            while (tt >= c_hi) {
-              ++c;
-              c_lo = c_hi;
-              c_hi = s_pre[c + 1];
-              c_start = s_start[c];
-            }
-            m[u] = A.gpts[c_start + (tt - c_lo)];
-          } else {
-            m[u] = make_float4(1e30f, 1e30f, 1e30f, 0.0f);
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
-          float dd = 0.0f;   // flann::L2_Simple<float>: ((0 + dx*dx) + dy*dy) + dz*dz
-          float df = wx - m[u].x;
-          dd += df * df;
-          df = wy - m[u].y;
-          dd += df * df;
-          df = wz - m[u].z;
-          dd += df * df;
-          if (dd < 1.0f) {
-            ++cnt;
-            top5_insert(t, ((unsigned long long)__float_as_uint(dd) << 32) | (unsigned)__float_as_int(m[u].w));
-          }
-        }
-      }
+      stencil_scan<G, U, false>(A, p, max(0, qx - 1), min(p.nx - 1, qx + 1), max(0, qy - 1), min(p.ny - 1, qy + 1),
+                                max(0, qz - 1), min(p.nz - 1, qz + 1), wx, wy, wz, lane, s_pre, s_start, t, cnt);
+      group_merge<G>(t, cnt);
+      const bool complete = p.c >= 1.0 || (cnt >= 5 && __uint_as_float((unsigned)(t.k[4] >> 32)) < cc2);
       if (A.dbg) {
         const unsigned long long tn = __builtin_amdgcn_s_memrealtime();
-        dsum[1] += tn - ts;
+        dsum[0] += tn - ts;
         ts = tn;
-        dsum[5] += (unsigned long long)tot;
       }
+      if (!complete) {   // coarse cells [floor((q-o-1)/2c), floor((q-o+1)/2c)] per axis
 #pragma unroll
-      for (int mm = kGroup / 2; mm > 0; mm >>= 1) {
-        Top5 o;
+        for (int k = 0; k < 5; ++k) t.k[k] = ~0ull;
+        cnt = 0;
+        stencil_scan<G, U, true>(A, p, max(0, (int)floor((rx - 1.0) * cinv)), min(p.cnx - 1, (int)floor((rx + 1.0) * cinv)),
+                                 max(0, (int)floor((ry - 1.0) * cinv)), min(p.cny - 1, (int)floor((ry + 1.0) * cinv)),
+                                 max(0, (int)floor((rz - 1.0) * cinv)), min(p.cnz - 1, (int)floor((rz + 1.0) * cinv)),
+                                 wx, wy, wz, lane, s_pre, s_start, t, cnt);
+        group_merge<G>(t, cnt);
+        flags |= 2;
+        if (A.dbg) {
+          const unsigned long long tn = __builtin_amdgcn_s_memrealtime();
+          dsum[1] += tn - ts;
+          dsum[2] += 1;
+        }
+      }
+      if (cnt >= 5) {   // sqd[4] < 1 (:154, :210)
+        flags |= 1;
+        if (lane < 5) {   // lane k writes the coordinates of neighbour k (cached: just scanned)
+          unsigned long long kk = t.k[0];
 #pragma unroll
-        for (int k = 0; k < 5; ++k) o.k[k] = shfl_xor_u64(t.k[k], mm);
-        top5_merge(t, o);
-        cnt += __shfl_xor(cnt, mm, kGroup);
+          for (int k = 1; k < 5; ++k)
+            if (lane == k) kk = t.k[k];
+          const float4 m = A.gpts[(int)(kk & 0xFFFFFFFFull)];
+          A.nnxyz[(3 * lane + 0) * A.cap + i] = m.x;
+          A.nnxyz[(3 * lane + 1) * A.cap + i] = m.y;
+          A.nnxyz[(3 * lane + 2) * A.cap + i] = m.z;
+        }
       }
-      wave_lds_order();   // this group's LDS slot is rewritten by its next query
-      ok = cnt >= 5;      // sqd[4] < 1 (:154, :210)
-      if (ok && lane < 5) {
-        unsigned long long kk = t.k[0];
-#pragma unroll
-        for (int k = 1; k < 5; ++k)
-          if (lane == k) kk = t.k[k];
-        A.nn[lane * A.cap + i] = (int)(kk & 0xFFFFFFFFull);
-      }
-      if (A.dbg) {
-        const unsigned long long tn = __builtin_amdgcn_s_memrealtime();
-        dsum[2] += tn - ts;
-        dsum[4] += 1;
-      }
+      if (A.dbg) dsum[4] += 1;
     }
-    if (lane == 0) A.valid[i] = ok ? 1 : 0;
+    if (lane == 0) A.valid[i] = (uint8_t)flags;
   }
   if (A.dbg && lane == 0 && dsum[4])
 #pragma unroll
@@ -632,20 +753,21 @@ __device__ __forceinline__ void knn_group(const LMState* __restrict__ st, const 
 }
 
 // Edge and surf kNN in one launch: blocks [0, nbE) run edge groups, the others surf groups.
+template <int G, int U>
 __global__ __launch_bounds__(kTB) void knn_kernel(const LMState* __restrict__ st, CorrArgs E, CorrArgs S, int nbE,
                                                   const int* __restrict__ d_me, const int* __restrict__ d_ms,
                                                   int rank, int world) {
-  __shared__ int s_pre[kGroupsPerBlock][28];
-  __shared__ int s_start[kGroupsPerBlock][27];
-  const int lane = threadIdx.x & (kGroup - 1);
-  const int g = threadIdx.x / kGroup;
+  __shared__ int s_pre[kTB / G][kMaxStencil + 1];
+  __shared__ int s_start[kTB / G][kMaxStencil];
+  const int lane = threadIdx.x & (G - 1);
+  const int g = threadIdx.x / G;
   const bool gate = *d_me > 10 && *d_ms > 50;   // map-size gate (odomEstimationClass.cpp:77)
   if ((int)blockIdx.x < nbE)
-    knn_group(st, E, (blockIdx.x * blockDim.x + threadIdx.x) / kGroup, nbE * kGroupsPerBlock, lane, gate, rank,
-              world, s_pre[g], s_start[g]);
+    knn_group<G, U>(st, E, (blockIdx.x * blockDim.x + threadIdx.x) / G, nbE * (kTB / G), lane, gate, rank, world,
+                    s_pre[g], s_start[g]);
   else
-    knn_group(st, S, ((blockIdx.x - nbE) * blockDim.x + threadIdx.x) / kGroup, (gridDim.x - nbE) * kGroupsPerBlock,
-              lane, gate, rank, world, s_pre[g], s_start[g]);
+    knn_group<G, U>(st, S, ((blockIdx.x - nbE) * blockDim.x + threadIdx.x) / G, (gridDim.x - nbE) * (kTB / G), lane,
+                    gate, rank, world, s_pre[g], s_start[g]);
 }
 
 // Pass 2: fp64 line / plane geometry, one query per lane (all 64 lanes busy).
@@ -653,13 +775,13 @@ template <bool EDGE>
 __device__ __forceinline__ void geom_query(LMState* __restrict__ st, const CorrArgs& A, int i) {
   const int n = min(*A.d_n, A.n_ub);
   bool ok = false;
-  if (i < n && A.valid[i]) {
+  const int flags = i < n ? A.valid[i] : 0;
+  if (flags & 1) {
     double P[5][3];
 #pragma unroll
-    for (int j = 0; j < 5; ++j) {
-      const float4 mp = *reinterpret_cast<const float4*>(&A.map[A.nn[j * A.cap + i]].x);
-      P[j][0] = mp.x; P[j][1] = mp.y; P[j][2] = mp.z;
-    }
+    for (int j = 0; j < 5; ++j)
+#pragma unroll
+      for (int a = 0; a < 3; ++a) P[j][a] = A.nnxyz[(3 * j + a) * A.cap + i];
     const float4 pq = *reinterpret_cast<const float4*>(&A.q[i].x);
     const double cpx = pq.x, cpy = pq.y, cpz = pq.z;
     double* rec = A.rec;
@@ -712,7 +834,7 @@ __device__ __forceinline__ void geom_query(LMState* __restrict__ st, const CorrA
         rec[6 * cap + i] = d;
       }
     }
-    A.valid[i] = ok ? 1 : 0;
+    A.valid[i] = (uint8_t)((flags & 2) | (ok ? 1 : 0));
   }
   const unsigned long long b = __ballot(ok);
   if ((threadIdx.x & 63) == 0 && b) atomicAdd(EDGE ? &st->corr_edge : &st->corr_surf, __popcll(b));
@@ -725,51 +847,59 @@ __global__ __launch_bounds__(kTB) void geom_kernel(LMState* __restrict__ st, Cor
     geom_query<false>(st, S, (blockIdx.x - nbE) * blockDim.x + threadIdx.x);
 }
 
-// Algorithmic traffic of one correspondence launch (SURVEY.md §8 d): every occupied 1-m query cell streams its
-// 27-cell candidate set once (16 B per map point), every query is read once (16 B) and writes its valid flag
-// (1 B) and, if accepted, its record.  Runs untimed, after the kernel it describes, only when profiling.
+// Algorithmic traffic of one correspondence pass (SURVEY.md §8 d): every map cell any query scans
+// is streamed once (16 B per map point: the union over queries of the fine 3x3x3 block around the query's cell —
+// level 0 — and of the coarse +-1 m stencil for the queries whose bit 1 says they needed stage 2 — level 1), every
+// query is read once (16 B) and writes its flag (1 B) and, if accepted, its record (counted at level 0).  Runs
+// untimed, on a replay, only when profiling.
 __global__ __launch_bounds__(kTB) void knn_traffic(const LMState* __restrict__ st, const PointRec* __restrict__ q,
                                                    const int* __restrict__ d_n, int n_ub,
                                                    const GridParams* __restrict__ gp, const int4* __restrict__ tab,
-                                                   const uint8_t* __restrict__ valid,
-                                                   int rec_bytes, int rank, int world, uint32_t* __restrict__ set,
-                                                   unsigned set_mask, int set_shift,
+                                                   const int4* __restrict__ ctab, const uint8_t* __restrict__ valid,
+                                                   int rec_bytes, int rank, int world, int level,
+                                                   uint32_t* __restrict__ set, unsigned set_mask, int set_shift,
                                                    unsigned long long* __restrict__ out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_ub) return;
   const int n = *d_n;
   const int lo = (int)(((long long)n * rank) / world), hi = (int)(((long long)n * (rank + 1)) / world);
   if (i < lo || i >= hi) return;
+  const int f = valid[i];
+  if (level == 1 && !(f & 2)) return;
   const PointRec pr = q[i];
   float wx, wy, wz;
   associate_to_map(st->x, pr.x, pr.y, pr.z, wx, wy, wz);
   const GridParams p = *gp;
-  const double inv = 1.0 / p.c;
-  const int cx = (int)floor(((double)wx - p.ox) * inv), cy = (int)floor(((double)wy - p.oy) * inv),
-            cz = (int)floor(((double)wz - p.oz) * inv);
-  unsigned long long bytes = 16ull + 1ull + (valid[i] ? (unsigned long long)rec_bytes : 0ull);
-  const uint32_t key = ((uint32_t)(cx + 2) & 0x7FFu) | (((uint32_t)(cy + 2) & 0x7FFu) << 11) |
-                       (((uint32_t)(cz + 2) & 0x3FFu) << 22);
-  uint32_t h = hash_slot(key, set_shift);
-  bool fresh = false;
-  for (;;) {
-    const uint32_t prev = atomicCAS(&set[h], kEmpty, key);
-    if (prev == kEmpty) { fresh = true; break; }
-    if (prev == key) break;
-    h = (h + 1) & set_mask;
+  const double inv = 1.0 / p.c, cinv = 0.5 / p.c;
+  const double rx = (double)wx - p.ox, ry = (double)wy - p.oy, rz = (double)wz - p.oz;
+  unsigned long long bytes = level ? 0ull : 16ull + 1ull + ((f & 1) ? (unsigned long long)rec_bytes : 0ull);
+  int x0, x1, y0, y1, z0, z1, nx, ny, nz;
+  if (level) {
+    x0 = (int)floor((rx - 1.0) * cinv); x1 = (int)floor((rx + 1.0) * cinv);
+    y0 = (int)floor((ry - 1.0) * cinv); y1 = (int)floor((ry + 1.0) * cinv);
+    z0 = (int)floor((rz - 1.0) * cinv); z1 = (int)floor((rz + 1.0) * cinv);
+    nx = p.cnx; ny = p.cny; nz = p.cnz;
+  } else {
+    x0 = (int)floor(rx * inv) - 1; x1 = x0 + 2;
+    y0 = (int)floor(ry * inv) - 1; y1 = y0 + 2;
+    z0 = (int)floor(rz * inv) - 1; z1 = z0 + 2;
+    nx = p.nx; ny = p.ny; nz = p.nz;
   }
-  if (fresh) {
-    unsigned long long cand = 0;
-    for (int z = cz - 1; z <= cz + 1; ++z)
-      for (int y = cy - 1; y <= cy + 1; ++y)
-        for (int x = cx - 1; x <= cx + 1; ++x) {
-          if (x < 0 || y < 0 || z < 0 || x >= p.nx || y >= p.ny || z >= p.nz) continue;
-          const uint32_t k = (uint32_t)x + (uint32_t)p.nx * ((uint32_t)y + (uint32_t)p.ny * (uint32_t)z);
-          cand += (unsigned long long)grid_lookup(tab, k, p.shift, p.mask).y;
+  for (int z = max(0, z0); z <= min(nz - 1, z1); ++z)
+    for (int y = max(0, y0); y <= min(ny - 1, y1); ++y)
+      for (int x = max(0, x0); x <= min(nx - 1, x1); ++x) {
+        const uint32_t k = level ? coarse_key(p, x, y, z) : fine_key(p, x, y, z);
+        const int cnt = grid_lookup(level ? ctab : tab, k, p.shift, p.mask).y;
+        if (cnt == 0) continue;
+        uint32_t h = hash_slot(k, set_shift);
+        for (;;) {
+          const uint32_t prev = atomicCAS(&set[h], kEmpty, k);
+          if (prev == kEmpty) { bytes += 16ull * (unsigned long long)cnt; break; }
+          if (prev == k) break;
+          h = (h + 1) & set_mask;
         }
-    bytes += 16ull * cand;
-  }
-  atomicAdd(out, bytes);
+      }
+  if (bytes) atomicAdd(out, bytes);
 }
 
 __global__ void lm_init(LMState* st, X7 x0) {
@@ -871,14 +1001,14 @@ __device__ void eval_block(const LMState* __restrict__ st, const double* __restr
   for (int idx = blk * blockDim.x + threadIdx.x; idx < total; idx += nblk * blockDim.x) {
     double J[6], r;
     if (idx < ne) {
-      if (!evalid[idx]) continue;
+      if (!(evalid[idx] & 1)) continue;
       double f[9];
 #pragma unroll
       for (int k = 0; k < 9; ++k) f[k] = erec[k * ecap + idx];
       r = edge_residual(x, f, J);
     } else {
       const int s = idx - ne;
-      if (!svalid[s]) continue;
+      if (!(svalid[s] & 1)) continue;
       double f[7];
 #pragma unroll
       for (int k = 0; k < 7; ++k) f[k] = srec[k * scap + s];
@@ -1359,6 +1489,7 @@ void grid_build_launch(Grid& g, GridScratch& sc, const PointRec* map, const int*
   int tsize = 1024, shift = 32 - 10;
   while (tsize < 2 * ub) { tsize <<= 1; --shift; }
   g.tab.reserve(tsize);
+  g.ctab.reserve(tsize);
   g.table_size = tsize;
   g.shift = shift;
   minmax_launch(map, d_m, ub, sc.mm.p, st);
@@ -1366,11 +1497,13 @@ void grid_build_launch(Grid& g, GridScratch& sc, const PointRec* map, const int*
   FLOAM_LAUNCH_CHECK();
   const unsigned gb = div_up(ub, kTB);
   hipLaunchKernelGGL(grid_keys, dim3(gb), dim3(kTB), 0, st, map, d_m, ub, g.params.p, sc.s.k0.p, sc.s.v0.p, g.tab.p,
-                     tsize);
+                     g.ctab.p, tsize);
   FLOAM_LAUNCH_CHECK();
   sort_pairs_u32(sc.s.temp.p, sc.s.temp_bytes, sc.s.k0.p, sc.s.k1.p, sc.s.v0.p, sc.s.v1.p, ub, 32, st);
   hipLaunchKernelGGL(grid_fill, dim3(gb), dim3(kTB), 0, st, map, d_m, sc.s.k1.p, sc.s.v1.p, g.params.p, g.pts.p,
-                     g.tab.p);
+                     g.tab.p, g.ctab.p);
+  FLOAM_LAUNCH_CHECK();
+  hipLaunchKernelGGL(grid_counts, dim3(gb), dim3(kTB), 0, st, d_m, sc.s.k1.p, g.params.p, g.tab.p, g.ctab.p);
   FLOAM_LAUNCH_CHECK();
 }
 
@@ -1408,20 +1541,54 @@ void gather_status_launch(const LMState* lm, const int* dcnt, const int* mapE_co
   FLOAM_LAUNCH_CHECK();
 }
 
-void corr_launch(LMState* d_st, const QuerySet& qe, const Grid& ge, const PointRec* mapE, CorrSet& ce,
-                 const QuerySet& qs, const Grid& gs, const PointRec* mapS, CorrSet& cs, const int* d_me,
-                 const int* d_ms, int rank, int world, hipStream_t st, unsigned long long* dbg) {
+static void corr_args(const QuerySet& qe, const Grid& ge, const PointRec* mapE, CorrSet& ce, const QuerySet& qs,
+                      const Grid& gs, const PointRec* mapS, CorrSet& cs, unsigned long long* dbg, CorrArgs& E,
+                      CorrArgs& S) {
   ce.reserve(std::max(qe.n_ub, 1), EDGE_FIELDS);
   cs.reserve(std::max(qs.n_ub, 1), SURF_FIELDS);
-  if (qe.n_ub <= 0 && qs.n_ub <= 0) return;
-  const CorrArgs E{qe.pts, qe.d_n, qe.n_ub, ge.params.p, ge.pts.p, ge.tab.p, mapE, ce.rec.p, ce.valid.p, ce.nn.p,
-                   ce.cap, dbg};
-  const CorrArgs S{qs.pts, qs.d_n, qs.n_ub, gs.params.p, gs.pts.p, gs.tab.p, mapS, cs.rec.p, cs.valid.p, cs.nn.p,
-                   cs.cap, dbg ? dbg + 8 : nullptr};
-  const unsigned nbE = std::min(div_up((size_t)std::max(qe.n_ub, 1) * kGroup, kTB), 2048u);
-  const unsigned nbS = std::min(div_up((size_t)std::max(qs.n_ub, 1) * kGroup, kTB), 4096u);
-  hipLaunchKernelGGL(knn_kernel, dim3(nbE + nbS), dim3(kTB), 0, st, d_st, E, S, (int)nbE, d_me, d_ms, rank, world);
+  (void)mapE;
+  (void)mapS;
+  E = CorrArgs{qe.pts, qe.d_n, qe.n_ub, ge.params.p, ge.pts.p, ge.tab.p, ge.ctab.p, ce.rec.p, ce.valid.p, ce.nnxyz.p,
+               ce.cap, dbg};
+  S = CorrArgs{qs.pts, qs.d_n, qs.n_ub, gs.params.p, gs.pts.p, gs.tab.p, gs.ctab.p, cs.rec.p, cs.valid.p, cs.nnxyz.p,
+               cs.cap, dbg ? dbg + 8 : nullptr};
+}
+
+template <int G, int U>
+static void knn_launch_t(const LMState* d_st, const QuerySet& qe, const QuerySet& qs, const CorrArgs& E,
+                         const CorrArgs& S, const int* d_me, const int* d_ms, int rank, int world, hipStream_t st) {
+  const unsigned nbE = std::min(div_up((size_t)std::max(qe.n_ub, 1) * G, kTB), 4096u);
+  const unsigned nbS = std::min(div_up((size_t)std::max(qs.n_ub, 1) * G, kTB), 8192u);
+  hipLaunchKernelGGL((knn_kernel<G, U>), dim3(nbE + nbS), dim3(kTB), 0, st, d_st, E, S, (int)nbE, d_me, d_ms, rank,
+                     world);
   FLOAM_LAUNCH_CHECK();
+}
+
+void knn_launch(const LMState* d_st, const QuerySet& qe, const Grid& ge, const PointRec* mapE, CorrSet& ce,
+                const QuerySet& qs, const Grid& gs, const PointRec* mapS, CorrSet& cs, const int* d_me,
+                const int* d_ms, int rank, int world, hipStream_t st, unsigned long long* dbg) {
+  CorrArgs E, S;
+  corr_args(qe, ge, mapE, ce, qs, gs, mapS, cs, dbg, E, S);
+  if (qe.n_ub <= 0 && qs.n_ub <= 0) return;
+  static const int variant = [] {   // FLOAM_KNN_VARIANT: lanes per query x loads in flight (tuning only)
+    const char* v = std::getenv("FLOAM_KNN_VARIANT");
+    return v ? std::atoi(v) : 0;
+  }();
+  switch (variant) {
+    case 1: knn_launch_t<8, 4>(d_st, qe, qs, E, S, d_me, d_ms, rank, world, st); break;
+    case 2: knn_launch_t<8, 2>(d_st, qe, qs, E, S, d_me, d_ms, rank, world, st); break;
+    case 3: knn_launch_t<32, 2>(d_st, qe, qs, E, S, d_me, d_ms, rank, world, st); break;
+    case 4: knn_launch_t<16, 2>(d_st, qe, qs, E, S, d_me, d_ms, rank, world, st); break;
+    case 5: knn_launch_t<4, 4>(d_st, qe, qs, E, S, d_me, d_ms, rank, world, st); break;
+    default: knn_launch_t<kGroupDefault, kUnrollDefault>(d_st, qe, qs, E, S, d_me, d_ms, rank, world, st); break;
+  }
+}
+
+void geom_launch(LMState* d_st, const QuerySet& qe, const Grid& ge, const PointRec* mapE, CorrSet& ce,
+                 const QuerySet& qs, const Grid& gs, const PointRec* mapS, CorrSet& cs, hipStream_t st) {
+  CorrArgs E, S;
+  corr_args(qe, ge, mapE, ce, qs, gs, mapS, cs, nullptr, E, S);
+  if (qe.n_ub <= 0 && qs.n_ub <= 0) return;
   const unsigned gE = div_up(std::max(qe.n_ub, 1), kTB), gS = div_up(std::max(qs.n_ub, 1), kTB);
   hipLaunchKernelGGL(geom_kernel, dim3(gE + gS), dim3(kTB), 0, st, d_st, E, S, (int)gE);
   FLOAM_LAUNCH_CHECK();
@@ -1431,13 +1598,15 @@ void knn_traffic_launch(const LMState* d_st, const QuerySet& q, const Grid& g, c
                         int rank, int world, DevBuf<uint32_t>& set, unsigned long long* d_bytes, hipStream_t st) {
   if (q.n_ub <= 0) return;
   int size = 1024, shift = 22;
-  while (size < 2 * q.n_ub) { size <<= 1; --shift; }
+  while (size < 64 * q.n_ub) { size <<= 1; --shift; }   // distinct occupied cells scanned (<= 27 per query)
   set.reserve(size);
-  FLOAM_HIP(hipMemsetAsync(set.p, 0xFF, sizeof(uint32_t) * size, st));
-  hipLaunchKernelGGL(knn_traffic, dim3(div_up(q.n_ub, kTB)), dim3(kTB), 0, st, d_st, q.pts, q.d_n, q.n_ub,
-                     g.params.p, g.tab.p, c.valid.p, rec_bytes, rank, world, set.p, (unsigned)(size - 1),
-                     shift, d_bytes);
-  FLOAM_LAUNCH_CHECK();
+  for (int level = 0; level < 2; ++level) {
+    FLOAM_HIP(hipMemsetAsync(set.p, 0xFF, sizeof(uint32_t) * size, st));
+    hipLaunchKernelGGL(knn_traffic, dim3(div_up(q.n_ub, kTB)), dim3(kTB), 0, st, d_st, q.pts, q.d_n, q.n_ub,
+                       g.params.p, g.tab.p, g.ctab.p, c.valid.p, rec_bytes, rank, world, level, set.p,
+                       (unsigned)(size - 1), shift, d_bytes);
+    FLOAM_LAUNCH_CHECK();
+  }
 }
 
 int lm_eval_launch(const LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const CorrSet& cs,

@@ -5,23 +5,26 @@
 namespace floam {
 
 // ----------------------------------------------------------------------------------------- hash grid
-// Map points bucketed into cubic cells (edge >= 1 m, power of two) over the map's bounding box, cell-sorted as
-// float4 {x, y, z, map index bits}; occupied cells in an open-addressing hash table key -> (start, count).
-// Exact replacement of the 5-NN KD-tree under the reference's sqd[4] < 1 gate: every map
-// point with float sq-distance < 1 lies within one cell of the query's cell along each axis.
+// Map points bucketed into a two-level cubic grid over the map's bounding box: fine cells of edge c (0.5 m, doubled
+// only if the bbox would overflow 2^29 coarse cells) nested 2x2x2 in coarse cells of edge 2c.  The points are sorted
+// by (coarse cell, fine sub-cell) so every fine and every coarse cell is a contiguous run of `pts` (float4 {x, y, z,
+// map index bits}); two open-addressing tables map cell keys to (start, count).  Exact replacement of the 5-NN
+// KD-tree under the reference's sqd[4] < 1 gate (knn_group in odom_kernels.hip).
 struct GridParams {
   double ox, oy, oz;     // origin = floor(bbox min)
-  double c;              // cell edge (1, 2, 4, ... m)
-  int nx, ny, nz;
-  int shift;             // hash: (key * 0x9E3779B1) >> shift
+  double c;              // fine cell edge (0.5, 1, 2, ... m); coarse cells are 2c
+  int nx, ny, nz;        // fine cells per axis
+  int cnx, cny, cnz;     // coarse cells per axis
+  int shift;             // hash: (key * 0x9E3779B1) >> shift (both tables)
   unsigned mask;
   int n;                 // map points
 };
 
 struct Grid {
   DevBuf<GridParams> params;
-  DevBuf<float4> pts;      // cell-sorted
-  DevBuf<int4> tab;        // open addressing: {cell key, start, count, 0}; key 0xFFFFFFFF = empty (one 16-B probe)
+  DevBuf<float4> pts;      // sorted by (coarse cell, fine sub-cell)
+  DevBuf<int4> tab;        // fine cells:   {key, start, count, 0}; key 0xFFFFFFFF = empty (one 16-B probe)
+  DevBuf<int4> ctab;       // coarse cells: same layout
   int table_size = 0;
   int shift = 0;
 };
@@ -40,8 +43,9 @@ enum { EDGE_FIELDS = 9, SURF_FIELDS = 7 };
 
 struct CorrSet {
   DevBuf<double> rec;
-  DevBuf<uint8_t> valid;   // after the kNN pass: 5 neighbours within sqd < 1; after geometry: record accepted
-  DevBuf<int> nn;          // the 5 nearest map indices of each query, nn[k * cap + i]
+  DevBuf<uint8_t> valid;   // bit 0: after the kNN pass, 5 neighbours within sqd < 1; after geometry, record accepted
+                           // bit 1: the query needed the full +-1 m search (profiling byte counter)
+  DevBuf<float> nnxyz;     // coordinates of the 5 nearest map points, nnxyz[(3 * k + axis) * cap + i]
   int cap = 0;
   void reserve(int n, int fields) {
     if (n <= cap) return;
@@ -49,7 +53,7 @@ struct CorrSet {
     valid.reserve(c);
     cap = (int)valid.cap;
     rec.reserve((size_t)cap * fields);
-    nn.reserve((size_t)cap * 5);
+    nnxyz.reserve((size_t)cap * 15);
   }
 };
 
@@ -96,11 +100,14 @@ struct UpdateStatus {
 };
 void gather_status_launch(const LMState* lm, const int* dcnt, const int* mapE_count, const int* mapS_count,
                           const unsigned long long* prof, UpdateStatus* out, hipStream_t st);
-// correspondence search (kNN + line / plane geometry) for the edge and the surf query sets at the pose in st->x,
-// one launch: blocks [0, nbE) take edge queries against the corner map, the rest surf queries against the surf map
-void corr_launch(LMState* d_st, const QuerySet& qe, const Grid& ge, const PointRec* mapE, CorrSet& ce,
-                 const QuerySet& qs, const Grid& gs, const PointRec* mapS, CorrSet& cs, const int* d_me,
-                 const int* d_ms, int rank, int world, hipStream_t st, unsigned long long* dbg = nullptr);
+// Correspondence search for the edge and the surf query sets at the pose in st->x, in two launches:
+// knn_launch — exact 5-NN (blocks [0, nbE) edge queries against the corner map, the rest surf against the surf map);
+// geom_launch — fp64 line / plane fits and the residual records.
+void knn_launch(const LMState* d_st, const QuerySet& qe, const Grid& ge, const PointRec* mapE, CorrSet& ce,
+                const QuerySet& qs, const Grid& gs, const PointRec* mapS, CorrSet& cs, const int* d_me,
+                const int* d_ms, int rank, int world, hipStream_t st, unsigned long long* dbg = nullptr);
+void geom_launch(LMState* d_st, const QuerySet& qe, const Grid& ge, const PointRec* mapE, CorrSet& ce,
+                 const QuerySet& qs, const Grid& gs, const PointRec* mapS, CorrSet& cs, hipStream_t st);
 // algorithmic bytes of the correspondence launch just issued (profiling only), accumulated into *d_bytes
 void knn_traffic_launch(const LMState* d_st, const QuerySet& q, const Grid& g, const CorrSet& c, int rec_bytes,
                         int rank, int world, DevBuf<uint32_t>& set, unsigned long long* d_bytes, hipStream_t st);

@@ -149,6 +149,7 @@ floam_status floam_device_synchronize(int device);
  * FLOAM_PROF_KNN_BYTES adds an extra (non-product) kernel after each correspondence launch that counts its
  * algorithmic bytes; it is kept out of timed runs and used on an identical replay instead. */
 enum { FLOAM_PROF_KNN = 1, FLOAM_PROF_LM = 2, FLOAM_PROF_CLOUD = 4, FLOAM_PROF_FE = 8, FLOAM_PROF_KNN_BYTES = 16,
+       FLOAM_PROF_KNN_DETAIL = 32 /* separate search / geometry timers (each event pair perturbs the timeline) */,
        FLOAM_PROF_ALL = 0xEF };
 typedef struct floam_kernel_timing {
   char name[32];
