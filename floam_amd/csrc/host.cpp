@@ -184,7 +184,6 @@ struct floam_odom {
   DevBuf<PointRec> dE, dS, tmp;
   DevBuf<int> cnt;   // [0] dE count [1] dS count [2] tmp count
   VoxelScratch vs;
-  GridScratch gsc;
   Grid gE, gS;
   bool grid_dirty = true;
   CorrSet ce, cs;
@@ -195,7 +194,7 @@ struct floam_odom {
   DevBuf<UpdateStatus> ustat;
   HostBuf<UpdateStatus> h_ustat;
   DevBuf<unsigned long long> prof_bytes;
-  DevBuf<uint32_t> traffic_set;
+  DevBuf<unsigned long long> traffic_set;
   bool prof_bytes_init = false;
   // pose state (host, double)
   Pose odom = pose_identity(), last_odom = pose_identity();
@@ -305,8 +304,7 @@ void odom_update(floam_odom* o, const floam_cloud* edge, const floam_cloud* surf
   const int mE_ub = (int)o->mapE_n, mS_ub = (int)o->mapS_n;   // exact or upper bounds
   if (o->grid_dirty) {
     ProfScope ps(ctx, "grid_build", FLOAM_PROF_CLOUD);
-    grid_build_launch(o->gE, o->gsc, o->mapE.pts.p, o->mapE.count.p, std::max(mE_ub, 1), st);
-    grid_build_launch(o->gS, o->gsc, o->mapS.pts.p, o->mapS.count.p, std::max(mS_ub, 1), st);
+    grid_build_launch(o->gE, o->mapE.pts.p, o->mapE.count.p, mE_ub, o->gS, o->mapS.pts.p, o->mapS.count.p, mS_ub, st);
     o->grid_dirty = false;
   }
   o->lm.reserve(1);
@@ -341,9 +339,9 @@ void odom_update(floam_odom* o, const floam_cloud* edge, const floam_cloud* surf
       geom_launch(o->lm.p, qe, o->gE, o->mapE.pts.p, o->ce, qs, o->gS, o->mapS.pts.p, o->cs, st);
     }
     if (ctx.profile & FLOAM_PROF_KNN_BYTES) {   // replay only: algorithmic bytes of the two launches above
-      knn_traffic_launch(o->lm.p, qe, o->gE, o->ce, 8 * EDGE_FIELDS, o->rank, o->world, o->traffic_set,
+      knn_traffic_launch(o->lm.p, qe, o->gE, o->mapE.pts.p, o->ce, 8 * EDGE_FIELDS, o->rank, o->world, o->traffic_set,
                          o->prof_bytes.p + 0, st);
-      knn_traffic_launch(o->lm.p, qs, o->gS, o->cs, 8 * SURF_FIELDS, o->rank, o->world, o->traffic_set,
+      knn_traffic_launch(o->lm.p, qs, o->gS, o->mapS.pts.p, o->cs, 8 * SURF_FIELDS, o->rank, o->world, o->traffic_set,
                          o->prof_bytes.p + 1, st);
     }
     // iteration zero + at most max_num_iterations = 4 candidates (odomEstimationClass.cpp:102)

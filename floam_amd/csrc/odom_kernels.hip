@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <climits>
 
+#include "grid.hpp"
 #include "odom_kernels.hpp"
 #include "primitives.hpp"
 
@@ -18,153 +19,6 @@ namespace {
 constexpr int kTB = 256;
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 constexpr unsigned kEvalBlocks = 128;   // LM evaluation grid (grid-stride over the device-resident slots)
-// Hash-grid cell edge (m).  Half the 1-m search radius: the 3x3x3 block around the query's cell covers every point
-// closer than one cell edge, so the 5-NN search usually ends there (see knn_group).
-constexpr double kBaseCell = 0.5;
-
-// ===================================================================================== hash grid build
-__global__ void grid_setup(const int* __restrict__ mm, const int* __restrict__ d_m, int shift, unsigned mask,
-                           GridParams* __restrict__ gp) {
-  if (threadIdx.x != 0) return;
-  const int m = *d_m;
-  GridParams p;
-  p.shift = shift;
-  p.mask = mask;
-  p.n = m;
-  if (m <= 0) {
-    p.ox = p.oy = p.oz = 0.0;
-    p.c = kBaseCell;
-    p.nx = p.ny = p.nz = 1;
-    p.cnx = p.cny = p.cnz = 1;
-    *gp = p;
-    return;
-  }
-  double o[3], mx[3];
-  for (int d = 0; d < 3; ++d) {
-    o[d] = floor((double)ord2f(mm[d]));
-    mx[d] = (double)ord2f(mm[3 + d]);
-  }
-  double c = kBaseCell;
-  int n[3];
-  for (;;) {
-    for (int d = 0; d < 3; ++d) n[d] = (int)floor((mx[d] - o[d]) / c) + 1;
-    const double coarse = (double)((n[0] + 1) / 2) * (double)((n[1] + 1) / 2) * (double)((n[2] + 1) / 2);
-    if (coarse < 536870000.0) break;   // (coarse key << 3 | sub-cell) fits 32 bits, fine keys < 2^31
-    c *= 2.0;
-  }
-  p.ox = o[0]; p.oy = o[1]; p.oz = o[2];
-  p.c = c;
-  p.nx = n[0]; p.ny = n[1]; p.nz = n[2];
-  p.cnx = (n[0] + 1) / 2; p.cny = (n[1] + 1) / 2; p.cnz = (n[2] + 1) / 2;
-  *gp = p;
-}
-
-__device__ __forceinline__ int cell_of(double v, double o, double inv_c, int n) {
-  int c = (int)floor((v - o) * inv_c);
-  return c < 0 ? 0 : (c >= n ? n - 1 : c);
-}
-
-__device__ __forceinline__ uint32_t fine_key(const GridParams& p, int fx, int fy, int fz) {
-  return (uint32_t)fx + (uint32_t)p.nx * ((uint32_t)fy + (uint32_t)p.ny * (uint32_t)fz);
-}
-__device__ __forceinline__ uint32_t coarse_key(const GridParams& p, int cx, int cy, int cz) {
-  return (uint32_t)cx + (uint32_t)p.cnx * ((uint32_t)cy + (uint32_t)p.cny * (uint32_t)cz);
-}
-
-// sort key = coarse cell key << 3 | fine sub-cell (x bit 0, y bit 1, z bit 2)
-__global__ __launch_bounds__(kTB) void grid_keys(const PointRec* __restrict__ map, const int* __restrict__ d_m, int m_ub,
-                                                 const GridParams* __restrict__ gp, uint32_t* __restrict__ keys,
-                                                 int* __restrict__ vals, int4* __restrict__ tab,
-                                                 int4* __restrict__ ctab, int tsize) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  // clear the hash tables here (grid_fill inserts only after the sort), saving memset nodes
-  for (int t = i; t < tsize; t += gridDim.x * blockDim.x) {
-    tab[t] = make_int4((int)kEmpty, 0, 0, 0);
-    ctab[t] = make_int4((int)kEmpty, 0, 0, 0);
-  }
-  if (i >= m_ub) return;
-  uint32_t key = kEmpty;
-  if (i < *d_m) {
-    const GridParams p = *gp;
-    const double inv = 1.0 / p.c;
-    const float4 q = *reinterpret_cast<const float4*>(&map[i].x);
-    const int fx = cell_of(q.x, p.ox, inv, p.nx), fy = cell_of(q.y, p.oy, inv, p.ny), fz = cell_of(q.z, p.oz, inv, p.nz);
-    key = (coarse_key(p, fx >> 1, fy >> 1, fz >> 1) << 3) | (uint32_t)((fx & 1) | ((fy & 1) << 1) | ((fz & 1) << 2));
-  }
-  keys[i] = key;
-  vals[i] = i;
-}
-
-__device__ __forceinline__ uint32_t hash_slot(uint32_t key, int shift) { return (key * 0x9E3779B1u) >> shift; }
-
-__device__ __forceinline__ int table_insert(int4* __restrict__ tab, uint32_t key, int start, int shift, unsigned mask) {
-  uint32_t h = hash_slot(key, shift);
-  for (;;) {
-    const uint32_t prev = atomicCAS(reinterpret_cast<uint32_t*>(&tab[h].x), kEmpty, key);
-    if (prev == kEmpty) {
-      tab[h].y = start;
-      return (int)h;
-    }
-    h = (h + 1) & mask;
-  }
-}
-
-__device__ __forceinline__ int table_find(const int4* __restrict__ tab, uint32_t key, int shift, unsigned mask) {
-  uint32_t h = hash_slot(key, shift);
-  for (;;) {
-    const uint32_t k = (uint32_t)tab[h].x;
-    if (k == key) return (int)h;
-    if (k == kEmpty) return -1;
-    h = (h + 1) & mask;
-  }
-}
-
-// cell-sorted copy of the map + the run heads of every fine and coarse cell inserted with their start
-__global__ __launch_bounds__(kTB) void grid_fill(const PointRec* __restrict__ map, const int* __restrict__ d_m,
-                                                 const uint32_t* __restrict__ keys, const int* __restrict__ vals,
-                                                 const GridParams* __restrict__ gp, float4* __restrict__ pts,
-                                                 int4* __restrict__ tab, int4* __restrict__ ctab) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const int m = *d_m;
-  if (i >= m) return;
-  const int j = vals[i];
-  const float4 q = *reinterpret_cast<const float4*>(&map[j].x);
-  pts[i] = make_float4(q.x, q.y, q.z, __int_as_float(j));
-  const uint32_t k = keys[i];
-  const uint32_t kp = i > 0 ? keys[i - 1] : kEmpty;
-  if (i == 0 || kp != k) {
-    const GridParams p = *gp;
-    const uint32_t ck = k >> 3, sub = k & 7u;
-    const int cx = (int)(ck % (uint32_t)p.cnx), cy = (int)((ck / (uint32_t)p.cnx) % (uint32_t)p.cny),
-              cz = (int)(ck / ((uint32_t)p.cnx * (uint32_t)p.cny));
-    table_insert(tab, fine_key(p, 2 * cx + (int)(sub & 1u), 2 * cy + (int)((sub >> 1) & 1u), 2 * cz + (int)(sub >> 2)),
-                 i, p.shift, p.mask);
-    if (i == 0 || (kp >> 3) != ck) table_insert(ctab, ck, i, p.shift, p.mask);
-  }
-}
-
-// run tails complete the counts (the heads' inserts are visible after the kernel boundary)
-__global__ __launch_bounds__(kTB) void grid_counts(const int* __restrict__ d_m, const uint32_t* __restrict__ keys,
-                                                   const GridParams* __restrict__ gp, int4* __restrict__ tab,
-                                                   int4* __restrict__ ctab) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const int m = *d_m;
-  if (i >= m) return;
-  const uint32_t k = keys[i];
-  const uint32_t kn = i + 1 < m ? keys[i + 1] : kEmpty;
-  if (i + 1 < m && kn == k) return;
-  const GridParams p = *gp;
-  const uint32_t ck = k >> 3, sub = k & 7u;
-  const int cx = (int)(ck % (uint32_t)p.cnx), cy = (int)((ck / (uint32_t)p.cnx) % (uint32_t)p.cny),
-            cz = (int)(ck / ((uint32_t)p.cnx * (uint32_t)p.cny));
-  const int h = table_find(tab, fine_key(p, 2 * cx + (int)(sub & 1u), 2 * cy + (int)((sub >> 1) & 1u),
-                                         2 * cz + (int)(sub >> 2)), p.shift, p.mask);
-  if (h >= 0) tab[h].z = i + 1 - tab[h].y;
-  if (i + 1 >= m || (kn >> 3) != ck) {
-    const int hc = table_find(ctab, ck, p.shift, p.mask);
-    if (hc >= 0) ctab[hc].z = i + 1 - ctab[hc].y;
-  }
-}
 
 // ===================================================================================== geometry (fp64)
 // Eigen 3.3 SelfAdjointEigenSolver<Matrix3d>::compute and ColPivHouseholderQR<Matrix<double,5,3>>::solve restated
@@ -481,12 +335,16 @@ __device__ void plane_solve(const double (&A)[5][3], double (&x)[3]) {
 constexpr int kGroupDefault = 16;   // lanes per query (template parameter G below)
 constexpr int kUnrollDefault = 4;   // candidate loads in flight per lane (U)
 
-__device__ __forceinline__ int2 grid_lookup(const int4* __restrict__ tab, uint32_t key, int shift, unsigned mask) {
-  uint32_t h = hash_slot(key, shift);
+// (start, count) of a cell, or (0, 0): fine and coarse entries share the {key, start, count} head (one 16-B load)
+template <typename Cell>
+__device__ __forceinline__ int2 grid_lookup(const Cell* __restrict__ tab, unsigned long long key, int bits,
+                                            unsigned mask) {
+  unsigned h = hash_slot64(key, bits);
   for (;;) {
-    const int4 e = tab[h];
-    if ((uint32_t)e.x == key) return make_int2(e.y, e.z);
-    if ((uint32_t)e.x == kEmpty) return make_int2(0, 0);
+    const int4 e = *reinterpret_cast<const int4*>(&tab[h]);
+    const unsigned long long k = ((unsigned long long)(unsigned)e.y << 32) | (unsigned)e.x;
+    if (k == key) return make_int2(e.z, e.w);
+    if (k == kEmptyKey) return make_int2(0, 0);
     h = (h + 1) & mask;
   }
 }
@@ -550,10 +408,12 @@ struct CorrArgs {
   const PointRec* q;       // downsampled scan points (sensor frame)
   const int* d_n;          // device count
   int n_ub;
-  const GridParams* gp;
-  const float4* gpts;
-  const int4* tab;         // fine cells
-  const int4* ctab;        // coarse cells
+  const float4* gpts;      // the map grouped by cell: {x, y, z, map index bits}
+  const FineCell* fine;
+  const CoarseCell* coarse;
+  int bits;                // table size 1 << bits (both tables)
+  unsigned mask;
+  const PointRec* map;     // the map in its own order (neighbour coordinates by map index)
   double* rec;
   uint8_t* valid;
   float* nnxyz;
@@ -569,28 +429,26 @@ struct CorrArgs {
 constexpr int kMaxStencil = 27;
 
 template <int G, int U, bool COARSE>
-__device__ __forceinline__ void stencil_scan(const CorrArgs& A, const GridParams& p, int x0, int x1, int y0, int y1,
-                                             int z0, int z1, float wx, float wy, float wz, int lane,
-                                             int* __restrict__ s_pre, int* __restrict__ s_start, Top5& t, int& cnt) {
+__device__ __forceinline__ void stencil_scan(const CorrArgs& A, int x0, int x1, int y0, int y1, int z0, int z1,
+                                             float wx, float wy, float wz, int lane, int* __restrict__ s_pre,
+                                             int* __restrict__ s_start, Top5& t, int& cnt) {
   constexpr int P = (kMaxStencil + G - 1) / G;   // cells per lane
-  const int4* __restrict__ tab = COARSE ? A.ctab : A.tab;
-  const int nxr = max(0, x1 - x0 + 1), nyr = max(0, y1 - y0 + 1), nzr = max(0, z1 - z0 + 1);
+  const int nxr = x1 - x0 + 1, nyr = y1 - y0 + 1, nzr = z1 - z0 + 1;
   const int ncell = nxr * nyr * nzr;
   const int per = (ncell + G - 1) / G;
   const int cb = min(ncell, lane * per), ce = min(ncell, cb + per);
-  uint32_t key[P];
-  uint32_t slot[P];
+  unsigned long long key[P];
+  unsigned slot[P];
   int4 e[P];
 #pragma unroll
   for (int j = 0; j < P; ++j) {
     const int c = cb + j;
-    key[j] = kEmpty;
-    e[j] = make_int4((int)kEmpty, 0, 0, 0);
+    key[j] = kEmptyKey;
+    e[j] = make_int4(-1, -1, 0, 0);
     if (c < ce) {
-      const int cx = x0 + c % nxr, cy = y0 + (c / nxr) % nyr, cz = z0 + c / (nxr * nyr);
-      key[j] = COARSE ? coarse_key(p, cx, cy, cz) : fine_key(p, cx, cy, cz);
-      slot[j] = hash_slot(key[j], p.shift);
-      e[j] = tab[slot[j]];
+      key[j] = cell_key(x0 + c % nxr, y0 + (c / nxr) % nyr, z0 + c / (nxr * nyr));
+      slot[j] = hash_slot64(key[j], A.bits);
+      e[j] = COARSE ? *reinterpret_cast<const int4*>(&A.coarse[slot[j]]) : *reinterpret_cast<const int4*>(&A.fine[slot[j]]);
     }
   }
   int local = 0;
@@ -598,15 +456,17 @@ __device__ __forceinline__ void stencil_scan(const CorrArgs& A, const GridParams
   for (int j = 0; j < P; ++j) {
     const int c = cb + j;
     if (c < ce) {
-      while ((uint32_t)e[j].x != key[j] && (uint32_t)e[j].x != kEmpty) {   // collision chain (rare)
-        slot[j] = (slot[j] + 1) & p.mask;
-        e[j] = tab[slot[j]];
+      unsigned long long k = ((unsigned long long)(unsigned)e[j].y << 32) | (unsigned)e[j].x;
+      while (k != key[j] && k != kEmptyKey) {   // collision chain (rare)
+        slot[j] = (slot[j] + 1) & A.mask;
+        e[j] = COARSE ? *reinterpret_cast<const int4*>(&A.coarse[slot[j]])
+                      : *reinterpret_cast<const int4*>(&A.fine[slot[j]]);
+        k = ((unsigned long long)(unsigned)e[j].y << 32) | (unsigned)e[j].x;
       }
-      const int start = (uint32_t)e[j].x == key[j] ? e[j].y : 0;
-      const int count = (uint32_t)e[j].x == key[j] ? e[j].z : 0;
-      s_start[c] = start;
+      const bool hit = k == key[j];
+      s_start[c] = hit ? e[j].z : 0;
       s_pre[c] = local;
-      local += count;
+      local += hit ? e[j].w : 0;
     }
   }
   const int incl = group_incl_scan<G>(local, lane);
@@ -617,14 +477,12 @@ __device__ __forceinline__ void stencil_scan(const CorrArgs& A, const GridParams
   const int tot = __shfl(incl, G - 1, G);
   if (lane == 0) s_pre[ncell] = tot;
   wave_lds_order();
-  int c = 0, c_lo = 0, c_hi = ncell ? s_pre[1] : 0, c_start = ncell ? s_start[0] : 0;   // cell c = [c_lo, c_hi)
+  int c = 0, c_lo = 0, c_hi = s_pre[1], c_start = s_start[0];   // cursor: cell c = [c_lo, c_hi)
   for (int tb = 0; tb < tot; tb += G * U) {
     float4 m[U];
-    int pos[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int tt = tb + u * G + lane;
-      pos[u] = 0;
       if (tt < tot) {
         while (tt >= c_hi) {
           ++c;
@@ -632,8 +490,7 @@ __device__ __forceinline__ void stencil_scan(const CorrArgs& A, const GridParams
           c_hi = s_pre[c + 1];
           c_start = s_start[c];
         }
-        pos[u] = c_start + (tt - c_lo);
-        m[u] = A.gpts[pos[u]];
+        m[u] = A.gpts[c_start + (tt - c_lo)];
       } else {
         m[u] = make_float4(1e30f, 1e30f, 1e30f, 0.0f);
       }
@@ -649,7 +506,7 @@ __device__ __forceinline__ void stencil_scan(const CorrArgs& A, const GridParams
       dd += df * df;
       if (dd < 1.0f) {
         ++cnt;
-        top5_insert(t, ((unsigned long long)__float_as_uint(dd) << 32) | (unsigned)pos[u]);
+        top5_insert(t, ((unsigned long long)__float_as_uint(dd) << 32) | (unsigned)__float_as_int(m[u].w));
       }
     }
   }
@@ -671,12 +528,12 @@ __device__ __forceinline__ void group_merge(Top5& t, int& cnt) {
 
 // Pass 1: exact 5-NN of every query (no fp64 geometry here, so the kernel stays small and at high occupancy).
 // The reference keeps a correspondence iff the 5th-nearest float sq-distance is < 1 (:154, :210), so only map
-// points within 1 m matter.  Stage 1 scans the 3x3x3 FINE cells (edge c = 0.5 m) around the query's cell: every
-// point outside that block is at least c away along some axis, so its float sq-distance is >= c*c (exact: the cell
-// bounds are exact and fl(dx) >= c by monotone rounding); if 5 points with sq-distance < c*c were found they are
-// the exact 5-NN.  Otherwise stage 2 scans the COARSE cells (edge 2c = 1 m) spanning [q-1, q+1] on every axis
-// (<= 3x3x3), which contain every point within 1 m.  Ties at equal float distance go to the lower grid position
-// (FLANN's own order depends on its tree traversal; tie-free data is identical).
+// points within 1 m matter.  Stage 1 scans the 3x3x3 FINE cells (edge 0.5 m) around the query's cell: every point
+// outside that block is at least 0.5 m away along some axis, so its float sq-distance is >= 0.25 (exact: the cell
+// bounds are exact and fl(dx) >= 0.5 by monotone rounding); if 5 points with sq-distance < 0.25 were found they are
+// the exact 5-NN.  Otherwise stage 2 scans the COARSE cells (1 m) spanning [q-1, q+1] on every axis (<= 3x3x3),
+// which contain every point within 1 m.  Ties at equal float distance go to the lower map index (FLANN's own order
+// depends on its tree traversal; tie-free data is identical).
 // Output: valid bit 0 = 5 neighbours within sqd < 1 (their coordinates in nnxyz), bit 1 = stage 2 was needed.
 template <int G, int U>
 __device__ __forceinline__ void knn_group(const LMState* __restrict__ st, const CorrArgs& A, int gid, int ngroups,
@@ -684,9 +541,6 @@ __device__ __forceinline__ void knn_group(const LMState* __restrict__ st, const 
                                           int* __restrict__ s_start) {
   const int n = min(*A.d_n, A.n_ub);
   const int lo = (int)(((long long)n * rank) / world), hi = (int)(((long long)n * (rank + 1)) / world);
-  const GridParams p = *A.gp;
-  const double inv = 1.0 / p.c, cinv = 0.5 / p.c;
-  const float cc2 = (float)(p.c * p.c);
   unsigned long long dsum[6] = {0, 0, 0, 0, 0, 0};
   unsigned long long ts = 0;
   // grid-stride over the queries the device holds (the host only knows an upper bound)
@@ -699,29 +553,29 @@ __device__ __forceinline__ void knn_group(const LMState* __restrict__ st, const 
       const float4 pq = *reinterpret_cast<const float4*>(&A.q[i].x);
       float wx, wy, wz;
       associate_to_map(st->x, pq.x, pq.y, pq.z, wx, wy, wz);   // pointAssociateToMap (:126-135)
-      const double rx = (double)wx - p.ox, ry = (double)wy - p.oy, rz = (double)wz - p.oz;   // exact
-      const int qx = (int)floor(rx * inv), qy = (int)floor(ry * inv), qz = (int)floor(rz * inv);
+      int qx, qy, qz;
+      fine_cell(wx, wy, wz, qx, qy, qz);
       Top5 t;
 #pragma unroll
       for (int k = 0; k < 5; ++k) t.k[k] = ~0ull;
       int cnt = 0;
-      stencil_scan<G, U, false>(A, p, max(0, qx - 1), min(p.nx - 1, qx + 1), max(0, qy - 1), min(p.ny - 1, qy + 1),
-                                max(0, qz - 1), min(p.nz - 1, qz + 1), wx, wy, wz, lane, s_pre, s_start, t, cnt);
+      stencil_scan<G, U, false>(A, qx - 1, qx + 1, qy - 1, qy + 1, qz - 1, qz + 1, wx, wy, wz, lane, s_pre, s_start,
+                                t, cnt);
       group_merge<G>(t, cnt);
-      const bool complete = p.c >= 1.0 || (cnt >= 5 && __uint_as_float((unsigned)(t.k[4] >> 32)) < cc2);
+      const bool complete = cnt >= 5 && __uint_as_float((unsigned)(t.k[4] >> 32)) < 0.25f;
       if (A.dbg) {
         const unsigned long long tn = __builtin_amdgcn_s_memrealtime();
         dsum[0] += tn - ts;
         ts = tn;
       }
-      if (!complete) {   // coarse cells [floor((q-o-1)/2c), floor((q-o+1)/2c)] per axis
+      if (!complete) {   // coarse cells floor(q - 1) .. floor(q + 1) per axis (exact in double)
 #pragma unroll
         for (int k = 0; k < 5; ++k) t.k[k] = ~0ull;
         cnt = 0;
-        stencil_scan<G, U, true>(A, p, max(0, (int)floor((rx - 1.0) * cinv)), min(p.cnx - 1, (int)floor((rx + 1.0) * cinv)),
-                                 max(0, (int)floor((ry - 1.0) * cinv)), min(p.cny - 1, (int)floor((ry + 1.0) * cinv)),
-                                 max(0, (int)floor((rz - 1.0) * cinv)), min(p.cnz - 1, (int)floor((rz + 1.0) * cinv)),
-                                 wx, wy, wz, lane, s_pre, s_start, t, cnt);
+        stencil_scan<G, U, true>(A, (int)floor((double)wx - 1.0), (int)floor((double)wx + 1.0),
+                                 (int)floor((double)wy - 1.0), (int)floor((double)wy + 1.0),
+                                 (int)floor((double)wz - 1.0), (int)floor((double)wz + 1.0), wx, wy, wz, lane, s_pre,
+                                 s_start, t, cnt);
         group_merge<G>(t, cnt);
         flags |= 2;
         if (A.dbg) {
@@ -732,12 +586,12 @@ __device__ __forceinline__ void knn_group(const LMState* __restrict__ st, const 
       }
       if (cnt >= 5) {   // sqd[4] < 1 (:154, :210)
         flags |= 1;
-        if (lane < 5) {   // lane k writes the coordinates of neighbour k (cached: just scanned)
+        if (lane < 5) {   // lane k writes the coordinates of neighbour k
           unsigned long long kk = t.k[0];
 #pragma unroll
           for (int k = 1; k < 5; ++k)
             if (lane == k) kk = t.k[k];
-          const float4 m = A.gpts[(int)(kk & 0xFFFFFFFFull)];
+          const float4 m = *reinterpret_cast<const float4*>(&A.map[(int)(kk & 0xFFFFFFFFull)].x);
           A.nnxyz[(3 * lane + 0) * A.cap + i] = m.x;
           A.nnxyz[(3 * lane + 1) * A.cap + i] = m.y;
           A.nnxyz[(3 * lane + 2) * A.cap + i] = m.z;
@@ -852,49 +706,41 @@ __global__ __launch_bounds__(kTB) void geom_kernel(LMState* __restrict__ st, Cor
 // level 0 — and of the coarse +-1 m stencil for the queries whose bit 1 says they needed stage 2 — level 1), every
 // query is read once (16 B) and writes its flag (1 B) and, if accepted, its record (counted at level 0).  Runs
 // untimed, on a replay, only when profiling.
-__global__ __launch_bounds__(kTB) void knn_traffic(const LMState* __restrict__ st, const PointRec* __restrict__ q,
-                                                   const int* __restrict__ d_n, int n_ub,
-                                                   const GridParams* __restrict__ gp, const int4* __restrict__ tab,
-                                                   const int4* __restrict__ ctab, const uint8_t* __restrict__ valid,
-                                                   int rec_bytes, int rank, int world, int level,
-                                                   uint32_t* __restrict__ set, unsigned set_mask, int set_shift,
+__global__ __launch_bounds__(kTB) void knn_traffic(const LMState* __restrict__ st, CorrArgs A, int rec_bytes, int rank,
+                                                   int world, int level, unsigned long long* __restrict__ set,
+                                                   unsigned set_mask, int set_bits,
                                                    unsigned long long* __restrict__ out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_ub) return;
-  const int n = *d_n;
+  if (i >= A.n_ub) return;
+  const int n = *A.d_n;
   const int lo = (int)(((long long)n * rank) / world), hi = (int)(((long long)n * (rank + 1)) / world);
   if (i < lo || i >= hi) return;
-  const int f = valid[i];
+  const int f = A.valid[i];
   if (level == 1 && !(f & 2)) return;
-  const PointRec pr = q[i];
+  const PointRec pr = A.q[i];
   float wx, wy, wz;
   associate_to_map(st->x, pr.x, pr.y, pr.z, wx, wy, wz);
-  const GridParams p = *gp;
-  const double inv = 1.0 / p.c, cinv = 0.5 / p.c;
-  const double rx = (double)wx - p.ox, ry = (double)wy - p.oy, rz = (double)wz - p.oz;
   unsigned long long bytes = level ? 0ull : 16ull + 1ull + ((f & 1) ? (unsigned long long)rec_bytes : 0ull);
-  int x0, x1, y0, y1, z0, z1, nx, ny, nz;
+  int x0, y0, z0, x1, y1, z1;
   if (level) {
-    x0 = (int)floor((rx - 1.0) * cinv); x1 = (int)floor((rx + 1.0) * cinv);
-    y0 = (int)floor((ry - 1.0) * cinv); y1 = (int)floor((ry + 1.0) * cinv);
-    z0 = (int)floor((rz - 1.0) * cinv); z1 = (int)floor((rz + 1.0) * cinv);
-    nx = p.cnx; ny = p.cny; nz = p.cnz;
+    x0 = (int)floor((double)wx - 1.0); x1 = (int)floor((double)wx + 1.0);
+    y0 = (int)floor((double)wy - 1.0); y1 = (int)floor((double)wy + 1.0);
+    z0 = (int)floor((double)wz - 1.0); z1 = (int)floor((double)wz + 1.0);
   } else {
-    x0 = (int)floor(rx * inv) - 1; x1 = x0 + 2;
-    y0 = (int)floor(ry * inv) - 1; y1 = y0 + 2;
-    z0 = (int)floor(rz * inv) - 1; z1 = z0 + 2;
-    nx = p.nx; ny = p.ny; nz = p.nz;
+    fine_cell(wx, wy, wz, x0, y0, z0);
+    --x0; --y0; --z0;
+    x1 = x0 + 2; y1 = y0 + 2; z1 = z0 + 2;
   }
-  for (int z = max(0, z0); z <= min(nz - 1, z1); ++z)
-    for (int y = max(0, y0); y <= min(ny - 1, y1); ++y)
-      for (int x = max(0, x0); x <= min(nx - 1, x1); ++x) {
-        const uint32_t k = level ? coarse_key(p, x, y, z) : fine_key(p, x, y, z);
-        const int cnt = grid_lookup(level ? ctab : tab, k, p.shift, p.mask).y;
+  for (int z = z0; z <= z1; ++z)
+    for (int y = y0; y <= y1; ++y)
+      for (int x = x0; x <= x1; ++x) {
+        const unsigned long long k = cell_key(x, y, z);
+        const int cnt = level ? grid_lookup(A.coarse, k, A.bits, A.mask).y : grid_lookup(A.fine, k, A.bits, A.mask).y;
         if (cnt == 0) continue;
-        uint32_t h = hash_slot(k, set_shift);
+        unsigned h = hash_slot64(k, set_bits);
         for (;;) {
-          const uint32_t prev = atomicCAS(&set[h], kEmpty, k);
-          if (prev == kEmpty) { bytes += 16ull * (unsigned long long)cnt; break; }
+          const unsigned long long prev = atomicCAS(&set[h], kEmptyKey, k);
+          if (prev == kEmptyKey) { bytes += 16ull * (unsigned long long)cnt; break; }
           if (prev == k) break;
           h = (h + 1) & set_mask;
         }
@@ -1480,33 +1326,6 @@ __global__ __launch_bounds__(kTB) void lm_reduce(const double* __restrict__ part
 }  // namespace
 
 // ===================================================================================== launchers
-void grid_build_launch(Grid& g, GridScratch& sc, const PointRec* map, const int* d_m, int m_ub, hipStream_t st) {
-  g.params.reserve(1);
-  sc.mm.reserve(8);
-  const int ub = m_ub > 0 ? m_ub : 1;
-  sc.s.reserve(ub);
-  g.pts.reserve(ub);
-  int tsize = 1024, shift = 32 - 10;
-  while (tsize < 2 * ub) { tsize <<= 1; --shift; }
-  g.tab.reserve(tsize);
-  g.ctab.reserve(tsize);
-  g.table_size = tsize;
-  g.shift = shift;
-  minmax_launch(map, d_m, ub, sc.mm.p, st);
-  hipLaunchKernelGGL(grid_setup, dim3(1), dim3(64), 0, st, sc.mm.p, d_m, shift, (unsigned)(tsize - 1), g.params.p);
-  FLOAM_LAUNCH_CHECK();
-  const unsigned gb = div_up(ub, kTB);
-  hipLaunchKernelGGL(grid_keys, dim3(gb), dim3(kTB), 0, st, map, d_m, ub, g.params.p, sc.s.k0.p, sc.s.v0.p, g.tab.p,
-                     g.ctab.p, tsize);
-  FLOAM_LAUNCH_CHECK();
-  sort_pairs_u32(sc.s.temp.p, sc.s.temp_bytes, sc.s.k0.p, sc.s.k1.p, sc.s.v0.p, sc.s.v1.p, ub, 32, st);
-  hipLaunchKernelGGL(grid_fill, dim3(gb), dim3(kTB), 0, st, map, d_m, sc.s.k1.p, sc.s.v1.p, g.params.p, g.pts.p,
-                     g.tab.p, g.ctab.p);
-  FLOAM_LAUNCH_CHECK();
-  hipLaunchKernelGGL(grid_counts, dim3(gb), dim3(kTB), 0, st, d_m, sc.s.k1.p, g.params.p, g.tab.p, g.ctab.p);
-  FLOAM_LAUNCH_CHECK();
-}
-
 void lm_init_launch(LMState* d_st, const double* x0, hipStream_t st) {
   X7 x{};
   if (x0) {
@@ -1546,12 +1365,10 @@ static void corr_args(const QuerySet& qe, const Grid& ge, const PointRec* mapE, 
                       CorrArgs& S) {
   ce.reserve(std::max(qe.n_ub, 1), EDGE_FIELDS);
   cs.reserve(std::max(qs.n_ub, 1), SURF_FIELDS);
-  (void)mapE;
-  (void)mapS;
-  E = CorrArgs{qe.pts, qe.d_n, qe.n_ub, ge.params.p, ge.pts.p, ge.tab.p, ge.ctab.p, ce.rec.p, ce.valid.p, ce.nnxyz.p,
-               ce.cap, dbg};
-  S = CorrArgs{qs.pts, qs.d_n, qs.n_ub, gs.params.p, gs.pts.p, gs.tab.p, gs.ctab.p, cs.rec.p, cs.valid.p, cs.nnxyz.p,
-               cs.cap, dbg ? dbg + 8 : nullptr};
+  E = CorrArgs{qe.pts, qe.d_n, qe.n_ub, ge.pts.p, ge.fine.p, ge.coarse.p, ge.bits, ge.mask, mapE, ce.rec.p,
+               ce.valid.p, ce.nnxyz.p, ce.cap, dbg};
+  S = CorrArgs{qs.pts, qs.d_n, qs.n_ub, gs.pts.p, gs.fine.p, gs.coarse.p, gs.bits, gs.mask, mapS, cs.rec.p,
+               cs.valid.p, cs.nnxyz.p, cs.cap, dbg ? dbg + 8 : nullptr};
 }
 
 template <int G, int U>
@@ -1594,17 +1411,19 @@ void geom_launch(LMState* d_st, const QuerySet& qe, const Grid& ge, const PointR
   FLOAM_LAUNCH_CHECK();
 }
 
-void knn_traffic_launch(const LMState* d_st, const QuerySet& q, const Grid& g, const CorrSet& c, int rec_bytes,
-                        int rank, int world, DevBuf<uint32_t>& set, unsigned long long* d_bytes, hipStream_t st) {
+void knn_traffic_launch(const LMState* d_st, const QuerySet& q, const Grid& g, const PointRec* map, CorrSet& c,
+                        int rec_bytes, int rank, int world, DevBuf<unsigned long long>& set,
+                        unsigned long long* d_bytes, hipStream_t st) {
   if (q.n_ub <= 0) return;
-  int size = 1024, shift = 22;
-  while (size < 64 * q.n_ub) { size <<= 1; --shift; }   // distinct occupied cells scanned (<= 27 per query)
-  set.reserve(size);
+  int bits = 10;
+  while ((1 << bits) < 64 * q.n_ub) ++bits;   // distinct occupied cells scanned (<= 27 per query)
+  set.reserve((size_t)1 << bits);
+  CorrArgs A, B;
+  corr_args(q, g, map, c, q, g, map, c, nullptr, A, B);
   for (int level = 0; level < 2; ++level) {
-    FLOAM_HIP(hipMemsetAsync(set.p, 0xFF, sizeof(uint32_t) * size, st));
-    hipLaunchKernelGGL(knn_traffic, dim3(div_up(q.n_ub, kTB)), dim3(kTB), 0, st, d_st, q.pts, q.d_n, q.n_ub,
-                       g.params.p, g.tab.p, g.ctab.p, c.valid.p, rec_bytes, rank, world, level, set.p,
-                       (unsigned)(size - 1), shift, d_bytes);
+    FLOAM_HIP(hipMemsetAsync(set.p, 0xFF, sizeof(unsigned long long) << bits, st));
+    hipLaunchKernelGGL(knn_traffic, dim3(div_up(q.n_ub, kTB)), dim3(kTB), 0, st, d_st, A, rec_bytes, rank, world,
+                       level, set.p, (1u << bits) - 1u, bits, d_bytes);
     FLOAM_LAUNCH_CHECK();
   }
 }

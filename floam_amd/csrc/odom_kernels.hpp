@@ -5,36 +5,39 @@
 namespace floam {
 
 // ----------------------------------------------------------------------------------------- hash grid
-// Map points bucketed into a two-level cubic grid over the map's bounding box: fine cells of edge c (0.5 m, doubled
-// only if the bbox would overflow 2^29 coarse cells) nested 2x2x2 in coarse cells of edge 2c.  The points are sorted
-// by (coarse cell, fine sub-cell) so every fine and every coarse cell is a contiguous run of `pts` (float4 {x, y, z,
-// map index bits}); two open-addressing tables map cell keys to (start, count).  Exact replacement of the 5-NN
-// KD-tree under the reference's sqd[4] < 1 gate (knn_group in odom_kernels.hip).
-struct GridParams {
-  double ox, oy, oz;     // origin = floor(bbox min)
-  double c;              // fine cell edge (0.5, 1, 2, ... m); coarse cells are 2c
-  int nx, ny, nz;        // fine cells per axis
-  int cnx, cny, cnz;     // coarse cells per axis
-  int shift;             // hash: (key * 0x9E3779B1) >> shift (both tables)
-  unsigned mask;
-  int n;                 // map points
+// Map points bucketed into a two-level cubic grid with ABSOLUTE cell coordinates (no bounding box): fine cells of
+// edge kFineCell = 0.5 m nested 2x2x2 in coarse cells of 1 m.  Built without sorting (grid.hip): points are counted
+// per coarse cell and fine sub-cell (atomics into an open-addressing table of coarse cells), every coarse cell gets
+// a contiguous range of `pts` (block-aggregated bump allocation, fine sub-cells consecutive inside it), and the
+// points are scattered into place.  A fine table and the coarse table map 64-bit cell keys to (start, count).
+// Layout order inside a cell is not deterministic; the kNN breaks distance ties by map index, so results are.
+// Exact replacement of the 5-NN KD-tree under the reference's sqd[4] < 1 gate (knn_group).
+constexpr double kFineCell = 0.5;
+
+struct FineCell {            // 16 B: one probe = one dwordx4 load
+  unsigned long long key;    // kEmptyKey = empty
+  int start, count;
 };
+struct CoarseCell {          // 48 B; the kNN reads the first 16 B
+  unsigned long long key;
+  int start, total;
+  int sub[8];                // points per fine sub-cell (x bit 0, y bit 1, z bit 2)
+};
+constexpr unsigned long long kEmptyKey = ~0ull;
 
 struct Grid {
-  DevBuf<GridParams> params;
-  DevBuf<float4> pts;      // sorted by (coarse cell, fine sub-cell)
-  DevBuf<int4> tab;        // fine cells:   {key, start, count, 0}; key 0xFFFFFFFF = empty (one 16-B probe)
-  DevBuf<int4> ctab;       // coarse cells: same layout
-  int table_size = 0;
-  int shift = 0;
+  DevBuf<float4> pts;        // {x, y, z, map index bits}, grouped by coarse cell then fine sub-cell
+  DevBuf<FineCell> fine;
+  DevBuf<CoarseCell> coarse;
+  DevBuf<uint2> where;       // per map point: coarse slot, sub-cell << 28 | rank in the sub-cell
+  DevBuf<int> cursor;        // bump allocator
+  int bits = 0;              // table size = 1 << bits (both tables)
+  unsigned mask = 0;
 };
 
-struct GridScratch {
-  SortScratch s;
-  DevBuf<int> mm;
-};
-
-void grid_build_launch(Grid& g, GridScratch& sc, const PointRec* map, const int* d_m, int m_ub, hipStream_t st);
+// Rebuild the grids of both local maps (corner and surf) in four launches.
+void grid_build_launch(Grid& gE, const PointRec* mapE, const int* d_mE, int mE_ub, Grid& gS, const PointRec* mapS,
+                       const int* d_mS, int mS_ub, hipStream_t st);
 
 // ----------------------------------------------------------------------------------------- correspondences
 // Edge record (EdgeAnalyticCostFunction inputs): cp (sensor point), a, b.  Surf: cp, unit normal n, d.
@@ -108,9 +111,10 @@ void knn_launch(const LMState* d_st, const QuerySet& qe, const Grid& ge, const P
                 const int* d_ms, int rank, int world, hipStream_t st, unsigned long long* dbg = nullptr);
 void geom_launch(LMState* d_st, const QuerySet& qe, const Grid& ge, const PointRec* mapE, CorrSet& ce,
                  const QuerySet& qs, const Grid& gs, const PointRec* mapS, CorrSet& cs, hipStream_t st);
-// algorithmic bytes of the correspondence launch just issued (profiling only), accumulated into *d_bytes
-void knn_traffic_launch(const LMState* d_st, const QuerySet& q, const Grid& g, const CorrSet& c, int rec_bytes,
-                        int rank, int world, DevBuf<uint32_t>& set, unsigned long long* d_bytes, hipStream_t st);
+// algorithmic bytes of the correspondence pass just issued (profiling only), accumulated into *d_bytes
+void knn_traffic_launch(const LMState* d_st, const QuerySet& q, const Grid& g, const PointRec* map, CorrSet& c,
+                        int rec_bytes, int rank, int world, DevBuf<unsigned long long>& set,
+                        unsigned long long* d_bytes, hipStream_t st);
 // one LM evaluation (at x in phase 0, else at cand): block partial sums of (cost, J^T J, J^T r, count)
 int lm_eval_launch(const LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const CorrSet& cs,
                    const int* d_ns, int ns_ub, bool huber, double* partials, hipStream_t st);
