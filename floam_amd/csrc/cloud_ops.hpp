@@ -26,22 +26,6 @@ struct SortScratch {
   void reserve(int n);
 };
 
-struct VoxelScratch {
-  SortScratch s;
-  DevBuf<int> mm;     // 6 ordered-int min/max + mode flag
-};
-
-// out = pcl::VoxelGrid(in[0, *d_n)) with cubic leaf (PCL 1.8.1 semantics, stable within-voxel order).
-// n_ub: host upper bound on *d_n.  Writes *d_out_count.  out must hold n_ub points.
-void voxel_launch(VoxelScratch& sc, const PointRec* in, const int* d_n, int n_ub, float leaf, PointRec* out,
-                  int* d_out_count, hipStream_t st);
-
-// out = pcl::CropBox([old[0,*d_old) ; associate(pose, neu[0,*d_new))], t +- 100) — the map half of
-// addPointsToMap (src/odomEstimationClass.cpp:253-287).  out must hold old_ub + new_ub points.
-void crop_concat_launch(SortScratch& sc, const PointRec* old, const int* d_old, int old_ub, const PointRec* neu,
-                        const int* d_new, int new_ub, const double* d_pose, PointRec* out, int* d_out_count,
-                        hipStream_t st);
-
 // dmapping::CompensateVelocity (src/dataHandler.cpp:82-92), in place
 void compensate_velocity_launch(PointRec* pts, const int* d_n, int n_ub, double vx, double vy, double vz,
                                 hipStream_t st);
@@ -50,9 +34,6 @@ void compensate_velocity_launch(PointRec* pts, const int* d_n, int n_ub, double 
 // xyzi: VelToIntensityCopy semantics (src/odomEstimationClass.cpp:308-318): keep x, y, z, intensity only.
 void append_launch(PointRec* dst, int* d_dst_count, const PointRec* src, const int* d_src_count, int src_ub,
                    bool xyzi, hipStream_t st);
-
-// ordered-int min/max of x,y,z into d_mm[0..5] (min x,y,z, max x,y,z)
-void minmax_launch(const PointRec* in, const int* d_n, int n_ub, int* d_mm, hipStream_t st);
 
 __device__ __forceinline__ int f2ord(float f) {
   const int i = __float_as_int(f);

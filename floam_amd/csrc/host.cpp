@@ -27,6 +27,7 @@
 #include "floam_common.hpp"
 #include "odom_kernels.hpp"
 #include "pose.hpp"
+#include "voxel.hpp"
 
 namespace floam {
 
@@ -155,6 +156,14 @@ static void cloud_init(floam_cloud* c, int device, size_t capacity) {
   if (capacity) cloud_reserve(c, capacity, 0, ctx.stream);
 }
 
+// exchange the device storage of two clouds (stream-ordered users see the new contents after the swap)
+static void cloud_swap(floam_cloud* a, floam_cloud* b) {
+  std::swap(a->pts.p, b->pts.p);
+  std::swap(a->pts.cap, b->pts.cap);
+  std::swap(a->count.p, b->count.p);
+  std::swap(a->count.cap, b->count.cap);
+}
+
 static bool g_keyframe_first = true;   // KeyFrameUpdate's function-static `first` (odomEstimationClass.cpp:323, Q6)
 
 }  // namespace floam
@@ -178,12 +187,13 @@ struct floam_odom {
   float leafE = 0.4f, leafS = 0.8f;
   // local map (device) and host-known exact sizes (valid as of the last synchronisation)
   floam_cloud mapE, mapS;
+  floam_cloud mapE_next, mapS_next;   // double buffers: the map update writes here, then the two swap
   size_t mapE_n = 0, mapS_n = 0;
   bool maps_exact = true;
   // scratch
   DevBuf<PointRec> dE, dS, tmp;
   DevBuf<int> cnt;   // [0] dE count [1] dS count [2] tmp count
-  VoxelScratch vs;
+  VoxelScratch2 vs;
   Grid gE, gS;
   bool grid_dirty = true;
   CorrSet ce, cs;
@@ -297,9 +307,13 @@ void odom_update(floam_odom* o, const floam_cloud* edge, const floam_cloud* surf
   o->cnt.reserve(4);
   {
     ProfScope ps(ctx, "voxel_downsample", FLOAM_PROF_CLOUD);
-    // VelToIntensityCopy + downSamplingToMap (:53-54, :75, :137-142)
-    voxel_launch(o->vs, edge->pts.p, edge->count.p, ne_ub, o->leafE, o->dE.p, o->cnt.p + 0, st);
-    voxel_launch(o->vs, surf->pts.p, surf->count.p, ns_ub, o->leafS, o->dS.p, o->cnt.p + 1, st);
+    // VelToIntensityCopy + downSamplingToMap (:53-54, :75, :137-142): both grids in one pipeline
+    VoxelJob je, js;
+    je.part0 = edge->pts.p; je.d_n0 = edge->count.p; je.n0_ub = ne_ub; je.leaf = o->leafE;
+    je.out = o->dE.p; je.d_out = o->cnt.p + 0;
+    js.part0 = surf->pts.p; js.d_n0 = surf->count.p; js.n0_ub = ns_ub; js.leaf = o->leafS;
+    js.out = o->dS.p; js.d_out = o->cnt.p + 1;
+    voxel2_launch(o->vs, je, js, st);
   }
   const int mE_ub = (int)o->mapE_n, mS_ub = (int)o->mapS_n;   // exact or upper bounds
   if (o->grid_dirty) {
@@ -410,17 +424,19 @@ void odom_update(floam_odom* o, const floam_cloud* edge, const floam_cloud* surf
       if (!gate) {   // lm->x still holds the prediction we uploaded: identical to parameters
       }
       const int ubS = (int)o->mapS_n + nSd, ubE = (int)o->mapE_n + nEd;
-      const int ub = std::max(std::max(ubS, ubE), 1);
-      o->tmp.reserve(ub);
-      o->cnt.reserve(4);
-      cloud_reserve(&o->mapS, std::max(ubS, 1), o->mapS_n, st);
-      cloud_reserve(&o->mapE, std::max(ubE, 1), o->mapE_n, st);
-      crop_concat_launch(o->vs.s, o->mapS.pts.p, o->mapS.count.p, (int)o->mapS_n, o->dS.p, o->cnt.p + 1, nSd,
-                         o->lm.p->x, o->tmp.p, o->cnt.p + 2, st);
-      voxel_launch(o->vs, o->tmp.p, o->cnt.p + 2, std::max(ubS, 1), o->leafS, o->mapS.pts.p, o->mapS.count.p, st);
-      crop_concat_launch(o->vs.s, o->mapE.pts.p, o->mapE.count.p, (int)o->mapE_n, o->dE.p, o->cnt.p + 0, nEd,
-                         o->lm.p->x, o->tmp.p, o->cnt.p + 2, st);
-      voxel_launch(o->vs, o->tmp.p, o->cnt.p + 2, std::max(ubE, 1), o->leafE, o->mapE.pts.p, o->mapE.count.p, st);
+      cloud_reserve(&o->mapS_next, std::max(ubS, 1), 0, st);
+      cloud_reserve(&o->mapE_next, std::max(ubE, 1), 0, st);
+      // [map ; pointAssociateToMap(downsampled scan)] -> CropBox -> VoxelGrid, both maps in one pipeline
+      VoxelJob je, js;
+      je.part0 = o->mapE.pts.p; je.d_n0 = o->mapE.count.p; je.n0_ub = (int)o->mapE_n;
+      je.part1 = o->dE.p; je.d_n1 = o->cnt.p + 0; je.n1_ub = nEd;
+      je.pose = o->lm.p->x; je.leaf = o->leafE; je.out = o->mapE_next.pts.p; je.d_out = o->mapE_next.count.p;
+      js.part0 = o->mapS.pts.p; js.d_n0 = o->mapS.count.p; js.n0_ub = (int)o->mapS_n;
+      js.part1 = o->dS.p; js.d_n1 = o->cnt.p + 1; js.n1_ub = nSd;
+      js.pose = o->lm.p->x; js.leaf = o->leafS; js.out = o->mapS_next.pts.p; js.d_out = o->mapS_next.count.p;
+      voxel2_launch(o->vs, je, js, st);
+      cloud_swap(&o->mapE, &o->mapE_next);
+      cloud_swap(&o->mapS, &o->mapS_next);
       o->mapS_n = (size_t)ubS;   // upper bounds until the next synchronisation
       o->mapE_n = (size_t)ubE;
       o->mapS.host_count_valid = false;
@@ -645,6 +661,8 @@ floam_status floam_odom_create(const floam_lidar_params* p, double map_resolutio
     o->leafS = (float)(map_resolution * 2);    // downSizeFilterSurf.setLeafSize(2r) (:14)
     cloud_init(&o->mapE, device, 1024);
     cloud_init(&o->mapS, device, 1024);
+    cloud_init(&o->mapE_next, device, 1024);
+    cloud_init(&o->mapS_next, device, 1024);
     o->cnt.reserve(4);
     DeviceCtx& ctx = ctx_for(device);
     FLOAM_HIP(hipMemsetAsync(o->cnt.p, 0, sizeof(int) * 4, ctx.stream));

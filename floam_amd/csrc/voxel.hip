@@ -1,0 +1,298 @@
+// pcl::VoxelGrid (PCL 1.8.1 semantics) for two independent clouds per call, optionally fused with the map-side
+// half of addPointsToMap (transform + concatenation + CropBox).
+//
+// Reference call sites: src/odomEstimationClass.cpp:137-142 (downSamplingToMap: edge leaf r, surf leaf 2r, both in
+// one updatePointsToMap call) and :253-294 (addPointsToMap: transform the downsampled scan into the map frame,
+// append it to the map, CropBox [t-100, t+100], VoxelGrid — for the corner and the surf map).
+//
+// PCL's VoxelGrid: min/max over the input, leaf index ijk = floor(p * inv) - min_b (float), idx = i + j*dx + k*dx*dy,
+// input returned unchanged if dx*dy*dz > INT_MAX, std::sort of (idx, point) pairs, one centroid (float sums of
+// x, y, z, intensity in sorted order / float(count)) per voxel in ascending idx.  Here the within-voxel order is
+// the stable (input) order; PCL's unstable std::sort can only change a centroid's float summation order.
+//
+// Launches per call (both clouds): vox_minmax (block partials), vox_keys (reduce partials -> 32-bit keys with the
+// cloud in bit 31, dropped points -> 0xFFFFFFFF), one stable radix sort (rocPRIM), vox_compact (run heads +
+// single-pass decoupled-lookback positions for both clouds at once + centroids).
+#include <cfloat>
+#include <climits>
+
+#include "cloud_ops.hpp"
+#include "lookback.hpp"
+#include "primitives.hpp"
+#include "voxel.hpp"
+
+namespace floam {
+
+namespace {
+constexpr int kTB = 256;
+constexpr int kMinMaxBlocks = 64;       // partials per cloud
+constexpr int kPerThread = 4;
+constexpr int kTile = kTB * kPerThread;   // elements per compaction tile
+
+struct VoxelJobDev {
+  const PointRec* part0;
+  const int* d_n0;
+  int n0_ub;
+  const PointRec* part1;
+  const int* d_n1;
+  int n1_ub;
+  const double* pose;   // non-null: part1 -> map frame, CropBox(t +- 100) over both parts
+  float inv;
+  PointRec* out;
+  int* d_out;
+  int base;             // first element of this cloud in the combined key array
+};
+
+// element i of the (virtual) concatenation; false if it does not exist or is cropped away
+__device__ __forceinline__ bool vox_fetch(const VoxelJobDev& J, int n0, int n1, int i, PointRec& p) {
+  if (i < n0) {
+    p = J.part0[i];
+  } else if (i < n0 + n1) {
+    const PointRec s = J.part1[i - n0];
+    if (J.pose) {   // pointAssociateToMap (:126-135) into an XYZI record
+      float x, y, z;
+      associate_to_map(J.pose, s.x, s.y, s.z, x, y, z);
+      p.x = x; p.y = y; p.z = z; p.pad0 = 1.0f;
+      p.intensity = s.intensity;
+      p.ring = 0; p.pad1 = 0; p.time = 0.0f; p.pad2 = 0.0f;
+    } else {
+      p = s;
+    }
+  } else {
+    return false;
+  }
+  if (J.pose) {   // CropBox min/max = Vector4f(t -+ 100) (double -> float), inclusive (:270-287)
+    const double* t = J.pose + 4;
+    const float mnx = (float)(t[0] - 100), mny = (float)(t[1] - 100), mnz = (float)(t[2] - 100);
+    const float mxx = (float)(t[0] + 100), mxy = (float)(t[1] + 100), mxz = (float)(t[2] + 100);
+    if (p.x < mnx || p.y < mny || p.z < mnz || p.x > mxx || p.y > mxy || p.z > mxz) return false;
+  }
+  return true;
+}
+
+__global__ __launch_bounds__(kTB) void vox_minmax(VoxelJobDev A, VoxelJobDev B, float* __restrict__ partials) {
+  const VoxelJobDev& J = blockIdx.y == 0 ? A : B;
+  const int n0 = *J.d_n0, n1 = J.d_n1 ? *J.d_n1 : 0;
+  float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n0 + n1; i += gridDim.x * blockDim.x) {
+    PointRec p;
+    if (!vox_fetch(J, n0, n1, i, p)) continue;
+    mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
+    mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      mn[d] = fminf(mn[d], __shfl_down(mn[d], o, 64));
+      mx[d] = fmaxf(mx[d], __shfl_down(mx[d], o, 64));
+    }
+  __shared__ float s[6][kTB / 64];
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0)
+    for (int d = 0; d < 3; ++d) { s[d][w] = mn[d]; s[3 + d][w] = mx[d]; }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    float v = s[threadIdx.x][0];
+    for (int k = 1; k < kTB / 64; ++k) v = threadIdx.x < 3 ? fminf(v, s[threadIdx.x][k]) : fmaxf(v, s[threadIdx.x][k]);
+    partials[(blockIdx.y * kMinMaxBlocks + blockIdx.x) * 6 + threadIdx.x] = v;
+  }
+}
+
+struct VoxelGeom {
+  int min_b[3];
+  int divb_mul[3];
+  bool overflow;
+};
+
+// PCL 1.8.1 VoxelGrid::applyFilter index arithmetic (float leaf inverse, int min/max boxes)
+__device__ __forceinline__ VoxelGeom voxel_geom(const float (&mn)[3], const float (&mx)[3], float inv) {
+  VoxelGeom g;
+  const long long dx = (long long)((mx[0] - mn[0]) * inv) + 1;
+  const long long dy = (long long)((mx[1] - mn[1]) * inv) + 1;
+  const long long dz = (long long)((mx[2] - mn[2]) * inv) + 1;
+  g.overflow = (dx * dy * dz) > (long long)INT_MAX;
+  int div_b[3];
+  for (int d = 0; d < 3; ++d) {
+    g.min_b[d] = (int)floorf(mn[d] * inv);
+    const int max_b = (int)floorf(mx[d] * inv);
+    div_b[d] = max_b - g.min_b[d] + 1;
+  }
+  g.divb_mul[0] = 1;
+  g.divb_mul[1] = div_b[0];
+  g.divb_mul[2] = div_b[0] * div_b[1];
+  return g;
+}
+
+__global__ __launch_bounds__(kTB) void vox_keys(VoxelJobDev A, VoxelJobDev B, const float* __restrict__ partials,
+                                                uint32_t* __restrict__ keys, int* __restrict__ vals,
+                                                int* __restrict__ overflow, unsigned long long* __restrict__ status,
+                                                int ntiles, unsigned* __restrict__ ticket) {
+  const int job = blockIdx.y;
+  const VoxelJobDev& J = job == 0 ? A : B;
+  __shared__ float s_mm[6];
+  if (threadIdx.x < 6) {
+    const bool is_min = threadIdx.x < 3;
+    float v = is_min ? FLT_MAX : -FLT_MAX;
+    for (int b = 0; b < kMinMaxBlocks; ++b) {
+      const float u = partials[(job * kMinMaxBlocks + b) * 6 + threadIdx.x];
+      v = is_min ? fminf(v, u) : fmaxf(v, u);
+    }
+    s_mm[threadIdx.x] = v;
+  }
+  // lookback state of the compaction launch that follows this one
+  for (int t = (job * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x; t < ntiles; t += 2 * gridDim.x * blockDim.x)
+    status[t] = 0ull;
+  if (job == 0 && blockIdx.x == 0 && threadIdx.x == 0) *ticket = 0u;
+  __syncthreads();
+  const float mn[3] = {s_mm[0], s_mm[1], s_mm[2]}, mx[3] = {s_mm[3], s_mm[4], s_mm[5]};
+  const VoxelGeom g = voxel_geom(mn, mx, J.inv);
+  if (blockIdx.x == 0 && threadIdx.x == 0) overflow[job] = g.overflow ? 1 : 0;
+  const int n0 = *J.d_n0, n1 = J.d_n1 ? *J.d_n1 : 0;
+  const int U = J.n0_ub + J.n1_ub;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < U; i += gridDim.x * blockDim.x) {
+    uint32_t key = 0xFFFFFFFFu;
+    PointRec p;
+    if (vox_fetch(J, n0, n1, i, p)) {
+      uint32_t idx;
+      if (g.overflow) {
+        idx = (uint32_t)i;   // output = input unchanged (Q9): identity order, one "voxel" per point
+      } else {
+        const int ijk0 = (int)(floorf(p.x * J.inv) - (float)g.min_b[0]);
+        const int ijk1 = (int)(floorf(p.y * J.inv) - (float)g.min_b[1]);
+        const int ijk2 = (int)(floorf(p.z * J.inv) - (float)g.min_b[2]);
+        idx = (uint32_t)(ijk0 * g.divb_mul[0] + ijk1 * g.divb_mul[1] + ijk2 * g.divb_mul[2]);
+      }
+      key = ((uint32_t)job << 31) | idx;
+    }
+    keys[J.base + i] = key;
+    vals[J.base + i] = i;
+  }
+}
+
+// Run heads of the sorted keys -> output slot per cloud (decoupled lookback over tiles) -> centroid of the run.
+__global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B, const uint32_t* __restrict__ keys,
+                                                   const int* __restrict__ vals, const int* __restrict__ overflow,
+                                                   int total, unsigned long long* __restrict__ status,
+                                                   unsigned* __restrict__ ticket) {
+  const int tile = lookback_ticket(ticket);
+  const int ntiles = (int)gridDim.x;
+  const int t0 = tile * kTile;
+  __shared__ uint32_t s_key[kTile + 1];
+  for (int k = threadIdx.x; k <= kTile; k += blockDim.x) {
+    const int i = t0 - 1 + k;
+    s_key[k] = (i >= 0 && i < total) ? keys[i] : 0xFFFFFFFFu;
+  }
+  __syncthreads();
+  // heads in this thread's 4 consecutive elements
+  int cnt[2] = {0, 0};
+  unsigned headmask = 0;
+#pragma unroll
+  for (int u = 0; u < kPerThread; ++u) {
+    const int k = threadIdx.x * kPerThread + u;   // element t0 + k, previous key at s_key[k]
+    const uint32_t key = s_key[k + 1];
+    if (key != 0xFFFFFFFFu && (t0 + k == 0 || key != s_key[k])) {
+      headmask |= 1u << u;
+      ++cnt[key >> 31];
+    }
+  }
+  // block exclusive scan of (cnt0, cnt1)
+  __shared__ int s_w[2][kTB / 64];
+  int inc[2];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    int v = cnt[c];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int x = __shfl_up(v, o, 64);
+      if (lane >= o) v += x;
+    }
+    inc[c] = v;
+    if (lane == 63) s_w[c][w] = v;
+  }
+  __syncthreads();
+  int wb[2] = {0, 0}, agg[2] = {0, 0};
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int k = 0; k < kTB / 64; ++k) {
+      if (k < w) wb[c] += s_w[c][k];
+      agg[c] += s_w[c][k];
+    }
+  const Prefix2 pre = lookback_prefix(status, tile, Prefix2{agg[0], agg[1]});
+  if (pre.a < 0) {   // lookback timed out (never expected): report through the output counts
+    if (threadIdx.x == 0) { *A.d_out = -1; *B.d_out = -1; }
+    return;
+  }
+  int pos[2] = {pre.a + wb[0] + inc[0] - cnt[0], pre.b + wb[1] + inc[1] - cnt[1]};
+  const int ovf[2] = {overflow[0], overflow[1]};
+#pragma unroll
+  for (int u = 0; u < kPerThread; ++u) {
+    if (!(headmask & (1u << u))) continue;
+    const int k = threadIdx.x * kPerThread + u;
+    const int i = t0 + k;
+    const uint32_t key = s_key[k + 1];
+    const int job = (int)(key >> 31);
+    const VoxelJobDev& J = job == 0 ? A : B;
+    const int n0 = *J.d_n0, n1 = J.d_n1 ? *J.d_n1 : 0;
+    PointRec f;
+    vox_fetch(J, n0, n1, vals[i], f);
+    PointRec o;
+    if (ovf[job]) {
+      o = f;
+    } else {
+      float c0 = f.x, c1 = f.y, c2 = f.z, c3 = f.intensity;
+      int j = i + 1;
+      for (; j < total; ++j) {
+        const int kj = j - t0;
+        const uint32_t kk = kj <= kTile - 1 ? s_key[kj + 1] : keys[j];
+        if (kk != key) break;
+        PointRec p;
+        vox_fetch(J, n0, n1, vals[j], p);
+        c0 += p.x; c1 += p.y; c2 += p.z; c3 += p.intensity;
+      }
+      const float cn = (float)(j - i);
+      o.x = c0 / cn; o.y = c1 / cn; o.z = c2 / cn; o.pad0 = 1.0f;
+      o.intensity = c3 / cn;
+      o.ring = 0; o.pad1 = 0; o.time = 0.0f; o.pad2 = 0.0f;
+    }
+    J.out[pos[job]++] = o;
+  }
+  if (tile == ntiles - 1 && threadIdx.x == 0) {
+    *A.d_out = pre.a + agg[0];
+    *B.d_out = pre.b + agg[1];
+  }
+}
+
+VoxelJobDev to_dev(const VoxelJob& j, int base) {
+  return VoxelJobDev{j.part0, j.d_n0, j.n0_ub, j.part1, j.d_n1, j.part1 ? j.n1_ub : 0, j.pose, 1.0f / j.leaf,
+                     j.out, j.d_out, base};
+}
+}  // namespace
+
+void voxel2_launch(VoxelScratch2& sc, const VoxelJob& a, const VoxelJob& b, hipStream_t st) {
+  const VoxelJobDev A = to_dev(a, 0);
+  const VoxelJobDev B = to_dev(b, a.n0_ub + (a.part1 ? a.n1_ub : 0));
+  const int total = B.base + b.n0_ub + (b.part1 ? b.n1_ub : 0);
+  const int n = std::max(total, 1);
+  sc.s.reserve(n);
+  sc.partials.reserve(2 * kMinMaxBlocks * 6);
+  sc.overflow.reserve(2);
+  const int ntiles = (int)div_up(n, kTile);
+  sc.status.reserve(ntiles);
+  sc.ticket.reserve(1);
+  const int umax = std::max(A.n0_ub + A.n1_ub, b.n0_ub + (b.part1 ? b.n1_ub : 0));
+  hipLaunchKernelGGL(vox_minmax, dim3(kMinMaxBlocks, 2), dim3(kTB), 0, st, A, B, sc.partials.p);
+  FLOAM_LAUNCH_CHECK();
+  const unsigned kb = std::max(1u, std::min(div_up(std::max(umax, 1), kTB), 1024u));
+  hipLaunchKernelGGL(vox_keys, dim3(kb, 2), dim3(kTB), 0, st, A, B, sc.partials.p, sc.s.k0.p, sc.s.v0.p,
+                     sc.overflow.p, sc.status.p, ntiles, sc.ticket.p);
+  FLOAM_LAUNCH_CHECK();
+  sort_pairs_u32(sc.s.temp.p, sc.s.temp_bytes, sc.s.k0.p, sc.s.k1.p, sc.s.v0.p, sc.s.v1.p, n, 32, st);
+  hipLaunchKernelGGL(vox_compact, dim3(ntiles), dim3(kTB), 0, st, A, B, sc.s.k1.p, sc.s.v1.p, sc.overflow.p, n,
+                     sc.status.p, sc.ticket.p);
+  FLOAM_LAUNCH_CHECK();
+}
+
+}  // namespace floam
