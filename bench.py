@@ -141,7 +141,7 @@ def main():
     def make_pipeline():
         nonlocal allreduce_impl, n_pipelines
         reset_process_state()
-        lp = floam_amd.LaserProcessingClass(device=dev)
+        lp = floam_amd.LaserProcessingClass(device=dev, asynchronous=True)   # one sync per scan (the pose read)
         lp.init(params)
         odo = floam_amd.OdomEstimationClass(device=dev)
         odo.init(params, MAP_RES, LOSS)

@@ -93,4 +93,6 @@ struct floam_cloud {
   floam::DevBuf<int> count;    // count.p[0] = number of points (device-resident)
   size_t host_count = 0;       // last value the host knows (valid when host_count_valid)
   bool host_count_valid = true;
+  size_t ub = 0;               // upper bound on the device count while host_count_valid is false
+  const int* fe_status = nullptr;   // device status flags of the (asynchronous) feature extraction that filled it
 };

@@ -3,11 +3,11 @@
 // Reference: src/odomEstimationClass.cpp:78-79 rebuilds pcl::KdTreeFLANN over both maps on every
 // updatePointsToMap call; here the grids are rebuilt only when the maps changed (a keyframe, :117-122), both maps in
 // the same four launches:
-//   grid_clear   empty both tables of both maps
-//   grid_count   per point: insert its coarse cell (1 m, absolute coordinates -> 64-bit key), count it in its fine
-//                sub-cell (0.5 m) and keep its rank there
-//   grid_alloc   per occupied coarse cell: a contiguous range of the cell-grouped array (one atomic per block on a
-//                bump cursor), fine sub-cells consecutive inside it, fine cells inserted into the fine table
+//   grid_clear   empty the table entries the previous build occupied (its slot lists; everything after a resize)
+//   grid_count   per point: insert its coarse cell (1 m, absolute coordinates -> 64-bit key; new cells appended to
+//                the occupied list), count it in its fine sub-cell (0.5 m) and keep its rank there
+//   grid_alloc   per occupied coarse cell (from the list): a contiguous range of the cell-grouped array (one atomic
+//                per block on a bump cursor), fine sub-cells consecutive inside it, fine cells inserted (and listed)
 //   grid_scatter per point: its slot = coarse start + preceding sub-cells + rank
 // No bounding box, no sort: O(M) work, every step one launch.
 #include "floam_common.hpp"
@@ -27,62 +27,102 @@ struct GridJob {
   FineCell* fine;
   CoarseCell* coarse;
   uint2* where;
-  int* cursor;
+  int* clist_new;   // appended by this build
+  int* flist_new;
+  const int* clist_old;   // cleared by this build
+  const int* flist_old;
+  int* counters;    // [0] cursor, [1 + parity] coarse list size, [3 + parity] fine list size
+  int parity;
+  int full_clear;
   int bits;
   unsigned mask;
 };
 
+__device__ __forceinline__ CoarseCell empty_coarse() {
+  CoarseCell c;
+  c.key = kEmptyKey;
+  c.start = 0;
+  c.total = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) c.sub[k] = 0;
+  return c;
+}
+
+// wave-aggregated append of `slot` (lanes with take) to list[*count ...]
+__device__ __forceinline__ void list_append(int* __restrict__ list, int* __restrict__ count, bool take, int slot) {
+  const unsigned long long b = __ballot(take);
+  if (!b) return;
+  const int lane = threadIdx.x & 63;
+  const int leader = __ffsll((long long)b) - 1;
+  int base = 0;
+  if (lane == leader) base = atomicAdd(count, __popcll(b));
+  base = __shfl(base, leader, 64);
+  if (take) list[base + __popcll(b & ((1ull << lane) - 1ull))] = slot;
+}
+
 __global__ __launch_bounds__(kTB) void grid_clear(GridJob E, GridJob S) {
   const GridJob& J = blockIdx.y == 0 ? E : S;
-  const int size = (int)J.mask + 1;
   const int stride = gridDim.x * blockDim.x;
-  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < size; t += stride) {
-    J.fine[t].key = kEmptyKey;
-    CoarseCell c;
-    c.key = kEmptyKey;
-    c.start = 0;
-    c.total = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) c.sub[k] = 0;
-    J.coarse[t] = c;
+  const int t0 = blockIdx.x * blockDim.x + threadIdx.x;
+  if (J.full_clear) {
+    const int size = (int)J.mask + 1;
+    for (int t = t0; t < size; t += stride) {
+      J.fine[t].key = kEmptyKey;
+      J.coarse[t] = empty_coarse();
+    }
+  } else {
+    const int nc = J.counters[1 + (J.parity ^ 1)], nf = J.counters[3 + (J.parity ^ 1)];
+    for (int t = t0; t < nc; t += stride) J.coarse[J.clist_old[t]] = empty_coarse();
+    for (int t = t0; t < nf; t += stride) J.fine[J.flist_old[t]].key = kEmptyKey;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) *J.cursor = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    J.counters[0] = 0;
+    J.counters[1 + J.parity] = 0;
+    J.counters[3 + J.parity] = 0;
+  }
 }
 
 __global__ __launch_bounds__(kTB) void grid_count(GridJob E, GridJob S) {
   const GridJob& J = blockIdx.y == 0 ? E : S;
   const int m = min(*J.d_m, J.m_ub);
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
-    const float4 p = *reinterpret_cast<const float4*>(&J.map[i].x);
-    int fx, fy, fz;
-    fine_cell(p.x, p.y, p.z, fx, fy, fz);
-    const unsigned long long key = cell_key(fx >> 1, fy >> 1, fz >> 1);
-    const int sub = (fx & 1) | ((fy & 1) << 1) | ((fz & 1) << 2);
-    unsigned h = hash_slot64(key, J.bits);
-    for (;;) {
-      const unsigned long long prev = atomicCAS(&J.coarse[h].key, kEmptyKey, key);
-      if (prev == kEmptyKey || prev == key) break;
-      h = (h + 1) & J.mask;
+  for (int i0 = blockIdx.x * blockDim.x; i0 < m; i0 += gridDim.x * blockDim.x) {   // wave-uniform trip count
+    const int i = i0 + threadIdx.x;
+    bool fresh = false;
+    unsigned h = 0;
+    if (i < m) {
+      const float4 p = *reinterpret_cast<const float4*>(&J.map[i].x);
+      int fx, fy, fz;
+      fine_cell(p.x, p.y, p.z, fx, fy, fz);
+      const unsigned long long key = cell_key(fx >> 1, fy >> 1, fz >> 1);
+      const int sub = (fx & 1) | ((fy & 1) << 1) | ((fz & 1) << 2);
+      h = hash_slot64(key, J.bits);
+      for (;;) {
+        const unsigned long long prev = atomicCAS(&J.coarse[h].key, kEmptyKey, key);
+        if (prev == kEmptyKey) fresh = true;
+        if (prev == kEmptyKey || prev == key) break;
+        h = (h + 1) & J.mask;
+      }
+      const int rank = atomicAdd(&J.coarse[h].sub[sub], 1);
+      J.where[i] = make_uint2(h, ((unsigned)sub << 28) | (unsigned)rank);
     }
-    const int rank = atomicAdd(&J.coarse[h].sub[sub], 1);
-    J.where[i] = make_uint2(h, ((unsigned)sub << 28) | (unsigned)rank);
+    list_append(J.clist_new, &J.counters[1 + J.parity], fresh, (int)h);
   }
 }
 
 __global__ __launch_bounds__(kTB) void grid_alloc(GridJob E, GridJob S) {
   const GridJob& J = blockIdx.y == 0 ? E : S;
-  const int size = (int)J.mask + 1;
+  const int nc = J.counters[1 + J.parity];
   __shared__ int s_wave[kTB / 64];
   __shared__ int s_base;
-  for (int t0 = blockIdx.x * blockDim.x; t0 < size; t0 += gridDim.x * blockDim.x) {   // block-uniform trip count
+  for (int t0 = blockIdx.x * blockDim.x; t0 < nc; t0 += gridDim.x * blockDim.x) {   // block-uniform trip count
     const int t = t0 + threadIdx.x;
     CoarseCell c;
-    int total = 0;
-    if (t < size) {
-      c = J.coarse[t];
-      if (c.key != kEmptyKey)
+    int total = 0, slot = 0;
+    if (t < nc) {
+      slot = J.clist_new[t];
+      c = J.coarse[slot];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) total += c.sub[k];
+      for (int k = 0; k < 8; ++k) total += c.sub[k];
     }
     // block exclusive scan of the totals: wave inclusive scan, then the wave totals
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -100,29 +140,33 @@ __global__ __launch_bounds__(kTB) void grid_alloc(GridJob E, GridJob S) {
       if (k < w) wbase += s_wave[k];
       btotal += s_wave[k];
     }
-    if (threadIdx.x == 0) s_base = btotal ? atomicAdd(J.cursor, btotal) : 0;
+    if (threadIdx.x == 0) s_base = btotal ? atomicAdd(&J.counters[0], btotal) : 0;
     __syncthreads();
-    if (t < size && total > 0) {
-      const int start = s_base + wbase + incl - total;
-      J.coarse[t].start = start;
-      J.coarse[t].total = total;
-      const int cx = key_x(c.key), cy = key_y(c.key), cz = key_z(c.key);
-      int off = start;
+    for (int k = 0; k < 8; ++k) {   // fine cells of this coarse cell (wave-uniform loop for the list appends)
+      bool ins = false;
+      unsigned h = 0;
+      if (t < nc && c.sub[k] > 0) {
+        int off = s_base + wbase + incl - total;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        if (c.sub[k] > 0) {
-          const unsigned long long fk = cell_key(2 * cx + (k & 1), 2 * cy + ((k >> 1) & 1), 2 * cz + (k >> 2));
-          unsigned h = hash_slot64(fk, J.bits);
-          for (;;) {
-            const unsigned long long prev = atomicCAS(&J.fine[h].key, kEmptyKey, fk);
-            if (prev == kEmptyKey) break;
-            h = (h + 1) & J.mask;
-          }
-          J.fine[h].start = off;
-          J.fine[h].count = c.sub[k];
+        for (int kk = 0; kk < 8; ++kk)
+          if (kk < k) off += c.sub[kk];
+        const int cx = key_x(c.key), cy = key_y(c.key), cz = key_z(c.key);
+        const unsigned long long fk = cell_key(2 * cx + (k & 1), 2 * cy + ((k >> 1) & 1), 2 * cz + (k >> 2));
+        h = hash_slot64(fk, J.bits);
+        for (;;) {
+          const unsigned long long prev = atomicCAS(&J.fine[h].key, kEmptyKey, fk);
+          if (prev == kEmptyKey) break;
+          h = (h + 1) & J.mask;
         }
-        off += c.sub[k];
+        J.fine[h].start = off;
+        J.fine[h].count = c.sub[k];
+        ins = true;
       }
+      list_append(J.flist_new, &J.counters[3 + J.parity], ins, (int)h);
+    }
+    if (t < nc) {
+      J.coarse[slot].start = s_base + wbase + incl - total;
+      J.coarse[slot].total = total;
     }
     __syncthreads();   // s_wave / s_base reuse
   }
@@ -147,13 +191,32 @@ __global__ __launch_bounds__(kTB) void grid_scatter(GridJob E, GridJob S) {
 void reserve_grid(Grid& g, int ub) {
   g.pts.reserve(ub);
   g.where.reserve(ub);
-  g.cursor.reserve(1);
+  g.counters.reserve(8);
   int bits = 10;
   while ((1 << bits) < 2 * ub) ++bits;   // load <= 1/2 (cells <= points)
-  g.fine.reserve((size_t)1 << bits);
-  g.coarse.reserve((size_t)1 << bits);
-  g.bits = bits;
-  g.mask = (1u << bits) - 1u;
+  if (bits > g.bits) {
+    g.fine.release();
+    g.coarse.release();
+    for (int k = 0; k < 2; ++k) {
+      g.clist[k].release();
+      g.flist[k].release();
+    }
+    g.fine.reserve((size_t)1 << bits);
+    g.coarse.reserve((size_t)1 << bits);
+    for (int k = 0; k < 2; ++k) {
+      g.clist[k].reserve((size_t)1 << bits);
+      g.flist[k].reserve((size_t)1 << bits);
+    }
+    g.bits = bits;
+    g.mask = (1u << bits) - 1u;
+    g.fresh = true;
+  }
+}
+
+GridJob make_job(Grid& g, const PointRec* map, const int* d_m, int m_ub) {
+  const int p = g.parity;
+  return GridJob{map, d_m, m_ub, g.pts.p, g.fine.p, g.coarse.p, g.where.p, g.clist[p].p, g.flist[p].p,
+                 g.clist[p ^ 1].p, g.flist[p ^ 1].p, g.counters.p, p, g.fresh ? 1 : 0, g.bits, g.mask};
 }
 }  // namespace
 
@@ -163,19 +226,25 @@ void grid_build_launch(Grid& gE, const PointRec* mapE, const int* d_mE, int mE_u
   mS_ub = std::max(mS_ub, 1);
   reserve_grid(gE, mE_ub);
   reserve_grid(gS, mS_ub);
-  const GridJob E{mapE, d_mE, mE_ub, gE.pts.p, gE.fine.p, gE.coarse.p, gE.where.p, gE.cursor.p, gE.bits, gE.mask};
-  const GridJob S{mapS, d_mS, mS_ub, gS.pts.p, gS.fine.p, gS.coarse.p, gS.where.p, gS.cursor.p, gS.bits, gS.mask};
+  if (gE.fresh) FLOAM_HIP(hipMemsetAsync(gE.counters.p, 0, sizeof(int) * 8, st));
+  if (gS.fresh) FLOAM_HIP(hipMemsetAsync(gS.counters.p, 0, sizeof(int) * 8, st));
+  const GridJob E = make_job(gE, mapE, d_mE, mE_ub), S = make_job(gS, mapS, d_mS, mS_ub);
+  const bool full = gE.fresh || gS.fresh;
   const int tmax = (int)std::max(gE.mask, gS.mask) + 1;
-  const unsigned tb = std::min(div_up(tmax, kTB), 2048u);
+  const unsigned tb = full ? std::min(div_up(tmax, kTB), 2048u) : std::min(div_up(std::max(mE_ub, mS_ub), kTB), 512u);
   const unsigned pb = std::min(div_up(std::max(mE_ub, mS_ub), kTB), 2048u);
   hipLaunchKernelGGL(grid_clear, dim3(tb, 2), dim3(kTB), 0, st, E, S);
   FLOAM_LAUNCH_CHECK();
   hipLaunchKernelGGL(grid_count, dim3(pb, 2), dim3(kTB), 0, st, E, S);
   FLOAM_LAUNCH_CHECK();
-  hipLaunchKernelGGL(grid_alloc, dim3(tb, 2), dim3(kTB), 0, st, E, S);
+  hipLaunchKernelGGL(grid_alloc, dim3(std::min(pb, 512u), 2), dim3(kTB), 0, st, E, S);
   FLOAM_LAUNCH_CHECK();
   hipLaunchKernelGGL(grid_scatter, dim3(pb, 2), dim3(kTB), 0, st, E, S);
   FLOAM_LAUNCH_CHECK();
+  for (Grid* g : {&gE, &gS}) {
+    g->fresh = false;
+    g->parity ^= 1;
+  }
 }
 
 }  // namespace floam

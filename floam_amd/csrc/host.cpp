@@ -131,6 +131,9 @@ static size_t cloud_count_sync(const floam_cloud* c) {
   return mc->host_count;
 }
 
+// host upper bound of a cloud's size without synchronising (exact when the host knows the count)
+static size_t cloud_ub(const floam_cloud* c) { return c->host_count_valid ? c->host_count : c->ub; }
+
 // grow keeping the first `keep` points (stream-ordered copy, then the old buffer is freed after a sync)
 static void cloud_reserve(floam_cloud* c, size_t n, size_t keep, hipStream_t st) {
   if (n <= c->pts.cap) return;
@@ -177,6 +180,7 @@ struct floam_lp {
   FeScratch sc;
   DevBuf<int> status;
   HostBuf<int> h_out;   // edge count, surf count, status
+  bool async = false;   // floam_lp_set_async: no synchronisation, counts stay on the device (upper bounds on host)
 };
 
 struct floam_odom {
@@ -201,8 +205,9 @@ struct floam_odom {
   DevBuf<unsigned> step_counter;
   DevBuf<unsigned long long> dbg_stamps;   // FLOAM_DEBUG_STAMPS=1: lm_step segment times (diagnostic)
   DevBuf<LMState> lm;
-  DevBuf<UpdateStatus> ustat;
+  DevBuf<UpdateStatus> ustat;     // slot 0: first / only call, slot 1: second call of a deskewed selector
   HostBuf<UpdateStatus> h_ustat;
+  DevBuf<double> x0buf;           // the second call's prediction, formed on the device
   DevBuf<unsigned long long> prof_bytes;
   DevBuf<unsigned long long> traffic_set;
   bool prof_bytes_init = false;
@@ -288,20 +293,24 @@ void allreduce_sums(floam_odom* o, DeviceCtx& ctx) {
   FLOAM_HIP(hipStreamSynchronize(ctx.stream));
 }
 
-// updatePointsToMap (src/odomEstimationClass.cpp:52-124)
-void odom_update(floam_odom* o, const floam_cloud* edge, const floam_cloud* surf, int type) {
-  DeviceCtx& ctx = ctx_for(o->device);
-  hipStream_t st = ctx.stream;
-  FLOAM_HIP(hipSetDevice(o->device));
-  const int ne_ub = (int)cloud_count_sync(edge);
-  const int ns_ub = (int)cloud_count_sync(surf);
-
+// updatePointsToMap (src/odomEstimationClass.cpp:52-124) is split into four steps so that the two calls of a
+// deskewed UpdatePointsToMapSelector can be issued back to back with a single synchronisation:
+//   odom_predict  host: optimization_count, the constant-velocity prediction (:59-71; branch always taken, Q2)
+//   odom_issue    device: downsample, [grid rebuild], optimization_count x {kNN + geometry, 5 LM steps}, and a
+//                 gather of the solve result into status slot `slot` — no synchronisation
+//   odom_finish   host, after the synchronisation: gate (:77), pose writeback (:114-116), warnings, stats
+//   odom_map_update  host keyframe test (:117-122, KeyFrameUpdate :320-343) and the device map update (:253-294)
+void odom_predict(floam_odom* o) {
   if (o->optimization_count > 2) o->optimization_count--;
   const Pose pred = pose_mul(o->odom, pose_mul(pose_inverse(o->last_odom), o->odom));
   o->last_odom = o->odom;   // Q2: the branch is taken for every update type
   o->odom = pred;
   odom_set_params_from_odom(o);
+}
 
+void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const floam_cloud* surf, int ne_ub, int ns_ub,
+                const double* x0_host, const double* x0_dev, int slot) {
+  hipStream_t st = ctx.stream;
   o->dE.reserve(std::max(ne_ub, 1));
   o->dS.reserve(std::max(ns_ub, 1));
   o->cnt.reserve(4);
@@ -341,13 +350,14 @@ void odom_update(floam_odom* o, const floam_cloud* edge, const floam_cloud* surf
   const QuerySet qs{o->dS.p, o->cnt.p + 1, ns_ub};
   const bool sharded = o->world > 1;
   for (int it = 0; it < o->optimization_count; ++it) {
-    lm_init_launch(o->lm.p, it == 0 ? o->parameters : nullptr, st);   // first solve starts at the prediction
     {
       ProfScope ps(ctx, "knn", FLOAM_PROF_KNN);   // the correspondence pass: search + geometry
       {
         ProfScope ps1(ctx, "knn_search", FLOAM_PROF_KNN_DETAIL);
-        knn_launch(o->lm.p, qe, o->gE, o->mapE.pts.p, o->ce, qs, o->gS, o->mapS.pts.p, o->cs, o->mapE.count.p,
-                   o->mapS.count.p, o->rank, o->world, st, o->dbg_stamps.p ? o->dbg_stamps.p + 8 : nullptr);
+        // (also resets the LM state; the first solve starts at the prediction)
+        knn_launch(o->lm.p, it == 0 ? x0_host : nullptr, it == 0 ? x0_dev : nullptr, qe, o->gE, o->mapE.pts.p,
+                   o->ce, qs, o->gS, o->mapS.pts.p, o->cs, o->mapE.count.p, o->mapS.count.p, o->rank, o->world, st,
+                   o->dbg_stamps.p ? o->dbg_stamps.p + 8 : nullptr);
       }
       ProfScope ps2(ctx, "knn_geometry", FLOAM_PROF_KNN_DETAIL);
       geom_launch(o->lm.p, qe, o->gE, o->mapE.pts.p, o->ce, qs, o->gS, o->mapS.pts.p, o->cs, st);
@@ -373,25 +383,42 @@ void odom_update(floam_odom* o, const floam_cloud* edge, const floam_cloud* surf
       }
     }
   }
+  if (o->optimization_count <= 0) lm_init_launch(o->lm.p, x0_host, st);
   const bool prof_knn = (ctx.profile & FLOAM_PROF_KNN_BYTES) != 0;
-  o->ustat.reserve(1);
-  o->h_ustat.reserve(1);
-  if (o->optimization_count <= 0) lm_init_launch(o->lm.p, o->parameters, st);
-  gather_status_launch(o->lm.p, o->cnt.p, o->mapE.count.p, o->mapS.count.p, prof_knn ? o->prof_bytes.p : nullptr,
-                       o->ustat.p, st);
-  FLOAM_HIP(hipMemcpyAsync(o->h_ustat.p, o->ustat.p, sizeof(UpdateStatus), hipMemcpyDeviceToHost, st));
+  o->ustat.reserve(2);
+  gather_status_launch(o->lm.p, o->cnt.p, o->mapE.count.p, o->mapS.count.p, edge->fe_status,
+                       prof_knn ? o->prof_bytes.p : nullptr, o->ustat.p + slot, st);
   if (prof_knn) FLOAM_HIP(hipMemsetAsync(o->prof_bytes.p, 0, sizeof(unsigned long long) * 2, st));
-  FLOAM_HIP(hipStreamSynchronize(st));
+}
+
+// the one synchronisation: status slots [0, nslots) to the host
+void odom_sync(floam_odom* o, DeviceCtx& ctx, int nslots) {
+  o->h_ustat.reserve(2);
+  FLOAM_HIP(hipMemcpyAsync(o->h_ustat.p, o->ustat.p, sizeof(UpdateStatus) * nslots, hipMemcpyDeviceToHost,
+                           ctx.stream));
+  FLOAM_HIP(hipStreamSynchronize(ctx.stream));
   ctx.drain();
-  if (prof_knn) {
-    floam_kernel_timing& t = ctx.totals["knn"];
-    std::strncpy(t.name, "knn", sizeof(t.name) - 1);
-    t.algorithmic_bytes += (double)o->h_ustat.p->prof[0] + (double)o->h_ustat.p->prof[1];
+  for (int k = 0; k < nslots; ++k) {
+    const UpdateStatus& U = o->h_ustat.p[k];
+    if (ctx.profile & FLOAM_PROF_KNN_BYTES) {
+      floam_kernel_timing& t = ctx.totals["knn"];
+      std::strncpy(t.name, "knn", sizeof(t.name) - 1);
+      t.algorithmic_bytes += (double)U.prof[0] + (double)U.prof[1];
+    }
+    if (U.lm.n_res < 0)
+      throw Error(FLOAM_ERR_DEVICE, "LM evaluation blocks did not arrive at the control block (timeout)");
+    if (U.counts[0] < 0 || U.counts[1] < 0 || U.counts[2] < 0 || U.counts[3] < 0)
+      throw Error(FLOAM_ERR_DEVICE, "voxel-grid compaction failed (lookback timeout)");
+    if (U.fe_status & FE_STATUS_SECTOR_TOO_LONG)
+      throw Error(FLOAM_ERR_UNSUPPORTED, "a ring sector exceeds 4096 points (ring longer than ~24k points)");
+    if (U.fe_status & FE_STATUS_BAD_RING)
+      throw Error(FLOAM_ERR_INVALID_ARGUMENT, "point ring index >= num_lines (out of bounds in the reference)");
   }
-  const LMState& L = o->h_ustat.p->lm;
-  if (L.n_res < 0) throw Error(FLOAM_ERR_DEVICE, "LM evaluation blocks did not arrive at the control block (timeout)");
-  const int* hc = o->h_ustat.p->counts;
-  const int nEd = hc[0], nSd = hc[1];
+}
+
+void odom_finish(floam_odom* o, const UpdateStatus& U) {
+  const LMState& L = U.lm;
+  const int* hc = U.counts;
   o->mapE_n = (size_t)hc[2];
   o->mapS_n = (size_t)hc[3];
   o->mapE.host_count = o->mapE_n; o->mapE.host_count_valid = true;
@@ -409,42 +436,88 @@ void odom_update(floam_odom* o, const floam_cloud* edge, const floam_cloud* surf
   for (int i = 0; i < 3; ++i) o->odom.t[i] = o->parameters[4 + i];
   o->stats.optimization_count = o->optimization_count;
   o->stats.solves = gate ? o->optimization_count : 0;
-  o->stats.edge_queries = nEd;
-  o->stats.surf_queries = nSd;
+  o->stats.edge_queries = hc[0];
+  o->stats.surf_queries = hc[1];
   o->stats.edge_correspondences = gate ? L.corr_edge : 0;
   o->stats.surf_correspondences = gate ? L.corr_surf : 0;
   o->stats.lm_iterations = gate ? L.iteration : 0;
   o->stats.final_cost = gate ? L.x_cost : 0.0;
   o->stats.map_updated = 0;
-  if (type == FLOAM_VANILLA || type == FLOAM_REFINEMENT_AND_UPDATE) {
-    if (keyframe_update(o, o->odom)) {
-      // addPointsToMap (:253-294): device-side transform + append + CropBox + VoxelGrid of both maps, using the
-      // optimised pose, which is lm->x (== parameters) on the device.
-      ProfScope ps(ctx, "map_update", FLOAM_PROF_CLOUD);
-      if (!gate) {   // lm->x still holds the prediction we uploaded: identical to parameters
-      }
-      const int ubS = (int)o->mapS_n + nSd, ubE = (int)o->mapE_n + nEd;
-      cloud_reserve(&o->mapS_next, std::max(ubS, 1), 0, st);
-      cloud_reserve(&o->mapE_next, std::max(ubE, 1), 0, st);
-      // [map ; pointAssociateToMap(downsampled scan)] -> CropBox -> VoxelGrid, both maps in one pipeline
-      VoxelJob je, js;
-      je.part0 = o->mapE.pts.p; je.d_n0 = o->mapE.count.p; je.n0_ub = (int)o->mapE_n;
-      je.part1 = o->dE.p; je.d_n1 = o->cnt.p + 0; je.n1_ub = nEd;
-      je.pose = o->lm.p->x; je.leaf = o->leafE; je.out = o->mapE_next.pts.p; je.d_out = o->mapE_next.count.p;
-      js.part0 = o->mapS.pts.p; js.d_n0 = o->mapS.count.p; js.n0_ub = (int)o->mapS_n;
-      js.part1 = o->dS.p; js.d_n1 = o->cnt.p + 1; js.n1_ub = nSd;
-      js.pose = o->lm.p->x; js.leaf = o->leafS; js.out = o->mapS_next.pts.p; js.d_out = o->mapS_next.count.p;
-      voxel2_launch(o->vs, je, js, st);
-      cloud_swap(&o->mapE, &o->mapE_next);
-      cloud_swap(&o->mapS, &o->mapS_next);
-      o->mapS_n = (size_t)ubS;   // upper bounds until the next synchronisation
-      o->mapE_n = (size_t)ubE;
-      o->mapS.host_count_valid = false;
-      o->mapE.host_count_valid = false;
-      o->grid_dirty = true;
-      o->stats.map_updated = 1;
-    }
+}
+
+void odom_map_update(floam_odom* o, DeviceCtx& ctx, int type, const UpdateStatus& U) {
+  if (!(type == FLOAM_VANILLA || type == FLOAM_REFINEMENT_AND_UPDATE)) return;
+  if (!keyframe_update(o, o->odom)) return;
+  // addPointsToMap (:253-294): device-side transform + append + CropBox + VoxelGrid of both maps, using the
+  // optimised pose, which is lm->x (== parameters) on the device.
+  hipStream_t st = ctx.stream;
+  ProfScope ps(ctx, "map_update", FLOAM_PROF_CLOUD);
+  const int nEd = U.counts[0], nSd = U.counts[1];
+  const int ubS = (int)o->mapS_n + nSd, ubE = (int)o->mapE_n + nEd;
+  cloud_reserve(&o->mapS_next, std::max(ubS, 1), 0, st);
+  cloud_reserve(&o->mapE_next, std::max(ubE, 1), 0, st);
+  // [map ; pointAssociateToMap(downsampled scan)] -> CropBox -> VoxelGrid, both maps in one pipeline
+  VoxelJob je, js;
+  je.part0 = o->mapE.pts.p; je.d_n0 = o->mapE.count.p; je.n0_ub = (int)o->mapE_n;
+  je.part1 = o->dE.p; je.d_n1 = o->cnt.p + 0; je.n1_ub = nEd;
+  je.pose = o->lm.p->x; je.leaf = o->leafE; je.out = o->mapE_next.pts.p; je.d_out = o->mapE_next.count.p;
+  js.part0 = o->mapS.pts.p; js.d_n0 = o->mapS.count.p; js.n0_ub = (int)o->mapS_n;
+  js.part1 = o->dS.p; js.d_n1 = o->cnt.p + 1; js.n1_ub = nSd;
+  js.pose = o->lm.p->x; js.leaf = o->leafS; js.out = o->mapS_next.pts.p; js.d_out = o->mapS_next.count.p;
+  voxel2_launch(o->vs, je, js, st);
+  cloud_swap(&o->mapE, &o->mapE_next);
+  cloud_swap(&o->mapS, &o->mapS_next);
+  o->mapS_n = (size_t)ubS;   // upper bounds until the next synchronisation
+  o->mapE_n = (size_t)ubE;
+  o->mapS.host_count_valid = false;
+  o->mapE.host_count_valid = false;
+  o->mapS.ub = o->mapS_n;
+  o->mapE.ub = o->mapE_n;
+  o->grid_dirty = true;
+  o->stats.map_updated = 1;
+}
+
+// updatePointsToMap (src/odomEstimationClass.cpp:52-124), one call
+void odom_update(floam_odom* o, const floam_cloud* edge, const floam_cloud* surf, int type) {
+  DeviceCtx& ctx = ctx_for(o->device);
+  FLOAM_HIP(hipSetDevice(o->device));
+  odom_predict(o);
+  odom_issue(o, ctx, edge, surf, (int)cloud_ub(edge), (int)cloud_ub(surf), o->parameters, nullptr, 0);
+  odom_sync(o, ctx, 1);
+  odom_finish(o, o->h_ustat.p[0]);
+  odom_map_update(o, ctx, type, o->h_ustat.p[0]);
+}
+
+// UpdatePointsToMapSelector with deskew (src/odomEstimationClass.cpp:38-47): call 1 (edge, edge) INITIAL_ITERATION
+// (Q4), GetVelocity + CompensateVelocity of both clouds in place (Q5), call 2 (edge, surf) REFINEMENT_AND_UPDATE.
+// The velocity and the second prediction are formed on the device (deskew_bridge), so the whole selector runs with
+// one synchronisation; the host then replays the same pose algebra to keep its state.
+floam_status odom_update_deskew(floam_odom* o, floam_cloud* edge, floam_cloud* surf) {
+  DeviceCtx& ctx = ctx_for(o->device);
+  FLOAM_HIP(hipSetDevice(o->device));
+  const int ne_ub = (int)cloud_ub(edge), ns_ub = (int)cloud_ub(surf);
+  odom_predict(o);
+  const Pose odom0 = o->last_odom;
+  odom_issue(o, ctx, edge, edge, ne_ub, ne_ub, o->parameters, nullptr, 0);
+  o->x0buf.reserve(7);
+  {
+    ProfScope ps(ctx, "deskew", FLOAM_PROF_CLOUD);
+    deskew_bridge_launch(o->lm.p, odom0, o->lp.scan_period, edge->pts.p, edge->count.p, ne_ub, surf->pts.p,
+                         surf->count.p, ns_ub, o->x0buf.p, ctx.stream);
   }
+  if (o->optimization_count > 2) o->optimization_count--;   // call 2's decrement (the host replays the rest below)
+  odom_issue(o, ctx, edge, surf, ne_ub, ns_ub, nullptr, o->x0buf.p, 1);
+  odom_sync(o, ctx, 2);
+  odom_finish(o, o->h_ustat.p[0]);
+  const floam_status w1 = o->last_warning;
+  // call 2's prediction on the host (bit-identical to the device's, pose.hpp)
+  const Pose pred = pose_mul(o->odom, pose_mul(pose_inverse(o->last_odom), o->odom));
+  o->last_odom = o->odom;
+  o->odom = pred;
+  odom_set_params_from_odom(o);
+  odom_finish(o, o->h_ustat.p[1]);
+  odom_map_update(o, ctx, FLOAM_REFINEMENT_AND_UPDATE, o->h_ustat.p[1]);
+  return o->last_warning != FLOAM_OK ? o->last_warning : w1;
 }
 
 // CompensateVelocity (src/dataHandler.cpp:82-92) with GetVelocity (include/odomEstimationClass.h:78)
@@ -591,6 +664,29 @@ floam_status floam_lp_create(const floam_lidar_params* p, int device, floam_lp**
   });
 }
 
+floam_status floam_lp_set_async(floam_lp* lp, int async) {
+  return guarded([&] {
+    if (!lp) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
+    lp->async = async != 0;
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_lp_wait(floam_lp* lp) {
+  return guarded([&] {
+    if (!lp) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
+    DeviceCtx& ctx = ctx_for(lp->device);
+    FLOAM_HIP(hipMemcpyAsync(lp->h_out.p, lp->sc.out3.p, sizeof(int) * 3, hipMemcpyDeviceToHost, ctx.stream));
+    FLOAM_HIP(hipStreamSynchronize(ctx.stream));
+    const int status = lp->h_out.p[2];
+    if (status & FE_STATUS_SECTOR_TOO_LONG)
+      throw Error(FLOAM_ERR_UNSUPPORTED, "a ring sector exceeds 4096 points (ring longer than ~24k points)");
+    if (status & FE_STATUS_BAD_RING)
+      throw Error(FLOAM_ERR_INVALID_ARGUMENT, "point ring index >= num_lines (out of bounds in the reference)");
+    return FLOAM_OK;
+  });
+}
+
 floam_status floam_lp_destroy(floam_lp* lp) {
   return guarded([&] {
     if (lp) {
@@ -612,13 +708,26 @@ floam_status floam_lp_feature_extraction(floam_lp* lp, const floam_cloud* in, fl
     hipStream_t st = ctx.stream;
     FLOAM_HIP(hipSetDevice(lp->device));
     const size_t n = cloud_count_sync(in);
-    const size_t ne0 = cloud_count_sync(edge), ns0 = cloud_count_sync(surf);
-    cloud_reserve(edge, ne0 + std::min(n, (size_t)lp->prm.num_lines * 6 * 20) + 1, ne0, st);
+    const size_t ne0 = lp->async ? cloud_ub(edge) : cloud_count_sync(edge);
+    const size_t ns0 = lp->async ? cloud_ub(surf) : cloud_count_sync(surf);
+    const size_t ne_add = std::min(n, (size_t)lp->prm.num_lines * 6 * 20);
+    cloud_reserve(edge, ne0 + ne_add + 1, ne0, st);
     cloud_reserve(surf, ns0 + n + 1, ns0, st);
     if (n > 0) {
       ProfScope ps(ctx, "feature_extraction", FLOAM_PROF_FE, 64.0 * (double)n);
       fe_launch(lp->sc, lp->prm, in->pts.p, (int)n, edge->pts.p, edge->count.p, surf->pts.p, surf->count.p, st);
     }
+    if (lp->async && n > 0) {
+      // counts stay on the device; the status flags travel with the clouds and are checked at the consumer's
+      // synchronisation (odometry update) or by floam_lp_wait
+      edge->host_count_valid = false;
+      edge->ub = ne0 + ne_add;
+      surf->host_count_valid = false;
+      surf->ub = ns0 + n;
+      edge->fe_status = surf->fe_status = lp->sc.out3.p + 2;
+      return FLOAM_OK;
+    }
+    edge->fe_status = surf->fe_status = nullptr;
     if (n > 0) {
       FLOAM_HIP(hipMemcpyAsync(lp->h_out.p, lp->sc.out3.p, sizeof(int) * 3, hipMemcpyDeviceToHost, st));
       FLOAM_HIP(hipStreamSynchronize(st));
@@ -739,18 +848,7 @@ floam_status floam_odom_update_selector(floam_odom* o, floam_cloud* edge, floam_
       odom_update(o, edge, surf, FLOAM_VANILLA);
       return o->last_warning;
     }
-    odom_update(o, edge, edge, FLOAM_INITIAL_ITERATION);   // Q4: the edge cloud is passed as the surf input
-    const floam_status w1 = o->last_warning;
-    double v[3];
-    odom_velocity(o, v);
-    DeviceCtx& ctx = ctx_for(o->device);
-    {
-      ProfScope ps(ctx, "deskew", FLOAM_PROF_CLOUD);
-      compensate_velocity_launch(edge->pts.p, edge->count.p, (int)cloud_count_sync(edge), v[0], v[1], v[2], ctx.stream);
-      compensate_velocity_launch(surf->pts.p, surf->count.p, (int)cloud_count_sync(surf), v[0], v[1], v[2], ctx.stream);
-    }
-    odom_update(o, edge, surf, FLOAM_REFINEMENT_AND_UPDATE);
-    return o->last_warning != FLOAM_OK ? o->last_warning : w1;
+    return odom_update_deskew(o, edge, surf);
   });
 }
 

@@ -21,38 +21,61 @@ __device__ __forceinline__ unsigned long long lb_pack(unsigned long long flag, i
 }
 
 // Called by ALL threads of the block (contains barriers).  Returns the tile's exclusive prefix; tile = ticket.
+// Wave 0 looks back over a window of 64 predecessors at once (one status word per lane): the nearest inclusive
+// prefix in the window ends the walk, otherwise the whole window's aggregates are added and the window moves back.
 // The wait on a predecessor is bounded (~1 s); on timeout the prefix comes back with a = -1 (caller reports it).
 __device__ __forceinline__ Prefix2 lookback_prefix(unsigned long long* __restrict__ status, int tile, Prefix2 agg) {
   __shared__ Prefix2 s_prefix;
-  if (threadIdx.x == 0) {
-    Prefix2 pre{0, 0};
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
     if (tile == 0) {
-      __hip_atomic_store(&status[0], lb_pack(kLbInclusive, agg.a, agg.b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0) {
+        __hip_atomic_store(&status[0], lb_pack(kLbInclusive, agg.a, agg.b), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        s_prefix = Prefix2{0, 0};
+      }
     } else {
-      __hip_atomic_store(&status[tile], lb_pack(kLbAggregate, agg.a, agg.b), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0)
+        __hip_atomic_store(&status[tile], lb_pack(kLbAggregate, agg.a, agg.b), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      long long pa = 0, pb = 0;
+      bool failed = false;
       long long polls = 0;
-      for (int j = tile - 1; j >= 0;) {
-        const unsigned long long w = __hip_atomic_load(&status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int hi = tile - 1; hi >= 0;) {   // window [hi - 63, hi]; lane k reads tile hi - k
+        const int j = hi - lane;
+        unsigned long long w = kLbInclusive;   // beyond tile 0: acts as an inclusive zero
+        if (j >= 0) w = __hip_atomic_load(&status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned long long flag = w & (3ull << 62);
-        if (flag == 0) {
-          if (++polls > (1ll << 24)) {
-            pre.a = -1;
-            break;
-          }
+        const unsigned long long incl = __ballot(flag == kLbInclusive);
+        const int stop = incl ? __ffsll((long long)incl) - 1 : 63;   // nearest inclusive lane (or whole window)
+        const unsigned long long notready = __ballot(flag == 0) & ((stop == 63) ? ~0ull : ((2ull << stop) - 1ull));
+        if (notready) {
+          if (++polls > (1ll << 24)) { failed = true; break; }
           __builtin_amdgcn_s_sleep(1);
           continue;
         }
-        pre.a += (int)(w & 0x7FFFFFFFull);
-        pre.b += (int)((w >> 31) & 0x7FFFFFFFull);
-        if (flag == kLbInclusive) break;
-        --j;
+        long long va = (lane <= stop && j >= 0) ? (long long)(w & 0x7FFFFFFFull) : 0;
+        long long vb = (lane <= stop && j >= 0) ? (long long)((w >> 31) & 0x7FFFFFFFull) : 0;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          va += __shfl_xor(va, o, 64);
+          vb += __shfl_xor(vb, o, 64);
+        }
+        pa += va;
+        pb += vb;
+        if (incl) break;
+        hi -= 64;
       }
-      if (pre.a >= 0)
-        __hip_atomic_store(&status[tile], lb_pack(kLbInclusive, pre.a + agg.a, pre.b + agg.b), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0) {
+        if (failed) {
+          s_prefix = Prefix2{-1, 0};
+        } else {
+          __hip_atomic_store(&status[tile], lb_pack(kLbInclusive, (int)pa + agg.a, (int)pb + agg.b),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          s_prefix = Prefix2{(int)pa, (int)pb};
+        }
+      }
     }
-    s_prefix = pre;
   }
   __syncthreads();
   const Prefix2 r = s_prefix;

@@ -324,6 +324,24 @@ __device__ void plane_solve(const double (&A)[5][3], double (&x)[3]) {
     }
 }
 
+// LM state at the start of a solve (the former lm_init launch)
+__device__ __forceinline__ void lm_reset(LMState* st, const X7& x0) {
+  if (x0.set)
+#pragma unroll
+    for (int k = 0; k < 7; ++k) st->x[k] = x0.v[k];
+  st->phase = 0;
+  st->done = 0;
+  st->iteration = 0;
+  st->reuse = 0;
+  st->invalid = 0;
+  st->successful = 0;
+  st->n_res = 0;
+  st->corr_edge = 0;
+  st->corr_surf = 0;
+  st->radius = 1e4;
+  st->dfac = 2.0;
+}
+
 // ===================================================================================== correspondence search
 // One query per group of kGroup lanes.  The group looks up the (<= 27) stencil cells of its query in parallel
 // (one 16-B hash probe per cell), scans their counts into an exclusive prefix held in LDS, and then walks the
@@ -536,7 +554,7 @@ __device__ __forceinline__ void group_merge(Top5& t, int& cnt) {
 // depends on its tree traversal; tie-free data is identical).
 // Output: valid bit 0 = 5 neighbours within sqd < 1 (their coordinates in nnxyz), bit 1 = stage 2 was needed.
 template <int G, int U>
-__device__ __forceinline__ void knn_group(const LMState* __restrict__ st, const CorrArgs& A, int gid, int ngroups,
+__device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArgs& A, int gid, int ngroups,
                                           int lane, bool gate, int rank, int world, int* __restrict__ s_pre,
                                           int* __restrict__ s_start) {
   const int n = min(*A.d_n, A.n_ub);
@@ -552,7 +570,7 @@ __device__ __forceinline__ void knn_group(const LMState* __restrict__ st, const 
       if (A.dbg) ts = __builtin_amdgcn_s_memrealtime();
       const float4 pq = *reinterpret_cast<const float4*>(&A.q[i].x);
       float wx, wy, wz;
-      associate_to_map(st->x, pq.x, pq.y, pq.z, wx, wy, wz);   // pointAssociateToMap (:126-135)
+      associate_to_map(pose, pq.x, pq.y, pq.z, wx, wy, wz);   // pointAssociateToMap (:126-135)
       int qx, qy, qz;
       fine_cell(wx, wy, wz, qx, qy, qz);
       Top5 t;
@@ -606,21 +624,34 @@ __device__ __forceinline__ void knn_group(const LMState* __restrict__ st, const 
     for (int k = 0; k < 6; ++k) atomicAdd(&A.dbg[k], dsum[k]);
 }
 
-// Edge and surf kNN in one launch: blocks [0, nbE) run edge groups, the others surf groups.
+// Edge and surf kNN in one launch: blocks [0, nbE) run edge groups, the others surf groups.  The launch also starts
+// the solve (lm_init folded in): block 0 resets the LM state and, for the first solve of an update, stores the
+// prediction x0 that every block uses for its transforms (the others never read st->x in that case).
 template <int G, int U>
-__global__ __launch_bounds__(kTB) void knn_kernel(const LMState* __restrict__ st, CorrArgs E, CorrArgs S, int nbE,
+__global__ __launch_bounds__(kTB) void knn_kernel(LMState* __restrict__ st, X7 x0, const double* __restrict__ x0_dev,
+                                                  CorrArgs E, CorrArgs S, int nbE,
                                                   const int* __restrict__ d_me, const int* __restrict__ d_ms,
                                                   int rank, int world) {
   __shared__ int s_pre[kTB / G][kMaxStencil + 1];
   __shared__ int s_start[kTB / G][kMaxStencil];
   const int lane = threadIdx.x & (G - 1);
   const int g = threadIdx.x / G;
+  double pose[7];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) pose[k] = x0_dev ? x0_dev[k] : (x0.set ? x0.v[k] : st->x[k]);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    X7 xs;
+    xs.set = (x0_dev || x0.set) ? 1 : 0;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) xs.v[k] = pose[k];
+    lm_reset(st, xs);
+  }
   const bool gate = *d_me > 10 && *d_ms > 50;   // map-size gate (odomEstimationClass.cpp:77)
   if ((int)blockIdx.x < nbE)
-    knn_group<G, U>(st, E, (blockIdx.x * blockDim.x + threadIdx.x) / G, nbE * (kTB / G), lane, gate, rank, world,
+    knn_group<G, U>(pose, E, (blockIdx.x * blockDim.x + threadIdx.x) / G, nbE * (kTB / G), lane, gate, rank, world,
                     s_pre[g], s_start[g]);
   else
-    knn_group<G, U>(st, S, ((blockIdx.x - nbE) * blockDim.x + threadIdx.x) / G, (gridDim.x - nbE) * (kTB / G), lane,
+    knn_group<G, U>(pose, S, ((blockIdx.x - nbE) * blockDim.x + threadIdx.x) / G, (gridDim.x - nbE) * (kTB / G), lane,
                     gate, rank, world, s_pre[g], s_start[g]);
 }
 
@@ -748,22 +779,53 @@ __global__ __launch_bounds__(kTB) void knn_traffic(const LMState* __restrict__ s
   if (bytes) atomicAdd(out, bytes);
 }
 
+
 __global__ void lm_init(LMState* st, X7 x0) {
+  if (threadIdx.x == 0) lm_reset(st, x0);
+}
+
+__global__ void lm_init_dev(LMState* st, X7 x0, const double* __restrict__ x0_dev) {
   if (threadIdx.x != 0) return;
-  if (x0.set)
+  if (x0_dev) {
+    x0.set = 1;
 #pragma unroll
-    for (int k = 0; k < 7; ++k) st->x[k] = x0.v[k];
-  st->phase = 0;
-  st->done = 0;
-  st->iteration = 0;
-  st->reuse = 0;
-  st->invalid = 0;
-  st->successful = 0;
-  st->n_res = 0;
-  st->corr_edge = 0;
-  st->corr_surf = 0;
-  st->radius = 1e4;
-  st->dfac = 2.0;
+    for (int k = 0; k < 7; ++k) x0.v[k] = x0_dev[k];
+  }
+  lm_reset(st, x0);
+}
+
+__global__ __launch_bounds__(kTB) void deskew_bridge(const LMState* __restrict__ st, Pose odom0, double period,
+                                                     PointRec* __restrict__ edge, const int* __restrict__ d_ne,
+                                                     int ne_ub, PointRec* __restrict__ surf,
+                                                     const int* __restrict__ d_ns, int ns_ub,
+                                                     double* __restrict__ x0_out) {
+  double x1[7];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) x1[k] = st->x[k];
+  // GetVelocity (include/odomEstimationClass.h:78): (odom.translation() - last_odom.translation()) / scan_period
+  const double vx = (x1[4] - odom0.t[0]) / period, vy = (x1[5] - odom0.t[1]) / period,
+               vz = (x1[6] - odom0.t[2]) / period;
+  const int ne = min(*d_ne, ne_ub), ns = min(*d_ns, ns_ub);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < ne + ns; i += gridDim.x * blockDim.x) {
+    PointRec& p = i < ne ? edge[i] : surf[i - ne];   // CompensateVelocity: p += v * time, double -> float
+    const double t = p.time;
+    p.x = (float)((double)p.x + vx * t);
+    p.y = (float)((double)p.y + vy * t);
+    p.z = (float)((double)p.z + vz * t);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    // the second call's prediction (:62-71): odom1 * (last_odom^-1 * odom1), last_odom = odom0
+    Pose odom1;
+    odom1.R = quat_to_mat(x1);
+    odom1.t[0] = x1[4]; odom1.t[1] = x1[5]; odom1.t[2] = x1[6];
+    const Pose pred = pose_mul(odom1, pose_mul(pose_inverse(odom0), odom1));
+    double q[4];
+    mat_to_quat(pred.R, q);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x0_out[k] = q[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) x0_out[4 + k] = pred.t[k];
+  }
 }
 
 // ===================================================================================== residuals + reduction
@@ -1326,6 +1388,14 @@ __global__ __launch_bounds__(kTB) void lm_reduce(const double* __restrict__ part
 }  // namespace
 
 // ===================================================================================== launchers
+void deskew_bridge_launch(const LMState* d_st, const Pose& odom0, double scan_period, PointRec* edge, const int* d_ne,
+                          int ne_ub, PointRec* surf, const int* d_ns, int ns_ub, double* x0_out, hipStream_t stream) {
+  const unsigned nb = std::max(1u, std::min(div_up(std::max(ne_ub + ns_ub, 1), kTB), 1024u));
+  hipLaunchKernelGGL(deskew_bridge, dim3(nb), dim3(kTB), 0, stream, d_st, odom0, scan_period, edge, d_ne, ne_ub, surf,
+                     d_ns, ns_ub, x0_out);
+  FLOAM_LAUNCH_CHECK();
+}
+
 void lm_init_launch(LMState* d_st, const double* x0, hipStream_t st) {
   X7 x{};
   if (x0) {
@@ -1339,7 +1409,8 @@ void lm_init_launch(LMState* d_st, const double* x0, hipStream_t st) {
 // One D2H per update: LM state + query / map counts (+ profiling bytes) gathered into one block.
 __global__ void gather_status(const LMState* __restrict__ lm, const int* __restrict__ dcnt,
                               const int* __restrict__ mapE_count, const int* __restrict__ mapS_count,
-                              const unsigned long long* __restrict__ prof, UpdateStatus* __restrict__ out) {
+                              const int* __restrict__ fe_status, const unsigned long long* __restrict__ prof,
+                              UpdateStatus* __restrict__ out) {
   constexpr int kWords = (int)(sizeof(LMState) / sizeof(unsigned));
   const unsigned* src = reinterpret_cast<const unsigned*>(lm);
   unsigned* dst = reinterpret_cast<unsigned*>(&out->lm);
@@ -1349,14 +1420,16 @@ __global__ void gather_status(const LMState* __restrict__ lm, const int* __restr
     out->counts[1] = dcnt[1];
     out->counts[2] = *mapE_count;
     out->counts[3] = *mapS_count;
+    out->fe_status = fe_status ? *fe_status : 0;
     out->prof[0] = prof ? prof[0] : 0ull;
     out->prof[1] = prof ? prof[1] : 0ull;
   }
 }
 
 void gather_status_launch(const LMState* lm, const int* dcnt, const int* mapE_count, const int* mapS_count,
-                          const unsigned long long* prof, UpdateStatus* out, hipStream_t st) {
-  hipLaunchKernelGGL(gather_status, dim3(1), dim3(256), 0, st, lm, dcnt, mapE_count, mapS_count, prof, out);
+                          const int* fe_status, const unsigned long long* prof, UpdateStatus* out, hipStream_t st) {
+  hipLaunchKernelGGL(gather_status, dim3(1), dim3(256), 0, st, lm, dcnt, mapE_count, mapS_count, fe_status, prof,
+                     out);
   FLOAM_LAUNCH_CHECK();
 }
 
@@ -1372,32 +1445,41 @@ static void corr_args(const QuerySet& qe, const Grid& ge, const PointRec* mapE, 
 }
 
 template <int G, int U>
-static void knn_launch_t(const LMState* d_st, const QuerySet& qe, const QuerySet& qs, const CorrArgs& E,
+static void knn_launch_t(LMState* d_st, const X7& x0, const double* x0_dev, const QuerySet& qe, const QuerySet& qs, const CorrArgs& E,
                          const CorrArgs& S, const int* d_me, const int* d_ms, int rank, int world, hipStream_t st) {
   const unsigned nbE = std::min(div_up((size_t)std::max(qe.n_ub, 1) * G, kTB), 4096u);
   const unsigned nbS = std::min(div_up((size_t)std::max(qs.n_ub, 1) * G, kTB), 8192u);
-  hipLaunchKernelGGL((knn_kernel<G, U>), dim3(nbE + nbS), dim3(kTB), 0, st, d_st, E, S, (int)nbE, d_me, d_ms, rank,
-                     world);
+  hipLaunchKernelGGL((knn_kernel<G, U>), dim3(nbE + nbS), dim3(kTB), 0, st, d_st, x0, x0_dev, E, S, (int)nbE, d_me,
+                     d_ms, rank, world);
   FLOAM_LAUNCH_CHECK();
 }
 
-void knn_launch(const LMState* d_st, const QuerySet& qe, const Grid& ge, const PointRec* mapE, CorrSet& ce,
-                const QuerySet& qs, const Grid& gs, const PointRec* mapS, CorrSet& cs, const int* d_me,
+void knn_launch(LMState* d_st, const double* x0, const double* x0_dev, const QuerySet& qe, const Grid& ge, const PointRec* mapE,
+                CorrSet& ce, const QuerySet& qs, const Grid& gs, const PointRec* mapS, CorrSet& cs, const int* d_me,
                 const int* d_ms, int rank, int world, hipStream_t st, unsigned long long* dbg) {
   CorrArgs E, S;
   corr_args(qe, ge, mapE, ce, qs, gs, mapS, cs, dbg, E, S);
-  if (qe.n_ub <= 0 && qs.n_ub <= 0) return;
+  X7 x{};
+  if (x0) {
+    for (int k = 0; k < 7; ++k) x.v[k] = x0[k];
+    x.set = 1;
+  }
+  if (qe.n_ub <= 0 && qs.n_ub <= 0) {   // nothing to search: still start the solve
+    hipLaunchKernelGGL(lm_init_dev, dim3(1), dim3(64), 0, st, d_st, x, x0_dev);
+    FLOAM_LAUNCH_CHECK();
+    return;
+  }
   static const int variant = [] {   // FLOAM_KNN_VARIANT: lanes per query x loads in flight (tuning only)
     const char* v = std::getenv("FLOAM_KNN_VARIANT");
     return v ? std::atoi(v) : 0;
   }();
   switch (variant) {
-    case 1: knn_launch_t<8, 4>(d_st, qe, qs, E, S, d_me, d_ms, rank, world, st); break;
-    case 2: knn_launch_t<8, 2>(d_st, qe, qs, E, S, d_me, d_ms, rank, world, st); break;
-    case 3: knn_launch_t<32, 2>(d_st, qe, qs, E, S, d_me, d_ms, rank, world, st); break;
-    case 4: knn_launch_t<16, 2>(d_st, qe, qs, E, S, d_me, d_ms, rank, world, st); break;
-    case 5: knn_launch_t<4, 4>(d_st, qe, qs, E, S, d_me, d_ms, rank, world, st); break;
-    default: knn_launch_t<kGroupDefault, kUnrollDefault>(d_st, qe, qs, E, S, d_me, d_ms, rank, world, st); break;
+    case 1: knn_launch_t<8, 4>(d_st, x, x0_dev, qe, qs, E, S, d_me, d_ms, rank, world, st); break;
+    case 2: knn_launch_t<8, 2>(d_st, x, x0_dev, qe, qs, E, S, d_me, d_ms, rank, world, st); break;
+    case 3: knn_launch_t<32, 2>(d_st, x, x0_dev, qe, qs, E, S, d_me, d_ms, rank, world, st); break;
+    case 4: knn_launch_t<16, 2>(d_st, x, x0_dev, qe, qs, E, S, d_me, d_ms, rank, world, st); break;
+    case 5: knn_launch_t<4, 4>(d_st, x, x0_dev, qe, qs, E, S, d_me, d_ms, rank, world, st); break;
+    default: knn_launch_t<kGroupDefault, kUnrollDefault>(d_st, x, x0_dev, qe, qs, E, S, d_me, d_ms, rank, world, st); break;
   }
 }
 
@@ -1430,8 +1512,11 @@ void knn_traffic_launch(const LMState* d_st, const QuerySet& q, const Grid& g, c
 
 int lm_eval_launch(const LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const CorrSet& cs,
                    const int* d_ns, int ns_ub, bool huber, double* partials, hipStream_t st) {
-  const int total = std::max(ne_ub + ns_ub, 1);
-  const int nblk = (int)std::min<unsigned>(div_up(total, kTB), kEvalBlocks);
+  // a fixed evaluation grid: the partition of the records over blocks (hence the fixed reduction order) must not
+  // depend on the host's upper bounds, only on the device counts
+  const int nblk = (int)kEvalBlocks;
+  (void)ne_ub;
+  (void)ns_ub;
   hipLaunchKernelGGL(lm_eval, dim3(nblk), dim3(kTB), 0, st, d_st, ce.rec.p, ce.valid.p, ce.cap, d_ne, ne_ub,
                      cs.rec.p, cs.valid.p, cs.cap, d_ns, ns_ub, huber ? 1 : 0, partials);
   FLOAM_LAUNCH_CHECK();
@@ -1441,8 +1526,11 @@ int lm_eval_launch(const LMState* d_st, const CorrSet& ce, const int* d_ne, int 
 void lm_step_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const CorrSet& cs,
                     const int* d_ns, int ns_ub, bool huber, double* partials, unsigned* counter, hipStream_t st,
                     unsigned long long* dbg) {
-  const int total = std::max(ne_ub + ns_ub, 1);
-  const int nblk = (int)std::min<unsigned>(div_up(total, kTB), kEvalBlocks);
+  // a fixed evaluation grid: the partition of the records over blocks (hence the fixed reduction order) must not
+  // depend on the host's upper bounds, only on the device counts
+  const int nblk = (int)kEvalBlocks;
+  (void)ne_ub;
+  (void)ns_ub;
   hipLaunchKernelGGL(lm_step, dim3(nblk + 1), dim3(kTB), 0, st, d_st, ce.rec.p, ce.valid.p, ce.cap, d_ne, ne_ub,
                      cs.rec.p, cs.valid.p, cs.cap, d_ns, ns_ub, huber ? 1 : 0, partials, counter, dbg);
   FLOAM_LAUNCH_CHECK();

@@ -1,6 +1,7 @@
 #pragma once
 #include "cloud_ops.hpp"
 #include "floam_common.hpp"
+#include "pose.hpp"
 
 namespace floam {
 
@@ -30,9 +31,13 @@ struct Grid {
   DevBuf<FineCell> fine;
   DevBuf<CoarseCell> coarse;
   DevBuf<uint2> where;       // per map point: coarse slot, sub-cell << 28 | rank in the sub-cell
-  DevBuf<int> cursor;        // bump allocator
+  // occupied slots of the coarse / fine table, per build parity: the next build clears exactly these entries
+  DevBuf<int> clist[2], flist[2];
+  DevBuf<int> counters;      // [0] bump cursor, [1..2] coarse list sizes, [3..4] fine list sizes (by parity)
   int bits = 0;              // table size = 1 << bits (both tables)
   unsigned mask = 0;
+  int parity = 0;
+  bool fresh = true;         // tables (re)allocated: the next clear is a full one
 };
 
 // Rebuild the grids of both local maps (corner and surf) in four launches.
@@ -99,15 +104,25 @@ void lm_init_launch(LMState* d_st, const double* x0, hipStream_t st);
 struct UpdateStatus {
   LMState lm;
   int counts[4];                  // downsampled edge, surf; corner map, surf map
+  int fe_status;                  // status flags of the feature extraction that produced the inputs (async FE)
+  int pad;
   unsigned long long prof[2];     // algorithmic bytes of the kNN launches (profiling)
 };
 void gather_status_launch(const LMState* lm, const int* dcnt, const int* mapE_count, const int* mapS_count,
-                          const unsigned long long* prof, UpdateStatus* out, hipStream_t st);
+                          const int* fe_status, const unsigned long long* prof, UpdateStatus* out, hipStream_t st);
+
+// Between the two updatePointsToMap calls of a deskewed UpdatePointsToMapSelector (odomEstimationClass.cpp:40-46),
+// without a host round trip: GetVelocity from the first call's result (x1 = st->x) and the pose before it (odom0),
+// CompensateVelocity of both clouds in place (dataHandler.cpp:82-92, Q5), and the second call's prediction
+// odom1 * (odom0^-1 * odom1) as parameters {q, t} into x0_out (same algebra as the host, pose.hpp).
+void deskew_bridge_launch(const LMState* st, const Pose& odom0, double scan_period, PointRec* edge, const int* d_ne,
+                          int ne_ub, PointRec* surf, const int* d_ns, int ns_ub, double* x0_out, hipStream_t stream);
 // Correspondence search for the edge and the surf query sets at the pose in st->x, in two launches:
 // knn_launch — exact 5-NN (blocks [0, nbE) edge queries against the corner map, the rest surf against the surf map);
 // geom_launch — fp64 line / plane fits and the residual records.
-void knn_launch(const LMState* d_st, const QuerySet& qe, const Grid& ge, const PointRec* mapE, CorrSet& ce,
-                const QuerySet& qs, const Grid& gs, const PointRec* mapS, CorrSet& cs, const int* d_me,
+// knn_launch also starts the solve (the former lm_init): LM state reset, x = x0 when x0 != null (7 doubles, by value)
+void knn_launch(LMState* d_st, const double* x0, const double* x0_dev, const QuerySet& qe, const Grid& ge, const PointRec* mapE,
+                CorrSet& ce, const QuerySet& qs, const Grid& gs, const PointRec* mapS, CorrSet& cs, const int* d_me,
                 const int* d_ms, int rank, int world, hipStream_t st, unsigned long long* dbg = nullptr);
 void geom_launch(LMState* d_st, const QuerySet& qe, const Grid& ge, const PointRec* mapE, CorrSet& ce,
                  const QuerySet& qs, const Grid& gs, const PointRec* mapS, CorrSet& cs, hipStream_t st);

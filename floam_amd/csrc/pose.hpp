@@ -1,6 +1,10 @@
-// Host-side rigid-transform algebra used by the odometry controller (Eigen::Isometry3d / Quaterniond semantics
-// as the reference uses them: src/odomEstimationClass.cpp:62-71, 114-116, 320-343).
+// Rigid-transform algebra of the odometry controller (Eigen::Isometry3d / Quaterniond semantics as the reference
+// uses them: src/odomEstimationClass.cpp:62-71, 114-116, 320-343).  Host and device share these definitions so the
+// prediction the device forms between the two updatePointsToMap calls of a deskewed scan is bit-identical to the
+// host's (both built with -ffp-contract=off; only +, *, / and sqrt, all correctly rounded in IEEE double).
 #pragma once
+#include <hip/hip_runtime.h>
+
 #include <cmath>
 
 namespace floam {
@@ -13,27 +17,27 @@ struct Pose {   // rotation matrix + translation (Eigen::Isometry3d)
   double t[3];
 };
 
-inline Mat3 mat_identity() {
+__host__ __device__ inline Mat3 mat_identity() {
   Mat3 r{};
   r.m[0][0] = r.m[1][1] = r.m[2][2] = 1.0;
   return r;
 }
-inline Pose pose_identity() {
+__host__ __device__ inline Pose pose_identity() {
   Pose p;
   p.R = mat_identity();
   p.t[0] = p.t[1] = p.t[2] = 0.0;
   return p;
 }
-inline Mat3 mat_mul(const Mat3& a, const Mat3& b) {
+__host__ __device__ inline Mat3 mat_mul(const Mat3& a, const Mat3& b) {
   Mat3 r;
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) r.m[i][j] = a.m[i][0] * b.m[0][j] + a.m[i][1] * b.m[1][j] + a.m[i][2] * b.m[2][j];
   return r;
 }
-inline void mat_vec(const Mat3& a, const double v[3], double o[3]) {
+__host__ __device__ inline void mat_vec(const Mat3& a, const double v[3], double o[3]) {
   for (int i = 0; i < 3; ++i) o[i] = a.m[i][0] * v[0] + a.m[i][1] * v[1] + a.m[i][2] * v[2];
 }
-inline Pose pose_mul(const Pose& a, const Pose& b) {
+__host__ __device__ inline Pose pose_mul(const Pose& a, const Pose& b) {
   Pose r;
   r.R = mat_mul(a.R, b.R);
   double v[3];
@@ -41,7 +45,7 @@ inline Pose pose_mul(const Pose& a, const Pose& b) {
   for (int i = 0; i < 3; ++i) r.t[i] = v[i] + a.t[i];
   return r;
 }
-inline Pose pose_inverse(const Pose& a) {
+__host__ __device__ inline Pose pose_inverse(const Pose& a) {
   Pose r;
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) r.R.m[i][j] = a.R.m[j][i];
@@ -51,7 +55,7 @@ inline Pose pose_inverse(const Pose& a) {
   return r;
 }
 // Quaternion (x, y, z, w) -> rotation matrix (Eigen QuaternionBase::toRotationMatrix)
-inline Mat3 quat_to_mat(const double q[4]) {
+__host__ __device__ inline Mat3 quat_to_mat(const double q[4]) {
   const double x = q[0], y = q[1], z = q[2], w = q[3];
   const double tx = 2 * x, ty = 2 * y, tz = 2 * z;
   const double twx = tx * w, twy = ty * w, twz = tz * w;
@@ -64,10 +68,10 @@ inline Mat3 quat_to_mat(const double q[4]) {
   return r;
 }
 // Rotation matrix -> quaternion (x, y, z, w) (Eigen quaternionbase_assign_impl, Shepperd's method)
-inline void mat_to_quat(const Mat3& a, double q[4]) {
+__host__ __device__ inline void mat_to_quat(const Mat3& a, double q[4]) {
   double t = a.m[0][0] + a.m[1][1] + a.m[2][2];
   if (t > 0) {
-    t = std::sqrt(t + 1.0);
+    t = sqrt(t + 1.0);
     q[3] = 0.5 * t;
     t = 0.5 / t;
     q[0] = (a.m[2][1] - a.m[1][2]) * t;
@@ -78,7 +82,7 @@ inline void mat_to_quat(const Mat3& a, double q[4]) {
     if (a.m[1][1] > a.m[0][0]) i = 1;
     if (a.m[2][2] > a.m[i][i]) i = 2;
     const int j = (i + 1) % 3, k = (j + 1) % 3;
-    t = std::sqrt(a.m[i][i] - a.m[j][j] - a.m[k][k] + 1.0);
+    t = sqrt(a.m[i][i] - a.m[j][j] - a.m[k][k] + 1.0);
     double c[3];
     c[i] = 0.5 * t;
     t = 0.5 / t;
@@ -92,7 +96,7 @@ inline void mat_to_quat(const Mat3& a, double q[4]) {
 inline double rotation_angle(const Mat3& R) {
   double q[4];
   mat_to_quat(R, q);
-  const double n = std::sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2]);
+  const double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2]);
   if (n == 0) return 0.0;
   return 2.0 * std::atan2(n, std::fabs(q[3]));
 }

@@ -184,6 +184,34 @@ __global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B,
     s_key[k] = (i >= 0 && i < total) ? keys[i] : 0xFFFFFFFFu;
   }
   __syncthreads();
+  // gather every element's point (x, y, z, intensity) of the tile into LDS: one parallel round trip, issued
+  // before the lookback wait so the two latencies overlap; the runs are then summed from LDS
+  __shared__ float4 s_pt[kTile];
+  const int nA0 = *A.d_n0, nA1 = A.d_n1 ? *A.d_n1 : 0, nB0 = *B.d_n0, nB1 = B.d_n1 ? *B.d_n1 : 0;
+  const int4* __restrict__ vals4 = reinterpret_cast<const int4*>(vals);
+  {
+    const int k0 = threadIdx.x * kPerThread;
+    int v[kPerThread];
+    if (t0 + k0 + kPerThread <= total) {
+      const int4 vv = vals4[(t0 + k0) / kPerThread];
+      v[0] = vv.x; v[1] = vv.y; v[2] = vv.z; v[3] = vv.w;
+    } else {
+#pragma unroll
+      for (int u = 0; u < kPerThread; ++u) v[u] = t0 + k0 + u < total ? vals[t0 + k0 + u] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kPerThread; ++u) {
+      const uint32_t key = s_key[k0 + u + 1];
+      float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (key != 0xFFFFFFFFu) {
+        PointRec p;
+        if (key >> 31) vox_fetch(B, nB0, nB1, v[u], p);
+        else vox_fetch(A, nA0, nA1, v[u], p);
+        q = make_float4(p.x, p.y, p.z, p.intensity);
+      }
+      s_pt[k0 + u] = q;
+    }
+  }
   // heads in this thread's 4 consecutive elements
   int cnt[2] = {0, 0};
   unsigned headmask = 0;
@@ -235,22 +263,26 @@ __global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B,
     const uint32_t key = s_key[k + 1];
     const int job = (int)(key >> 31);
     const VoxelJobDev& J = job == 0 ? A : B;
-    const int n0 = *J.d_n0, n1 = J.d_n1 ? *J.d_n1 : 0;
-    PointRec f;
-    vox_fetch(J, n0, n1, vals[i], f);
+    const int n0 = job ? nB0 : nA0, n1 = job ? nB1 : nA1;
     PointRec o;
-    if (ovf[job]) {
-      o = f;
+    if (ovf[job]) {   // input returned unchanged: the whole record
+      vox_fetch(J, n0, n1, vals[i], o);
     } else {
-      float c0 = f.x, c1 = f.y, c2 = f.z, c3 = f.intensity;
+      const float4 f = s_pt[k];
+      float c0 = f.x, c1 = f.y, c2 = f.z, c3 = f.w;
       int j = i + 1;
       for (; j < total; ++j) {
         const int kj = j - t0;
-        const uint32_t kk = kj <= kTile - 1 ? s_key[kj + 1] : keys[j];
-        if (kk != key) break;
-        PointRec p;
-        vox_fetch(J, n0, n1, vals[j], p);
-        c0 += p.x; c1 += p.y; c2 += p.z; c3 += p.intensity;
+        if (kj < kTile) {
+          if (s_key[kj + 1] != key) break;
+          const float4 p = s_pt[kj];
+          c0 += p.x; c1 += p.y; c2 += p.z; c3 += p.w;
+        } else {   // run continues past the tile (rare)
+          if (keys[j] != key) break;
+          PointRec p;
+          vox_fetch(J, n0, n1, vals[j], p);
+          c0 += p.x; c1 += p.y; c2 += p.z; c3 += p.intensity;
+        }
       }
       const float cn = (float)(j - i);
       o.x = c0 / cn; o.y = c1 / cn; o.z = c2 / cn; o.pad0 = 1.0f;

@@ -43,9 +43,13 @@ class LidarParams:
 
 
 class LaserProcessingClass:
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, asynchronous: bool = False):
+        """asynchronous=True: featureExtraction does not synchronise (floam_lp_set_async); output sizes stay on the
+        device and input-validation errors surface at the next odometry update that consumes the clouds (or at
+        wait()).  Default False: the reference's synchronous behaviour."""
         self._L = _ffi.load()
         self.device = device
+        self.asynchronous = asynchronous
         self._h = None
 
     def init(self, lidar_param: LidarParams) -> None:
@@ -55,6 +59,13 @@ class LaserProcessingClass:
         p = lidar_param.to_c()
         _ffi.check(self._L.floam_lp_create(C.byref(p), self.device, C.byref(h)))
         self._h = h
+        if self.asynchronous:
+            _ffi.check(self._L.floam_lp_set_async(self._h, 1))
+
+    def wait(self) -> None:
+        """Synchronise and raise the validation error of the last asynchronous featureExtraction, if any."""
+        if self._h is not None:
+            _ffi.check(self._L.floam_lp_wait(self._h))
 
     def featureExtraction(self, pc_in: DeviceCloud, pc_out_edge: DeviceCloud, pc_out_surf: DeviceCloud) -> None:
         """LaserProcessingClass::featureExtraction (src/laserProcessingClass.cpp:72-118): appends edge / surf

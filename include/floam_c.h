@@ -85,6 +85,12 @@ floam_status floam_lp_destroy(floam_lp* lp);
 /* featureExtraction(pc_in, pc_out_edge, pc_out_surf) (include/laserProcessingClass.h:40,
  * src/laserProcessingClass.cpp:72-118).  Appends to edge/surf like the reference (never clears them). */
 floam_status floam_lp_feature_extraction(floam_lp* lp, const floam_cloud* in, floam_cloud* edge, floam_cloud* surf);
+/* Asynchronous mode (extension, default off): featureExtraction returns without synchronising; the output counts
+ * stay on the device (the odometry sizes its work from upper bounds) and the input-validation flags travel with
+ * the output clouds, so an out-of-range ring or an over-long sector is reported by the next odometry update that
+ * consumes them, or by floam_lp_wait. */
+floam_status floam_lp_set_async(floam_lp* lp, int async);
+floam_status floam_lp_wait(floam_lp* lp);
 
 /* -------------------------------------------------------------------------------- OdomEstimationClass */
 typedef struct floam_odom floam_odom;

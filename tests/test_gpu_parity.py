@@ -87,14 +87,14 @@ def _angle_between(q1, q2):
     return 2.0 * math.acos(min(1.0, d))
 
 
-def _run_sequence(floam_gpu, oracle_lib, config, nscan, loss="Cauchy", deskew=True):
+def _run_sequence(floam_gpu, oracle_lib, config, nscan, loss="Cauchy", deskew=True, asynchronous=False):
     from floam_amd.odom_estimation import reset_process_state
     R = synth.lidar_model(config).rings
     odo_ref = oracle_lib.Odometry(R, 0.1, 0.5, 90.0, 0.1, loss, stable_voxel=True)
     oracle_lib.reset_process_statics()
     reset_process_state()
     p = _params(R)
-    lp = floam_gpu.LaserProcessingClass()
+    lp = floam_gpu.LaserProcessingClass(asynchronous=asynchronous)
     lp.init(p)
     odo = floam_gpu.OdomEstimationClass()
     odo.init(p, 0.1, loss)
@@ -115,7 +115,7 @@ def _run_sequence(floam_gpu, oracle_lib, config, nscan, loss="Cauchy", deskew=Tr
                 _assert_same_cloud(de.download(), e_ref, f"deskewed edge scan {k}")
         qr, tr = odo_ref.pose()
         qg, tg = odo.pose()
-        out.append((k, np.linalg.norm(tr - tg), _angle_between(qr, qg), odo.stats(), odo_ref))
+        out.append((k, np.linalg.norm(tr - tg), _angle_between(qr, qg), odo.stats(), (qg, tg)))
     return out, odo, odo_ref
 
 
@@ -132,6 +132,41 @@ def test_odometry_sequence_c1(floam_gpu, oracle_lib, loss):
     for g, r in ((ge, re_), (gs, rs)):
         d = np.abs(np.stack([g["x"] - r["x"], g["y"] - r["y"], g["z"] - r["z"]]))
         assert d.max() < 1e-4, d.max()
+
+
+def test_odometry_async_feature_extraction(floam_gpu, oracle_lib):
+    """featureExtraction without synchronisation (counts stay on the device, one sync per scan in the selector)
+    gives bit-identical poses."""
+    sync, _, _ = _run_sequence(floam_gpu, oracle_lib, "c1", 6)
+    asyn, _, _ = _run_sequence(floam_gpu, oracle_lib, "c1", 6, asynchronous=True)
+    for a, b in zip(sync, asyn):
+        np.testing.assert_array_equal(a[4][0], b[4][0])
+        np.testing.assert_array_equal(a[4][1], b[4][1])
+
+
+def test_async_feature_extraction_error_surfaces(floam_gpu):
+    """An out-of-range ring (UB in the reference) is reported by the consumer in asynchronous mode."""
+    from floam_amd import FloamError
+    raw = synth.generate_scan("c1", 1)
+    raw["ring"][100] = 40   # num_lines = 16
+    lp = floam_gpu.LaserProcessingClass(asynchronous=True)
+    lp.init(_params(16))
+    de, ds = floam_gpu.DeviceCloud(), floam_gpu.DeviceCloud()
+    lp.featureExtraction(floam_gpu.DeviceCloud(raw), de, ds)   # returns without synchronising
+    with pytest.raises(FloamError):
+        lp.wait()
+    odo = floam_gpu.OdomEstimationClass()
+    odo.init(_params(16), 0.1, "Cauchy")
+    good = synth.generate_scan("c1", 0)
+    ge, gs = floam_gpu.DeviceCloud(), floam_gpu.DeviceCloud()
+    lp2 = floam_gpu.LaserProcessingClass()
+    lp2.init(_params(16))
+    lp2.featureExtraction(floam_gpu.DeviceCloud(good), ge, gs)
+    odo.initMapWithPoints(ge, gs)
+    de, ds = floam_gpu.DeviceCloud(), floam_gpu.DeviceCloud()
+    lp.featureExtraction(floam_gpu.DeviceCloud(raw), de, ds)
+    with pytest.raises(FloamError):
+        odo.UpdatePointsToMapSelector(de, ds, True)
 
 
 def test_odometry_no_deskew(floam_gpu, oracle_lib):
