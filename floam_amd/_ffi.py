@@ -29,6 +29,7 @@ EXPORTS = [
     "floam_cloud_create", "floam_cloud_destroy", "floam_cloud_upload", "floam_cloud_download", "floam_cloud_size",
     "floam_cloud_clear", "floam_cloud_copy", "floam_cloud_device_ptr",
     "floam_lp_create", "floam_lp_destroy", "floam_lp_feature_extraction", "floam_lp_set_async", "floam_lp_wait",
+    "floam_voxel_grid",
     "floam_odom_create", "floam_odom_destroy", "floam_odom_init_map", "floam_odom_update_selector",
     "floam_odom_update", "floam_odom_get_pose", "floam_odom_get_last_pose", "floam_odom_get_velocity",
     "floam_odom_get_map", "floam_odom_get_map_sizes", "floam_odom_download_maps", "floam_odom_get_stats",
@@ -87,6 +88,7 @@ def load(path: str | None = None):
         "floam_cloud_size": [vp, szp], "floam_cloud_clear": [vp], "floam_cloud_copy": [vp, vp],
         "floam_lp_create": [C.POINTER(LidarParams), i32, pp], "floam_lp_destroy": [vp],
         "floam_lp_feature_extraction": [vp, vp, vp, vp], "floam_lp_set_async": [vp, i32], "floam_lp_wait": [vp],
+        "floam_voxel_grid": [vp, C.c_float, vp],
         "floam_odom_create": [C.POINTER(LidarParams), dbl, C.c_char_p, i32, pp], "floam_odom_destroy": [vp],
         "floam_odom_init_map": [vp, vp, vp], "floam_odom_update_selector": [vp, vp, vp, i32],
         "floam_odom_update": [vp, vp, vp, i32], "floam_odom_get_pose": [vp, dp, dp],

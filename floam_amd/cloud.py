@@ -49,6 +49,12 @@ class DeviceCloud:
     def copy_from(self, other: "DeviceCloud") -> None:
         _ffi.check(self._L.floam_cloud_copy(self._h, other._h))
 
+    def voxel_grid(self, leaf: float, out: "DeviceCloud | None" = None) -> "DeviceCloud":
+        """pcl::VoxelGrid with a cubic leaf (PCL 1.8.1 semantics) into ``out`` (a new cloud by default)."""
+        out = out if out is not None else DeviceCloud(device=self.device)
+        _ffi.check(self._L.floam_voxel_grid(self._h, C.c_float(leaf), out._h))
+        return out
+
     def device_ptr(self) -> int:
         return self._L.floam_cloud_device_ptr(self._h) or 0
 

@@ -41,6 +41,8 @@ struct PendingTiming {
 struct DeviceCtx {
   int device = 0;
   hipStream_t stream = nullptr;
+  VoxelScratch2 vs;           // standalone floam_voxel_grid
+  DevBuf<int> zero;           // a device 0 (empty second job)
   int profile = 0;   // bitmask of FLOAM_PROF_* categories
   std::vector<PendingTiming> pending;
   std::vector<hipEvent_t> free_events;
@@ -125,6 +127,7 @@ static size_t cloud_count_sync(const floam_cloud* c) {
   int v = 0;
   FLOAM_HIP(hipMemcpyAsync(&v, c->count.p, sizeof(int), hipMemcpyDeviceToHost, ctx.stream));
   FLOAM_HIP(hipStreamSynchronize(ctx.stream));
+  if (v < 0) throw Error(FLOAM_ERR_DEVICE, "device-side compaction failed (lookback timeout)");
   auto* mc = const_cast<floam_cloud*>(c);
   mc->host_count = (size_t)v;
   mc->host_count_valid = true;
@@ -643,6 +646,33 @@ floam_status floam_cloud_copy(floam_cloud* dst, const floam_cloud* src) {
 }
 
 void* floam_cloud_device_ptr(floam_cloud* c) { return c ? c->pts.p : nullptr; }
+
+floam_status floam_voxel_grid(const floam_cloud* in, float leaf, floam_cloud* out) {
+  return guarded([&] {
+    if (!in || !out || in == out) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null or aliased cloud");
+    if (in->device != out->device) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "clouds on different devices");
+    if (!(leaf > 0.0f)) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "leaf size must be > 0");
+    DeviceCtx& ctx = ctx_for(in->device);
+    FLOAM_HIP(hipSetDevice(in->device));
+    const size_t n = cloud_ub(in);
+    if (n > (size_t)INT32_MAX / 2) throw Error(FLOAM_ERR_UNSUPPORTED, "cloud too large");
+    cloud_reserve(out, std::max<size_t>(n, 1), 0, ctx.stream);
+    if (!ctx.zero.p) {
+      ctx.zero.reserve(2);
+      FLOAM_HIP(hipMemsetAsync(ctx.zero.p, 0, sizeof(int) * 2, ctx.stream));
+    }
+    VoxelJob a, b;
+    a.part0 = in->pts.p; a.d_n0 = in->count.p; a.n0_ub = (int)n; a.leaf = leaf;
+    a.out = out->pts.p; a.d_out = out->count.p;
+    b.part0 = in->pts.p; b.d_n0 = ctx.zero.p; b.n0_ub = 0; b.leaf = leaf;
+    b.out = out->pts.p; b.d_out = ctx.zero.p + 1;   // the empty job's count lands in a scratch word
+    ctx.vs.s.reserve(1);
+    voxel2_launch(ctx.vs, a, b, ctx.stream);
+    out->host_count_valid = false;
+    out->ub = n;
+    return FLOAM_OK;
+  });
+}
 
 // ------------------------------------------------------------------------------------------ laser processing
 floam_status floam_lp_create(const floam_lidar_params* p, int device, floam_lp** out) {

@@ -178,12 +178,27 @@ __global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B,
   const int tile = lookback_ticket(ticket);
   const int ntiles = (int)gridDim.x;
   const int t0 = tile * kTile;
-  __shared__ uint32_t s_key[kTile + 1];
-  for (int k = threadIdx.x; k <= kTile; k += blockDim.x) {
+  // s_key[k] = key of element t0 - 1 + k, k in [0, kTile + 1]
+  __shared__ uint32_t s_key[kTile + 2];
+  for (int k = threadIdx.x; k <= kTile + 1; k += blockDim.x) {
     const int i = t0 - 1 + k;
     s_key[k] = (i >= 0 && i < total) ? keys[i] : 0xFFFFFFFFu;
   }
   __syncthreads();
+  // run tails of the tile as a bitmask: bit k set if element t0 + k is the last of its run
+  __shared__ unsigned s_tail[kTile / 32];
+  {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int r = 0; r < kTile / kTB; ++r) {
+      const int k = r * kTB + threadIdx.x;
+      const unsigned long long b = __ballot(s_key[k + 1] != s_key[k + 2]);
+      if (lane == 0) {
+        s_tail[(r * kTB + w * 64) / 32] = (unsigned)b;
+        s_tail[(r * kTB + w * 64) / 32 + 1] = (unsigned)(b >> 32);
+      }
+    }
+  }
   // gather every element's point (x, y, z, intensity) of the tile into LDS: one parallel round trip, issued
   // before the lookback wait so the two latencies overlap; the runs are then summed from LDS
   __shared__ float4 s_pt[kTile];
@@ -255,6 +270,11 @@ __global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B,
   }
   int pos[2] = {pre.a + wb[0] + inc[0] - cnt[0], pre.b + wb[1] + inc[1] - cnt[1]};
   const int ovf[2] = {overflow[0], overflow[1]};
+  // the run that crosses the tile end (at most one): its head's partial sums, finished cooperatively below
+  __shared__ float s_cross[4];
+  __shared__ int s_cross_pos, s_cross_head, s_cross_job;
+  if (threadIdx.x == 0) s_cross_head = -1;
+  __syncthreads();
 #pragma unroll
   for (int u = 0; u < kPerThread; ++u) {
     if (!(headmask & (1u << u))) continue;
@@ -263,33 +283,83 @@ __global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B,
     const uint32_t key = s_key[k + 1];
     const int job = (int)(key >> 31);
     const VoxelJobDev& J = job == 0 ? A : B;
-    const int n0 = job ? nB0 : nA0, n1 = job ? nB1 : nA1;
-    PointRec o;
     if (ovf[job]) {   // input returned unchanged: the whole record
-      vox_fetch(J, n0, n1, vals[i], o);
-    } else {
-      const float4 f = s_pt[k];
-      float c0 = f.x, c1 = f.y, c2 = f.z, c3 = f.w;
-      int j = i + 1;
-      for (; j < total; ++j) {
-        const int kj = j - t0;
-        if (kj < kTile) {
-          if (s_key[kj + 1] != key) break;
-          const float4 p = s_pt[kj];
-          c0 += p.x; c1 += p.y; c2 += p.z; c3 += p.w;
-        } else {   // run continues past the tile (rare)
-          if (keys[j] != key) break;
-          PointRec p;
-          vox_fetch(J, n0, n1, vals[j], p);
-          c0 += p.x; c1 += p.y; c2 += p.z; c3 += p.intensity;
-        }
-      }
-      const float cn = (float)(j - i);
-      o.x = c0 / cn; o.y = c1 / cn; o.z = c2 / cn; o.pad0 = 1.0f;
-      o.intensity = c3 / cn;
-      o.ring = 0; o.pad1 = 0; o.time = 0.0f; o.pad2 = 0.0f;
+      PointRec o;
+      vox_fetch(J, job ? nB0 : nA0, job ? nB1 : nA1, vals[i], o);
+      J.out[pos[job]++] = o;
+      continue;
     }
+    // run end: the next tail at or after k (bitmask search), or the tile end
+    int end = kTile;
+    for (int wd = k >> 5; wd < kTile / 32; ++wd) {
+      unsigned m = s_tail[wd];
+      if (wd == (k >> 5)) m &= ~0u << (k & 31);
+      if (m) {
+        end = wd * 32 + __ffs(m);   // one past the tail
+        break;
+      }
+    }
+    const float4 f = s_pt[k];
+    float c0 = f.x, c1 = f.y, c2 = f.z, c3 = f.w;
+    for (int j = k + 1; j < end; ++j) {   // sequential sum in sorted (= input) order
+      const float4 p = s_pt[j];
+      c0 += p.x; c1 += p.y; c2 += p.z; c3 += p.w;
+    }
+    const bool crosses = end == kTile && t0 + kTile < total && s_key[kTile + 1] == key;
+    if (crosses) {
+      s_cross[0] = c0; s_cross[1] = c1; s_cross[2] = c2; s_cross[3] = c3;
+      s_cross_pos = pos[job]++;
+      s_cross_head = i;
+      s_cross_job = job;
+      continue;
+    }
+    const float cn = (float)(t0 + end - i);
+    PointRec o;
+    o.x = c0 / cn; o.y = c1 / cn; o.z = c2 / cn; o.pad0 = 1.0f;
+    o.intensity = c3 / cn;
+    o.ring = 0; o.pad1 = 0; o.time = 0.0f; o.pad2 = 0.0f;
     J.out[pos[job]++] = o;
+  }
+  __syncthreads();
+  if (s_cross_head >= 0) {   // block-uniform: gather the run's continuation chunk by chunk, thread 0 sums in order
+    const int job = s_cross_job;
+    const VoxelJobDev& J = job == 0 ? A : B;
+    const uint32_t key = s_key[kTile];   // the tile's last element belongs to the crossing run
+    const int n0 = job ? nB0 : nA0, n1 = job ? nB1 : nA1;
+    __shared__ int s_done;
+    int j0 = t0 + kTile;
+    for (;;) {
+      const int j = j0 + threadIdx.x;
+      const bool in = j < total && keys[j] == key;
+      float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (in) {
+        PointRec p;
+        vox_fetch(J, n0, n1, vals[j], p);
+        q = make_float4(p.x, p.y, p.z, p.intensity);
+      }
+      s_pt[threadIdx.x] = q;
+      const int nin = __syncthreads_count(in);   // the run is a prefix of the chunk
+      if (threadIdx.x == 0) {
+        float c0 = s_cross[0], c1 = s_cross[1], c2 = s_cross[2], c3 = s_cross[3];
+        for (int r = 0; r < nin; ++r) {
+          const float4 p = s_pt[r];
+          c0 += p.x; c1 += p.y; c2 += p.z; c3 += p.w;
+        }
+        s_cross[0] = c0; s_cross[1] = c1; s_cross[2] = c2; s_cross[3] = c3;
+        s_done = nin < (int)blockDim.x;
+      }
+      __syncthreads();
+      j0 += nin;
+      if (s_done) break;
+    }
+    if (threadIdx.x == 0) {
+      const float cn = (float)(j0 - s_cross_head);
+      PointRec o;
+      o.x = s_cross[0] / cn; o.y = s_cross[1] / cn; o.z = s_cross[2] / cn; o.pad0 = 1.0f;
+      o.intensity = s_cross[3] / cn;
+      o.ring = 0; o.pad1 = 0; o.time = 0.0f; o.pad2 = 0.0f;
+      J.out[s_cross_pos] = o;
+    }
   }
   if (tile == ntiles - 1 && threadIdx.x == 0) {
     *A.d_out = pre.a + agg[0];
@@ -307,7 +377,12 @@ void voxel2_launch(VoxelScratch2& sc, const VoxelJob& a, const VoxelJob& b, hipS
   const VoxelJobDev A = to_dev(a, 0);
   const VoxelJobDev B = to_dev(b, a.n0_ub + (a.part1 ? a.n1_ub : 0));
   const int total = B.base + b.n0_ub + (b.part1 ? b.n1_ub : 0);
-  const int n = std::max(total, 1);
+  if (total == 0) {   // both clouds empty
+    FLOAM_HIP(hipMemsetAsync(a.d_out, 0, sizeof(int), st));
+    FLOAM_HIP(hipMemsetAsync(b.d_out, 0, sizeof(int), st));
+    return;
+  }
+  const int n = total;
   sc.s.reserve(n);
   sc.partials.reserve(2 * kMinMaxBlocks * 6);
   sc.overflow.reserve(2);

@@ -85,6 +85,11 @@ floam_status floam_lp_destroy(floam_lp* lp);
 /* featureExtraction(pc_in, pc_out_edge, pc_out_surf) (include/laserProcessingClass.h:40,
  * src/laserProcessingClass.cpp:72-118).  Appends to edge/surf like the reference (never clears them). */
 floam_status floam_lp_feature_extraction(floam_lp* lp, const floam_cloud* in, floam_cloud* edge, floam_cloud* surf);
+/* pcl::VoxelGrid<PointXYZI> with a cubic leaf (PCL 1.8.1 semantics; the filter of downSamplingToMap,
+ * src/odomEstimationClass.cpp:137-142, and of the mapping node, src/laserMappingClass.cpp:174-183): one centroid
+ * of x, y, z, intensity per occupied voxel in ascending voxel index, the input returned unchanged when the index
+ * range overflows int.  Within-voxel summation in input order.  out is overwritten; asynchronous. */
+floam_status floam_voxel_grid(const floam_cloud* in, float leaf, floam_cloud* out);
 /* Asynchronous mode (extension, default off): featureExtraction returns without synchronising; the output counts
  * stay on the device (the odometry sizes its work from upper bounds) and the input-validation flags travel with
  * the output clouds, so an out-of-range ring or an over-long sector is reported by the next odometry update that
