@@ -84,7 +84,7 @@ def hbm_traffic(kernel_substr):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--config", default="c3")
     ap.add_argument("--mode", choices=["shard", "replica"], default="shard")

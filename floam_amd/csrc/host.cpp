@@ -206,6 +206,12 @@ struct floam_odom {
   CorrSet ce, cs;
   DevBuf<double> partials, sums;
   DevBuf<unsigned> step_counter;
+  DevBuf<unsigned long long> lm_go;     // lm_solve hand-off word
+  DevBuf<double> lm_point;              // lm_solve: the evaluation point released to the evaluation blocks
+  unsigned long long lm_epoch = 0;
+  int lm_mode = 0;   // FLOAM_LM_MODE: 0 lm_step_gram (squared loss), 1 resident lm_solve, 2 per-record lm_step
+  DevBuf<double> gpart;                 // per-block surf Gram partials
+  DevBuf<double> gmat;                  // the solve's surf Gram matrix + its origin
   DevBuf<unsigned long long> dbg_stamps;   // FLOAM_DEBUG_STAMPS=1: lm_step segment times (diagnostic)
   DevBuf<LMState> lm;
   DevBuf<UpdateStatus> ustat;     // slot 0: first / only call, slot 1: second call of a deskewed selector
@@ -338,6 +344,11 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
   if (!o->step_counter.p) {
     o->step_counter.reserve(1);
     FLOAM_HIP(hipMemsetAsync(o->step_counter.p, 0, sizeof(unsigned), st));
+    o->lm_go.reserve(1);
+    o->lm_point.reserve(8);
+    FLOAM_HIP(hipMemsetAsync(o->lm_go.p, 0, sizeof(unsigned long long), st));
+    const char* pe = std::getenv("FLOAM_LM_MODE");
+    o->lm_mode = pe ? std::atoi(pe) : 0;
     if (std::getenv("FLOAM_DEBUG_STAMPS")) {
       o->dbg_stamps.reserve(32);
       FLOAM_HIP(hipMemsetAsync(o->dbg_stamps.p, 0, sizeof(unsigned long long) * 32, st));
@@ -352,6 +363,12 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
   const QuerySet qe{o->dE.p, o->cnt.p + 0, ne_ub};
   const QuerySet qs{o->dS.p, o->cnt.p + 1, ns_ub};
   const bool sharded = o->world > 1;
+  // the single-block Gram solve (squared loss, bounded edge count); else one launch per evaluation (or lm_solve)
+  const bool gram = !sharded && o->lm_mode == 0 && lm_gram_supported(o->huber);
+  if (gram) {
+    o->gpart.reserve(lm_gram_partials());
+    o->gmat.reserve(lm_gram_words());
+  }
   for (int it = 0; it < o->optimization_count; ++it) {
     {
       ProfScope ps(ctx, "knn", FLOAM_PROF_KNN);   // the correspondence pass: search + geometry
@@ -363,7 +380,8 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
                    o->dbg_stamps.p ? o->dbg_stamps.p + 8 : nullptr);
       }
       ProfScope ps2(ctx, "knn_geometry", FLOAM_PROF_KNN_DETAIL);
-      geom_launch(o->lm.p, qe, o->gE, o->mapE.pts.p, o->ce, qs, o->gS, o->mapS.pts.p, o->cs, st);
+      geom_launch(o->lm.p, qe, o->gE, o->mapE.pts.p, o->ce, qs, o->gS, o->mapS.pts.p, o->cs, gram ? o->gpart.p : nullptr,
+                  st);
     }
     if (ctx.profile & FLOAM_PROF_KNN_BYTES) {   // replay only: algorithmic bytes of the two launches above
       knn_traffic_launch(o->lm.p, qe, o->gE, o->mapE.pts.p, o->ce, 8 * EDGE_FIELDS, o->rank, o->world, o->traffic_set,
@@ -372,9 +390,18 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
                          o->prof_bytes.p + 1, st);
     }
     // iteration zero + at most max_num_iterations = 4 candidates (odomEstimationClass.cpp:102)
+    if (!sharded && o->lm_mode == 1) {
+      ProfScope ps(ctx, "lm_solve", FLOAM_PROF_LM);
+      lm_solve_launch(o->lm.p, o->ce, o->cnt.p + 0, ne_ub, o->cs, o->cnt.p + 1, ns_ub, o->huber, o->partials.p,
+                      o->lm_point.p, o->step_counter.p, o->lm_go.p, ++o->lm_epoch, st, o->dbg_stamps.p);
+      continue;
+    }
     for (int ev = 0; ev < 5; ++ev) {
       ProfScope ps(ctx, "lm_step", FLOAM_PROF_LM);
-      if (sharded) {
+      if (gram) {
+        lm_step_gram_launch(o->lm.p, o->ce, o->cnt.p + 0, ne_ub, o->gpart.p, o->gmat.p, ev == 0, o->partials.p,
+                            o->step_counter.p, st, o->dbg_stamps.p);
+      } else if (sharded) {
         const int nblk = lm_eval_launch(o->lm.p, o->ce, o->cnt.p + 0, ne_ub, o->cs, o->cnt.p + 1, ns_ub, o->huber,
                                         o->partials.p, st);
         lm_reduce_launch(o->partials.p, nblk, o->sums.p, st);

@@ -656,8 +656,16 @@ __global__ __launch_bounds__(kTB) void knn_kernel(LMState* __restrict__ st, X7 x
 }
 
 // Pass 2: fp64 line / plane geometry, one query per lane (all 64 lanes busy).
+// Surf record i as the 13-vector w = [n (x) p (9), n (3), d + n.o] (p the sensor-frame point, n the unit normal,
+// d the plane offset, o the solve's starting translation): every surf residual and Jacobian entry is linear in w
+// (see surf_sums_from_gram), so the surf half of each LM evaluation needs only the Gram matrix sum(w w^T).
+constexpr int kGramW = 13;
+constexpr int kGram = kGramW * (kGramW + 1) / 2;   // 91 unique entries (upper triangle, row-major)
+constexpr int kSurfGeomBlocks = 256;               // fixed surf geometry grid: fixed Gram reduction order
+
 template <bool EDGE>
-__device__ __forceinline__ void geom_query(LMState* __restrict__ st, const CorrArgs& A, int i) {
+__device__ __forceinline__ void geom_query(LMState* __restrict__ st, const CorrArgs& A, int i,
+                                           double* __restrict__ w = nullptr, const double* o = nullptr) {
   const int n = min(*A.d_n, A.n_ub);
   bool ok = false;
   const int flags = i < n ? A.valid[i] : 0;
@@ -717,6 +725,15 @@ __device__ __forceinline__ void geom_query(LMState* __restrict__ st, const CorrA
         rec[0 * cap + i] = cpx; rec[1 * cap + i] = cpy; rec[2 * cap + i] = cpz;
         rec[3 * cap + i] = nv[0]; rec[4 * cap + i] = nv[1]; rec[5 * cap + i] = nv[2];
         rec[6 * cap + i] = d;
+        if (w) {
+          const double pp[3] = {cpx, cpy, cpz};
+#pragma unroll
+          for (int a = 0; a < 3; ++a)
+#pragma unroll
+            for (int e = 0; e < 3; ++e) w[3 * a + e] = nv[a] * pp[e];
+          w[9] = nv[0]; w[10] = nv[1]; w[11] = nv[2];
+          w[12] = d + ((nv[0] * o[0] + nv[1] * o[1]) + nv[2] * o[2]);
+        }
       }
     }
     A.valid[i] = (uint8_t)((flags & 2) | (ok ? 1 : 0));
@@ -725,11 +742,65 @@ __device__ __forceinline__ void geom_query(LMState* __restrict__ st, const CorrA
   if ((threadIdx.x & 63) == 0 && b) atomicAdd(EDGE ? &st->corr_edge : &st->corr_surf, __popcll(b));
 }
 
-__global__ __launch_bounds__(kTB) void geom_kernel(LMState* __restrict__ st, CorrArgs E, CorrArgs S, int nbE) {
-  if ((int)blockIdx.x < nbE)
+__device__ __forceinline__ void gram_pair(int e, int& i, int& j) {   // upper-triangle entry e -> (i, j), i <= j
+  i = 0;
+  while (e >= kGramW - i) {
+    e -= kGramW - i;
+    ++i;
+  }
+  j = i + e;
+}
+
+// Edge blocks: one query per lane.  Surf blocks (fixed grid, grid-stride): one query per lane, and the block's
+// partial Gram matrix of its accepted surf records (waves stage w in LDS, lane e sums entry e over the wave's 64
+// records in lane order, waves combined in order) into gpart[block][91].
+__global__ __launch_bounds__(kTB) void geom_kernel(LMState* __restrict__ st, CorrArgs E, CorrArgs S, int nbE,
+                                                   double* __restrict__ gpart) {
+  if ((int)blockIdx.x < nbE) {
     geom_query<true>(st, E, blockIdx.x * blockDim.x + threadIdx.x);
-  else
-    geom_query<false>(st, S, (blockIdx.x - nbE) * blockDim.x + threadIdx.x);
+    return;
+  }
+  const int sb = (int)blockIdx.x - nbE;
+  if (!gpart) {
+    for (int i0 = sb * kTB; i0 < S.n_ub; i0 += kSurfGeomBlocks * kTB) geom_query<false>(st, S, i0 + threadIdx.x);
+    return;
+  }
+  __shared__ double s_w[kTB / 64][kGramW][65];   // padded rows: lanes reading different rows hit different banks
+  __shared__ double s_part[kTB / 64][kGram];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  double o[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) o[k] = st->x[4 + k];
+  int ei0, ej0, ei1 = 0, ej1 = 0;
+  gram_pair(lane, ei0, ej0);
+  if (lane + 64 < kGram) gram_pair(lane + 64, ei1, ej1);
+  double g0 = 0.0, g1 = 0.0;
+  for (int i0 = sb * kTB; i0 < S.n_ub; i0 += kSurfGeomBlocks * kTB) {   // wave-uniform trip count
+    double w[kGramW];
+#pragma unroll
+    for (int k = 0; k < kGramW; ++k) w[k] = 0.0;
+    geom_query<false>(st, S, i0 + threadIdx.x, w, o);
+#pragma unroll
+    for (int k = 0; k < kGramW; ++k) s_w[wv][k][lane] = w[k];
+    wave_lds_order();
+    double a0 = 0.0, a1 = 0.0;
+    for (int r = 0; r < 64; ++r) {
+      a0 += s_w[wv][ei0][r] * s_w[wv][ej0][r];
+      a1 += s_w[wv][ei1][r] * s_w[wv][ej1][r];
+    }
+    g0 += a0;
+    g1 += a1;
+    wave_lds_order();
+  }
+  s_part[wv][lane] = g0;
+  if (lane + 64 < kGram) s_part[wv][lane + 64] = g1;
+  __syncthreads();
+  if (threadIdx.x < kGram) {
+    double v = s_part[0][threadIdx.x];
+#pragma unroll
+    for (int k = 1; k < kTB / 64; ++k) v += s_part[k][threadIdx.x];
+    gpart[sb * kGram + threadIdx.x] = v;
+  }
 }
 
 // Algorithmic traffic of one correspondence pass (SURVEY.md §8 d): every map cell any query scans
@@ -890,6 +961,24 @@ __device__ __forceinline__ double wave_sum(double v) {
 
 // Per-block partial sums (cost, J^T J upper, J^T r, count) of one LM evaluation over the device-resident
 // correspondence slots [0, *d_ne) and [0, *d_ns).  Evaluated at x (phase 0, iteration zero) or at the candidate.
+// Stores / loads of words handed between blocks of one launch without fences: agent-scope relaxed atomics compile
+// to sc1 (L2-coherent) accesses, so the consumer needs no cache invalidation (MI355X_MICROARCH.md "Valid forms":
+// sc1 stores drained with vmcnt(0) before the flag, sc1 loads after it).
+__device__ __forceinline__ void store_sc1(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double load_sc1(const double* p) {
+  return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
+                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+template <bool SC1>
+__device__ void eval_block_at(const double (&x)[7], const double* __restrict__ erec,
+                              const uint8_t* __restrict__ evalid, int ecap, int ne, const double* __restrict__ srec,
+                              const uint8_t* __restrict__ svalid, int scap, int ns, int huber,
+                              double* __restrict__ partials, int blk, int nblk);
+
 __device__ void eval_block(const LMState* __restrict__ st, const double* __restrict__ erec,
                            const uint8_t* __restrict__ evalid, int ecap, int ne, const double* __restrict__ srec,
                            const uint8_t* __restrict__ svalid, int scap, int ns, int huber, double* __restrict__ partials,
@@ -902,6 +991,14 @@ __device__ void eval_block(const LMState* __restrict__ st, const double* __restr
   double x[7];
 #pragma unroll
   for (int k = 0; k < 7; ++k) x[k] = at_x ? xa[k] : xc[k];
+  eval_block_at<false>(x, erec, evalid, ecap, ne, srec, svalid, scap, ns, huber, partials, blk, nblk);
+}
+
+template <bool SC1>
+__device__ void eval_block_at(const double (&x)[7], const double* __restrict__ erec,
+                              const uint8_t* __restrict__ evalid, int ecap, int ne, const double* __restrict__ srec,
+                              const uint8_t* __restrict__ svalid, int scap, int ns, int huber,
+                              double* __restrict__ partials, int blk, int nblk) {
   double acc[LM_NSUM];
 #pragma unroll
   for (int k = 0; k < LM_NSUM; ++k) acc[k] = 0.0;
@@ -966,7 +1063,8 @@ __device__ void eval_block(const LMState* __restrict__ st, const double* __restr
   if (threadIdx.x < LM_NSUM) {
     double v = 0.0;
     for (int p = 0; p < 8; ++p) v += strip[threadIdx.x][p];
-    partials[threadIdx.x * nblk + blk] = v;
+    if (SC1) store_sc1(&partials[threadIdx.x * nblk + blk], v);
+    else partials[threadIdx.x * nblk + blk] = v;
   }
 }
 
@@ -979,6 +1077,29 @@ __global__ __launch_bounds__(kTB) void lm_eval(const LMState* __restrict__ st, c
   if (st->done) return;
   eval_block(st, erec, evalid, ecap, min(*d_ne, ne_ub), srec, svalid, scap, min(*d_ns, ns_ub), huber, partials,
              blockIdx.x, gridDim.x);
+}
+
+// fixed-size variant for the resident solve: the kEvalBlocks partials of a component are loaded sc1, all in flight
+__device__ void reduce_partials_sc1(const double* __restrict__ partials, double* sums /* shared */) {
+  __shared__ double strip[LM_NSUM][8];
+  constexpr int per = (int)kEvalBlocks / 8;
+  if (threadIdx.x < LM_NSUM * 8) {
+    const int c = threadIdx.x >> 3, p = threadIdx.x & 7;
+    double w[per];
+#pragma unroll
+    for (int k = 0; k < per; ++k) w[k] = load_sc1(&partials[c * (int)kEvalBlocks + p * per + k]);
+    double v = 0.0;
+#pragma unroll
+    for (int k = 0; k < per; ++k) v += w[k];
+    strip[c][p] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < LM_NSUM) {
+    double v = 0.0;
+    for (int p = 0; p < 8; ++p) v += strip[threadIdx.x][p];
+    sums[threadIdx.x] = v;
+  }
+  __syncthreads();
 }
 
 __device__ void reduce_partials_block(const double* __restrict__ partials, int nblk, double* sums /* shared */) {
@@ -1078,36 +1199,44 @@ __host__ __device__ constexpr int hidx(int a, int b) {   // upper-triangle row-m
 // (The oracle solves the equivalent [J; sqrt(D/radius)] least-squares problem by Householder QR like Ceres'
 // DENSE_QR; the two agree to ~cond * eps.)  Returns false for an invalid step; delta = scaled step.
 __device__ __forceinline__ bool solve_step(LMState& s, double (&delta)[6]) {
-  double Hs[6][6], gs[6];
+  // packed lower triangle (row-major, l(i,j) = i(i+1)/2 + j): Hs = S H S, then A = Hs + diag/radius factored in place
+  double sc[6], gs[6];
 #pragma unroll
   for (int a = 0; a < 6; ++a) {
-    gs[a] = s.scale[a] * s.g[a];
-#pragma unroll
-    for (int b = 0; b < 6; ++b) Hs[a][b] = s.scale[a] * s.H[a <= b ? hidx(a, b) : hidx(b, a)] * s.scale[b];
+    sc[a] = s.scale[a];
+    gs[a] = sc[a] * s.g[a];
   }
+  double A[21];
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int j = 0; j <= i; ++j) A[i * (i + 1) / 2 + j] = sc[i] * s.H[hidx(j, i)] * sc[j];
   if (!s.reuse) {
 #pragma unroll
-    for (int k = 0; k < 6; ++k) s.diag[k] = fmin(fmax(Hs[k][k], 1e-6), 1e32);
+    for (int k = 0; k < 6; ++k) s.diag[k] = fmin(fmax(A[k * (k + 1) / 2 + k], 1e-6), 1e32);
   }
   s.reuse = 1;
   // Cholesky of A = Hs + diag / radius, with one reciprocal per pivot
   const double inv_radius = 1.0 / s.radius;
-  double L[6][6], rd[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) A[k * (k + 1) / 2 + k] += s.diag[k] * inv_radius;
+  double rd[6];
   bool pd = true;
 #pragma unroll
   for (int j = 0; j < 6; ++j) {
-    double d = Hs[j][j] + s.diag[j] * inv_radius;
+    double d = A[j * (j + 1) / 2 + j];
 #pragma unroll
-    for (int k = 0; k < j; ++k) d -= L[j][k] * L[j][k];
+    for (int k = 0; k < j; ++k) d -= A[j * (j + 1) / 2 + k] * A[j * (j + 1) / 2 + k];
     pd = pd && (d > 0.0);
-    L[j][j] = sqrt(d);
-    rd[j] = 1.0 / L[j][j];
+    const double ljj = sqrt(d);
+    A[j * (j + 1) / 2 + j] = ljj;
+    rd[j] = 1.0 / ljj;
 #pragma unroll
     for (int i = j + 1; i < 6; ++i) {
-      double v = Hs[i][j];
+      double v = A[i * (i + 1) / 2 + j];
 #pragma unroll
-      for (int k = 0; k < j; ++k) v -= L[i][k] * L[j][k];
-      L[i][j] = v * rd[j];
+      for (int k = 0; k < j; ++k) v -= A[i * (i + 1) / 2 + k] * A[j * (j + 1) / 2 + k];
+      A[i * (i + 1) / 2 + j] = v * rd[j];
     }
   }
   if (!pd) return false;
@@ -1116,38 +1245,38 @@ __device__ __forceinline__ bool solve_step(LMState& s, double (&delta)[6]) {
   for (int i = 0; i < 6; ++i) {
     double v = gs[i];
 #pragma unroll
-    for (int k = 0; k < i; ++k) v -= L[i][k] * y[k];
+    for (int k = 0; k < i; ++k) v -= A[i * (i + 1) / 2 + k] * y[k];
     y[i] = v * rd[i];
   }
 #pragma unroll
   for (int i = 5; i >= 0; --i) {
     double v = y[i];
 #pragma unroll
-    for (int k = i + 1; k < 6; ++k) v -= L[k][i] * y[k];
+    for (int k = i + 1; k < 6; ++k) v -= A[k * (k + 1) / 2 + i] * y[k];
     y[i] = v * rd[i];
   }
-  double step[6];
   bool finite = true;
 #pragma unroll
   for (int k = 0; k < 6; ++k) {
-    step[k] = -y[k];
-    finite = finite && isfinite(step[k]);
+    y[k] = -y[k];   // the step
+    finite = finite && isfinite(y[k]);
   }
   if (!finite) return false;
+  // model cost change -(step^T gs + step^T Hs step / 2), Hs re-formed from the state
   double sg = 0.0, sHs = 0.0;
 #pragma unroll
   for (int a = 0; a < 6; ++a) {
-    sg += step[a] * gs[a];
+    sg += y[a] * gs[a];
     double hv = 0.0;
 #pragma unroll
-    for (int b = 0; b < 6; ++b) hv += Hs[a][b] * step[b];
-    sHs += step[a] * hv;
+    for (int b = 0; b < 6; ++b) hv += (sc[a] * s.H[a <= b ? hidx(a, b) : hidx(b, a)] * sc[b]) * y[b];
+    sHs += y[a] * hv;
   }
   const double mcc = -(sg + 0.5 * sHs);
   if (!(mcc > 0.0)) return false;
   s.mcc = mcc;
 #pragma unroll
-  for (int k = 0; k < 6; ++k) delta[k] = step[k] * s.scale[k];
+  for (int k = 0; k < 6; ++k) delta[k] = y[k] * sc[k];
   return true;
 }
 
@@ -1379,6 +1508,375 @@ __global__ __launch_bounds__(kTB) void lm_step(LMState* __restrict__ st, const d
   }
 }
 
+// A whole Ceres solve in one launch (single-GPU path): iteration zero + at most 4 candidates, i.e. up to 5
+// evaluations, each followed by the control step.  Block 0 is the control block, blocks 1..nblk evaluate.  The
+// blocks stay resident across the evaluations and hand off without cache invalidations (sc1 words):
+//   evaluation -> control: the block's 29 partial sums stored sc1, drained, then one atomicAdd on `cnt`;
+//   control -> evaluation: the next evaluation point (7 doubles) stored sc1 into `point`, drained, then the word
+//        go = (epoch << 8) | (done << 7) | evaluations released; epoch is a per-launch host counter, so go never
+//        has to be reset.  The records stay hot in the evaluating blocks' L2 across the evaluations.
+// All 1 + nblk blocks must be co-resident (nblk = 128 <= one block per CU on 256 CUs); every wait is bounded
+// (~1 s) and a timeout ends the solve with st->n_res = -1, which the host reports as an error.
+__device__ __forceinline__ bool wait_u32_geq(unsigned* p, unsigned target) {
+  for (long long it = 0; it < (1ll << 24); ++it) {
+    if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return false;
+}
+
+__global__ __launch_bounds__(kTB) void lm_solve(LMState* __restrict__ st, const double* __restrict__ erec,
+                                                const uint8_t* __restrict__ evalid, int ecap,
+                                                const int* __restrict__ d_ne, int ne_ub,
+                                                const double* __restrict__ srec, const uint8_t* __restrict__ svalid,
+                                                int scap, const int* __restrict__ d_ns, int ns_ub, int huber,
+                                                double* __restrict__ partials, double* __restrict__ point,
+                                                unsigned* __restrict__ cnt, unsigned long long* __restrict__ go,
+                                                unsigned long long epoch, unsigned long long* __restrict__ dbg) {
+  const int nblk = (int)gridDim.x - 1;
+  __shared__ int s_flag;
+  if (blockIdx.x > 0) {
+    const int ne = min(*d_ne, ne_ub), ns = min(*d_ns, ns_ub);
+    __shared__ double s_x[7];
+    for (int it = 0; it < 5; ++it) {
+      if (it == 0) {   // iteration zero evaluates at x (set by the kNN launch; kernel boundary)
+        if (threadIdx.x < 7) s_x[threadIdx.x] = st->x[threadIdx.x];
+      } else {         // wait for the control step of evaluation it - 1, then read the point it released
+        if (threadIdx.x == 0) {
+          int f = 2;   // 0: go, 1: done, 2: timeout
+          for (long long k = 0; k < (1ll << 24); ++k) {
+            const unsigned long long g = __hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((g >> 8) == epoch && (int)(g & 0x7F) >= it) {
+              f = (g & 0x80) ? 1 : 0;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
+          s_flag = f;
+        }
+        __syncthreads();
+        if (s_flag) return;
+        if (threadIdx.x < 7) s_x[threadIdx.x] = load_sc1(&point[threadIdx.x]);
+      }
+      __syncthreads();
+      double x[7];
+#pragma unroll
+      for (int k = 0; k < 7; ++k) x[k] = s_x[k];
+      eval_block_at<true>(x, erec, evalid, ecap, ne, srec, svalid, scap, ns, huber, partials, blockIdx.x - 1, nblk);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) atomicAdd(cnt, 1u);
+    }
+    return;
+  }
+  // control block
+  __shared__ LMState sst;
+  __shared__ double sums[LM_NSUM];
+  constexpr int kWords = (int)(sizeof(LMState) / sizeof(unsigned));
+  static_assert(sizeof(LMState) % sizeof(unsigned) == 0, "LMState must be a whole number of dwords");
+  {
+    const unsigned* gsrc = reinterpret_cast<const unsigned*>(st);
+    unsigned* ldst = reinterpret_cast<unsigned*>(&sst);
+    for (int w = threadIdx.x; w < kWords; w += blockDim.x) ldst[w] = gsrc[w];
+  }
+  __syncthreads();
+  unsigned long long t_wait = 0, t_reduce = 0, t_ctrl = 0, n_it = 0;
+  int it = 0;
+  bool failed = false;
+  for (; it < 5 && !sst.done; ++it) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) s_flag = wait_u32_geq(cnt, (unsigned)(nblk * (it + 1))) ? 0 : 1;
+    __syncthreads();
+    if (s_flag) {
+      failed = true;
+      break;
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+    reduce_partials_sc1(partials, sums);
+    const unsigned long long t2 = __builtin_amdgcn_s_memrealtime();
+    lm_logic_wave0(sst, sums);
+    __syncthreads();
+    if (threadIdx.x == 0) {   // release the next evaluation point (cand after a step; x never changes here)
+      if (!sst.done) {
+#pragma unroll
+        for (int k = 0; k < 7; ++k) store_sc1(&point[k], sst.phase == 0 ? sst.x[k] : sst.cand[k]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __hip_atomic_store(go, (epoch << 8) | (sst.done ? 0x80ull : 0ull) | (unsigned long long)(it + 1),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const unsigned long long t3 = __builtin_amdgcn_s_memrealtime();
+    t_wait += t1 - t0;
+    t_reduce += t2 - t1;
+    t_ctrl += t3 - t2;
+    ++n_it;
+  }
+  __syncthreads();
+  {   // the final state for the host gather / the next launches (kernel boundary makes it visible)
+    unsigned* gdst = reinterpret_cast<unsigned*>(st);
+    const unsigned* lsrc = reinterpret_cast<const unsigned*>(&sst);
+    for (int w = threadIdx.x; w < kWords; w += blockDim.x) gdst[w] = lsrc[w];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (failed) {   // never expected: end the solve, release the evaluation blocks, report through n_res
+      st->done = 1;
+      st->n_res = -1;
+      __hip_atomic_store(go, (epoch << 8) | 0x80ull | 0x7Full, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (it == 0) {   // done before the first evaluation: let any waiting evaluation block go
+      __hip_atomic_store(go, (epoch << 8) | 0x80ull | 0x7Full, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    *cnt = 0u;   // every evaluation block has arrived for the last released evaluation (kernel boundary orders it)
+    if (dbg && n_it) {   // diagnostic stamps (100 MHz): wait for the evaluations, reduce, control step + publish
+      atomicAdd(&dbg[1], t_wait);
+      atomicAdd(&dbg[2], t_reduce);
+      atomicAdd(&dbg[3], t_ctrl);
+      atomicAdd(&dbg[4], n_it);
+    }
+  }
+}
+
+// ================================================================= LM step with the surf half from a Gram matrix
+// With the squared loss (the launch default: "Cauchy" means no robust loss, Q3) a surf residual and its Jacobian are
+// LINEAR in the record vector w of geom_kernel: with M the matrix of Eigen's q * v (M = I + 2 w [u]x + 2 [u]x^2,
+// u = q.vec) and t' = t - o,
+//   r      = c^T w,     c   = [M (row-major a,e) | t' | 1]     (w[12] = d + n.o absorbs the origin)
+//   J[3+a] = n_a        = e_{9+a}^T w
+//   J[i]   = (lp x n)_i = K_i^T w,  K_i[3c+e] = sum_b eps_ibc M_be,  K_i[9+c] = sum_b eps_ibc t_b,  K_i[12] = 0
+// so the surf part of J^T J, J^T r and the cost are quadratic forms of the Gram matrix G = sum w w^T (reduced once
+// per solve).  The edge records are still evaluated per record (EdgeAnalyticCostFunction's J has the direction
+// nu/|nu|, which depends on the pose).  The residuals cancel inside G c (terms ~|p|^2 per record); recentring c on o
+// keeps those terms independent of how far the pose is from the map origin.  Same function values as the
+// per-residual evaluation in exact arithmetic; the rounding differs (~|G| eps in c^T G c, ~1e-9 of the cost at C3;
+// poses agree with the per-record path to ~1e-14).
+constexpr unsigned kEdgeEvalBlocks = 32;   // edge-only evaluation grid (fixed: fixed reduction order)
+constexpr int kGramWords = kGram + 3;      // G (upper triangle) + the origin o it was built on
+
+// G (LDS, full symmetric) -> the 29 surf sums at x (LDS out).  Called by the whole block (256 threads).
+__device__ void surf_sums_from_gram(const double (&x)[7], const double* o /* shared [3] */,
+                                    const double (*G)[kGramW] /* shared */, double n_surf, double* out /* shared */) {
+  __shared__ double V[7][kGramW];   // K_0..K_5, c
+  __shared__ double Y[7][kGramW];   // G V
+  const int t = threadIdx.x;
+  if (t < kGramW) {   // lanes 0..12 build one component of all 7 vectors
+    const double qx = x[0], qy = x[1], qz = x[2], qw = x[3];
+    const double U[3][3] = {{0, -qz, qy}, {qz, 0, -qx}, {-qy, qx, 0}};
+    double Mm[3][3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+      for (int b = 0; b < 3; ++b) {
+        const double u2 = U[a][0] * U[0][b] + U[a][1] * U[1][b] + U[a][2] * U[2][b];
+        Mm[a][b] = ((a == b) ? 1.0 : 0.0) + 2.0 * qw * U[a][b] + 2.0 * u2;
+      }
+    const double tp[3] = {x[4] - o[0], x[5] - o[1], x[6] - o[2]};   // c: recentred (d absorbed n.o)
+    const double tf[3] = {x[4], x[5], x[6]};                        // K: the Jacobian's lp = M p + t itself
+    const int m = t;   // component of w
+    // register-resident selects instead of run-time array indexing (no scratch)
+    auto Msel = [&](int r, int c) {
+      double v = 0.0;
+#pragma unroll
+      for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b)
+          if (a == r && b == c) v = Mm[a][b];
+      return v;
+    };
+    auto vsel = [&](const double (&vv)[3], int k) { return k == 0 ? vv[0] : (k == 1 ? vv[1] : vv[2]); };
+    double cm = 1.0;
+    if (m < 9) cm = Msel(m / 3, m % 3);
+    else if (m < 12) cm = vsel(tp, m - 9);
+    V[6][m] = cm;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {   // K_i for i = 0..2 (lp x n)
+      const int b1 = (i + 1) % 3, b2 = (i + 2) % 3;   // eps_{i b1 b2} = +1, eps_{i b2 b1} = -1
+      double km = 0.0;
+      if (m < 9) {
+        const int c = m / 3, e = m % 3;   // w index 3c + e: sum_b eps_{ibc} M_be
+        if (c == b2) km = Msel(b1, e);
+        else if (c == b1) km = -Msel(b2, e);
+      } else if (m < 12) {
+        const int c = m - 9;              // sum_b eps_{ibc} t_b
+        if (c == b2) km = vsel(tf, b1);
+        else if (c == b1) km = -vsel(tf, b2);
+      }
+      V[i][m] = km;
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) V[3 + a][m] = (m == 9 + a) ? 1.0 : 0.0;   // K_{3+a} = e_{9+a}
+  }
+  __syncthreads();
+  if (t < 7 * kGramW) {   // Y = G V
+    const int v = t / kGramW, i = t % kGramW;
+    double a = 0.0;
+#pragma unroll
+    for (int j = 0; j < kGramW; ++j) a += G[i][j] * V[v][j];
+    Y[v][i] = a;
+  }
+  __syncthreads();
+  if (t < LM_NSUM) {   // cost, J^T J upper (row-major), J^T r, count
+    double s;
+    if (t == 0) {
+      double a = 0.0;
+#pragma unroll
+      for (int i = 0; i < kGramW; ++i) a += V[6][i] * Y[6][i];
+      s = 0.5 * a;
+    } else if (t < 22) {
+      int hh = t - 1, ja = 0;
+      while (hh >= 6 - ja) { hh -= 6 - ja; ++ja; }
+      const int jb = ja + hh;
+      double a = 0.0;
+#pragma unroll
+      for (int i = 0; i < kGramW; ++i) a += V[ja][i] * Y[jb][i];
+      s = a;
+    } else if (t < 28) {
+      double a = 0.0;
+#pragma unroll
+      for (int i = 0; i < kGramW; ++i) a += V[t - 22][i] * Y[6][i];
+      s = a;
+    } else {
+      s = n_surf;
+    }
+    out[t] = s;
+  }
+  __syncthreads();
+}
+
+// G of this solve into LDS: either reduced from the surf geometry blocks' partials (first evaluation of the solve;
+// fixed order: 8 strips of 32 blocks, then the strips) and published to gmat with the origin o = x (no step has been
+// taken yet), or loaded from gmat.
+__device__ void gram_load(const double* __restrict__ gpart, double* __restrict__ gmat, bool reduce,
+                          const LMState& sst, double (*G)[kGramW], double* o) {
+  __shared__ double s_gp[kGram][8];
+  const int t = threadIdx.x;
+  if (reduce) {
+    for (int q = t; q < kGram * 8; q += blockDim.x) {
+      const int e = q >> 3, p = q & 7;
+      constexpr int per = kSurfGeomBlocks / 8;
+      double v[per];
+#pragma unroll
+      for (int k = 0; k < per; ++k) v[k] = gpart[(p * per + k) * kGram + e];
+      double a = 0.0;
+#pragma unroll
+      for (int k = 0; k < per; ++k) a += v[k];
+      s_gp[e][p] = a;
+    }
+    __syncthreads();
+  }
+  if (t < kGram) {
+    double a;
+    if (reduce) {
+      a = s_gp[t][0];
+#pragma unroll
+      for (int p = 1; p < 8; ++p) a += s_gp[t][p];
+      gmat[t] = a;
+    } else {
+      a = gmat[t];
+    }
+    int i, j;
+    gram_pair(t, i, j);
+    G[i][j] = a;
+    G[j][i] = a;
+  } else if (t < kGramWords) {
+    const int k = t - kGram;
+    const double v = reduce ? sst.x[4 + k] : gmat[t];
+    if (reduce) gmat[t] = v;
+    o[k] = v;
+  }
+  __syncthreads();
+}
+
+// One LM iteration in one launch, surf half from G.  Block 0 (control) stages the state and G and computes the
+// surf sums at the evaluation point while blocks 1..nblk evaluate the edge records; then it waits for them (same
+// hand-off as lm_step), adds the edge sums and runs the control step.
+__global__ __launch_bounds__(kTB) void lm_step_gram(LMState* __restrict__ st, const double* __restrict__ erec,
+                                                    const uint8_t* __restrict__ evalid, int ecap,
+                                                    const int* __restrict__ d_ne, int ne_ub,
+                                                    const double* __restrict__ gpart, double* __restrict__ gmat,
+                                                    int reduce_g, double* __restrict__ partials,
+                                                    unsigned* __restrict__ counter, unsigned long long* __restrict__ dbg) {
+  const int nblk = (int)gridDim.x - 1;
+  if (blockIdx.x > 0) {
+    if (st->done) return;
+    eval_block(st, erec, evalid, ecap, min(*d_ne, ne_ub), nullptr, nullptr, 0, 0, 0, partials, blockIdx.x - 1, nblk);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      atomicAdd(counter, 1u);
+    }
+    return;
+  }
+  __shared__ LMState sst;
+  __shared__ double G[kGramW][kGramW];
+  __shared__ double o[3];
+  __shared__ double ssum[LM_NSUM];
+  __shared__ double sums[LM_NSUM];
+  __shared__ int s_timeout;
+  constexpr int kWords = (int)(sizeof(LMState) / sizeof(unsigned));
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  {
+    const unsigned* gsrc = reinterpret_cast<const unsigned*>(st);
+    unsigned* ldst = reinterpret_cast<unsigned*>(&sst);
+    for (int w = threadIdx.x; w < kWords; w += blockDim.x) ldst[w] = gsrc[w];
+  }
+  __syncthreads();
+  if (sst.done) return;
+  gram_load(gpart, gmat, reduce_g != 0, sst, G, o);
+  {
+    double x[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) x[k] = sst.phase == 0 ? sst.x[k] : sst.cand[k];
+    surf_sums_from_gram(x, o, G, (double)sst.corr_surf, ssum);
+  }
+  unsigned long long t1 = __builtin_amdgcn_s_memrealtime(), t2 = 0, t3 = 0;
+  if (threadIdx.x == 0) {
+    int timeout = 1;   // bounded wait (~1 s)
+    for (long long it = 0; it < (1ll << 24); ++it) {
+      if (__hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)nblk) {
+        timeout = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    s_timeout = timeout;
+    t2 = __builtin_amdgcn_s_memrealtime();
+  }
+  __syncthreads();
+  if (s_timeout) {   // never expected: give up on this solve instead of hanging the device
+    if (threadIdx.x == 0) {
+      st->done = 1;
+      st->n_res = -1;
+      *counter = 0u;
+    }
+    return;
+  }
+  reduce_partials_block(partials, nblk, sums);
+  if (threadIdx.x < LM_NSUM) sums[threadIdx.x] = sums[threadIdx.x] + ssum[threadIdx.x];   // edge + surf
+  __syncthreads();
+  t3 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) *counter = 0u;   // ready for the next launch (kernel boundary orders it)
+  lm_logic_wave0(sst, sums);
+  __syncthreads();
+  {
+    unsigned* gdst = reinterpret_cast<unsigned*>(st);
+    const unsigned* lsrc = reinterpret_cast<const unsigned*>(&sst);
+    for (int w = threadIdx.x; w < kWords; w += blockDim.x) gdst[w] = lsrc[w];
+  }
+  if (dbg && threadIdx.x == 0) {   // stamps (100 MHz): stage + G + surf sums, wait, reduce, control step + store
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    const unsigned long long t4 = __builtin_amdgcn_s_memrealtime();
+    atomicAdd(&dbg[0], t1 - t0);
+    atomicAdd(&dbg[1], t2 - t1);
+    atomicAdd(&dbg[2], t3 - t2);
+    atomicAdd(&dbg[3], t4 - t3);
+    atomicAdd(&dbg[4], 1ull);
+  }
+}
+
 __global__ __launch_bounds__(kTB) void lm_reduce(const double* __restrict__ partials, int nblk, double* __restrict__ out) {
   __shared__ double sums[LM_NSUM];
   reduce_partials_block(partials, nblk, sums);
@@ -1484,12 +1982,13 @@ void knn_launch(LMState* d_st, const double* x0, const double* x0_dev, const Que
 }
 
 void geom_launch(LMState* d_st, const QuerySet& qe, const Grid& ge, const PointRec* mapE, CorrSet& ce,
-                 const QuerySet& qs, const Grid& gs, const PointRec* mapS, CorrSet& cs, hipStream_t st) {
+                 const QuerySet& qs, const Grid& gs, const PointRec* mapS, CorrSet& cs, double* gpart,
+                 hipStream_t st) {
   CorrArgs E, S;
   corr_args(qe, ge, mapE, ce, qs, gs, mapS, cs, nullptr, E, S);
   if (qe.n_ub <= 0 && qs.n_ub <= 0) return;
-  const unsigned gE = div_up(std::max(qe.n_ub, 1), kTB), gS = div_up(std::max(qs.n_ub, 1), kTB);
-  hipLaunchKernelGGL(geom_kernel, dim3(gE + gS), dim3(kTB), 0, st, d_st, E, S, (int)gE);
+  const unsigned gE = div_up(std::max(qe.n_ub, 1), kTB);
+  hipLaunchKernelGGL(geom_kernel, dim3(gE + kSurfGeomBlocks), dim3(kTB), 0, st, d_st, E, S, (int)gE, gpart);
   FLOAM_LAUNCH_CHECK();
 }
 
@@ -1533,6 +2032,27 @@ void lm_step_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub
   (void)ns_ub;
   hipLaunchKernelGGL(lm_step, dim3(nblk + 1), dim3(kTB), 0, st, d_st, ce.rec.p, ce.valid.p, ce.cap, d_ne, ne_ub,
                      cs.rec.p, cs.valid.p, cs.cap, d_ns, ns_ub, huber ? 1 : 0, partials, counter, dbg);
+  FLOAM_LAUNCH_CHECK();
+}
+
+void lm_solve_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const CorrSet& cs,
+                     const int* d_ns, int ns_ub, bool huber, double* partials, double* point, unsigned* cnt,
+                     unsigned long long* go, unsigned long long epoch, hipStream_t st, unsigned long long* dbg) {
+  const int nblk = (int)kEvalBlocks;   // fixed: the reduction order must not depend on the upper bounds
+  hipLaunchKernelGGL(lm_solve, dim3(nblk + 1), dim3(kTB), 0, st, d_st, ce.rec.p, ce.valid.p, ce.cap, d_ne, ne_ub,
+                     cs.rec.p, cs.valid.p, cs.cap, d_ns, ns_ub, huber ? 1 : 0, partials, point, cnt, go, epoch, dbg);
+  FLOAM_LAUNCH_CHECK();
+}
+
+bool lm_gram_supported(bool huber) { return !huber; }
+size_t lm_gram_partials() { return (size_t)kSurfGeomBlocks * kGram; }
+size_t lm_gram_words() { return (size_t)kGramWords; }
+
+void lm_step_gram_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const double* gpart,
+                         double* gmat, bool first, double* partials, unsigned* counter, hipStream_t st,
+                         unsigned long long* dbg) {
+  hipLaunchKernelGGL(lm_step_gram, dim3(kEdgeEvalBlocks + 1), dim3(kTB), 0, st, d_st, ce.rec.p, ce.valid.p, ce.cap,
+                     d_ne, ne_ub, gpart, gmat, first ? 1 : 0, partials, counter, dbg);
   FLOAM_LAUNCH_CHECK();
 }
 

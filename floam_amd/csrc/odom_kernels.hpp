@@ -124,8 +124,10 @@ void deskew_bridge_launch(const LMState* st, const Pose& odom0, double scan_peri
 void knn_launch(LMState* d_st, const double* x0, const double* x0_dev, const QuerySet& qe, const Grid& ge, const PointRec* mapE,
                 CorrSet& ce, const QuerySet& qs, const Grid& gs, const PointRec* mapS, CorrSet& cs, const int* d_me,
                 const int* d_ms, int rank, int world, hipStream_t st, unsigned long long* dbg = nullptr);
+// gpart (nullable): per-block partial Gram matrices of the surf records for lm_step_gram ([256][91] doubles)
 void geom_launch(LMState* d_st, const QuerySet& qe, const Grid& ge, const PointRec* mapE, CorrSet& ce,
-                 const QuerySet& qs, const Grid& gs, const PointRec* mapS, CorrSet& cs, hipStream_t st);
+                 const QuerySet& qs, const Grid& gs, const PointRec* mapS, CorrSet& cs, double* gpart,
+                 hipStream_t st);
 // algorithmic bytes of the correspondence pass just issued (profiling only), accumulated into *d_bytes
 void knn_traffic_launch(const LMState* d_st, const QuerySet& q, const Grid& g, const PointRec* map, CorrSet& c,
                         int rec_bytes, int rank, int world, DevBuf<unsigned long long>& set,
@@ -137,6 +139,21 @@ int lm_eval_launch(const LMState* d_st, const CorrSet& ce, const int* d_ne, int 
 void lm_step_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const CorrSet& cs,
                     const int* d_ns, int ns_ub, bool huber, double* partials, unsigned* counter, hipStream_t st,
                     unsigned long long* dbg = nullptr);
+// a whole Ceres solve (up to 5 evaluations + control steps) in one launch with resident blocks; cnt (u32) and go
+// (u64) are device words: cnt zero before the first launch, go any value; epoch strictly increasing per launch
+void lm_solve_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const CorrSet& cs,
+                     const int* d_ns, int ns_ub, bool huber, double* partials, double* point, unsigned* cnt,
+                     unsigned long long* go, unsigned long long epoch, hipStream_t st,
+                     unsigned long long* dbg = nullptr);
+// LM iteration for the squared loss: surf sums from the Gram matrix of the surf records (geom_launch with gpart),
+// edge records per record on a small grid.  first: this is the solve's first evaluation (reduce gpart into gmat,
+// lm_gram_words() doubles); later launches of the solve reuse gmat.
+bool lm_gram_supported(bool huber);
+size_t lm_gram_partials();   // doubles in gpart
+size_t lm_gram_words();      // doubles in gmat
+void lm_step_gram_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const double* gpart,
+                         double* gmat, bool first, double* partials, unsigned* counter, hipStream_t st,
+                         unsigned long long* dbg = nullptr);
 // reduce partials (nblk > 0) or read 29 pre-reduced sums (nblk == 0), then run the Ceres LM control step
 void lm_control_launch(LMState* d_st, const double* partials, int nblk, hipStream_t st);
 void lm_reduce_launch(const double* partials, int nblk, double* sums, hipStream_t st);

@@ -47,8 +47,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("run", help="gpurun_out/<tag> directory")
     ap.add_argument("tag")
-    ap.add_argument("--last", type=int, default=80,
-                    help="dispatches per kernel averaged for hbm_traffic.json (the timed tail; default = 20 scans x 4 "
+    ap.add_argument("--last", type=int, default=240,
+                    help="dispatches per kernel averaged for hbm_traffic.json (the timed tail; default = 60 scans x 4 "
                          "solves)")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles"))
     args = ap.parse_args()
