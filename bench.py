@@ -163,14 +163,26 @@ def main():
         return lp, odo
 
     lp, odo = make_pipeline()
-    d_edge, d_surf = floam_amd.DeviceCloud(device=dev), floam_amd.DeviceCloud(device=dev)
+    # two feature buffers: the extraction of scan k+1 (its own stream) is issued before the odometry of scan k, so
+    # the two overlap on the device, as the reference's laserProcessingNode runs beside odomEstimationNode
+    bufs = [(floam_amd.DeviceCloud(device=dev), floam_amd.DeviceCloud(device=dev)) for _ in range(2)]
 
-    def step(lp, odo, k, poses):
-        d_edge.clear()
-        d_surf.clear()
-        lp.featureExtraction(d_raw[k], d_edge, d_surf)
-        odo.UpdatePointsToMapSelector(d_edge, d_surf, True)
-        poses.append(odo.pose())
+    def extract(lp, k):
+        e, s = bufs[k & 1]
+        e.clear()
+        s.clear()
+        lp.featureExtraction(d_raw[k], e, s)
+
+    def run(lp, odo, a, b, poses):
+        """scans [a, b): featureExtraction + UpdatePointsToMapSelector each, extraction one scan ahead"""
+        if a < b:
+            extract(lp, a)
+        for k in range(a, b):
+            if k + 1 < b:
+                extract(lp, k + 1)
+            e, s = bufs[k & 1]
+            odo.UpdatePointsToMapSelector(e, s, True)
+            poses.append(odo.pose())
 
     def barrier_sync():
         if dist is not None:
@@ -178,16 +190,14 @@ def main():
         _ffi.check(L.floam_device_synchronize(dev))
 
     poses = []
-    for k in range(args.warmup):
-        step(lp, odo, k, poses)
+    run(lp, odo, 0, args.warmup, poses)
     if not args.no_roofline:
         _ffi.check(L.floam_profile_reset(dev))
         # FLOAM_PROF_KNN: HIP events around the correspondence pass only (+ FLOAM_PROF_KNN_DETAIL: per launch)
         _ffi.check(L.floam_profile_enable(dev, 1 | (32 if args.knn_detail else 0)))
     barrier_sync()
     t_start = time.perf_counter()
-    for k in range(args.warmup, n_scans):
-        step(lp, odo, k, poses)
+    run(lp, odo, args.warmup, n_scans, poses)
     barrier_sync()
     elapsed = time.perf_counter() - t_start
     _ffi.check(L.floam_profile_enable(dev, 0))
@@ -214,12 +224,10 @@ def main():
         # is deterministic) with the byte-counting kernel after each correspondence launch (FLOAM_PROF_KNN_BYTES).
         lp, odo = make_pipeline()
         replay = []
-        for k in range(args.warmup):
-            step(lp, odo, k, replay)
+        run(lp, odo, 0, args.warmup, replay)
         _ffi.check(L.floam_profile_reset(dev))
         _ffi.check(L.floam_profile_enable(dev, 16))
-        for k in range(args.warmup, n_scans):
-            step(lp, odo, k, replay)
+        run(lp, odo, args.warmup, n_scans, replay)
         _ffi.check(L.floam_profile_enable(dev, 0))
         counted = read_timings()
         same = all(np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) for a, b in zip(poses, replay))

@@ -2,19 +2,14 @@
 // CompensateVelocity: src/dataHandler.cpp:82-92.  VoxelGrid / CropBox live in voxel.hip.
 
 #include "cloud_ops.hpp"
-#include "primitives.hpp"
 
 namespace floam {
 
 void SortScratch::reserve(int n) {
-  if ((size_t)n <= k0.cap && temp_bytes > 0) return;
+  if ((size_t)n <= k0.cap) return;
   const size_t want = (size_t)n < 4096 ? 4096 : (size_t)n + (size_t)n / 4;
   k0.reserve(want); k1.reserve(want);
   v0.reserve(want); v1.reserve(want);
-  flags.reserve(want); pos.reserve(want);
-  const size_t tb = std::max(sort_pairs_temp_bytes((int)k0.cap), scan_temp_bytes((int)k0.cap));
-  if (tb > temp.cap) temp.reserve(tb);
-  temp_bytes = temp.cap;
 }
 
 namespace {

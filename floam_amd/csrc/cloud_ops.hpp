@@ -18,11 +18,9 @@ __device__ __forceinline__ void associate_to_map(const double* __restrict__ pose
   oz = (float)((az + cz) + pose[6]);
 }
 
-struct SortScratch {
+struct SortScratch {   // (key, value) ping-pong buffers of the voxel sort
   DevBuf<uint32_t> k0, k1;
-  DevBuf<int> v0, v1, flags, pos;
-  DevBuf<char> temp;
-  size_t temp_bytes = 0;
+  DevBuf<int> v0, v1;
   void reserve(int n);
 };
 

@@ -332,7 +332,8 @@ __global__ __launch_bounds__(kSectorThreads) void fe_output(const PointRec* __re
 // per-call counters for the next call (so no memset nodes are needed).
 __global__ void fe_commit(int n_sectors, const int* __restrict__ sec_edge_cnt, const int* __restrict__ sec_surf_cnt,
                           int* __restrict__ edge_count, int* __restrict__ surf_count, int* __restrict__ ring_count,
-                          int num_lines, int* __restrict__ status, int* __restrict__ out3) {
+                          int num_lines, int* __restrict__ status, int* __restrict__ out3,
+                          int* __restrict__ stat_edge, int* __restrict__ stat_surf) {
   __shared__ int red[2][4];
   int pe = 0, ps = 0;
   for (int k = threadIdx.x; k < n_sectors; k += blockDim.x) {
@@ -356,7 +357,10 @@ __global__ void fe_commit(int n_sectors, const int* __restrict__ sec_edge_cnt, c
     surf_count[0] += ts;
     out3[0] = edge_count[0];
     out3[1] = surf_count[0];
-    out3[2] = *status;
+    const int sv = *status;
+    out3[2] = sv;
+    if (stat_edge) *stat_edge = sv;   // the status travels with the output clouds (asynchronous consumers)
+    if (stat_surf) *stat_surf = sv;
     *status = 0;
   }
   for (int r = threadIdx.x; r < num_lines; r += blockDim.x) ring_count[r] = 0;
@@ -365,7 +369,8 @@ __global__ void fe_commit(int n_sectors, const int* __restrict__ sec_edge_cnt, c
 }  // namespace
 
 void fe_launch(FeScratch& sc, const FeParams& prm, const PointRec* d_in, int n, PointRec* edge_out,
-               int* edge_count, PointRec* surf_out, int* surf_count, hipStream_t st) {
+               int* edge_count, PointRec* surf_out, int* surf_count, hipStream_t st, int* stat_edge,
+               int* stat_surf) {
   const int R = prm.num_lines;
   const int n_pad = ((n + 8191) / 8192) * 8192;   // whole uint4 groups for every bucket thread
   sc.keys.reserve(n_pad);
@@ -409,7 +414,7 @@ void fe_launch(FeScratch& sc, const FeParams& prm, const PointRec* d_in, int n, 
                      surf_out, surf_count);
   FLOAM_LAUNCH_CHECK();
   hipLaunchKernelGGL(fe_commit, dim3(1), dim3(256), 0, st, 6 * R, sc.sec_edge_cnt.p, sc.sec_surf_cnt.p, edge_count,
-                     surf_count, sc.ring_count.p, R, sc.status, sc.out3.p);
+                     surf_count, sc.ring_count.p, R, sc.status, sc.out3.p, stat_edge, stat_surf);
   FLOAM_LAUNCH_CHECK();
 }
 

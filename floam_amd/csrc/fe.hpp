@@ -22,6 +22,7 @@ struct FeScratch {
 
 // Appends edge/surf features of d_in[0, n) to edge_out/surf_out at their device counts (which are advanced).
 void fe_launch(FeScratch& sc, const FeParams& prm, const PointRec* d_in, int n, PointRec* edge_out, int* edge_count,
-               PointRec* surf_out, int* surf_count, hipStream_t st);
+               PointRec* surf_out, int* surf_count, hipStream_t st, int* stat_edge = nullptr,
+               int* stat_surf = nullptr);
 
 }  // namespace floam

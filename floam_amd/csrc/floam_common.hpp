@@ -95,4 +95,9 @@ struct floam_cloud {
   bool host_count_valid = true;
   size_t ub = 0;               // upper bound on the device count while host_count_valid is false
   const int* fe_status = nullptr;   // device status flags of the (asynchronous) feature extraction that filled it
+  floam::DevBuf<int> fe_stat;       // ... stored here (per cloud: the next extraction cannot overwrite it)
+  // cross-stream ordering: the stream of the last operation on the cloud, and an event marking its end
+  hipStream_t last_stream = nullptr;
+  hipEvent_t ev = nullptr;
+  bool ev_valid = false;            // ev recorded after the last operation (else recorded lazily when needed)
 };

@@ -105,24 +105,52 @@ struct ProfScope {
   const char* name;
   double bytes;
   hipEvent_t e0 = nullptr;
-  ProfScope(DeviceCtx& ctx, const char* n, int category, double b = 0.0) : c(ctx), name(n), bytes(b) {
+  hipStream_t s;
+  ProfScope(DeviceCtx& ctx, const char* n, int category, double b = 0.0, hipStream_t stream = nullptr)
+      : c(ctx), name(n), bytes(b), s(stream ? stream : ctx.stream) {
     if (c.profile & category) {
       e0 = c.get_event();
-      FLOAM_HIP(hipEventRecord(e0, c.stream));
+      FLOAM_HIP(hipEventRecord(e0, s));
     }
   }
   ~ProfScope() {
     if (e0) {
       hipEvent_t e1 = c.get_event();
-      (void)hipEventRecord(e1, c.stream);
+      (void)hipEventRecord(e1, s);
       c.pending.push_back(PendingTiming{name, e0, e1, bytes});
     }
   }
 };
 
 // ----------------------------------------------------------------------------------------- cloud helpers
+// Cross-stream ordering of the operations on a cloud.  The feature extraction runs on its handle's own stream (so
+// the next scan's extraction overlaps the current scan's odometry, as the reference's laserProcessingNode runs beside
+// odomEstimationNode); every other operation runs on the device stream.  Before an operation on stream s, s waits
+// for the cloud's last operation if that ran on another stream: for the side stream the event was recorded right
+// after its operation (cloud_publish), for the device stream it is recorded when needed (all of the stream's work
+// issued so far, the cloud's last operation included).
+static void cloud_on(const floam_cloud* cc, hipStream_t s) {
+  auto* c = const_cast<floam_cloud*>(cc);
+  if (c->last_stream && c->last_stream != s) {
+    if (!c->ev) FLOAM_HIP(hipEventCreateWithFlags(&c->ev, hipEventDisableTiming));
+    if (!c->ev_valid) FLOAM_HIP(hipEventRecord(c->ev, c->last_stream));
+    FLOAM_HIP(hipStreamWaitEvent(s, c->ev, 0));
+  }
+  c->last_stream = s;
+  c->ev_valid = false;
+}
+static void cloud_on_main(const floam_cloud* c) { cloud_on(c, ctx_for(c->device).stream); }
+static void cloud_publish(const floam_cloud* cc, hipStream_t s) {   // after an operation on a side stream
+  auto* c = const_cast<floam_cloud*>(cc);
+  if (!c->ev) FLOAM_HIP(hipEventCreateWithFlags(&c->ev, hipEventDisableTiming));
+  FLOAM_HIP(hipEventRecord(c->ev, s));
+  c->last_stream = s;
+  c->ev_valid = true;
+}
+
 static size_t cloud_count_sync(const floam_cloud* c) {
   if (c->host_count_valid) return c->host_count;
+  cloud_on_main(c);
   DeviceCtx& ctx = ctx_for(c->device);
   int v = 0;
   FLOAM_HIP(hipMemcpyAsync(&v, c->count.p, sizeof(int), hipMemcpyDeviceToHost, ctx.stream));
@@ -157,6 +185,7 @@ static void cloud_init(floam_cloud* c, int device, size_t capacity) {
   c->count.reserve(1);
   DeviceCtx& ctx = ctx_for(device);
   FLOAM_HIP(hipMemsetAsync(c->count.p, 0, sizeof(int), ctx.stream));
+  c->last_stream = ctx.stream;
   c->host_count = 0;
   c->host_count_valid = true;
   if (capacity) cloud_reserve(c, capacity, 0, ctx.stream);
@@ -184,6 +213,7 @@ struct floam_lp {
   DevBuf<int> status;
   HostBuf<int> h_out;   // edge count, surf count, status
   bool async = false;   // floam_lp_set_async: no synchronisation, counts stay on the device (upper bounds on host)
+  hipStream_t stream = nullptr;   // the extraction's own stream (overlaps the odometry on the device stream)
 };
 
 struct floam_odom {
@@ -352,6 +382,7 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
     if (std::getenv("FLOAM_DEBUG_STAMPS")) {
       o->dbg_stamps.reserve(32);
       FLOAM_HIP(hipMemsetAsync(o->dbg_stamps.p, 0, sizeof(unsigned long long) * 32, st));
+      FLOAM_HIP(hipMemsetAsync(o->dbg_stamps.p + 25, 0xFF, sizeof(unsigned long long), st));
     }
   }
   o->prof_bytes.reserve(2);
@@ -566,8 +597,9 @@ void floam_reset_process_state(void) { g_keyframe_first = true; }
 
 floam_status floam_device_synchronize(int device) {
   return guarded([&] {
-    DeviceCtx& c = ctx_for(device);
-    FLOAM_HIP(hipStreamSynchronize(c.stream));
+    ctx_for(device);
+    FLOAM_HIP(hipSetDevice(device));
+    FLOAM_HIP(hipDeviceSynchronize());   // every stream (the feature extraction handles' included)
     return FLOAM_OK;
   });
 }
@@ -588,6 +620,10 @@ floam_status floam_cloud_destroy(floam_cloud* c) {
     if (c) {
       DeviceCtx& ctx = ctx_for(c->device);
       FLOAM_HIP(hipStreamSynchronize(ctx.stream));
+      if (c->ev) {
+        if (c->ev_valid) FLOAM_HIP(hipEventSynchronize(c->ev));
+        FLOAM_HIP(hipEventDestroy(c->ev));
+      }
       delete c;
     }
     return FLOAM_OK;
@@ -601,6 +637,7 @@ floam_status floam_cloud_upload(floam_cloud* c, const void* host, size_t n, size
     if (stride < 28) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "stride must cover the PointXYZIRT fields");
     DeviceCtx& ctx = ctx_for(c->device);
     FLOAM_HIP(hipSetDevice(c->device));
+    cloud_on_main(c);
     FLOAM_HIP(hipStreamSynchronize(ctx.stream));
     cloud_reserve(c, std::max<size_t>(n, 1), 0, ctx.stream);
     if (stride == sizeof(PointRec)) {
@@ -632,6 +669,7 @@ floam_status floam_cloud_size(const floam_cloud* c, size_t* n) {
 floam_status floam_cloud_download(const floam_cloud* c, void* host, size_t capacity, size_t* n_out) {
   return guarded([&] {
     if (!c) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null cloud");
+    cloud_on_main(c);
     const size_t n = cloud_count_sync(c);
     if (n_out) *n_out = n;
     const size_t k = std::min(n, capacity);
@@ -649,6 +687,7 @@ floam_status floam_cloud_clear(floam_cloud* c) {
   return guarded([&] {
     if (!c) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null cloud");
     DeviceCtx& ctx = ctx_for(c->device);
+    cloud_on_main(c);
     FLOAM_HIP(hipMemsetAsync(c->count.p, 0, sizeof(int), ctx.stream));
     c->host_count = 0;
     c->host_count_valid = true;
@@ -661,6 +700,8 @@ floam_status floam_cloud_copy(floam_cloud* dst, const floam_cloud* src) {
     if (!dst || !src) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null cloud");
     if (dst->device != src->device) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "clouds on different devices");
     DeviceCtx& ctx = ctx_for(dst->device);
+    cloud_on_main(src);
+    cloud_on_main(dst);
     const size_t n = cloud_count_sync(src);
     cloud_reserve(dst, std::max<size_t>(n, 1), 0, ctx.stream);
     if (n)
@@ -681,6 +722,8 @@ floam_status floam_voxel_grid(const floam_cloud* in, float leaf, floam_cloud* ou
     if (!(leaf > 0.0f)) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "leaf size must be > 0");
     DeviceCtx& ctx = ctx_for(in->device);
     FLOAM_HIP(hipSetDevice(in->device));
+    cloud_on_main(in);
+    cloud_on_main(out);
     const size_t n = cloud_ub(in);
     if (n > (size_t)INT32_MAX / 2) throw Error(FLOAM_ERR_UNSUPPORTED, "cloud too large");
     cloud_reserve(out, std::max<size_t>(n, 1), 0, ctx.stream);
@@ -716,6 +759,7 @@ floam_status floam_lp_create(const floam_lidar_params* p, int device, floam_lp**
     lp->status.reserve(1);
     lp->h_out.reserve(4);
     lp->sc.status = lp->status.p;
+    FLOAM_HIP(hipStreamCreateWithFlags(&lp->stream, hipStreamNonBlocking));
     *out = lp.release();
     return FLOAM_OK;
   });
@@ -732,9 +776,8 @@ floam_status floam_lp_set_async(floam_lp* lp, int async) {
 floam_status floam_lp_wait(floam_lp* lp) {
   return guarded([&] {
     if (!lp) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
-    DeviceCtx& ctx = ctx_for(lp->device);
-    FLOAM_HIP(hipMemcpyAsync(lp->h_out.p, lp->sc.out3.p, sizeof(int) * 3, hipMemcpyDeviceToHost, ctx.stream));
-    FLOAM_HIP(hipStreamSynchronize(ctx.stream));
+    FLOAM_HIP(hipMemcpyAsync(lp->h_out.p, lp->sc.out3.p, sizeof(int) * 3, hipMemcpyDeviceToHost, lp->stream));
+    FLOAM_HIP(hipStreamSynchronize(lp->stream));
     const int status = lp->h_out.p[2];
     if (status & FE_STATUS_SECTOR_TOO_LONG)
       throw Error(FLOAM_ERR_UNSUPPORTED, "a ring sector exceeds 4096 points (ring longer than ~24k points)");
@@ -747,8 +790,10 @@ floam_status floam_lp_wait(floam_lp* lp) {
 floam_status floam_lp_destroy(floam_lp* lp) {
   return guarded([&] {
     if (lp) {
-      DeviceCtx& ctx = ctx_for(lp->device);
-      FLOAM_HIP(hipStreamSynchronize(ctx.stream));
+      if (lp->stream) {
+        FLOAM_HIP(hipStreamSynchronize(lp->stream));
+        FLOAM_HIP(hipStreamDestroy(lp->stream));
+      }
       delete lp;
     }
     return FLOAM_OK;
@@ -762,18 +807,27 @@ floam_status floam_lp_feature_extraction(floam_lp* lp, const floam_cloud* in, fl
       throw Error(FLOAM_ERR_INVALID_ARGUMENT, "clouds and handle on different devices");
     if (edge == surf || in == edge || in == surf) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "clouds must be distinct");
     DeviceCtx& ctx = ctx_for(lp->device);
-    hipStream_t st = ctx.stream;
+    hipStream_t st = lp->stream;
     FLOAM_HIP(hipSetDevice(lp->device));
     const size_t n = cloud_count_sync(in);
     const size_t ne0 = lp->async ? cloud_ub(edge) : cloud_count_sync(edge);
     const size_t ns0 = lp->async ? cloud_ub(surf) : cloud_count_sync(surf);
     const size_t ne_add = std::min(n, (size_t)lp->prm.num_lines * 6 * 20);
+    cloud_on(in, st);
+    cloud_on(edge, st);
+    cloud_on(surf, st);
     cloud_reserve(edge, ne0 + ne_add + 1, ne0, st);
     cloud_reserve(surf, ns0 + n + 1, ns0, st);
+    edge->fe_stat.reserve(1);
+    surf->fe_stat.reserve(1);
     if (n > 0) {
-      ProfScope ps(ctx, "feature_extraction", FLOAM_PROF_FE, 64.0 * (double)n);
-      fe_launch(lp->sc, lp->prm, in->pts.p, (int)n, edge->pts.p, edge->count.p, surf->pts.p, surf->count.p, st);
+      ProfScope ps(ctx, "feature_extraction", FLOAM_PROF_FE, 64.0 * (double)n, st);
+      fe_launch(lp->sc, lp->prm, in->pts.p, (int)n, edge->pts.p, edge->count.p, surf->pts.p, surf->count.p, st,
+                edge->fe_stat.p, surf->fe_stat.p);
     }
+    cloud_publish(in, st);
+    cloud_publish(edge, st);
+    cloud_publish(surf, st);
     if (lp->async && n > 0) {
       // counts stay on the device; the status flags travel with the clouds and are checked at the consumer's
       // synchronisation (odometry update) or by floam_lp_wait
@@ -781,7 +835,8 @@ floam_status floam_lp_feature_extraction(floam_lp* lp, const floam_cloud* in, fl
       edge->ub = ne0 + ne_add;
       surf->host_count_valid = false;
       surf->ub = ns0 + n;
-      edge->fe_status = surf->fe_status = lp->sc.out3.p + 2;
+      edge->fe_status = edge->fe_stat.p;
+      surf->fe_status = surf->fe_stat.p;
       return FLOAM_OK;
     }
     edge->fe_status = surf->fe_status = nullptr;
@@ -852,6 +907,10 @@ floam_status floam_odom_destroy(floam_odom* o) {
         std::fprintf(stderr, "[floam stamps] lm_step x%llu (control block): stage %.2f us, wait %.2f us, reduce %.2f us,"
                    " control step %.2f us\n", h[4], h[0] / n / 100.0, h[1] / n / 100.0, h[2] / n / 100.0,
                    h[3] / n / 100.0);
+        if (h[6])
+          std::fprintf(stderr, "[floam stamps] evaluation blocks: %.2f us each; first start %.2f us, last arrival "
+                       "%.2f us after the control block's start\n", h[5] / (double)h[6] / 100.0, h[7] / n / 100.0,
+                       h[27] / n / 100.0);
         for (int set = 0; set < 2; ++set) {
           const unsigned long long* c = h + 8 + 8 * set;
           const double q = c[4] ? (double)c[4] : 1.0;
@@ -872,6 +931,8 @@ floam_status floam_odom_init_map(floam_odom* o, const floam_cloud* edge, const f
     if (!o || !edge || !surf) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
     DeviceCtx& ctx = ctx_for(o->device);
     hipStream_t st = ctx.stream;
+    cloud_on_main(edge);
+    cloud_on_main(surf);
     const size_t ne = cloud_count_sync(edge), ns = cloud_count_sync(surf);
     const size_t mE = cloud_count_sync(&o->mapE), mS = cloud_count_sync(&o->mapS);
     cloud_reserve(&o->mapE, mE + ne + 1, mE, st);
@@ -893,6 +954,8 @@ floam_status floam_odom_update(floam_odom* o, const floam_cloud* edge, const flo
   return guarded([&] {
     if (!o || !edge || !surf) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
     if (type < 0 || type > 2) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "bad update type");
+    cloud_on_main(edge);
+    cloud_on_main(surf);
     odom_update(o, edge, surf, type);
     return o->last_warning;
   });
@@ -901,6 +964,8 @@ floam_status floam_odom_update(floam_odom* o, const floam_cloud* edge, const flo
 floam_status floam_odom_update_selector(floam_odom* o, floam_cloud* edge, floam_cloud* surf, int deskew) {
   return guarded([&] {
     if (!o || !edge || !surf) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
+    cloud_on_main(edge);
+    cloud_on_main(surf);
     if (!deskew) {
       odom_update(o, edge, surf, FLOAM_VANILLA);
       return o->last_warning;
@@ -961,6 +1026,7 @@ floam_status floam_odom_get_map(floam_odom* o, floam_cloud* out) {
   return guarded([&] {
     if (!o || !out) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
     DeviceCtx& ctx = ctx_for(o->device);
+    cloud_on_main(out);
     const size_t e = cloud_count_sync(&o->mapE), s = cloud_count_sync(&o->mapS), n0 = cloud_count_sync(out);
     cloud_reserve(out, n0 + e + s + 1, n0, ctx.stream);
     append_launch(out->pts.p, out->count.p, o->mapS.pts.p, o->mapS.count.p, (int)s, false, ctx.stream);

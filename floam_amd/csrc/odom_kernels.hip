@@ -11,7 +11,6 @@
 
 #include "grid.hpp"
 #include "odom_kernels.hpp"
-#include "primitives.hpp"
 
 namespace floam {
 
@@ -979,6 +978,7 @@ __device__ void eval_block_at(const double (&x)[7], const double* __restrict__ e
                               const uint8_t* __restrict__ svalid, int scap, int ns, int huber,
                               double* __restrict__ partials, int blk, int nblk);
 
+template <bool SC1>
 __device__ void eval_block(const LMState* __restrict__ st, const double* __restrict__ erec,
                            const uint8_t* __restrict__ evalid, int ecap, int ne, const double* __restrict__ srec,
                            const uint8_t* __restrict__ svalid, int scap, int ns, int huber, double* __restrict__ partials,
@@ -991,7 +991,7 @@ __device__ void eval_block(const LMState* __restrict__ st, const double* __restr
   double x[7];
 #pragma unroll
   for (int k = 0; k < 7; ++k) x[k] = at_x ? xa[k] : xc[k];
-  eval_block_at<false>(x, erec, evalid, ecap, ne, srec, svalid, scap, ns, huber, partials, blk, nblk);
+  eval_block_at<SC1>(x, erec, evalid, ecap, ne, srec, svalid, scap, ns, huber, partials, blk, nblk);
 }
 
 template <bool SC1>
@@ -1075,8 +1075,8 @@ __global__ __launch_bounds__(kTB) void lm_eval(const LMState* __restrict__ st, c
                                                const int* __restrict__ d_ns, int ns_ub, int huber,
                                                double* __restrict__ partials) {
   if (st->done) return;
-  eval_block(st, erec, evalid, ecap, min(*d_ne, ne_ub), srec, svalid, scap, min(*d_ns, ns_ub), huber, partials,
-             blockIdx.x, gridDim.x);
+  eval_block<false>(st, erec, evalid, ecap, min(*d_ne, ne_ub), srec, svalid, scap, min(*d_ns, ns_ub), huber,
+                    partials, blockIdx.x, gridDim.x);
 }
 
 // fixed-size variant for the resident solve: the kEvalBlocks partials of a component are loaded sc1, all in flight
@@ -1102,6 +1102,7 @@ __device__ void reduce_partials_sc1(const double* __restrict__ partials, double*
   __syncthreads();
 }
 
+template <bool SC1 = false>
 __device__ void reduce_partials_block(const double* __restrict__ partials, int nblk, double* sums /* shared */) {
   // component c = t / 8 sums its 8 block strips in order, then thread c sums the 8 strip totals (fixed order)
   __shared__ double strip[LM_NSUM][8];
@@ -1110,7 +1111,7 @@ __device__ void reduce_partials_block(const double* __restrict__ partials, int n
     const int per = (nblk + 7) / 8;
     const int b0 = p * per, b1 = min(nblk, b0 + per);
     double v = 0.0;
-    for (int bb = b0; bb < b1; ++bb) v += partials[c * nblk + bb];
+    for (int bb = b0; bb < b1; ++bb) v += SC1 ? load_sc1(&partials[c * nblk + bb]) : partials[c * nblk + bb];
     strip[c][p] = v;
   }
   __syncthreads();
@@ -1438,15 +1439,11 @@ __global__ __launch_bounds__(kTB) void lm_step(LMState* __restrict__ st, const d
   const int nblk = (int)gridDim.x - 1;
   if (blockIdx.x > 0) {
     if (st->done) return;
-    eval_block(st, erec, evalid, ecap, min(*d_ne, ne_ub), srec, svalid, scap, min(*d_ns, ns_ub), huber, partials,
-               blockIdx.x - 1, nblk);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    eval_block<true>(st, erec, evalid, ecap, min(*d_ne, ne_ub), srec, svalid, scap, min(*d_ns, ns_ub), huber,
+                     partials, blockIdx.x - 1, nblk);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the sc1 partials have reached L2-coherent memory
     __syncthreads();
-    if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      atomicAdd(counter, 1u);
-    }
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
   __shared__ LMState sst;
@@ -1473,8 +1470,6 @@ __global__ __launch_bounds__(kTB) void lm_step(LMState* __restrict__ st, const d
       }
       __builtin_amdgcn_s_sleep(1);
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     s_timeout = timeout;
     t2 = __builtin_amdgcn_s_memrealtime();
   }
@@ -1487,7 +1482,7 @@ __global__ __launch_bounds__(kTB) void lm_step(LMState* __restrict__ st, const d
     }
     return;
   }
-  reduce_partials_block(partials, nblk, sums);
+  reduce_partials_block<true>(partials, nblk, sums);   // sc1 loads: no invalidation needed
   t3 = __builtin_amdgcn_s_memrealtime();
   if (threadIdx.x == 0) *counter = 0u;   // ready for the next launch (kernel boundary orders it)
   lm_logic_wave0(sst, sums);
@@ -1744,8 +1739,8 @@ __device__ void surf_sums_from_gram(const double (&x)[7], const double* o /* sha
 
 // G of this solve into LDS: either reduced from the surf geometry blocks' partials (first evaluation of the solve;
 // fixed order: 8 strips of 32 blocks, then the strips) and published to gmat with the origin o = x (no step has been
-// taken yet), or loaded from gmat.
-__device__ void gram_load(const double* __restrict__ gpart, double* __restrict__ gmat, bool reduce,
+// taken yet), or unpacked from gv = gmat[t] (loaded by the caller together with the LM state).
+__device__ void gram_load(const double* __restrict__ gpart, double* __restrict__ gmat, bool reduce, double gv,
                           const LMState& sst, double (*G)[kGramW], double* o) {
   __shared__ double s_gp[kGram][8];
   const int t = threadIdx.x;
@@ -1764,14 +1759,12 @@ __device__ void gram_load(const double* __restrict__ gpart, double* __restrict__
     __syncthreads();
   }
   if (t < kGram) {
-    double a;
+    double a = gv;
     if (reduce) {
       a = s_gp[t][0];
 #pragma unroll
       for (int p = 1; p < 8; ++p) a += s_gp[t][p];
       gmat[t] = a;
-    } else {
-      a = gmat[t];
     }
     int i, j;
     gram_pair(t, i, j);
@@ -1779,7 +1772,7 @@ __device__ void gram_load(const double* __restrict__ gpart, double* __restrict__
     G[j][i] = a;
   } else if (t < kGramWords) {
     const int k = t - kGram;
-    const double v = reduce ? sst.x[4 + k] : gmat[t];
+    const double v = reduce ? sst.x[4 + k] : gv;
     if (reduce) gmat[t] = v;
     o[k] = v;
   }
@@ -1797,14 +1790,21 @@ __global__ __launch_bounds__(kTB) void lm_step_gram(LMState* __restrict__ st, co
                                                     unsigned* __restrict__ counter, unsigned long long* __restrict__ dbg) {
   const int nblk = (int)gridDim.x - 1;
   if (blockIdx.x > 0) {
+    const unsigned long long e0 = __builtin_amdgcn_s_memrealtime();
     if (st->done) return;
-    eval_block(st, erec, evalid, ecap, min(*d_ne, ne_ub), nullptr, nullptr, 0, 0, 0, partials, blockIdx.x - 1, nblk);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    eval_block<true>(st, erec, evalid, ecap, min(*d_ne, ne_ub), nullptr, nullptr, 0, 0, 0, partials, blockIdx.x - 1,
+                     nblk);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the sc1 partials have reached L2-coherent memory
     __syncthreads();
     if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      atomicAdd(counter, 1u);
+      if (dbg) {   // evaluation block window: first start, last arrival, summed duration
+        const unsigned long long e1 = __builtin_amdgcn_s_memrealtime();
+        atomicMin(&dbg[25], e0);
+        atomicMax(&dbg[26], e1);
+        atomicAdd(&dbg[5], e1 - e0);
+        atomicAdd(&dbg[6], 1ull);
+      }
+      __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     return;
   }
@@ -1816,14 +1816,16 @@ __global__ __launch_bounds__(kTB) void lm_step_gram(LMState* __restrict__ st, co
   __shared__ int s_timeout;
   constexpr int kWords = (int)(sizeof(LMState) / sizeof(unsigned));
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  {
+  double gv = 0.0;
+  {   // the LM state and (after the first evaluation of the solve) G + o, in one round trip
     const unsigned* gsrc = reinterpret_cast<const unsigned*>(st);
     unsigned* ldst = reinterpret_cast<unsigned*>(&sst);
+    if (!reduce_g && threadIdx.x < kGramWords) gv = gmat[threadIdx.x];
     for (int w = threadIdx.x; w < kWords; w += blockDim.x) ldst[w] = gsrc[w];
   }
   __syncthreads();
   if (sst.done) return;
-  gram_load(gpart, gmat, reduce_g != 0, sst, G, o);
+  gram_load(gpart, gmat, reduce_g != 0, gv, sst, G, o);
   {
     double x[7];
 #pragma unroll
@@ -1840,8 +1842,6 @@ __global__ __launch_bounds__(kTB) void lm_step_gram(LMState* __restrict__ st, co
       }
       __builtin_amdgcn_s_sleep(1);
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     s_timeout = timeout;
     t2 = __builtin_amdgcn_s_memrealtime();
   }
@@ -1854,7 +1854,7 @@ __global__ __launch_bounds__(kTB) void lm_step_gram(LMState* __restrict__ st, co
     }
     return;
   }
-  reduce_partials_block(partials, nblk, sums);
+  reduce_partials_block<true>(partials, nblk, sums);
   if (threadIdx.x < LM_NSUM) sums[threadIdx.x] = sums[threadIdx.x] + ssum[threadIdx.x];   // edge + surf
   __syncthreads();
   t3 = __builtin_amdgcn_s_memrealtime();
@@ -1874,6 +1874,11 @@ __global__ __launch_bounds__(kTB) void lm_step_gram(LMState* __restrict__ st, co
     atomicAdd(&dbg[2], t3 - t2);
     atomicAdd(&dbg[3], t4 - t3);
     atomicAdd(&dbg[4], 1ull);
+    const unsigned long long first = dbg[25], last = dbg[26];
+    atomicAdd(&dbg[7], first > t0 ? first - t0 : 0ull);   // control start -> first evaluation block start
+    atomicAdd(&dbg[27], last > t0 ? last - t0 : 0ull);    // control start -> last arrival
+    dbg[25] = ~0ull;
+    dbg[26] = 0ull;
   }
 }
 

@@ -1,0 +1,167 @@
+// Stable LSD radix sort, one single-pass launch per 8-bit digit (see radix.hpp).
+//
+// A launch sorts by one digit.  Each block takes a ticket (its tile: 256 threads x kItems consecutive elements, so a
+// tile only ever waits on tiles that were already running) and
+//   1. loads its elements: wave w owns the 64 * kItems elements [w * 64 * kItems, ...), lane l element r * 64 + l in
+//      round r, so (round, lane) order is input order;
+//   2. ranks them stably: per round, the lanes holding the same digit find each other with 8 ballots, each takes
+//      its position among them, and the highest of them advances the wave's counter of that digit (LDS; one wave
+//      reads and writes its own counters in program order);
+//   3. thread d (one per digit): the wave offsets of digit d, the tile's count of d published to the lookback
+//      word (tile, d), the exclusive prefix of d over the earlier tiles by walking back to an inclusive word, and
+//      the digit's bucket start (exclusive scan of the global histogram);
+//   4. scatters every element to bucket start + tile prefix + wave offset + rank.
+// Lookback words are 64 bits — epoch (30) | flag (2) | count (32) — stored and loaded with agent-scope atomics,
+// so no array has to be cleared between sorts: a word from an older sort carries an older epoch.
+#include "radix.hpp"
+
+namespace floam {
+
+namespace {
+constexpr int kTB = 256;
+constexpr int kItems = 8;
+constexpr int kTile = kTB * kItems;
+constexpr unsigned long long kFlagAgg = 1ull << 32, kFlagInc = 2ull << 32;
+
+__device__ __forceinline__ unsigned long long lb_word(unsigned epoch, unsigned long long flag, unsigned v) {
+  return ((unsigned long long)epoch << 34) | flag | (unsigned long long)v;
+}
+
+__device__ __forceinline__ unsigned long long match_digit(unsigned d, bool valid) {
+  unsigned long long m = __ballot(valid);
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    const bool bit = (d >> b) & 1u;
+    const unsigned long long v = __ballot(bit);
+    m &= bit ? v : ~v;
+  }
+  return m;
+}
+
+__global__ __launch_bounds__(kTB) void radix_pass(const uint32_t* __restrict__ kin, const int* __restrict__ vin,
+                                                  uint32_t* __restrict__ kout, int* __restrict__ vout, int n,
+                                                  int pass, unsigned* __restrict__ ctl,
+                                                  unsigned long long* __restrict__ status, unsigned epoch) {
+  __shared__ unsigned s_wcnt[kTB / 64][kRadixDigits];
+  __shared__ unsigned s_off[kRadixDigits];
+  __shared__ unsigned s_wsum[kTB / 64];
+  __shared__ int s_tile;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int shift = 8 * pass;
+  if (t == 0) s_tile = (int)atomicAdd(&ctl[kRadixHistWords + pass], 1u);
+#pragma unroll
+  for (int k = 0; k < kTB / 64; ++k) s_wcnt[k][t] = 0u;
+  __syncthreads();
+  const int tile = s_tile;
+  const int base = tile * kTile + w * 64 * kItems;
+  uint32_t key[kItems];
+  int val[kItems];
+#pragma unroll
+  for (int r = 0; r < kItems; ++r) {
+    const int i = base + r * 64 + lane;
+    key[r] = i < n ? kin[i] : 0u;
+    val[r] = i < n ? vin[i] : 0;
+  }
+  // 2. stable rank within (wave, digit)
+  unsigned rank[kItems];
+  const unsigned long long lt = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int r = 0; r < kItems; ++r) {
+    const bool valid = base + r * 64 + lane < n;
+    const unsigned d = (key[r] >> shift) & 255u;
+    const unsigned long long peers = match_digit(d, valid);
+    const unsigned before = s_wcnt[w][d];
+    rank[r] = before + (unsigned)__popcll(peers & lt);
+    if (valid && lane == 63 - __clzll((long long)peers)) s_wcnt[w][d] = before + (unsigned)__popcll(peers);
+  }
+  __syncthreads();
+  // 3. thread t = digit t: wave offsets, tile count, bucket start, lookback over the earlier tiles
+  unsigned c[kTB / 64], cnt = 0;
+#pragma unroll
+  for (int k = 0; k < kTB / 64; ++k) {
+    c[k] = s_wcnt[k][t];
+    s_wcnt[k][t] = cnt;   // exclusive over the waves
+    cnt += c[k];
+  }
+  unsigned long long* st = status;   // this pass's [tiles][256] region is passed in
+  __hip_atomic_store(&st[(size_t)tile * kRadixDigits + t], lb_word(epoch, tile == 0 ? kFlagInc : kFlagAgg, cnt),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // bucket start of digit t: exclusive scan of the pass histogram (wave scan + wave totals)
+  const unsigned h = ctl[pass * kRadixDigits + t];
+  unsigned incl = h;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned u = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += u;
+  }
+  if (lane == 63) s_wsum[w] = incl;
+  unsigned prefix = 0;
+  if (tile > 0) {
+    bool failed = false;
+    long long polls = 0;
+    for (int j = tile - 1; j >= 0;) {
+      const unsigned long long x =
+          __hip_atomic_load(&st[(size_t)j * kRadixDigits + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long flag = x & (3ull << 32);
+      if ((unsigned)(x >> 34) != (epoch & 0x3FFFFFFFu) || flag == 0) {
+        if (++polls > (1ll << 22)) { failed = true; break; }
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      prefix += (unsigned)(x & 0xFFFFFFFFull);
+      if (flag == kFlagInc) break;
+      --j;
+    }
+    if (failed) atomicOr(&ctl[kRadixHistWords + 4], 1u);
+    __hip_atomic_store(&st[(size_t)tile * kRadixDigits + t], lb_word(epoch, kFlagInc, prefix + cnt), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  unsigned wb = 0;
+#pragma unroll
+  for (int k = 0; k < kTB / 64; ++k)
+    if (k < w) wb += s_wsum[k];
+  s_off[t] = wb + incl - h + prefix;
+  __syncthreads();
+  // 4. scatter
+#pragma unroll
+  for (int r = 0; r < kItems; ++r) {
+    if (base + r * 64 + lane < n) {
+      const unsigned d = (key[r] >> shift) & 255u;
+      const unsigned dst = s_off[d] + s_wcnt[w][d] + rank[r];
+      kout[dst] = key[r];
+      vout[dst] = val[r];
+    }
+  }
+}
+}  // namespace
+
+void RadixScratch::reserve(int n) {
+  ctl.reserve(kRadixCtlWords);
+  const int tiles = (int)div_up((unsigned)std::max(n, 1), (unsigned)kTile);
+  if (tiles > tiles_cap) {
+    const int cap = tiles + tiles / 4 + 4;
+    status.release();
+    status.reserve((size_t)kRadixPasses * cap * kRadixDigits);
+    // a fresh array: make every word's epoch field differ from the next epochs
+    FLOAM_HIP(hipMemset(status.p, 0xFF, sizeof(unsigned long long) * kRadixPasses * cap * kRadixDigits));
+    tiles_cap = cap;
+  }
+}
+
+void radix_sort_launch(RadixScratch& sc, uint32_t* k0, int* v0, uint32_t* k1, int* v1, int n, hipStream_t st) {
+  if (n <= 0) return;
+  sc.reserve(n);
+  sc.epoch = (sc.epoch + 1) & 0x3FFFFFFFu;
+  if (sc.epoch == 0x3FFFFFFFu) sc.epoch = 0;   // all-ones is the fresh-array pattern
+  const int tiles = (int)div_up((unsigned)n, (unsigned)kTile);
+  for (int p = 0; p < kRadixPasses; ++p) {
+    const bool even = (p & 1) == 0;
+    hipLaunchKernelGGL(radix_pass, dim3(tiles), dim3(kTB), 0, st, even ? k0 : k1, even ? v0 : v1, even ? k1 : k0,
+                       even ? v1 : v0, n, p, sc.ctl.p, sc.status.p + (size_t)p * sc.tiles_cap * kRadixDigits,
+                       sc.epoch);
+    FLOAM_LAUNCH_CHECK();
+  }
+}
+
+}  // namespace floam

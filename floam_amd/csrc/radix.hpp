@@ -1,0 +1,51 @@
+// Stable LSD radix sort of (u32 key, i32 value) pairs for the VoxelGrid pipeline (voxel.hip): 8-bit digits, one
+// single-pass ("onesweep") launch per digit — tile ranking by wave-level digit matching, per-digit decoupled
+// lookback across tiles, scatter — with the four digit histograms accumulated by the key-producing kernel.
+#pragma once
+#include "floam_common.hpp"
+
+namespace floam {
+
+constexpr int kRadixDigits = 256;
+constexpr int kRadixPasses = 4;
+constexpr int kRadixHistWords = kRadixPasses * kRadixDigits;   // followed by 4 tile tickets + 1 error word
+constexpr int kRadixCtlWords = kRadixHistWords + 8;
+
+struct RadixScratch {
+  DevBuf<unsigned> ctl;                  // [4][256] digit histograms, [4] tickets, [1] error (zeroed per sort)
+  DevBuf<unsigned long long> status;     // [4][tiles][256] lookback words, tagged with the sort's epoch
+  int tiles_cap = 0;
+  unsigned epoch = 0;
+  void reserve(int n);
+};
+
+// Producer side (inside the kernel that writes the keys; all threads of the block call both):
+//   radix_hist_begin(s_hist)            zero a [1024] LDS histogram
+//   radix_hist_add(s_hist, key)         per key (LDS atomics)
+//   radix_hist_end(s_hist, ctl)         fold the block's histogram into ctl (global atomics, non-zero bins)
+// ctl must be zero before the producer runs (radix_ctl_zero, e.g. from an earlier kernel of the same stream).
+__device__ __forceinline__ void radix_hist_begin(unsigned* s_hist) {
+  for (int k = threadIdx.x; k < kRadixHistWords; k += blockDim.x) s_hist[k] = 0u;
+  __syncthreads();
+}
+__device__ __forceinline__ void radix_hist_add(unsigned* s_hist, uint32_t key) {
+#pragma unroll
+  for (int p = 0; p < kRadixPasses; ++p) atomicAdd(&s_hist[p * kRadixDigits + ((key >> (8 * p)) & 255u)], 1u);
+}
+__device__ __forceinline__ void radix_hist_end(const unsigned* s_hist, unsigned* ctl) {
+  __syncthreads();
+  for (int k = threadIdx.x; k < kRadixHistWords; k += blockDim.x) {
+    const unsigned v = s_hist[k];
+    if (v) atomicAdd(&ctl[k], v);
+  }
+}
+__device__ __forceinline__ void radix_ctl_zero(unsigned* ctl, int t, int stride) {
+  for (int k = t; k < kRadixCtlWords; k += stride) ctl[k] = 0u;
+}
+
+// The four passes: (k0, v0) -> (k1, v1) -> (k0, v0) -> (k1, v1) -> (k0, v0); the sorted pairs end in k0 / v0.
+// n must be the element count the histograms were built over.  ctl[1028] != 0 afterwards if a lookback timed out
+// (never expected; the consumer reports it).
+void radix_sort_launch(RadixScratch& sc, uint32_t* k0, int* v0, uint32_t* k1, int* v1, int n, hipStream_t st);
+
+}  // namespace floam

@@ -11,14 +11,15 @@
 // the stable (input) order; PCL's unstable std::sort can only change a centroid's float summation order.
 //
 // Launches per call (both clouds): vox_minmax (block partials), vox_keys (reduce partials -> 32-bit keys with the
-// cloud in bit 31, dropped points -> 0xFFFFFFFF), one stable radix sort (rocPRIM), vox_compact (run heads +
-// single-pass decoupled-lookback positions for both clouds at once + centroids).
+// cloud in bit 31, dropped points -> 0xFFFFFFFF, + the sort's digit histograms), the four single-pass digit launches
+// of a stable radix sort (radix.hip), vox_compact (run heads + single-pass decoupled-lookback positions for both
+// clouds at once + centroids).
 #include <cfloat>
 #include <climits>
 
 #include "cloud_ops.hpp"
 #include "lookback.hpp"
-#include "primitives.hpp"
+#include "radix.hpp"
 #include "voxel.hpp"
 
 namespace floam {
@@ -70,8 +71,10 @@ __device__ __forceinline__ bool vox_fetch(const VoxelJobDev& J, int n0, int n1, 
   return true;
 }
 
-__global__ __launch_bounds__(kTB) void vox_minmax(VoxelJobDev A, VoxelJobDev B, float* __restrict__ partials) {
+__global__ __launch_bounds__(kTB) void vox_minmax(VoxelJobDev A, VoxelJobDev B, float* __restrict__ partials,
+                                                  unsigned* __restrict__ radix_ctl) {
   const VoxelJobDev& J = blockIdx.y == 0 ? A : B;
+  if (blockIdx.x == 0 && blockIdx.y == 0) radix_ctl_zero(radix_ctl, threadIdx.x, blockDim.x);   // for vox_keys
   const int n0 = *J.d_n0, n1 = J.d_n1 ? *J.d_n1 : 0;
   float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n0 + n1; i += gridDim.x * blockDim.x) {
@@ -127,10 +130,13 @@ __device__ __forceinline__ VoxelGeom voxel_geom(const float (&mn)[3], const floa
 __global__ __launch_bounds__(kTB) void vox_keys(VoxelJobDev A, VoxelJobDev B, const float* __restrict__ partials,
                                                 uint32_t* __restrict__ keys, int* __restrict__ vals,
                                                 int* __restrict__ overflow, unsigned long long* __restrict__ status,
-                                                int ntiles, unsigned* __restrict__ ticket) {
+                                                int ntiles, unsigned* __restrict__ ticket,
+                                                unsigned* __restrict__ radix_ctl) {
   const int job = blockIdx.y;
   const VoxelJobDev& J = job == 0 ? A : B;
   __shared__ float s_mm[6];
+  __shared__ unsigned s_hist[kRadixHistWords];
+  radix_hist_begin(s_hist);
   if (threadIdx.x < 6) {
     const bool is_min = threadIdx.x < 3;
     float v = is_min ? FLT_MAX : -FLT_MAX;
@@ -167,14 +173,16 @@ __global__ __launch_bounds__(kTB) void vox_keys(VoxelJobDev A, VoxelJobDev B, co
     }
     keys[J.base + i] = key;
     vals[J.base + i] = i;
+    radix_hist_add(s_hist, key);
   }
+  radix_hist_end(s_hist, radix_ctl);
 }
 
 // Run heads of the sorted keys -> output slot per cloud (decoupled lookback over tiles) -> centroid of the run.
 __global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B, const uint32_t* __restrict__ keys,
                                                    const int* __restrict__ vals, const int* __restrict__ overflow,
                                                    int total, unsigned long long* __restrict__ status,
-                                                   unsigned* __restrict__ ticket) {
+                                                   unsigned* __restrict__ ticket, const unsigned* __restrict__ radix_ctl) {
   const int tile = lookback_ticket(ticket);
   const int ntiles = (int)gridDim.x;
   const int t0 = tile * kTile;
@@ -362,8 +370,9 @@ __global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B,
     }
   }
   if (tile == ntiles - 1 && threadIdx.x == 0) {
-    *A.d_out = pre.a + agg[0];
-    *B.d_out = pre.b + agg[1];
+    const bool sort_failed = radix_ctl[kRadixHistWords + 4] != 0u;   // a sort lookback timed out (never expected)
+    *A.d_out = sort_failed ? -1 : pre.a + agg[0];
+    *B.d_out = sort_failed ? -1 : pre.b + agg[1];
   }
 }
 
@@ -390,15 +399,17 @@ void voxel2_launch(VoxelScratch2& sc, const VoxelJob& a, const VoxelJob& b, hipS
   sc.status.reserve(ntiles);
   sc.ticket.reserve(1);
   const int umax = std::max(A.n0_ub + A.n1_ub, b.n0_ub + (b.part1 ? b.n1_ub : 0));
-  hipLaunchKernelGGL(vox_minmax, dim3(kMinMaxBlocks, 2), dim3(kTB), 0, st, A, B, sc.partials.p);
+  sc.rs.reserve(n);
+  hipLaunchKernelGGL(vox_minmax, dim3(kMinMaxBlocks, 2), dim3(kTB), 0, st, A, B, sc.partials.p, sc.rs.ctl.p);
   FLOAM_LAUNCH_CHECK();
-  const unsigned kb = std::max(1u, std::min(div_up(std::max(umax, 1), kTB), 1024u));
+  // few blocks: each folds its LDS digit histograms into the global ones with one atomic per non-zero bin
+  const unsigned kb = std::max(1u, std::min(div_up(std::max(umax, 1), kTB), 64u));
   hipLaunchKernelGGL(vox_keys, dim3(kb, 2), dim3(kTB), 0, st, A, B, sc.partials.p, sc.s.k0.p, sc.s.v0.p,
-                     sc.overflow.p, sc.status.p, ntiles, sc.ticket.p);
+                     sc.overflow.p, sc.status.p, ntiles, sc.ticket.p, sc.rs.ctl.p);
   FLOAM_LAUNCH_CHECK();
-  sort_pairs_u32(sc.s.temp.p, sc.s.temp_bytes, sc.s.k0.p, sc.s.k1.p, sc.s.v0.p, sc.s.v1.p, n, 32, st);
-  hipLaunchKernelGGL(vox_compact, dim3(ntiles), dim3(kTB), 0, st, A, B, sc.s.k1.p, sc.s.v1.p, sc.overflow.p, n,
-                     sc.status.p, sc.ticket.p);
+  radix_sort_launch(sc.rs, sc.s.k0.p, sc.s.v0.p, sc.s.k1.p, sc.s.v1.p, n, st);   // sorted pairs in k0 / v0
+  hipLaunchKernelGGL(vox_compact, dim3(ntiles), dim3(kTB), 0, st, A, B, sc.s.k0.p, sc.s.v0.p, sc.overflow.p, n,
+                     sc.status.p, sc.ticket.p, sc.rs.ctl.p);
   FLOAM_LAUNCH_CHECK();
 }
 

@@ -2,6 +2,7 @@
 #pragma once
 #include "cloud_ops.hpp"
 #include "floam_common.hpp"
+#include "radix.hpp"
 
 namespace floam {
 
@@ -28,9 +29,10 @@ struct VoxelScratch2 {
   DevBuf<int> overflow;
   DevBuf<unsigned long long> status;
   DevBuf<unsigned> ticket;
+  RadixScratch rs;
 };
 
-// Two independent voxel grids in one pipeline (4 kernels + one sort).  *d_out of each job receives the voxel count
+// Two independent voxel grids in one pipeline (3 kernels + the 4 radix passes).  *d_out of each job receives the voxel count
 // (-1 if the single-pass compaction failed, never expected).
 void voxel2_launch(VoxelScratch2& sc, const VoxelJob& a, const VoxelJob& b, hipStream_t st);
 

@@ -144,6 +144,46 @@ def test_odometry_async_feature_extraction(floam_gpu, oracle_lib):
         np.testing.assert_array_equal(a[4][1], b[4][1])
 
 
+def test_odometry_pipelined_feature_extraction(floam_gpu, oracle_lib):
+    """The bench's streaming order: the extraction of scan k+1 (its own stream) is issued before the odometry of
+    scan k, into alternating buffers and into a buffer the previous odometry still reads.  Poses bit-identical to
+    the sequential run."""
+    from floam_amd.odom_estimation import reset_process_state
+    sync, _, _ = _run_sequence(floam_gpu, oracle_lib, "c1", 8)
+    R = synth.lidar_model("c1").rings
+    lp = floam_gpu.LaserProcessingClass(asynchronous=True)
+    lp.init(_params(R))
+    raws = [floam_gpu.DeviceCloud(synth.generate_scan("c1", k)) for k in range(8)]
+    for nbuf in (2, 1):   # 1: every extraction rewrites the clouds the previous odometry just used
+        reset_process_state()
+        odo = floam_gpu.OdomEstimationClass()
+        odo.init(_params(R), 0.1, "Cauchy")
+        bufs = [(floam_gpu.DeviceCloud(), floam_gpu.DeviceCloud()) for _ in range(nbuf)]
+
+        def extract(k):
+            e, s = bufs[k % nbuf]
+            e.clear()
+            s.clear()
+            lp.featureExtraction(raws[k], e, s)
+
+        poses = []
+        extract(0)
+        for k in range(8):
+            e, s = bufs[k % nbuf]
+            if k == 0:
+                odo.initMapWithPoints(e, s)
+            if nbuf > 1 and k + 1 < 8:
+                extract(k + 1)
+            if k > 0:
+                odo.UpdatePointsToMapSelector(e, s, True)
+            poses.append(odo.pose())
+            if nbuf == 1 and k + 1 < 8:
+                extract(k + 1)
+        for a, (q, t) in zip(sync, poses):
+            np.testing.assert_array_equal(a[4][0], q)
+            np.testing.assert_array_equal(a[4][1], t)
+
+
 def test_async_feature_extraction_error_surfaces(floam_gpu):
     """An out-of-range ring (UB in the reference) is reported by the consumer in asynchronous mode."""
     from floam_amd import FloamError
