@@ -159,6 +159,7 @@ def main():
                 odo.set_shard_callback(rank, world, _allreduce)
                 allreduce_impl = "gloo-host"
         odo.initMapWithPoints(d_mapE, d_mapS)
+        odo.set_async(2)
         n_pipelines += 1
         return lp, odo
 
@@ -173,16 +174,24 @@ def main():
         s.clear()
         lp.featureExtraction(d_raw[k], e, s)
 
+    host_split = [0.0, 0.0]   # host seconds issuing / waiting (diagnostic, FLOAM_BENCH_HOST=1)
+
     def run(lp, odo, a, b, poses):
-        """scans [a, b): featureExtraction + UpdatePointsToMapSelector each, extraction one scan ahead"""
+        """scans [a, b): featureExtraction + UpdatePointsToMapSelector each, extraction one scan ahead; the odometry
+        streams (floam_odom_set_async): scan k's pose is collected after scan k+1 has been issued"""
         if a < b:
             extract(lp, a)
         for k in range(a, b):
+            t0 = time.perf_counter()
             if k + 1 < b:
                 extract(lp, k + 1)
             e, s = bufs[k & 1]
             odo.UpdatePointsToMapSelector(e, s, True)
-            poses.append(odo.pose())
+            t1 = time.perf_counter()
+            poses.extend(odo.wait(1))
+            host_split[0] += t1 - t0
+            host_split[1] += time.perf_counter() - t1
+        poses.extend(odo.wait(0))
 
     def barrier_sync():
         if dist is not None:
@@ -200,6 +209,9 @@ def main():
     run(lp, odo, args.warmup, n_scans, poses)
     barrier_sync()
     elapsed = time.perf_counter() - t_start
+    if os.environ.get("FLOAM_BENCH_HOST"):
+        log(f"[host] per scan over the whole run: issue {1e6 * host_split[0] / n_scans:.0f} us, "
+            f"wait {1e6 * host_split[1] / n_scans:.0f} us")
     _ffi.check(L.floam_profile_enable(dev, 0))
     if dist is not None:
         import torch

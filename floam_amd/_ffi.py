@@ -33,6 +33,7 @@ EXPORTS = [
     "floam_odom_create", "floam_odom_destroy", "floam_odom_init_map", "floam_odom_update_selector",
     "floam_odom_update", "floam_odom_get_pose", "floam_odom_get_last_pose", "floam_odom_get_velocity",
     "floam_odom_get_map", "floam_odom_get_map_sizes", "floam_odom_download_maps", "floam_odom_get_stats",
+    "floam_odom_set_async", "floam_odom_wait",
     "floam_comm_unique_id", "floam_odom_set_shard", "floam_odom_set_shard_callback",
     "floam_last_error", "floam_version", "floam_reset_process_state", "floam_device_synchronize",
     "floam_profile_enable", "floam_profile_read", "floam_profile_reset",
@@ -95,6 +96,7 @@ def load(path: str | None = None):
         "floam_odom_get_last_pose": [vp, dp, dp], "floam_odom_get_velocity": [vp, dp],
         "floam_odom_get_map": [vp, vp], "floam_odom_get_map_sizes": [vp, szp, szp],
         "floam_odom_download_maps": [vp, vp, sz, vp, sz], "floam_odom_get_stats": [vp, C.POINTER(OdomStats)],
+        "floam_odom_set_async": [vp, i32], "floam_odom_wait": [vp, sz, dp, sz, szp],
         "floam_comm_unique_id": [vp], "floam_odom_set_shard": [vp, i32, i32, vp],
         "floam_odom_set_shard_callback": [vp, i32, i32, ALLREDUCE_FN, vp],
         "floam_device_synchronize": [i32], "floam_profile_enable": [i32, i32],

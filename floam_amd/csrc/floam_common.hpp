@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
+#include <cstdio>
+#include <cstdlib>
 #include <cstdint>
 #include <stdexcept>
 #include <string>
@@ -60,10 +62,15 @@ struct DevBuf {
   // grow-only; contents are not preserved
   void reserve(size_t n) {
     if (n <= cap) return;
+    if (alloc_log()) std::fprintf(stderr, "[floam alloc] %zu x %zu B (had %zu)\n", n, sizeof(T), cap);
     release();
-    size_t c = n < 1024 ? 1024 : n + n / 4;
+    size_t c = n < 1024 ? 1024 : n + n / 2;   // headroom: a reallocation (hipFree) stalls the device
     FLOAM_HIP(hipMalloc(&p, c * sizeof(T)));
     cap = c;
+  }
+  static bool alloc_log() {   // FLOAM_LOG_ALLOC=1: report device (re)allocations (diagnostic)
+    static const bool on = std::getenv("FLOAM_LOG_ALLOC") != nullptr;
+    return on;
   }
 };
 

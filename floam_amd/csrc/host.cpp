@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -168,7 +169,7 @@ static size_t cloud_ub(const floam_cloud* c) { return c->host_count_valid ? c->h
 // grow keeping the first `keep` points (stream-ordered copy, then the old buffer is freed after a sync)
 static void cloud_reserve(floam_cloud* c, size_t n, size_t keep, hipStream_t st) {
   if (n <= c->pts.cap) return;
-  const size_t cap = std::max<size_t>(n + n / 4, 1024);
+  const size_t cap = std::max<size_t>(n + n / 2, 1024);
   PointRec* p = nullptr;
   FLOAM_HIP(hipMalloc(&p, cap * sizeof(PointRec)));
   if (keep && c->pts.p) {
@@ -225,8 +226,7 @@ struct floam_odom {
   // local map (device) and host-known exact sizes (valid as of the last synchronisation)
   floam_cloud mapE, mapS;
   floam_cloud mapE_next, mapS_next;   // double buffers: the map update writes here, then the two swap
-  size_t mapE_n = 0, mapS_n = 0;
-  bool maps_exact = true;
+  size_t mapE_n = 0, mapS_n = 0;   // map sizes: exact after a synchronisation, else upper bounds
   // scratch
   DevBuf<PointRec> dE, dS, tmp;
   DevBuf<int> cnt;   // [0] dE count [1] dS count [2] tmp count
@@ -244,17 +244,29 @@ struct floam_odom {
   DevBuf<double> gmat;                  // the solve's surf Gram matrix + its origin
   DevBuf<unsigned long long> dbg_stamps;   // FLOAM_DEBUG_STAMPS=1: lm_step segment times (diagnostic)
   DevBuf<LMState> lm;
-  DevBuf<UpdateStatus> ustat;     // slot 0: first / only call, slot 1: second call of a deskewed selector
+  // status slots, two per in-flight update (first / only call, second call of a deskewed selector)
+  DevBuf<UpdateStatus> ustat;
   HostBuf<UpdateStatus> h_ustat;
-  DevBuf<double> x0buf;           // the second call's prediction, formed on the device
+  DevBuf<OdomDev> ds;             // device-resident controller state (poses, keyframe)
+  // updates issued but not yet collected (asynchronous mode keeps up to `depth` of them in flight)
+  struct Pending {
+    int ring;                     // status slots [2 ring, 2 ring + nslots)
+    int nslots;
+    int map_slot;                 // slot whose map counts precede this update's map update (-1: no map update)
+    size_t addE, addS;            // upper bounds of the points the map update may add
+    hipEvent_t ev;
+  };
+  std::deque<Pending> inflight;
+  int depth = 0;                  // floam_odom_set_async: 0 = every update synchronises (the reference's contract)
+  unsigned long long issued = 0;
+  size_t pendE = 0, pendS = 0;    // sum of addE / addS over the in-flight updates
+  std::vector<double> collected;  // poses {q, t} of the updates collected since the last floam_odom_wait
   DevBuf<unsigned long long> prof_bytes;
   DevBuf<unsigned long long> traffic_set;
   bool prof_bytes_init = false;
-  // pose state (host, double)
+  // host mirror of the controller poses, as of the last collected update
   Pose odom = pose_identity(), last_odom = pose_identity();
-  double parameters[7] = {0, 0, 0, 1, 0, 0, 0};
   int optimization_count = 2;
-  std::vector<Pose> keyframes;
   // sharding
   int rank = 0, world = 1;
   ncclComm_t comm = nullptr;
@@ -292,31 +304,6 @@ void check_params(const floam_lidar_params* p) {
 }
 
 // ------------------------------------------------------------------------------------- odometry internals
-void odom_set_params_from_odom(floam_odom* o) {
-  // q_w_curr = Quaterniond(odom.rotation()); t_w_curr = odom.translation() (odomEstimationClass.cpp:70-71)
-  double q[4];
-  mat_to_quat(o->odom.R, q);
-  for (int i = 0; i < 4; ++i) o->parameters[i] = q[i];
-  for (int i = 0; i < 3; ++i) o->parameters[4 + i] = o->odom.t[i];
-}
-
-bool keyframe_update(floam_odom* o, const Pose& pose) {   // KeyFrameUpdate (odomEstimationClass.cpp:320-343)
-  if (g_keyframe_first || o->keyframes.empty()) {
-    g_keyframe_first = false;
-    o->keyframes.push_back(pose);
-    return true;
-  }
-  const Pose delta = pose_mul(pose_inverse(o->keyframes.back()), pose);
-  const double dm = std::sqrt(delta.t[0] * delta.t[0] + delta.t[1] * delta.t[1] + delta.t[2] * delta.t[2]);
-  const double dr = rotation_angle(delta.R);
-  if (dm > 0.07 || dr > 2 * M_PI / 180.0) {
-    o->keyframes.push_back(pose);
-    if (o->keyframes.size() > 3) o->keyframes.erase(o->keyframes.begin());
-    return true;
-  }
-  return false;
-}
-
 void allreduce_sums(floam_odom* o, DeviceCtx& ctx) {
   if (o->comm) {
     const ncclResult_t r = ncclAllReduce(o->sums.p, o->sums.p, LM_NSUM, ncclDouble, ncclSum, o->comm, ctx.stream);
@@ -332,23 +319,15 @@ void allreduce_sums(floam_odom* o, DeviceCtx& ctx) {
   FLOAM_HIP(hipStreamSynchronize(ctx.stream));
 }
 
-// updatePointsToMap (src/odomEstimationClass.cpp:52-124) is split into four steps so that the two calls of a
-// deskewed UpdatePointsToMapSelector can be issued back to back with a single synchronisation:
-//   odom_predict  host: optimization_count, the constant-velocity prediction (:59-71; branch always taken, Q2)
-//   odom_issue    device: downsample, [grid rebuild], optimization_count x {kNN + geometry, 5 LM steps}, and a
-//                 gather of the solve result into status slot `slot` — no synchronisation
-//   odom_finish   host, after the synchronisation: gate (:77), pose writeback (:114-116), warnings, stats
-//   odom_map_update  host keyframe test (:117-122, KeyFrameUpdate :320-343) and the device map update (:253-294)
-void odom_predict(floam_odom* o) {
-  if (o->optimization_count > 2) o->optimization_count--;
-  const Pose pred = pose_mul(o->odom, pose_mul(pose_inverse(o->last_odom), o->odom));
-  o->last_odom = o->odom;   // Q2: the branch is taken for every update type
-  o->odom = pred;
-  odom_set_params_from_odom(o);
-}
-
+// updatePointsToMap (src/odomEstimationClass.cpp:52-124) runs on the device end to end, the controller included:
+//   odom_predict_launch  optimization_count (host), the constant-velocity prediction (:59-71; always taken, Q2)
+//   odom_issue           downsample, [grid rebuild], optimization_count x {kNN + geometry, 5 LM steps}, and the
+//                        status gather with the pose writeback (:114-116) and KeyFrameUpdate (:117-122, :320-343)
+//   odom_map_update      addPointsToMap (:253-294), gated on the device by the keyframe decision
+// then one device-to-host copy of the status slots; odom_collect reads them (errors, warnings, stats, poses, map
+// sizes) — right away in synchronous mode, later in asynchronous mode.
 void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const floam_cloud* surf, int ne_ub, int ns_ub,
-                const double* x0_host, const double* x0_dev, int slot) {
+                const double* x0_dev, int slot, int gather_mode) {
   hipStream_t st = ctx.stream;
   o->dE.reserve(std::max(ne_ub, 1));
   o->dS.reserve(std::max(ns_ub, 1));
@@ -406,7 +385,7 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
       {
         ProfScope ps1(ctx, "knn_search", FLOAM_PROF_KNN_DETAIL);
         // (also resets the LM state; the first solve starts at the prediction)
-        knn_launch(o->lm.p, it == 0 ? x0_host : nullptr, it == 0 ? x0_dev : nullptr, qe, o->gE, o->mapE.pts.p,
+        knn_launch(o->lm.p, nullptr, it == 0 ? x0_dev : nullptr, qe, o->gE, o->mapE.pts.p,
                    o->ce, qs, o->gS, o->mapS.pts.p, o->cs, o->mapE.count.p, o->mapS.count.p, o->rank, o->world, st,
                    o->dbg_stamps.p ? o->dbg_stamps.p + 8 : nullptr);
       }
@@ -444,23 +423,48 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
       }
     }
   }
-  if (o->optimization_count <= 0) lm_init_launch(o->lm.p, x0_host, st);
+  if (o->optimization_count <= 0) lm_init_dev_launch(o->lm.p, x0_dev, st);
   const bool prof_knn = (ctx.profile & FLOAM_PROF_KNN_BYTES) != 0;
-  o->ustat.reserve(2);
   gather_status_launch(o->lm.p, o->cnt.p, o->mapE.count.p, o->mapS.count.p, edge->fe_status,
-                       prof_knn ? o->prof_bytes.p : nullptr, o->ustat.p + slot, st);
+                       prof_knn ? o->prof_bytes.p : nullptr, o->ustat.p + slot, o->ds.p, gather_mode, st);
   if (prof_knn) FLOAM_HIP(hipMemsetAsync(o->prof_bytes.p, 0, sizeof(unsigned long long) * 2, st));
 }
 
-// the one synchronisation: status slots [0, nslots) to the host
-void odom_sync(floam_odom* o, DeviceCtx& ctx, int nslots) {
-  o->h_ustat.reserve(2);
-  FLOAM_HIP(hipMemcpyAsync(o->h_ustat.p, o->ustat.p, sizeof(UpdateStatus) * nslots, hipMemcpyDeviceToHost,
-                           ctx.stream));
-  FLOAM_HIP(hipStreamSynchronize(ctx.stream));
+// stats and warning of one call from its status slot (the gate :77 and the warnings :112, :193, :248)
+floam_status odom_call_status(floam_odom* o, const UpdateStatus& U) {
+  const LMState& L = U.lm;
+  const int* hc = U.counts;
+  const bool gate = hc[2] > 10 && hc[3] > 50;
+  floam_status w = FLOAM_OK;
+  if (!gate) w = FLOAM_WARN_MAP_TOO_SMALL;
+  else if (L.corr_edge < 20 || L.corr_surf < 20) w = FLOAM_WARN_FEW_CORRESPONDENCES;
+  o->stats.optimization_count = o->optimization_count;
+  o->stats.solves = gate ? o->optimization_count : 0;
+  o->stats.edge_queries = hc[0];
+  o->stats.surf_queries = hc[1];
+  o->stats.edge_correspondences = gate ? L.corr_edge : 0;
+  o->stats.surf_correspondences = gate ? L.corr_surf : 0;
+  o->stats.lm_iterations = gate ? L.iteration : 0;
+  o->stats.final_cost = gate ? L.x_cost : 0.0;
+  o->stats.map_updated = 0;
+  o->stats.corner_map = (size_t)hc[2];
+  o->stats.surf_map = (size_t)hc[3];
+  return w;
+}
+
+// Collect the oldest in-flight update: wait for its status copy, raise its device errors, take its warning, stats,
+// poses and (exact) map sizes.  Returns the update's warning (the second call's, else the first call's).
+floam_status odom_collect_one(floam_odom* o, DeviceCtx& ctx) {
+  const floam_odom::Pending P = o->inflight.front();
+  o->inflight.pop_front();
+  o->pendE -= P.addE;
+  o->pendS -= P.addS;
+  FLOAM_HIP(hipEventSynchronize(P.ev));
+  FLOAM_HIP(hipEventDestroy(P.ev));
   ctx.drain();
-  for (int k = 0; k < nslots; ++k) {
-    const UpdateStatus& U = o->h_ustat.p[k];
+  const UpdateStatus* slots = o->h_ustat.p + 2 * P.ring;
+  for (int k = 0; k < P.nslots; ++k) {
+    const UpdateStatus& U = slots[k];
     if (ctx.profile & FLOAM_PROF_KNN_BYTES) {
       floam_kernel_timing& t = ctx.totals["knn"];
       std::strncpy(t.name, "knn", sizeof(t.name) - 1);
@@ -475,110 +479,141 @@ void odom_sync(floam_odom* o, DeviceCtx& ctx, int nslots) {
     if (U.fe_status & FE_STATUS_BAD_RING)
       throw Error(FLOAM_ERR_INVALID_ARGUMENT, "point ring index >= num_lines (out of bounds in the reference)");
   }
-}
-
-void odom_finish(floam_odom* o, const UpdateStatus& U) {
-  const LMState& L = U.lm;
-  const int* hc = U.counts;
-  o->mapE_n = (size_t)hc[2];
-  o->mapS_n = (size_t)hc[3];
-  o->mapE.host_count = o->mapE_n; o->mapE.host_count_valid = true;
-  o->mapS.host_count = o->mapS_n; o->mapS.host_count_valid = true;
-  o->last_warning = FLOAM_OK;
-  const bool gate = o->mapE_n > 10 && o->mapS_n > 50;   // (:77)
-  if (gate) {
-    std::memcpy(o->parameters, L.x, sizeof(double) * 7);
-    if (L.corr_edge < 20 || L.corr_surf < 20) o->last_warning = FLOAM_WARN_FEW_CORRESPONDENCES;
-  } else {
-    o->last_warning = FLOAM_WARN_MAP_TOO_SMALL;
+  floam_status w = FLOAM_OK;
+  for (int k = 0; k < P.nslots; ++k) {
+    const floam_status wk = odom_call_status(o, slots[k]);
+    if (wk != FLOAM_OK) w = wk;
   }
-  // odom = Isometry(q_w_curr.toRotationMatrix(), t_w_curr) (:114-116)
-  o->odom.R = quat_to_mat(o->parameters);
-  for (int i = 0; i < 3; ++i) o->odom.t[i] = o->parameters[4 + i];
-  o->stats.optimization_count = o->optimization_count;
-  o->stats.solves = gate ? o->optimization_count : 0;
-  o->stats.edge_queries = hc[0];
-  o->stats.surf_queries = hc[1];
-  o->stats.edge_correspondences = gate ? L.corr_edge : 0;
-  o->stats.surf_correspondences = gate ? L.corr_surf : 0;
-  o->stats.lm_iterations = gate ? L.iteration : 0;
-  o->stats.final_cost = gate ? L.x_cost : 0.0;
-  o->stats.map_updated = 0;
+  const UpdateStatus& last = slots[P.nslots - 1];
+  o->odom = last.odom;
+  o->last_odom = last.last_odom;
+  if (P.map_slot >= 0) o->stats.map_updated = slots[P.map_slot].kf_flag;
+  // map sizes: exact before this update's map update, plus what the later in-flight updates may add
+  const UpdateStatus& M = slots[P.map_slot >= 0 ? P.map_slot : P.nslots - 1];
+  o->mapE_n = (size_t)M.counts[2] + P.addE + o->pendE;
+  o->mapS_n = (size_t)M.counts[3] + P.addS + o->pendS;
+  const bool exact = o->inflight.empty() && P.map_slot < 0;
+  o->mapE.host_count_valid = o->mapS.host_count_valid = exact;
+  o->mapE.host_count = o->mapE.ub = o->mapE_n;
+  o->mapS.host_count = o->mapS.ub = o->mapS_n;
+  if (o->depth > 0) {   // asynchronous mode: the poses wait for floam_odom_wait
+    double q[4];
+    mat_to_quat(o->odom.R, q);
+    for (int i = 0; i < 4; ++i) o->collected.push_back(q[i]);
+    for (int i = 0; i < 3; ++i) o->collected.push_back(o->odom.t[i]);
+  }
+  return w;
 }
 
-void odom_map_update(floam_odom* o, DeviceCtx& ctx, int type, const UpdateStatus& U) {
-  if (!(type == FLOAM_VANILLA || type == FLOAM_REFINEMENT_AND_UPDATE)) return;
-  if (!keyframe_update(o, o->odom)) return;
-  // addPointsToMap (:253-294): device-side transform + append + CropBox + VoxelGrid of both maps, using the
-  // optimised pose, which is lm->x (== parameters) on the device.
+floam_status odom_collect(floam_odom* o, DeviceCtx& ctx, size_t max_pending) {
+  floam_status w = FLOAM_OK;
+  while (o->inflight.size() > max_pending) {
+    const floam_status wk = odom_collect_one(o, ctx);
+    if (wk != FLOAM_OK) w = wk;
+  }
+  return w;
+}
+
+// status slots for the next update (collecting the oldest in-flight update if the ring is full)
+int odom_begin(floam_odom* o, DeviceCtx& ctx) {
+  const int ring_n = std::max(o->depth, 1);
+  if (o->inflight.size() >= (size_t)ring_n) {
+    const floam_status w = odom_collect(o, ctx, (size_t)ring_n - 1);
+    if (w != FLOAM_OK) o->last_warning = w;   // reported by the next floam_odom_wait
+  }
+  o->ustat.reserve((size_t)2 * ring_n);
+  o->h_ustat.reserve((size_t)2 * ring_n);
+  return (int)(o->issued++ % (unsigned long long)ring_n);
+}
+
+// the status copy of the update just issued; synchronous mode collects it right away
+floam_status odom_end(floam_odom* o, DeviceCtx& ctx, int ring, int nslots, int map_slot, size_t addE, size_t addS) {
+  FLOAM_HIP(hipMemcpyAsync(o->h_ustat.p + 2 * ring, o->ustat.p + 2 * ring, sizeof(UpdateStatus) * nslots,
+                           hipMemcpyDeviceToHost, ctx.stream));
+  hipEvent_t ev;
+  FLOAM_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  FLOAM_HIP(hipEventRecord(ev, ctx.stream));
+  o->inflight.push_back(floam_odom::Pending{ring, nslots, map_slot, addE, addS, ev});
+  o->pendE += addE;
+  o->pendS += addS;
+  if (o->depth == 0) return odom_collect(o, ctx, 0);
+  return FLOAM_OK;
+}
+
+int gather_keyframe_mode() {   // KeyFrameUpdate's process-wide `first` flag (Q6) is consumed by this call
+  const int m = GATHER_KEYFRAME | (g_keyframe_first ? GATHER_KEYFRAME_FIRST : 0);
+  g_keyframe_first = false;
+  return m;
+}
+
+// addPointsToMap (:253-294), issued unconditionally and gated on the device by the keyframe decision (a skipped
+// update copies the maps unchanged): transform + append + CropBox + VoxelGrid of both maps with the optimised pose
+// (lm->x), one pipeline.  Returns the upper bounds of the points it may add.
+void odom_map_update(floam_odom* o, DeviceCtx& ctx, int ne_ub, int ns_ub, size_t& addE, size_t& addS) {
   hipStream_t st = ctx.stream;
   ProfScope ps(ctx, "map_update", FLOAM_PROF_CLOUD);
-  const int nEd = U.counts[0], nSd = U.counts[1];
-  const int ubS = (int)o->mapS_n + nSd, ubE = (int)o->mapE_n + nEd;
+  const int ubS = (int)o->mapS_n + ns_ub, ubE = (int)o->mapE_n + ne_ub;
   cloud_reserve(&o->mapS_next, std::max(ubS, 1), 0, st);
   cloud_reserve(&o->mapE_next, std::max(ubE, 1), 0, st);
-  // [map ; pointAssociateToMap(downsampled scan)] -> CropBox -> VoxelGrid, both maps in one pipeline
   VoxelJob je, js;
   je.part0 = o->mapE.pts.p; je.d_n0 = o->mapE.count.p; je.n0_ub = (int)o->mapE_n;
-  je.part1 = o->dE.p; je.d_n1 = o->cnt.p + 0; je.n1_ub = nEd;
+  je.part1 = o->dE.p; je.d_n1 = o->cnt.p + 0; je.n1_ub = ne_ub;
   je.pose = o->lm.p->x; je.leaf = o->leafE; je.out = o->mapE_next.pts.p; je.d_out = o->mapE_next.count.p;
   js.part0 = o->mapS.pts.p; js.d_n0 = o->mapS.count.p; js.n0_ub = (int)o->mapS_n;
-  js.part1 = o->dS.p; js.d_n1 = o->cnt.p + 1; js.n1_ub = nSd;
+  js.part1 = o->dS.p; js.d_n1 = o->cnt.p + 1; js.n1_ub = ns_ub;
   js.pose = o->lm.p->x; js.leaf = o->leafS; js.out = o->mapS_next.pts.p; js.d_out = o->mapS_next.count.p;
-  voxel2_launch(o->vs, je, js, st);
+  voxel2_launch(o->vs, je, js, st, &o->ds.p->kf_flag);
   cloud_swap(&o->mapE, &o->mapE_next);
   cloud_swap(&o->mapS, &o->mapS_next);
-  o->mapS_n = (size_t)ubS;   // upper bounds until the next synchronisation
+  addE = (size_t)ne_ub;
+  addS = (size_t)ns_ub;
+  o->mapS_n = (size_t)ubS;   // upper bounds until the update is collected
   o->mapE_n = (size_t)ubE;
   o->mapS.host_count_valid = false;
   o->mapE.host_count_valid = false;
   o->mapS.ub = o->mapS_n;
   o->mapE.ub = o->mapE_n;
   o->grid_dirty = true;
-  o->stats.map_updated = 1;
 }
 
 // updatePointsToMap (src/odomEstimationClass.cpp:52-124), one call
-void odom_update(floam_odom* o, const floam_cloud* edge, const floam_cloud* surf, int type) {
+floam_status odom_update(floam_odom* o, const floam_cloud* edge, const floam_cloud* surf, int type) {
   DeviceCtx& ctx = ctx_for(o->device);
   FLOAM_HIP(hipSetDevice(o->device));
-  odom_predict(o);
-  odom_issue(o, ctx, edge, surf, (int)cloud_ub(edge), (int)cloud_ub(surf), o->parameters, nullptr, 0);
-  odom_sync(o, ctx, 1);
-  odom_finish(o, o->h_ustat.p[0]);
-  odom_map_update(o, ctx, type, o->h_ustat.p[0]);
+  const int ring = odom_begin(o, ctx);
+  const int ne_ub = (int)cloud_ub(edge), ns_ub = (int)cloud_ub(surf);
+  if (o->optimization_count > 2) o->optimization_count--;
+  odom_predict_launch(o->ds.p, ctx.stream);
+  const bool update_map = type == FLOAM_VANILLA || type == FLOAM_REFINEMENT_AND_UPDATE;
+  odom_issue(o, ctx, edge, surf, ne_ub, ns_ub, o->ds.p->x0[0], 2 * ring,
+             GATHER_FINISH | (update_map ? gather_keyframe_mode() : 0));
+  size_t addE = 0, addS = 0;
+  if (update_map) odom_map_update(o, ctx, ne_ub, ns_ub, addE, addS);
+  return odom_end(o, ctx, ring, 1, update_map ? 0 : -1, addE, addS);
 }
 
 // UpdatePointsToMapSelector with deskew (src/odomEstimationClass.cpp:38-47): call 1 (edge, edge) INITIAL_ITERATION
-// (Q4), GetVelocity + CompensateVelocity of both clouds in place (Q5), call 2 (edge, surf) REFINEMENT_AND_UPDATE.
-// The velocity and the second prediction are formed on the device (deskew_bridge), so the whole selector runs with
-// one synchronisation; the host then replays the same pose algebra to keep its state.
+// (Q4), GetVelocity + CompensateVelocity of both clouds in place (Q5), call 2 (edge, surf) REFINEMENT_AND_UPDATE,
+// all issued without a host round trip (the velocity and the second prediction are formed by deskew_bridge).
 floam_status odom_update_deskew(floam_odom* o, floam_cloud* edge, floam_cloud* surf) {
   DeviceCtx& ctx = ctx_for(o->device);
   FLOAM_HIP(hipSetDevice(o->device));
+  const int ring = odom_begin(o, ctx);
   const int ne_ub = (int)cloud_ub(edge), ns_ub = (int)cloud_ub(surf);
-  odom_predict(o);
-  const Pose odom0 = o->last_odom;
-  odom_issue(o, ctx, edge, edge, ne_ub, ne_ub, o->parameters, nullptr, 0);
-  o->x0buf.reserve(7);
+  if (o->optimization_count > 2) o->optimization_count--;
+  odom_predict_launch(o->ds.p, ctx.stream);
+  odom_issue(o, ctx, edge, edge, ne_ub, ne_ub, o->ds.p->x0[0], 2 * ring, 0);
   {
     ProfScope ps(ctx, "deskew", FLOAM_PROF_CLOUD);
-    deskew_bridge_launch(o->lm.p, odom0, o->lp.scan_period, edge->pts.p, edge->count.p, ne_ub, surf->pts.p,
-                         surf->count.p, ns_ub, o->x0buf.p, ctx.stream);
+    deskew_bridge_launch(o->lm.p, o->ds.p, o->lp.scan_period, edge->pts.p, edge->count.p, ne_ub, surf->pts.p,
+                         surf->count.p, ns_ub, ctx.stream);
   }
-  if (o->optimization_count > 2) o->optimization_count--;   // call 2's decrement (the host replays the rest below)
-  odom_issue(o, ctx, edge, surf, ne_ub, ns_ub, nullptr, o->x0buf.p, 1);
-  odom_sync(o, ctx, 2);
-  odom_finish(o, o->h_ustat.p[0]);
-  const floam_status w1 = o->last_warning;
-  // call 2's prediction on the host (bit-identical to the device's, pose.hpp)
-  const Pose pred = pose_mul(o->odom, pose_mul(pose_inverse(o->last_odom), o->odom));
-  o->last_odom = o->odom;
-  o->odom = pred;
-  odom_set_params_from_odom(o);
-  odom_finish(o, o->h_ustat.p[1]);
-  odom_map_update(o, ctx, FLOAM_REFINEMENT_AND_UPDATE, o->h_ustat.p[1]);
-  return o->last_warning != FLOAM_OK ? o->last_warning : w1;
+  if (o->optimization_count > 2) o->optimization_count--;
+  odom_issue(o, ctx, edge, surf, ne_ub, ns_ub, o->ds.p->x0[1], 2 * ring + 1,
+             GATHER_FINISH | GATHER_AFTER_MID | gather_keyframe_mode());
+  size_t addE = 0, addS = 0;
+  odom_map_update(o, ctx, ne_ub, ns_ub, addE, addS);
+  return odom_end(o, ctx, ring, 2, 1, addE, addS);
 }
 
 // CompensateVelocity (src/dataHandler.cpp:82-92) with GetVelocity (include/odomEstimationClass.h:78)
@@ -889,6 +924,8 @@ floam_status floam_odom_create(const floam_lidar_params* p, double map_resolutio
     FLOAM_HIP(hipMemsetAsync(o->cnt.p, 0, sizeof(int) * 4, ctx.stream));
     o->lm.reserve(1);
     FLOAM_HIP(hipMemsetAsync(o->lm.p, 0, sizeof(LMState), ctx.stream));
+    o->ds.reserve(1);
+    odom_dev_init_launch(o->ds.p, ctx.stream);
     FLOAM_HIP(hipStreamSynchronize(ctx.stream));
     *out = o.release();
     return FLOAM_OK;
@@ -900,6 +937,8 @@ floam_status floam_odom_destroy(floam_odom* o) {
     if (o) {
       DeviceCtx& ctx = ctx_for(o->device);
       FLOAM_HIP(hipStreamSynchronize(ctx.stream));
+      for (auto& P : o->inflight) FLOAM_HIP(hipEventDestroy(P.ev));
+      o->inflight.clear();
       if (o->dbg_stamps.p) {
         unsigned long long h[32];
         FLOAM_HIP(hipMemcpy(h, o->dbg_stamps.p, sizeof(h), hipMemcpyDeviceToHost));
@@ -931,6 +970,7 @@ floam_status floam_odom_init_map(floam_odom* o, const floam_cloud* edge, const f
     if (!o || !edge || !surf) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
     DeviceCtx& ctx = ctx_for(o->device);
     hipStream_t st = ctx.stream;
+    odom_collect(o, ctx, 0);
     cloud_on_main(edge);
     cloud_on_main(surf);
     const size_t ne = cloud_count_sync(edge), ns = cloud_count_sync(surf);
@@ -956,8 +996,7 @@ floam_status floam_odom_update(floam_odom* o, const floam_cloud* edge, const flo
     if (type < 0 || type > 2) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "bad update type");
     cloud_on_main(edge);
     cloud_on_main(surf);
-    odom_update(o, edge, surf, type);
-    return o->last_warning;
+    return odom_update(o, edge, surf, type);
   });
 }
 
@@ -966,10 +1005,7 @@ floam_status floam_odom_update_selector(floam_odom* o, floam_cloud* edge, floam_
     if (!o || !edge || !surf) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
     cloud_on_main(edge);
     cloud_on_main(surf);
-    if (!deskew) {
-      odom_update(o, edge, surf, FLOAM_VANILLA);
-      return o->last_warning;
-    }
+    if (!deskew) return odom_update(o, edge, surf, FLOAM_VANILLA);
     return odom_update_deskew(o, edge, surf);
   });
 }
@@ -1003,6 +1039,7 @@ floam_status floam_odom_get_velocity(const floam_odom* o, double v[3]) {
 floam_status floam_odom_get_map_sizes(floam_odom* o, size_t* corner, size_t* surf) {
   return guarded([&] {
     if (!o) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
+    odom_collect(o, ctx_for(o->device), 0);
     const size_t e = cloud_count_sync(&o->mapE), s = cloud_count_sync(&o->mapS);
     o->mapE_n = e;
     o->mapS_n = s;
@@ -1026,6 +1063,7 @@ floam_status floam_odom_get_map(floam_odom* o, floam_cloud* out) {
   return guarded([&] {
     if (!o || !out) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
     DeviceCtx& ctx = ctx_for(o->device);
+    odom_collect(o, ctx, 0);
     cloud_on_main(out);
     const size_t e = cloud_count_sync(&o->mapE), s = cloud_count_sync(&o->mapS), n0 = cloud_count_sync(out);
     cloud_reserve(out, n0 + e + s + 1, n0, ctx.stream);
@@ -1041,9 +1079,33 @@ floam_status floam_odom_get_stats(const floam_odom* o, floam_odom_stats* s) {
   return guarded([&] {
     if (!o || !s) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
     *s = o->stats;
-    s->corner_map = o->mapE_n;
-    s->surf_map = o->mapS_n;
     return FLOAM_OK;
+  });
+}
+
+floam_status floam_odom_set_async(floam_odom* o, int depth) {
+  return guarded([&] {
+    if (!o || depth < 0 || depth > 16) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null handle or depth not in [0, 16]");
+    DeviceCtx& ctx = ctx_for(o->device);
+    const floam_status w = odom_collect(o, ctx, 0);
+    o->collected.clear();
+    o->depth = depth;
+    return w;
+  });
+}
+
+floam_status floam_odom_wait(floam_odom* o, size_t max_pending, double* poses, size_t capacity, size_t* n_out) {
+  return guarded([&] {
+    if (!o) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null handle");
+    DeviceCtx& ctx = ctx_for(o->device);
+    floam_status w = odom_collect(o, ctx, max_pending);
+    if (w == FLOAM_OK) w = o->last_warning;
+    o->last_warning = FLOAM_OK;
+    const size_t n = o->collected.size() / 7;
+    if (n_out) *n_out = n;
+    if (poses) std::memcpy(poses, o->collected.data(), sizeof(double) * 7 * std::min(n, capacity));
+    o->collected.clear();
+    return w;
   });
 }
 

@@ -864,17 +864,17 @@ __global__ void lm_init_dev(LMState* st, X7 x0, const double* __restrict__ x0_de
   lm_reset(st, x0);
 }
 
-__global__ __launch_bounds__(kTB) void deskew_bridge(const LMState* __restrict__ st, Pose odom0, double period,
-                                                     PointRec* __restrict__ edge, const int* __restrict__ d_ne,
-                                                     int ne_ub, PointRec* __restrict__ surf,
-                                                     const int* __restrict__ d_ns, int ns_ub,
-                                                     double* __restrict__ x0_out) {
+__global__ __launch_bounds__(kTB) void deskew_bridge(const LMState* __restrict__ st, OdomDev* __restrict__ s,
+                                                     double period, PointRec* __restrict__ edge,
+                                                     const int* __restrict__ d_ne, int ne_ub,
+                                                     PointRec* __restrict__ surf, const int* __restrict__ d_ns,
+                                                     int ns_ub) {
   double x1[7];
 #pragma unroll
   for (int k = 0; k < 7; ++k) x1[k] = st->x[k];
+  const double* t0 = s->last_odom.t;   // the pose before the first call (read-only in this launch)
   // GetVelocity (include/odomEstimationClass.h:78): (odom.translation() - last_odom.translation()) / scan_period
-  const double vx = (x1[4] - odom0.t[0]) / period, vy = (x1[5] - odom0.t[1]) / period,
-               vz = (x1[6] - odom0.t[2]) / period;
+  const double vx = (x1[4] - t0[0]) / period, vy = (x1[5] - t0[1]) / period, vz = (x1[6] - t0[2]) / period;
   const int ne = min(*d_ne, ne_ub), ns = min(*d_ns, ns_ub);
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < ne + ns; i += gridDim.x * blockDim.x) {
     PointRec& p = i < ne ? edge[i] : surf[i - ne];   // CompensateVelocity: p += v * time, double -> float
@@ -884,18 +884,32 @@ __global__ __launch_bounds__(kTB) void deskew_bridge(const LMState* __restrict__
     p.z = (float)((double)p.z + vz * t);
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    // the second call's prediction (:62-71): odom1 * (last_odom^-1 * odom1), last_odom = odom0
-    Pose odom1;
-    odom1.R = quat_to_mat(x1);
-    odom1.t[0] = x1[4]; odom1.t[1] = x1[5]; odom1.t[2] = x1[6];
-    const Pose pred = pose_mul(odom1, pose_mul(pose_inverse(odom0), odom1));
-    double q[4];
-    mat_to_quat(pred.R, q);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) x0_out[k] = q[k];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) x0_out[4 + k] = pred.t[k];
+    // the first call's writeback (:114-116) and the second call's prediction (:62-71): odom1 (last^-1 odom1)
+    const Pose odom1 = params_to_pose(x1);
+    const Pose pred = pose_mul(odom1, pose_mul(pose_inverse(s->last_odom), odom1));
+    s->mid = odom1;
+    pose_to_params(pred, s->x0[1]);
   }
+}
+
+__global__ void odom_dev_init(OdomDev* s) {
+  if (threadIdx.x != 0) return;
+  s->odom = pose_identity();
+  s->last_odom = pose_identity();
+  s->mid = pose_identity();
+  s->kf = pose_identity();
+  s->kf_count = 0;
+  s->kf_flag = 0;
+  pose_to_params(pose_identity(), s->x0[0]);
+  pose_to_params(pose_identity(), s->x0[1]);
+}
+
+__global__ void odom_predict(OdomDev* s) {
+  if (threadIdx.x != 0) return;
+  const Pose pred = pose_mul(s->odom, pose_mul(pose_inverse(s->last_odom), s->odom));
+  s->last_odom = s->odom;   // Q2: the branch is taken for every update type
+  s->odom = pred;
+  pose_to_params(pred, s->x0[0]);
 }
 
 // ===================================================================================== residuals + reduction
@@ -1891,11 +1905,11 @@ __global__ __launch_bounds__(kTB) void lm_reduce(const double* __restrict__ part
 }  // namespace
 
 // ===================================================================================== launchers
-void deskew_bridge_launch(const LMState* d_st, const Pose& odom0, double scan_period, PointRec* edge, const int* d_ne,
-                          int ne_ub, PointRec* surf, const int* d_ns, int ns_ub, double* x0_out, hipStream_t stream) {
+void deskew_bridge_launch(const LMState* d_st, OdomDev* s, double scan_period, PointRec* edge, const int* d_ne,
+                          int ne_ub, PointRec* surf, const int* d_ns, int ns_ub, hipStream_t stream) {
   const unsigned nb = std::max(1u, std::min(div_up(std::max(ne_ub + ns_ub, 1), kTB), 1024u));
-  hipLaunchKernelGGL(deskew_bridge, dim3(nb), dim3(kTB), 0, stream, d_st, odom0, scan_period, edge, d_ne, ne_ub, surf,
-                     d_ns, ns_ub, x0_out);
+  hipLaunchKernelGGL(deskew_bridge, dim3(nb), dim3(kTB), 0, stream, d_st, s, scan_period, edge, d_ne, ne_ub, surf,
+                     d_ns, ns_ub);
   FLOAM_LAUNCH_CHECK();
 }
 
@@ -1913,7 +1927,7 @@ void lm_init_launch(LMState* d_st, const double* x0, hipStream_t st) {
 __global__ void gather_status(const LMState* __restrict__ lm, const int* __restrict__ dcnt,
                               const int* __restrict__ mapE_count, const int* __restrict__ mapS_count,
                               const int* __restrict__ fe_status, const unsigned long long* __restrict__ prof,
-                              UpdateStatus* __restrict__ out) {
+                              UpdateStatus* __restrict__ out, OdomDev* __restrict__ s, int mode) {
   constexpr int kWords = (int)(sizeof(LMState) / sizeof(unsigned));
   const unsigned* src = reinterpret_cast<const unsigned*>(lm);
   unsigned* dst = reinterpret_cast<unsigned*>(&out->lm);
@@ -1926,13 +1940,51 @@ __global__ void gather_status(const LMState* __restrict__ lm, const int* __restr
     out->fe_status = fe_status ? *fe_status : 0;
     out->prof[0] = prof ? prof[0] : 0ull;
     out->prof[1] = prof ? prof[1] : 0ull;
+    out->kf_flag = 0;
+    if (mode & GATHER_FINISH) {
+      if (mode & GATHER_AFTER_MID) s->last_odom = s->mid;
+      s->odom = params_to_pose(lm->x);   // x == the prediction when the solve did not run (gate, no residuals)
+    }
+    if (mode & GATHER_KEYFRAME) {   // KeyFrameUpdate (odomEstimationClass.cpp:320-343)
+      bool key = true;
+      if (!(mode & GATHER_KEYFRAME_FIRST) && s->kf_count > 0) {
+        const Pose delta = pose_mul(pose_inverse(s->kf), s->odom);
+        const double dm = sqrt(delta.t[0] * delta.t[0] + delta.t[1] * delta.t[1] + delta.t[2] * delta.t[2]);
+        const double dr = rotation_angle(delta.R);
+        key = dm > 0.07 || dr > 2 * M_PI / 180.0;
+      }
+      if (key) {
+        s->kf = s->odom;
+        s->kf_count = min(s->kf_count + 1, 3);
+      }
+      s->kf_flag = key ? 1 : 0;
+      out->kf_flag = s->kf_flag;
+    }
+    out->odom = s->odom;
+    out->last_odom = s->last_odom;
   }
 }
 
 void gather_status_launch(const LMState* lm, const int* dcnt, const int* mapE_count, const int* mapS_count,
-                          const int* fe_status, const unsigned long long* prof, UpdateStatus* out, hipStream_t st) {
+                          const int* fe_status, const unsigned long long* prof, UpdateStatus* out, OdomDev* s,
+                          int mode, hipStream_t st) {
   hipLaunchKernelGGL(gather_status, dim3(1), dim3(256), 0, st, lm, dcnt, mapE_count, mapS_count, fe_status, prof,
-                     out);
+                     out, s, mode);
+  FLOAM_LAUNCH_CHECK();
+}
+
+void odom_dev_init_launch(OdomDev* s, hipStream_t st) {
+  hipLaunchKernelGGL(odom_dev_init, dim3(1), dim3(64), 0, st, s);
+  FLOAM_LAUNCH_CHECK();
+}
+
+void odom_predict_launch(OdomDev* s, hipStream_t st) {
+  hipLaunchKernelGGL(odom_predict, dim3(1), dim3(64), 0, st, s);
+  FLOAM_LAUNCH_CHECK();
+}
+
+void lm_init_dev_launch(LMState* d_st, const double* x0_dev, hipStream_t st) {
+  hipLaunchKernelGGL(lm_init_dev, dim3(1), dim3(64), 0, st, d_st, X7{}, x0_dev);
   FLOAM_LAUNCH_CHECK();
 }
 

@@ -100,23 +100,47 @@ struct X7 {
 };
 // reset the per-solve LM state; x0 (7 doubles, by value) replaces x when non-null, else x is kept
 void lm_init_launch(LMState* d_st, const double* x0, hipStream_t st);
+void lm_init_dev_launch(LMState* d_st, const double* x0_dev, hipStream_t st);   // x = x0_dev (device pointer)
+
+// Device-resident controller state (OdomEstimationClass members odom, last_odom, the keyframe list): the pose
+// algebra between the solves runs on the device, so a whole selector is issued without a host round trip; the host
+// mirrors the poses from the status slots when it collects a scan.
+struct OdomDev {
+  Pose odom, last_odom;
+  Pose mid;                // deskewed selector: the first call's result (last_odom of the second call)
+  Pose kf;                 // keyframes.back()
+  int kf_count;            // keyframes.size() (0..3)
+  int kf_flag;             // the last KeyFrameUpdate result: gates the map update
+  double x0[2][7];         // parameters {q, t} of the predictions of the first / second call
+};
+void odom_dev_init_launch(OdomDev* s, hipStream_t st);   // identity poses, no keyframes
+
+// odomEstimationClass.cpp:59-71 (branch always taken, Q2): pred = odom (last^-1 odom); last = odom; odom = pred;
+// x0[0] = the parameters {q, t} of pred (the first call's starting point)
+void odom_predict_launch(OdomDev* s, hipStream_t st);
 
 struct UpdateStatus {
   LMState lm;
   int counts[4];                  // downsampled edge, surf; corner map, surf map
   int fe_status;                  // status flags of the feature extraction that produced the inputs (async FE)
-  int pad;
+  int kf_flag;                    // KeyFrameUpdate result of this call (when it ran)
   unsigned long long prof[2];     // algorithmic bytes of the kNN launches (profiling)
+  Pose odom, last_odom;           // controller poses after this call
 };
+// status gather; with finish: the call's writeback odom = Isometry(q(x), t(x)) (:114-116; x is the prediction when
+// the gate (:77) kept the solve from running), after a deskewed first call last_odom = the first call's result, and
+// with keyframe (1: normal, 2: the process-wide first call, Q6) KeyFrameUpdate (:320-343) into kf_flag
+enum { GATHER_FINISH = 1, GATHER_AFTER_MID = 2, GATHER_KEYFRAME = 4, GATHER_KEYFRAME_FIRST = 8 };
 void gather_status_launch(const LMState* lm, const int* dcnt, const int* mapE_count, const int* mapS_count,
-                          const int* fe_status, const unsigned long long* prof, UpdateStatus* out, hipStream_t st);
+                          const int* fe_status, const unsigned long long* prof, UpdateStatus* out, OdomDev* s,
+                          int mode, hipStream_t st);
 
 // Between the two updatePointsToMap calls of a deskewed UpdatePointsToMapSelector (odomEstimationClass.cpp:40-46),
-// without a host round trip: GetVelocity from the first call's result (x1 = st->x) and the pose before it (odom0),
-// CompensateVelocity of both clouds in place (dataHandler.cpp:82-92, Q5), and the second call's prediction
-// odom1 * (odom0^-1 * odom1) as parameters {q, t} into x0_out (same algebra as the host, pose.hpp).
-void deskew_bridge_launch(const LMState* st, const Pose& odom0, double scan_period, PointRec* edge, const int* d_ne,
-                          int ne_ub, PointRec* surf, const int* d_ns, int ns_ub, double* x0_out, hipStream_t stream);
+// without a host round trip: GetVelocity from the first call's result (x1 = st->x) and s->last_odom (the pose before
+// it), CompensateVelocity of both clouds in place (dataHandler.cpp:82-92, Q5); s->mid = odom1 and the second call's
+// prediction odom1 * (last_odom^-1 * odom1) into s->x0[1] (same algebra as the host, pose.hpp).
+void deskew_bridge_launch(const LMState* st, OdomDev* s, double scan_period, PointRec* edge, const int* d_ne,
+                          int ne_ub, PointRec* surf, const int* d_ns, int ns_ub, hipStream_t stream);
 // Correspondence search for the edge and the surf query sets at the pose in st->x, in two launches:
 // knn_launch — exact 5-NN (blocks [0, nbE) edge queries against the corner map, the rest surf against the surf map);
 // geom_launch — fp64 line / plane fits and the residual records.

@@ -93,12 +93,29 @@ __host__ __device__ inline void mat_to_quat(const Mat3& a, double q[4]) {
   }
 }
 // Eigen::AngleAxisd(R).angle()
-inline double rotation_angle(const Mat3& R) {
+__host__ __device__ inline double rotation_angle(const Mat3& R) {
   double q[4];
   mat_to_quat(R, q);
   const double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2]);
   if (n == 0) return 0.0;
-  return 2.0 * std::atan2(n, std::fabs(q[3]));
+  return 2.0 * atan2(n, fabs(q[3]));
+}
+
+// Eigen Quaterniond(odom.rotation()), odom.translation() -> parameters {qx, qy, qz, qw, tx, ty, tz}
+__host__ __device__ inline void pose_to_params(const Pose& p, double x[7]) {
+  mat_to_quat(p.R, x);
+  x[4] = p.t[0];
+  x[5] = p.t[1];
+  x[6] = p.t[2];
+}
+// Isometry3d(q.toRotationMatrix(), t) from parameters
+__host__ __device__ inline Pose params_to_pose(const double x[7]) {
+  Pose p;
+  p.R = quat_to_mat(x);
+  p.t[0] = x[4];
+  p.t[1] = x[5];
+  p.t[2] = x[6];
+  return p;
 }
 
 }  // namespace floam

@@ -41,7 +41,9 @@ __device__ __forceinline__ unsigned long long match_digit(unsigned d, bool valid
 __global__ __launch_bounds__(kTB) void radix_pass(const uint32_t* __restrict__ kin, const int* __restrict__ vin,
                                                   uint32_t* __restrict__ kout, int* __restrict__ vout, int n,
                                                   int pass, unsigned* __restrict__ ctl,
-                                                  unsigned long long* __restrict__ status, unsigned epoch) {
+                                                  unsigned long long* __restrict__ status, unsigned epoch,
+                                                  const int* __restrict__ gate) {
+  if (gate && !*gate) return;
   __shared__ unsigned s_wcnt[kTB / 64][kRadixDigits];
   __shared__ unsigned s_off[kRadixDigits];
   __shared__ unsigned s_wsum[kTB / 64];
@@ -149,7 +151,8 @@ void RadixScratch::reserve(int n) {
   }
 }
 
-void radix_sort_launch(RadixScratch& sc, uint32_t* k0, int* v0, uint32_t* k1, int* v1, int n, hipStream_t st) {
+void radix_sort_launch(RadixScratch& sc, uint32_t* k0, int* v0, uint32_t* k1, int* v1, int n, hipStream_t st,
+                       const int* gate) {
   if (n <= 0) return;
   sc.reserve(n);
   sc.epoch = (sc.epoch + 1) & 0x3FFFFFFFu;
@@ -159,7 +162,7 @@ void radix_sort_launch(RadixScratch& sc, uint32_t* k0, int* v0, uint32_t* k1, in
     const bool even = (p & 1) == 0;
     hipLaunchKernelGGL(radix_pass, dim3(tiles), dim3(kTB), 0, st, even ? k0 : k1, even ? v0 : v1, even ? k1 : k0,
                        even ? v1 : v0, n, p, sc.ctl.p, sc.status.p + (size_t)p * sc.tiles_cap * kRadixDigits,
-                       sc.epoch);
+                       sc.epoch, gate);
     FLOAM_LAUNCH_CHECK();
   }
 }

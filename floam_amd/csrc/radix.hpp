@@ -46,6 +46,8 @@ __device__ __forceinline__ void radix_ctl_zero(unsigned* ctl, int t, int stride)
 // The four passes: (k0, v0) -> (k1, v1) -> (k0, v0) -> (k1, v1) -> (k0, v0); the sorted pairs end in k0 / v0.
 // n must be the element count the histograms were built over.  ctl[1028] != 0 afterwards if a lookback timed out
 // (never expected; the consumer reports it).
-void radix_sort_launch(RadixScratch& sc, uint32_t* k0, int* v0, uint32_t* k1, int* v1, int n, hipStream_t st);
+// gate (device int, nullable): the passes do nothing when it reads 0.
+void radix_sort_launch(RadixScratch& sc, uint32_t* k0, int* v0, uint32_t* k1, int* v1, int n, hipStream_t st,
+                       const int* gate = nullptr);
 
 }  // namespace floam

@@ -72,7 +72,8 @@ __device__ __forceinline__ bool vox_fetch(const VoxelJobDev& J, int n0, int n1, 
 }
 
 __global__ __launch_bounds__(kTB) void vox_minmax(VoxelJobDev A, VoxelJobDev B, float* __restrict__ partials,
-                                                  unsigned* __restrict__ radix_ctl) {
+                                                  unsigned* __restrict__ radix_ctl, const int* __restrict__ gate) {
+  if (gate && !*gate) return;
   const VoxelJobDev& J = blockIdx.y == 0 ? A : B;
   if (blockIdx.x == 0 && blockIdx.y == 0) radix_ctl_zero(radix_ctl, threadIdx.x, blockDim.x);   // for vox_keys
   const int n0 = *J.d_n0, n1 = J.d_n1 ? *J.d_n1 : 0;
@@ -131,7 +132,8 @@ __global__ __launch_bounds__(kTB) void vox_keys(VoxelJobDev A, VoxelJobDev B, co
                                                 uint32_t* __restrict__ keys, int* __restrict__ vals,
                                                 int* __restrict__ overflow, unsigned long long* __restrict__ status,
                                                 int ntiles, unsigned* __restrict__ ticket,
-                                                unsigned* __restrict__ radix_ctl) {
+                                                unsigned* __restrict__ radix_ctl, const int* __restrict__ gate) {
+  if (gate && !*gate) return;
   const int job = blockIdx.y;
   const VoxelJobDev& J = job == 0 ? A : B;
   __shared__ float s_mm[6];
@@ -182,7 +184,17 @@ __global__ __launch_bounds__(kTB) void vox_keys(VoxelJobDev A, VoxelJobDev B, co
 __global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B, const uint32_t* __restrict__ keys,
                                                    const int* __restrict__ vals, const int* __restrict__ overflow,
                                                    int total, unsigned long long* __restrict__ status,
-                                                   unsigned* __restrict__ ticket, const unsigned* __restrict__ radix_ctl) {
+                                                   unsigned* __restrict__ ticket, const unsigned* __restrict__ radix_ctl,
+                                                   const int* __restrict__ gate) {
+  if (gate && !*gate) {   // gated off (no keyframe): the output is the unchanged first part (the map)
+    for (int job = 0; job < 2; ++job) {
+      const VoxelJobDev& J = job == 0 ? A : B;
+      const int n0 = *J.d_n0;
+      for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n0; i += gridDim.x * blockDim.x) J.out[i] = J.part0[i];
+      if (blockIdx.x == 0 && threadIdx.x == 0) *J.d_out = n0;
+    }
+    return;
+  }
   const int tile = lookback_ticket(ticket);
   const int ntiles = (int)gridDim.x;
   const int t0 = tile * kTile;
@@ -382,7 +394,7 @@ VoxelJobDev to_dev(const VoxelJob& j, int base) {
 }
 }  // namespace
 
-void voxel2_launch(VoxelScratch2& sc, const VoxelJob& a, const VoxelJob& b, hipStream_t st) {
+void voxel2_launch(VoxelScratch2& sc, const VoxelJob& a, const VoxelJob& b, hipStream_t st, const int* gate) {
   const VoxelJobDev A = to_dev(a, 0);
   const VoxelJobDev B = to_dev(b, a.n0_ub + (a.part1 ? a.n1_ub : 0));
   const int total = B.base + b.n0_ub + (b.part1 ? b.n1_ub : 0);
@@ -400,16 +412,16 @@ void voxel2_launch(VoxelScratch2& sc, const VoxelJob& a, const VoxelJob& b, hipS
   sc.ticket.reserve(1);
   const int umax = std::max(A.n0_ub + A.n1_ub, b.n0_ub + (b.part1 ? b.n1_ub : 0));
   sc.rs.reserve(n);
-  hipLaunchKernelGGL(vox_minmax, dim3(kMinMaxBlocks, 2), dim3(kTB), 0, st, A, B, sc.partials.p, sc.rs.ctl.p);
+  hipLaunchKernelGGL(vox_minmax, dim3(kMinMaxBlocks, 2), dim3(kTB), 0, st, A, B, sc.partials.p, sc.rs.ctl.p, gate);
   FLOAM_LAUNCH_CHECK();
   // few blocks: each folds its LDS digit histograms into the global ones with one atomic per non-zero bin
   const unsigned kb = std::max(1u, std::min(div_up(std::max(umax, 1), kTB), 64u));
   hipLaunchKernelGGL(vox_keys, dim3(kb, 2), dim3(kTB), 0, st, A, B, sc.partials.p, sc.s.k0.p, sc.s.v0.p,
-                     sc.overflow.p, sc.status.p, ntiles, sc.ticket.p, sc.rs.ctl.p);
+                     sc.overflow.p, sc.status.p, ntiles, sc.ticket.p, sc.rs.ctl.p, gate);
   FLOAM_LAUNCH_CHECK();
-  radix_sort_launch(sc.rs, sc.s.k0.p, sc.s.v0.p, sc.s.k1.p, sc.s.v1.p, n, st);   // sorted pairs in k0 / v0
+  radix_sort_launch(sc.rs, sc.s.k0.p, sc.s.v0.p, sc.s.k1.p, sc.s.v1.p, n, st, gate);   // sorted pairs in k0 / v0
   hipLaunchKernelGGL(vox_compact, dim3(ntiles), dim3(kTB), 0, st, A, B, sc.s.k0.p, sc.s.v0.p, sc.overflow.p, n,
-                     sc.status.p, sc.ticket.p, sc.rs.ctl.p);
+                     sc.status.p, sc.ticket.p, sc.rs.ctl.p, gate);
   FLOAM_LAUNCH_CHECK();
 }
 

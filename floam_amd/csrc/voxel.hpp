@@ -32,8 +32,10 @@ struct VoxelScratch2 {
   RadixScratch rs;
 };
 
-// Two independent voxel grids in one pipeline (3 kernels + the 4 radix passes).  *d_out of each job receives the voxel count
-// (-1 if the single-pass compaction failed, never expected).
-void voxel2_launch(VoxelScratch2& sc, const VoxelJob& a, const VoxelJob& b, hipStream_t st);
+// Two independent voxel grids in one pipeline (3 kernels + the 4 radix passes).  *d_out of each job receives the
+// voxel count (-1 if the single-pass compaction failed, never expected).  gate (device int, nullable): when it reads
+// 0 the pipeline does nothing but copy each job's part0 to its output (a map update skipped on the device).
+void voxel2_launch(VoxelScratch2& sc, const VoxelJob& a, const VoxelJob& b, hipStream_t st,
+                   const int* gate = nullptr);
 
 }  // namespace floam

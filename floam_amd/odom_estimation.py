@@ -73,6 +73,22 @@ class OdomEstimationClass:
                                                                  int(update_type)))
         return self.last_status
 
+    def set_async(self, depth: int) -> int:
+        """Streaming mode (floam_odom_set_async): with depth > 0 the update calls only issue device work, up to
+        `depth` updates stay in flight, and wait() collects their poses and warnings."""
+        return _ffi.check(self._L.floam_odom_set_async(self._need(), int(depth)))
+
+    def wait(self, max_pending: int = 0) -> list:
+        """Collect in-flight updates until at most max_pending remain; returns the (q_xyzw, t) pose of every update
+        collected since the previous wait(), in issue order."""
+        cap = 64
+        buf = np.zeros((cap, 7))
+        n = C.c_size_t()
+        self.last_status = _ffi.check(self._L.floam_odom_wait(self._need(), int(max_pending),
+                                                              buf.ctypes.data_as(C.POINTER(C.c_double)), cap,
+                                                              C.byref(n)))
+        return [(buf[i, :4].copy(), buf[i, 4:].copy()) for i in range(min(n.value, cap))]
+
     def getMap(self, laserCloudMap: DeviceCloud) -> None:
         """src/odomEstimationClass.cpp:296-300 (appends surf map, then corner map)."""
         _ffi.check(self._L.floam_odom_get_map(self._need(), laserCloudMap.handle))

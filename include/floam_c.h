@@ -112,6 +112,16 @@ floam_status floam_odom_init_map(floam_odom* o, const floam_cloud* edge, const f
 floam_status floam_odom_update_selector(floam_odom* o, floam_cloud* edge, floam_cloud* surf, int deskew);
 /* updatePointsToMap(edge_in, surf_in, update_type) (src/odomEstimationClass.cpp:52-124) */
 floam_status floam_odom_update(floam_odom* o, const floam_cloud* edge, const floam_cloud* surf, int update_type);
+/* Streaming mode (no reference counterpart: the reference's odometry node processes one scan per callback,
+ * src/odomEstimationNode.cpp:222-244).  depth > 0: update / update_selector only issue the device work (the whole
+ * controller runs on the device) and keep up to `depth` updates in flight; their warnings, errors and poses are
+ * collected by floam_odom_wait, and get_pose / get_last_pose / get_stats report the last collected update.
+ * depth 0 (default): every update synchronises and returns its own warning, as the reference's calls do. */
+floam_status floam_odom_set_async(floam_odom* o, int depth);
+/* Collect in-flight updates until at most max_pending remain.  Writes the pose {qx,qy,qz,qw,tx,ty,tz} of every
+ * update collected since the previous call (in issue order) to poses[0..min(n, capacity)) and n to *n_out.
+ * Returns the first device error, else the last warning among them. */
+floam_status floam_odom_wait(floam_odom* o, size_t max_pending, double* poses, size_t capacity, size_t* n_out);
 /* public member `odom` (include/odomEstimationClass.h:84): quaternion (x,y,z,w) + translation */
 floam_status floam_odom_get_pose(const floam_odom* o, double q_xyzw[4], double t[3]);
 floam_status floam_odom_get_last_pose(const floam_odom* o, double q_xyzw[4], double t[3]);

@@ -184,6 +184,42 @@ def test_odometry_pipelined_feature_extraction(floam_gpu, oracle_lib):
             np.testing.assert_array_equal(a[4][1], t)
 
 
+@pytest.mark.parametrize("depth", [1, 3])
+def test_odometry_streaming(floam_gpu, oracle_lib, depth):
+    """floam_odom_set_async: the selector only issues device work (controller, keyframe decision and map update
+    on the device); wait() collects the poses in order.  Bit-identical to the synchronous run."""
+    from floam_amd.odom_estimation import reset_process_state
+    sync, odo_sync, _ = _run_sequence(floam_gpu, oracle_lib, "c1", 9)
+    R = synth.lidar_model("c1").rings
+    reset_process_state()
+    lp = floam_gpu.LaserProcessingClass(asynchronous=True)
+    lp.init(_params(R))
+    odo = floam_gpu.OdomEstimationClass()
+    odo.init(_params(R), 0.1, "Cauchy")
+    clouds = []
+    for k in range(9):
+        e, s = floam_gpu.DeviceCloud(), floam_gpu.DeviceCloud()
+        lp.featureExtraction(floam_gpu.DeviceCloud(synth.generate_scan("c1", k)), e, s)
+        clouds.append((e, s))
+    odo.initMapWithPoints(*clouds[0])
+    odo.set_async(depth)
+    poses = [odo.pose()]
+    for k in range(1, 9):
+        odo.UpdatePointsToMapSelector(*clouds[k], True)
+        poses.extend(odo.wait(depth - 1))
+    poses.extend(odo.wait(0))
+    assert len(poses) == 9
+    for a, (q, t) in zip(sync, poses):
+        np.testing.assert_array_equal(a[4][0], q)
+        np.testing.assert_array_equal(a[4][1], t)
+    # the maps after the stream are the synchronous run's, bit for bit
+    assert odo.map_sizes() == odo_sync.map_sizes()
+    for a, b in ((odo.laserCloudCornerMap, odo_sync.laserCloudCornerMap),
+                 (odo.laserCloudSurfMap, odo_sync.laserCloudSurfMap)):
+        for f in ("x", "y", "z", "intensity"):
+            np.testing.assert_array_equal(a[f], b[f])
+
+
 def test_async_feature_extraction_error_surfaces(floam_gpu):
     """An out-of-range ring (UB in the reference) is reported by the consumer in asynchronous mode."""
     from floam_amd import FloamError
