@@ -200,10 +200,6 @@ def main():
 
     poses = []
     run(lp, odo, 0, args.warmup, poses)
-    if not args.no_roofline:
-        _ffi.check(L.floam_profile_reset(dev))
-        # FLOAM_PROF_KNN: HIP events around the correspondence pass only (+ FLOAM_PROF_KNN_DETAIL: per launch)
-        _ffi.check(L.floam_profile_enable(dev, 1 | (32 if args.knn_detail else 0)))
     barrier_sync()
     t_start = time.perf_counter()
     run(lp, odo, args.warmup, n_scans, poses)
@@ -229,19 +225,23 @@ def main():
 
     roof = None
     if not args.no_roofline:
-        timed = read_timings()
         odo.close()
         lp.close()
-        # Algorithmic bytes of the timed launches: an identical, untimed replay of the same sequence (the pipeline
-        # is deterministic) with the byte-counting kernel after each correspondence launch (FLOAM_PROF_KNN_BYTES).
+        # The dominant kernel's launch durations and algorithmic bytes: an identical replay of the same sequence
+        # (the pipeline is deterministic; the poses are checked bit for bit) with HIP events around each
+        # correspondence launch (FLOAM_PROF_KNN, + FLOAM_PROF_KNN_DETAIL: per kernel) and the byte-counting kernel
+        # after it (FLOAM_PROF_KNN_BYTES).  Profiling issues the updates launch by launch: the timed run above
+        # replays each update as one hipGraph, and timing events recorded inside a graph cannot be read back on
+        # this ROCm (hipEventElapsedTime fails for them).
         lp, odo = make_pipeline()
         replay = []
         run(lp, odo, 0, args.warmup, replay)
         _ffi.check(L.floam_profile_reset(dev))
-        _ffi.check(L.floam_profile_enable(dev, 16))
+        _ffi.check(L.floam_profile_enable(dev, 1 | 16 | (32 if args.knn_detail else 0)))
         run(lp, odo, args.warmup, n_scans, replay)
         _ffi.check(L.floam_profile_enable(dev, 0))
         counted = read_timings()
+        timed = counted
         same = all(np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) for a, b in zip(poses, replay))
         kt, kb = timed.get("knn"), counted.get("knn")
         if kt is not None and kt[0] > 0 and kb is not None:

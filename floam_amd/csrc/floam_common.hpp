@@ -8,6 +8,7 @@
 #include <cstdint>
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 #include "../../include/floam_c.h"
 
@@ -46,6 +47,22 @@ struct Error : std::runtime_error {
 inline unsigned div_up(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
 
 // ------------------------------------------------------------------------------------- device buffers
+// Stream capture of an update into a hipGraph (host.cpp): while a capture is active, device memory replaced by a
+// growing buffer is not freed (hipFree would synchronise) but kept until the captured work has run.
+struct CaptureState {
+  bool active = false;
+  std::vector<void*> graveyard;
+};
+inline CaptureState& capture_state() {
+  static thread_local CaptureState s;
+  return s;
+}
+inline void dev_free(void* p) {
+  if (!p) return;
+  if (capture_state().active) capture_state().graveyard.push_back(p);
+  else (void)hipFree(p);
+}
+
 template <typename T>
 struct DevBuf {
   T* p = nullptr;
@@ -55,7 +72,7 @@ struct DevBuf {
   DevBuf& operator=(const DevBuf&) = delete;
   ~DevBuf() { release(); }
   void release() {
-    if (p) (void)hipFree(p);
+    dev_free(p);
     p = nullptr;
     cap = 0;
   }

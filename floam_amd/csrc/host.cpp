@@ -174,9 +174,9 @@ static void cloud_reserve(floam_cloud* c, size_t n, size_t keep, hipStream_t st)
   FLOAM_HIP(hipMalloc(&p, cap * sizeof(PointRec)));
   if (keep && c->pts.p) {
     FLOAM_HIP(hipMemcpyAsync(p, c->pts.p, keep * sizeof(PointRec), hipMemcpyDeviceToDevice, st));
-    FLOAM_HIP(hipStreamSynchronize(st));
+    if (!capture_state().active) FLOAM_HIP(hipStreamSynchronize(st));
   }
-  if (c->pts.p) FLOAM_HIP(hipFree(c->pts.p));
+  dev_free(c->pts.p);   // deferred while capturing (the copy above runs first)
   c->pts.p = p;
   c->pts.cap = cap;
 }
@@ -236,10 +236,9 @@ struct floam_odom {
   CorrSet ce, cs;
   DevBuf<double> partials, sums;
   DevBuf<unsigned> step_counter;
-  DevBuf<unsigned long long> lm_go;     // lm_solve hand-off word
-  DevBuf<double> lm_point;              // lm_solve: the evaluation point released to the evaluation blocks
-  unsigned long long lm_epoch = 0;
-  int lm_mode = 0;   // FLOAM_LM_MODE: 0 lm_step_gram (squared loss), 1 resident lm_solve, 2 per-record lm_step
+  // FLOAM_LM_MODE (squared loss): 0 resident lm_solve_gram (one launch per solve), 1 lm_step_gram (one launch per
+  // evaluation), 2 per-record lm_step (also the Huber path)
+  int lm_mode = 0;
   DevBuf<double> gpart;                 // per-block surf Gram partials
   DevBuf<double> gmat;                  // the solve's surf Gram matrix + its origin
   DevBuf<unsigned long long> dbg_stamps;   // FLOAM_DEBUG_STAMPS=1: lm_step segment times (diagnostic)
@@ -255,12 +254,20 @@ struct floam_odom {
     int map_slot;                 // slot whose map counts precede this update's map update (-1: no map update)
     size_t addE, addS;            // upper bounds of the points the map update may add
     hipEvent_t ev;
+    std::vector<void*> graveyard; // device buffers replaced while the update was captured (freed once it ran)
   };
   std::deque<Pending> inflight;
   int depth = 0;                  // floam_odom_set_async: 0 = every update synchronises (the reference's contract)
   unsigned long long issued = 0;
   size_t pendE = 0, pendS = 0;    // sum of addE / addS over the in-flight updates
   std::vector<double> collected;  // poses {q, t} of the updates collected since the last floam_odom_wait
+  // each update is captured into a hipGraph and the executable graph of its kind updated in place
+  // (hipGraphExecUpdate): one launch per update, and back-to-back kernel dispatch on the device
+  bool use_graph = false;         // FLOAM_GRAPH=1 enables
+  // [kind][k]: kind 0 updatePointsToMap, 1 deskewed selector; update i uses k = i % (depth + 1), so an executable
+  // graph is never updated while a launch of it may still be in flight
+  static constexpr int kExecRing = 17;
+  hipGraphExec_t graph_exec[2][kExecRing] = {};
   DevBuf<unsigned long long> prof_bytes;
   DevBuf<unsigned long long> traffic_set;
   bool prof_bytes_init = false;
@@ -353,9 +360,6 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
   if (!o->step_counter.p) {
     o->step_counter.reserve(1);
     FLOAM_HIP(hipMemsetAsync(o->step_counter.p, 0, sizeof(unsigned), st));
-    o->lm_go.reserve(1);
-    o->lm_point.reserve(8);
-    FLOAM_HIP(hipMemsetAsync(o->lm_go.p, 0, sizeof(unsigned long long), st));
     const char* pe = std::getenv("FLOAM_LM_MODE");
     o->lm_mode = pe ? std::atoi(pe) : 0;
     if (std::getenv("FLOAM_DEBUG_STAMPS")) {
@@ -374,7 +378,8 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
   const QuerySet qs{o->dS.p, o->cnt.p + 1, ns_ub};
   const bool sharded = o->world > 1;
   // the single-block Gram solve (squared loss, bounded edge count); else one launch per evaluation (or lm_solve)
-  const bool gram = !sharded && o->lm_mode == 0 && lm_gram_supported(o->huber);
+  // squared loss: surf sums from the Gram matrix (resident solve, or one launch per evaluation); else per record
+  const bool gram = !sharded && o->lm_mode != 2 && lm_gram_supported(o->huber);
   if (gram) {
     o->gpart.reserve(lm_gram_partials());
     o->gmat.reserve(lm_gram_words());
@@ -400,10 +405,10 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
                          o->prof_bytes.p + 1, st);
     }
     // iteration zero + at most max_num_iterations = 4 candidates (odomEstimationClass.cpp:102)
-    if (!sharded && o->lm_mode == 1) {
+    if (gram && o->lm_mode == 0) {
       ProfScope ps(ctx, "lm_solve", FLOAM_PROF_LM);
-      lm_solve_launch(o->lm.p, o->ce, o->cnt.p + 0, ne_ub, o->cs, o->cnt.p + 1, ns_ub, o->huber, o->partials.p,
-                      o->lm_point.p, o->step_counter.p, o->lm_go.p, ++o->lm_epoch, st, o->dbg_stamps.p);
+      lm_solve_gram_launch(o->lm.p, o->ce, o->cnt.p + 0, ne_ub, o->gpart.p, o->gmat.p, o->partials.p,
+                           o->step_counter.p, st, o->dbg_stamps.p);
       continue;
     }
     for (int ev = 0; ev < 5; ++ev) {
@@ -461,6 +466,7 @@ floam_status odom_collect_one(floam_odom* o, DeviceCtx& ctx) {
   o->pendS -= P.addS;
   FLOAM_HIP(hipEventSynchronize(P.ev));
   FLOAM_HIP(hipEventDestroy(P.ev));
+  for (void* b : P.graveyard) (void)hipFree(b);
   ctx.drain();
   const UpdateStatus* slots = o->h_ustat.p + 2 * P.ring;
   for (int k = 0; k < P.nslots; ++k) {
@@ -526,14 +532,60 @@ int odom_begin(floam_odom* o, DeviceCtx& ctx) {
   return (int)(o->issued++ % (unsigned long long)ring_n);
 }
 
+// Graph capture of one update (when enabled): odom_capture_begin before its first device operation,
+// odom_capture_end after its last one instantiates or updates the executable graph of its kind and launches it.
+bool odom_capture_begin(floam_odom* o, DeviceCtx& ctx) {
+  if (!o->use_graph || ctx.profile != 0 || o->world > 1) return false;
+  FLOAM_HIP(hipStreamBeginCapture(ctx.stream, hipStreamCaptureModeRelaxed));
+  capture_state().active = true;
+  return true;
+}
+
+void odom_capture_abort(DeviceCtx& ctx) {   // after an exception inside the captured region
+  CaptureState& cs = capture_state();
+  if (!cs.active) return;
+  cs.active = false;
+  hipGraph_t g = nullptr;
+  (void)hipStreamEndCapture(ctx.stream, &g);
+  if (g) (void)hipGraphDestroy(g);
+}
+
+void odom_capture_end(floam_odom* o, DeviceCtx& ctx, int kind) {
+  CaptureState& cs = capture_state();
+  cs.active = false;
+  hipGraph_t g = nullptr;
+  FLOAM_HIP(hipStreamEndCapture(ctx.stream, &g));
+  hipGraphExec_t& ex = o->graph_exec[kind][(o->issued - 1) % (unsigned long long)(o->depth + 1)];
+  bool ok = false;
+  if (ex) {
+    hipGraphNode_t err_node = nullptr;
+    hipGraphExecUpdateResult res;
+    ok = hipGraphExecUpdate(ex, g, &err_node, &res) == hipSuccess && res == hipGraphExecUpdateSuccess;
+    if (!ok) {   // the topology changed (e.g. optimization_count): a fresh executable graph
+      (void)hipGetLastError();
+      FLOAM_HIP(hipGraphExecDestroy(ex));
+      ex = nullptr;
+    }
+  }
+  if (!ok) FLOAM_HIP(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+  FLOAM_HIP(hipGraphDestroy(g));
+  FLOAM_HIP(hipGraphLaunch(ex, ctx.stream));
+}
+
 // the status copy of the update just issued; synchronous mode collects it right away
-floam_status odom_end(floam_odom* o, DeviceCtx& ctx, int ring, int nslots, int map_slot, size_t addE, size_t addS) {
+floam_status odom_end(floam_odom* o, DeviceCtx& ctx, int ring, int nslots, int map_slot, size_t addE, size_t addS,
+                      bool captured, int kind) {
   FLOAM_HIP(hipMemcpyAsync(o->h_ustat.p + 2 * ring, o->ustat.p + 2 * ring, sizeof(UpdateStatus) * nslots,
                            hipMemcpyDeviceToHost, ctx.stream));
+  std::vector<void*> graveyard;
+  if (captured) {
+    graveyard.swap(capture_state().graveyard);
+    odom_capture_end(o, ctx, kind);
+  }
   hipEvent_t ev;
   FLOAM_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   FLOAM_HIP(hipEventRecord(ev, ctx.stream));
-  o->inflight.push_back(floam_odom::Pending{ring, nslots, map_slot, addE, addS, ev});
+  o->inflight.push_back(floam_odom::Pending{ring, nslots, map_slot, addE, addS, ev, std::move(graveyard)});
   o->pendE += addE;
   o->pendS += addS;
   if (o->depth == 0) return odom_collect(o, ctx, 0);
@@ -582,14 +634,20 @@ floam_status odom_update(floam_odom* o, const floam_cloud* edge, const floam_clo
   FLOAM_HIP(hipSetDevice(o->device));
   const int ring = odom_begin(o, ctx);
   const int ne_ub = (int)cloud_ub(edge), ns_ub = (int)cloud_ub(surf);
-  if (o->optimization_count > 2) o->optimization_count--;
-  odom_predict_launch(o->ds.p, ctx.stream);
-  const bool update_map = type == FLOAM_VANILLA || type == FLOAM_REFINEMENT_AND_UPDATE;
-  odom_issue(o, ctx, edge, surf, ne_ub, ns_ub, o->ds.p->x0[0], 2 * ring,
-             GATHER_FINISH | (update_map ? gather_keyframe_mode() : 0));
-  size_t addE = 0, addS = 0;
-  if (update_map) odom_map_update(o, ctx, ne_ub, ns_ub, addE, addS);
-  return odom_end(o, ctx, ring, 1, update_map ? 0 : -1, addE, addS);
+  const bool captured = odom_capture_begin(o, ctx);
+  try {
+    if (o->optimization_count > 2) o->optimization_count--;
+    odom_predict_launch(o->ds.p, ctx.stream);
+    const bool update_map = type == FLOAM_VANILLA || type == FLOAM_REFINEMENT_AND_UPDATE;
+    odom_issue(o, ctx, edge, surf, ne_ub, ns_ub, o->ds.p->x0[0], 2 * ring,
+               GATHER_FINISH | (update_map ? gather_keyframe_mode() : 0));
+    size_t addE = 0, addS = 0;
+    if (update_map) odom_map_update(o, ctx, ne_ub, ns_ub, addE, addS);
+    return odom_end(o, ctx, ring, 1, update_map ? 0 : -1, addE, addS, captured, 0);
+  } catch (...) {
+    odom_capture_abort(ctx);
+    throw;
+  }
 }
 
 // UpdatePointsToMapSelector with deskew (src/odomEstimationClass.cpp:38-47): call 1 (edge, edge) INITIAL_ITERATION
@@ -600,20 +658,26 @@ floam_status odom_update_deskew(floam_odom* o, floam_cloud* edge, floam_cloud* s
   FLOAM_HIP(hipSetDevice(o->device));
   const int ring = odom_begin(o, ctx);
   const int ne_ub = (int)cloud_ub(edge), ns_ub = (int)cloud_ub(surf);
-  if (o->optimization_count > 2) o->optimization_count--;
-  odom_predict_launch(o->ds.p, ctx.stream);
-  odom_issue(o, ctx, edge, edge, ne_ub, ne_ub, o->ds.p->x0[0], 2 * ring, 0);
-  {
-    ProfScope ps(ctx, "deskew", FLOAM_PROF_CLOUD);
-    deskew_bridge_launch(o->lm.p, o->ds.p, o->lp.scan_period, edge->pts.p, edge->count.p, ne_ub, surf->pts.p,
-                         surf->count.p, ns_ub, ctx.stream);
+  const bool captured = odom_capture_begin(o, ctx);
+  try {
+    if (o->optimization_count > 2) o->optimization_count--;
+    odom_predict_launch(o->ds.p, ctx.stream);
+    odom_issue(o, ctx, edge, edge, ne_ub, ne_ub, o->ds.p->x0[0], 2 * ring, 0);
+    {
+      ProfScope ps(ctx, "deskew", FLOAM_PROF_CLOUD);
+      deskew_bridge_launch(o->lm.p, o->ds.p, o->lp.scan_period, edge->pts.p, edge->count.p, ne_ub, surf->pts.p,
+                           surf->count.p, ns_ub, ctx.stream);
+    }
+    if (o->optimization_count > 2) o->optimization_count--;
+    odom_issue(o, ctx, edge, surf, ne_ub, ns_ub, o->ds.p->x0[1], 2 * ring + 1,
+               GATHER_FINISH | GATHER_AFTER_MID | gather_keyframe_mode());
+    size_t addE = 0, addS = 0;
+    odom_map_update(o, ctx, ne_ub, ns_ub, addE, addS);
+    return odom_end(o, ctx, ring, 2, 1, addE, addS, captured, 1);
+  } catch (...) {
+    odom_capture_abort(ctx);
+    throw;
   }
-  if (o->optimization_count > 2) o->optimization_count--;
-  odom_issue(o, ctx, edge, surf, ne_ub, ns_ub, o->ds.p->x0[1], 2 * ring + 1,
-             GATHER_FINISH | GATHER_AFTER_MID | gather_keyframe_mode());
-  size_t addE = 0, addS = 0;
-  odom_map_update(o, ctx, ne_ub, ns_ub, addE, addS);
-  return odom_end(o, ctx, ring, 2, 1, addE, addS);
 }
 
 // CompensateVelocity (src/dataHandler.cpp:82-92) with GetVelocity (include/odomEstimationClass.h:78)
@@ -926,6 +990,8 @@ floam_status floam_odom_create(const floam_lidar_params* p, double map_resolutio
     FLOAM_HIP(hipMemsetAsync(o->lm.p, 0, sizeof(LMState), ctx.stream));
     o->ds.reserve(1);
     odom_dev_init_launch(o->ds.p, ctx.stream);
+    const char* pg = std::getenv("FLOAM_GRAPH");   // measured slower than direct launches at C3: opt-in
+    o->use_graph = pg && std::atoi(pg) != 0;
     FLOAM_HIP(hipStreamSynchronize(ctx.stream));
     *out = o.release();
     return FLOAM_OK;
@@ -937,13 +1003,19 @@ floam_status floam_odom_destroy(floam_odom* o) {
     if (o) {
       DeviceCtx& ctx = ctx_for(o->device);
       FLOAM_HIP(hipStreamSynchronize(ctx.stream));
-      for (auto& P : o->inflight) FLOAM_HIP(hipEventDestroy(P.ev));
+      for (auto& P : o->inflight) {
+        FLOAM_HIP(hipEventDestroy(P.ev));
+        for (void* b : P.graveyard) (void)hipFree(b);
+      }
       o->inflight.clear();
+      for (auto& row : o->graph_exec)
+        for (auto& ex : row)
+          if (ex) FLOAM_HIP(hipGraphExecDestroy(ex));
       if (o->dbg_stamps.p) {
         unsigned long long h[32];
         FLOAM_HIP(hipMemcpy(h, o->dbg_stamps.p, sizeof(h), hipMemcpyDeviceToHost));
         const double n = h[4] ? (double)h[4] : 1.0;
-        std::fprintf(stderr, "[floam stamps] lm_step x%llu (control block): stage %.2f us, wait %.2f us, reduce %.2f us,"
+        std::fprintf(stderr, "[floam stamps] LM evaluations x%llu (control block): stage / surf sums %.2f us, wait %.2f us, reduce %.2f us,"
                    " control step %.2f us\n", h[4], h[0] / n / 100.0, h[1] / n / 100.0, h[2] / n / 100.0,
                    h[3] / n / 100.0);
         if (h[6])

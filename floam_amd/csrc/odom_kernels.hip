@@ -339,6 +339,7 @@ __device__ __forceinline__ void lm_reset(LMState* st, const X7& x0) {
   st->corr_surf = 0;
   st->radius = 1e4;
   st->dfac = 2.0;
+  st->go = 0ull;
 }
 
 // ===================================================================================== correspondence search
@@ -1093,29 +1094,6 @@ __global__ __launch_bounds__(kTB) void lm_eval(const LMState* __restrict__ st, c
                     partials, blockIdx.x, gridDim.x);
 }
 
-// fixed-size variant for the resident solve: the kEvalBlocks partials of a component are loaded sc1, all in flight
-__device__ void reduce_partials_sc1(const double* __restrict__ partials, double* sums /* shared */) {
-  __shared__ double strip[LM_NSUM][8];
-  constexpr int per = (int)kEvalBlocks / 8;
-  if (threadIdx.x < LM_NSUM * 8) {
-    const int c = threadIdx.x >> 3, p = threadIdx.x & 7;
-    double w[per];
-#pragma unroll
-    for (int k = 0; k < per; ++k) w[k] = load_sc1(&partials[c * (int)kEvalBlocks + p * per + k]);
-    double v = 0.0;
-#pragma unroll
-    for (int k = 0; k < per; ++k) v += w[k];
-    strip[c][p] = v;
-  }
-  __syncthreads();
-  if (threadIdx.x < LM_NSUM) {
-    double v = 0.0;
-    for (int p = 0; p < 8; ++p) v += strip[threadIdx.x][p];
-    sums[threadIdx.x] = v;
-  }
-  __syncthreads();
-}
-
 template <bool SC1 = false>
 __device__ void reduce_partials_block(const double* __restrict__ partials, int nblk, double* sums /* shared */) {
   // component c = t / 8 sums its 8 block strips in order, then thread c sums the 8 strip totals (fixed order)
@@ -1414,7 +1392,7 @@ __device__ __forceinline__ void lm_logic_wave0(LMState& sst, const double* sums_
 
 __device__ __forceinline__ void lm_logic_lds(LMState* __restrict__ st, const double* sums) {
   __shared__ LMState sst;
-  constexpr int kWords = (int)(sizeof(LMState) / sizeof(unsigned));
+  constexpr int kWords = kStateWords;
   static_assert(sizeof(LMState) % sizeof(unsigned) == 0, "LMState must be a whole number of dwords");
   const unsigned* gsrc = reinterpret_cast<const unsigned*>(st);
   unsigned* ldst = reinterpret_cast<unsigned*>(&sst);
@@ -1463,7 +1441,7 @@ __global__ __launch_bounds__(kTB) void lm_step(LMState* __restrict__ st, const d
   __shared__ LMState sst;
   __shared__ double sums[LM_NSUM];
   __shared__ int s_timeout;
-  constexpr int kWords = (int)(sizeof(LMState) / sizeof(unsigned));
+  constexpr int kWords = kStateWords;
   static_assert(sizeof(LMState) % sizeof(unsigned) == 0, "LMState must be a whole number of dwords");
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   {
@@ -1514,134 +1492,6 @@ __global__ __launch_bounds__(kTB) void lm_step(LMState* __restrict__ st, const d
     atomicAdd(&dbg[2], t3 - t2);
     atomicAdd(&dbg[3], t4 - t3);
     atomicAdd(&dbg[4], 1ull);
-  }
-}
-
-// A whole Ceres solve in one launch (single-GPU path): iteration zero + at most 4 candidates, i.e. up to 5
-// evaluations, each followed by the control step.  Block 0 is the control block, blocks 1..nblk evaluate.  The
-// blocks stay resident across the evaluations and hand off without cache invalidations (sc1 words):
-//   evaluation -> control: the block's 29 partial sums stored sc1, drained, then one atomicAdd on `cnt`;
-//   control -> evaluation: the next evaluation point (7 doubles) stored sc1 into `point`, drained, then the word
-//        go = (epoch << 8) | (done << 7) | evaluations released; epoch is a per-launch host counter, so go never
-//        has to be reset.  The records stay hot in the evaluating blocks' L2 across the evaluations.
-// All 1 + nblk blocks must be co-resident (nblk = 128 <= one block per CU on 256 CUs); every wait is bounded
-// (~1 s) and a timeout ends the solve with st->n_res = -1, which the host reports as an error.
-__device__ __forceinline__ bool wait_u32_geq(unsigned* p, unsigned target) {
-  for (long long it = 0; it < (1ll << 24); ++it) {
-    if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
-    __builtin_amdgcn_s_sleep(1);
-  }
-  return false;
-}
-
-__global__ __launch_bounds__(kTB) void lm_solve(LMState* __restrict__ st, const double* __restrict__ erec,
-                                                const uint8_t* __restrict__ evalid, int ecap,
-                                                const int* __restrict__ d_ne, int ne_ub,
-                                                const double* __restrict__ srec, const uint8_t* __restrict__ svalid,
-                                                int scap, const int* __restrict__ d_ns, int ns_ub, int huber,
-                                                double* __restrict__ partials, double* __restrict__ point,
-                                                unsigned* __restrict__ cnt, unsigned long long* __restrict__ go,
-                                                unsigned long long epoch, unsigned long long* __restrict__ dbg) {
-  const int nblk = (int)gridDim.x - 1;
-  __shared__ int s_flag;
-  if (blockIdx.x > 0) {
-    const int ne = min(*d_ne, ne_ub), ns = min(*d_ns, ns_ub);
-    __shared__ double s_x[7];
-    for (int it = 0; it < 5; ++it) {
-      if (it == 0) {   // iteration zero evaluates at x (set by the kNN launch; kernel boundary)
-        if (threadIdx.x < 7) s_x[threadIdx.x] = st->x[threadIdx.x];
-      } else {         // wait for the control step of evaluation it - 1, then read the point it released
-        if (threadIdx.x == 0) {
-          int f = 2;   // 0: go, 1: done, 2: timeout
-          for (long long k = 0; k < (1ll << 24); ++k) {
-            const unsigned long long g = __hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if ((g >> 8) == epoch && (int)(g & 0x7F) >= it) {
-              f = (g & 0x80) ? 1 : 0;
-              break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-          }
-          s_flag = f;
-        }
-        __syncthreads();
-        if (s_flag) return;
-        if (threadIdx.x < 7) s_x[threadIdx.x] = load_sc1(&point[threadIdx.x]);
-      }
-      __syncthreads();
-      double x[7];
-#pragma unroll
-      for (int k = 0; k < 7; ++k) x[k] = s_x[k];
-      eval_block_at<true>(x, erec, evalid, ecap, ne, srec, svalid, scap, ns, huber, partials, blockIdx.x - 1, nblk);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (threadIdx.x == 0) atomicAdd(cnt, 1u);
-    }
-    return;
-  }
-  // control block
-  __shared__ LMState sst;
-  __shared__ double sums[LM_NSUM];
-  constexpr int kWords = (int)(sizeof(LMState) / sizeof(unsigned));
-  static_assert(sizeof(LMState) % sizeof(unsigned) == 0, "LMState must be a whole number of dwords");
-  {
-    const unsigned* gsrc = reinterpret_cast<const unsigned*>(st);
-    unsigned* ldst = reinterpret_cast<unsigned*>(&sst);
-    for (int w = threadIdx.x; w < kWords; w += blockDim.x) ldst[w] = gsrc[w];
-  }
-  __syncthreads();
-  unsigned long long t_wait = 0, t_reduce = 0, t_ctrl = 0, n_it = 0;
-  int it = 0;
-  bool failed = false;
-  for (; it < 5 && !sst.done; ++it) {
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    if (threadIdx.x == 0) s_flag = wait_u32_geq(cnt, (unsigned)(nblk * (it + 1))) ? 0 : 1;
-    __syncthreads();
-    if (s_flag) {
-      failed = true;
-      break;
-    }
-    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
-    reduce_partials_sc1(partials, sums);
-    const unsigned long long t2 = __builtin_amdgcn_s_memrealtime();
-    lm_logic_wave0(sst, sums);
-    __syncthreads();
-    if (threadIdx.x == 0) {   // release the next evaluation point (cand after a step; x never changes here)
-      if (!sst.done) {
-#pragma unroll
-        for (int k = 0; k < 7; ++k) store_sc1(&point[k], sst.phase == 0 ? sst.x[k] : sst.cand[k]);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __hip_atomic_store(go, (epoch << 8) | (sst.done ? 0x80ull : 0ull) | (unsigned long long)(it + 1),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    const unsigned long long t3 = __builtin_amdgcn_s_memrealtime();
-    t_wait += t1 - t0;
-    t_reduce += t2 - t1;
-    t_ctrl += t3 - t2;
-    ++n_it;
-  }
-  __syncthreads();
-  {   // the final state for the host gather / the next launches (kernel boundary makes it visible)
-    unsigned* gdst = reinterpret_cast<unsigned*>(st);
-    const unsigned* lsrc = reinterpret_cast<const unsigned*>(&sst);
-    for (int w = threadIdx.x; w < kWords; w += blockDim.x) gdst[w] = lsrc[w];
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    if (failed) {   // never expected: end the solve, release the evaluation blocks, report through n_res
-      st->done = 1;
-      st->n_res = -1;
-      __hip_atomic_store(go, (epoch << 8) | 0x80ull | 0x7Full, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else if (it == 0) {   // done before the first evaluation: let any waiting evaluation block go
-      __hip_atomic_store(go, (epoch << 8) | 0x80ull | 0x7Full, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    *cnt = 0u;   // every evaluation block has arrived for the last released evaluation (kernel boundary orders it)
-    if (dbg && n_it) {   // diagnostic stamps (100 MHz): wait for the evaluations, reduce, control step + publish
-      atomicAdd(&dbg[1], t_wait);
-      atomicAdd(&dbg[2], t_reduce);
-      atomicAdd(&dbg[3], t_ctrl);
-      atomicAdd(&dbg[4], n_it);
-    }
   }
 }
 
@@ -1828,7 +1678,7 @@ __global__ __launch_bounds__(kTB) void lm_step_gram(LMState* __restrict__ st, co
   __shared__ double ssum[LM_NSUM];
   __shared__ double sums[LM_NSUM];
   __shared__ int s_timeout;
-  constexpr int kWords = (int)(sizeof(LMState) / sizeof(unsigned));
+  constexpr int kWords = kStateWords;
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   double gv = 0.0;
   {   // the LM state and (after the first evaluation of the solve) G + o, in one round trip
@@ -1896,6 +1746,149 @@ __global__ __launch_bounds__(kTB) void lm_step_gram(LMState* __restrict__ st, co
   }
 }
 
+// A whole Ceres solve in one launch (single GPU, squared loss): block 0 is the control block, blocks 1..nblk
+// evaluate the edge records; the surf half of every evaluation comes from G (reduced once, at the start, by the
+// control block while the evaluation blocks run iteration zero).  The blocks stay resident across the up to 5
+// evaluations and hand off without cache invalidations (sc1 words, MI355X_MICROARCH.md "Valid forms"):
+//   evaluation -> control: the block's 29 partial sums stored sc1, drained, then one agent-scope add on `cnt`;
+//   control -> evaluation: the next point (7 doubles) stored sc1 into `point`, drained, then the word
+//        go = (done << 7) | evaluations released.  go and cnt are zero at the launch (the kNN launch of the solve
+//        clears go; the control block leaves cnt at zero).
+// All 1 + nblk blocks must be co-resident (33 blocks); every wait is bounded (~1 s) and a timeout ends the solve
+// with st->n_res = -1, which the host reports as an error.
+__device__ __forceinline__ bool wait_u32_geq(unsigned* p, unsigned target) {
+  for (long long it = 0; it < (1ll << 24); ++it) {
+    if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return false;
+}
+
+__global__ __launch_bounds__(kTB) void lm_solve_gram(LMState* __restrict__ st, const double* __restrict__ erec,
+                                                     const uint8_t* __restrict__ evalid, int ecap,
+                                                     const int* __restrict__ d_ne, int ne_ub,
+                                                     const double* __restrict__ gpart, double* __restrict__ gmat,
+                                                     double* __restrict__ partials, unsigned* __restrict__ cnt,
+                                                     unsigned long long* __restrict__ dbg) {
+  const int nblk = (int)gridDim.x - 1;
+  unsigned long long* go = &st->go;
+  double* point = st->point;
+  __shared__ int s_flag;
+  if (blockIdx.x > 0) {
+    const int ne = min(*d_ne, ne_ub);
+    __shared__ double s_x[7];
+    for (int it = 0; it < 5; ++it) {
+      if (it == 0) {   // iteration zero evaluates at x (set by the kNN launch; kernel boundary)
+        if (threadIdx.x == 0) s_flag = st->done ? 1 : 0;
+        if (threadIdx.x < 7) s_x[threadIdx.x] = st->x[threadIdx.x];
+      } else {         // wait for the control step of evaluation it - 1, then read the point it released
+        if (threadIdx.x == 0) {
+          int f = 2;   // 0: go, 1: done, 2: timeout
+          for (long long k = 0; k < (1ll << 24); ++k) {
+            const unsigned long long g = __hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (g & 0x80ull) { f = 1; break; }
+            if ((int)(g & 0x7F) >= it) { f = 0; break; }
+            __builtin_amdgcn_s_sleep(1);
+          }
+          s_flag = f;
+        }
+        __syncthreads();
+        if (threadIdx.x < 7) s_x[threadIdx.x] = load_sc1(&point[threadIdx.x]);
+      }
+      __syncthreads();
+      if (s_flag) return;
+      double x[7];
+#pragma unroll
+      for (int k = 0; k < 7; ++k) x[k] = s_x[k];
+      eval_block_at<true>(x, erec, evalid, ecap, ne, nullptr, nullptr, 0, 0, 0, partials, blockIdx.x - 1, nblk);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the sc1 partials have reached L2-coherent memory
+      __syncthreads();
+      if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
+  // control block
+  __shared__ LMState sst;
+  __shared__ double G[kGramW][kGramW];
+  __shared__ double o[3];
+  __shared__ double ssum[LM_NSUM];
+  __shared__ double sums[LM_NSUM];
+  constexpr int kWords = kStateWords;
+  {
+    const unsigned* gsrc = reinterpret_cast<const unsigned*>(st);
+    unsigned* ldst = reinterpret_cast<unsigned*>(&sst);
+    for (int w = threadIdx.x; w < kWords; w += blockDim.x) ldst[w] = gsrc[w];
+  }
+  __syncthreads();
+  if (sst.done) return;   // (the evaluation blocks saw st->done too)
+  gram_load(gpart, gmat, true, 0.0, sst, G, o);
+  unsigned long long t_surf = 0, t_wait = 0, t_reduce = 0, t_ctrl = 0, n_it = 0;
+  int it = 0;
+  bool failed = false;
+  for (; it < 5 && !sst.done; ++it) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    {   // the surf half at this evaluation's point, while the evaluation blocks work
+      double x[7];
+#pragma unroll
+      for (int k = 0; k < 7; ++k) x[k] = sst.phase == 0 ? sst.x[k] : sst.cand[k];
+      surf_sums_from_gram(x, o, G, (double)sst.corr_surf, ssum);
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) s_flag = wait_u32_geq(cnt, (unsigned)(nblk * (it + 1))) ? 0 : 1;
+    __syncthreads();
+    if (s_flag) {
+      failed = true;
+      break;
+    }
+    const unsigned long long t2 = __builtin_amdgcn_s_memrealtime();
+    reduce_partials_block<true>(partials, nblk, sums);
+    if (threadIdx.x < LM_NSUM) sums[threadIdx.x] = sums[threadIdx.x] + ssum[threadIdx.x];   // edge + surf
+    __syncthreads();
+    const unsigned long long t3 = __builtin_amdgcn_s_memrealtime();
+    lm_logic_wave0(sst, sums);
+    __syncthreads();
+    if (threadIdx.x == 0) {   // release the next evaluation point (cand after a step; x never changes here)
+      if (!sst.done) {
+#pragma unroll
+        for (int k = 0; k < 7; ++k) store_sc1(&point[k], sst.phase == 0 ? sst.x[k] : sst.cand[k]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __hip_atomic_store(go, (sst.done ? 0x80ull : 0ull) | (unsigned long long)(it + 1), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const unsigned long long t4 = __builtin_amdgcn_s_memrealtime();
+    t_surf += t1 - t0;
+    t_wait += t2 - t1;
+    t_reduce += t3 - t2;
+    t_ctrl += t4 - t3;
+    ++n_it;
+  }
+  __syncthreads();
+  {   // the final state for the host gather / the next launches (kernel boundary makes it visible)
+    unsigned* gdst = reinterpret_cast<unsigned*>(st);
+    const unsigned* lsrc = reinterpret_cast<const unsigned*>(&sst);
+    for (int w = threadIdx.x; w < kWords; w += blockDim.x) gdst[w] = lsrc[w];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (failed) {   // never expected: end the solve, release the evaluation blocks, report through n_res
+      st->done = 1;
+      st->n_res = -1;
+      __hip_atomic_store(go, 0x80ull | 0x7Full, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (it == 0) {   // done before the first evaluation: let any waiting evaluation block go
+      __hip_atomic_store(go, 0x80ull | 0x7Full, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    *cnt = 0u;   // every evaluation block has arrived for the last released evaluation (kernel boundary orders it)
+    if (dbg && n_it) {   // diagnostic stamps (100 MHz): surf sums, wait, reduce, control step + publish
+      atomicAdd(&dbg[0], t_surf);
+      atomicAdd(&dbg[1], t_wait);
+      atomicAdd(&dbg[2], t_reduce);
+      atomicAdd(&dbg[3], t_ctrl);
+      atomicAdd(&dbg[4], n_it);
+    }
+  }
+}
+
 __global__ __launch_bounds__(kTB) void lm_reduce(const double* __restrict__ partials, int nblk, double* __restrict__ out) {
   __shared__ double sums[LM_NSUM];
   reduce_partials_block(partials, nblk, sums);
@@ -1928,7 +1921,7 @@ __global__ void gather_status(const LMState* __restrict__ lm, const int* __restr
                               const int* __restrict__ mapE_count, const int* __restrict__ mapS_count,
                               const int* __restrict__ fe_status, const unsigned long long* __restrict__ prof,
                               UpdateStatus* __restrict__ out, OdomDev* __restrict__ s, int mode) {
-  constexpr int kWords = (int)(sizeof(LMState) / sizeof(unsigned));
+  constexpr int kWords = kStateWords;
   const unsigned* src = reinterpret_cast<const unsigned*>(lm);
   unsigned* dst = reinterpret_cast<unsigned*>(&out->lm);
   for (int w = threadIdx.x; w < kWords; w += blockDim.x) dst[w] = src[w];
@@ -2092,12 +2085,10 @@ void lm_step_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub
   FLOAM_LAUNCH_CHECK();
 }
 
-void lm_solve_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const CorrSet& cs,
-                     const int* d_ns, int ns_ub, bool huber, double* partials, double* point, unsigned* cnt,
-                     unsigned long long* go, unsigned long long epoch, hipStream_t st, unsigned long long* dbg) {
-  const int nblk = (int)kEvalBlocks;   // fixed: the reduction order must not depend on the upper bounds
-  hipLaunchKernelGGL(lm_solve, dim3(nblk + 1), dim3(kTB), 0, st, d_st, ce.rec.p, ce.valid.p, ce.cap, d_ne, ne_ub,
-                     cs.rec.p, cs.valid.p, cs.cap, d_ns, ns_ub, huber ? 1 : 0, partials, point, cnt, go, epoch, dbg);
+void lm_solve_gram_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const double* gpart,
+                          double* gmat, double* partials, unsigned* cnt, hipStream_t st, unsigned long long* dbg) {
+  hipLaunchKernelGGL(lm_solve_gram, dim3(kEdgeEvalBlocks + 1), dim3(kTB), 0, st, d_st, ce.rec.p, ce.valid.p, ce.cap,
+                     d_ne, ne_ub, gpart, gmat, partials, cnt, dbg);
   FLOAM_LAUNCH_CHECK();
 }
 

@@ -84,7 +84,12 @@ struct LMState {
   int n_res;
   int corr_edge, corr_surf;   // accepted correspondences (this solve)
   int pad;
+  // hand-off words of the resident solve (lm_solve_gram), after the state proper: the control block copies only
+  // the state (kStateWords) in and out
+  unsigned long long go;      // (done << 7) | evaluations released; zeroed with the rest of the solve state
+  double point[8];            // the evaluation point released to the evaluation blocks
 };
+constexpr int kStateWords = (int)(offsetof(LMState, go) / sizeof(unsigned));
 
 enum { LM_NSUM = 29 };   // cost, H[21], g[6], count
 
@@ -163,12 +168,12 @@ int lm_eval_launch(const LMState* d_st, const CorrSet& ce, const int* d_ne, int 
 void lm_step_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const CorrSet& cs,
                     const int* d_ns, int ns_ub, bool huber, double* partials, unsigned* counter, hipStream_t st,
                     unsigned long long* dbg = nullptr);
-// a whole Ceres solve (up to 5 evaluations + control steps) in one launch with resident blocks; cnt (u32) and go
-// (u64) are device words: cnt zero before the first launch, go any value; epoch strictly increasing per launch
-void lm_solve_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const CorrSet& cs,
-                     const int* d_ns, int ns_ub, bool huber, double* partials, double* point, unsigned* cnt,
-                     unsigned long long* go, unsigned long long epoch, hipStream_t st,
-                     unsigned long long* dbg = nullptr);
+// a whole Ceres solve for the squared loss (up to 5 evaluations + control steps) in one launch with resident blocks
+// (surf half from the Gram matrix of geom_launch's gpart, edge records per record); cnt (u32) is a device word,
+// zero before the first launch (the kernel leaves it at zero)
+void lm_solve_gram_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const double* gpart,
+                          double* gmat, double* partials, unsigned* cnt, hipStream_t st,
+                          unsigned long long* dbg = nullptr);
 // LM iteration for the squared loss: surf sums from the Gram matrix of the surf records (geom_launch with gpart),
 // edge records per record on a small grid.  first: this is the solve's first evaluation (reduce gpart into gmat,
 // lm_gram_words() doubles); later launches of the solve reuse gmat.

@@ -41,9 +41,10 @@ __device__ __forceinline__ unsigned long long match_digit(unsigned d, bool valid
 __global__ __launch_bounds__(kTB) void radix_pass(const uint32_t* __restrict__ kin, const int* __restrict__ vin,
                                                   uint32_t* __restrict__ kout, int* __restrict__ vout, int n,
                                                   int pass, unsigned* __restrict__ ctl,
-                                                  unsigned long long* __restrict__ status, unsigned epoch,
+                                                  unsigned long long* __restrict__ status,
                                                   const int* __restrict__ gate) {
   if (gate && !*gate) return;
+  const unsigned epoch = ctl[kRadixEpochWord];
   __shared__ unsigned s_wcnt[kTB / 64][kRadixDigits];
   __shared__ unsigned s_off[kRadixDigits];
   __shared__ unsigned s_wsum[kTB / 64];
@@ -138,15 +139,18 @@ __global__ __launch_bounds__(kTB) void radix_pass(const uint32_t* __restrict__ k
 }
 }  // namespace
 
-void RadixScratch::reserve(int n) {
-  ctl.reserve(kRadixCtlWords);
+void RadixScratch::reserve(int n, hipStream_t st) {
+  if (!ctl.p) {
+    ctl.reserve(kRadixCtlWords);
+    FLOAM_HIP(hipMemsetAsync(ctl.p, 0, sizeof(unsigned) * kRadixCtlWords, st));
+  }
   const int tiles = (int)div_up((unsigned)std::max(n, 1), (unsigned)kTile);
   if (tiles > tiles_cap) {
     const int cap = tiles + tiles / 4 + 4;
     status.release();
     status.reserve((size_t)kRadixPasses * cap * kRadixDigits);
     // a fresh array: make every word's epoch field differ from the next epochs
-    FLOAM_HIP(hipMemset(status.p, 0xFF, sizeof(unsigned long long) * kRadixPasses * cap * kRadixDigits));
+    FLOAM_HIP(hipMemsetAsync(status.p, 0xFF, sizeof(unsigned long long) * kRadixPasses * cap * kRadixDigits, st));
     tiles_cap = cap;
   }
 }
@@ -154,15 +158,13 @@ void RadixScratch::reserve(int n) {
 void radix_sort_launch(RadixScratch& sc, uint32_t* k0, int* v0, uint32_t* k1, int* v1, int n, hipStream_t st,
                        const int* gate) {
   if (n <= 0) return;
-  sc.reserve(n);
-  sc.epoch = (sc.epoch + 1) & 0x3FFFFFFFu;
-  if (sc.epoch == 0x3FFFFFFFu) sc.epoch = 0;   // all-ones is the fresh-array pattern
+  sc.reserve(n, st);
   const int tiles = (int)div_up((unsigned)n, (unsigned)kTile);
   for (int p = 0; p < kRadixPasses; ++p) {
     const bool even = (p & 1) == 0;
     hipLaunchKernelGGL(radix_pass, dim3(tiles), dim3(kTB), 0, st, even ? k0 : k1, even ? v0 : v1, even ? k1 : k0,
                        even ? v1 : v0, n, p, sc.ctl.p, sc.status.p + (size_t)p * sc.tiles_cap * kRadixDigits,
-                       sc.epoch, gate);
+                       gate);
     FLOAM_LAUNCH_CHECK();
   }
 }

@@ -9,14 +9,16 @@ namespace floam {
 constexpr int kRadixDigits = 256;
 constexpr int kRadixPasses = 4;
 constexpr int kRadixHistWords = kRadixPasses * kRadixDigits;   // followed by 4 tile tickets + 1 error word
+constexpr int kRadixZeroWords = kRadixHistWords + 5;            // zeroed per sort
+constexpr int kRadixEpochWord = kRadixHistWords + 5;            // sort counter (tags the lookback words)
 constexpr int kRadixCtlWords = kRadixHistWords + 8;
 
 struct RadixScratch {
-  DevBuf<unsigned> ctl;                  // [4][256] digit histograms, [4] tickets, [1] error (zeroed per sort)
+  DevBuf<unsigned> ctl;                  // [4][256] digit histograms, [4] tickets, [1] error (zeroed per sort),
+                                         // [1] the sort counter (advanced per sort on the device)
   DevBuf<unsigned long long> status;     // [4][tiles][256] lookback words, tagged with the sort's epoch
   int tiles_cap = 0;
-  unsigned epoch = 0;
-  void reserve(int n);
+  void reserve(int n, hipStream_t st);
 };
 
 // Producer side (inside the kernel that writes the keys; all threads of the block call both):
@@ -39,12 +41,18 @@ __device__ __forceinline__ void radix_hist_end(const unsigned* s_hist, unsigned*
     if (v) atomicAdd(&ctl[k], v);
   }
 }
+// zero the per-sort words and advance the sort counter (epoch 0x3FFFFFFF is the fresh-array pattern: skipped)
 __device__ __forceinline__ void radix_ctl_zero(unsigned* ctl, int t, int stride) {
-  for (int k = t; k < kRadixCtlWords; k += stride) ctl[k] = 0u;
+  for (int k = t; k < kRadixZeroWords; k += stride) ctl[k] = 0u;
+  if (t == 0) {
+    unsigned e = (ctl[kRadixEpochWord] + 1u) & 0x3FFFFFFFu;
+    if (e == 0x3FFFFFFFu) e = 0u;
+    ctl[kRadixEpochWord] = e;
+  }
 }
 
 // The four passes: (k0, v0) -> (k1, v1) -> (k0, v0) -> (k1, v1) -> (k0, v0); the sorted pairs end in k0 / v0.
-// n must be the element count the histograms were built over.  ctl[1028] != 0 afterwards if a lookback timed out
+// n must be the element count the histograms were built over; radix_ctl_zero must have run since the last sort.  ctl[1028] != 0 afterwards if a lookback timed out
 // (never expected; the consumer reports it).
 // gate (device int, nullable): the passes do nothing when it reads 0.
 void radix_sort_launch(RadixScratch& sc, uint32_t* k0, int* v0, uint32_t* k1, int* v1, int n, hipStream_t st,

@@ -411,7 +411,7 @@ void voxel2_launch(VoxelScratch2& sc, const VoxelJob& a, const VoxelJob& b, hipS
   sc.status.reserve(ntiles);
   sc.ticket.reserve(1);
   const int umax = std::max(A.n0_ub + A.n1_ub, b.n0_ub + (b.part1 ? b.n1_ub : 0));
-  sc.rs.reserve(n);
+  sc.rs.reserve(n, st);
   hipLaunchKernelGGL(vox_minmax, dim3(kMinMaxBlocks, 2), dim3(kTB), 0, st, A, B, sc.partials.p, sc.rs.ctl.p, gate);
   FLOAM_LAUNCH_CHECK();
   // few blocks: each folds its LDS digit histograms into the global ones with one atomic per non-zero bin
