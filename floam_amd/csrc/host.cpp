@@ -241,6 +241,7 @@ struct floam_odom {
   int lm_mode = 0;
   DevBuf<double> gpart;                 // per-block surf Gram partials
   DevBuf<double> gmat;                  // the solve's surf Gram matrix + its origin
+  DevBuf<unsigned> gcnt;                // ticket words of its reduction
   DevBuf<unsigned long long> dbg_stamps;   // FLOAM_DEBUG_STAMPS=1: lm_step segment times (diagnostic)
   DevBuf<LMState> lm;
   // status slots, two per in-flight update (first / only call, second call of a deskewed selector)
@@ -383,6 +384,10 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
   if (gram) {
     o->gpart.reserve(lm_gram_partials());
     o->gmat.reserve(lm_gram_words());
+    if (!o->gcnt.p) {
+      o->gcnt.reserve(lm_gram_counters());
+      FLOAM_HIP(hipMemsetAsync(o->gcnt.p, 0, sizeof(unsigned) * lm_gram_counters(), st));
+    }
   }
   for (int it = 0; it < o->optimization_count; ++it) {
     {
@@ -395,8 +400,8 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
                    o->dbg_stamps.p ? o->dbg_stamps.p + 8 : nullptr);
       }
       ProfScope ps2(ctx, "knn_geometry", FLOAM_PROF_KNN_DETAIL);
-      geom_launch(o->lm.p, qe, o->gE, o->mapE.pts.p, o->ce, qs, o->gS, o->mapS.pts.p, o->cs, gram ? o->gpart.p : nullptr,
-                  st);
+      geom_launch(o->lm.p, qe, o->gE, o->mapE.pts.p, o->ce, qs, o->gS, o->mapS.pts.p, o->cs,
+                  gram ? o->gpart.p : nullptr, gram ? o->gmat.p : nullptr, o->gcnt.p, st);
     }
     if (ctx.profile & FLOAM_PROF_KNN_BYTES) {   // replay only: algorithmic bytes of the two launches above
       knn_traffic_launch(o->lm.p, qe, o->gE, o->mapE.pts.p, o->ce, 8 * EDGE_FIELDS, o->rank, o->world, o->traffic_set,
@@ -414,7 +419,7 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
     for (int ev = 0; ev < 5; ++ev) {
       ProfScope ps(ctx, "lm_step", FLOAM_PROF_LM);
       if (gram) {
-        lm_step_gram_launch(o->lm.p, o->ce, o->cnt.p + 0, ne_ub, o->gpart.p, o->gmat.p, ev == 0, o->partials.p,
+        lm_step_gram_launch(o->lm.p, o->ce, o->cnt.p + 0, ne_ub, o->gpart.p, o->gmat.p, false, o->partials.p,
                             o->step_counter.p, st, o->dbg_stamps.p);
       } else if (sharded) {
         const int nblk = lm_eval_launch(o->lm.p, o->ce, o->cnt.p + 0, ne_ub, o->cs, o->cnt.p + 1, ns_ub, o->huber,

@@ -754,8 +754,11 @@ __device__ __forceinline__ void gram_pair(int e, int& i, int& j) {   // upper-tr
 // Edge blocks: one query per lane.  Surf blocks (fixed grid, grid-stride): one query per lane, and the block's
 // partial Gram matrix of its accepted surf records (waves stage w in LDS, lane e sums entry e over the wave's 64
 // records in lane order, waves combined in order) into gpart[block][91].
+constexpr int kGramGroups = 8;   // the surf blocks' partials are reduced in 8 groups of 32, then the groups
+
 __global__ __launch_bounds__(kTB) void geom_kernel(LMState* __restrict__ st, CorrArgs E, CorrArgs S, int nbE,
-                                                   double* __restrict__ gpart) {
+                                                   double* __restrict__ gpart, double* __restrict__ gmat,
+                                                   unsigned* __restrict__ gcnt) {
   if ((int)blockIdx.x < nbE) {
     geom_query<true>(st, E, blockIdx.x * blockDim.x + threadIdx.x);
     return;
@@ -801,6 +804,44 @@ __global__ __launch_bounds__(kTB) void geom_kernel(LMState* __restrict__ st, Cor
     for (int k = 1; k < kTB / 64; ++k) v += s_part[k][threadIdx.x];
     gpart[sb * kGram + threadIdx.x] = v;
   }
+  // G of the solve, reduced by the last-arriving blocks (fixed order: the 32 blocks of a group, then the 8 groups):
+  // producer stores -> vmcnt(0) -> barrier -> agent release -> ticket; the block whose ticket is last acquires
+  constexpr int per = kSurfGeomBlocks / kGramGroups;
+  __shared__ int s_last;
+  const int grp = sb / per;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    s_last = atomicAdd(&gcnt[grp], 1u) == (unsigned)(per - 1);
+    if (s_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+  if (!s_last) return;
+  double* gpart2 = gpart + kSurfGeomBlocks * kGram;   // [8][91] group partials
+  if (threadIdx.x < kGram) {
+    double v = 0.0;
+    for (int k = 0; k < per; ++k) v += gpart[(grp * per + k) * kGram + threadIdx.x];
+    gpart2[grp * kGram + threadIdx.x] = v;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    gcnt[grp] = 0u;   // every block of the group has arrived (next launch: kernel boundary)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    s_last = atomicAdd(&gcnt[kGramGroups], 1u) == (unsigned)(kGramGroups - 1);
+    if (s_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+  if (!s_last) return;
+  if (threadIdx.x < kGram) {
+    double v = gpart2[threadIdx.x];
+    for (int k = 1; k < kGramGroups; ++k) v += gpart2[k * kGram + threadIdx.x];
+    gmat[threadIdx.x] = v;
+  } else if (threadIdx.x < kGram + 3) {
+    gmat[threadIdx.x] = o[threadIdx.x - kGram];   // the origin the records were recentred on
+  }
+  if (threadIdx.x == 0) gcnt[kGramGroups] = 0u;
 }
 
 // Algorithmic traffic of one correspondence pass (SURVEY.md §8 d): every map cell any query scans
@@ -1009,6 +1050,60 @@ __device__ void eval_block(const LMState* __restrict__ st, const double* __restr
   eval_block_at<SC1>(x, erec, evalid, ecap, ne, srec, svalid, scap, ns, huber, partials, blk, nblk);
 }
 
+// one residual (r, J) into the 29 sums (cost, J^T J upper, J^T r, count), with the Huber corrector if asked
+__device__ __forceinline__ void accumulate_residual(double (&acc)[LM_NSUM], double r, double (&J)[6], int huber) {
+  const double sq = r * r;
+  if (huber) {   // ceres::HuberLoss(0.1) + Corrector (rho'' <= 0: residual scaling sqrt(rho'))
+    double rho0, rho1;
+    if (sq > 0.01) {
+      const double rr = sqrt(sq);
+      rho0 = 2.0 * 0.1 * rr - 0.01;
+      rho1 = fmax(DBL_MIN, 0.1 / rr);
+    } else {
+      rho0 = sq;
+      rho1 = 1.0;
+    }
+    acc[0] += 0.5 * rho0;
+    const double sr = sqrt(rho1);
+    r *= sr;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) J[k] *= sr;
+  } else {
+    acc[0] += 0.5 * sq;
+  }
+  int h = 1;
+#pragma unroll
+  for (int a = 0; a < 6; ++a)
+#pragma unroll
+    for (int b = a; b < 6; ++b) acc[h++] += J[a] * J[b];
+#pragma unroll
+  for (int a = 0; a < 6; ++a) acc[22 + a] += J[a] * r;
+  acc[28] += 1.0;
+}
+
+// fixed-order block reduction through LDS: [component][thread] -> 8 strips of 32 per component -> 8 partials
+template <bool SC1>
+__device__ void store_block_partials(const double (&acc)[LM_NSUM], double* __restrict__ partials, int blk, int nblk) {
+  __shared__ double red[LM_NSUM][kTB];
+  __shared__ double strip[LM_NSUM][8];
+#pragma unroll
+  for (int k = 0; k < LM_NSUM; ++k) red[k][threadIdx.x] = acc[k];
+  __syncthreads();
+  if (threadIdx.x < LM_NSUM * 8) {
+    const int c = threadIdx.x >> 3, p = threadIdx.x & 7;
+    double v = 0.0;
+    for (int j = 0; j < kTB / 8; ++j) v += red[c][p * (kTB / 8) + j];
+    strip[c][p] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < LM_NSUM) {
+    double v = 0.0;
+    for (int p = 0; p < 8; ++p) v += strip[threadIdx.x][p];
+    if (SC1) store_sc1(&partials[threadIdx.x * nblk + blk], v);
+    else partials[threadIdx.x * nblk + blk] = v;
+  }
+}
+
 template <bool SC1>
 __device__ void eval_block_at(const double (&x)[7], const double* __restrict__ erec,
                               const uint8_t* __restrict__ evalid, int ecap, int ne, const double* __restrict__ srec,
@@ -1034,53 +1129,9 @@ __device__ void eval_block_at(const double (&x)[7], const double* __restrict__ e
       for (int k = 0; k < 7; ++k) f[k] = srec[k * scap + s];
       r = surf_residual(x, f, J);
     }
-    const double sq = r * r;
-    if (huber) {   // ceres::HuberLoss(0.1) + Corrector (rho'' <= 0: residual scaling sqrt(rho'))
-      double rho0, rho1;
-      if (sq > 0.01) {
-        const double rr = sqrt(sq);
-        rho0 = 2.0 * 0.1 * rr - 0.01;
-        rho1 = fmax(DBL_MIN, 0.1 / rr);
-      } else {
-        rho0 = sq;
-        rho1 = 1.0;
-      }
-      acc[0] += 0.5 * rho0;
-      const double sr = sqrt(rho1);
-      r *= sr;
-#pragma unroll
-      for (int k = 0; k < 6; ++k) J[k] *= sr;
-    } else {
-      acc[0] += 0.5 * sq;
-    }
-    int h = 1;
-#pragma unroll
-    for (int a = 0; a < 6; ++a)
-#pragma unroll
-      for (int b = a; b < 6; ++b) acc[h++] += J[a] * J[b];
-#pragma unroll
-    for (int a = 0; a < 6; ++a) acc[22 + a] += J[a] * r;
-    acc[28] += 1.0;
+    accumulate_residual(acc, r, J, huber);
   }
-  // fixed-order block reduction through LDS: [component][thread] -> 8 strips of 32 per component -> 8 partials
-  __shared__ double red[LM_NSUM][kTB];
-  __shared__ double strip[LM_NSUM][8];
-#pragma unroll
-  for (int k = 0; k < LM_NSUM; ++k) red[k][threadIdx.x] = acc[k];
-  __syncthreads();
-  if (threadIdx.x < LM_NSUM * 8) {
-    const int c = threadIdx.x >> 3, p = threadIdx.x & 7;
-    double v = 0.0;
-    for (int j = 0; j < kTB / 8; ++j) v += red[c][p * (kTB / 8) + j];
-    strip[c][p] = v;
-  }
-  __syncthreads();
-  if (threadIdx.x < LM_NSUM) {
-    double v = 0.0;
-    for (int p = 0; p < 8; ++p) v += strip[threadIdx.x][p];
-    if (SC1) store_sc1(&partials[threadIdx.x * nblk + blk], v);
-    else partials[threadIdx.x * nblk + blk] = v;
-  }
+  store_block_partials<SC1>(acc, partials, blk, nblk);
 }
 
 __global__ __launch_bounds__(kTB) void lm_eval(const LMState* __restrict__ st, const double* __restrict__ erec,
@@ -1777,6 +1828,12 @@ __global__ __launch_bounds__(kTB) void lm_solve_gram(LMState* __restrict__ st, c
   if (blockIdx.x > 0) {
     const int ne = min(*d_ne, ne_ub);
     __shared__ double s_x[7];
+    // the thread's first edge record stays in registers across the evaluations (all of them at C3: ne <= 8192)
+    const int blk = blockIdx.x - 1, stride = nblk * kTB, i0 = blk * kTB + threadIdx.x;
+    double f0[9];
+    const bool has0 = i0 < ne && (evalid[i0] & 1);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) f0[k] = has0 ? erec[k * ecap + i0] : 0.0;
     for (int it = 0; it < 5; ++it) {
       if (it == 0) {   // iteration zero evaluates at x (set by the kNN launch; kernel boundary)
         if (threadIdx.x == 0) s_flag = st->done ? 1 : 0;
@@ -1800,7 +1857,23 @@ __global__ __launch_bounds__(kTB) void lm_solve_gram(LMState* __restrict__ st, c
       double x[7];
 #pragma unroll
       for (int k = 0; k < 7; ++k) x[k] = s_x[k];
-      eval_block_at<true>(x, erec, evalid, ecap, ne, nullptr, nullptr, 0, 0, 0, partials, blockIdx.x - 1, nblk);
+      double acc[LM_NSUM];
+#pragma unroll
+      for (int k = 0; k < LM_NSUM; ++k) acc[k] = 0.0;
+      if (has0) {
+        double J[6];
+        const double r = edge_residual(x, f0, J);
+        accumulate_residual(acc, r, J, 0);
+      }
+      for (int idx = i0 + stride; idx < ne; idx += stride) {   // beyond one record per thread
+        if (!(evalid[idx] & 1)) continue;
+        double f[9], J[6];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) f[k] = erec[k * ecap + idx];
+        const double r = edge_residual(x, f, J);
+        accumulate_residual(acc, r, J, 0);
+      }
+      store_block_partials<true>(acc, partials, blk, nblk);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the sc1 partials have reached L2-coherent memory
       __syncthreads();
       if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1821,7 +1894,10 @@ __global__ __launch_bounds__(kTB) void lm_solve_gram(LMState* __restrict__ st, c
   }
   __syncthreads();
   if (sst.done) return;   // (the evaluation blocks saw st->done too)
-  gram_load(gpart, gmat, true, 0.0, sst, G, o);
+  {
+    const double gv = threadIdx.x < kGramWords ? gmat[threadIdx.x] : 0.0;
+    gram_load(gpart, gmat, false, gv, sst, G, o);
+  }
   unsigned long long t_surf = 0, t_wait = 0, t_reduce = 0, t_ctrl = 0, n_it = 0;
   int it = 0;
   bool failed = false;
@@ -2032,13 +2108,14 @@ void knn_launch(LMState* d_st, const double* x0, const double* x0_dev, const Que
 }
 
 void geom_launch(LMState* d_st, const QuerySet& qe, const Grid& ge, const PointRec* mapE, CorrSet& ce,
-                 const QuerySet& qs, const Grid& gs, const PointRec* mapS, CorrSet& cs, double* gpart,
-                 hipStream_t st) {
+                 const QuerySet& qs, const Grid& gs, const PointRec* mapS, CorrSet& cs, double* gpart, double* gmat,
+                 unsigned* gcnt, hipStream_t st) {
   CorrArgs E, S;
   corr_args(qe, ge, mapE, ce, qs, gs, mapS, cs, nullptr, E, S);
   if (qe.n_ub <= 0 && qs.n_ub <= 0) return;
   const unsigned gE = div_up(std::max(qe.n_ub, 1), kTB);
-  hipLaunchKernelGGL(geom_kernel, dim3(gE + kSurfGeomBlocks), dim3(kTB), 0, st, d_st, E, S, (int)gE, gpart);
+  hipLaunchKernelGGL(geom_kernel, dim3(gE + kSurfGeomBlocks), dim3(kTB), 0, st, d_st, E, S, (int)gE, gpart, gmat,
+                     gcnt);
   FLOAM_LAUNCH_CHECK();
 }
 
@@ -2093,7 +2170,8 @@ void lm_solve_gram_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int
 }
 
 bool lm_gram_supported(bool huber) { return !huber; }
-size_t lm_gram_partials() { return (size_t)kSurfGeomBlocks * kGram; }
+size_t lm_gram_partials() { return (size_t)(kSurfGeomBlocks + kGramGroups) * kGram; }
+int lm_gram_counters() { return kGramGroups + 1; }
 size_t lm_gram_words() { return (size_t)kGramWords; }
 
 void lm_step_gram_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const double* gpart,

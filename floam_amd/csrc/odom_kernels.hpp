@@ -154,9 +154,11 @@ void knn_launch(LMState* d_st, const double* x0, const double* x0_dev, const Que
                 CorrSet& ce, const QuerySet& qs, const Grid& gs, const PointRec* mapS, CorrSet& cs, const int* d_me,
                 const int* d_ms, int rank, int world, hipStream_t st, unsigned long long* dbg = nullptr);
 // gpart (nullable): per-block partial Gram matrices of the surf records for lm_step_gram ([256][91] doubles)
+// and, with gpart, the solve's surf Gram matrix into gmat (lm_gram_words() doubles) through gpart's block and group
+// partials (lm_gram_partials() doubles) and the ticket words gcnt (lm_gram_counters(), zero before the first use)
 void geom_launch(LMState* d_st, const QuerySet& qe, const Grid& ge, const PointRec* mapE, CorrSet& ce,
-                 const QuerySet& qs, const Grid& gs, const PointRec* mapS, CorrSet& cs, double* gpart,
-                 hipStream_t st);
+                 const QuerySet& qs, const Grid& gs, const PointRec* mapS, CorrSet& cs, double* gpart, double* gmat,
+                 unsigned* gcnt, hipStream_t st);
 // algorithmic bytes of the correspondence pass just issued (profiling only), accumulated into *d_bytes
 void knn_traffic_launch(const LMState* d_st, const QuerySet& q, const Grid& g, const PointRec* map, CorrSet& c,
                         int rec_bytes, int rank, int world, DevBuf<unsigned long long>& set,
@@ -179,6 +181,7 @@ void lm_solve_gram_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int
 // lm_gram_words() doubles); later launches of the solve reuse gmat.
 bool lm_gram_supported(bool huber);
 size_t lm_gram_partials();   // doubles in gpart
+int lm_gram_counters();       // ticket words of the geometry kernel's Gram reduction
 size_t lm_gram_words();      // doubles in gmat
 void lm_step_gram_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const double* gpart,
                          double* gmat, bool first, double* partials, unsigned* counter, hipStream_t st,
