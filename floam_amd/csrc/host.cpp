@@ -1008,6 +1008,7 @@ floam_status floam_odom_destroy(floam_odom* o) {
     if (o) {
       DeviceCtx& ctx = ctx_for(o->device);
       FLOAM_HIP(hipStreamSynchronize(ctx.stream));
+      ctrl_stamps_print();
       for (auto& P : o->inflight) {
         FLOAM_HIP(hipEventDestroy(P.ev));
         for (void* b : P.graveyard) (void)hipFree(b);

@@ -1329,15 +1329,31 @@ __device__ __forceinline__ double bcast(double v, int src) { return __shfl(v, sr
 // NextStep with the gradient-norm test folded in: ComputeTrustRegionStep (+ HandleInvalidStep retries) and, when
 // check_gmax, the projected-gradient max norm at x (lane 1) computed alongside the candidate (lane 0).  If the
 // gradient test ends the solve the step is discarded, as in the sequential order (test first, then step).
+#ifdef FLOAM_CTRL_STAMPS
+__device__ unsigned long long g_ctrl_stamps[8];
+#define CTRL_STAMP(i, t)                                                        \
+  do {                                                                          \
+    const unsigned long long tn_ = __builtin_amdgcn_s_memrealtime();            \
+    if (lane == 0) atomicAdd(&g_ctrl_stamps[i], tn_ - (t));                      \
+    (t) = tn_;                                                                  \
+  } while (0)
+#else
+#define CTRL_STAMP(i, t) (void)0
+#endif
 __device__ __forceinline__ void next_step_wave(LMState& s, bool check_gmax, int lane) {
   for (;;) {
+#ifdef FLOAM_CTRL_STAMPS
+    unsigned long long ts = __builtin_amdgcn_s_memrealtime();
+#endif
     double delta[6];
     const bool valid = solve_step(s, delta);
+    CTRL_STAMP(0, ts);
     double d[6];
 #pragma unroll
     for (int k = 0; k < 6; ++k) d[k] = lane == 1 ? -s.g[k] : (valid ? delta[k] : 0.0);
     double out[7];
     se3_plus(s.x, d, out);
+    CTRL_STAMP(1, ts);
     if (check_gmax) {
       double m = 0.0;
 #pragma unroll
@@ -1434,10 +1450,18 @@ __device__ __forceinline__ void lm_logic(LMState& s, const double (&sums)[LM_NSU
 // same fields (LDS broadcast) and store identical values, so the state never has to fit in registers.
 __device__ __forceinline__ void lm_logic_wave0(LMState& sst, const double* sums_lds) {
   if (threadIdx.x < 64) {
+#ifdef FLOAM_CTRL_STAMPS
+    const int lane = threadIdx.x;
+    unsigned long long ts = __builtin_amdgcn_s_memrealtime();
+#endif
     double sm[LM_NSUM];
 #pragma unroll
     for (int k = 0; k < LM_NSUM; ++k) sm[k] = sums_lds[k];
     lm_logic(sst, sm, (int)threadIdx.x);
+    CTRL_STAMP(2, ts);
+#ifdef FLOAM_CTRL_STAMPS
+    if (lane == 0) atomicAdd(&g_ctrl_stamps[3], 1ull);
+#endif
   }
 }
 
@@ -2167,6 +2191,15 @@ void lm_solve_gram_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int
   hipLaunchKernelGGL(lm_solve_gram, dim3(kEdgeEvalBlocks + 1), dim3(kTB), 0, st, d_st, ce.rec.p, ce.valid.p, ce.cap,
                      d_ne, ne_ub, gpart, gmat, partials, cnt, dbg);
   FLOAM_LAUNCH_CHECK();
+}
+
+void ctrl_stamps_print() {
+#ifdef FLOAM_CTRL_STAMPS
+  unsigned long long h[8];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_ctrl_stamps), sizeof(h)) == hipSuccess && h[3])
+    std::fprintf(stderr, "[floam ctrl] %llu control steps: solve_step %.2f us, se3_plus %.2f us (per step), whole %.2f us\n",
+                 h[3], h[0] / (double)h[3] / 100.0, h[1] / (double)h[3] / 100.0, h[2] / (double)h[3] / 100.0);
+#endif
 }
 
 bool lm_gram_supported(bool huber) { return !huber; }

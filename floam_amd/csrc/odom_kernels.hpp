@@ -180,6 +180,7 @@ void lm_solve_gram_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int
 // edge records per record on a small grid.  first: this is the solve's first evaluation (reduce gpart into gmat,
 // lm_gram_words() doubles); later launches of the solve reuse gmat.
 bool lm_gram_supported(bool huber);
+void ctrl_stamps_print();   // diagnostic build (-DFLOAM_CTRL_STAMPS): control-step breakdown
 size_t lm_gram_partials();   // doubles in gpart
 int lm_gram_counters();       // ticket words of the geometry kernel's Gram reduction
 size_t lm_gram_words();      // doubles in gmat

@@ -42,9 +42,10 @@ __global__ __launch_bounds__(kTB) void radix_pass(const uint32_t* __restrict__ k
                                                   uint32_t* __restrict__ kout, int* __restrict__ vout, int n,
                                                   int pass, unsigned* __restrict__ ctl,
                                                   unsigned long long* __restrict__ status,
-                                                  const int* __restrict__ gate) {
+                                                  const int* __restrict__ gate, const int* __restrict__ n_dev) {
   if (gate && !*gate) return;
   const unsigned epoch = ctl[kRadixEpochWord];
+  if (n_dev) n = min(n, *n_dev);
   __shared__ unsigned s_wcnt[kTB / 64][kRadixDigits];
   __shared__ unsigned s_off[kRadixDigits];
   __shared__ unsigned s_wsum[kTB / 64];
@@ -56,6 +57,7 @@ __global__ __launch_bounds__(kTB) void radix_pass(const uint32_t* __restrict__ k
   for (int k = 0; k < kTB / 64; ++k) s_wcnt[k][t] = 0u;
   __syncthreads();
   const int tile = s_tile;
+  if (tile * kTile >= n) return;   // beyond the elements (block-uniform); nobody waits on a later tile
   const int base = tile * kTile + w * 64 * kItems;
   uint32_t key[kItems];
   int val[kItems];
@@ -156,7 +158,7 @@ void RadixScratch::reserve(int n, hipStream_t st) {
 }
 
 void radix_sort_launch(RadixScratch& sc, uint32_t* k0, int* v0, uint32_t* k1, int* v1, int n, hipStream_t st,
-                       const int* gate) {
+                       const int* gate, const int* n_dev) {
   if (n <= 0) return;
   sc.reserve(n, st);
   const int tiles = (int)div_up((unsigned)n, (unsigned)kTile);
@@ -164,7 +166,7 @@ void radix_sort_launch(RadixScratch& sc, uint32_t* k0, int* v0, uint32_t* k1, in
     const bool even = (p & 1) == 0;
     hipLaunchKernelGGL(radix_pass, dim3(tiles), dim3(kTB), 0, st, even ? k0 : k1, even ? v0 : v1, even ? k1 : k0,
                        even ? v1 : v0, n, p, sc.ctl.p, sc.status.p + (size_t)p * sc.tiles_cap * kRadixDigits,
-                       gate);
+                       gate, n_dev);
     FLOAM_LAUNCH_CHECK();
   }
 }

@@ -55,7 +55,8 @@ __device__ __forceinline__ void radix_ctl_zero(unsigned* ctl, int t, int stride)
 // n must be the element count the histograms were built over; radix_ctl_zero must have run since the last sort.  ctl[1028] != 0 afterwards if a lookback timed out
 // (never expected; the consumer reports it).
 // gate (device int, nullable): the passes do nothing when it reads 0.
+// n_dev (device int, nullable): the element count actually sorted (<= n, which sizes the grid).
 void radix_sort_launch(RadixScratch& sc, uint32_t* k0, int* v0, uint32_t* k1, int* v1, int n, hipStream_t st,
-                       const int* gate = nullptr);
+                       const int* gate = nullptr, const int* n_dev = nullptr);
 
 }  // namespace floam

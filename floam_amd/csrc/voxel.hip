@@ -132,7 +132,8 @@ __global__ __launch_bounds__(kTB) void vox_keys(VoxelJobDev A, VoxelJobDev B, co
                                                 uint32_t* __restrict__ keys, int* __restrict__ vals,
                                                 int* __restrict__ overflow, unsigned long long* __restrict__ status,
                                                 int ntiles, unsigned* __restrict__ ticket,
-                                                unsigned* __restrict__ radix_ctl, const int* __restrict__ gate) {
+                                                unsigned* __restrict__ radix_ctl, const int* __restrict__ gate,
+                                                int* __restrict__ n_dev) {
   if (gate && !*gate) return;
   const int job = blockIdx.y;
   const VoxelJobDev& J = job == 0 ? A : B;
@@ -156,9 +157,13 @@ __global__ __launch_bounds__(kTB) void vox_keys(VoxelJobDev A, VoxelJobDev B, co
   const float mn[3] = {s_mm[0], s_mm[1], s_mm[2]}, mx[3] = {s_mm[3], s_mm[4], s_mm[5]};
   const VoxelGeom g = voxel_geom(mn, mx, J.inv);
   if (blockIdx.x == 0 && threadIdx.x == 0) overflow[job] = g.overflow ? 1 : 0;
-  const int n0 = *J.d_n0, n1 = J.d_n1 ? *J.d_n1 : 0;
-  const int U = J.n0_ub + J.n1_ub;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < U; i += gridDim.x * blockDim.x) {
+  // the elements the device holds, packed: cloud A at [0, nA), cloud B at [nA, nA + nB) (no upper-bound padding)
+  const int nA0 = min(*A.d_n0, A.n0_ub), nA1 = A.d_n1 ? min(*A.d_n1, A.n1_ub) : 0;
+  const int nB0 = min(*B.d_n0, B.n0_ub), nB1 = B.d_n1 ? min(*B.d_n1, B.n1_ub) : 0;
+  const int n0 = job ? nB0 : nA0, n1 = job ? nB1 : nA1;
+  const int base = job ? nA0 + nA1 : 0;
+  if (job == 0 && blockIdx.x == 0 && threadIdx.x == 0) *n_dev = nA0 + nA1 + nB0 + nB1;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n0 + n1; i += gridDim.x * blockDim.x) {
     uint32_t key = 0xFFFFFFFFu;
     PointRec p;
     if (vox_fetch(J, n0, n1, i, p)) {
@@ -173,8 +178,8 @@ __global__ __launch_bounds__(kTB) void vox_keys(VoxelJobDev A, VoxelJobDev B, co
       }
       key = ((uint32_t)job << 31) | idx;
     }
-    keys[J.base + i] = key;
-    vals[J.base + i] = i;
+    keys[base + i] = key;
+    vals[base + i] = i;
     radix_hist_add(s_hist, key);
   }
   radix_hist_end(s_hist, radix_ctl);
@@ -183,7 +188,7 @@ __global__ __launch_bounds__(kTB) void vox_keys(VoxelJobDev A, VoxelJobDev B, co
 // Run heads of the sorted keys -> output slot per cloud (decoupled lookback over tiles) -> centroid of the run.
 __global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B, const uint32_t* __restrict__ keys,
                                                    const int* __restrict__ vals, const int* __restrict__ overflow,
-                                                   int total, unsigned long long* __restrict__ status,
+                                                   const int* __restrict__ n_dev, unsigned long long* __restrict__ status,
                                                    unsigned* __restrict__ ticket, const unsigned* __restrict__ radix_ctl,
                                                    const int* __restrict__ gate) {
   if (gate && !*gate) {   // gated off (no keyframe): the output is the unchanged first part (the map)
@@ -196,7 +201,12 @@ __global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B,
     return;
   }
   const int tile = lookback_ticket(ticket);
-  const int ntiles = (int)gridDim.x;
+  const int total = *n_dev;   // packed elements (vox_keys)
+  const int ntiles = (total + kTile - 1) / kTile;
+  if (tile >= ntiles) {   // beyond the device's elements (the grid is sized by the host's upper bounds)
+    if (tile == 0 && threadIdx.x == 0) { *A.d_out = 0; *B.d_out = 0; }   // no elements at all
+    return;
+  }
   const int t0 = tile * kTile;
   // s_key[k] = key of element t0 - 1 + k, k in [0, kTile + 1]
   __shared__ uint32_t s_key[kTile + 2];
@@ -406,7 +416,7 @@ void voxel2_launch(VoxelScratch2& sc, const VoxelJob& a, const VoxelJob& b, hipS
   const int n = total;
   sc.s.reserve(n);
   sc.partials.reserve(2 * kMinMaxBlocks * 6);
-  sc.overflow.reserve(2);
+  sc.overflow.reserve(3);   // [0, 1] index overflow per cloud, [2] packed element count
   const int ntiles = (int)div_up(n, kTile);
   sc.status.reserve(ntiles);
   sc.ticket.reserve(1);
@@ -417,11 +427,12 @@ void voxel2_launch(VoxelScratch2& sc, const VoxelJob& a, const VoxelJob& b, hipS
   // few blocks: each folds its LDS digit histograms into the global ones with one atomic per non-zero bin
   const unsigned kb = std::max(1u, std::min(div_up(std::max(umax, 1), kTB), 64u));
   hipLaunchKernelGGL(vox_keys, dim3(kb, 2), dim3(kTB), 0, st, A, B, sc.partials.p, sc.s.k0.p, sc.s.v0.p,
-                     sc.overflow.p, sc.status.p, ntiles, sc.ticket.p, sc.rs.ctl.p, gate);
+                     sc.overflow.p, sc.status.p, ntiles, sc.ticket.p, sc.rs.ctl.p, gate, sc.overflow.p + 2);
   FLOAM_LAUNCH_CHECK();
-  radix_sort_launch(sc.rs, sc.s.k0.p, sc.s.v0.p, sc.s.k1.p, sc.s.v1.p, n, st, gate);   // sorted pairs in k0 / v0
-  hipLaunchKernelGGL(vox_compact, dim3(ntiles), dim3(kTB), 0, st, A, B, sc.s.k0.p, sc.s.v0.p, sc.overflow.p, n,
-                     sc.status.p, sc.ticket.p, sc.rs.ctl.p, gate);
+  // sorted pairs in k0 / v0; the passes and the compaction work on the packed device count
+  radix_sort_launch(sc.rs, sc.s.k0.p, sc.s.v0.p, sc.s.k1.p, sc.s.v1.p, n, st, gate, sc.overflow.p + 2);
+  hipLaunchKernelGGL(vox_compact, dim3(ntiles), dim3(kTB), 0, st, A, B, sc.s.k0.p, sc.s.v0.p, sc.overflow.p,
+                     sc.overflow.p + 2, sc.status.p, sc.ticket.p, sc.rs.ctl.p, gate);
   FLOAM_LAUNCH_CHECK();
 }
 
