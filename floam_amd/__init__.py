@@ -6,6 +6,7 @@ include/floam_c.h (libfloam_amd.so); this package is the host-side mirror of tho
 """
 from ._ffi import FloamError, load  # noqa: F401
 from .cloud import DeviceCloud  # noqa: F401
+from .imu import CenterTime, Compensate, ImuHandler, euler2Quaternion  # noqa: F401
 from .laser_processing import LaserProcessingClass, LidarParams  # noqa: F401
 from .odom_estimation import OdomEstimationClass, UpdateType  # noqa: F401
 from .synth import POINT_DTYPE  # noqa: F401

@@ -20,9 +20,11 @@ ERR_UNSUPPORTED = 4
 ERR_COMM = 5
 WARN_MAP_TOO_SMALL = 100
 WARN_FEW_CORRESPONDENCES = 101
+WARN_NO_IMU_DATA = 102
 
 STATUS_NAMES = {0: "OK", 1: "ERR_INVALID_ARGUMENT", 2: "ERR_DEVICE", 3: "ERR_OUT_OF_MEMORY", 4: "ERR_UNSUPPORTED",
-                5: "ERR_COMM", 100: "WARN_MAP_TOO_SMALL", 101: "WARN_FEW_CORRESPONDENCES"}
+                5: "ERR_COMM", 100: "WARN_MAP_TOO_SMALL", 101: "WARN_FEW_CORRESPONDENCES",
+                102: "WARN_NO_IMU_DATA"}
 
 # every entry point include/floam_c.h declares (checked by tests/test_abi.py)
 EXPORTS = [
@@ -37,6 +39,9 @@ EXPORTS = [
     "floam_comm_unique_id", "floam_odom_set_shard", "floam_odom_set_shard_callback",
     "floam_last_error", "floam_version", "floam_reset_process_state", "floam_device_synchronize",
     "floam_profile_enable", "floam_profile_read", "floam_profile_reset",
+    "floam_imu_create", "floam_imu_destroy", "floam_imu_add_msg", "floam_imu_add_msgs", "floam_imu_size",
+    "floam_imu_get", "floam_imu_time_contained", "floam_euler_to_quaternion", "floam_center_time",
+    "floam_imu_compensate", "floam_imu_preprocess",
 ]
 
 
@@ -83,6 +88,8 @@ def load(path: str | None = None):
     pp = C.POINTER(C.c_void_p)
     szp = C.POINTER(C.c_size_t)
     dp = C.POINTER(C.c_double)
+    ip = C.POINTER(C.c_int)
+    u64p = C.POINTER(C.c_uint64)
     sig = {
         "floam_cloud_create": [i32, sz, pp], "floam_cloud_destroy": [vp],
         "floam_cloud_upload": [vp, vp, sz, sz], "floam_cloud_download": [vp, vp, sz, szp],
@@ -101,6 +108,11 @@ def load(path: str | None = None):
         "floam_odom_set_shard_callback": [vp, i32, i32, ALLREDUCE_FN, vp],
         "floam_device_synchronize": [i32], "floam_profile_enable": [i32, i32],
         "floam_profile_read": [i32, C.POINTER(KernelTiming), i32, C.POINTER(C.c_int)], "floam_profile_reset": [i32],
+        "floam_imu_create": [i32, pp], "floam_imu_destroy": [vp], "floam_imu_add_msg": [vp, dbl, dp, ip],
+        "floam_imu_add_msgs": [vp, dp, dp, sz, szp], "floam_imu_size": [vp, szp],
+        "floam_imu_get": [vp, dbl, dp, ip], "floam_imu_time_contained": [vp, dbl, ip],
+        "floam_euler_to_quaternion": [dbl, dbl, dbl, dp], "floam_center_time": [vp, u64p],
+        "floam_imu_compensate": [vp, vp, C.c_uint64, dp, vp], "floam_imu_preprocess": [vp, vp, u64p, dp, vp],
     }
     for name, args in sig.items():
         f = getattr(L, name)

@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <cctype>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -26,6 +27,7 @@
 #include "cloud_ops.hpp"
 #include "fe.hpp"
 #include "floam_common.hpp"
+#include "imu.hpp"
 #include "odom_kernels.hpp"
 #include "pose.hpp"
 #include "voxel.hpp"
@@ -44,6 +46,8 @@ struct DeviceCtx {
   hipStream_t stream = nullptr;
   VoxelScratch2 vs;           // standalone floam_voxel_grid
   DevBuf<int> zero;           // a device 0 (empty second job)
+  DevBuf<int> ends;           // {count, front.time, back.time} read-back of the IMU pre-processing
+  HostBuf<int> h_ends;
   int profile = 0;   // bitmask of FLOAM_PROF_* categories
   std::vector<PendingTiming> pending;
   std::vector<hipEvent_t> free_events;
@@ -283,6 +287,17 @@ struct floam_odom {
   HostBuf<double> h_sums;
   floam_odom_stats stats{};
   floam_status last_warning = FLOAM_OK;
+};
+
+// dmapping::ImuHandler (include/dataHandler.h:31-66): the stamped orientation stream, host-side (AddMsg / Get /
+// TimeContained are scalar look-ups) with an append-only HBM mirror for the pre-processing kernel.
+struct floam_imu {
+  int device = 0;
+  std::vector<double> t;
+  std::vector<Q4> q;
+  double* d_t = nullptr;
+  Q4* d_q = nullptr;
+  size_t dcap = 0, uploaded = 0;
 };
 
 namespace {
@@ -1267,6 +1282,278 @@ floam_status floam_profile_read(int device, floam_kernel_timing* out, int max_en
     }
     if (n_out) *n_out = k;
     return FLOAM_OK;
+  });
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------------------------------ IMU pre-processing
+namespace {
+// pcl_conversions::fromPCL(stamp, ros::Time) (fromNSec(stamp * 1000)) + ros::Time::toSec()
+double pcl_stamp_to_sec(uint64_t stamp_us) {
+  const uint64_t ns = stamp_us * 1000ull;
+  return (double)(uint32_t)(ns / 1000000000ull) + 1e-9 * (double)(uint32_t)(ns % 1000000000ull);
+}
+// ros::Time(double) (roscpp_core fromSec: floor, round-half-away nanoseconds, carry) + pcl_conversions::toPCL
+// (toNSec() / 1000).  false where ros::Time throws (out of the dual 32-bit range): the stamp is then kept.
+bool sec_to_pcl_stamp(double t, uint64_t* stamp_us) {
+  const double fl = std::floor(t);
+  if (!(fl >= 0.0) || fl > 4294967295.0) return false;
+  uint32_t sec = (uint32_t)(int64_t)fl;
+  uint32_t nsec = (uint32_t)std::round((t - (double)sec) * 1e9);
+  sec += nsec / 1000000000ul;
+  nsec %= 1000000000ul;
+  *stamp_us = ((uint64_t)sec * 1000000000ull + (uint64_t)nsec) / 1000ull;
+  return true;
+}
+size_t imu_lower_bound(const floam_imu* h, double ts) {   // std::lower_bound with dmapping::compare
+  return (size_t)(std::lower_bound(h->t.begin(), h->t.end(), ts) - h->t.begin());
+}
+// ImuHandler::Get (src/dataHandler.cpp:48-75): the sample before the lower bound, or the zero orientation of a
+// default-constructed sensor_msgs::Imu
+bool imu_get(const floam_imu* h, double ts, Q4* out) {
+  const size_t a = imu_lower_bound(h, ts);
+  if (a != h->t.size() && a != 0 && a - 1 != 0) {
+    *out = h->q[a - 1];
+    return true;
+  }
+  *out = Q4{0.0, 0.0, 0.0, 0.0};
+  return false;
+}
+bool imu_time_contained(const floam_imu* h, double ts) {   // ImuHandler::TimeContained (:76-81)
+  return !h->t.empty() && ts >= h->t.front() && ts <= h->t.back();
+}
+bool imu_add(floam_imu* h, double stamp, const double* q) {   // ImuHandler::AddMsg (:23-38)
+  if (!h->t.empty() && !(stamp - h->t.back() > 0.00001)) return false;
+  h->t.push_back(stamp);
+  h->q.push_back(Q4{q[0], q[1], q[2], q[3]});
+  return true;
+}
+// bring the HBM mirror of the stream up to date (stream-ordered; the caller synchronises before returning)
+void imu_upload(floam_imu* h, hipStream_t st) {
+  const size_t n = h->t.size();
+  if (n > h->dcap) {
+    const size_t cap = std::max<size_t>(1024, n + n / 2);
+    double* nt = nullptr;
+    Q4* nq = nullptr;
+    FLOAM_HIP(hipMalloc(&nt, cap * sizeof(double)));
+    FLOAM_HIP(hipMalloc(&nq, cap * sizeof(Q4)));
+    if (h->uploaded) {
+      FLOAM_HIP(hipMemcpyAsync(nt, h->d_t, h->uploaded * sizeof(double), hipMemcpyDeviceToDevice, st));
+      FLOAM_HIP(hipMemcpyAsync(nq, h->d_q, h->uploaded * sizeof(Q4), hipMemcpyDeviceToDevice, st));
+      FLOAM_HIP(hipStreamSynchronize(st));
+    }
+    if (h->d_t) FLOAM_HIP(hipFree(h->d_t));
+    if (h->d_q) FLOAM_HIP(hipFree(h->d_q));
+    h->d_t = nt;
+    h->d_q = nq;
+    h->dcap = cap;
+  }
+  if (n > h->uploaded) {
+    FLOAM_HIP(hipMemcpyAsync(h->d_t + h->uploaded, h->t.data() + h->uploaded, (n - h->uploaded) * sizeof(double),
+                             hipMemcpyHostToDevice, st));
+    FLOAM_HIP(hipMemcpyAsync(h->d_q + h->uploaded, h->q.data() + h->uploaded, (n - h->uploaded) * sizeof(Q4),
+                             hipMemcpyHostToDevice, st));
+    h->uploaded = n;
+  }
+}
+
+// mode = OR of IMU_CENTER / IMU_COMPENSATE / IMU_ALIGN.  The scalar part (stamps, TimeContained, qInit, the LDS
+// window) runs on the host from the cloud's front / back times (one 12-B read-back); the per-point part is one
+// fused pass.  Returns false when Compensate would return false ("no imu data"); `in` is centred regardless.
+bool imu_pre(int mode, floam_imu* h, floam_cloud* in, uint64_t* stamp_us, const double* extr, floam_cloud* out) {
+  DeviceCtx& ctx = ctx_for(in->device);
+  hipStream_t st = ctx.stream;
+  FLOAM_HIP(hipSetDevice(in->device));
+  cloud_on_main(in);
+  if (out) cloud_on_main(out);
+  if (mode & IMU_COMPENSATE) imu_upload(h, st);
+  ctx.ends.reserve(3);
+  ctx.h_ends.reserve(3);
+  int* h_ends = ctx.h_ends.p;
+  cloud_ends_launch(in->pts.p, in->count.p, ctx.ends.p, st);
+  FLOAM_HIP(hipMemcpyAsync(h_ends, ctx.ends.p, sizeof(int) * 3, hipMemcpyDeviceToHost, st));
+  FLOAM_HIP(hipStreamSynchronize(st));
+  const int n = h_ends[0];
+  in->host_count = (size_t)std::max(n, 0);
+  in->host_count_valid = true;
+  if (n <= 0) return false;
+  float front, back;
+  std::memcpy(&front, &h_ends[1], 4);
+  std::memcpy(&back, &h_ends[2], 4);
+  ImuPrepArgs a{};
+  uint64_t stamp = *stamp_us;
+  if (mode & IMU_CENTER) {   // CenterTime (src/laserProcessingNode.cpp:65-78)
+    a.tScan = pcl_stamp_to_sec(stamp);
+    const double tEnd = a.tScan + (double)back;
+    const double tBegin = a.tScan + (double)front;
+    a.tCenter = tBegin + (tEnd - tBegin) / 2.0;
+    sec_to_pcl_stamp(a.tCenter, &stamp);
+    front = (float)(((double)front + a.tScan) - a.tCenter);
+    back = (float)(((double)back + a.tScan) - a.tCenter);
+  }
+  int launch_mode = mode;
+  bool ok = true;
+  if (mode & IMU_COMPENSATE) {   // dmapping::Compensate (src/dataHandler.cpp:93-122)
+    a.tScan2 = pcl_stamp_to_sec(stamp);
+    const double t0 = (double)front + a.tScan2, t1 = (double)back + a.tScan2;
+    if (!imu_time_contained(h, t0) || !imu_time_contained(h, t1)) {
+      ok = false;
+      launch_mode = mode & IMU_CENTER;
+    } else {
+      a.extr = Q4{extr[0], extr[1], extr[2], extr[3]};
+      Q4 qs;
+      imu_get(h, a.tScan2, &qs);
+      const Q4 qInit = q4_mul(qs, a.extr);
+      a.qInitInv = q4_inverse(qInit);
+      const double qv[4] = {qInit.x, qInit.y, qInit.z, qInit.w};
+      const Mat3 R = quat_to_mat(qv);   // Eigen::Affine3d ImuNowT(q) (:109-110), translation 0
+      for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) a.R[3 * r + c] = R.m[r][c];
+      a.stamps = h->d_t;
+      a.orient = h->d_q;
+      a.n_imu = (int)h->t.size();
+      const size_t lb0 = imu_lower_bound(h, std::min(t0, t1)), lb1 = imu_lower_bound(h, std::max(t0, t1));
+      a.win_lo = (int)(lb0 > 0 ? lb0 - 1 : 0);
+      a.win_hi = (int)std::min(h->t.size(), lb1 + 1);
+      a.win_hi = std::min(a.win_hi, a.win_lo + kImuWindow);
+    }
+  }
+  if (launch_mode & IMU_COMPENSATE) {
+    cloud_reserve(out, (size_t)n, 0, st);
+    ProfScope ps(ctx, "imu_preprocess", FLOAM_PROF_CLOUD, 68.0 * (double)n);
+    imu_prep_launch(launch_mode, in->pts.p, out->pts.p, in->count.p, n, a, st);
+    FLOAM_HIP(hipMemcpyAsync(out->count.p, in->count.p, sizeof(int), hipMemcpyDeviceToDevice, st));
+    out->host_count = (size_t)n;
+    out->host_count_valid = true;
+  } else if (launch_mode & IMU_CENTER) {
+    ProfScope ps(ctx, "center_time", FLOAM_PROF_CLOUD, 36.0 * (double)n);
+    imu_prep_launch(IMU_CENTER, in->pts.p, nullptr, in->count.p, n, a, st);
+  }
+  *stamp_us = stamp;
+  return ok;
+}
+}  // namespace
+
+extern "C" {
+
+floam_status floam_imu_create(int device, floam_imu** out) {
+  return guarded([&] {
+    if (!out) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null out");
+    ctx_for(device);
+    auto h = std::make_unique<floam_imu>();
+    h->device = device;
+    *out = h.release();
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_imu_destroy(floam_imu* h) {
+  return guarded([&] {
+    if (h) {
+      FLOAM_HIP(hipStreamSynchronize(ctx_for(h->device).stream));
+      if (h->d_t) FLOAM_HIP(hipFree(h->d_t));
+      if (h->d_q) FLOAM_HIP(hipFree(h->d_q));
+      delete h;
+    }
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_imu_add_msg(floam_imu* h, double stamp, const double q_xyzw[4], int* added) {
+  return guarded([&] {
+    if (!h || !q_xyzw) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
+    const bool a = imu_add(h, stamp, q_xyzw);
+    if (added) *added = a ? 1 : 0;
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_imu_add_msgs(floam_imu* h, const double* stamps, const double* q_xyzw, size_t n, size_t* added) {
+  return guarded([&] {
+    if (!h || (n && (!stamps || !q_xyzw))) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
+    size_t k = 0;
+    for (size_t i = 0; i < n; ++i) k += imu_add(h, stamps[i], q_xyzw + 4 * i) ? 1 : 0;
+    if (added) *added = k;
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_imu_size(const floam_imu* h, size_t* n) {
+  return guarded([&] {
+    if (!h || !n) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
+    *n = h->t.size();
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_imu_get(const floam_imu* h, double t, double q_xyzw[4], int* found) {
+  return guarded([&] {
+    if (!h || !q_xyzw) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
+    Q4 q;
+    const bool f = imu_get(h, t, &q);
+    q_xyzw[0] = q.x; q_xyzw[1] = q.y; q_xyzw[2] = q.z; q_xyzw[3] = q.w;
+    if (found) *found = f ? 1 : 0;
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_imu_time_contained(const floam_imu* h, double t, int* contained) {
+  return guarded([&] {
+    if (!h || !contained) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
+    *contained = imu_time_contained(h, t) ? 1 : 0;
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_euler_to_quaternion(double roll, double pitch, double yaw, double q_xyzw[4]) {
+  return guarded([&] {
+    if (!q_xyzw) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
+    auto aa = [](double deg, int axis) {   // AngleAxisd(deg * M_PI / 180.0, Unit*()) -> Quaterniond
+      const double ha = 0.5 * (deg * M_PI / 180.0);
+      const double s = std::sin(ha);
+      Q4 q{0.0 * s, 0.0 * s, 0.0 * s, std::cos(ha)};
+      if (axis == 0) q.x = 1.0 * s;
+      if (axis == 1) q.y = 1.0 * s;
+      if (axis == 2) q.z = 1.0 * s;
+      return q;
+    };
+    const Q4 q = q4_mul(q4_mul(aa(roll, 0), aa(yaw, 2)), aa(pitch, 1));   // rollAngle * yawAngle * pitchAngle
+    q_xyzw[0] = q.x; q_xyzw[1] = q.y; q_xyzw[2] = q.z; q_xyzw[3] = q.w;
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_center_time(floam_cloud* cloud, uint64_t* stamp_us) {
+  return guarded([&] {
+    if (!cloud || !stamp_us) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
+    imu_pre(IMU_CENTER, nullptr, cloud, stamp_us, nullptr, nullptr);
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_imu_compensate(floam_imu* h, floam_cloud* in, uint64_t stamp_us, const double extr_xyzw[4],
+                                  floam_cloud* compensated) {
+  return guarded([&] {
+    if (!h || !in || !extr_xyzw || !compensated) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
+    if (in == compensated) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "clouds must be distinct");
+    if (in->device != h->device || compensated->device != h->device)
+      throw Error(FLOAM_ERR_INVALID_ARGUMENT, "clouds and handle on different devices");
+    uint64_t st = stamp_us;
+    return imu_pre(IMU_COMPENSATE, h, in, &st, extr_xyzw, compensated) ? FLOAM_OK : FLOAM_WARN_NO_IMU_DATA;
+  });
+}
+
+floam_status floam_imu_preprocess(floam_imu* h, floam_cloud* in, uint64_t* stamp_us, const double extr_xyzw[4],
+                                  floam_cloud* aligned) {
+  return guarded([&] {
+    if (!h || !in || !stamp_us || !extr_xyzw || !aligned) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
+    if (in == aligned) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "clouds must be distinct");
+    if (in->device != h->device || aligned->device != h->device)
+      throw Error(FLOAM_ERR_INVALID_ARGUMENT, "clouds and handle on different devices");
+    return imu_pre(IMU_CENTER | IMU_COMPENSATE | IMU_ALIGN, h, in, stamp_us, extr_xyzw, aligned)
+               ? FLOAM_OK
+               : FLOAM_WARN_NO_IMU_DATA;
   });
 }
 

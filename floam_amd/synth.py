@@ -255,3 +255,54 @@ def to_xyzi(pts: np.ndarray) -> np.ndarray:
         out[f] = pts[f]
     out["pad0"] = 1.0
     return out
+
+
+# ----------------------------------------------------------------------------------------------- IMU stream
+EPOCH = 1_700_000_000.0   # absolute time of scan 0's centre (s); ROS stamps are absolute
+
+
+def _quat_mul(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    """Hamilton product of (..., 4) quaternions in (x, y, z, w) order (generator only, not a reference formula)."""
+    ax, ay, az, aw = np.moveaxis(a, -1, 0)
+    bx, by, bz, bw = np.moveaxis(b, -1, 0)
+    return np.stack([aw * bx + ax * bw + ay * bz - az * by, aw * by - ax * bz + ay * bw + az * bx,
+                     aw * bz + ax * by - ay * bx + az * bw, aw * bw - ax * bx - ay * by - az * bz], axis=-1)
+
+
+def imu_stream(t_begin: float, t_end: float, rate: float = 200.0, extrinsics_xyzw=(0.0, 0.0, 1.0, 0.0),
+               wobble_deg: float = 1.5, seed: int = 11):
+    """IMU messages (stamps, orientations (n, 4) x,y,z,w) covering [t_begin, t_end] (seconds relative to EPOCH).
+
+    The orientation is the ground-truth sensor yaw plus a slow roll/pitch wobble, expressed so that
+    q_imu * extrinsics = q_sensor (the node composes Imu2Orientation(...) * extrinsics, src/dataHandler.cpp:108,112).
+    Stamps are absolute (EPOCH + t) with a small seeded jitter; one duplicated stamp is injected to exercise
+    AddMsg's de-duplication (src/dataHandler.cpp:23-38)."""
+    rng = np.random.default_rng(seed)
+    n = int(math.ceil((t_end - t_begin) * rate)) + 1
+    t = t_begin + np.arange(n) / rate + rng.uniform(-0.1, 0.1, n) / rate
+    yaw = YAW_RATE * t
+    roll = np.radians(wobble_deg) * np.sin(2.0 * math.pi * 0.7 * t)
+    pitch = np.radians(wobble_deg) * np.cos(2.0 * math.pi * 0.45 * t)
+    def axis_q(ang, k):
+        q = np.zeros((ang.shape[0], 4))
+        q[:, k] = np.sin(0.5 * ang)
+        q[:, 3] = np.cos(0.5 * ang)
+        return q
+    q_sensor = _quat_mul(_quat_mul(axis_q(yaw, 2), axis_q(pitch, 1)), axis_q(roll, 0))
+    e = np.asarray(extrinsics_xyzw, dtype=np.float64)
+    e_inv = np.array([-e[0], -e[1], -e[2], e[3]]) / float(e @ e)
+    q_imu = _quat_mul(q_sensor, np.broadcast_to(e_inv, q_sensor.shape))
+    stamps = EPOCH + t
+    if n > 4:
+        stamps[n // 2] = stamps[n // 2 - 1]   # a duplicate the handler must drop
+    return stamps, q_imu
+
+
+def driver_scan(config: str, scan_idx: int):
+    """A scan as the driver publishes it: point times from the start of the sweep (0 .. 0.1 s) and the header
+    stamp at the sweep start, in PCL microseconds — the input CenterTime (src/laserProcessingNode.cpp:65-78)
+    re-centres.  Returns (points, stamp_us)."""
+    pts = generate_scan(config, scan_idx)
+    pts["time"] = (pts["time"].astype(np.float64) + 0.5 * SCAN_PERIOD).astype(np.float32)
+    stamp_us = int(round((EPOCH + scan_idx * SCAN_PERIOD - 0.5 * SCAN_PERIOD) * 1e6))
+    return pts, stamp_us

@@ -33,7 +33,8 @@ typedef enum floam_status {
   FLOAM_ERR_COMM = 5,          /* RCCL failure in the sharded path */
   /* non-fatal, same conditions as the reference's printf warnings */
   FLOAM_WARN_MAP_TOO_SMALL = 100,       /* src/odomEstimationClass.cpp:112 "not enough points in map" */
-  FLOAM_WARN_FEW_CORRESPONDENCES = 101  /* src/odomEstimationClass.cpp:192-194, 247-249 (< 20 factors) */
+  FLOAM_WARN_FEW_CORRESPONDENCES = 101, /* src/odomEstimationClass.cpp:192-194, 247-249 (< 20 factors) */
+  FLOAM_WARN_NO_IMU_DATA = 102          /* src/dataHandler.cpp:101-104 "no imu data" (Compensate returns false) */
 } floam_status;
 
 /* 32-byte point record, byte-compatible with vel_point::PointXYZIRT (include/lidar.h:14-32) and with
@@ -96,6 +97,45 @@ floam_status floam_voxel_grid(const floam_cloud* in, float leaf, floam_cloud* ou
  * consumes them, or by floam_lp_wait. */
 floam_status floam_lp_set_async(floam_lp* lp, int async);
 floam_status floam_lp_wait(floam_lp* lp);
+
+/* ------------------------------------------------------------------------------- IMU pre-processing */
+/* The laser-processing node's steps before featureExtraction (src/laserProcessingNode.cpp:92-120; SURVEY.md §8
+ * f-2).  Quaternions are (x, y, z, w), the coefficient order of Eigen::Quaterniond and of
+ * sensor_msgs::Imu::orientation.  Stamps are seconds (ros::Time::toSec()); cloud stamps are PCL header stamps in
+ * microseconds (pcl::PCLHeader::stamp). */
+typedef struct floam_imu floam_imu;
+
+/* dmapping::ImuHandler() (include/dataHandler.h:35) on `device` */
+floam_status floam_imu_create(int device, floam_imu** out);
+floam_status floam_imu_destroy(floam_imu* h);
+/* ImuHandler::AddMsg (src/dataHandler.cpp:23-38): appended iff the handler is empty or stamp > last + 1e-5 s.
+ * Only the orientation is kept (Imu2Orientation, :7-9, is the only accessor the path uses). *added may be NULL. */
+floam_status floam_imu_add_msg(floam_imu* h, double stamp, const double orientation_xyzw[4], int* added);
+floam_status floam_imu_add_msgs(floam_imu* h, const double* stamps, const double* orientations_xyzw, size_t n,
+                                size_t* added);
+floam_status floam_imu_size(const floam_imu* h, size_t* n);
+/* ImuHandler::Get (src/dataHandler.cpp:48-75): the sample before std::lower_bound(stamp) (no interpolation, :45-47);
+ * not found -> *found = 0 and the zero orientation of a default-constructed sensor_msgs::Imu. */
+floam_status floam_imu_get(const floam_imu* h, double stamp, double orientation_xyzw[4], int* found);
+/* ImuHandler::TimeContained (src/dataHandler.cpp:76-81) */
+floam_status floam_imu_time_contained(const floam_imu* h, double stamp, int* contained);
+/* euler2Quaternion(roll, pitch, yaw) in degrees (src/lidar.cpp:8-16): AngleAxis roll * yaw * pitch */
+floam_status floam_euler_to_quaternion(double roll, double pitch, double yaw, double q_xyzw[4]);
+/* CenterTime(cloud) (src/laserProcessingNode.cpp:65-78): point times re-referenced to the centre of
+ * [front.time, back.time] in place; *stamp_us is replaced by the centre stamp (microsecond PCL stamp).  One 12-B
+ * read-back of the cloud's ends; an empty cloud is left untouched (points.back() of an empty cloud is UB there). */
+floam_status floam_center_time(floam_cloud* cloud, uint64_t* stamp_us);
+/* dmapping::Compensate(input, compensated, handler, extrinsics) (src/dataHandler.cpp:93-122): every point rotated by
+ * (q(Get(stamp)) * extr)^-1 * (q(Get(stamp + time)) * extr).  Returns FLOAM_WARN_NO_IMU_DATA (the reference returns
+ * false) when the front or back point time is outside the IMU stream; `compensated` is then left unchanged. */
+floam_status floam_imu_compensate(floam_imu* h, floam_cloud* in, uint64_t stamp_us, const double extrinsics_xyzw[4],
+                                  floam_cloud* compensated);
+/* The node's whole sequence, fused into one pass (src/laserProcessingNode.cpp:92-113): CenterTime(in) (in place,
+ * *stamp_us updated), Compensate, then pcl::transformPointCloud by Eigen::Affine3d(q(Get(stamp)) * extr) into
+ * `aligned`, the cloud featureExtraction receives.  FLOAM_WARN_NO_IMU_DATA: the node's "cannot compensate" skip
+ * (:104-107); `in` is centred regardless and `aligned` is unchanged. */
+floam_status floam_imu_preprocess(floam_imu* h, floam_cloud* in, uint64_t* stamp_us, const double extrinsics_xyzw[4],
+                                  floam_cloud* aligned);
 
 /* -------------------------------------------------------------------------------- OdomEstimationClass */
 typedef struct floam_odom floam_odom;

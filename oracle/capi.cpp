@@ -125,4 +125,42 @@ double oracle_surf_residual(const double* cp, const double* n, double d, const d
 }
 void oracle_se3_plus(const double* x, const double* delta, double* out) { test_se3_plus(x, delta, out); }
 
+// ---- IMU pre-processing (oracle/imu.cpp).  Quaternions are (x, y, z, w); handler data is passed as arrays.
+static ImuHandler make_handler(const double* stamps, const double* q_xyzw, size_t m) {
+  ImuHandler h;
+  for (size_t i = 0; i < m; ++i)
+    h.add_msg(stamps[i], Quat{q_xyzw[4 * i], q_xyzw[4 * i + 1], q_xyzw[4 * i + 2], q_xyzw[4 * i + 3]});
+  return h;
+}
+// AddMsg over a message stream: keep[i] = 1 if message i was appended
+size_t oracle_imu_filter(const double* stamps, size_t m, unsigned char* keep) {
+  ImuHandler h;
+  for (size_t i = 0; i < m; ++i) keep[i] = h.add_msg(stamps[i], Quat{0, 0, 0, 1}) ? 1 : 0;
+  return h.t.size();
+}
+int oracle_imu_get(const double* stamps, const double* q_xyzw, size_t m, double ts, double* out_xyzw) {
+  const ImuHandler h = make_handler(stamps, q_xyzw, m);
+  const Quat r = h.get_or_zero(ts);
+  out_xyzw[0] = r.x; out_xyzw[1] = r.y; out_xyzw[2] = r.z; out_xyzw[3] = r.w;
+  Quat tmp;
+  return h.get(ts, &tmp) ? 1 : 0;
+}
+int oracle_imu_time_contained(const double* stamps, const double* q_xyzw, size_t m, double ts) {
+  return make_handler(stamps, q_xyzw, m).time_contained(ts) ? 1 : 0;
+}
+void oracle_euler_to_quaternion(double roll, double pitch, double yaw, double* out_xyzw) {
+  const Quat q = euler_to_quaternion(roll, pitch, yaw);
+  out_xyzw[0] = q.x; out_xyzw[1] = q.y; out_xyzw[2] = q.z; out_xyzw[3] = q.w;
+}
+void oracle_center_time(void* pts, size_t n, uint64_t* stamp_us) { center_time(static_cast<Pt*>(pts), n, stamp_us); }
+// mode 2: Compensate only (in untouched); mode 7: the node's CenterTime + Compensate + alignment (in centred)
+int oracle_imu_preprocess(int mode, void* in, size_t n, uint64_t* stamp_us, const double* stamps,
+                          const double* q_xyzw, size_t m, const double* extr_xyzw, void* out) {
+  const ImuHandler h = make_handler(stamps, q_xyzw, m);
+  const Quat e{extr_xyzw[0], extr_xyzw[1], extr_xyzw[2], extr_xyzw[3]};
+  Pt* p = static_cast<Pt*>(in);
+  if (mode == 2) return compensate(p, n, *stamp_us, h, e, static_cast<Pt*>(out)) ? 1 : 0;
+  return imu_preprocess(p, n, stamp_us, h, e, static_cast<Pt*>(out)) ? 1 : 0;
+}
+
 }  // extern "C"

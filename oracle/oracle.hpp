@@ -23,6 +23,8 @@
 #include <string>
 #include <vector>
 
+#include "la.hpp"
+
 namespace oracle {
 
 // vel_point::PointXYZIRT (include/lidar.h:14-32) — 32 B, EIGEN_ALIGN16.  pcl::PointXYZI has x,y,z,intensity at the
@@ -112,6 +114,27 @@ const Pt* odom_map_data(const OdomState*, int which);
 const std::vector<SolveTrace>& odom_traces(const OdomState*);
 void odom_clear_traces(OdomState*);
 int odom_optimization_count(const OdomState*);
+// ---------------------------------------------------------------------------------------------- IMU pre-processing
+// (oracle/imu.cpp).  Quat is Eigen's (x, y, z, w) order (la.hpp).
+struct ImuHandler {                       // dmapping::ImuHandler (include/dataHandler.h:31-66), orientation only
+  std::vector<double> t;
+  std::vector<Quat> q;
+  bool add_msg(double stamp, const Quat& orientation);
+  size_t lower_bound(double ts) const;
+  bool get(double ts, Quat* out) const;
+  Quat get_or_zero(double ts) const;
+  bool time_contained(double ts) const;
+};
+Quat qmul_sse2(const Quat& a, const Quat& b);
+Quat qinverse(const Quat& q);
+Quat euler_to_quaternion(double roll, double pitch, double yaw);
+double pcl_stamp_to_sec(uint64_t stamp_us);
+bool sec_to_pcl_stamp(double t, uint64_t* stamp_us);
+void center_time(Pt* pts, size_t n, uint64_t* stamp_us);
+bool compensate(const Pt* in, size_t n, uint64_t stamp_us, const ImuHandler& h, const Quat& extr, Pt* out);
+void transform_by_quaternion(const Pt* in, size_t n, const Quat& q, Pt* out);
+bool imu_preprocess(Pt* in, size_t n, uint64_t* stamp_us, const ImuHandler& h, const Quat& extr, Pt* out);
+
 void reset_process_statics();   // KeyFrameUpdate's function-static `first` (odomEstimationClass.cpp:323, Q6)
 double test_edge_eval(const double cp[3], const double a[3], const double b[3], const double* x, double* J);
 double test_surf_eval(const double cp[3], const double n[3], double d, const double* x, double* J);

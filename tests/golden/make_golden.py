@@ -8,6 +8,11 @@ generator's transcendental ufuncs may differ by an ulp across CPUs).  Inputs AND
 fe_tiny.npz   a 16x400 synthetic scan + the indices (into the input) of featureExtraction's edge / surf outputs
 odom_c1.npz   4 consecutive VLP-16-style scans (scan 0 seeds the map) + per-scan poses, map sizes and per-solve
               correspondence counts / costs of OdomEstimationClass::UpdatePointsToMapSelector (deskew on)
+imu_c1.npz    a 16x400 driver-style scan (times from the sweep start) + an IMU stream + extrinsics, and the node's
+              CenterTime + Compensate + IMU alignment outputs (centred input, aligned cloud, centred stamp) as raw
+              32-B records
+
+Usage: python tests/golden/make_golden.py [fe] [odom] [imu]   (default: all)
 """
 import os
 import sys
@@ -68,7 +73,24 @@ def make_odom():
     print("odom_c1:", n, "scans, final pose", np.array(poses[-1]).round(5).tolist())
 
 
+def make_imu():
+    pts, stamp_us = synth.driver_scan("tiny16x400", 1)
+    stamps, q = synth.imu_stream(-0.5, 0.6, rate=200.0)
+    extr = oracle.euler_to_quaternion(0, 0, 180)
+    ok, centred, aligned, stamp2 = oracle.imu_preprocess(pts, stamp_us, stamps, q, extr)
+    assert ok
+    np.savez_compressed(os.path.join(OUT, "imu_c1.npz"), input=pts.view(np.uint8), stamp_us=np.uint64(stamp_us),
+                        imu_stamps=stamps, imu_q=q, extrinsics=extr, centred=centred.view(np.uint8),
+                        aligned=aligned.view(np.uint8), stamp_out_us=np.uint64(stamp2))
+    print("imu_c1:", pts.shape[0], "pts,", stamps.shape[0], "IMU messages, stamp", stamp_us, "->", stamp2)
+
+
 if __name__ == "__main__":
     oracle.build()
-    make_fe()
-    make_odom()
+    which = set(sys.argv[1:]) or {"fe", "odom", "imu"}
+    if "fe" in which:
+        make_fe()
+    if "odom" in which:
+        make_odom()
+    if "imu" in which:
+        make_imu()
