@@ -90,8 +90,6 @@ def main():
     ap.add_argument("--mode", choices=["shard", "replica"], default="shard")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-roofline", action="store_true")
-    ap.add_argument("--knn-detail", action="store_true", help="also time the search and geometry launches separately "
-                    "(extra events inside the timed region)")
     ap.add_argument("--json-out", default="")
     args = ap.parse_args()
 
@@ -227,37 +225,36 @@ def main():
     if not args.no_roofline:
         odo.close()
         lp.close()
-        # The dominant kernel's launch durations and algorithmic bytes: an identical replay of the same sequence
-        # (the pipeline is deterministic; the poses are checked bit for bit) with HIP events around each
-        # correspondence launch (FLOAM_PROF_KNN, + FLOAM_PROF_KNN_DETAIL: per kernel) and the byte-counting kernel
-        # after it (FLOAM_PROF_KNN_BYTES).  Profiling issues the updates launch by launch: the timed run above
-        # replays each update as one hipGraph, and timing events recorded inside a graph cannot be read back on
-        # this ROCm (hipEventElapsedTime fails for them).
+        # The dominant kernel — the exact 5-NN search (knn_kernel, edge + surf queries in one launch) — measured on an
+        # identical replay of the same sequence (the pipeline is deterministic; the poses are checked bit for bit):
+        # HIP events on the library stream around every search launch (FLOAM_PROF_KNN_DETAIL) and the byte-counting
+        # kernel after each pass (FLOAM_PROF_KNN_BYTES, SURVEY.md §8 d).  Profiling issues the updates launch by
+        # launch: the timed run above replays each update as one hipGraph, and timing events recorded inside a graph
+        # cannot be read back on this ROCm (hipEventElapsedTime fails for them).
         lp, odo = make_pipeline()
         replay = []
         run(lp, odo, 0, args.warmup, replay)
         _ffi.check(L.floam_profile_reset(dev))
-        _ffi.check(L.floam_profile_enable(dev, 1 | 16 | (32 if args.knn_detail else 0)))
+        _ffi.check(L.floam_profile_enable(dev, 1 | 16 | 32))
         run(lp, odo, args.warmup, n_scans, replay)
         _ffi.check(L.floam_profile_enable(dev, 0))
-        counted = read_timings()
-        timed = counted
+        timed = read_timings()
         same = all(np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) for a, b in zip(poses, replay))
-        kt, kb = timed.get("knn"), counted.get("knn")
-        if kt is not None and kt[0] > 0 and kb is not None:
+        kt = timed.get("knn_search")
+        if kt is not None and kt[0] > 0:
             avg_ms = kt[1] / kt[0]
-            bytes_per = kb[2] / kt[0]
+            bytes_per = kt[2] / kt[0]
             ach = bytes_per / (avg_ms * 1e-3) / 1e9
-            traffic, traffic_src = hbm_traffic("corr_kernel(")
+            traffic, traffic_src = hbm_traffic("knn_kernel<")
             roof = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": traffic_src,
-                    "kernel": "corr_kernel (edge + surf kNN, line / plane geometry)", "avg_us": round(avg_ms * 1e3, 2),
-                    "launches": int(kt[0]), "algorithmic_bytes_per_launch": round(bytes_per),
-                    "replay_bitwise_identical": bool(same)}
-            for sub in ("knn_search", "knn_geometry"):
+                    "kernel": "knn_kernel (exact 5-NN search over the hash grid, edge + surf queries)",
+                    "avg_us": round(avg_ms * 1e3, 2), "launches": int(kt[0]),
+                    "algorithmic_bytes_per_launch": round(bytes_per), "replay_bitwise_identical": bool(same)}
+            for sub in ("knn", "knn_geometry"):
                 ks = timed.get(sub)
                 if ks is not None and ks[0]:
-                    roof[sub + "_avg_us"] = round(ks[1] / ks[0] * 1e3, 2)
+                    roof[("correspondence_pass" if sub == "knn" else sub) + "_avg_us"] = round(ks[1] / ks[0] * 1e3, 2)
 
     cpu = None
     pose_err = None

@@ -21,10 +21,11 @@ ERR_COMM = 5
 WARN_MAP_TOO_SMALL = 100
 WARN_FEW_CORRESPONDENCES = 101
 WARN_NO_IMU_DATA = 102
+WARN_FIELD_MISSING = 103
 
 STATUS_NAMES = {0: "OK", 1: "ERR_INVALID_ARGUMENT", 2: "ERR_DEVICE", 3: "ERR_OUT_OF_MEMORY", 4: "ERR_UNSUPPORTED",
                 5: "ERR_COMM", 100: "WARN_MAP_TOO_SMALL", 101: "WARN_FEW_CORRESPONDENCES",
-                102: "WARN_NO_IMU_DATA"}
+                102: "WARN_NO_IMU_DATA", 103: "WARN_FIELD_MISSING"}
 
 # every entry point include/floam_c.h declares (checked by tests/test_abi.py)
 EXPORTS = [
@@ -42,6 +43,7 @@ EXPORTS = [
     "floam_imu_create", "floam_imu_destroy", "floam_imu_add_msg", "floam_imu_add_msgs", "floam_imu_size",
     "floam_imu_get", "floam_imu_time_contained", "floam_euler_to_quaternion", "floam_center_time",
     "floam_imu_compensate", "floam_imu_preprocess",
+    "floam_pointcloud2_fields", "floam_cloud_from_pointcloud2", "floam_transform_cloud",
 ]
 
 
@@ -64,6 +66,11 @@ class OdomStats(C.Structure):
 
 
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.c_int, C.c_void_p)
+
+
+class PC2Field(C.Structure):
+    """floam_pc2_field == sensor_msgs/PointField (name, offset, datatype, count)."""
+    _fields_ = [("name", C.c_char * 32), ("offset", C.c_uint32), ("datatype", C.c_uint8), ("count", C.c_uint32)]
 
 
 class KernelTiming(C.Structure):
@@ -113,6 +120,10 @@ def load(path: str | None = None):
         "floam_imu_get": [vp, dbl, dp, ip], "floam_imu_time_contained": [vp, dbl, ip],
         "floam_euler_to_quaternion": [dbl, dbl, dbl, dp], "floam_center_time": [vp, u64p],
         "floam_imu_compensate": [vp, vp, C.c_uint64, dp, vp], "floam_imu_preprocess": [vp, vp, u64p, dp, vp],
+        "floam_pointcloud2_fields": [i32, C.POINTER(PC2Field), sz, szp, C.POINTER(C.c_uint32)],
+        "floam_cloud_from_pointcloud2": [vp, i32, vp, sz, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                         C.POINTER(PC2Field), sz],
+        "floam_transform_cloud": [vp, dp, vp],
     }
     for name, args in sig.items():
         f = getattr(L, name)

@@ -27,6 +27,7 @@
 #include "cloud_ops.hpp"
 #include "fe.hpp"
 #include "floam_common.hpp"
+#include "formats.hpp"
 #include "imu.hpp"
 #include "odom_kernels.hpp"
 #include "pose.hpp"
@@ -47,6 +48,7 @@ struct DeviceCtx {
   VoxelScratch2 vs;           // standalone floam_voxel_grid
   DevBuf<int> zero;           // a device 0 (empty second job)
   DevBuf<int> ends;           // {count, front.time, back.time} read-back of the IMU pre-processing
+  DevBuf<uint8_t> msg;        // staged PointCloud2 bytes (floam_cloud_from_pointcloud2)
   HostBuf<int> h_ends;
   int profile = 0;   // bitmask of FLOAM_PROF_* categories
   std::vector<PendingTiming> pending;
@@ -419,9 +421,9 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
                   gram ? o->gpart.p : nullptr, gram ? o->gmat.p : nullptr, o->gcnt.p, st);
     }
     if (ctx.profile & FLOAM_PROF_KNN_BYTES) {   // replay only: algorithmic bytes of the two launches above
-      knn_traffic_launch(o->lm.p, qe, o->gE, o->mapE.pts.p, o->ce, 8 * EDGE_FIELDS, o->rank, o->world, o->traffic_set,
+      knn_traffic_launch(o->lm.p, qe, o->gE, o->mapE.pts.p, o->ce, o->rank, o->world, o->traffic_set,
                          o->prof_bytes.p + 0, st);
-      knn_traffic_launch(o->lm.p, qs, o->gS, o->mapS.pts.p, o->cs, 8 * SURF_FIELDS, o->rank, o->world, o->traffic_set,
+      knn_traffic_launch(o->lm.p, qs, o->gS, o->mapS.pts.p, o->cs, o->rank, o->world, o->traffic_set,
                          o->prof_bytes.p + 1, st);
     }
     // iteration zero + at most max_num_iterations = 4 candidates (odomEstimationClass.cpp:102)
@@ -492,8 +494,8 @@ floam_status odom_collect_one(floam_odom* o, DeviceCtx& ctx) {
   for (int k = 0; k < P.nslots; ++k) {
     const UpdateStatus& U = slots[k];
     if (ctx.profile & FLOAM_PROF_KNN_BYTES) {
-      floam_kernel_timing& t = ctx.totals["knn"];
-      std::strncpy(t.name, "knn", sizeof(t.name) - 1);
+      floam_kernel_timing& t = ctx.totals["knn_search"];   // the search kernel's algorithmic bytes (knn_traffic)
+      std::strncpy(t.name, "knn_search", sizeof(t.name) - 1);
       t.algorithmic_bytes += (double)U.prof[0] + (double)U.prof[1];
     }
     if (U.lm.n_res < 0)
@@ -1554,6 +1556,150 @@ floam_status floam_imu_preprocess(floam_imu* h, floam_cloud* in, uint64_t* stamp
     return imu_pre(IMU_CENTER | IMU_COMPENSATE | IMU_ALIGN, h, in, stamp_us, extr_xyzw, aligned)
                ? FLOAM_OK
                : FLOAM_WARN_NO_IMU_DATA;
+  });
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------------------------------ wire formats
+namespace {
+struct FieldDesc {   // the registered fields of the point type (POINT_CLOUD_REGISTER_POINT_STRUCT order)
+  const char* name;
+  uint32_t offset;
+  uint8_t datatype;
+  uint32_t count;
+};
+// vel_point::PointXYZIRT (include/lidar.h:26-32) and pcl::PointXYZI
+const FieldDesc kXYZIRT[] = {{"x", 0, 7, 1}, {"y", 4, 7, 1}, {"z", 8, 7, 1},
+                             {"intensity", 16, 7, 1}, {"ring", 20, 4, 1}, {"time", 24, 7, 1}};
+const FieldDesc kXYZI[] = {{"x", 0, 7, 1}, {"y", 4, 7, 1}, {"z", 8, 7, 1}, {"intensity", 16, 7, 1}};
+size_t field_bytes(uint8_t dt) { return dt == 4 ? 2 : 4; }   // sizeof the struct member type (uint16 / float)
+}  // namespace
+
+extern "C" {
+
+floam_status floam_pointcloud2_fields(int point_type, floam_pc2_field* out, size_t capacity, size_t* n_out,
+                                      uint32_t* point_step) {
+  return guarded([&] {
+    if (point_type != FLOAM_POINT_XYZIRT && point_type != FLOAM_POINT_XYZI)
+      throw Error(FLOAM_ERR_INVALID_ARGUMENT, "unknown point type");
+    const FieldDesc* f = point_type == FLOAM_POINT_XYZIRT ? kXYZIRT : kXYZI;
+    const size_t n = point_type == FLOAM_POINT_XYZIRT ? 6 : 4;
+    for (size_t i = 0; i < n && i < capacity && out; ++i) {
+      std::memset(&out[i], 0, sizeof(out[i]));
+      std::strncpy(out[i].name, f[i].name, sizeof(out[i].name) - 1);
+      out[i].offset = f[i].offset;
+      out[i].datatype = f[i].datatype;
+      out[i].count = f[i].count;
+    }
+    if (n_out) *n_out = n;
+    if (point_step) *point_step = (uint32_t)sizeof(PointRec);
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_cloud_from_pointcloud2(floam_cloud* out, int point_type, const void* data, size_t data_size,
+                                          uint32_t width, uint32_t height, uint32_t point_step, uint32_t row_step,
+                                          const floam_pc2_field* fields, size_t nfields) {
+  return guarded([&] {
+    if (!out || (nfields && !fields)) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
+    if (point_type != FLOAM_POINT_XYZIRT && point_type != FLOAM_POINT_XYZI)
+      throw Error(FLOAM_ERR_INVALID_ARGUMENT, "unknown point type");
+    const size_t n = (size_t)width * height;
+    if (n > (size_t)INT32_MAX) throw Error(FLOAM_ERR_UNSUPPORTED, "cloud larger than 2^31 points");
+    if (n && !data) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null data");
+    if (n && ((size_t)(height - 1) * row_step + (size_t)(width - 1) * point_step + point_step > data_size))
+      throw Error(FLOAM_ERR_INVALID_ARGUMENT, "data smaller than height * row_step");
+    // detail::FieldMapper (PCL 1.8.1 conversions.h): per registered field, the first message field with the same
+    // name, datatype and count (count 0 accepted for scalars); missing fields only warn (#595)
+    const FieldDesc* f = point_type == FLOAM_POINT_XYZIRT ? kXYZIRT : kXYZI;
+    const size_t nf = point_type == FLOAM_POINT_XYZIRT ? 6 : 4;
+    std::vector<Pc2Mapping> map;
+    bool missing = false;
+    for (size_t k = 0; k < nf; ++k) {
+      bool found = false;
+      for (size_t j = 0; j < nfields; ++j) {
+        const floam_pc2_field& m = fields[j];
+        if (std::strncmp(m.name, f[k].name, sizeof(m.name)) == 0 && m.datatype == f[k].datatype &&
+            (m.count == 1 || m.count == 0)) {
+          map.push_back(Pc2Mapping{(int)m.offset, (int)f[k].offset, (int)field_bytes(f[k].datatype)});
+          found = true;
+          break;
+        }
+      }
+      if (!found) missing = true;
+    }
+    for (const auto& m : map)
+      if ((size_t)m.serialized_offset + (size_t)m.size > point_step)
+        throw Error(FLOAM_ERR_INVALID_ARGUMENT, "field extends past point_step");
+    // coalesce adjacent fields with equal serialized / struct gaps (createMapping)
+    std::sort(map.begin(), map.end(),
+              [](const Pc2Mapping& a, const Pc2Mapping& b) { return a.serialized_offset < b.serialized_offset; });
+    if (map.size() > 1) {
+      size_t i = 0;
+      for (size_t j = 1; j < map.size();) {
+        if (map[j].serialized_offset - map[i].serialized_offset == map[j].struct_offset - map[i].struct_offset) {
+          map[i].size += (map[j].struct_offset + map[j].size) - (map[i].struct_offset + map[i].size);
+          map.erase(map.begin() + (long)j);
+        } else {
+          ++i;
+          ++j;
+        }
+      }
+    }
+    Pc2Decode d{};
+    d.row_step = row_step;
+    d.point_step = (int)point_step;
+    d.width = (int)width;
+    d.height = (int)height;
+    d.nmap = (int)map.size();
+    for (size_t k = 0; k < map.size(); ++k) d.map[k] = map[k];
+    d.whole = (map.size() == 1 && map[0].serialized_offset == 0 && map[0].struct_offset == 0 &&
+               point_step == sizeof(PointRec)) ? 1 : 0;
+    DeviceCtx& ctx = ctx_for(out->device);
+    FLOAM_HIP(hipSetDevice(out->device));
+    cloud_on_main(out);
+    FLOAM_HIP(hipStreamSynchronize(ctx.stream));   // the staging buffer may still feed an earlier decode
+    cloud_reserve(out, std::max<size_t>(n, 1), 0, ctx.stream);
+    if (n) {
+      const size_t bytes = (size_t)(height - 1) * row_step + (size_t)width * point_step;
+      ctx.msg.reserve(bytes);
+      FLOAM_HIP(hipMemcpyAsync(ctx.msg.p, data, bytes, hipMemcpyHostToDevice, ctx.stream));
+      d.data = ctx.msg.p;
+      ProfScope ps(ctx, "pc2_decode", FLOAM_PROF_CLOUD, (double)bytes + 32.0 * (double)n);
+      pc2_decode_launch(d, out->pts.p, ctx.stream);
+    }
+    const int cnt = (int)n;
+    FLOAM_HIP(hipMemcpyAsync(out->count.p, &cnt, sizeof(int), hipMemcpyHostToDevice, ctx.stream));
+    FLOAM_HIP(hipStreamSynchronize(ctx.stream));   // pageable sources: the caller may reuse its buffers
+    out->host_count = n;
+    out->host_count_valid = true;
+    return missing ? FLOAM_WARN_FIELD_MISSING : FLOAM_OK;
+  });
+}
+
+floam_status floam_transform_cloud(const floam_cloud* in, const double m[16], floam_cloud* out) {
+  return guarded([&] {
+    if (!in || !m || !out) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
+    if (in->device != out->device) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "clouds on different devices");
+    DeviceCtx& ctx = ctx_for(in->device);
+    FLOAM_HIP(hipSetDevice(in->device));
+    cloud_on_main(in);
+    cloud_on_main(out);
+    const size_t n = cloud_ub(in);
+    if (in != out) cloud_reserve(out, std::max<size_t>(n, 1), 0, ctx.stream);
+    const double m34[12] = {m[0], m[1], m[2], m[3], m[4], m[5], m[6], m[7], m[8], m[9], m[10], m[11]};
+    if (n) {
+      ProfScope ps(ctx, "transform_cloud", FLOAM_PROF_CLOUD, 64.0 * (double)n);
+      transform_cloud_launch(in->pts.p, in->count.p, (int)n, m34, out->pts.p, ctx.stream);
+    }
+    if (in != out) {
+      FLOAM_HIP(hipMemcpyAsync(out->count.p, in->count.p, sizeof(int), hipMemcpyDeviceToDevice, ctx.stream));
+      out->host_count = in->host_count;
+      out->host_count_valid = in->host_count_valid;
+      out->ub = in->ub;
+    }
+    return FLOAM_OK;
   });
 }
 

@@ -544,6 +544,14 @@ __device__ __forceinline__ void group_merge(Top5& t, int& cnt) {
   }
 }
 
+// Physical block p of the first `nactive` blocks -> logical block, so that the blocks with equal p % 8 (one XCD
+// under the round-robin dispatch of MI355X_MICROARCH.md "Workgroup dispatch") get consecutive logical indices.
+// A bijection on [0, nactive); placement only affects speed, never results.
+__device__ __forceinline__ int xcd_block(int p, int nactive) {
+  const int x = p & 7, r = p >> 3, base = nactive >> 3, rem = nactive & 7;
+  return x * base + min(x, rem) + r;
+}
+
 // Pass 1: exact 5-NN of every query (no fp64 geometry here, so the kernel stays small and at high occupancy).
 // The reference keeps a correspondence iff the 5th-nearest float sq-distance is < 1 (:154, :210), so only map
 // points within 1 m matter.  Stage 1 scans the 3x3x3 FINE cells (edge 0.5 m) around the query's cell: every point
@@ -647,12 +655,18 @@ __global__ __launch_bounds__(kTB) void knn_kernel(LMState* __restrict__ st, X7 x
     lm_reset(st, xs);
   }
   const bool gate = *d_me > 10 && *d_ms > 50;   // map-size gate (odomEstimationClass.cpp:77)
-  if ((int)blockIdx.x < nbE)
-    knn_group<G, U>(pose, E, (blockIdx.x * blockDim.x + threadIdx.x) / G, nbE * (kTB / G), lane, gate, rank, world,
-                    s_pre[g], s_start[g]);
-  else
-    knn_group<G, U>(pose, S, ((blockIdx.x - nbE) * blockDim.x + threadIdx.x) / G, (gridDim.x - nbE) * (kTB / G), lane,
-                    gate, rank, world, s_pre[g], s_start[g]);
+  // XCD-aware placement: the blocks that hold queries are renumbered so that the blocks sharing an XCD (physical
+  // index mod 8 under round-robin dispatch) take consecutive query ranges.  The queries are in voxel order, so each
+  // XCD then works on a compact slab of the scene and its L2 holds that slab's map cells instead of all of them.
+  const bool edge = (int)blockIdx.x < nbE;
+  const CorrArgs& A = edge ? E : S;
+  const int nb = edge ? nbE : (int)gridDim.x - nbE;
+  int p = edge ? (int)blockIdx.x : (int)blockIdx.x - nbE;
+  const int nq = min(*A.d_n, A.n_ub);
+  const int nact = min(nb, (int)(((long long)nq * G + kTB - 1) / kTB));
+  if (p < nact) p = xcd_block(p, nact);
+  knn_group<G, U>(pose, A, (p * kTB + (int)threadIdx.x) / G, nb * (kTB / G), lane, gate, rank, world, s_pre[g],
+                  s_start[g]);
 }
 
 // Pass 2: fp64 line / plane geometry, one query per lane (all 64 lanes busy).
@@ -736,7 +750,7 @@ __device__ __forceinline__ void geom_query(LMState* __restrict__ st, const CorrA
         }
       }
     }
-    A.valid[i] = (uint8_t)((flags & 2) | (ok ? 1 : 0));
+    A.valid[i] = (uint8_t)((flags & 2) | (ok ? 1 : 0) | 4);   // bit 2: the search found 5 neighbours
   }
   const unsigned long long b = __ballot(ok);
   if ((threadIdx.x & 63) == 0 && b) atomicAdd(EDGE ? &st->corr_edge : &st->corr_surf, __popcll(b));
@@ -844,12 +858,12 @@ __global__ __launch_bounds__(kTB) void geom_kernel(LMState* __restrict__ st, Cor
   if (threadIdx.x == 0) gcnt[kGramGroups] = 0u;
 }
 
-// Algorithmic traffic of one correspondence pass (SURVEY.md §8 d): every map cell any query scans
-// is streamed once (16 B per map point: the union over queries of the fine 3x3x3 block around the query's cell —
-// level 0 — and of the coarse +-1 m stencil for the queries whose bit 1 says they needed stage 2 — level 1), every
-// query is read once (16 B) and writes its flag (1 B) and, if accepted, its record (counted at level 0).  Runs
-// untimed, on a replay, only when profiling.
-__global__ __launch_bounds__(kTB) void knn_traffic(const LMState* __restrict__ st, CorrArgs A, int rec_bytes, int rank,
+// Algorithmic traffic of one launch of the search kernel (knn_kernel; SURVEY.md §8 d): every map
+// cell any query scans is streamed once (16 B per map point: the union over queries of the fine 3x3x3 block around
+// the query's cell — level 0 — and of the coarse +-1 m stencil for the queries whose bit 1 says they needed stage 2
+// — level 1), every query is read once (16 B) and writes its flag (1 B) and, with 5 neighbours, their coordinates
+// (60 B) (counted at level 0).  Runs untimed, on a replay, only when profiling.
+__global__ __launch_bounds__(kTB) void knn_traffic(const LMState* __restrict__ st, CorrArgs A, int rank,
                                                    int world, int level, unsigned long long* __restrict__ set,
                                                    unsigned set_mask, int set_bits,
                                                    unsigned long long* __restrict__ out) {
@@ -863,7 +877,9 @@ __global__ __launch_bounds__(kTB) void knn_traffic(const LMState* __restrict__ s
   const PointRec pr = A.q[i];
   float wx, wy, wz;
   associate_to_map(st->x, pr.x, pr.y, pr.z, wx, wy, wz);
-  unsigned long long bytes = level ? 0ull : 16ull + 1ull + ((f & 1) ? (unsigned long long)rec_bytes : 0ull);
+  // the search kernel's own bytes: query (16 B) + flag (1 B) + the neighbours' coordinates it hands to the
+  // geometry pass (5 x 12 B, for the queries with 5 neighbours: bit 2 after the geometry pass)
+  unsigned long long bytes = level ? 0ull : 16ull + 1ull + ((f & 4) ? 60ull : 0ull);
   int x0, y0, z0, x1, y1, z1;
   if (level) {
     x0 = (int)floor((double)wx - 1.0); x1 = (int)floor((double)wx + 1.0);
@@ -2144,7 +2160,7 @@ void geom_launch(LMState* d_st, const QuerySet& qe, const Grid& ge, const PointR
 }
 
 void knn_traffic_launch(const LMState* d_st, const QuerySet& q, const Grid& g, const PointRec* map, CorrSet& c,
-                        int rec_bytes, int rank, int world, DevBuf<unsigned long long>& set,
+                        int rank, int world, DevBuf<unsigned long long>& set,
                         unsigned long long* d_bytes, hipStream_t st) {
   if (q.n_ub <= 0) return;
   int bits = 10;
@@ -2154,7 +2170,7 @@ void knn_traffic_launch(const LMState* d_st, const QuerySet& q, const Grid& g, c
   corr_args(q, g, map, c, q, g, map, c, nullptr, A, B);
   for (int level = 0; level < 2; ++level) {
     FLOAM_HIP(hipMemsetAsync(set.p, 0xFF, sizeof(unsigned long long) << bits, st));
-    hipLaunchKernelGGL(knn_traffic, dim3(div_up(q.n_ub, kTB)), dim3(kTB), 0, st, d_st, A, rec_bytes, rank, world,
+    hipLaunchKernelGGL(knn_traffic, dim3(div_up(q.n_ub, kTB)), dim3(kTB), 0, st, d_st, A, rank, world,
                        level, set.p, (1u << bits) - 1u, bits, d_bytes);
     FLOAM_LAUNCH_CHECK();
   }

@@ -161,7 +161,7 @@ void geom_launch(LMState* d_st, const QuerySet& qe, const Grid& ge, const PointR
                  unsigned* gcnt, hipStream_t st);
 // algorithmic bytes of the correspondence pass just issued (profiling only), accumulated into *d_bytes
 void knn_traffic_launch(const LMState* d_st, const QuerySet& q, const Grid& g, const PointRec* map, CorrSet& c,
-                        int rec_bytes, int rank, int world, DevBuf<unsigned long long>& set,
+                        int rank, int world, DevBuf<unsigned long long>& set,
                         unsigned long long* d_bytes, hipStream_t st);
 // one LM evaluation (at x in phase 0, else at cand): block partial sums of (cost, J^T J, J^T r, count)
 int lm_eval_launch(const LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const CorrSet& cs,

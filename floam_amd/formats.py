@@ -1,0 +1,298 @@
+"""Wire and disk formats around the odometry path — host mirror over the C ABI.
+
+* ``PointCloud2`` / ``fromROSMsg`` / ``toROSMsg``: sensor_msgs/PointCloud2 <-> device clouds (pcl::fromROSMsg /
+  pcl::toROSMsg, PCL 1.8.1 conversions.h); decoding runs on the device (floam_cloud_from_pointcloud2).
+* ``odometry_msg``: the /odom nav_msgs/Odometry fields the odometry node publishes (src/odomEstimationNode.cpp:
+  242-267).
+* ``transformPointCloud``: pcl::transformPointCloud with a double Affine3d, on the device.
+* Exporters of the odometry node: ``SaveOdom`` / ``SavePosegraph`` (src/utils.cpp:3-106), ``SavePosesHomogeneousBALM``
+  and ``SaveMerged`` (src/odomEstimationNode.cpp:66-121), with ``savePCDFileBinary`` (pcl::io::savePCDFileBinary,
+  PCL 1.8.1 PCDWriter::writeBinary) — host file I/O; the merge's transform + VoxelGrid run on the device.
+
+Text follows C++ iostream defaults (6 significant digits, ``%g``) and Eigen's matrix printing (column-aligned,
+space-separated) as the reference's ``operator<<`` calls produce them.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+import os
+from dataclasses import dataclass, field
+from typing import List, Sequence
+
+import numpy as np
+
+from . import _ffi
+from .cloud import DeviceCloud
+from .synth import POINT_DTYPE
+
+XYZIRT, XYZI = 0, 1   # FLOAM_POINT_XYZIRT, FLOAM_POINT_XYZI
+INT8, UINT8, INT16, UINT16, INT32, UINT32, FLOAT32, FLOAT64 = 1, 2, 3, 4, 5, 6, 7, 8
+_SIZES = {INT8: 1, UINT8: 1, INT16: 2, UINT16: 2, INT32: 4, UINT32: 4, FLOAT32: 4, FLOAT64: 8}
+_TYPES = {INT8: "I", UINT8: "U", INT16: "I", UINT16: "U", INT32: "I", UINT32: "U", FLOAT32: "F", FLOAT64: "F"}
+
+
+@dataclass
+class PointField:
+    name: str
+    offset: int
+    datatype: int
+    count: int = 1
+
+
+@dataclass
+class PointCloud2:
+    """sensor_msgs/PointCloud2 (header stamp in seconds)."""
+    height: int = 1
+    width: int = 0
+    fields: List[PointField] = field(default_factory=list)
+    is_bigendian: bool = False
+    point_step: int = 0
+    row_step: int = 0
+    data: bytes = b""
+    is_dense: bool = True
+    stamp: float = 0.0
+    frame_id: str = ""
+
+
+def fields_of(point_type: int = XYZIRT):
+    """The field table pcl::toROSMsg writes for PointXYZIRT (include/lidar.h:26-32) / PointXYZI; point_step 32."""
+    arr = (_ffi.PC2Field * 8)()
+    n = C.c_size_t()
+    step = C.c_uint32()
+    _ffi.check(_ffi.load().floam_pointcloud2_fields(point_type, arr, 8, C.byref(n), C.byref(step)))
+    return [PointField(arr[i].name.decode(), arr[i].offset, arr[i].datatype, arr[i].count) for i in range(n.value)], \
+        step.value
+
+
+def fromROSMsg(msg: PointCloud2, cloud: DeviceCloud, point_type: int = XYZIRT) -> bool:
+    """pcl::fromROSMsg(msg, cloud) (src/laserProcessingNode.cpp:89, src/odomEstimationNode.cpp:205-206), decoded on the
+    device.  Returns False when a point field had no match in the message (PCL warns and leaves it zero)."""
+    arr = (_ffi.PC2Field * max(1, len(msg.fields)))()
+    for i, f in enumerate(msg.fields):
+        arr[i].name = f.name.encode()[:31]
+        arr[i].offset, arr[i].datatype, arr[i].count = f.offset, f.datatype, f.count
+    buf = np.frombuffer(msg.data, dtype=np.uint8) if len(msg.data) else np.zeros(1, np.uint8)
+    rc = _ffi.check(_ffi.load().floam_cloud_from_pointcloud2(
+        cloud.handle, point_type, buf.ctypes.data_as(C.c_void_p), len(msg.data), msg.width, msg.height,
+        msg.point_step, msg.row_step, arr, len(msg.fields)))
+    return rc != _ffi.WARN_FIELD_MISSING
+
+
+def toROSMsg(cloud: DeviceCloud, point_type: int = XYZIRT, stamp: float = 0.0, frame_id: str = "") -> PointCloud2:
+    """pcl::toROSMsg of a PointXYZIRT / PointXYZI cloud (the edge / surf / scan_registered topics)."""
+    pts = cloud.download()
+    flds, step = fields_of(point_type)
+    return PointCloud2(height=1, width=pts.shape[0], fields=flds, point_step=step, row_step=step * pts.shape[0],
+                       data=pts.tobytes(), stamp=stamp, frame_id=frame_id)
+
+
+def transformPointCloud(cloud_in: DeviceCloud, cloud_out: DeviceCloud, T) -> None:
+    """pcl::transformPointCloud(in, out, Eigen::Affine3d T) (PCL 1.8.1, dense path), on the device."""
+    m = np.ascontiguousarray(T, dtype=np.float64).reshape(16)
+    _ffi.check(_ffi.load().floam_transform_cloud(cloud_in.handle, m.ctypes.data_as(C.POINTER(C.c_double)),
+                                                 cloud_out.handle))
+
+
+def odometry_msg(q_xyzw, t, stamp: float):
+    """The nav_msgs/Odometry the odometry node publishes on /odom (src/odomEstimationNode.cpp:256-267):
+    frame 'map', child 'base_link', pose = odom (q as Eigen::Quaterniond(odom.rotation()))."""
+    q = np.asarray(q_xyzw, dtype=np.float64)
+    t = np.asarray(t, dtype=np.float64)
+    return {"header": {"frame_id": "map", "stamp": float(stamp)}, "child_frame_id": "base_link",
+            "pose": {"position": {"x": t[0], "y": t[1], "z": t[2]},
+                     "orientation": {"x": q[0], "y": q[1], "z": q[2], "w": q[3]}}}
+
+
+# ------------------------------------------------------------------------------------------- text helpers
+def _g(x: float) -> str:
+    """std::ostream << double with the default format (precision 6, %g)."""
+    x = float(x)
+    if math.isnan(x):
+        return "-nan" if math.copysign(1.0, x) < 0 else "nan"
+    return "%g" % x
+
+
+def eigen_str(m) -> str:
+    """operator<<(ostream, Eigen matrix) with the default IOFormat: coefficients at stream precision, right-aligned
+    to the widest one, ' ' between columns, '\\n' between rows, no trailing newline."""
+    m = np.atleast_2d(np.asarray(m, dtype=np.float64))
+    s = [[_g(v) for v in row] for row in m]
+    w = max(len(c) for row in s for c in row)
+    return "\n".join(" ".join(c.rjust(w) for c in row) for row in s)
+
+
+def ros_time(t: float):
+    """ros::Time(double): (sec, nsec) with roscpp_core's fromSec rounding."""
+    sec = math.floor(t)
+    x = (t - float(sec)) * 1e9
+    nsec = int(math.floor(x + 0.5)) if x >= 0 else -int(math.floor(-x + 0.5))
+    sec += nsec // 1_000_000_000
+    return int(sec), int(nsec % 1_000_000_000)
+
+
+def _quat_from_matrix(R):
+    """Eigen::Quaterniond(Matrix3d) (quaternionbase_assign_impl, Shepperd) -> (x, y, z, w)."""
+    a = np.asarray(R, dtype=np.float64)
+    t = a[0, 0] + a[1, 1] + a[2, 2]
+    if t > 0:
+        t = math.sqrt(t + 1.0)
+        w = 0.5 * t
+        t = 0.5 / t
+        return np.array([(a[2, 1] - a[1, 2]) * t, (a[0, 2] - a[2, 0]) * t, (a[1, 0] - a[0, 1]) * t, w])
+    i = 0
+    if a[1, 1] > a[0, 0]:
+        i = 1
+    if a[2, 2] > a[i, i]:
+        i = 2
+    j, k = (i + 1) % 3, (i + 2) % 3
+    t = math.sqrt(a[i, i] - a[j, j] - a[k, k] + 1.0)
+    c = [0.0, 0.0, 0.0]
+    c[i] = 0.5 * t
+    t = 0.5 / t
+    w = (a[k, j] - a[j, k]) * t
+    c[j] = (a[j, i] + a[i, j]) * t
+    c[k] = (a[k, i] + a[i, k]) * t
+    return np.array([c[0], c[1], c[2], w])
+
+
+def _affine_inverse(T):
+    """Eigen::Affine3d::inverse() (Affine mode): general 3x3 inverse by cofactors, t' = -A^-1 t."""
+    A = np.asarray(T, dtype=np.float64)[:3, :3]
+
+    def cof(i, j):
+        i1, i2, j1, j2 = (i + 1) % 3, (i + 2) % 3, (j + 1) % 3, (j + 2) % 3
+        return A[i1, j1] * A[i2, j2] - A[i1, j2] * A[i2, j1]
+    c0 = [cof(0, 0), cof(1, 0), cof(2, 0)]
+    det = (c0[0] * A[0, 0] + c0[1] * A[1, 0]) + c0[2] * A[2, 0]
+    inv = 1.0 / det
+    Ai = np.empty((3, 3))
+    Ai[0] = [c0[0] * inv, c0[1] * inv, c0[2] * inv]
+    Ai[1] = [cof(0, 1) * inv, cof(1, 1) * inv, cof(2, 1) * inv]
+    Ai[2] = [cof(0, 2) * inv, cof(1, 2) * inv, cof(2, 2) * inv]
+    out = np.eye(4)
+    out[:3, :3] = Ai
+    t = np.asarray(T, dtype=np.float64)[:3, 3]
+    out[:3, 3] = -(Ai @ t)
+    return out
+
+
+# ------------------------------------------------------------------------------------------- PCD
+def savePCDFileBinary(path: str, points: np.ndarray, point_type: int = XYZI) -> None:
+    """pcl::io::savePCDFileBinary (PCL 1.8.1 PCDWriter::generateHeader + writeBinary): v0.7 header, then the fields
+    packed without padding (16 B per PointXYZI)."""
+    pts = np.ascontiguousarray(points).view(POINT_DTYPE)
+    flds, _ = fields_of(point_type)
+    hdr = ("# .PCD v0.7 - Point Cloud Data file format\nVERSION 0.7\nFIELDS" + "".join(" " + f.name for f in flds)
+           + "\nSIZE" + "".join(f" {_SIZES[f.datatype]}" for f in flds)
+           + "\nTYPE" + "".join(f" {_TYPES[f.datatype]}" for f in flds)
+           + "\nCOUNT" + "".join(f" {max(1, abs(f.count))}" for f in flds)
+           + f"\nWIDTH {pts.shape[0]}\nHEIGHT 1\nVIEWPOINT 0 0 0 1 0 0 0\nPOINTS {pts.shape[0]}\nDATA binary\n")
+    packed = np.empty(pts.shape[0], dtype=np.dtype({"names": [f.name for f in flds],
+                                                    "formats": ["<u2" if f.datatype == UINT16 else "<f4" for f in flds],
+                                                    "offsets": list(np.cumsum([0] + [_SIZES[f.datatype] for f in flds])[:-1]),
+                                                    "itemsize": sum(_SIZES[f.datatype] for f in flds)}))
+    for f in flds:
+        packed[f.name] = pts[f.name]
+    with open(path, "wb") as fh:
+        fh.write(hdr.encode())
+        fh.write(packed.tobytes())
+
+
+def loadPCDFileBinary(path: str) -> np.ndarray:
+    """Reader for the files savePCDFileBinary writes (tests and tooling)."""
+    raw = open(path, "rb").read()
+    end = raw.index(b"DATA binary\n") + len(b"DATA binary\n")
+    hdr = raw[:end].decode().splitlines()
+    meta = {ln.split()[0]: ln.split()[1:] for ln in hdr if ln and not ln.startswith("#")}
+    names = meta["FIELDS"]
+    sizes = [int(s) for s in meta["SIZE"]]
+    n = int(meta["POINTS"][0])
+    dt = np.dtype({"names": names, "formats": ["<u2" if s == 2 else "<f4" for s in sizes],
+                   "offsets": list(np.cumsum([0] + sizes)[:-1]), "itemsize": sum(sizes)})
+    packed = np.frombuffer(raw[end:end + n * dt.itemsize], dtype=dt)
+    out = np.zeros(n, POINT_DTYPE)
+    out["pad0"] = 1.0
+    for f in names:
+        out[f] = packed[f]
+    return out
+
+
+# ------------------------------------------------------------------------------------------- exporters
+def SaveOdom(dump_directory: str, poses: Sequence[np.ndarray], keyframe_stamps: Sequence[float],
+             clouds: Sequence[np.ndarray]) -> None:
+    """SaveOdom (src/utils.cpp:78-106): per keyframe <sec>_<nsec>.pcd and .odom (4x4 pose, rows of 4)."""
+    os.makedirs(dump_directory, exist_ok=True)
+    for i in range(len(clouds)):
+        sec, nsec = ros_time(keyframe_stamps[i])
+        base = os.path.join(dump_directory, f"{sec}_{nsec}")
+        savePCDFileBinary(base + ".pcd", clouds[i])
+        m = np.asarray(poses[i], dtype=np.float64)
+        with open(base + ".odom", "w") as fh:
+            for r in range(4):
+                fh.write(" ".join(_g(m[r, c]) for c in range(4)) + "\n")
+
+
+def SavePosegraph(dump_directory: str, poses: Sequence[np.ndarray], keyframe_stamps: Sequence[float],
+                  clouds: Sequence[np.ndarray]) -> None:
+    """SavePosegraph (src/utils.cpp:3-75): graph.g2o (VERTEX_SE3:QUAT per pose, FIX 0, EDGE_SE3:QUAT between
+    consecutive poses with the diagonal information 0.01 x3, 0.001 x3) and one directory per keyframe
+    (cloud.pcd + data)."""
+    os.makedirs(dump_directory, exist_ok=True)
+    P = [np.asarray(p, dtype=np.float64) for p in poses]
+    with open(os.path.join(dump_directory, "graph.g2o"), "w") as g:
+        for count, T in enumerate(P):
+            q = _quat_from_matrix(T[:3, :3])
+            t = T[:3, 3]
+            g.write(f"VERTEX_SE3:QUAT {count} " + " ".join(_g(v) for v in (*t, *q)) + "\n")
+        g.write("FIX 0\n")
+        info = np.diag([0.01, 0.01, 0.01, 0.001, 0.001, 0.001])
+        for i in range(len(P) - 1):
+            rel = _affine_inverse(P[i]) @ P[i + 1]
+            q = _quat_from_matrix(rel[:3, :3])
+            t = rel[:3, 3]
+            line = f"EDGE_SE3:QUAT {i} {i + 1} " + " ".join(_g(v) for v in (*t, *q))
+            line += "".join(" " + _g(info[r, c]) for r in range(6) for c in range(r, 6))
+            g.write(line + "\n")
+    for i, cl in enumerate(clouds):
+        d = os.path.join(dump_directory, "%06d" % i)
+        os.makedirs(d, exist_ok=True)
+        savePCDFileBinary(os.path.join(d, "cloud.pcd"), cl)
+        sec, nsec = ros_time(keyframe_stamps[i])
+        with open(os.path.join(d, "data"), "w") as fh:
+            fh.write(f"stamp {sec} {nsec}\nestimate\n{eigen_str(P[i])}\nodom\n{eigen_str(P[i])}\n"
+                     f"accum_distance -1\nid {i}\n")
+
+
+def SavePosesHomogeneousBALM(clouds: Sequence[np.ndarray], poses: Sequence[np.ndarray],
+                             stamps: Sequence[float], directory: str) -> None:
+    """SavePosesHomogeneousBALM (src/odomEstimationNode.cpp:97-117): alidarPose.csv (std::fixed rows of the 4x4
+    pose, the stamp in place of element (3, 3)) and full<i>.pcd."""
+    os.makedirs(directory, exist_ok=True)
+    with open(os.path.join(directory, "alidarPose.csv"), "w") as fh:
+        for i, T in enumerate(poses):
+            m = np.asarray(T, dtype=np.float64)
+            rows = [list(m[r]) for r in range(3)] + [[m[3, 0], m[3, 1], m[3, 2], float(stamps[i])]]
+            for row in rows:
+                fh.write(",".join("%.6f" % v for v in row) + ",\n")
+            savePCDFileBinary(os.path.join(directory, f"full{i}.pcd"), clouds[i])
+
+
+def SaveMerged(clouds: Sequence[np.ndarray], poses: Sequence[np.ndarray], directory: str, downsample_size: float,
+               device: int = 0) -> None:
+    """SaveMerged (src/odomEstimationNode.cpp:66-96): every keyframe cloud transformed by its pose and concatenated
+    (floam_merged.pcd), then VoxelGrid(downsample_size) (floam_merged_downsampled_leaf_<size>.pcd); the transforms
+    and the voxel grid run on the device."""
+    os.makedirs(directory, exist_ok=True)
+    parts = []
+    d_in, d_out = DeviceCloud(device=device), DeviceCloud(device=device)
+    for cl, T in zip(clouds, poses):
+        d_in.upload(np.ascontiguousarray(cl).view(POINT_DTYPE))
+        transformPointCloud(d_in, d_out, T)
+        parts.append(d_out.download())
+    merged = np.concatenate(parts) if parts else np.zeros(0, POINT_DTYPE)
+    d_m = DeviceCloud(merged, device=device) if merged.shape[0] else DeviceCloud(device=device)
+    down = d_m.voxel_grid(float(downsample_size)).download() if merged.shape[0] else merged
+    savePCDFileBinary(directory + "floam_merged.pcd", merged)
+    if down.shape[0]:
+        savePCDFileBinary(directory + "floam_merged_downsampled_leaf_" + ("%f" % downsample_size) + ".pcd", down)

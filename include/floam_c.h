@@ -34,7 +34,8 @@ typedef enum floam_status {
   /* non-fatal, same conditions as the reference's printf warnings */
   FLOAM_WARN_MAP_TOO_SMALL = 100,       /* src/odomEstimationClass.cpp:112 "not enough points in map" */
   FLOAM_WARN_FEW_CORRESPONDENCES = 101, /* src/odomEstimationClass.cpp:192-194, 247-249 (< 20 factors) */
-  FLOAM_WARN_NO_IMU_DATA = 102          /* src/dataHandler.cpp:101-104 "no imu data" (Compensate returns false) */
+  FLOAM_WARN_NO_IMU_DATA = 102,         /* src/dataHandler.cpp:101-104 "no imu data" (Compensate returns false) */
+  FLOAM_WARN_FIELD_MISSING = 103        /* PCL fromPCLPointCloud2 "Failed to find match for field" (the field stays 0) */
 } floam_status;
 
 /* 32-byte point record, byte-compatible with vel_point::PointXYZIRT (include/lidar.h:14-32) and with
@@ -136,6 +137,35 @@ floam_status floam_imu_compensate(floam_imu* h, floam_cloud* in, uint64_t stamp_
  * (:104-107); `in` is centred regardless and `aligned` is unchanged. */
 floam_status floam_imu_preprocess(floam_imu* h, floam_cloud* in, uint64_t* stamp_us, const double extrinsics_xyzw[4],
                                   floam_cloud* aligned);
+
+/* ---------------------------------------------------------------------------------------- wire formats */
+/* sensor_msgs/PointField (name, offset, datatype, count); datatype codes as PointField: UINT16 = 4, FLOAT32 = 7. */
+typedef struct floam_pc2_field {
+  char name[32];
+  uint32_t offset;
+  uint8_t datatype;
+  uint32_t count;
+} floam_pc2_field;
+enum { FLOAM_POINT_XYZIRT = 0, FLOAM_POINT_XYZI = 1 };
+/* The field table pcl::toROSMsg writes for vel_point::PointXYZIRT (x, y, z, intensity, ring, time) or pcl::PointXYZI
+ * (x, y, z, intensity) with point_step 32; the message data is then floam_cloud_download's 32-B records
+ * (row_step = 32 * width, height 1).  Used for /laser_cloud_edge, /laser_cloud_surf (src/laserProcessingNode.cpp:
+ * 145-155) and /scan_registered (src/odomEstimationNode.cpp:273). */
+floam_status floam_pointcloud2_fields(int point_type, floam_pc2_field* out, size_t capacity, size_t* n_out,
+                                      uint32_t* point_step);
+/* pcl::fromROSMsg(msg, cloud) (pcl_conversions + PCL 1.8.1 fromPCLPointCloud2), the decode at
+ * src/laserProcessingNode.cpp:89 and src/odomEstimationNode.cpp:205-206: fields matched by name, datatype and count,
+ * adjacent fields coalesced, bytes copied per point (row-major over height x width, row_step / point_step strides),
+ * unmatched struct bytes zero; a single coalesced mapping at offset 0 with point_step 32 copies whole records.
+ * The bytes are staged through HBM and decoded on the device; `out` is replaced.  FLOAM_WARN_FIELD_MISSING when a
+ * point field has no match (PCL only warns). */
+floam_status floam_cloud_from_pointcloud2(floam_cloud* out, int point_type, const void* data, size_t data_size,
+                                          uint32_t width, uint32_t height, uint32_t point_step, uint32_t row_step,
+                                          const floam_pc2_field* fields, size_t nfields);
+/* pcl::transformPointCloud(in, out, Eigen::Affine3d T) (PCL 1.8.1 transforms.hpp, dense path): x' =
+ * float(((T00 x + T01 y) + T02 z) + T03) in double; other fields copied.  m = row-major 4x4; in == out allowed.
+ * SaveMerged's per-keyframe transform (src/odomEstimationNode.cpp:72-76). */
+floam_status floam_transform_cloud(const floam_cloud* in, const double m[16], floam_cloud* out);
 
 /* -------------------------------------------------------------------------------- OdomEstimationClass */
 typedef struct floam_odom floam_odom;

@@ -85,6 +85,10 @@ def lib():
         L.oracle_imu_preprocess.argtypes = [C.c_int, C.c_void_p, C.c_size_t, C.POINTER(C.c_uint64), c_double_p,
                                             c_double_p, C.c_size_t, c_double_p, C.c_void_p]
         L.oracle_imu_preprocess.restype = C.c_int
+        L.oracle_from_pointcloud2.argtypes = [C.c_int, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                              C.c_void_p, C.c_size_t, C.c_void_p]
+        L.oracle_from_pointcloud2.restype = C.c_int
+        L.oracle_transform_cloud.argtypes = [C.c_void_p, C.c_size_t, c_double_p, C.c_void_p]
         _LIB = L
     return _LIB
 
@@ -332,3 +336,32 @@ def imu_preprocess(points: np.ndarray, stamp_us: int, stamps, q_xyzw, extrinsics
     ok = lib().oracle_imu_preprocess(int(mode), _ptr(p), p.shape[0], C.byref(st), _dptr(s), _dptr(q), s.shape[0],
                                      _dptr(e), _ptr(out))
     return bool(ok), p, out, int(st.value)
+
+
+# ------------------------------------------------------------------ wire formats (oracle/formats.cpp, §8 f-3)
+PC2_FIELD_DTYPE = np.dtype({"names": ["name", "offset", "datatype", "count"],
+                            "formats": ["S32", "<u4", "u1", "<u4"], "offsets": [0, 32, 36, 40], "itemsize": 44})
+
+
+def from_pointcloud2(data: bytes, width: int, height: int, point_step: int, row_step: int, fields,
+                     point_type: int = 0):
+    """pcl::fromROSMsg / fromPCLPointCloud2 restated.  fields: [(name, offset, datatype, count)].
+    Returns (points, number of point fields without a match)."""
+    from floam_amd.synth import POINT_DTYPE
+    f = np.zeros(max(1, len(fields)), PC2_FIELD_DTYPE)
+    for i, (nm, off, dt, cnt) in enumerate(fields):
+        f[i] = (nm.encode(), off, dt, cnt)
+    buf = np.frombuffer(data, np.uint8) if len(data) else np.zeros(1, np.uint8)
+    out = np.zeros(max(1, width * height), POINT_DTYPE)
+    miss = lib().oracle_from_pointcloud2(point_type, _ptr(buf), width, height, point_step, row_step, _ptr(f),
+                                         len(fields), _ptr(out))
+    return out[: width * height].copy(), miss
+
+
+def transform_cloud(points: np.ndarray, T) -> np.ndarray:
+    """pcl::transformPointCloud with a double Affine3d (row-major 4x4)."""
+    p = _as_points(points)
+    out = np.zeros_like(p)
+    m = np.ascontiguousarray(T, dtype=np.float64).reshape(16)
+    lib().oracle_transform_cloud(_ptr(p), p.shape[0], _dptr(m), _ptr(out))
+    return out

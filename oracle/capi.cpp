@@ -163,4 +163,14 @@ int oracle_imu_preprocess(int mode, void* in, size_t n, uint64_t* stamp_us, cons
   return imu_preprocess(p, n, stamp_us, h, e, static_cast<Pt*>(out)) ? 1 : 0;
 }
 
+// ---- wire formats (oracle/formats.cpp)
+int oracle_from_pointcloud2(int point_type, const void* data, uint32_t width, uint32_t height, uint32_t point_step,
+                            uint32_t row_step, const void* fields, size_t nfields, void* out) {
+  return from_pointcloud2(point_type, static_cast<const uint8_t*>(data), width, height, point_step, row_step,
+                          static_cast<const Pc2Field*>(fields), nfields, static_cast<Pt*>(out));
+}
+void oracle_transform_cloud(const void* in, size_t n, const double* m, void* out) {
+  transform_cloud(static_cast<const Pt*>(in), n, m, static_cast<Pt*>(out));
+}
+
 }  // extern "C"

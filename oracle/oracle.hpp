@@ -135,6 +135,18 @@ bool compensate(const Pt* in, size_t n, uint64_t stamp_us, const ImuHandler& h, 
 void transform_by_quaternion(const Pt* in, size_t n, const Quat& q, Pt* out);
 bool imu_preprocess(Pt* in, size_t n, uint64_t* stamp_us, const ImuHandler& h, const Quat& extr, Pt* out);
 
+// ---------------------------------------------------------------------------------------------- wire formats
+// (oracle/formats.cpp)
+struct Pc2Field {   // sensor_msgs/PointField, the layout of floam_pc2_field
+  char name[32];
+  uint32_t offset;
+  uint8_t datatype;
+  uint32_t count;
+};
+int from_pointcloud2(int point_type, const uint8_t* data, uint32_t width, uint32_t height, uint32_t point_step,
+                     uint32_t row_step, const Pc2Field* fields, size_t nfields, Pt* out);
+void transform_cloud(const Pt* in, size_t n, const double m[16], Pt* out);
+
 void reset_process_statics();   // KeyFrameUpdate's function-static `first` (odomEstimationClass.cpp:323, Q6)
 double test_edge_eval(const double cp[3], const double a[3], const double b[3], const double* x, double* J);
 double test_surf_eval(const double cp[3], const double n[3], double d, const double* x, double* J);

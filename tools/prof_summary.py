@@ -69,7 +69,7 @@ def main():
     traffic = {}
     lines = [f"# rocprofv3 summary — {args.tag}", "",
              "Command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --cpu-baseline-seconds 0` (C3, 8 warm-up + "
-             "20 timed scans; all dispatches of the run, warm-up and map prefill included).  HBM bytes: separate "
+             "60 timed scans, then the same 68 scans replayed with per-launch events for the roofline; all dispatches of the run, map prefill included).  HBM bytes: separate "
              "`--pmc FETCH_SIZE` and `--pmc WRITE_SIZE` runs of the same command; FETCH_SIZE doubled (gfx950 16-B/lane "
              "read correction), KiB → bytes.", "",
              "| kernel | calls | total us | avg us | % | HBM read B/launch | HBM write B/launch |",
