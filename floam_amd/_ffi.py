@@ -44,6 +44,8 @@ EXPORTS = [
     "floam_imu_get", "floam_imu_time_contained", "floam_euler_to_quaternion", "floam_center_time",
     "floam_imu_compensate", "floam_imu_preprocess",
     "floam_pointcloud2_fields", "floam_cloud_from_pointcloud2", "floam_transform_cloud",
+    "floam_mapping_create", "floam_mapping_destroy", "floam_mapping_update", "floam_mapping_get_map",
+    "floam_mapping_size",
 ]
 
 
@@ -124,6 +126,8 @@ def load(path: str | None = None):
         "floam_cloud_from_pointcloud2": [vp, i32, vp, sz, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                                          C.POINTER(PC2Field), sz],
         "floam_transform_cloud": [vp, dp, vp],
+        "floam_mapping_create": [dbl, i32, pp], "floam_mapping_destroy": [vp], "floam_mapping_update": [vp, vp, dp, dp],
+        "floam_mapping_get_map": [vp, vp], "floam_mapping_size": [vp, szp],
     }
     for name, args in sig.items():
         f = getattr(L, name)

@@ -29,9 +29,11 @@
 #include "floam_common.hpp"
 #include "formats.hpp"
 #include "imu.hpp"
+#include "mapping.hpp"
 #include "odom_kernels.hpp"
 #include "pose.hpp"
 #include "voxel.hpp"
+#include <unordered_map>
 
 namespace floam {
 
@@ -300,6 +302,25 @@ struct floam_imu {
   double* d_t = nullptr;
   Q4* d_q = nullptr;
   size_t dcap = 0, uploaded = 0;
+};
+
+// LaserMappingClass (include/laserMappingClass.h:38-66): the cell map in HBM (cell-grouped records in getMap order),
+// the cell table (absolute cell key, size) on the host.
+struct floam_mapping {
+  int device = 0;
+  float leaf = 0.4f;
+  floam_cloud map, next;                 // current map / the rebuild target (swapped per update)
+  std::vector<unsigned long long> keys;  // cell keys, ascending
+  std::vector<int> counts;               // points per cell
+  // scratch
+  DevBuf<PointRec> stage, sorted, vox;
+  DevBuf<int> slot, hcnt, hrank, cellv, total;
+  DevBuf<unsigned long long> hkeys;
+  SortScratch ss;
+  RadixScratch rs;
+  VoxelScratch2 vs;
+  HostBuf<unsigned long long> h_keys;
+  HostBuf<int> h_cnt, h_cellv;
 };
 
 namespace {
@@ -1699,6 +1720,246 @@ floam_status floam_transform_cloud(const floam_cloud* in, const double m[16], fl
       out->host_count_valid = in->host_count_valid;
       out->ub = in->ub;
     }
+    return FLOAM_OK;
+  });
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------------------------------ global map
+namespace {
+void mapping_update(floam_mapping* m, const floam_cloud* in, const double* q, const double* t) {
+  DeviceCtx& ctx = ctx_for(m->device);
+  hipStream_t st = ctx.stream;
+  FLOAM_HIP(hipSetDevice(m->device));
+  cloud_on_main(in);
+  const int n = (int)cloud_count_sync(in);
+  // current_pose = Isometry3d::Identity().rotate(q).pretranslate(t) (src/laserMappingNode.cpp:108-110)
+  const Mat3 R = quat_to_mat(q);
+  auto cell_of = [](double v) { return (int)std::floor(v / 50.0 + 0.5); };
+  const int px = cell_of(t[0]), py = cell_of(t[1]), pz = cell_of(t[2]);
+  const int ncell_old = (int)m->keys.size();
+  // 1. transform + cells of the new points, distinct cells counted
+  std::unordered_map<unsigned long long, int> touched;   // key -> new points
+  std::vector<int> slot_of;                              // touched cell -> hash slot
+  if (n > 0) {
+    m->stage.reserve(n);
+    m->slot.reserve(n);
+    m->hkeys.reserve(kMapHashSlots);
+    m->hcnt.reserve(kMapHashSlots + 1);   // [kMapHashSlots] = overflow flag
+    m->h_keys.reserve(kMapHashSlots);
+    m->h_cnt.reserve(kMapHashSlots + 1);
+    m->rs.reserve(n, st);
+    FLOAM_HIP(hipMemsetAsync(m->hkeys.p, 0xFF, sizeof(unsigned long long) * kMapHashSlots, st));
+    FLOAM_HIP(hipMemsetAsync(m->hcnt.p, 0, sizeof(int) * (kMapHashSlots + 1), st));
+    MapPrepArgs a{};
+    a.in = in->pts.p; a.d_n = in->count.p; a.n = n;
+    for (int r = 0; r < 3; ++r) {   // pose_current.cast<float>() (src/laserMappingClass.cpp:157)
+      for (int c = 0; c < 3; ++c) a.m[4 * r + c] = (float)R.m[r][c];
+      a.m[4 * r + 3] = (float)t[r];
+    }
+    a.stage = m->stage.p; a.slot = m->slot.p; a.hkeys = m->hkeys.p; a.hcnt = m->hcnt.p;
+    a.overflow = m->hcnt.p + kMapHashSlots; a.radix_ctl = m->rs.ctl.p;
+    {
+      ProfScope ps(ctx, "map_prep", FLOAM_PROF_CLOUD, 64.0 * n);
+      map_prep_launch(a, st);
+    }
+    FLOAM_HIP(hipMemcpyAsync(m->h_keys.p, m->hkeys.p, sizeof(unsigned long long) * kMapHashSlots,
+                             hipMemcpyDeviceToHost, st));
+    FLOAM_HIP(hipMemcpyAsync(m->h_cnt.p, m->hcnt.p, sizeof(int) * (kMapHashSlots + 1), hipMemcpyDeviceToHost, st));
+    FLOAM_HIP(hipStreamSynchronize(st));
+    if (m->h_cnt.p[kMapHashSlots])
+      throw Error(FLOAM_ERR_UNSUPPORTED, "one update touches more than 2048 map cells (100 km of 50-m cells)");
+    for (int h = 0; h < kMapHashSlots; ++h)
+      if (m->h_keys.p[h] != ~0ull) touched[m->h_keys.p[h]] = m->h_cnt.p[h];
+  }
+  // 2. the merged cell table; the neighbourhood of the pose is filtered (src/laserMappingClass.cpp:174-183)
+  std::vector<unsigned long long> keys = m->keys;
+  for (const auto& kv : touched)
+    if (!std::binary_search(m->keys.begin(), m->keys.end(), kv.first)) keys.push_back(kv.first);
+  std::sort(keys.begin(), keys.end());
+  const int nc = (int)keys.size();
+  // per cell: [0] old start, [1] old count, [2] new count, [3] new start, [4] voxel offset (-1: copied), [5] out count
+  std::vector<int> old_start(nc, -1), seg(2 * nc, 0), new_start(nc, 0), vox_off(nc, -1), outcnt(nc, 0);
+  {
+    int os = 0, k = 0;
+    for (int c = 0; c < nc; ++c) {
+      if (k < ncell_old && m->keys[k] == keys[c]) {
+        old_start[c] = os;
+        seg[2 * c] = m->counts[k];
+        os += m->counts[k];
+        ++k;
+      }
+      auto it = touched.find(keys[c]);
+      seg[2 * c + 1] = it == touched.end() ? 0 : it->second;
+    }
+  }
+  int ns = 0, vs_total = 0;
+  std::vector<int> filtered;
+  for (int c = 0; c < nc; ++c) {
+    new_start[c] = ns;
+    ns += seg[2 * c + 1];
+    int x, y, z;
+    map_cell_coords(keys[c], x, y, z);
+    const bool in_nb = std::abs(x - px) <= 2 && std::abs(y - py) <= 2 && std::abs(z - pz) <= 2;
+    const int tot = seg[2 * c] + seg[2 * c + 1];
+    outcnt[c] = tot;
+    if (in_nb && tot > 0) {
+      vox_off[c] = vs_total;
+      vs_total += tot;
+      filtered.push_back(c);
+    }
+  }
+  const int total_ub = ns + (int)(m->map.host_count_valid ? m->map.host_count : m->map.ub);
+  // device copies of the per-cell tables: [old_start | seg (2) | new_start | vox_off | outcnt | off (nc + 1)]
+  m->cellv.reserve((size_t)7 * nc + 2);
+  m->h_cellv.reserve((size_t)7 * nc + 2);
+  int* hv = m->h_cellv.p;
+  std::memcpy(hv, old_start.data(), sizeof(int) * nc);
+  std::memcpy(hv + nc, seg.data(), sizeof(int) * 2 * nc);
+  std::memcpy(hv + 3 * nc, new_start.data(), sizeof(int) * nc);
+  std::memcpy(hv + 4 * nc, vox_off.data(), sizeof(int) * nc);
+  std::memcpy(hv + 5 * nc, outcnt.data(), sizeof(int) * nc);
+  FLOAM_HIP(hipMemcpyAsync(m->cellv.p, hv, sizeof(int) * 6 * nc, hipMemcpyHostToDevice, st));
+  int* d_old_start = m->cellv.p;
+  int* d_seg = m->cellv.p + nc;
+  int* d_new_start = m->cellv.p + 3 * nc;
+  int* d_vox_off = m->cellv.p + 4 * nc;
+  int* d_outcnt = m->cellv.p + 5 * nc;
+  int* d_off = m->cellv.p + 6 * nc;
+  // 3. new points grouped by cell (stable radix sort by the cell's rank)
+  if (n > 0) {
+    m->hrank.reserve(kMapHashSlots);
+    std::vector<int> hrank(kMapHashSlots, 0);
+    for (int h = 0; h < kMapHashSlots; ++h)
+      if (m->h_keys.p[h] != ~0ull)
+        hrank[h] = (int)(std::lower_bound(keys.begin(), keys.end(), m->h_keys.p[h]) - keys.begin());
+    FLOAM_HIP(hipMemcpyAsync(m->hrank.p, hrank.data(), sizeof(int) * kMapHashSlots, hipMemcpyHostToDevice, st));
+    m->ss.reserve(n);
+    m->sorted.reserve(n);
+    map_rank_keys_launch(m->slot.p, m->hrank.p, n, m->ss.k0.p, m->ss.v0.p, m->rs.ctl.p, st);
+    radix_sort_launch(m->rs, m->ss.k0.p, m->ss.v0.p, m->ss.k1.p, m->ss.v1.p, n, st);
+    map_gather_launch(m->stage.p, m->ss.v0.p, n, m->sorted.p, st);
+    FLOAM_HIP(hipStreamSynchronize(st));   // hrank is a pageable source
+  }
+  // 4. VoxelGrid of the neighbourhood's cells, two per pipeline launch
+  m->vox.reserve(std::max(vs_total, 1));
+  if (!ctx.zero.p) {
+    ctx.zero.reserve(2);
+    FLOAM_HIP(hipMemsetAsync(ctx.zero.p, 0, sizeof(int) * 2, st));
+  }
+  m->vs.s.reserve(1);
+  for (size_t f = 0; f < filtered.size(); f += 2) {
+    VoxelJob job[2];
+    for (int u = 0; u < 2; ++u) {
+      VoxelJob& J = job[u];
+      J.leaf = m->leaf;
+      if (f + u < filtered.size()) {
+        const int c = filtered[f + u];
+        J.part0 = m->map.pts.p + std::max(old_start[c], 0);
+        J.d_n0 = d_seg + 2 * c;
+        J.n0_ub = seg[2 * c];
+        J.part1 = m->sorted.p + new_start[c];
+        J.d_n1 = d_seg + 2 * c + 1;
+        J.n1_ub = seg[2 * c + 1];
+        J.out = m->vox.p + vox_off[c];
+        J.d_out = d_outcnt + c;
+      } else {   // empty second job
+        J.part0 = m->vox.p; J.d_n0 = ctx.zero.p; J.n0_ub = 0;
+        J.out = m->vox.p; J.d_out = ctx.zero.p + 1;
+      }
+    }
+    ProfScope ps(ctx, "map_voxel", FLOAM_PROF_CLOUD, 0.0);
+    voxel2_launch(m->vs, job[0], job[1], st);
+  }
+  // 5. the new map in cell order
+  cloud_reserve(&m->next, std::max(total_ub, 1), 0, st);
+  MapCopyArgs c{};
+  c.ncell = nc; c.outcnt = d_outcnt; c.off = d_off; c.old_start = d_old_start; c.seg = d_seg;
+  c.new_start = d_new_start; c.vox_off = d_vox_off; c.old_map = m->map.pts.p; c.new_pts = m->sorted.p;
+  c.vox = m->vox.p; c.out = m->next.pts.p; c.d_total = m->next.count.p;
+  {
+    ProfScope ps(ctx, "map_rebuild", FLOAM_PROF_CLOUD, 64.0 * total_ub);
+    map_rebuild_launch(c, total_ub, st);
+  }
+  FLOAM_HIP(hipMemcpyAsync(hv + 5 * nc, d_outcnt, sizeof(int) * (size_t)nc, hipMemcpyDeviceToHost, st));
+  FLOAM_HIP(hipStreamSynchronize(st));
+  m->keys.clear();
+  m->counts.clear();
+  size_t total = 0;
+  for (int k = 0; k < nc; ++k) {
+    const int v = hv[5 * nc + k];
+    if (v < 0) throw Error(FLOAM_ERR_DEVICE, "voxel-grid compaction failed (lookback timeout)");
+    if (v == 0) continue;   // empty cells contribute nothing to getMap
+    m->keys.push_back(keys[k]);
+    m->counts.push_back(v);
+    total += (size_t)v;
+  }
+  cloud_swap(&m->map, &m->next);
+  m->map.host_count = total;
+  m->map.host_count_valid = true;
+  m->map.last_stream = st;
+}
+}  // namespace
+
+extern "C" {
+
+floam_status floam_mapping_create(double map_resolution, int device, floam_mapping** out) {
+  return guarded([&] {
+    if (!out) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null out");
+    if (!(map_resolution > 0.0)) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "map_resolution must be > 0");
+    ctx_for(device);
+    FLOAM_HIP(hipSetDevice(device));
+    auto m = std::make_unique<floam_mapping>();
+    m->device = device;
+    m->leaf = (float)map_resolution;   // downSizeFilter.setLeafSize (src/laserMappingClass.cpp:31)
+    cloud_init(&m->map, device, 0);
+    cloud_init(&m->next, device, 0);
+    *out = m.release();
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_mapping_destroy(floam_mapping* m) {
+  return guarded([&] {
+    if (m) {
+      FLOAM_HIP(hipStreamSynchronize(ctx_for(m->device).stream));
+      delete m;
+    }
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_mapping_update(floam_mapping* m, const floam_cloud* in, const double q_xyzw[4], const double t[3]) {
+  return guarded([&] {
+    if (!m || !in || !q_xyzw || !t) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
+    if (in->device != m->device) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "cloud and handle on different devices");
+    mapping_update(m, in, q_xyzw, t);
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_mapping_size(const floam_mapping* m, size_t* n) {
+  return guarded([&] {
+    if (!m || !n) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
+    *n = m->map.host_count;
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_mapping_get_map(floam_mapping* m, floam_cloud* out) {
+  return guarded([&] {
+    if (!m || !out) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
+    if (out->device != m->device) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "cloud and handle on different devices");
+    DeviceCtx& ctx = ctx_for(m->device);
+    cloud_on_main(out);
+    const size_t n = m->map.host_count;
+    cloud_reserve(out, std::max<size_t>(n, 1), 0, ctx.stream);
+    if (n)
+      FLOAM_HIP(hipMemcpyAsync(out->pts.p, m->map.pts.p, n * sizeof(PointRec), hipMemcpyDeviceToDevice, ctx.stream));
+    FLOAM_HIP(hipMemcpyAsync(out->count.p, m->map.count.p, sizeof(int), hipMemcpyDeviceToDevice, ctx.stream));
+    out->host_count = n;
+    out->host_count_valid = true;
     return FLOAM_OK;
   });
 }

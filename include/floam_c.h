@@ -167,6 +167,23 @@ floam_status floam_cloud_from_pointcloud2(floam_cloud* out, int point_type, cons
  * SaveMerged's per-keyframe transform (src/odomEstimationNode.cpp:72-76). */
 floam_status floam_transform_cloud(const floam_cloud* in, const double m[16], floam_cloud* out);
 
+/* ------------------------------------------------------------------------------- LaserMappingClass */
+/* The mapping node's global map (src/laserMappingClass.cpp): 50-m cells of pcl::PointXYZI,
+ * VoxelGrid(map_resolution) of the 5 x 5 x 5 cells around the pose after every update. */
+typedef struct floam_mapping floam_mapping;
+/* LaserMappingClass() + init(map_resolution) (src/laserMappingClass.cpp:7-32) */
+floam_status floam_mapping_create(double map_resolution, int device, floam_mapping** out);
+floam_status floam_mapping_destroy(floam_mapping* m);
+/* updateCurrentPointsToMap(pc_in, pose_current) (src/laserMappingClass.cpp:148-186), the pose as the node builds it
+ * from /odom (Isometry3d::Identity().rotate(q).pretranslate(t), src/laserMappingNode.cpp:108-110): points
+ * transformed by pose.cast<float>(), intensity = min(1, max(z_in + 2, 0) / 5), appended to their cells, then the
+ * neighbourhood's cells voxel-filtered in place.  Points beyond the reference's allocated cells (out of bounds
+ * there) are kept in their cells.  Two synchronisations. */
+floam_status floam_mapping_update(floam_mapping* m, const floam_cloud* pc_in, const double q_xyzw[4], const double t[3]);
+/* getMap() (src/laserMappingClass.cpp:188-200): every cell's points in (x, y, z) cell order; `out` is replaced. */
+floam_status floam_mapping_get_map(floam_mapping* m, floam_cloud* out);
+floam_status floam_mapping_size(const floam_mapping* m, size_t* n);
+
 /* -------------------------------------------------------------------------------- OdomEstimationClass */
 typedef struct floam_odom floam_odom;
 

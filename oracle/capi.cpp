@@ -173,4 +173,13 @@ void oracle_transform_cloud(const void* in, size_t n, const double* m, void* out
   transform_cloud(static_cast<const Pt*>(in), n, m, static_cast<Pt*>(out));
 }
 
+// ---- global map (oracle/mapping.cpp)
+void* oracle_mapping_create(double res, int stable) { return mapping_create(res, stable != 0); }
+void oracle_mapping_destroy(void* h) { mapping_destroy(static_cast<MappingState*>(h)); }
+void oracle_mapping_update(void* h, const void* in, size_t n, const double* q, const double* t) {
+  mapping_update(static_cast<MappingState*>(h), static_cast<const Pt*>(in), n, q, t);
+}
+size_t oracle_mapping_size(void* h) { return mapping_size(static_cast<MappingState*>(h)); }
+void oracle_mapping_get_map(void* h, void* out) { mapping_get_map(static_cast<MappingState*>(h), static_cast<Pt*>(out)); }
+
 }  // extern "C"

@@ -147,6 +147,15 @@ int from_pointcloud2(int point_type, const uint8_t* data, uint32_t width, uint32
                      uint32_t row_step, const Pc2Field* fields, size_t nfields, Pt* out);
 void transform_cloud(const Pt* in, size_t n, const double m[16], Pt* out);
 
+// ---------------------------------------------------------------------------------------------- global map
+// LaserMappingClass (oracle/mapping.cpp)
+struct MappingState;
+MappingState* mapping_create(double map_resolution, bool stable_voxel);
+void mapping_destroy(MappingState* m);
+void mapping_update(MappingState* m, const Pt* in, size_t n, const double q_xyzw[4], const double t[3]);
+size_t mapping_size(const MappingState* m);
+void mapping_get_map(const MappingState* m, Pt* out);
+
 void reset_process_statics();   // KeyFrameUpdate's function-static `first` (odomEstimationClass.cpp:323, Q6)
 double test_edge_eval(const double cp[3], const double a[3], const double b[3], const double* x, double* J);
 double test_surf_eval(const double cp[3], const double n[3], double d, const double* x, double* J);
