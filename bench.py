@@ -199,13 +199,14 @@ def main():
     poses = []
     run(lp, odo, 0, args.warmup, poses)
     barrier_sync()
+    host_split[:] = [0.0, 0.0]
     t_start = time.perf_counter()
     run(lp, odo, args.warmup, n_scans, poses)
     barrier_sync()
     elapsed = time.perf_counter() - t_start
     if os.environ.get("FLOAM_BENCH_HOST"):
-        log(f"[host] per scan over the whole run: issue {1e6 * host_split[0] / n_scans:.0f} us, "
-            f"wait {1e6 * host_split[1] / n_scans:.0f} us")
+        log(f"[host] per timed scan: issue {1e6 * host_split[0] / args.steps:.0f} us, "
+            f"wait {1e6 * host_split[1] / args.steps:.0f} us")
     _ffi.check(L.floam_profile_enable(dev, 0))
     if dist is not None:
         import torch

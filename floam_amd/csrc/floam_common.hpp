@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstdint>
@@ -81,7 +82,9 @@ struct DevBuf {
     if (n <= cap) return;
     if (alloc_log()) std::fprintf(stderr, "[floam alloc] %zu x %zu B (had %zu)\n", n, sizeof(T), cap);
     release();
-    size_t c = n < 1024 ? 1024 : n + n / 2;   // headroom: a reallocation (hipFree) stalls the device
+    // headroom: a reallocation (hipFree) stalls the whole device for 100-500 us, so the arrays that grow with the
+    // map double and start at 1 M elements (HBM is plentiful; the steady state must not reallocate)
+    size_t c = n < 1024 ? 1024 : (n < 4096 ? n + n / 2 : std::max(2 * n, (size_t)1 << 20));
     FLOAM_HIP(hipMalloc(&p, c * sizeof(T)));
     cap = c;
   }
@@ -124,4 +127,6 @@ struct floam_cloud {
   hipStream_t last_stream = nullptr;
   hipEvent_t ev = nullptr;
   bool ev_valid = false;            // ev recorded after the last operation (else recorded lazily when needed)
+  bool clear_pending = false;       // floam_cloud_clear: the device count is zeroed by the cloud's next operation,
+                                    // on that operation's stream
 };

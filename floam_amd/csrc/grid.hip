@@ -194,13 +194,7 @@ void reserve_grid(Grid& g, int ub) {
   g.counters.reserve(8);
   int bits = 10;
   while ((1 << bits) < 2 * ub) ++bits;   // load <= 1/2 (cells <= points)
-  if (bits > g.bits) {
-    g.fine.release();
-    g.coarse.release();
-    for (int k = 0; k < 2; ++k) {
-      g.clist[k].release();
-      g.flist[k].release();
-    }
+  if (bits > g.bits) {   // (reserve keeps the arrays when their capacity already covers the larger table)
     g.fine.reserve((size_t)1 << bits);
     g.coarse.reserve((size_t)1 << bits);
     for (int k = 0; k < 2; ++k) {

@@ -147,6 +147,10 @@ static void cloud_on(const floam_cloud* cc, hipStream_t s) {
   }
   c->last_stream = s;
   c->ev_valid = false;
+  if (c->clear_pending) {
+    FLOAM_HIP(hipMemsetAsync(c->count.p, 0, sizeof(int), s));
+    c->clear_pending = false;
+  }
 }
 static void cloud_on_main(const floam_cloud* c) { cloud_on(c, ctx_for(c->device).stream); }
 static void cloud_publish(const floam_cloud* cc, hipStream_t s) {   // after an operation on a side stream
@@ -177,7 +181,8 @@ static size_t cloud_ub(const floam_cloud* c) { return c->host_count_valid ? c->h
 // grow keeping the first `keep` points (stream-ordered copy, then the old buffer is freed after a sync)
 static void cloud_reserve(floam_cloud* c, size_t n, size_t keep, hipStream_t st) {
   if (n <= c->pts.cap) return;
-  const size_t cap = std::max<size_t>(n + n / 2, 1024);
+  const size_t cap = n < 4096 ? std::max<size_t>(n + n / 2, 1024) : std::max<size_t>(2 * n, (size_t)1 << 20);
+  if (DevBuf<int>::alloc_log()) std::fprintf(stderr, "[floam alloc] cloud %zu pts (had %zu)\n", n, c->pts.cap);
   PointRec* p = nullptr;
   FLOAM_HIP(hipMalloc(&p, cap * sizeof(PointRec)));
   if (keep && c->pts.p) {
@@ -251,6 +256,8 @@ struct floam_odom {
   DevBuf<double> gmat;                  // the solve's surf Gram matrix + its origin
   DevBuf<unsigned> gcnt;                // ticket words of its reduction
   DevBuf<unsigned long long> dbg_stamps;   // FLOAM_DEBUG_STAMPS=1: lm_step segment times (diagnostic)
+  int qhint[2] = {0, 0};                   // recent downsampled edge / surf query counts (search grid sizing)
+  DevBuf<unsigned long long> knn_trace;    // FLOAM_KNN_TRACE=file: per-wave (start, end) of the kNN launch (diagnostic)
   DevBuf<LMState> lm;
   // status slots, two per in-flight update (first / only call, second call of a deskewed selector)
   DevBuf<UpdateStatus> ustat;
@@ -401,6 +408,7 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
     FLOAM_HIP(hipMemsetAsync(o->step_counter.p, 0, sizeof(unsigned), st));
     const char* pe = std::getenv("FLOAM_LM_MODE");
     o->lm_mode = pe ? std::atoi(pe) : 0;
+    if (std::getenv("FLOAM_KNN_TRACE")) o->knn_trace.reserve(1u << 17);
     if (std::getenv("FLOAM_DEBUG_STAMPS")) {
       o->dbg_stamps.reserve(32);
       FLOAM_HIP(hipMemsetAsync(o->dbg_stamps.p, 0, sizeof(unsigned long long) * 32, st));
@@ -413,8 +421,12 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
     o->prof_bytes_init = true;
   }
   o->sums.reserve(LM_NSUM);
-  const QuerySet qe{o->dE.p, o->cnt.p + 0, ne_ub};
-  const QuerySet qs{o->dS.p, o->cnt.p + 1, ns_ub};
+  // the search grid is sized from the downsampled counts seen recently (the device count of this call is not
+  // known on the host without a sync); the kernel grid-strides, so an underestimate only costs time
+  QuerySet qe{o->dE.p, o->cnt.p + 0, ne_ub};
+  QuerySet qs{o->dS.p, o->cnt.p + 1, ns_ub};
+  if (o->qhint[0] > 0) qe.grid_hint = std::min(ne_ub, o->qhint[0] + o->qhint[0] / 4 + 256);
+  if (o->qhint[1] > 0) qs.grid_hint = std::min(ns_ub, o->qhint[1] + o->qhint[1] / 4 + 256);
   const bool sharded = o->world > 1;
   // the single-block Gram solve (squared loss, bounded edge count); else one launch per evaluation (or lm_solve)
   // squared loss: surf sums from the Gram matrix (resident solve, or one launch per evaluation); else per record
@@ -435,7 +447,7 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
         // (also resets the LM state; the first solve starts at the prediction)
         knn_launch(o->lm.p, nullptr, it == 0 ? x0_dev : nullptr, qe, o->gE, o->mapE.pts.p,
                    o->ce, qs, o->gS, o->mapS.pts.p, o->cs, o->mapE.count.p, o->mapS.count.p, o->rank, o->world, st,
-                   o->dbg_stamps.p ? o->dbg_stamps.p + 8 : nullptr);
+                   o->knn_trace.p ? o->knn_trace.p : (o->dbg_stamps.p ? o->dbg_stamps.p + 8 : nullptr));
       }
       ProfScope ps2(ctx, "knn_geometry", FLOAM_PROF_KNN_DETAIL);
       geom_launch(o->lm.p, qe, o->gE, o->mapE.pts.p, o->ce, qs, o->gS, o->mapS.pts.p, o->cs,
@@ -490,6 +502,7 @@ floam_status odom_call_status(floam_odom* o, const UpdateStatus& U) {
   o->stats.solves = gate ? o->optimization_count : 0;
   o->stats.edge_queries = hc[0];
   o->stats.surf_queries = hc[1];
+  for (int k = 0; k < 2; ++k) o->qhint[k] = std::max(o->qhint[k] - o->qhint[k] / 8, hc[k]);   // decaying max
   o->stats.edge_correspondences = gate ? L.corr_edge : 0;
   o->stats.surf_correspondences = gate ? L.corr_surf : 0;
   o->stats.lm_iterations = gate ? L.iteration : 0;
@@ -828,9 +841,9 @@ floam_status floam_cloud_download(const floam_cloud* c, void* host, size_t capac
 floam_status floam_cloud_clear(floam_cloud* c) {
   return guarded([&] {
     if (!c) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null cloud");
-    DeviceCtx& ctx = ctx_for(c->device);
-    cloud_on_main(c);
-    FLOAM_HIP(hipMemsetAsync(c->count.p, 0, sizeof(int), ctx.stream));
+    // deferred to the cloud's next operation (cloud_on), so that clearing a feature buffer for the next scan does
+    // not queue a fill on the odometry stream between two updates
+    c->clear_pending = true;
     c->host_count = 0;
     c->host_count_valid = true;
     return FLOAM_OK;
@@ -1055,6 +1068,14 @@ floam_status floam_odom_destroy(floam_odom* o) {
       for (auto& row : o->graph_exec)
         for (auto& ex : row)
           if (ex) FLOAM_HIP(hipGraphExecDestroy(ex));
+      if (o->knn_trace.p) {   // the last kNN launch's per-wave stamps, raw (2 x u64 per wave)
+        std::vector<unsigned long long> h((size_t)1 << 17);
+        FLOAM_HIP(hipMemcpy(h.data(), o->knn_trace.p, h.size() * 8, hipMemcpyDeviceToHost));
+        if (FILE* f = std::fopen(std::getenv("FLOAM_KNN_TRACE"), "wb")) {
+          std::fwrite(h.data(), 8, h.size(), f);
+          std::fclose(f);
+        }
+      }
       if (o->dbg_stamps.p) {
         unsigned long long h[32];
         FLOAM_HIP(hipMemcpy(h, o->dbg_stamps.p, sizeof(h), hipMemcpyDeviceToHost));

@@ -567,15 +567,12 @@ __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArg
                                           int* __restrict__ s_start) {
   const int n = min(*A.d_n, A.n_ub);
   const int lo = (int)(((long long)n * rank) / world), hi = (int)(((long long)n * (rank + 1)) / world);
-  unsigned long long dsum[6] = {0, 0, 0, 0, 0, 0};
-  unsigned long long ts = 0;
   // grid-stride over the queries the device holds (the host only knows an upper bound)
   for (int i0 = 0; i0 < n; i0 += ngroups) {
     const int i = i0 + gid;   // query
     if (i >= n) break;
     int flags = 0;
     if (i >= lo && i < hi && gate) {
-      if (A.dbg) ts = __builtin_amdgcn_s_memrealtime();
       const float4 pq = *reinterpret_cast<const float4*>(&A.q[i].x);
       float wx, wy, wz;
       associate_to_map(pose, pq.x, pq.y, pq.z, wx, wy, wz);   // pointAssociateToMap (:126-135)
@@ -589,11 +586,6 @@ __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArg
                                 t, cnt);
       group_merge<G>(t, cnt);
       const bool complete = cnt >= 5 && __uint_as_float((unsigned)(t.k[4] >> 32)) < 0.25f;
-      if (A.dbg) {
-        const unsigned long long tn = __builtin_amdgcn_s_memrealtime();
-        dsum[0] += tn - ts;
-        ts = tn;
-      }
       if (!complete) {   // coarse cells floor(q - 1) .. floor(q + 1) per axis (exact in double)
 #pragma unroll
         for (int k = 0; k < 5; ++k) t.k[k] = ~0ull;
@@ -604,11 +596,6 @@ __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArg
                                  s_start, t, cnt);
         group_merge<G>(t, cnt);
         flags |= 2;
-        if (A.dbg) {
-          const unsigned long long tn = __builtin_amdgcn_s_memrealtime();
-          dsum[1] += tn - ts;
-          dsum[2] += 1;
-        }
       }
       if (cnt >= 5) {   // sqd[4] < 1 (:154, :210)
         flags |= 1;
@@ -623,20 +610,16 @@ __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArg
           A.nnxyz[(3 * lane + 2) * A.cap + i] = m.z;
         }
       }
-      if (A.dbg) dsum[4] += 1;
     }
     if (lane == 0) A.valid[i] = (uint8_t)flags;
   }
-  if (A.dbg && lane == 0 && dsum[4])
-#pragma unroll
-    for (int k = 0; k < 6; ++k) atomicAdd(&A.dbg[k], dsum[k]);
 }
 
 // Edge and surf kNN in one launch: blocks [0, nbE) run edge groups, the others surf groups.  The launch also starts
 // the solve (lm_init folded in): block 0 resets the LM state and, for the first solve of an update, stores the
 // prediction x0 that every block uses for its transforms (the others never read st->x in that case).
-template <int G, int U>
-__global__ __launch_bounds__(kTB) void knn_kernel(LMState* __restrict__ st, X7 x0, const double* __restrict__ x0_dev,
+template <int G, int U, int W>
+__global__ __launch_bounds__(kTB, W) void knn_kernel(LMState* __restrict__ st, X7 x0, const double* __restrict__ x0_dev,
                                                   CorrArgs E, CorrArgs S, int nbE,
                                                   const int* __restrict__ d_me, const int* __restrict__ d_ms,
                                                   int rank, int world) {
@@ -664,9 +647,18 @@ __global__ __launch_bounds__(kTB) void knn_kernel(LMState* __restrict__ st, X7 x
   int p = edge ? (int)blockIdx.x : (int)blockIdx.x - nbE;
   const int nq = min(*A.d_n, A.n_ub);
   const int nact = min(nb, (int)(((long long)nq * G + kTB - 1) / kTB));
+  const unsigned long long t_start = E.dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  const bool had = p < nact;
   if (p < nact) p = xcd_block(p, nact);
   knn_group<G, U>(pose, A, (p * kTB + (int)threadIdx.x) / G, nb * (kTB / G), lane, gate, rank, world, s_pre[g],
                   s_start[g]);
+  if (E.dbg && (threadIdx.x & 63) == 0) {   // FLOAM_KNN_TRACE: per-wave (start, end) of the launch (diagnostic)
+    const unsigned w = blockIdx.x * (kTB / 64) + (threadIdx.x >> 6);
+    if (w < (1u << 16)) {
+      E.dbg[2 * w] = t_start | (had ? (1ull << 63) : 0ull);
+      E.dbg[2 * w + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
 }
 
 // Pass 2: fp64 line / plane geometry, one query per lane (all 64 lanes busy).
@@ -1378,6 +1370,7 @@ __device__ __forceinline__ void next_step_wave(LMState& s, bool check_gmax, int 
       check_gmax = false;
       if (s.gmax <= 1e-10) { s.done = 1; return; }   // (phase 0: before any step; phase 1: success && gmax)
     }
+    CTRL_STAMP(5, ts);
     s.iteration++;
     if (valid) {
 #pragma unroll
@@ -1404,6 +1397,9 @@ __device__ __forceinline__ double norm7(const double (&a)[7]) {
 // One Ceres control step after an evaluation (sums = cost, J^T J, J^T r, count at x in phase 0, else at cand).
 // Called by all 64 lanes of one wave with identical s and sums; every lane ends with the same s.
 __device__ __forceinline__ void lm_logic(LMState& s, const double (&sums)[LM_NSUM], int lane) {
+#ifdef FLOAM_CTRL_STAMPS
+  unsigned long long ts = __builtin_amdgcn_s_memrealtime();
+#endif
   if (s.phase == 0) {   // IterationZero
     s.n_res = (int)sums[28];
     if (s.n_res == 0) { s.done = 1; return; }   // no residual blocks: parameters untouched
@@ -1423,6 +1419,7 @@ __device__ __forceinline__ void lm_logic(LMState& s, const double (&sums)[LM_NSU
     s.invalid = 0;
     s.iteration = 0;
     s.phase = 1;
+    CTRL_STAMP(4, ts);
     next_step_wave(s, true, lane);
     return;
   }
@@ -1459,6 +1456,7 @@ __device__ __forceinline__ void lm_logic(LMState& s, const double (&sums)[LM_NSU
     s.reuse = 1;
   }
   if (s.iteration >= 4 || s.radius < 1e-32) { s.done = 1; return; }
+  CTRL_STAMP(6, ts);
   next_step_wave(s, success, lane);
 }
 
@@ -2108,12 +2106,18 @@ static void corr_args(const QuerySet& qe, const Grid& ge, const PointRec* mapE, 
                cs.valid.p, cs.nnxyz.p, cs.cap, dbg ? dbg + 8 : nullptr};
 }
 
-template <int G, int U>
+template <int G, int U, int W = 1>
 static void knn_launch_t(LMState* d_st, const X7& x0, const double* x0_dev, const QuerySet& qe, const QuerySet& qs, const CorrArgs& E,
                          const CorrArgs& S, const int* d_me, const int* d_ms, int rank, int world, hipStream_t st) {
-  const unsigned nbE = std::min(div_up((size_t)std::max(qe.n_ub, 1) * G, kTB), 4096u);
-  const unsigned nbS = std::min(div_up((size_t)std::max(qs.n_ub, 1) * G, kTB), 8192u);
-  hipLaunchKernelGGL((knn_kernel<G, U>), dim3(nbE + nbS), dim3(kTB), 0, st, d_st, x0, x0_dev, E, S, (int)nbE, d_me,
+  static const unsigned cap = [] {   // FLOAM_KNN_MAXBLOCKS: grid cap per query set (tuning only)
+    const char* v = std::getenv("FLOAM_KNN_MAXBLOCKS");
+    return v ? (unsigned)std::atoi(v) : 8192u;
+  }();
+  const int nE = qe.grid_hint > 0 ? std::min(qe.grid_hint, qe.n_ub) : qe.n_ub;
+  const int nS = qs.grid_hint > 0 ? std::min(qs.grid_hint, qs.n_ub) : qs.n_ub;
+  const unsigned nbE = std::min(div_up((size_t)std::max(nE, 1) * G, kTB), std::min(cap, 4096u));
+  const unsigned nbS = std::min(div_up((size_t)std::max(nS, 1) * G, kTB), cap);
+  hipLaunchKernelGGL((knn_kernel<G, U, W>), dim3(nbE + nbS), dim3(kTB), 0, st, d_st, x0, x0_dev, E, S, (int)nbE, d_me,
                      d_ms, rank, world);
   FLOAM_LAUNCH_CHECK();
 }
@@ -2143,6 +2147,9 @@ void knn_launch(LMState* d_st, const double* x0, const double* x0_dev, const Que
     case 3: knn_launch_t<32, 2>(d_st, x, x0_dev, qe, qs, E, S, d_me, d_ms, rank, world, st); break;
     case 4: knn_launch_t<16, 2>(d_st, x, x0_dev, qe, qs, E, S, d_me, d_ms, rank, world, st); break;
     case 5: knn_launch_t<4, 4>(d_st, x, x0_dev, qe, qs, E, S, d_me, d_ms, rank, world, st); break;
+    case 6: knn_launch_t<16, 4, 6>(d_st, x, x0_dev, qe, qs, E, S, d_me, d_ms, rank, world, st); break;
+    case 7: knn_launch_t<16, 2, 6>(d_st, x, x0_dev, qe, qs, E, S, d_me, d_ms, rank, world, st); break;
+    case 8: knn_launch_t<16, 2, 8>(d_st, x, x0_dev, qe, qs, E, S, d_me, d_ms, rank, world, st); break;
     default: knn_launch_t<kGroupDefault, kUnrollDefault>(d_st, x, x0_dev, qe, qs, E, S, d_me, d_ms, rank, world, st); break;
   }
 }

@@ -97,6 +97,7 @@ struct QuerySet {
   const PointRec* pts;
   const int* d_n;
   int n_ub;
+  int grid_hint = 0;   // > 0: size the search grid for this many queries (the kernels grid-stride over the rest)
 };
 
 struct X7 {

@@ -148,7 +148,7 @@ void RadixScratch::reserve(int n, hipStream_t st) {
   }
   const int tiles = (int)div_up((unsigned)std::max(n, 1), (unsigned)kTile);
   if (tiles > tiles_cap) {
-    const int cap = tiles + tiles / 4 + 4;
+    const int cap = std::max(tiles + tiles / 4 + 4, 1024);   // 2 M elements before a reallocation (device stall)
     status.release();
     status.reserve((size_t)kRadixPasses * cap * kRadixDigits);
     // a fresh array: make every word's epoch field differ from the next epochs
