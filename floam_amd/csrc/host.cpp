@@ -259,6 +259,16 @@ struct floam_odom {
   int qhint[2] = {0, 0};                   // recent downsampled edge / surf query counts (search grid sizing)
   DevBuf<unsigned long long> knn_trace;    // FLOAM_KNN_TRACE=file: per-wave (start, end) of the kNN launch (diagnostic)
   DevBuf<LMState> lm;
+  // call 1 of a deskewed selector downsamples the edge cloud only (Q4), in the sensor frame: that VoxelGrid runs on a
+  // side stream as soon as the scan's features exist, overlapped with the previous update (double-buffered by parity)
+  hipStream_t side = nullptr;
+  hipEvent_t side_ev[2] = {nullptr, nullptr};     // call-1 buffers of a parity consumed (recorded on the main stream)
+  bool side_ev_rec[2] = {false, false};
+  DevBuf<PointRec> pE[2], pS[2];
+  DevBuf<int> pcnt[2];
+  VoxelScratch2 vs1;
+  int pre_par = 0;
+  int pre_valid = -1;                             // parity of the pre-downsampled call-1 clouds awaiting their update
   // status slots, two per in-flight update (first / only call, second call of a deskewed selector)
   DevBuf<UpdateStatus> ustat;
   HostBuf<UpdateStatus> h_ustat;
@@ -379,13 +389,17 @@ void allreduce_sums(floam_odom* o, DeviceCtx& ctx) {
 //   odom_map_update      addPointsToMap (:253-294), gated on the device by the keyframe decision
 // then one device-to-host copy of the status slots; odom_collect reads them (errors, warnings, stats, poses, map
 // sizes) — right away in synchronous mode, later in asynchronous mode.
+// pre >= 0: the call's clouds were downsampled on the side stream into the parity-`pre` buffers (odom_prevoxel)
 void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const floam_cloud* surf, int ne_ub, int ns_ub,
-                const double* x0_dev, int slot, int gather_mode) {
+                const double* x0_dev, int slot, int gather_mode, int pre = -1) {
   hipStream_t st = ctx.stream;
   o->dE.reserve(std::max(ne_ub, 1));
   o->dS.reserve(std::max(ns_ub, 1));
   o->cnt.reserve(4);
-  {
+  PointRec* const dE = pre >= 0 ? o->pE[pre].p : o->dE.p;
+  PointRec* const dS = pre >= 0 ? o->pS[pre].p : o->dS.p;
+  int* const dcnt = pre >= 0 ? o->pcnt[pre].p : o->cnt.p;
+  if (pre < 0) {
     ProfScope ps(ctx, "voxel_downsample", FLOAM_PROF_CLOUD);
     // VelToIntensityCopy + downSamplingToMap (:53-54, :75, :137-142): both grids in one pipeline
     VoxelJob je, js;
@@ -423,8 +437,8 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
   o->sums.reserve(LM_NSUM);
   // the search grid is sized from the downsampled counts seen recently (the device count of this call is not
   // known on the host without a sync); the kernel grid-strides, so an underestimate only costs time
-  QuerySet qe{o->dE.p, o->cnt.p + 0, ne_ub};
-  QuerySet qs{o->dS.p, o->cnt.p + 1, ns_ub};
+  QuerySet qe{dE, dcnt + 0, ne_ub};
+  QuerySet qs{dS, dcnt + 1, ns_ub};
   if (o->qhint[0] > 0) qe.grid_hint = std::min(ne_ub, o->qhint[0] + o->qhint[0] / 4 + 256);
   if (o->qhint[1] > 0) qs.grid_hint = std::min(ns_ub, o->qhint[1] + o->qhint[1] / 4 + 256);
   const bool sharded = o->world > 1;
@@ -462,30 +476,30 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
     // iteration zero + at most max_num_iterations = 4 candidates (odomEstimationClass.cpp:102)
     if (gram && o->lm_mode == 0) {
       ProfScope ps(ctx, "lm_solve", FLOAM_PROF_LM);
-      lm_solve_gram_launch(o->lm.p, o->ce, o->cnt.p + 0, ne_ub, o->gpart.p, o->gmat.p, o->partials.p,
+      lm_solve_gram_launch(o->lm.p, o->ce, dcnt + 0, ne_ub, o->gpart.p, o->gmat.p, o->partials.p,
                            o->step_counter.p, st, o->dbg_stamps.p);
       continue;
     }
     for (int ev = 0; ev < 5; ++ev) {
       ProfScope ps(ctx, "lm_step", FLOAM_PROF_LM);
       if (gram) {
-        lm_step_gram_launch(o->lm.p, o->ce, o->cnt.p + 0, ne_ub, o->gpart.p, o->gmat.p, false, o->partials.p,
+        lm_step_gram_launch(o->lm.p, o->ce, dcnt + 0, ne_ub, o->gpart.p, o->gmat.p, false, o->partials.p,
                             o->step_counter.p, st, o->dbg_stamps.p);
       } else if (sharded) {
-        const int nblk = lm_eval_launch(o->lm.p, o->ce, o->cnt.p + 0, ne_ub, o->cs, o->cnt.p + 1, ns_ub, o->huber,
+        const int nblk = lm_eval_launch(o->lm.p, o->ce, dcnt + 0, ne_ub, o->cs, dcnt + 1, ns_ub, o->huber,
                                         o->partials.p, st);
         lm_reduce_launch(o->partials.p, nblk, o->sums.p, st);
         allreduce_sums(o, ctx);
         lm_control_launch(o->lm.p, o->sums.p, 0, st);
       } else {
-        lm_step_launch(o->lm.p, o->ce, o->cnt.p + 0, ne_ub, o->cs, o->cnt.p + 1, ns_ub, o->huber, o->partials.p,
+        lm_step_launch(o->lm.p, o->ce, dcnt + 0, ne_ub, o->cs, dcnt + 1, ns_ub, o->huber, o->partials.p,
                        o->step_counter.p, st, o->dbg_stamps.p);
       }
     }
   }
   if (o->optimization_count <= 0) lm_init_dev_launch(o->lm.p, x0_dev, st);
   const bool prof_knn = (ctx.profile & FLOAM_PROF_KNN_BYTES) != 0;
-  gather_status_launch(o->lm.p, o->cnt.p, o->mapE.count.p, o->mapS.count.p, edge->fe_status,
+  gather_status_launch(o->lm.p, dcnt, o->mapE.count.p, o->mapS.count.p, edge->fe_status,
                        prof_knn ? o->prof_bytes.p : nullptr, o->ustat.p + slot, o->ds.p, gather_mode, st);
   if (prof_knn) FLOAM_HIP(hipMemsetAsync(o->prof_bytes.p, 0, sizeof(unsigned long long) * 2, st));
 }
@@ -706,10 +720,38 @@ floam_status odom_update(floam_odom* o, const floam_cloud* edge, const floam_clo
   }
 }
 
+// Call 1's VoxelGrids (edge cloud at the edge and the surf leaf, Q4) on the side stream, ordered after the cloud's
+// producer (the feature extraction) and after the update that last used this parity's buffers; the main stream
+// orders itself after it through the cloud (cloud_on_main).  Not used while an update is captured into a graph.
+void odom_prevoxel(floam_odom* o, floam_cloud* edge) {
+  if (o->use_graph) return;
+  if (!o->side) {
+    FLOAM_HIP(hipStreamCreateWithFlags(&o->side, hipStreamNonBlocking));
+    for (auto& e : o->side_ev) FLOAM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  const int par = o->pre_par;
+  o->pre_par ^= 1;
+  const int ne_ub = (int)cloud_ub(edge);
+  o->pE[par].reserve(std::max(ne_ub, 1));
+  o->pS[par].reserve(std::max(ne_ub, 1));
+  o->pcnt[par].reserve(2);
+  if (o->side_ev_rec[par]) FLOAM_HIP(hipStreamWaitEvent(o->side, o->side_ev[par], 0));
+  cloud_on(edge, o->side);
+  VoxelJob je, js;
+  je.part0 = edge->pts.p; je.d_n0 = edge->count.p; je.n0_ub = ne_ub; je.leaf = o->leafE;
+  je.out = o->pE[par].p; je.d_out = o->pcnt[par].p + 0;
+  js.part0 = edge->pts.p; js.d_n0 = edge->count.p; js.n0_ub = ne_ub; js.leaf = o->leafS;
+  js.out = o->pS[par].p; js.d_out = o->pcnt[par].p + 1;
+  voxel2_launch(o->vs1, je, js, o->side);
+  o->pre_valid = par;
+}
+
 // UpdatePointsToMapSelector with deskew (src/odomEstimationClass.cpp:38-47): call 1 (edge, edge) INITIAL_ITERATION
 // (Q4), GetVelocity + CompensateVelocity of both clouds in place (Q5), call 2 (edge, surf) REFINEMENT_AND_UPDATE,
 // all issued without a host round trip (the velocity and the second prediction are formed by deskew_bridge).
 floam_status odom_update_deskew(floam_odom* o, floam_cloud* edge, floam_cloud* surf) {
+  const int pre = o->pre_valid;   // consumed by this update whatever happens
+  o->pre_valid = -1;
   DeviceCtx& ctx = ctx_for(o->device);
   FLOAM_HIP(hipSetDevice(o->device));
   const int ring = odom_begin(o, ctx);
@@ -718,7 +760,11 @@ floam_status odom_update_deskew(floam_odom* o, floam_cloud* edge, floam_cloud* s
   try {
     if (o->optimization_count > 2) o->optimization_count--;
     odom_predict_launch(o->ds.p, ctx.stream);
-    odom_issue(o, ctx, edge, edge, ne_ub, ne_ub, o->ds.p->x0[0], 2 * ring, 0);
+    odom_issue(o, ctx, edge, edge, ne_ub, ne_ub, o->ds.p->x0[0], 2 * ring, 0, pre);
+    if (pre >= 0) {   // the side stream may refill this parity's buffers once call 1 has run
+      FLOAM_HIP(hipEventRecord(o->side_ev[pre], ctx.stream));
+      o->side_ev_rec[pre] = true;
+    }
     {
       ProfScope ps(ctx, "deskew", FLOAM_PROF_CLOUD);
       deskew_bridge_launch(o->lm.p, o->ds.p, o->lp.scan_period, edge->pts.p, edge->count.p, ne_ub, surf->pts.p,
@@ -1095,6 +1141,11 @@ floam_status floam_odom_destroy(floam_odom* o) {
                        c[1] / (c[2] ? (double)c[2] : 1.0) / 100.0);
         }
       }
+      if (o->side) {
+        (void)hipStreamSynchronize(o->side);
+        for (auto& e : o->side_ev) (void)hipEventDestroy(e);
+        (void)hipStreamDestroy(o->side);
+      }
       if (o->comm) ncclCommDestroy(o->comm);
       delete o;
     }
@@ -1140,6 +1191,7 @@ floam_status floam_odom_update(floam_odom* o, const floam_cloud* edge, const flo
 floam_status floam_odom_update_selector(floam_odom* o, floam_cloud* edge, floam_cloud* surf, int deskew) {
   return guarded([&] {
     if (!o || !edge || !surf) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
+    if (deskew && edge != surf) odom_prevoxel(o, edge);
     cloud_on_main(edge);
     cloud_on_main(surf);
     if (!deskew) return odom_update(o, edge, surf, FLOAM_VANILLA);
