@@ -627,9 +627,13 @@ __global__ __launch_bounds__(kTB, W) void knn_kernel(LMState* __restrict__ st, X
   __shared__ int s_start[kTB / G][kMaxStencil];
   const int lane = threadIdx.x & (G - 1);
   const int g = threadIdx.x / G;
-  double pose[7];
+  double pose[7];   // wave-uniform: kept in SGPRs (readfirstlane), not in 14 VGPRs of every lane
 #pragma unroll
-  for (int k = 0; k < 7; ++k) pose[k] = x0_dev ? x0_dev[k] : (x0.set ? x0.v[k] : st->x[k]);
+  for (int k = 0; k < 7; ++k) {
+    const long long b = __double_as_longlong(x0_dev ? x0_dev[k] : (x0.set ? x0.v[k] : st->x[k]));
+    const int lo = __builtin_amdgcn_readfirstlane((int)b), hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+    pose[k] = __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+  }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     X7 xs;
     xs.set = (x0_dev || x0.set) ? 1 : 0;
@@ -770,8 +774,9 @@ __global__ __launch_bounds__(kTB) void geom_kernel(LMState* __restrict__ st, Cor
     return;
   }
   const int sb = (int)blockIdx.x - nbE;
+  const int ns = min(*S.d_n, S.n_ub);   // the device count bounds the grid-stride loops (block-uniform)
   if (!gpart) {
-    for (int i0 = sb * kTB; i0 < S.n_ub; i0 += kSurfGeomBlocks * kTB) geom_query<false>(st, S, i0 + threadIdx.x);
+    for (int i0 = sb * kTB; i0 < ns; i0 += kSurfGeomBlocks * kTB) geom_query<false>(st, S, i0 + threadIdx.x);
     return;
   }
   __shared__ double s_w[kTB / 64][kGramW][65];   // padded rows: lanes reading different rows hit different banks
@@ -784,7 +789,7 @@ __global__ __launch_bounds__(kTB) void geom_kernel(LMState* __restrict__ st, Cor
   gram_pair(lane, ei0, ej0);
   if (lane + 64 < kGram) gram_pair(lane + 64, ei1, ej1);
   double g0 = 0.0, g1 = 0.0;
-  for (int i0 = sb * kTB; i0 < S.n_ub; i0 += kSurfGeomBlocks * kTB) {   // wave-uniform trip count
+  for (int i0 = sb * kTB; i0 < ns; i0 += kSurfGeomBlocks * kTB) {   // wave-uniform trip count
     double w[kGramW];
 #pragma unroll
     for (int k = 0; k < kGramW; ++k) w[k] = 0.0;
@@ -1251,27 +1256,39 @@ __host__ __device__ constexpr int hidx(int a, int b) {   // upper-triangle row-m
 // (The oracle solves the equivalent [J; sqrt(D/radius)] least-squares problem by Householder QR like Ceres'
 // DENSE_QR; the two agree to ~cond * eps.)  Returns false for an invalid step; delta = scaled step.
 __device__ __forceinline__ bool solve_step(LMState& s, double (&delta)[6]) {
-  // packed lower triangle (row-major, l(i,j) = i(i+1)/2 + j): Hs = S H S, then A = Hs + diag/radius factored in place
-  double sc[6], gs[6];
+  // every field the step reads is loaded once into registers up front (one LDS round trip), the two LDS writes
+  // (diag, reuse) go out at the end: no store-to-load waits on the state inside the dependent fp64 chain
+  double sc[6], gs[6], Hu[21], dg[6];
 #pragma unroll
   for (int a = 0; a < 6; ++a) {
     sc[a] = s.scale[a];
-    gs[a] = sc[a] * s.g[a];
+    dg[a] = s.diag[a];
   }
-  double A[21];
+#pragma unroll
+  for (int k = 0; k < 21; ++k) Hu[k] = s.H[k];
+#pragma unroll
+  for (int a = 0; a < 6; ++a) gs[a] = sc[a] * s.g[a];
+  const int reuse = s.reuse;
+  const double inv_radius = 1.0 / s.radius;
+  // packed lower triangle (row-major, l(i,j) = i(i+1)/2 + j): Hs = S H S, then A = Hs + diag/radius factored in place
+  double Hs[21], A[21];
 #pragma unroll
   for (int i = 0; i < 6; ++i)
 #pragma unroll
-    for (int j = 0; j <= i; ++j) A[i * (i + 1) / 2 + j] = sc[i] * s.H[hidx(j, i)] * sc[j];
-  if (!s.reuse) {
+    for (int j = 0; j <= i; ++j) {
+      Hs[i * (i + 1) / 2 + j] = sc[i] * Hu[hidx(j, i)] * sc[j];
+      A[i * (i + 1) / 2 + j] = Hs[i * (i + 1) / 2 + j];
+    }
+  if (!reuse) {
 #pragma unroll
-    for (int k = 0; k < 6; ++k) s.diag[k] = fmin(fmax(A[k * (k + 1) / 2 + k], 1e-6), 1e32);
+    for (int k = 0; k < 6; ++k) dg[k] = fmin(fmax(Hs[k * (k + 1) / 2 + k], 1e-6), 1e32);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) s.diag[k] = dg[k];
   }
   s.reuse = 1;
   // Cholesky of A = Hs + diag / radius, with one reciprocal per pivot
-  const double inv_radius = 1.0 / s.radius;
 #pragma unroll
-  for (int k = 0; k < 6; ++k) A[k * (k + 1) / 2 + k] += s.diag[k] * inv_radius;
+  for (int k = 0; k < 6; ++k) A[k * (k + 1) / 2 + k] += dg[k] * inv_radius;
   double rd[6];
   bool pd = true;
 #pragma unroll
@@ -1314,14 +1331,14 @@ __device__ __forceinline__ bool solve_step(LMState& s, double (&delta)[6]) {
     finite = finite && isfinite(y[k]);
   }
   if (!finite) return false;
-  // model cost change -(step^T gs + step^T Hs step / 2), Hs re-formed from the state
+  // model cost change -(step^T gs + step^T Hs step / 2)
   double sg = 0.0, sHs = 0.0;
 #pragma unroll
   for (int a = 0; a < 6; ++a) {
     sg += y[a] * gs[a];
     double hv = 0.0;
 #pragma unroll
-    for (int b = 0; b < 6; ++b) hv += (sc[a] * s.H[a <= b ? hidx(a, b) : hidx(b, a)] * sc[b]) * y[b];
+    for (int b = 0; b < 6; ++b) hv += Hs[a >= b ? a * (a + 1) / 2 + b : b * (b + 1) / 2 + a] * y[b];
     sHs += y[a] * hv;
   }
   const double mcc = -(sg + 0.5 * sHs);
@@ -1332,7 +1349,13 @@ __device__ __forceinline__ bool solve_step(LMState& s, double (&delta)[6]) {
   return true;
 }
 
-__device__ __forceinline__ double bcast(double v, int src) { return __shfl(v, src, 64); }
+// value of lane src (a compile-time / wave-uniform lane) to every lane: two v_readlane (no LDS round trip)
+__device__ __forceinline__ double bcast(double v, int src) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, src);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), src);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
 
 // NextStep with the gradient-norm test folded in: ComputeTrustRegionStep (+ HandleInvalidStep retries) and, when
 // check_gmax, the projected-gradient max norm at x (lane 1) computed alongside the candidate (lane 0).  If the
