@@ -798,6 +798,7 @@ __global__ __launch_bounds__(kTB) void geom_kernel(LMState* __restrict__ st, Cor
     for (int k = 0; k < kGramW; ++k) s_w[wv][k][lane] = w[k];
     wave_lds_order();
     double a0 = 0.0, a1 = 0.0;
+#pragma unroll 16
     for (int r = 0; r < 64; ++r) {
       a0 += s_w[wv][ei0][r] * s_w[wv][ej0][r];
       a1 += s_w[wv][ei1][r] * s_w[wv][ej1][r];
@@ -832,7 +833,11 @@ __global__ __launch_bounds__(kTB) void geom_kernel(LMState* __restrict__ st, Cor
   double* gpart2 = gpart + kSurfGeomBlocks * kGram;   // [8][91] group partials
   if (threadIdx.x < kGram) {
     double v = 0.0;
-    for (int k = 0; k < per; ++k) v += gpart[(grp * per + k) * kGram + threadIdx.x];
+    double gp[per];   // all loads in flight before the in-order sum
+#pragma unroll
+    for (int k = 0; k < per; ++k) gp[k] = gpart[(grp * per + k) * kGram + threadIdx.x];
+#pragma unroll
+    for (int k = 0; k < per; ++k) v += gp[k];
     gpart2[grp * kGram + threadIdx.x] = v;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1105,6 +1110,7 @@ __device__ void store_block_partials(const double (&acc)[LM_NSUM], double* __res
   if (threadIdx.x < LM_NSUM * 8) {
     const int c = threadIdx.x >> 3, p = threadIdx.x & 7;
     double v = 0.0;
+#pragma unroll
     for (int j = 0; j < kTB / 8; ++j) v += red[c][p * (kTB / 8) + j];
     strip[c][p] = v;
   }

@@ -8,3 +8,4 @@ python -c "
 import json; d=json.load(open('gpurun_out/q/bench.json')); r=d['roofline']
 print('scans/s', d['value'], 'ms/step', d['ms_per_step'], 'knn avg us', r['avg_us'], 'frac', r['frac'], 'corr pass', r['correspondence_pass_avg_us'], 'geom', r['knn_geometry_avg_us'], 'pose', d['pose_vs_oracle'])"
 grep host gpurun_out/q/bench.err
+if [ -n "$STAMPS" ]; then FLOAM_DEBUG_STAMPS=1 timeout -k 10 200 python bench.py --steps 20 --cpu-baseline-seconds 0 --no-roofline > gpurun_out/q/st.json 2> gpurun_out/q/st.err; grep stamps gpurun_out/q/st.err | head -3; fi
