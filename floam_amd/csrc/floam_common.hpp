@@ -102,11 +102,11 @@ struct HostBuf {
   ~HostBuf() {
     if (p) (void)hipHostFree(p);
   }
-  void reserve(size_t n) {
+  void reserve(size_t n, unsigned flags = hipHostMallocDefault) {
     if (n <= cap) return;
     if (p) (void)hipHostFree(p);
     p = nullptr;
-    FLOAM_HIP(hipHostMalloc(&p, n * sizeof(T), hipHostMallocDefault));
+    FLOAM_HIP(hipHostMalloc(&p, n * sizeof(T), flags));
     cap = n;
   }
 };

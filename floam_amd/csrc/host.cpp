@@ -270,7 +270,8 @@ struct floam_odom {
   int pre_par = 0;
   int pre_valid = -1;                             // parity of the pre-downsampled call-1 clouds awaiting their update
   // status slots, two per in-flight update (first / only call, second call of a deskewed selector)
-  DevBuf<UpdateStatus> ustat;
+  // written by the gather kernel straight into coherent pinned host memory (no copy launch on the stream); 32 slots
+  // cover the deepest ring (depth 16), so the buffer never moves while updates are in flight
   HostBuf<UpdateStatus> h_ustat;
   DevBuf<OdomDev> ds;             // device-resident controller state (poses, keyframe)
   // updates issued but not yet collected (asynchronous mode keeps up to `depth` of them in flight)
@@ -500,7 +501,7 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
   if (o->optimization_count <= 0) lm_init_dev_launch(o->lm.p, x0_dev, st);
   const bool prof_knn = (ctx.profile & FLOAM_PROF_KNN_BYTES) != 0;
   gather_status_launch(o->lm.p, dcnt, o->mapE.count.p, o->mapS.count.p, edge->fe_status,
-                       prof_knn ? o->prof_bytes.p : nullptr, o->ustat.p + slot, o->ds.p, gather_mode, st);
+                       prof_knn ? o->prof_bytes.p : nullptr, o->h_ustat.p + slot, o->ds.p, gather_mode, st);
   if (prof_knn) FLOAM_HIP(hipMemsetAsync(o->prof_bytes.p, 0, sizeof(unsigned long long) * 2, st));
 }
 
@@ -597,8 +598,7 @@ int odom_begin(floam_odom* o, DeviceCtx& ctx) {
     const floam_status w = odom_collect(o, ctx, (size_t)ring_n - 1);
     if (w != FLOAM_OK) o->last_warning = w;   // reported by the next floam_odom_wait
   }
-  o->ustat.reserve((size_t)2 * ring_n);
-  o->h_ustat.reserve((size_t)2 * ring_n);
+  o->h_ustat.reserve(32, hipHostMallocCoherent);
   return (int)(o->issued++ % (unsigned long long)ring_n);
 }
 
@@ -642,11 +642,10 @@ void odom_capture_end(floam_odom* o, DeviceCtx& ctx, int kind) {
   FLOAM_HIP(hipGraphLaunch(ex, ctx.stream));
 }
 
-// the status copy of the update just issued; synchronous mode collects it right away
+// the end of an issued update (its status slots are written to pinned host memory by the gather kernel); synchronous
+// mode collects it right away
 floam_status odom_end(floam_odom* o, DeviceCtx& ctx, int ring, int nslots, int map_slot, size_t addE, size_t addS,
                       bool captured, int kind) {
-  FLOAM_HIP(hipMemcpyAsync(o->h_ustat.p + 2 * ring, o->ustat.p + 2 * ring, sizeof(UpdateStatus) * nslots,
-                           hipMemcpyDeviceToHost, ctx.stream));
   std::vector<void*> graveyard;
   if (captured) {
     graveyard.swap(capture_state().graveyard);
