@@ -1173,7 +1173,23 @@ __device__ void reduce_partials_block(const double* __restrict__ partials, int n
     const int per = (nblk + 7) / 8;
     const int b0 = p * per, b1 = min(nblk, b0 + per);
     double v = 0.0;
-    for (int bb = b0; bb < b1; ++bb) v += SC1 ? load_sc1(&partials[c * nblk + bb]) : partials[c * nblk + bb];
+    int bb = b0;
+    for (; bb + 8 <= b1; bb += 8) {   // 8 loads in flight, then added in order
+      double t[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) t[k] = SC1 ? load_sc1(&partials[c * nblk + bb + k]) : partials[c * nblk + bb + k];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v += t[k];
+    }
+    {
+      double t[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        t[k] = bb + k < b1 ? (SC1 ? load_sc1(&partials[c * nblk + bb + k]) : partials[c * nblk + bb + k]) : 0.0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (bb + k < b1) v += t[k];
+    }
     strip[c][p] = v;
   }
   __syncthreads();
