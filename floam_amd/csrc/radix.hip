@@ -1,7 +1,7 @@
 // Stable LSD radix sort, one single-pass launch per 8-bit digit (see radix.hpp).
 //
-// A launch sorts by one digit.  Each block takes a ticket (its tile: 256 threads x kItems consecutive elements, so a
-// tile only ever waits on tiles that were already running) and
+// A launch sorts by one digit.  Each block is a tile (256 threads x kItems consecutive elements, tile = block index;
+// blocks are dispatched in index order, so a tile only ever waits on tiles that were already running) and
 //   1. loads its elements: wave w owns the 64 * kItems elements [w * 64 * kItems, ...), lane l element r * 64 + l in
 //      round r, so (round, lane) order is input order;
 //   2. ranks them stably: per round, the lanes holding the same digit find each other with 8 ballots, each takes
@@ -52,7 +52,10 @@ __global__ __launch_bounds__(kTB) void radix_pass(const uint32_t* __restrict__ k
   __shared__ int s_tile;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int shift = 8 * pass;
-  if (t == 0) s_tile = (int)atomicAdd(&ctl[kRadixHistWords + pass], 1u);
+  // the tile is the block index: workgroups are dispatched in index order and a launch has at most a few hundred
+  // tiles, so a tile only waits on tiles that are running or done (no ticket round trip)
+  if (t == 0) s_tile = (int)blockIdx.x;
+  const unsigned h = ctl[pass * kRadixDigits + t];   // digit t's histogram count, loaded with the keys
 #pragma unroll
   for (int k = 0; k < kTB / 64; ++k) s_wcnt[k][t] = 0u;
   __syncthreads();
@@ -92,7 +95,6 @@ __global__ __launch_bounds__(kTB) void radix_pass(const uint32_t* __restrict__ k
   __hip_atomic_store(&st[(size_t)tile * kRadixDigits + t], lb_word(epoch, tile == 0 ? kFlagInc : kFlagAgg, cnt),
                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // bucket start of digit t: exclusive scan of the pass histogram (wave scan + wave totals)
-  const unsigned h = ctl[pass * kRadixDigits + t];
   unsigned incl = h;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -102,20 +104,39 @@ __global__ __launch_bounds__(kTB) void radix_pass(const uint32_t* __restrict__ k
   if (lane == 63) s_wsum[w] = incl;
   unsigned prefix = 0;
   if (tile > 0) {
+    // windowed lookback: the words of the kLbWin nearest unconsumed predecessors are loaded together (one round
+    // trip per window instead of one per predecessor), then consumed in order up to the first inclusive prefix
+    // or the first word not yet published (the walk resumes there)
+    constexpr int kLbWin = 8;
     bool failed = false;
     long long polls = 0;
     for (int j = tile - 1; j >= 0;) {
-      const unsigned long long x =
-          __hip_atomic_load(&st[(size_t)j * kRadixDigits + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned long long flag = x & (3ull << 32);
-      if ((unsigned)(x >> 34) != (epoch & 0x3FFFFFFFu) || flag == 0) {
+      unsigned long long x[kLbWin];
+#pragma unroll
+      for (int k = 0; k < kLbWin; ++k)
+        x[k] = j - k >= 0 ? __hip_atomic_load(&st[(size_t)(j - k) * kRadixDigits + t], __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT)
+                          : 0ull;
+      int consumed = 0;
+      bool done = false, stall = false;
+#pragma unroll
+      for (int k = 0; k < kLbWin; ++k) {
+        if (done || stall || j - k < 0) continue;
+        const unsigned long long flag = x[k] & (3ull << 32);
+        if ((unsigned)(x[k] >> 34) != (epoch & 0x3FFFFFFFu) || flag == 0) {
+          stall = true;
+          continue;
+        }
+        prefix += (unsigned)(x[k] & 0xFFFFFFFFull);
+        ++consumed;
+        if (flag == kFlagInc) done = true;
+      }
+      if (done) break;
+      j -= consumed;
+      if (stall) {
         if (++polls > (1ll << 22)) { failed = true; break; }
         __builtin_amdgcn_s_sleep(1);
-        continue;
       }
-      prefix += (unsigned)(x & 0xFFFFFFFFull);
-      if (flag == kFlagInc) break;
-      --j;
     }
     if (failed) atomicOr(&ctl[kRadixHistWords + 4], 1u);
     __hip_atomic_store(&st[(size_t)tile * kRadixDigits + t], lb_word(epoch, kFlagInc, prefix + cnt), __ATOMIC_RELAXED,

@@ -200,7 +200,8 @@ __global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B,
     }
     return;
   }
-  const int tile = lookback_ticket(ticket);
+  // the tile is the block index (workgroups dispatch in index order: a tile only waits on running or finished tiles)
+  const int tile = (int)blockIdx.x;
   const int total = *n_dev;   // packed elements (vox_keys)
   const int ntiles = (total + kTile - 1) / kTile;
   if (tile >= ntiles) {   // beyond the device's elements (the grid is sized by the host's upper bounds)
