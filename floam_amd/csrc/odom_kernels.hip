@@ -1308,43 +1308,43 @@ __device__ __forceinline__ bool solve_step(LMState& s, double (&delta)[6]) {
     for (int k = 0; k < 6; ++k) s.diag[k] = dg[k];
   }
   s.reuse = 1;
-  // Cholesky of A = Hs + diag / radius, with one reciprocal per pivot
+  // LDL^T of A = Hs + diag / radius (no square roots on the dependent chain; one reciprocal per pivot): W[i][j] =
+  // L[i][j] D[j] is kept beside L, packed lower like A
 #pragma unroll
   for (int k = 0; k < 6; ++k) A[k * (k + 1) / 2 + k] += dg[k] * inv_radius;
-  double rd[6];
+  double W[21], rD[6];
   bool pd = true;
 #pragma unroll
   for (int j = 0; j < 6; ++j) {
     double d = A[j * (j + 1) / 2 + j];
 #pragma unroll
-    for (int k = 0; k < j; ++k) d -= A[j * (j + 1) / 2 + k] * A[j * (j + 1) / 2 + k];
+    for (int k = 0; k < j; ++k) d -= A[j * (j + 1) / 2 + k] * W[j * (j + 1) / 2 + k];
     pd = pd && (d > 0.0);
-    const double ljj = sqrt(d);
-    A[j * (j + 1) / 2 + j] = ljj;
-    rd[j] = 1.0 / ljj;
+    rD[j] = 1.0 / d;
 #pragma unroll
     for (int i = j + 1; i < 6; ++i) {
       double v = A[i * (i + 1) / 2 + j];
 #pragma unroll
-      for (int k = 0; k < j; ++k) v -= A[i * (i + 1) / 2 + k] * A[j * (j + 1) / 2 + k];
-      A[i * (i + 1) / 2 + j] = v * rd[j];
+      for (int k = 0; k < j; ++k) v -= A[i * (i + 1) / 2 + k] * W[j * (j + 1) / 2 + k];
+      W[i * (i + 1) / 2 + j] = v;            // L[i][j] D[j]
+      A[i * (i + 1) / 2 + j] = v * rD[j];    // L[i][j]
     }
   }
   if (!pd) return false;
   double y[6];
 #pragma unroll
-  for (int i = 0; i < 6; ++i) {
+  for (int i = 0; i < 6; ++i) {   // L z = gs
     double v = gs[i];
 #pragma unroll
     for (int k = 0; k < i; ++k) v -= A[i * (i + 1) / 2 + k] * y[k];
-    y[i] = v * rd[i];
+    y[i] = v;
   }
 #pragma unroll
-  for (int i = 5; i >= 0; --i) {
-    double v = y[i];
+  for (int i = 5; i >= 0; --i) {   // L^T y = D^-1 z
+    double v = y[i] * rD[i];
 #pragma unroll
     for (int k = i + 1; k < 6; ++k) v -= A[k * (k + 1) / 2 + i] * y[k];
-    y[i] = v * rd[i];
+    y[i] = v;
   }
   bool finite = true;
 #pragma unroll
