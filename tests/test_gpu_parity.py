@@ -36,7 +36,7 @@ def _gpu_fe(floam_gpu, raw, R):
     return de.download(), ds.download(), (lp, din, de, ds)
 
 
-@pytest.mark.parametrize("config,scan", [("c1", 0), ("c1", 7), ("c2", 3), ("c3", 1), ("c4", 2)])
+@pytest.mark.parametrize("config,scan", [("c1", 0), ("c1", 7), ("c2", 3), ("c3", 1), ("c4", 2), ("c5", 1)])
 def test_feature_extraction_bit_exact(floam_gpu, oracle_lib, config, scan):
     raw = synth.generate_scan(config, scan)
     R = synth.lidar_model(config).rings
