@@ -27,6 +27,7 @@ struct GridJob {
   FineCell* fine;
   CoarseCell* coarse;
   uint2* where;
+  float4* xyz;      // the map's coordinates by map index (the kNN's neighbour gathers)
   int* clist_new;   // appended by this build
   int* flist_new;
   const int* clist_old;   // cleared by this build
@@ -185,15 +186,19 @@ __global__ __launch_bounds__(kTB) void grid_scatter(GridJob E, GridJob S) {
       if (k < sub) pos += c.sub[k];
     const float4 p = *reinterpret_cast<const float4*>(&J.map[i].x);
     J.pts[pos] = make_float4(p.x, p.y, p.z, __int_as_float(i));
+    J.xyz[i] = make_float4(p.x, p.y, p.z, 0.0f);
   }
 }
 
 void reserve_grid(Grid& g, int ub) {
   g.pts.reserve(ub);
   g.where.reserve(ub);
+  g.xyz.reserve(ub);
   g.counters.reserve(8);
   int bits = 10;
-  while ((1 << bits) < 2 * ub) ++bits;   // load <= 1/2 (cells <= points)
+  // capacity >= points >= cells, so every insert terminates; the occupied cells are a fraction of the points (several
+  // map points per 0.5-m cell), so the load stays well below 1 and the probed tables stay compact in L2
+  while ((1 << bits) < ub) ++bits;
   if (bits > g.bits) {   // (reserve keeps the arrays when their capacity already covers the larger table)
     g.fine.reserve((size_t)1 << bits);
     g.coarse.reserve((size_t)1 << bits);
@@ -209,7 +214,7 @@ void reserve_grid(Grid& g, int ub) {
 
 GridJob make_job(Grid& g, const PointRec* map, const int* d_m, int m_ub) {
   const int p = g.parity;
-  return GridJob{map, d_m, m_ub, g.pts.p, g.fine.p, g.coarse.p, g.where.p, g.clist[p].p, g.flist[p].p,
+  return GridJob{map, d_m, m_ub, g.pts.p, g.fine.p, g.coarse.p, g.where.p, g.xyz.p, g.clist[p].p, g.flist[p].p,
                  g.clist[p ^ 1].p, g.flist[p ^ 1].p, g.counters.p, p, g.fresh ? 1 : 0, g.bits, g.mask};
 }
 }  // namespace

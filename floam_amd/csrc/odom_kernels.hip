@@ -431,7 +431,7 @@ struct CorrArgs {
   const CoarseCell* coarse;
   int bits;                // table size 1 << bits (both tables)
   unsigned mask;
-  const PointRec* map;     // the map in its own order (neighbour coordinates by map index)
+  const float4* map;       // the map's coordinates in its own order (neighbour coordinates by map index)
   double* rec;
   uint8_t* valid;
   float* nnxyz;
@@ -604,7 +604,7 @@ __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArg
 #pragma unroll
           for (int k = 1; k < 5; ++k)
             if (lane == k) kk = t.k[k];
-          const float4 m = *reinterpret_cast<const float4*>(&A.map[(int)(kk & 0xFFFFFFFFull)].x);
+          const float4 m = A.map[(int)(kk & 0xFFFFFFFFull)];
           A.nnxyz[(3 * lane + 0) * A.cap + i] = m.x;
           A.nnxyz[(3 * lane + 1) * A.cap + i] = m.y;
           A.nnxyz[(3 * lane + 2) * A.cap + i] = m.z;
@@ -2145,9 +2145,11 @@ static void corr_args(const QuerySet& qe, const Grid& ge, const PointRec* mapE, 
                       CorrArgs& S) {
   ce.reserve(std::max(qe.n_ub, 1), EDGE_FIELDS);
   cs.reserve(std::max(qs.n_ub, 1), SURF_FIELDS);
-  E = CorrArgs{qe.pts, qe.d_n, qe.n_ub, ge.pts.p, ge.fine.p, ge.coarse.p, ge.bits, ge.mask, mapE, ce.rec.p,
+  (void)mapE;
+  (void)mapS;
+  E = CorrArgs{qe.pts, qe.d_n, qe.n_ub, ge.pts.p, ge.fine.p, ge.coarse.p, ge.bits, ge.mask, ge.xyz.p, ce.rec.p,
                ce.valid.p, ce.nnxyz.p, ce.cap, dbg};
-  S = CorrArgs{qs.pts, qs.d_n, qs.n_ub, gs.pts.p, gs.fine.p, gs.coarse.p, gs.bits, gs.mask, mapS, cs.rec.p,
+  S = CorrArgs{qs.pts, qs.d_n, qs.n_ub, gs.pts.p, gs.fine.p, gs.coarse.p, gs.bits, gs.mask, gs.xyz.p, cs.rec.p,
                cs.valid.p, cs.nnxyz.p, cs.cap, dbg ? dbg + 8 : nullptr};
 }
 

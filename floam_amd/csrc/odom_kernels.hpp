@@ -28,6 +28,7 @@ constexpr unsigned long long kEmptyKey = ~0ull;
 
 struct Grid {
   DevBuf<float4> pts;        // {x, y, z, map index bits}, grouped by coarse cell then fine sub-cell
+  DevBuf<float4> xyz;        // {x, y, z, 0} by map index: 16-B neighbour gathers from a compact, L2-resident array
   DevBuf<FineCell> fine;
   DevBuf<CoarseCell> coarse;
   DevBuf<uint2> where;       // per map point: coarse slot, sub-cell << 28 | rank in the sub-cell
