@@ -446,13 +446,80 @@ struct CorrArgs {
 // cursor and U independent 16-B loads in flight (coalesced within a cell).
 constexpr int kMaxStencil = 27;
 
+// Fine 3x3x3 block (stage 1) without a fine-cell table: the block's 27 fine cells lie in exactly 2x2x2 coarse cells
+// (three consecutive fine indices halve to two consecutive coarse indices), whose entries carry the coarse range
+// start and the point count of each of their 8 fine sub-cells (sub-cells are consecutive inside the range, in sub
+// order: grid.hip).  Lanes 0..7 probe the 8 coarse cells (head and sub counts of a slot in one round trip) into LDS
+// (s_cc[8][9]: start, 8 counts), then every fine cell's range is start + the counts of the sub-cells before it.
+template <int G>
+__device__ __forceinline__ void fine_block_ranges(const CorrArgs& A, int qx, int qy, int qz, int lane,
+                                                  int* __restrict__ s_pre, int* __restrict__ s_start,
+                                                  int* __restrict__ s_cc) {
+  static_assert(G >= 8, "one coarse probe per lane");
+  const int cx0 = (qx - 1) >> 1, cy0 = (qy - 1) >> 1, cz0 = (qz - 1) >> 1;   // floor division by 2
+  if (lane < 8) {
+    const unsigned long long key = cell_key(cx0 + (lane & 1), cy0 + ((lane >> 1) & 1), cz0 + (lane >> 2));
+    unsigned slot = hash_slot64(key, A.bits);
+    const int4* e = reinterpret_cast<const int4*>(&A.coarse[slot]);
+    int4 h = e[0], s0 = e[1], s1 = e[2];
+    unsigned long long k = ((unsigned long long)(unsigned)h.y << 32) | (unsigned)h.x;
+    while (k != key && k != kEmptyKey) {   // collision chain (rare)
+      slot = (slot + 1) & A.mask;
+      e = reinterpret_cast<const int4*>(&A.coarse[slot]);
+      h = e[0];
+      s0 = e[1];
+      s1 = e[2];
+      k = ((unsigned long long)(unsigned)h.y << 32) | (unsigned)h.x;
+    }
+    const bool hit = k == key;
+    int* cc = s_cc + 9 * lane;
+    cc[0] = hit ? h.z : 0;
+    cc[1] = hit ? s0.x : 0; cc[2] = hit ? s0.y : 0; cc[3] = hit ? s0.z : 0; cc[4] = hit ? s0.w : 0;
+    cc[5] = hit ? s1.x : 0; cc[6] = hit ? s1.y : 0; cc[7] = hit ? s1.z : 0; cc[8] = hit ? s1.w : 0;
+  }
+  wave_lds_order();
+  constexpr int P = (kMaxStencil + G - 1) / G;   // fine cells per lane
+  const int cb = min(kMaxStencil, lane * P), ce = min(kMaxStencil, cb + P);
+  int local = 0;
+#pragma unroll
+  for (int j = 0; j < P; ++j) {
+    const int c = cb + j;
+    if (c < ce) {
+      const int fx = qx - 1 + c % 3, fy = qy - 1 + (c / 3) % 3, fz = qz - 1 + c / 9;
+      const int ci = ((fx >> 1) - cx0) | (((fy >> 1) - cy0) << 1) | (((fz >> 1) - cz0) << 2);
+      const int sub = (fx & 1) | ((fy & 1) << 1) | ((fz & 1) << 2);
+      const int* cc = s_cc + 9 * ci;
+      int start = cc[0];
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (k < sub) start += cc[1 + k];
+      s_start[c] = start;
+      s_pre[c] = local;
+      local += cc[1 + sub];
+    }
+  }
+  const int incl = group_incl_scan<G>(local, lane);
+  const int excl = incl - local;
+#pragma unroll
+  for (int j = 0; j < P; ++j)
+    if (cb + j < ce) s_pre[cb + j] += excl;
+  if (lane == G - 1) s_pre[kMaxStencil] = incl;
+  wave_lds_order();
+}
+
 template <int G, int U, bool COARSE>
 __device__ __forceinline__ void stencil_scan(const CorrArgs& A, int x0, int x1, int y0, int y1, int z0, int z1,
                                              float wx, float wy, float wz, int lane, int* __restrict__ s_pre,
-                                             int* __restrict__ s_start, Top5& t, int& cnt) {
+                                             int* __restrict__ s_start, Top5& t, int& cnt,
+                                             int* __restrict__ s_cc = nullptr) {
   constexpr int P = (kMaxStencil + G - 1) / G;   // cells per lane
   const int nxr = x1 - x0 + 1, nyr = y1 - y0 + 1, nzr = z1 - z0 + 1;
   const int ncell = nxr * nyr * nzr;
+  int tot;
+  if constexpr (!COARSE) {   // the fine block around (x0 + 1, y0 + 1, z0 + 1), ranges from the coarse entries
+    fine_block_ranges<G>(A, x0 + 1, y0 + 1, z0 + 1, lane, s_pre, s_start, s_cc);
+    tot = s_pre[kMaxStencil];
+  } else {
   const int per = (ncell + G - 1) / G;
   const int cb = min(ncell, lane * per), ce = min(ncell, cb + per);
   unsigned long long key[P];
@@ -492,9 +559,10 @@ __device__ __forceinline__ void stencil_scan(const CorrArgs& A, int x0, int x1, 
 #pragma unroll
   for (int j = 0; j < P; ++j)
     if (cb + j < ce) s_pre[cb + j] += excl;
-  const int tot = __shfl(incl, G - 1, G);
+  tot = __shfl(incl, G - 1, G);
   if (lane == 0) s_pre[ncell] = tot;
   wave_lds_order();
+  }
   int c = 0, c_lo = 0, c_hi = s_pre[1], c_start = s_start[0];   // cursor: cell c = [c_lo, c_hi)
   for (int tb = 0; tb < tot; tb += G * U) {
     float4 m[U];
@@ -564,7 +632,7 @@ __device__ __forceinline__ int xcd_block(int p, int nactive) {
 template <int G, int U>
 __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArgs& A, int gid, int ngroups,
                                           int lane, bool gate, int rank, int world, int* __restrict__ s_pre,
-                                          int* __restrict__ s_start) {
+                                          int* __restrict__ s_start, int* __restrict__ s_cc) {
   const int n = min(*A.d_n, A.n_ub);
   const int lo = (int)(((long long)n * rank) / world), hi = (int)(((long long)n * (rank + 1)) / world);
   // grid-stride over the queries the device holds (the host only knows an upper bound)
@@ -583,7 +651,7 @@ __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArg
       for (int k = 0; k < 5; ++k) t.k[k] = ~0ull;
       int cnt = 0;
       stencil_scan<G, U, false>(A, qx - 1, qx + 1, qy - 1, qy + 1, qz - 1, qz + 1, wx, wy, wz, lane, s_pre, s_start,
-                                t, cnt);
+                                t, cnt, s_cc);
       group_merge<G>(t, cnt);
       const bool complete = cnt >= 5 && __uint_as_float((unsigned)(t.k[4] >> 32)) < 0.25f;
       if (!complete) {   // coarse cells floor(q - 1) .. floor(q + 1) per axis (exact in double)
@@ -625,6 +693,7 @@ __global__ __launch_bounds__(kTB, W) void knn_kernel(LMState* __restrict__ st, X
                                                   int rank, int world) {
   __shared__ int s_pre[kTB / G][kMaxStencil + 1];
   __shared__ int s_start[kTB / G][kMaxStencil];
+  __shared__ int s_cc[kTB / G][8 * 9];
   const int lane = threadIdx.x & (G - 1);
   const int g = threadIdx.x / G;
   double pose[7];   // wave-uniform: kept in SGPRs (readfirstlane), not in 14 VGPRs of every lane
@@ -655,7 +724,7 @@ __global__ __launch_bounds__(kTB, W) void knn_kernel(LMState* __restrict__ st, X
   const bool had = p < nact;
   if (p < nact) p = xcd_block(p, nact);
   knn_group<G, U>(pose, A, (p * kTB + (int)threadIdx.x) / G, nb * (kTB / G), lane, gate, rank, world, s_pre[g],
-                  s_start[g]);
+                  s_start[g], s_cc[g]);
   if (E.dbg && (threadIdx.x & 63) == 0) {   // FLOAM_KNN_TRACE: per-wave (start, end) of the launch (diagnostic)
     const unsigned w = blockIdx.x * (kTB / 64) + (threadIdx.x >> 6);
     if (w < (1u << 16)) {
@@ -2193,11 +2262,10 @@ void knn_launch(LMState* d_st, const double* x0, const double* x0_dev, const Que
     case 2: knn_launch_t<8, 2>(d_st, x, x0_dev, qe, qs, E, S, d_me, d_ms, rank, world, st); break;
     case 3: knn_launch_t<32, 2>(d_st, x, x0_dev, qe, qs, E, S, d_me, d_ms, rank, world, st); break;
     case 4: knn_launch_t<16, 2>(d_st, x, x0_dev, qe, qs, E, S, d_me, d_ms, rank, world, st); break;
-    case 5: knn_launch_t<4, 4>(d_st, x, x0_dev, qe, qs, E, S, d_me, d_ms, rank, world, st); break;
     case 6: knn_launch_t<16, 4, 6>(d_st, x, x0_dev, qe, qs, E, S, d_me, d_ms, rank, world, st); break;
     case 7: knn_launch_t<16, 2, 6>(d_st, x, x0_dev, qe, qs, E, S, d_me, d_ms, rank, world, st); break;
     case 8: knn_launch_t<16, 2, 8>(d_st, x, x0_dev, qe, qs, E, S, d_me, d_ms, rank, world, st); break;
-    default: knn_launch_t<kGroupDefault, kUnrollDefault>(d_st, x, x0_dev, qe, qs, E, S, d_me, d_ms, rank, world, st); break;
+    default: knn_launch_t<kGroupDefault, kUnrollDefault, 6>(d_st, x, x0_dev, qe, qs, E, S, d_me, d_ms, rank, world, st); break;
   }
 }
 
