@@ -7,7 +7,7 @@
 //   grid_count   per point: insert its coarse cell (1 m, absolute coordinates -> 64-bit key; new cells appended to
 //                the occupied list), count it in its fine sub-cell (0.5 m) and keep its rank there
 //   grid_alloc   per occupied coarse cell (from the list): a contiguous range of the cell-grouped array (one atomic
-//                per block on a bump cursor), fine sub-cells consecutive inside it, fine cells inserted (and listed)
+//                per block on a bump cursor), fine sub-cells consecutive inside it
 //   grid_scatter per point: its slot = coarse start + preceding sub-cells + rank
 // No bounding box, no sort: O(M) work, every step one launch.
 #include "floam_common.hpp"
@@ -24,15 +24,12 @@ struct GridJob {
   const int* d_m;
   int m_ub;
   float4* pts;
-  FineCell* fine;
   CoarseCell* coarse;
   uint2* where;
   float4* xyz;      // the map's coordinates by map index (the kNN's neighbour gathers)
   int* clist_new;   // appended by this build
-  int* flist_new;
   const int* clist_old;   // cleared by this build
-  const int* flist_old;
-  int* counters;    // [0] cursor, [1 + parity] coarse list size, [3 + parity] fine list size
+  int* counters;    // [0] cursor, [1 + parity] coarse list size
   int parity;
   int full_clear;
   int bits;
@@ -67,19 +64,14 @@ __global__ __launch_bounds__(kTB) void grid_clear(GridJob E, GridJob S) {
   const int t0 = blockIdx.x * blockDim.x + threadIdx.x;
   if (J.full_clear) {
     const int size = (int)J.mask + 1;
-    for (int t = t0; t < size; t += stride) {
-      J.fine[t].key = kEmptyKey;
-      J.coarse[t] = empty_coarse();
-    }
+    for (int t = t0; t < size; t += stride) J.coarse[t] = empty_coarse();
   } else {
-    const int nc = J.counters[1 + (J.parity ^ 1)], nf = J.counters[3 + (J.parity ^ 1)];
+    const int nc = J.counters[1 + (J.parity ^ 1)];
     for (int t = t0; t < nc; t += stride) J.coarse[J.clist_old[t]] = empty_coarse();
-    for (int t = t0; t < nf; t += stride) J.fine[J.flist_old[t]].key = kEmptyKey;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     J.counters[0] = 0;
     J.counters[1 + J.parity] = 0;
-    J.counters[3 + J.parity] = 0;
   }
 }
 
@@ -143,28 +135,6 @@ __global__ __launch_bounds__(kTB) void grid_alloc(GridJob E, GridJob S) {
     }
     if (threadIdx.x == 0) s_base = btotal ? atomicAdd(&J.counters[0], btotal) : 0;
     __syncthreads();
-    for (int k = 0; k < 8; ++k) {   // fine cells of this coarse cell (wave-uniform loop for the list appends)
-      bool ins = false;
-      unsigned h = 0;
-      if (t < nc && c.sub[k] > 0) {
-        int off = s_base + wbase + incl - total;
-#pragma unroll
-        for (int kk = 0; kk < 8; ++kk)
-          if (kk < k) off += c.sub[kk];
-        const int cx = key_x(c.key), cy = key_y(c.key), cz = key_z(c.key);
-        const unsigned long long fk = cell_key(2 * cx + (k & 1), 2 * cy + ((k >> 1) & 1), 2 * cz + (k >> 2));
-        h = hash_slot64(fk, J.bits);
-        for (;;) {
-          const unsigned long long prev = atomicCAS(&J.fine[h].key, kEmptyKey, fk);
-          if (prev == kEmptyKey) break;
-          h = (h + 1) & J.mask;
-        }
-        J.fine[h].start = off;
-        J.fine[h].count = c.sub[k];
-        ins = true;
-      }
-      list_append(J.flist_new, &J.counters[3 + J.parity], ins, (int)h);
-    }
     if (t < nc) {
       J.coarse[slot].start = s_base + wbase + incl - total;
       J.coarse[slot].total = total;
@@ -200,12 +170,8 @@ void reserve_grid(Grid& g, int ub) {
   // map points per 0.5-m cell), so the load stays well below 1 and the probed tables stay compact in L2
   while ((1 << bits) < ub) ++bits;
   if (bits > g.bits) {   // (reserve keeps the arrays when their capacity already covers the larger table)
-    g.fine.reserve((size_t)1 << bits);
     g.coarse.reserve((size_t)1 << bits);
-    for (int k = 0; k < 2; ++k) {
-      g.clist[k].reserve((size_t)1 << bits);
-      g.flist[k].reserve((size_t)1 << bits);
-    }
+    for (int k = 0; k < 2; ++k) g.clist[k].reserve((size_t)1 << bits);
     g.bits = bits;
     g.mask = (1u << bits) - 1u;
     g.fresh = true;
@@ -214,8 +180,8 @@ void reserve_grid(Grid& g, int ub) {
 
 GridJob make_job(Grid& g, const PointRec* map, const int* d_m, int m_ub) {
   const int p = g.parity;
-  return GridJob{map, d_m, m_ub, g.pts.p, g.fine.p, g.coarse.p, g.where.p, g.xyz.p, g.clist[p].p, g.flist[p].p,
-                 g.clist[p ^ 1].p, g.flist[p ^ 1].p, g.counters.p, p, g.fresh ? 1 : 0, g.bits, g.mask};
+  return GridJob{map, d_m, m_ub, g.pts.p, g.coarse.p, g.where.p, g.xyz.p, g.clist[p].p, g.clist[p ^ 1].p,
+                 g.counters.p, p, g.fresh ? 1 : 0, g.bits, g.mask};
 }
 }  // namespace
 

@@ -353,7 +353,7 @@ __device__ __forceinline__ void lm_reset(LMState* st, const X7& x0) {
 constexpr int kGroupDefault = 16;   // lanes per query (template parameter G below)
 constexpr int kUnrollDefault = 4;   // candidate loads in flight per lane (U)
 
-// (start, count) of a cell, or (0, 0): fine and coarse entries share the {key, start, count} head (one 16-B load)
+// (start, count) of a coarse cell, or (0, 0): the entry's {key, start, total} head (one 16-B load)
 template <typename Cell>
 __device__ __forceinline__ int2 grid_lookup(const Cell* __restrict__ tab, unsigned long long key, int bits,
                                             unsigned mask) {
@@ -366,6 +366,9 @@ __device__ __forceinline__ int2 grid_lookup(const Cell* __restrict__ tab, unsign
     h = (h + 1) & mask;
   }
 }
+
+// points in the fine (0.5-m) cell (fx, fy, fz): its sub-cell count in the entry of the coarse cell that holds it
+__device__ __forceinline__ int fine_count(const struct CorrArgs& A, int fx, int fy, int fz);
 
 __device__ __forceinline__ void cswap(unsigned long long& a, unsigned long long& b) {
   const unsigned long long lo = a < b ? a : b, hi = a < b ? b : a;
@@ -427,7 +430,6 @@ struct CorrArgs {
   const int* d_n;          // device count
   int n_ub;
   const float4* gpts;      // the map grouped by cell: {x, y, z, map index bits}
-  const FineCell* fine;
   const CoarseCell* coarse;
   int bits;                // table size 1 << bits (both tables)
   unsigned mask;
@@ -438,6 +440,17 @@ struct CorrArgs {
   int cap;
   unsigned long long* dbg;   // FLOAM_DEBUG_STAMPS: per-phase latency sums (diagnostic, normally null)
 };
+
+__device__ __forceinline__ int fine_count(const CorrArgs& A, int fx, int fy, int fz) {
+  const unsigned long long key = cell_key(fx >> 1, fy >> 1, fz >> 1);
+  unsigned h = hash_slot64(key, A.bits);
+  for (;;) {
+    const CoarseCell& c = A.coarse[h];
+    if (c.key == key) return c.sub[(fx & 1) | ((fy & 1) << 1) | ((fz & 1) << 2)];
+    if (c.key == kEmptyKey) return 0;
+    h = (h + 1) & A.mask;
+  }
+}
 
 // Scan a block of up to 3 x 3 x 3 cells of one table into the lane-local top-5 (keys: float sq-distance bits << 32
 // | position in the cell-sorted array, so ties go to the lower position).  Lane l looks up a contiguous run of the
@@ -533,7 +546,7 @@ __device__ __forceinline__ void stencil_scan(const CorrArgs& A, int x0, int x1, 
     if (c < ce) {
       key[j] = cell_key(x0 + c % nxr, y0 + (c / nxr) % nyr, z0 + c / (nxr * nyr));
       slot[j] = hash_slot64(key[j], A.bits);
-      e[j] = COARSE ? *reinterpret_cast<const int4*>(&A.coarse[slot[j]]) : *reinterpret_cast<const int4*>(&A.fine[slot[j]]);
+      e[j] = *reinterpret_cast<const int4*>(&A.coarse[slot[j]]);
     }
   }
   int local = 0;
@@ -544,8 +557,7 @@ __device__ __forceinline__ void stencil_scan(const CorrArgs& A, int x0, int x1, 
       unsigned long long k = ((unsigned long long)(unsigned)e[j].y << 32) | (unsigned)e[j].x;
       while (k != key[j] && k != kEmptyKey) {   // collision chain (rare)
         slot[j] = (slot[j] + 1) & A.mask;
-        e[j] = COARSE ? *reinterpret_cast<const int4*>(&A.coarse[slot[j]])
-                      : *reinterpret_cast<const int4*>(&A.fine[slot[j]]);
+        e[j] = *reinterpret_cast<const int4*>(&A.coarse[slot[j]]);
         k = ((unsigned long long)(unsigned)e[j].y << 32) | (unsigned)e[j].x;
       }
       const bool hit = k == key[j];
@@ -965,7 +977,7 @@ __global__ __launch_bounds__(kTB) void knn_traffic(const LMState* __restrict__ s
     for (int y = y0; y <= y1; ++y)
       for (int x = x0; x <= x1; ++x) {
         const unsigned long long k = cell_key(x, y, z);
-        const int cnt = level ? grid_lookup(A.coarse, k, A.bits, A.mask).y : grid_lookup(A.fine, k, A.bits, A.mask).y;
+        const int cnt = level ? grid_lookup(A.coarse, k, A.bits, A.mask).y : fine_count(A, x, y, z);
         if (cnt == 0) continue;
         unsigned h = hash_slot64(k, set_bits);
         for (;;) {
@@ -2216,9 +2228,9 @@ static void corr_args(const QuerySet& qe, const Grid& ge, const PointRec* mapE, 
   cs.reserve(std::max(qs.n_ub, 1), SURF_FIELDS);
   (void)mapE;
   (void)mapS;
-  E = CorrArgs{qe.pts, qe.d_n, qe.n_ub, ge.pts.p, ge.fine.p, ge.coarse.p, ge.bits, ge.mask, ge.xyz.p, ce.rec.p,
+  E = CorrArgs{qe.pts, qe.d_n, qe.n_ub, ge.pts.p, ge.coarse.p, ge.bits, ge.mask, ge.xyz.p, ce.rec.p,
                ce.valid.p, ce.nnxyz.p, ce.cap, dbg};
-  S = CorrArgs{qs.pts, qs.d_n, qs.n_ub, gs.pts.p, gs.fine.p, gs.coarse.p, gs.bits, gs.mask, gs.xyz.p, cs.rec.p,
+  S = CorrArgs{qs.pts, qs.d_n, qs.n_ub, gs.pts.p, gs.coarse.p, gs.bits, gs.mask, gs.xyz.p, cs.rec.p,
                cs.valid.p, cs.nnxyz.p, cs.cap, dbg ? dbg + 8 : nullptr};
 }
 

@@ -10,16 +10,13 @@ namespace floam {
 // edge kFineCell = 0.5 m nested 2x2x2 in coarse cells of 1 m.  Built without sorting (grid.hip): points are counted
 // per coarse cell and fine sub-cell (atomics into an open-addressing table of coarse cells), every coarse cell gets
 // a contiguous range of `pts` (block-aggregated bump allocation, fine sub-cells consecutive inside it), and the
-// points are scattered into place.  A fine table and the coarse table map 64-bit cell keys to (start, count).
+// points are scattered into place.  The coarse table maps a 64-bit cell key to its range and its 8 sub-cell counts,
+// from which the kNN derives every fine cell's range (no fine-cell table).
 // Layout order inside a cell is not deterministic; the kNN breaks distance ties by map index, so results are.
 // Exact replacement of the 5-NN KD-tree under the reference's sqd[4] < 1 gate (knn_group).
 constexpr double kFineCell = 0.5;
 
-struct FineCell {            // 16 B: one probe = one dwordx4 load
-  unsigned long long key;    // kEmptyKey = empty
-  int start, count;
-};
-struct CoarseCell {          // 48 B; the kNN reads the first 16 B
+struct CoarseCell {          // 48 B: head (key, range) + the point count of each 0.5-m fine sub-cell
   unsigned long long key;
   int start, total;
   int sub[8];                // points per fine sub-cell (x bit 0, y bit 1, z bit 2)
@@ -29,13 +26,12 @@ constexpr unsigned long long kEmptyKey = ~0ull;
 struct Grid {
   DevBuf<float4> pts;        // {x, y, z, map index bits}, grouped by coarse cell then fine sub-cell
   DevBuf<float4> xyz;        // {x, y, z, 0} by map index: 16-B neighbour gathers from a compact, L2-resident array
-  DevBuf<FineCell> fine;
   DevBuf<CoarseCell> coarse;
   DevBuf<uint2> where;       // per map point: coarse slot, sub-cell << 28 | rank in the sub-cell
-  // occupied slots of the coarse / fine table, per build parity: the next build clears exactly these entries
-  DevBuf<int> clist[2], flist[2];
-  DevBuf<int> counters;      // [0] bump cursor, [1..2] coarse list sizes, [3..4] fine list sizes (by parity)
-  int bits = 0;              // table size = 1 << bits (both tables)
+  // occupied slots of the coarse table, per build parity: the next build clears exactly these entries
+  DevBuf<int> clist[2];
+  DevBuf<int> counters;      // [0] bump cursor, [1..2] coarse list sizes (by parity)
+  int bits = 0;              // table size = 1 << bits
   unsigned mask = 0;
   int parity = 0;
   bool fresh = true;         // tables (re)allocated: the next clear is a full one
