@@ -16,10 +16,11 @@ namespace floam {
 // Exact replacement of the 5-NN KD-tree under the reference's sqd[4] < 1 gate (knn_group).
 constexpr double kFineCell = 0.5;
 
-struct CoarseCell {          // 48 B: head (key, range) + the point count of each 0.5-m fine sub-cell
+struct alignas(64) CoarseCell {   // 64 B, one per half cache line: a probe never straddles two lines
   unsigned long long key;
   int start, total;
   int sub[8];                // points per fine sub-cell (x bit 0, y bit 1, z bit 2)
+  int pad[4];
 };
 constexpr unsigned long long kEmptyKey = ~0ull;
 
