@@ -75,19 +75,42 @@ __global__ __launch_bounds__(kTB) void grid_clear(GridJob E, GridJob S) {
   }
 }
 
+// Map points are in voxel order, so a wave's 64 points fall in a handful of coarse cells: the wave groups its lanes
+// by cell key (ballots, no memory traffic), one leader per cell inserts it, and one leader per (cell, sub-cell) adds
+// the group's count — a few atomics per wave on each cache line instead of two per point.  Ranks inside a group
+// follow lane order (the order inside a cell is not deterministic across waves either way; the kNN breaks distance
+// ties by map index).
 __global__ __launch_bounds__(kTB) void grid_count(GridJob E, GridJob S) {
   const GridJob& J = blockIdx.y == 0 ? E : S;
   const int m = min(*J.d_m, J.m_ub);
+  const int lane = threadIdx.x & 63;
+  const unsigned long long below = (1ull << lane) - 1ull;
   for (int i0 = blockIdx.x * blockDim.x; i0 < m; i0 += gridDim.x * blockDim.x) {   // wave-uniform trip count
     const int i = i0 + threadIdx.x;
-    bool fresh = false;
-    unsigned h = 0;
-    if (i < m) {
+    const bool valid = i < m;
+    unsigned long long key = kEmptyKey;
+    int sub = 0;
+    if (valid) {
       const float4 p = *reinterpret_cast<const float4*>(&J.map[i].x);
       int fx, fy, fz;
       fine_cell(p.x, p.y, p.z, fx, fy, fz);
-      const unsigned long long key = cell_key(fx >> 1, fy >> 1, fz >> 1);
-      const int sub = (fx & 1) | ((fy & 1) << 1) | ((fz & 1) << 2);
+      key = cell_key(fx >> 1, fy >> 1, fz >> 1);
+      sub = (fx & 1) | ((fy & 1) << 1) | ((fz & 1) << 2);
+    }
+    // lanes grouped by key: my_grp = the lanes sharing my cell, leader = its lowest lane
+    unsigned long long pending = __ballot(valid), my_grp = 0ull;
+    while (pending) {
+      const int l = __ffsll((long long)pending) - 1;
+      const unsigned lo = (unsigned)__shfl((int)(unsigned)key, l, 64);
+      const unsigned hi = (unsigned)__shfl((int)(unsigned)(key >> 32), l, 64);
+      const unsigned long long grp = __ballot(valid && key == (((unsigned long long)hi << 32) | lo)) & pending;
+      if ((grp >> lane) & 1ull) my_grp = grp;
+      pending &= ~grp;
+    }
+    const int leader = valid ? __ffsll((long long)my_grp) - 1 : lane;
+    bool fresh = false;
+    unsigned h = 0;
+    if (valid && leader == lane) {
       h = hash_slot64(key, J.bits);
       for (;;) {
         const unsigned long long prev = atomicCAS(&J.coarse[h].key, kEmptyKey, key);
@@ -95,9 +118,20 @@ __global__ __launch_bounds__(kTB) void grid_count(GridJob E, GridJob S) {
         if (prev == kEmptyKey || prev == key) break;
         h = (h + 1) & J.mask;
       }
-      const int rank = atomicAdd(&J.coarse[h].sub[sub], 1);
-      J.where[i] = make_uint2(h, ((unsigned)sub << 28) | (unsigned)rank);
     }
+    h = (unsigned)__shfl((int)h, leader, 64);
+    // lanes of my cell with my sub-cell: one add per (cell, sub-cell) group, ranks in lane order
+    unsigned long long sub_grp = 0ull;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const unsigned long long b = __ballot(valid && sub == s);
+      if (sub == s) sub_grp = b & my_grp;
+    }
+    const int leader2 = valid ? __ffsll((long long)sub_grp) - 1 : lane;
+    int base = 0;
+    if (valid && leader2 == lane) base = atomicAdd(&J.coarse[h].sub[sub], __popcll(sub_grp));
+    base = __shfl(base, leader2, 64);
+    if (valid) J.where[i] = make_uint2(h, ((unsigned)sub << 28) | (unsigned)(base + __popcll(sub_grp & below)));
     list_append(J.clist_new, &J.counters[1 + J.parity], fresh, (int)h);
   }
 }
