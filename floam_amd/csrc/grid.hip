@@ -80,8 +80,9 @@ __global__ __launch_bounds__(kTB) void grid_clear(GridJob E, GridJob S) {
 // the group's count — a few atomics per wave on each cache line instead of two per point.  Ranks inside a group
 // follow lane order (the order inside a cell is not deterministic across waves either way; the kNN breaks distance
 // ties by map index).
-__global__ __launch_bounds__(kTB) void grid_count(GridJob E, GridJob S) {
+__global__ __launch_bounds__(kTB) void grid_count(GridJob E, GridJob S, OdomDev* __restrict__ predict) {
   const GridJob& J = blockIdx.y == 0 ? E : S;
+  if (predict && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) odom_predict_step(predict);
   const int m = min(*J.d_m, J.m_ub);
   const int lane = threadIdx.x & 63;
   const unsigned long long below = (1ull << lane) - 1ull;
@@ -220,7 +221,7 @@ GridJob make_job(Grid& g, const PointRec* map, const int* d_m, int m_ub) {
 }  // namespace
 
 void grid_build_launch(Grid& gE, const PointRec* mapE, const int* d_mE, int mE_ub, Grid& gS, const PointRec* mapS,
-                       const int* d_mS, int mS_ub, hipStream_t st) {
+                       const int* d_mS, int mS_ub, hipStream_t st, OdomDev* predict) {
   mE_ub = std::max(mE_ub, 1);
   mS_ub = std::max(mS_ub, 1);
   reserve_grid(gE, mE_ub);
@@ -234,7 +235,7 @@ void grid_build_launch(Grid& gE, const PointRec* mapE, const int* d_mE, int mE_u
   const unsigned pb = std::min(div_up(std::max(mE_ub, mS_ub), kTB), 2048u);
   hipLaunchKernelGGL(grid_clear, dim3(tb, 2), dim3(kTB), 0, st, E, S);
   FLOAM_LAUNCH_CHECK();
-  hipLaunchKernelGGL(grid_count, dim3(pb, 2), dim3(kTB), 0, st, E, S);
+  hipLaunchKernelGGL(grid_count, dim3(pb, 2), dim3(kTB), 0, st, E, S, predict);
   FLOAM_LAUNCH_CHECK();
   hipLaunchKernelGGL(grid_alloc, dim3(std::min(pb, 512u), 2), dim3(kTB), 0, st, E, S);
   FLOAM_LAUNCH_CHECK();

@@ -391,9 +391,12 @@ void allreduce_sums(floam_odom* o, DeviceCtx& ctx) {
 // then one device-to-host copy of the status slots; odom_collect reads them (errors, warnings, stats, poses, map
 // sizes) — right away in synchronous mode, later in asynchronous mode.
 // pre >= 0: the call's clouds were downsampled on the side stream into the parity-`pre` buffers (odom_prevoxel)
+// predict: the update's prediction (odom_predict) is issued here — inside the grid rebuild's first launch when the
+// maps changed, else as a launch of its own — before anything reads x0_dev
 void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const floam_cloud* surf, int ne_ub, int ns_ub,
-                const double* x0_dev, int slot, int gather_mode, int pre = -1) {
+                const double* x0_dev, int slot, int gather_mode, int pre = -1, bool predict = false) {
   hipStream_t st = ctx.stream;
+  if (predict && !o->grid_dirty) odom_predict_launch(o->ds.p, st);
   o->dE.reserve(std::max(ne_ub, 1));
   o->dS.reserve(std::max(ns_ub, 1));
   o->cnt.reserve(4);
@@ -413,7 +416,8 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
   const int mE_ub = (int)o->mapE_n, mS_ub = (int)o->mapS_n;   // exact or upper bounds
   if (o->grid_dirty) {
     ProfScope ps(ctx, "grid_build", FLOAM_PROF_CLOUD);
-    grid_build_launch(o->gE, o->mapE.pts.p, o->mapE.count.p, mE_ub, o->gS, o->mapS.pts.p, o->mapS.count.p, mS_ub, st);
+    grid_build_launch(o->gE, o->mapE.pts.p, o->mapE.count.p, mE_ub, o->gS, o->mapS.pts.p, o->mapS.count.p, mS_ub, st,
+                      predict ? o->ds.p : nullptr);
     o->grid_dirty = false;
   }
   o->lm.reserve(1);
@@ -706,10 +710,9 @@ floam_status odom_update(floam_odom* o, const floam_cloud* edge, const floam_clo
   const bool captured = odom_capture_begin(o, ctx);
   try {
     if (o->optimization_count > 2) o->optimization_count--;
-    odom_predict_launch(o->ds.p, ctx.stream);
     const bool update_map = type == FLOAM_VANILLA || type == FLOAM_REFINEMENT_AND_UPDATE;
     odom_issue(o, ctx, edge, surf, ne_ub, ns_ub, o->ds.p->x0[0], 2 * ring,
-               GATHER_FINISH | (update_map ? gather_keyframe_mode() : 0));
+               GATHER_FINISH | (update_map ? gather_keyframe_mode() : 0), -1, true);
     size_t addE = 0, addS = 0;
     if (update_map) odom_map_update(o, ctx, ne_ub, ns_ub, addE, addS);
     return odom_end(o, ctx, ring, 1, update_map ? 0 : -1, addE, addS, captured, 0);
@@ -758,8 +761,7 @@ floam_status odom_update_deskew(floam_odom* o, floam_cloud* edge, floam_cloud* s
   const bool captured = odom_capture_begin(o, ctx);
   try {
     if (o->optimization_count > 2) o->optimization_count--;
-    odom_predict_launch(o->ds.p, ctx.stream);
-    odom_issue(o, ctx, edge, edge, ne_ub, ne_ub, o->ds.p->x0[0], 2 * ring, 0, pre);
+    odom_issue(o, ctx, edge, edge, ne_ub, ne_ub, o->ds.p->x0[0], 2 * ring, 0, pre, true);
     if (pre >= 0) {   // the side stream may refill this parity's buffers once call 1 has run
       FLOAM_HIP(hipEventRecord(o->side_ev[pre], ctx.stream));
       o->side_ev_rec[pre] = true;

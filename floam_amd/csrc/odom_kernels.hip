@@ -1046,11 +1046,7 @@ __global__ void odom_dev_init(OdomDev* s) {
 }
 
 __global__ void odom_predict(OdomDev* s) {
-  if (threadIdx.x != 0) return;
-  const Pose pred = pose_mul(s->odom, pose_mul(pose_inverse(s->last_odom), s->odom));
-  s->last_odom = s->odom;   // Q2: the branch is taken for every update type
-  s->odom = pred;
-  pose_to_params(pred, s->x0[0]);
+  if (threadIdx.x == 0) odom_predict_step(s);
 }
 
 // ===================================================================================== residuals + reduction

@@ -38,9 +38,11 @@ struct Grid {
   bool fresh = true;         // tables (re)allocated: the next clear is a full one
 };
 
-// Rebuild the grids of both local maps (corner and surf) in four launches.
+struct OdomDev;
+// Rebuild the grids of both local maps (corner and surf) in four launches.  predict (nullable): the update's
+// constant-velocity prediction (odom_predict_step) runs in the first of them instead of a launch of its own.
 void grid_build_launch(Grid& gE, const PointRec* mapE, const int* d_mE, int mE_ub, Grid& gS, const PointRec* mapS,
-                       const int* d_mS, int mS_ub, hipStream_t st);
+                       const int* d_mS, int mS_ub, hipStream_t st, OdomDev* predict = nullptr);
 
 // ----------------------------------------------------------------------------------------- correspondences
 // Edge record (EdgeAnalyticCostFunction inputs): cp (sensor point), a, b.  Surf: cp, unit normal n, d.
@@ -122,6 +124,12 @@ void odom_dev_init_launch(OdomDev* s, hipStream_t st);   // identity poses, no k
 // odomEstimationClass.cpp:59-71 (branch always taken, Q2): pred = odom (last^-1 odom); last = odom; odom = pred;
 // x0[0] = the parameters {q, t} of pred (the first call's starting point)
 void odom_predict_launch(OdomDev* s, hipStream_t st);
+__device__ inline void odom_predict_step(OdomDev* s) {   // one thread
+  const Pose pred = pose_mul(s->odom, pose_mul(pose_inverse(s->last_odom), s->odom));
+  s->last_odom = s->odom;   // Q2: the branch is taken for every update type
+  s->odom = pred;
+  pose_to_params(pred, s->x0[0]);
+}
 
 struct UpdateStatus {
   LMState lm;
