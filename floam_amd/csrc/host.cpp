@@ -394,7 +394,8 @@ void allreduce_sums(floam_odom* o, DeviceCtx& ctx) {
 // predict: the update's prediction (odom_predict) is issued here — inside the grid rebuild's first launch when the
 // maps changed, else as a launch of its own — before anything reads x0_dev
 void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const floam_cloud* surf, int ne_ub, int ns_ub,
-                const double* x0_dev, int slot, int gather_mode, int pre = -1, bool predict = false) {
+                const double* x0_dev, int slot, int gather_mode, int pre = -1, bool predict = false,
+                GatherArgs* defer_gather = nullptr) {
   hipStream_t st = ctx.stream;
   if (predict && !o->grid_dirty) odom_predict_launch(o->ds.p, st);
   o->dE.reserve(std::max(ne_ub, 1));
@@ -504,6 +505,10 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
   }
   if (o->optimization_count <= 0) lm_init_dev_launch(o->lm.p, x0_dev, st);
   const bool prof_knn = (ctx.profile & FLOAM_PROF_KNN_BYTES) != 0;
+  if (defer_gather && !prof_knn && gather_mode == 0) {   // carried out by the next launch (deskew_bridge)
+    *defer_gather = GatherArgs{dcnt, o->mapE.count.p, o->mapS.count.p, edge->fe_status, o->h_ustat.p + slot};
+    return;
+  }
   gather_status_launch(o->lm.p, dcnt, o->mapE.count.p, o->mapS.count.p, edge->fe_status,
                        prof_knn ? o->prof_bytes.p : nullptr, o->h_ustat.p + slot, o->ds.p, gather_mode, st);
   if (prof_knn) FLOAM_HIP(hipMemsetAsync(o->prof_bytes.p, 0, sizeof(unsigned long long) * 2, st));
@@ -761,7 +766,8 @@ floam_status odom_update_deskew(floam_odom* o, floam_cloud* edge, floam_cloud* s
   const bool captured = odom_capture_begin(o, ctx);
   try {
     if (o->optimization_count > 2) o->optimization_count--;
-    odom_issue(o, ctx, edge, edge, ne_ub, ne_ub, o->ds.p->x0[0], 2 * ring, 0, pre, true);
+    GatherArgs g1;
+    odom_issue(o, ctx, edge, edge, ne_ub, ne_ub, o->ds.p->x0[0], 2 * ring, 0, pre, true, &g1);
     if (pre >= 0) {   // the side stream may refill this parity's buffers once call 1 has run
       FLOAM_HIP(hipEventRecord(o->side_ev[pre], ctx.stream));
       o->side_ev_rec[pre] = true;
@@ -769,7 +775,7 @@ floam_status odom_update_deskew(floam_odom* o, floam_cloud* edge, floam_cloud* s
     {
       ProfScope ps(ctx, "deskew", FLOAM_PROF_CLOUD);
       deskew_bridge_launch(o->lm.p, o->ds.p, o->lp.scan_period, edge->pts.p, edge->count.p, ne_ub, surf->pts.p,
-                           surf->count.p, ns_ub, ctx.stream);
+                           surf->count.p, ns_ub, ctx.stream, g1);
     }
     if (o->optimization_count > 2) o->optimization_count--;
     odom_issue(o, ctx, edge, surf, ne_ub, ns_ub, o->ds.p->x0[1], 2 * ring + 1,

@@ -1005,11 +1005,20 @@ __global__ void lm_init_dev(LMState* st, X7 x0, const double* __restrict__ x0_de
   lm_reset(st, x0);
 }
 
+}  // namespace
+__device__ __forceinline__ void gather_block(const LMState* __restrict__ lm, const int* __restrict__ dcnt,
+                                             const int* __restrict__ mapE_count, const int* __restrict__ mapS_count,
+                                             const int* __restrict__ fe_status,
+                                             const unsigned long long* __restrict__ prof,
+                                             UpdateStatus* __restrict__ out, OdomDev* __restrict__ s, int mode);
+namespace {
+
 __global__ __launch_bounds__(kTB) void deskew_bridge(const LMState* __restrict__ st, OdomDev* __restrict__ s,
                                                      double period, PointRec* __restrict__ edge,
                                                      const int* __restrict__ d_ne, int ne_ub,
                                                      PointRec* __restrict__ surf, const int* __restrict__ d_ns,
-                                                     int ns_ub) {
+                                                     int ns_ub, GatherArgs g) {
+  if (g.out && blockIdx.x == 0) gather_block(st, g.dcnt, g.mapE_count, g.mapS_count, g.fe_status, nullptr, g.out, s, 0);
   double x1[7];
 #pragma unroll
   for (int k = 0; k < 7; ++k) x1[k] = st->x[k];
@@ -2135,10 +2144,11 @@ __global__ __launch_bounds__(kTB) void lm_reduce(const double* __restrict__ part
 
 // ===================================================================================== launchers
 void deskew_bridge_launch(const LMState* d_st, OdomDev* s, double scan_period, PointRec* edge, const int* d_ne,
-                          int ne_ub, PointRec* surf, const int* d_ns, int ns_ub, hipStream_t stream) {
+                          int ne_ub, PointRec* surf, const int* d_ns, int ns_ub, hipStream_t stream,
+                          const GatherArgs& gather) {
   const unsigned nb = std::max(1u, std::min(div_up(std::max(ne_ub + ns_ub, 1), kTB), 1024u));
   hipLaunchKernelGGL(deskew_bridge, dim3(nb), dim3(kTB), 0, stream, d_st, s, scan_period, edge, d_ne, ne_ub, surf,
-                     d_ns, ns_ub);
+                     d_ns, ns_ub, gather);
   FLOAM_LAUNCH_CHECK();
 }
 
@@ -2153,10 +2163,12 @@ void lm_init_launch(LMState* d_st, const double* x0, hipStream_t st) {
 }
 
 // One D2H per update: LM state + query / map counts (+ profiling bytes) gathered into one block.
-__global__ void gather_status(const LMState* __restrict__ lm, const int* __restrict__ dcnt,
-                              const int* __restrict__ mapE_count, const int* __restrict__ mapS_count,
-                              const int* __restrict__ fe_status, const unsigned long long* __restrict__ prof,
-                              UpdateStatus* __restrict__ out, OdomDev* __restrict__ s, int mode) {
+// Called by every thread of one block.
+__device__ __forceinline__ void gather_block(const LMState* __restrict__ lm, const int* __restrict__ dcnt,
+                                             const int* __restrict__ mapE_count, const int* __restrict__ mapS_count,
+                                             const int* __restrict__ fe_status,
+                                             const unsigned long long* __restrict__ prof,
+                                             UpdateStatus* __restrict__ out, OdomDev* __restrict__ s, int mode) {
   constexpr int kWords = kStateWords;
   const unsigned* src = reinterpret_cast<const unsigned*>(lm);
   unsigned* dst = reinterpret_cast<unsigned*>(&out->lm);
@@ -2192,6 +2204,13 @@ __global__ void gather_status(const LMState* __restrict__ lm, const int* __restr
     out->odom = s->odom;
     out->last_odom = s->last_odom;
   }
+}
+
+__global__ void gather_status(const LMState* __restrict__ lm, const int* __restrict__ dcnt,
+                              const int* __restrict__ mapE_count, const int* __restrict__ mapS_count,
+                              const int* __restrict__ fe_status, const unsigned long long* __restrict__ prof,
+                              UpdateStatus* __restrict__ out, OdomDev* __restrict__ s, int mode) {
+  gather_block(lm, dcnt, mapE_count, mapS_count, fe_status, prof, out, s, mode);
 }
 
 void gather_status_launch(const LMState* lm, const int* dcnt, const int* mapE_count, const int* mapS_count,

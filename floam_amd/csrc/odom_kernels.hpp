@@ -146,13 +146,23 @@ enum { GATHER_FINISH = 1, GATHER_AFTER_MID = 2, GATHER_KEYFRAME = 4, GATHER_KEYF
 void gather_status_launch(const LMState* lm, const int* dcnt, const int* mapE_count, const int* mapS_count,
                           const int* fe_status, const unsigned long long* prof, UpdateStatus* out, OdomDev* s,
                           int mode, hipStream_t st);
+struct GatherArgs {   // a status gather carried out by another launch (deskew_bridge for the first call's slot)
+  const int* dcnt = nullptr;
+  const int* mapE_count = nullptr;
+  const int* mapS_count = nullptr;
+  const int* fe_status = nullptr;
+  UpdateStatus* out = nullptr;   // null: nothing to gather
+};
 
 // Between the two updatePointsToMap calls of a deskewed UpdatePointsToMapSelector (odomEstimationClass.cpp:40-46),
 // without a host round trip: GetVelocity from the first call's result (x1 = st->x) and s->last_odom (the pose before
 // it), CompensateVelocity of both clouds in place (dataHandler.cpp:82-92, Q5); s->mid = odom1 and the second call's
 // prediction odom1 * (last_odom^-1 * odom1) into s->x0[1] (same algebra as the host, pose.hpp).
+// gather: the first call's status gather (mode 0: it only reads the LM state, the counts and the poses, none of
+// which this launch writes) done by block 0 instead of a launch of its own
 void deskew_bridge_launch(const LMState* st, OdomDev* s, double scan_period, PointRec* edge, const int* d_ne,
-                          int ne_ub, PointRec* surf, const int* d_ns, int ns_ub, hipStream_t stream);
+                          int ne_ub, PointRec* surf, const int* d_ns, int ns_ub, hipStream_t stream,
+                          const GatherArgs& gather = GatherArgs{});
 // Correspondence search for the edge and the surf query sets at the pose in st->x, in two launches:
 // knn_launch — exact 5-NN (blocks [0, nbE) edge queries against the corner map, the rest surf against the surf map);
 // geom_launch — fp64 line / plane fits and the residual records.
