@@ -41,6 +41,8 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (/opt/skills/guides/MI355X_MICROARCH.md: 8.0 TB/s)
 METRIC = "scans/sec scan-to-map odometry, 64-ring ~130k pts; pose RMSE vs reference"
 MAP_RES, LOSS, MIN_DIS, MAX_DIS, SCAN_PERIOD = 0.1, "Cauchy", 0.5, 90.0, 0.1
+# updates in flight (floam_odom_set_async) and feature buffers: the host issues scan k+DEPTH-1 while scan k runs
+DEPTH = int(os.environ.get("FLOAM_BENCH_DEPTH", "2"))
 
 
 def log(*a):
@@ -161,17 +163,17 @@ def main():
                 odo.set_shard_callback(rank, world, _allreduce)
                 allreduce_impl = "gloo-host"
         odo.initMapWithPoints(d_mapE, d_mapS)
-        odo.set_async(2)
+        odo.set_async(DEPTH)
         n_pipelines += 1
         return lp, odo
 
     lp, odo = make_pipeline()
     # two feature buffers: the extraction of scan k+1 (its own stream) is issued before the odometry of scan k, so
     # the two overlap on the device, as the reference's laserProcessingNode runs beside odomEstimationNode
-    bufs = [(floam_amd.DeviceCloud(device=dev), floam_amd.DeviceCloud(device=dev)) for _ in range(2)]
+    bufs = [(floam_amd.DeviceCloud(device=dev), floam_amd.DeviceCloud(device=dev)) for _ in range(max(2, DEPTH))]
 
     def extract(lp, k):
-        e, s = bufs[k & 1]
+        e, s = bufs[k % len(bufs)]
         e.clear()
         s.clear()
         lp.featureExtraction(d_raw[k], e, s)
@@ -187,10 +189,10 @@ def main():
             t0 = time.perf_counter()
             if k + 1 < b:
                 extract(lp, k + 1)
-            e, s = bufs[k & 1]
+            e, s = bufs[k % len(bufs)]
             odo.UpdatePointsToMapSelector(e, s, True)
             t1 = time.perf_counter()
-            poses.extend(odo.wait(1))
+            poses.extend(odo.wait(DEPTH - 1))
             host_split[0] += t1 - t0
             host_split[1] += time.perf_counter() - t1
         poses.extend(odo.wait(0))

@@ -269,6 +269,9 @@ struct floam_odom {
   VoxelScratch2 vs1;
   int pre_par = 0;
   int pre_valid = -1;                             // parity of the pre-downsampled call-1 clouds awaiting their update
+  // clouds the main stream orders itself after only once the grid rebuild is issued (pre-downsampled call 1: the
+  // rebuild reads neither cloud, so it runs while the side stream finishes)
+  const floam_cloud* late_wait[2] = {nullptr, nullptr};
   // status slots, two per in-flight update (first / only call, second call of a deskewed selector)
   // written by the gather kernel straight into coherent pinned host memory (no copy launch on the stream); 32 slots
   // cover the deepest ring (depth 16), so the buffer never moves while updates are in flight
@@ -421,6 +424,11 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
                       predict ? o->ds.p : nullptr);
     o->grid_dirty = false;
   }
+  for (const floam_cloud*& c : o->late_wait)
+    if (c) {
+      cloud_on_main(c);
+      c = nullptr;
+    }
   o->lm.reserve(1);
   o->partials.reserve((size_t)LM_NSUM * 512);
   if (!o->step_counter.p) {
@@ -1199,10 +1207,26 @@ floam_status floam_odom_update_selector(floam_odom* o, floam_cloud* edge, floam_
   return guarded([&] {
     if (!o || !edge || !surf) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
     if (deskew && edge != surf) odom_prevoxel(o, edge);
-    cloud_on_main(edge);
-    cloud_on_main(surf);
-    if (!deskew) return odom_update(o, edge, surf, FLOAM_VANILLA);
-    return odom_update_deskew(o, edge, surf);
+    if (deskew && o->pre_valid >= 0) {   // ordered after the grid rebuild (odom_issue)
+      o->late_wait[0] = edge;
+      o->late_wait[1] = surf;
+    } else {
+      cloud_on_main(edge);
+      cloud_on_main(surf);
+    }
+    floam_status r;
+    try {
+      r = deskew ? odom_update_deskew(o, edge, surf) : odom_update(o, edge, surf, FLOAM_VANILLA);
+    } catch (...) {
+      o->late_wait[0] = o->late_wait[1] = nullptr;
+      throw;
+    }
+    if (!o->use_graph) {   // an event right after the update's last use: a later producer on another stream (the
+      hipStream_t st = ctx_for(o->device).stream;   // next extraction into these buffers) waits for exactly this
+      cloud_publish(edge, st);                       // update, not for whatever the host has issued since
+      if (surf != edge) cloud_publish(surf, st);
+    }
+    return r;
   });
 }
 
