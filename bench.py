@@ -49,28 +49,6 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def prefill_map(synth, oracle_fe, config, R, target):
-    """Edge/surf features of scan 0 (sensor frame == map frame) plus features of earlier scans on the ground-truth
-    trajectory, transformed into the map frame, until `target` points (the raw map initMapWithPoints receives)."""
-    e0, s0 = oracle_fe(synth.generate_scan(config, 0), R)
-    E, S = [synth.to_xyzi(e0)], [synth.to_xyzi(s0)]
-    n = e0.shape[0] + s0.shape[0]
-    k = -3
-    while n < target:
-        raw = synth.generate_scan(config, k)
-        e, s = oracle_fe(raw, R)
-        T = synth.gt_pose_matrix(k)
-        E.append(synth.to_xyzi(synth.transform_points(e, T)))
-        S.append(synth.to_xyzi(synth.transform_points(s, T)))
-        n += e.shape[0] + s.shape[0]
-        k -= 3
-    E, S = np.concatenate(E), np.concatenate(S)
-    extra = E.shape[0] + S.shape[0] - target
-    if target and extra > 0:   # trim the surf tail to hit the stated size exactly
-        S = S[: S.shape[0] - extra]
-    return E, S
-
-
 def hbm_traffic(kernel_substr):
     """HBM bytes per launch of the dominant kernel from the newest committed rocprofv3 PMC summary
     (profiles/<tag>/hbm_traffic.json, written by tools/prof_summary.py from separate --pmc FETCH_SIZE / WRITE_SIZE
@@ -117,9 +95,19 @@ def main():
     R = model.rings
     target = synth.MAP_PREFILL.get(cfg, 0)
 
-    def oracle_fe(raw, R_):
+    def oracle_fe(raw, R_):   # the CPU baseline leg only
         e, s, _ = oracle.feature_extraction(raw, R_, MIN_DIS, MAX_DIS, canonical=True)
         return e, s
+
+    params = floam_amd.LidarParams(num_lines=R, scan_period=SCAN_PERIOD, vertical_angle=2.0, max_distance=MAX_DIS,
+                                   min_distance=MIN_DIS)
+    fe_lp = floam_amd.LaserProcessingClass(device=dev)
+    fe_lp.init(params)
+
+    def gpu_fe(raw, R_):   # featureExtraction on the GPU (untimed: the prefill's earlier scans)
+        de, ds = floam_amd.DeviceCloud(device=dev), floam_amd.DeviceCloud(device=dev)
+        fe_lp.featureExtraction(floam_amd.DeviceCloud(raw, device=dev), de, ds)
+        return de.download(), ds.download()
 
     t0 = time.time()
     n_scans = args.warmup + args.steps
@@ -127,12 +115,11 @@ def main():
     # a sequence that starts elsewhere on the trajectory would not match the map prefilled around the origin)
     scan_offset = 0
     raws = [synth.generate_scan(cfg, scan_offset + k) for k in range(1, n_scans + 1)]
-    mapE, mapS = prefill_map(synth, oracle_fe, cfg, R, target)
+    mapE, mapS = synth.prefill_map(cfg, gpu_fe, target)
+    fe_lp.close()
     log(f"[rank {rank}] generated {n_scans} scans ({raws[0].shape[0]} pts) + map {mapE.shape[0]}+{mapS.shape[0]} "
         f"in {time.time() - t0:.1f}s")
 
-    params = floam_amd.LidarParams(num_lines=R, scan_period=SCAN_PERIOD, vertical_angle=2.0, max_distance=MAX_DIS,
-                                   min_distance=MIN_DIS)
     d_raw = [floam_amd.DeviceCloud(r, device=dev) for r in raws]       # inputs resident in HBM
     d_mapE, d_mapS = floam_amd.DeviceCloud(mapE, device=dev), floam_amd.DeviceCloud(mapS, device=dev)
     allreduce_impl = None

@@ -36,7 +36,9 @@ EXPORTS = [
     "floam_odom_create", "floam_odom_destroy", "floam_odom_init_map", "floam_odom_update_selector",
     "floam_odom_update", "floam_odom_get_pose", "floam_odom_get_last_pose", "floam_odom_get_velocity",
     "floam_odom_get_map", "floam_odom_get_map_sizes", "floam_odom_download_maps", "floam_odom_get_stats",
-    "floam_odom_set_async", "floam_odom_wait",
+    "floam_odom_set_async", "floam_odom_wait", "floam_odom_keyframe_update", "floam_odom_set_precision",
+    "floam_odom_set_trace", "floam_odom_get_traces", "floam_odom_get_correspondences",
+    "floam_odom_find_correspondences",
     "floam_comm_unique_id", "floam_odom_set_shard", "floam_odom_set_shard_callback",
     "floam_last_error", "floam_version", "floam_reset_process_state", "floam_device_synchronize",
     "floam_profile_enable", "floam_profile_read", "floam_profile_reset",
@@ -66,6 +68,9 @@ class OdomStats(C.Structure):
                 ("lm_iterations", C.c_int), ("map_updated", C.c_int), ("corner_map", C.c_size_t),
                 ("surf_map", C.c_size_t), ("final_cost", C.c_double)]
 
+
+PRECISION_FP64, PRECISION_FP32 = 0, 1
+TRACE_WORDS = 49   # per-solve trace record (include/floam_c.h floam_odom_set_trace)
 
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.c_int, C.c_void_p)
 
@@ -113,6 +118,10 @@ def load(path: str | None = None):
         "floam_odom_get_map": [vp, vp], "floam_odom_get_map_sizes": [vp, szp, szp],
         "floam_odom_download_maps": [vp, vp, sz, vp, sz], "floam_odom_get_stats": [vp, C.POINTER(OdomStats)],
         "floam_odom_set_async": [vp, i32], "floam_odom_wait": [vp, sz, dp, sz, szp],
+        "floam_odom_keyframe_update": [vp, dp, dp, ip], "floam_odom_set_precision": [vp, i32],
+        "floam_odom_set_trace": [vp, sz], "floam_odom_get_traces": [vp, dp, sz, szp],
+        "floam_odom_get_correspondences": [vp, i32, vp, vp, ip, C.POINTER(C.c_float), dp, sz, szp],
+        "floam_odom_find_correspondences": [vp, vp, vp, dp, dp],
         "floam_comm_unique_id": [vp], "floam_odom_set_shard": [vp, i32, i32, vp],
         "floam_odom_set_shard_callback": [vp, i32, i32, ALLREDUCE_FN, vp],
         "floam_device_synchronize": [i32], "floam_profile_enable": [i32, i32],

@@ -201,9 +201,9 @@ void reserve_grid(Grid& g, int ub) {
   g.xyz.reserve(ub);
   g.counters.reserve(8);
   int bits = 10;
-  // capacity >= points >= cells, so every insert terminates; the occupied cells are a fraction of the points (several
-  // map points per 0.5-m cell), so the load stays well below 1 and the probed tables stay compact in L2
-  while ((1 << bits) < ub) ++bits;
+  // capacity >= 2 x points >= 2 x cells: the load never exceeds 1/2, so every insert and every probe of an absent
+  // cell (the kNN's lookups) reaches an empty slot and terminates, even when every point has a cell of its own
+  while ((1 << bits) < 2 * ub) ++bits;
   if (bits > g.bits) {   // (reserve keeps the arrays when their capacity already covers the larger table)
     g.coarse.reserve((size_t)1 << bits);
     for (int k = 0; k < 2; ++k) g.clist[k].reserve((size_t)1 << bits);

@@ -247,17 +247,17 @@ struct floam_odom {
   Grid gE, gS;
   bool grid_dirty = true;
   CorrSet ce, cs;
-  DevBuf<double> partials, sums;
-  DevBuf<unsigned> step_counter;
-  // FLOAM_LM_MODE (squared loss): 0 resident lm_solve_gram (one launch per solve), 1 lm_step_gram (one launch per
-  // evaluation), 2 per-record lm_step (also the Huber path)
-  int lm_mode = 0;
-  DevBuf<double> gpart;                 // per-block surf Gram partials
-  DevBuf<double> gmat;                  // the solve's surf Gram matrix + its origin
-  DevBuf<unsigned> gcnt;                // ticket words of its reduction
-  DevBuf<unsigned long long> dbg_stamps;   // FLOAM_DEBUG_STAMPS=1: lm_step segment times (diagnostic)
+  bool fp32 = false;                       // floam_odom_set_precision: fp32 geometry + residuals (C5 sweep)
+  LMBuffers lmb;                           // the solves' scratch (lm.hip)
+  DevBuf<unsigned long long> dbg_stamps;   // FLOAM_DEBUG_STAMPS=1: the resident solve's segment times (diagnostic)
   int qhint[2] = {0, 0};                   // recent downsampled edge / surf query counts (search grid sizing)
-  DevBuf<unsigned long long> knn_trace;    // FLOAM_KNN_TRACE=file: per-wave (start, end) of the kNN launch (diagnostic)
+  // stage inspection (floam_odom_set_trace): one record per solve, and the last correspondence pass's queries
+  int trace_cap = 0;
+  DevBuf<double> trace;
+  DevBuf<unsigned> trace_count;
+  const PointRec* last_q[2] = {nullptr, nullptr};   // the last pass's query clouds (downsampled, sensor frame)
+  const int* last_qn = nullptr;                     // their device counts
+  DevBuf<double> kf_io;                             // floam_odom_keyframe_update: pose in, flag out
   DevBuf<LMState> lm;
   // call 1 of a deskewed selector downsamples the edge cloud only (Q4), in the sensor frame: that VoxelGrid runs on a
   // side stream as soon as the scan's features exist, overlapped with the previous update (double-buffered by parity)
@@ -310,6 +310,7 @@ struct floam_odom {
   floam_allreduce_fn ar_fn = nullptr;   // host all-reduce (validation mode), used when comm is null
   void* ar_user = nullptr;
   HostBuf<double> h_sums;
+  bool sharded() const { return world > 1 || comm != nullptr; }
   floam_odom_stats stats{};
   floam_status last_warning = FLOAM_OK;
 };
@@ -371,18 +372,21 @@ void check_params(const floam_lidar_params* p) {
 }
 
 // ------------------------------------------------------------------------------------- odometry internals
+// the one collective of the sharded path: the 29 sums (cost, J^T J, J^T r, count) of an LM evaluation, summed over
+// the ranks in place — RCCL on the library stream (no host synchronisation), or the validation callback
 void allreduce_sums(floam_odom* o, DeviceCtx& ctx) {
+  double* sums = o->lmb.sums.p;
   if (o->comm) {
-    const ncclResult_t r = ncclAllReduce(o->sums.p, o->sums.p, LM_NSUM, ncclDouble, ncclSum, o->comm, ctx.stream);
+    const ncclResult_t r = ncclAllReduce(sums, sums, LM_NSUM, ncclDouble, ncclSum, o->comm, ctx.stream);
     if (r != ncclSuccess) throw Error(FLOAM_ERR_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
     return;
   }
   if (!o->ar_fn) throw Error(FLOAM_ERR_COMM, "sharded odometry without a communicator");
   o->h_sums.reserve(LM_NSUM);
-  FLOAM_HIP(hipMemcpyAsync(o->h_sums.p, o->sums.p, sizeof(double) * LM_NSUM, hipMemcpyDeviceToHost, ctx.stream));
+  FLOAM_HIP(hipMemcpyAsync(o->h_sums.p, sums, sizeof(double) * LM_NSUM, hipMemcpyDeviceToHost, ctx.stream));
   FLOAM_HIP(hipStreamSynchronize(ctx.stream));
   if (o->ar_fn(o->h_sums.p, LM_NSUM, o->ar_user) != 0) throw Error(FLOAM_ERR_COMM, "host all-reduce callback failed");
-  FLOAM_HIP(hipMemcpyAsync(o->sums.p, o->h_sums.p, sizeof(double) * LM_NSUM, hipMemcpyHostToDevice, ctx.stream));
+  FLOAM_HIP(hipMemcpyAsync(sums, o->h_sums.p, sizeof(double) * LM_NSUM, hipMemcpyHostToDevice, ctx.stream));
   FLOAM_HIP(hipStreamSynchronize(ctx.stream));
 }
 
@@ -430,86 +434,59 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
       c = nullptr;
     }
   o->lm.reserve(1);
-  o->partials.reserve((size_t)LM_NSUM * 512);
-  if (!o->step_counter.p) {
-    o->step_counter.reserve(1);
-    FLOAM_HIP(hipMemsetAsync(o->step_counter.p, 0, sizeof(unsigned), st));
-    const char* pe = std::getenv("FLOAM_LM_MODE");
-    o->lm_mode = pe ? std::atoi(pe) : 0;
-    if (std::getenv("FLOAM_KNN_TRACE")) o->knn_trace.reserve(1u << 17);
-    if (std::getenv("FLOAM_DEBUG_STAMPS")) {
-      o->dbg_stamps.reserve(32);
-      FLOAM_HIP(hipMemsetAsync(o->dbg_stamps.p, 0, sizeof(unsigned long long) * 32, st));
-      FLOAM_HIP(hipMemsetAsync(o->dbg_stamps.p + 25, 0xFF, sizeof(unsigned long long), st));
-    }
+  o->lmb.reserve(st);
+  if (!o->dbg_stamps.p && std::getenv("FLOAM_DEBUG_STAMPS")) {
+    o->dbg_stamps.reserve(8);
+    FLOAM_HIP(hipMemsetAsync(o->dbg_stamps.p, 0, sizeof(unsigned long long) * 8, st));
   }
   o->prof_bytes.reserve(2);
   if (!o->prof_bytes_init) {
     FLOAM_HIP(hipMemsetAsync(o->prof_bytes.p, 0, sizeof(unsigned long long) * 2, st));
     o->prof_bytes_init = true;
   }
-  o->sums.reserve(LM_NSUM);
   // the search grid is sized from the downsampled counts seen recently (the device count of this call is not
   // known on the host without a sync); the kernel grid-strides, so an underestimate only costs time
   QuerySet qe{dE, dcnt + 0, ne_ub};
   QuerySet qs{dS, dcnt + 1, ns_ub};
   if (o->qhint[0] > 0) qe.grid_hint = std::min(ne_ub, o->qhint[0] + o->qhint[0] / 4 + 256);
   if (o->qhint[1] > 0) qs.grid_hint = std::min(ns_ub, o->qhint[1] + o->qhint[1] / 4 + 256);
-  const bool sharded = o->world > 1;
-  // the single-block Gram solve (squared loss, bounded edge count); else one launch per evaluation (or lm_solve)
-  // squared loss: surf sums from the Gram matrix (resident solve, or one launch per evaluation); else per record
-  const bool gram = !sharded && o->lm_mode != 2 && lm_gram_supported(o->huber);
-  if (gram) {
-    o->gpart.reserve(lm_gram_partials());
-    o->gmat.reserve(lm_gram_words());
-    if (!o->gcnt.p) {
-      o->gcnt.reserve(lm_gram_counters());
-      FLOAM_HIP(hipMemsetAsync(o->gcnt.p, 0, sizeof(unsigned) * lm_gram_counters(), st));
-    }
-  }
+  o->ce.trace = o->cs.trace = o->trace_cap > 0;
+  o->last_q[0] = dE;
+  o->last_q[1] = dS;
+  o->last_qn = dcnt;
+  const bool sharded = o->sharded();
+  const int mode = lm_mode(o->huber, o->fp32);
+  const bool gram = (mode & LM_GRAM) != 0;
   for (int it = 0; it < o->optimization_count; ++it) {
     {
       ProfScope ps(ctx, "knn", FLOAM_PROF_KNN);   // the correspondence pass: search + geometry
       {
         ProfScope ps1(ctx, "knn_search", FLOAM_PROF_KNN_DETAIL);
-        // (also resets the LM state; the first solve starts at the prediction)
-        knn_launch(o->lm.p, nullptr, it == 0 ? x0_dev : nullptr, qe, o->gE, o->mapE.pts.p,
-                   o->ce, qs, o->gS, o->mapS.pts.p, o->cs, o->mapE.count.p, o->mapS.count.p, o->rank, o->world, st,
-                   o->knn_trace.p ? o->knn_trace.p : (o->dbg_stamps.p ? o->dbg_stamps.p + 8 : nullptr));
+        // (also starts the solve: LM state reset, the first solve at the prediction)
+        knn_launch(o->lm.p, it == 0 ? x0_dev : nullptr, qe, o->gE, o->ce, qs, o->gS, o->cs, o->mapE.count.p,
+                   o->mapS.count.p, o->rank, o->world, st);
       }
       ProfScope ps2(ctx, "knn_geometry", FLOAM_PROF_KNN_DETAIL);
-      geom_launch(o->lm.p, qe, o->gE, o->mapE.pts.p, o->ce, qs, o->gS, o->mapS.pts.p, o->cs,
-                  gram ? o->gpart.p : nullptr, gram ? o->gmat.p : nullptr, o->gcnt.p, st);
+      geom_launch(o->lm.p, qe, o->ce, qs, o->cs, gram, o->fp32, o->lmb, st);
     }
     if (ctx.profile & FLOAM_PROF_KNN_BYTES) {   // replay only: algorithmic bytes of the two launches above
-      knn_traffic_launch(o->lm.p, qe, o->gE, o->mapE.pts.p, o->ce, o->rank, o->world, o->traffic_set,
-                         o->prof_bytes.p + 0, st);
-      knn_traffic_launch(o->lm.p, qs, o->gS, o->mapS.pts.p, o->cs, o->rank, o->world, o->traffic_set,
-                         o->prof_bytes.p + 1, st);
+      knn_traffic_launch(o->lm.p, qe, o->gE, o->ce, o->rank, o->world, o->traffic_set, o->prof_bytes.p + 0, st);
+      knn_traffic_launch(o->lm.p, qs, o->gS, o->cs, o->rank, o->world, o->traffic_set, o->prof_bytes.p + 1, st);
     }
-    // iteration zero + at most max_num_iterations = 4 candidates (odomEstimationClass.cpp:102)
-    if (gram && o->lm_mode == 0) {
+    // ceres::Solve: iteration zero + at most max_num_iterations = 4 candidates (odomEstimationClass.cpp:102)
+    if (!sharded) {
       ProfScope ps(ctx, "lm_solve", FLOAM_PROF_LM);
-      lm_solve_gram_launch(o->lm.p, o->ce, dcnt + 0, ne_ub, o->gpart.p, o->gmat.p, o->partials.p,
-                           o->step_counter.p, st, o->dbg_stamps.p);
-      continue;
-    }
-    for (int ev = 0; ev < 5; ++ev) {
-      ProfScope ps(ctx, "lm_step", FLOAM_PROF_LM);
-      if (gram) {
-        lm_step_gram_launch(o->lm.p, o->ce, dcnt + 0, ne_ub, o->gpart.p, o->gmat.p, false, o->partials.p,
-                            o->step_counter.p, st, o->dbg_stamps.p);
-      } else if (sharded) {
-        const int nblk = lm_eval_launch(o->lm.p, o->ce, dcnt + 0, ne_ub, o->cs, dcnt + 1, ns_ub, o->huber,
-                                        o->partials.p, st);
-        lm_reduce_launch(o->partials.p, nblk, o->sums.p, st);
+      lm_solve_launch(o->lm.p, o->ce, dcnt + 0, ne_ub, o->cs, dcnt + 1, ns_ub, mode, o->lmb, st, o->dbg_stamps.p);
+    } else {   // one launch + one all-reduce of the 29 sums per evaluation, all on the stream
+      ProfScope ps(ctx, "lm_solve_sharded", FLOAM_PROF_LM);
+      for (int ev = 0; ev < 5; ++ev) {
+        lm_shard_eval_launch(ev, o->lm.p, o->ce, dcnt + 0, ne_ub, o->cs, dcnt + 1, ns_ub, mode, o->lmb, st);
         allreduce_sums(o, ctx);
-        lm_control_launch(o->lm.p, o->sums.p, 0, st);
-      } else {
-        lm_step_launch(o->lm.p, o->ce, dcnt + 0, ne_ub, o->cs, dcnt + 1, ns_ub, o->huber, o->partials.p,
-                       o->step_counter.p, st, o->dbg_stamps.p);
       }
+      lm_shard_final_launch(o->lm.p, o->lmb, st);
     }
+    if (o->trace_cap > 0)
+      lm_trace_launch(o->lm.p, dcnt, o->mapE.count.p, o->mapS.count.p, o->trace.p, o->trace_count.p, o->trace_cap, st);
   }
   if (o->optimization_count <= 0) lm_init_dev_launch(o->lm.p, x0_dev, st);
   const bool prof_knn = (ctx.profile & FLOAM_PROF_KNN_BYTES) != 0;
@@ -622,7 +599,7 @@ int odom_begin(floam_odom* o, DeviceCtx& ctx) {
 // Graph capture of one update (when enabled): odom_capture_begin before its first device operation,
 // odom_capture_end after its last one instantiates or updates the executable graph of its kind and launches it.
 bool odom_capture_begin(floam_odom* o, DeviceCtx& ctx) {
-  if (!o->use_graph || ctx.profile != 0 || o->world > 1) return false;
+  if (!o->use_graph || ctx.profile != 0 || o->sharded()) return false;
   FLOAM_HIP(hipStreamBeginCapture(ctx.stream, hipStreamCaptureModeRelaxed));
   capture_state().active = true;
   return true;
@@ -776,14 +753,14 @@ floam_status odom_update_deskew(floam_odom* o, floam_cloud* edge, floam_cloud* s
     if (o->optimization_count > 2) o->optimization_count--;
     GatherArgs g1;
     odom_issue(o, ctx, edge, edge, ne_ub, ne_ub, o->ds.p->x0[0], 2 * ring, 0, pre, true, &g1);
-    if (pre >= 0) {   // the side stream may refill this parity's buffers once call 1 has run
-      FLOAM_HIP(hipEventRecord(o->side_ev[pre], ctx.stream));
-      o->side_ev_rec[pre] = true;
-    }
     {
       ProfScope ps(ctx, "deskew", FLOAM_PROF_CLOUD);
       deskew_bridge_launch(o->lm.p, o->ds.p, o->lp.scan_period, edge->pts.p, edge->count.p, ne_ub, surf->pts.p,
                            surf->count.p, ns_ub, ctx.stream, g1);
+    }
+    if (pre >= 0) {   // the side stream may refill this parity's buffers once call 1 has run, including the deferred
+      FLOAM_HIP(hipEventRecord(o->side_ev[pre], ctx.stream));   // status gather in deskew_bridge (reads pcnt[pre])
+      o->side_ev_rec[pre] = true;
     }
     if (o->optimization_count > 2) o->optimization_count--;
     odom_issue(o, ctx, edge, surf, ne_ub, ns_ub, o->ds.p->x0[1], 2 * ring + 1,
@@ -1120,7 +1097,6 @@ floam_status floam_odom_destroy(floam_odom* o) {
     if (o) {
       DeviceCtx& ctx = ctx_for(o->device);
       FLOAM_HIP(hipStreamSynchronize(ctx.stream));
-      ctrl_stamps_print();
       for (auto& P : o->inflight) {
         FLOAM_HIP(hipEventDestroy(P.ev));
         for (void* b : P.graveyard) (void)hipFree(b);
@@ -1129,32 +1105,13 @@ floam_status floam_odom_destroy(floam_odom* o) {
       for (auto& row : o->graph_exec)
         for (auto& ex : row)
           if (ex) FLOAM_HIP(hipGraphExecDestroy(ex));
-      if (o->knn_trace.p) {   // the last kNN launch's per-wave stamps, raw (2 x u64 per wave)
-        std::vector<unsigned long long> h((size_t)1 << 17);
-        FLOAM_HIP(hipMemcpy(h.data(), o->knn_trace.p, h.size() * 8, hipMemcpyDeviceToHost));
-        if (FILE* f = std::fopen(std::getenv("FLOAM_KNN_TRACE"), "wb")) {
-          std::fwrite(h.data(), 8, h.size(), f);
-          std::fclose(f);
-        }
-      }
-      if (o->dbg_stamps.p) {
-        unsigned long long h[32];
+      if (o->dbg_stamps.p) {   // FLOAM_DEBUG_STAMPS: the resident solve's control-block segments (100 MHz ticks)
+        unsigned long long h[8];
         FLOAM_HIP(hipMemcpy(h, o->dbg_stamps.p, sizeof(h), hipMemcpyDeviceToHost));
         const double n = h[4] ? (double)h[4] : 1.0;
-        std::fprintf(stderr, "[floam stamps] LM evaluations x%llu (control block): stage / surf sums %.2f us, wait %.2f us, reduce %.2f us,"
-                   " control step %.2f us\n", h[4], h[0] / n / 100.0, h[1] / n / 100.0, h[2] / n / 100.0,
-                   h[3] / n / 100.0);
-        if (h[6])
-          std::fprintf(stderr, "[floam stamps] evaluation blocks: %.2f us each; first start %.2f us, last arrival "
-                       "%.2f us after the control block's start\n", h[5] / (double)h[6] / 100.0, h[7] / n / 100.0,
-                       h[27] / n / 100.0);
-        for (int set = 0; set < 2; ++set) {
-          const unsigned long long* c = h + 8 + 8 * set;
-          const double q = c[4] ? (double)c[4] : 1.0;
-          std::fprintf(stderr, "[floam stamps] knn %s: %llu queries, per query: 3x3x3 block %.2f us; %llu full-box "
-                       "fallbacks, %.2f us each\n", set ? "surf" : "edge", c[4], c[0] / q / 100.0, c[2],
-                       c[1] / (c[2] ? (double)c[2] : 1.0) / 100.0);
-        }
+        std::fprintf(stderr, "[floam stamps] %llu solves (control block, per solve): surf sums %.2f us, wait for the "
+                     "evaluation blocks %.2f us, reduce %.2f us, control step + release %.2f us\n", h[4],
+                     h[0] / n / 100.0, h[1] / n / 100.0, h[2] / n / 100.0, h[3] / n / 100.0);
       }
       if (o->side) {
         (void)hipStreamSynchronize(o->side);
@@ -1344,6 +1301,8 @@ floam_status floam_comm_unique_id(void* id) {
 floam_status floam_odom_set_shard(floam_odom* o, int rank, int world, const void* id) {
   return guarded([&] {
     if (!o || world < 1 || rank < 0 || rank >= world) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "bad rank / world");
+    if (world > 1 && !id) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null unique id");
+    odom_collect(o, ctx_for(o->device), 0);
     if (o->comm) {
       ncclCommDestroy(o->comm);
       o->comm = nullptr;
@@ -1351,8 +1310,7 @@ floam_status floam_odom_set_shard(floam_odom* o, int rank, int world, const void
     o->ar_fn = nullptr;
     o->rank = rank;
     o->world = world;
-    if (world > 1) {
-      if (!id) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null unique id");
+    if (id) {   // a communicator also for world = 1: the RCCL path of the sharded solve on one GPU
       FLOAM_HIP(hipSetDevice(o->device));
       ncclUniqueId u;
       std::memcpy(&u, id, sizeof(u));
@@ -1367,6 +1325,7 @@ floam_status floam_odom_set_shard_callback(floam_odom* o, int rank, int world, f
   return guarded([&] {
     if (!o || world < 1 || rank < 0 || rank >= world) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "bad rank / world");
     if (world > 1 && !fn) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null all-reduce callback");
+    odom_collect(o, ctx_for(o->device), 0);
     if (o->comm) {
       ncclCommDestroy(o->comm);
       o->comm = nullptr;
@@ -1375,6 +1334,156 @@ floam_status floam_odom_set_shard_callback(floam_odom* o, int rank, int world, f
     o->world = world;
     o->ar_fn = fn;
     o->ar_user = user;
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_odom_set_precision(floam_odom* o, int precision) {
+  return guarded([&] {
+    if (!o || (precision != FLOAM_PRECISION_FP64 && precision != FLOAM_PRECISION_FP32))
+      throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null handle or unknown precision");
+    odom_collect(o, ctx_for(o->device), 0);
+    o->fp32 = precision == FLOAM_PRECISION_FP32;
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_odom_set_trace(floam_odom* o, size_t capacity) {
+  return guarded([&] {
+    if (!o || capacity > (size_t)1 << 24) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null handle or capacity too large");
+    DeviceCtx& ctx = ctx_for(o->device);
+    odom_collect(o, ctx, 0);
+    o->trace_cap = (int)capacity;
+    if (capacity) {
+      o->trace.reserve(capacity * kTraceWords);
+      o->trace_count.reserve(1);
+      FLOAM_HIP(hipMemsetAsync(o->trace_count.p, 0, sizeof(unsigned), ctx.stream));
+      FLOAM_HIP(hipStreamSynchronize(ctx.stream));
+    }
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_odom_get_traces(floam_odom* o, double* out, size_t capacity, size_t* n_out) {
+  return guarded([&] {
+    if (!o || o->trace_cap <= 0) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null handle or tracing off");
+    DeviceCtx& ctx = ctx_for(o->device);
+    odom_collect(o, ctx, 0);
+    unsigned n = 0;
+    FLOAM_HIP(hipMemcpyAsync(&n, o->trace_count.p, sizeof(unsigned), hipMemcpyDeviceToHost, ctx.stream));
+    FLOAM_HIP(hipStreamSynchronize(ctx.stream));
+    const size_t k = std::min((size_t)n, capacity);
+    if (k) {
+      if (!out) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null output");
+      FLOAM_HIP(hipMemcpy(out, o->trace.p, k * kTraceWords * sizeof(double), hipMemcpyDeviceToHost));
+    }
+    if (n_out) *n_out = n;
+    FLOAM_HIP(hipMemsetAsync(o->trace_count.p, 0, sizeof(unsigned), ctx.stream));
+    FLOAM_HIP(hipStreamSynchronize(ctx.stream));
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_odom_find_correspondences(floam_odom* o, const floam_cloud* edge, const floam_cloud* surf,
+                                             const double q[4], const double t[3]) {
+  return guarded([&] {
+    if (!o || !edge || !surf || !q || !t) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
+    if (o->trace_cap <= 0) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "tracing off (floam_odom_set_trace)");
+    DeviceCtx& ctx = ctx_for(o->device);
+    hipStream_t st = ctx.stream;
+    FLOAM_HIP(hipSetDevice(o->device));
+    odom_collect(o, ctx, 0);
+    cloud_on_main(edge);
+    cloud_on_main(surf);
+    const int ne_ub = (int)cloud_ub(edge), ns_ub = (int)cloud_ub(surf);
+    o->dE.reserve(std::max(ne_ub, 1));
+    o->dS.reserve(std::max(ns_ub, 1));
+    o->cnt.reserve(4);
+    VoxelJob je, js;   // VelToIntensityCopy + downSamplingToMap (:53-54, :137-142)
+    je.part0 = edge->pts.p; je.d_n0 = edge->count.p; je.n0_ub = ne_ub; je.leaf = o->leafE;
+    je.out = o->dE.p; je.d_out = o->cnt.p + 0;
+    js.part0 = surf->pts.p; js.d_n0 = surf->count.p; js.n0_ub = ns_ub; js.leaf = o->leafS;
+    js.out = o->dS.p; js.d_out = o->cnt.p + 1;
+    voxel2_launch(o->vs, je, js, st);
+    if (o->grid_dirty) {
+      grid_build_launch(o->gE, o->mapE.pts.p, o->mapE.count.p, (int)o->mapE_n, o->gS, o->mapS.pts.p,
+                        o->mapS.count.p, (int)o->mapS_n, st, nullptr);
+      o->grid_dirty = false;
+    }
+    o->lm.reserve(1);
+    o->lmb.reserve(st);
+    o->kf_io.reserve(16);
+    const double x[7] = {q[0], q[1], q[2], q[3], t[0], t[1], t[2]};
+    FLOAM_HIP(hipMemcpyAsync(o->kf_io.p, x, sizeof(x), hipMemcpyHostToDevice, st));
+    o->ce.trace = o->cs.trace = true;
+    QuerySet qe{o->dE.p, o->cnt.p + 0, ne_ub}, qs{o->dS.p, o->cnt.p + 1, ns_ub};
+    knn_launch(o->lm.p, o->kf_io.p, qe, o->gE, o->ce, qs, o->gS, o->cs, o->mapE.count.p, o->mapS.count.p, 0, 1, st);
+    geom_launch(o->lm.p, qe, o->ce, qs, o->cs, false, o->fp32, o->lmb, st);
+    o->last_q[0] = o->dE.p;
+    o->last_q[1] = o->dS.p;
+    o->last_qn = o->cnt.p;
+    FLOAM_HIP(hipStreamSynchronize(st));
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_odom_get_correspondences(floam_odom* o, int which, void* queries, uint8_t* flags, int* idx,
+                                            float* sqd, double* records, size_t capacity, size_t* n_out) {
+  return guarded([&] {
+    if (!o || (which != 0 && which != 1)) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null handle or bad set");
+    if (o->trace_cap <= 0 || !o->last_qn) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "tracing off or no update yet");
+    DeviceCtx& ctx = ctx_for(o->device);
+    odom_collect(o, ctx, 0);
+    FLOAM_HIP(hipStreamSynchronize(ctx.stream));
+    int n = 0;
+    FLOAM_HIP(hipMemcpy(&n, o->last_qn + which, sizeof(int), hipMemcpyDeviceToHost));
+    const CorrSet& c = which ? o->cs : o->ce;
+    n = std::min(n, c.cap);
+    if (n_out) *n_out = (size_t)n;
+    const size_t k = std::min((size_t)n, capacity);
+    if (!k) return FLOAM_OK;
+    if (queries)
+      FLOAM_HIP(hipMemcpy(queries, o->last_q[which], k * sizeof(PointRec), hipMemcpyDeviceToHost));
+    if (flags) FLOAM_HIP(hipMemcpy(flags, c.valid.p, k, hipMemcpyDeviceToHost));
+    const int F = which ? SURF_FIELDS : EDGE_FIELDS;
+    std::vector<double> rb;
+    if (records) {   // SoA [field][cap] -> row-major [k][F]
+      rb.resize((size_t)F * c.cap);
+      FLOAM_HIP(hipMemcpy(rb.data(), c.rec.p, rb.size() * sizeof(double), hipMemcpyDeviceToHost));
+      for (size_t i = 0; i < k; ++i)
+        for (int f = 0; f < F; ++f) records[i * F + f] = rb[(size_t)f * c.cap + i];
+    }
+    if (idx || sqd) {   // k-major [5][cap] -> row-major [k][5]
+      std::vector<int> ib((size_t)5 * c.cap);
+      std::vector<float> sb((size_t)5 * c.cap);
+      FLOAM_HIP(hipMemcpy(ib.data(), c.nnidx.p, ib.size() * sizeof(int), hipMemcpyDeviceToHost));
+      FLOAM_HIP(hipMemcpy(sb.data(), c.nnsqd.p, sb.size() * sizeof(float), hipMemcpyDeviceToHost));
+      for (size_t i = 0; i < k; ++i)
+        for (int j = 0; j < 5; ++j) {
+          if (idx) idx[i * 5 + j] = ib[(size_t)j * c.cap + i];
+          if (sqd) sqd[i * 5 + j] = sb[(size_t)j * c.cap + i];
+        }
+    }
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_odom_keyframe_update(floam_odom* o, const double q[4], const double t[3], int* is_keyframe) {
+  return guarded([&] {
+    if (!o || !q || !t) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
+    DeviceCtx& ctx = ctx_for(o->device);
+    FLOAM_HIP(hipSetDevice(o->device));
+    odom_collect(o, ctx, 0);
+    o->kf_io.reserve(16);
+    const double x[7] = {q[0], q[1], q[2], q[3], t[0], t[1], t[2]};
+    FLOAM_HIP(hipMemcpyAsync(o->kf_io.p, x, sizeof(x), hipMemcpyHostToDevice, ctx.stream));
+    const bool first = g_keyframe_first;
+    g_keyframe_first = false;
+    keyframe_update_launch(o->ds.p, o->kf_io.p, first ? 1 : 0, reinterpret_cast<int*>(o->kf_io.p + 8), ctx.stream);
+    int flag = 0;
+    FLOAM_HIP(hipMemcpyAsync(&flag, o->kf_io.p + 8, sizeof(int), hipMemcpyDeviceToHost, ctx.stream));
+    FLOAM_HIP(hipStreamSynchronize(ctx.stream));
+    if (is_keyframe) *is_keyframe = flag;
     return FLOAM_OK;
   });
 }

@@ -1,0 +1,1064 @@
+// The Levenberg-Marquardt solve of updatePointsToMap on gfx950: ceres::Solve with LEVENBERG_MARQUARDT, DENSE_QR and
+// max_num_iterations = 4 (src/odomEstimationClass.cpp:95-108) over the residual blocks of src/lidarOptimization.cpp
+// (EdgeAnalyticCostFunction :12-43, SurfNormAnalyticCostFunction :51-74, PoseSE3Parameterization :77-140).  The
+// Ceres 1.13 TrustRegionMinimizer + LevenbergMarquardtStrategy control is restated in lm_logic (SURVEY.md §8 a-12;
+// oracle/odom.cpp ceres_solve is the CPU restatement).
+//
+// Single GPU — lm_solve, ONE launch per solve.  Block 0 (control) keeps the LM state in the registers of its first
+// wave and runs the control step; blocks 1..nblk (evaluation) keep their records in registers across the up to five
+// evaluations.  The hand-offs are data-tagged 8-byte granules (MI355X_MICROARCH.md "handoff-1to1": one sc1 store per
+// granule, {tag, 32 data bits}, the consumer polls until every granule carries the tag it expects; no flag words,
+// no counters, no drains):
+//   control -> evaluation: the next evaluation point as 14 granules (7 doubles in halves) + a stop granule;
+//   evaluation -> control: each block's 29 partial sums as 58 granules.
+// Tags are epoch + evaluation index, with the epoch advanced by 8 at every solve (lm_reset), so a granule of an
+// earlier evaluation or solve never matches and nothing is ever cleared.  Every poll is bounded (~0.5 s); a timeout
+// ends the solve with n_res = -1, which the host reports as FLOAM_ERR_DEVICE.
+//
+// Modes (LM_*): GRAM — squared loss (the launch default, Q3): the surf half of every evaluation comes from the Gram
+// matrix of the surf records (exact in real arithmetic, see surf_sums_from_gram) and 32 evaluation blocks evaluate the
+// edge records; otherwise (Huber, fp32) 128 evaluation blocks evaluate every record.  FP32: residuals, Jacobians and
+// the per-thread sums in float (the C5 precision sweep, BASELINE.json configs[4]); reductions and control in double.
+//
+// Multi-GPU — lm_shard_eval: one launch per evaluation, the control step of the previous evaluation (on the
+// all-reduced sums) run redundantly by every block, then this rank's block partials reduced in fixed order by the
+// last-arriving block into the 29 sums the host all-reduces (RCCL) between the launches.
+//
+// Fixed reduction orders throughout (thread -> 8 strips of 32 -> block; blocks -> 8 strips -> total), so the result
+// does not depend on timing; the sharded path on one rank reproduces the single-GPU solve bit for bit.
+#include <cfloat>
+#include <climits>
+
+#include "odom_kernels.hpp"
+
+namespace floam {
+
+namespace {
+constexpr int kTB = 256;
+constexpr long long kSpin = 1ll << 23;   // bounded polls (s_sleep 1 each): ~0.3 s
+
+template <typename R>
+__device__ __forceinline__ R real_min() { return DBL_MIN; }
+template <>
+__device__ __forceinline__ float real_min<float>() { return FLT_MIN; }
+
+// ===================================================================================== residuals (R = double | float)
+// Eigen's q * v: uv = 2 q.vec x v; v + w uv + q.vec x uv
+template <typename R>
+__device__ __forceinline__ void rot(const R* x, R vx, R vy, R vz, R& ox, R& oy, R& oz) {
+  const R qx = x[0], qy = x[1], qz = x[2], qw = x[3];
+  R ux = qy * vz - qz * vy, uy = qz * vx - qx * vz, uz = qx * vy - qy * vx;
+  ux = ux + ux; uy = uy + uy; uz = uz + uz;
+  const R ax = vx + qw * ux, ay = vy + qw * uy, az = vz + qw * uz;
+  ox = ax + (qy * uz - qz * uy);
+  oy = ay + (qz * ux - qx * uz);
+  oz = az + (qx * uy - qy * ux);
+}
+
+// EdgeAnalyticCostFunction::Evaluate (src/lidarOptimization.cpp:12-43): J = -(nu/|nu|)^T [de]x [-[lp]x, I] / |de|
+template <typename R>
+__device__ __forceinline__ R edge_residual(const R* x, const R* r9, R J[6]) {
+  R lx, ly, lz;
+  rot(x, r9[0], r9[1], r9[2], lx, ly, lz);
+  lx = lx + x[4]; ly = ly + x[5]; lz = lz + x[6];
+  const R pax = lx - r9[3], pay = ly - r9[4], paz = lz - r9[5];
+  const R pbx = lx - r9[6], pby = ly - r9[7], pbz = lz - r9[8];
+  const R nux = pay * pbz - paz * pby, nuy = paz * pbx - pax * pbz, nuz = pax * pby - pay * pbx;
+  const R dex = r9[3] - r9[6], dey = r9[4] - r9[7], dez = r9[5] - r9[8];
+  const R de_norm = sqrt(dex * dex + dey * dey + dez * dez);
+  const R nn = sqrt(nux * nux + nuy * nuy + nuz * nuz);
+  const R r = nn / de_norm;
+  const R w0 = -nux / nn, w1 = -nuy / nn, w2 = -nuz / nn;
+  // r1 = w * skew(de): skew(de) = [[0,-dz,dy],[dz,0,-dx],[-dy,dx,0]]
+  const R r10 = w1 * dez + w2 * (-dey);
+  const R r11 = w0 * (-dez) + w2 * dex;
+  const R r12 = w0 * dey + w1 * (-dex);
+  // dp = [-skew(lp), I]; -skew(lp) = [[0,lz,-ly],[-lz,0,lx],[ly,-lx,0]]
+  J[0] = (r11 * (-lz) + r12 * ly) / de_norm;
+  J[1] = (r10 * lz + r12 * (-lx)) / de_norm;
+  J[2] = (r10 * (-ly) + r11 * lx) / de_norm;
+  J[3] = r10 / de_norm;
+  J[4] = r11 / de_norm;
+  J[5] = r12 / de_norm;
+  return r;
+}
+
+// SurfNormAnalyticCostFunction::Evaluate (src/lidarOptimization.cpp:51-74): J = n^T [-[pw]x, I]
+template <typename R>
+__device__ __forceinline__ R surf_residual(const R* x, const R* r7, R J[6]) {
+  R px, py, pz;
+  rot(x, r7[0], r7[1], r7[2], px, py, pz);
+  px = px + x[4]; py = py + x[5]; pz = pz + x[6];
+  const R nx = r7[3], ny = r7[4], nz = r7[5];
+  const R r = (nx * px + ny * py + nz * pz) + r7[6];
+  J[0] = ny * (-pz) + nz * py;
+  J[1] = nx * pz + nz * (-px);
+  J[2] = nx * (-py) + ny * px;
+  J[3] = nx;
+  J[4] = ny;
+  J[5] = nz;
+  return r;
+}
+
+// one residual (r, J) into the 29 sums (cost, J^T J upper, J^T r, count), with ceres::HuberLoss(0.1) + Corrector
+// (rho'' <= 0 everywhere: residual scaling by sqrt(rho')) when HUBER (src/odomEstimationClass.cpp:84-87)
+template <bool HUBER, typename R>
+__device__ __forceinline__ void accumulate_residual(R (&acc)[LM_NSUM], R r, R (&J)[6]) {
+  const R sq = r * r;
+  if (HUBER) {
+    R rho0, rho1;
+    if (sq > R(0.01)) {
+      const R rr = sqrt(sq);
+      rho0 = R(2.0) * R(0.1) * rr - R(0.01);
+      rho1 = fmax(real_min<R>(), R(0.1) / rr);
+    } else {
+      rho0 = sq;
+      rho1 = R(1.0);
+    }
+    acc[0] += R(0.5) * rho0;
+    const R sr = sqrt(rho1);
+    r *= sr;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) J[k] *= sr;
+  } else {
+    acc[0] += R(0.5) * sq;
+  }
+  int h = 1;
+#pragma unroll
+  for (int a = 0; a < 6; ++a)
+#pragma unroll
+    for (int b = a; b < 6; ++b) acc[h++] += J[a] * J[b];
+#pragma unroll
+  for (int a = 0; a < 6; ++a) acc[22 + a] += J[a] * r;
+  acc[28] += R(1.0);
+}
+
+// record slot (edge: 9 fields, surf: 7) of the device-resident correspondence arrays, converted to R
+template <typename R, int N>
+__device__ __forceinline__ void load_rec(const double* __restrict__ rec, int cap, int i, R (&f)[9]) {
+#pragma unroll
+  for (int k = 0; k < 9; ++k) f[k] = k < N ? (R)rec[k * cap + i] : R(0);
+}
+
+// thread sums -> the block's 29 sums in out (LDS), fixed order: 8 strips of 32 threads, then the strips
+__device__ __forceinline__ void block_sums(const double (&acc)[LM_NSUM], double* red /* LDS [LM_NSUM][kTB] */,
+                                           double* strip /* LDS [LM_NSUM][8] */, double* out /* LDS [LM_NSUM] */) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < LM_NSUM; ++k) red[k * kTB + t] = acc[k];
+  __syncthreads();
+  if (t < LM_NSUM * 8) {
+    const int c = t >> 3, p = t & 7;
+    double v = 0.0;
+#pragma unroll
+    for (int j = 0; j < kTB / 8; ++j) v += red[c * kTB + p * (kTB / 8) + j];
+    strip[c * 8 + p] = v;
+  }
+  __syncthreads();
+  if (t < LM_NSUM) {
+    double v = 0.0;
+    for (int p = 0; p < 8; ++p) v += strip[t * 8 + p];
+    out[t] = v;
+  }
+  __syncthreads();
+}
+
+// block partials P(c, b) (c < 29, b < nblk) -> 29 sums in out (LDS), fixed order: component c sums 8 strips of
+// consecutive blocks in block order, then the strip totals in order
+template <typename Load>
+__device__ __forceinline__ void reduce_blocks(Load P, int nblk, double* strip /* LDS [LM_NSUM][8] */,
+                                              double* out /* LDS [LM_NSUM] */) {
+  const int t = threadIdx.x;
+  if (t < LM_NSUM * 8) {
+    const int c = t >> 3, p = t & 7;
+    const int per = (nblk + 7) / 8;
+    const int b0 = p * per, b1 = min(nblk, b0 + per);
+    double v = 0.0;
+    for (int b = b0; b < b1; ++b) v += P(c, b);
+    strip[c * 8 + p] = v;
+  }
+  __syncthreads();
+  if (t < LM_NSUM) {
+    double v = 0.0;
+    for (int p = 0; p < 8; ++p) v += strip[t * 8 + p];
+    out[t] = v;
+  }
+  __syncthreads();
+}
+
+// This block's share of one evaluation at x: every thread's records (the first one held in registers by the caller),
+// summed per thread in R, then reduced in double.  Record index space: edge slots [0, ne), then surf slots.
+template <bool HUBER, typename R>
+__device__ __forceinline__ void eval_records(const R (&x)[7], bool has0, bool edge0, const R (&f0)[9], int i1,
+                                             int stride, int ne, int total, const double* __restrict__ erec,
+                                             const uint8_t* __restrict__ evalid, int ecap,
+                                             const double* __restrict__ srec, const uint8_t* __restrict__ svalid,
+                                             int scap, double (&accd)[LM_NSUM]) {
+  R acc[LM_NSUM];
+#pragma unroll
+  for (int k = 0; k < LM_NSUM; ++k) acc[k] = R(0);
+  if (has0) {
+    R J[6];
+    const R r = edge0 ? edge_residual<R>(x, f0, J) : surf_residual<R>(x, f0, J);
+    accumulate_residual<HUBER, R>(acc, r, J);
+  }
+  for (int idx = i1; idx < total; idx += stride) {   // beyond the record held in registers
+    R f[9], J[6], r;
+    if (idx < ne) {
+      if (!(evalid[idx] & 1)) continue;
+      load_rec<R, EDGE_FIELDS>(erec, ecap, idx, f);
+      r = edge_residual<R>(x, f, J);
+    } else {
+      const int s = idx - ne;
+      if (!(svalid[s] & 1)) continue;
+      load_rec<R, SURF_FIELDS>(srec, scap, s, f);
+      r = surf_residual<R>(x, f, J);
+    }
+    accumulate_residual<HUBER, R>(acc, r, J);
+  }
+#pragma unroll
+  for (int k = 0; k < LM_NSUM; ++k) accd[k] = (double)acc[k];
+}
+
+// ===================================================================================== surf half from G
+// With the squared loss a surf residual and its Jacobian are LINEAR in the record vector w of geom_kernel: with M the
+// matrix of Eigen's q * v (M = I + 2 w [u]x + 2 [u]x^2, u = q.vec) and t' = t - o,
+//   r      = c^T w,     c   = [M (row-major a,e) | t' | 1]     (w[12] = d + n.o absorbs the origin)
+//   J[3+a] = n_a        = e_{9+a}^T w
+//   J[i]   = (lp x n)_i = K_i^T w,  K_i[3c+e] = sum_b eps_ibc M_be,  K_i[9+c] = sum_b eps_ibc t_b,  K_i[12] = 0
+// so the surf part of J^T J, J^T r and the cost are quadratic forms of G = sum w w^T (reduced once per solve by the
+// geometry launch).  The edge records are evaluated per record (EdgeAnalyticCostFunction's J has the direction
+// nu/|nu|, which depends on the pose).  Recentring c on o keeps the cancellation inside G c independent of how far the
+// pose is from the map origin.  Same function values as the per-residual evaluation in exact arithmetic; the rounding
+// differs (~|G| eps in c^T G c, ~1e-9 of the cost at C3; poses agree with the per-record path to ~1e-14).
+__device__ void surf_sums_from_gram(const double* x /* LDS [7] */, const double* o /* LDS [3] */,
+                                    const double (*G)[kGramW] /* LDS */, double n_surf, double* out /* LDS [29] */) {
+  __shared__ double V[7][kGramW];   // K_0..K_5, c
+  __shared__ double Y[7][kGramW];   // G V
+  const int t = threadIdx.x;
+  if (t < kGramW) {   // lanes 0..12 build one component of all 7 vectors
+    const double qx = x[0], qy = x[1], qz = x[2], qw = x[3];
+    const double U[3][3] = {{0, -qz, qy}, {qz, 0, -qx}, {-qy, qx, 0}};
+    double Mm[3][3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+      for (int b = 0; b < 3; ++b) {
+        const double u2 = U[a][0] * U[0][b] + U[a][1] * U[1][b] + U[a][2] * U[2][b];
+        Mm[a][b] = ((a == b) ? 1.0 : 0.0) + 2.0 * qw * U[a][b] + 2.0 * u2;
+      }
+    const double tp[3] = {x[4] - o[0], x[5] - o[1], x[6] - o[2]};   // c: recentred (d absorbed n.o)
+    const double tf[3] = {x[4], x[5], x[6]};                        // K: the Jacobian's lp = M p + t itself
+    const int m = t;   // component of w
+    // register-resident selects instead of run-time array indexing (no scratch)
+    auto Msel = [&](int r, int c) {
+      double v = 0.0;
+#pragma unroll
+      for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b)
+          if (a == r && b == c) v = Mm[a][b];
+      return v;
+    };
+    auto vsel = [&](const double (&vv)[3], int k) { return k == 0 ? vv[0] : (k == 1 ? vv[1] : vv[2]); };
+    double cm = 1.0;
+    if (m < 9) cm = Msel(m / 3, m % 3);
+    else if (m < 12) cm = vsel(tp, m - 9);
+    V[6][m] = cm;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {   // K_i for i = 0..2 (lp x n)
+      const int b1 = (i + 1) % 3, b2 = (i + 2) % 3;   // eps_{i b1 b2} = +1, eps_{i b2 b1} = -1
+      double km = 0.0;
+      if (m < 9) {
+        const int c = m / 3, e = m % 3;   // w index 3c + e: sum_b eps_{ibc} M_be
+        if (c == b2) km = Msel(b1, e);
+        else if (c == b1) km = -Msel(b2, e);
+      } else if (m < 12) {
+        const int c = m - 9;              // sum_b eps_{ibc} t_b
+        if (c == b2) km = vsel(tf, b1);
+        else if (c == b1) km = -vsel(tf, b2);
+      }
+      V[i][m] = km;
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) V[3 + a][m] = (m == 9 + a) ? 1.0 : 0.0;   // K_{3+a} = e_{9+a}
+  }
+  __syncthreads();
+  if (t < 7 * kGramW) {   // Y = G V
+    const int v = t / kGramW, i = t % kGramW;
+    double a = 0.0;
+#pragma unroll
+    for (int j = 0; j < kGramW; ++j) a += G[i][j] * V[v][j];
+    Y[v][i] = a;
+  }
+  __syncthreads();
+  if (t < LM_NSUM) {   // cost, J^T J upper (row-major), J^T r, count
+    double s;
+    if (t == 0) {
+      double a = 0.0;
+#pragma unroll
+      for (int i = 0; i < kGramW; ++i) a += V[6][i] * Y[6][i];
+      s = 0.5 * a;
+    } else if (t < 22) {
+      int hh = t - 1, ja = 0;
+      while (hh >= 6 - ja) { hh -= 6 - ja; ++ja; }
+      const int jb = ja + hh;
+      double a = 0.0;
+#pragma unroll
+      for (int i = 0; i < kGramW; ++i) a += V[ja][i] * Y[jb][i];
+      s = a;
+    } else if (t < 28) {
+      double a = 0.0;
+#pragma unroll
+      for (int i = 0; i < kGramW; ++i) a += V[t - 22][i] * Y[6][i];
+      s = a;
+    } else {
+      s = n_surf;
+    }
+    out[t] = s;
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void gram_pair(int e, int& i, int& j) {   // upper-triangle entry e -> (i, j), i <= j
+  i = 0;
+  while (e >= kGramW - i) {
+    e -= kGramW - i;
+    ++i;
+  }
+  j = i + e;
+}
+
+// G (full symmetric) and its origin o into LDS from the geometry launch's gmat (gv = gmat[threadIdx.x])
+__device__ __forceinline__ void gram_unpack(double gv, double (*G)[kGramW], double* o) {
+  const int t = threadIdx.x;
+  if (t < kGram) {
+    int i, j;
+    gram_pair(t, i, j);
+    G[i][j] = gv;
+    G[j][i] = gv;
+  } else if (t < kGramWords) {
+    o[t - kGram] = gv;
+  }
+  __syncthreads();
+}
+
+// ===================================================================================== LM control (Ceres 1.13)
+// The control step is serial fp64 code, so its cost is its dependent instruction count.  It runs on one wave whose 64
+// lanes all hold the same LM state in REGISTERS for the whole solve (loaded once, stored once); the two SE(3)
+// exponentials of a step — the candidate x [+] delta and the gradient projection x [+] -g of the gradient-norm test —
+// run side by side in lanes 0 and 1 of the same instruction stream; the 6x6 LDL^T divides by each pivot once.
+// Loops are fully unrolled with constant indices so nothing leaves registers.
+
+// PoseSE3Parameterization::Plus + getTransformFromSe3 (src/lidarOptimization.cpp:77-140).  theta^3 is formed by
+// multiplication where the reference calls pow(theta, 3) (<= 1 ulp apart).
+__device__ __forceinline__ void se3_plus(const double (&x)[7], const double (&d)[6], double (&out)[7]) {
+  const double wx = d[0], wy = d[1], wz = d[2];
+  const double theta = sqrt(wx * wx + wy * wy + wz * wz);
+  const double half = 0.5 * theta;
+  double sh, ch;
+  sincos(half, &sh, &ch);
+  const double real_factor = ch;
+  double imag;
+  const bool small = theta < 1e-10;
+  if (small) {
+    const double t2 = theta * theta, t4 = t2 * t2;
+    imag = 0.5 - 0.0208333 * t2 + 0.000260417 * t4;
+  } else {
+    imag = sh / theta;
+  }
+  const double dq[4] = {imag * wx, imag * wy, imag * wz, real_factor};   // x, y, z, w
+  double Jm[3][3];
+  if (small) {
+    const double tx = 2 * dq[0], ty = 2 * dq[1], tz = 2 * dq[2];
+    const double twx = tx * dq[3], twy = ty * dq[3], twz = tz * dq[3];
+    const double txx = tx * dq[0], txy = ty * dq[0], txz = tz * dq[0];
+    const double tyy = ty * dq[1], tyz = tz * dq[1], tzz = tz * dq[2];
+    Jm[0][0] = 1 - (tyy + tzz); Jm[0][1] = txy - twz; Jm[0][2] = txz + twy;
+    Jm[1][0] = txy + twz; Jm[1][1] = 1 - (txx + tzz); Jm[1][2] = tyz - twx;
+    Jm[2][0] = txz - twy; Jm[2][1] = tyz + twx; Jm[2][2] = 1 - (txx + tyy);
+  } else {
+    const double O[3][3] = {{0, -wz, wy}, {wz, 0, -wx}, {-wy, wx, 0}};
+    double O2[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) O2[i][j] = O[i][0] * O[0][j] + O[i][1] * O[1][j] + O[i][2] * O[2][j];
+    double st, ct;
+    sincos(theta, &st, &ct);
+    const double c1 = (1 - ct) / (theta * theta);
+    const double c2 = (theta - st) / (theta * theta * theta);
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) Jm[i][j] = ((i == j) ? 1.0 : 0.0) + c1 * O[i][j] + c2 * O2[i][j];
+  }
+  const double dtx = Jm[0][0] * d[3] + Jm[0][1] * d[4] + Jm[0][2] * d[5];
+  const double dty = Jm[1][0] * d[3] + Jm[1][1] * d[4] + Jm[1][2] * d[5];
+  const double dtz = Jm[2][0] * d[3] + Jm[2][1] * d[4] + Jm[2][2] * d[5];
+  // q+ = dq * q
+  const double ax = dq[0], ay = dq[1], az = dq[2], aw = dq[3];
+  const double bx = x[0], by = x[1], bz = x[2], bw = x[3];
+  out[0] = aw * bx + ax * bw + ay * bz - az * by;
+  out[1] = aw * by + ay * bw + az * bx - ax * bz;
+  out[2] = aw * bz + az * bw + ax * by - ay * bx;
+  out[3] = aw * bw - ax * bx - ay * by - az * bz;
+  double tx, ty, tz;
+  rot<double>(dq, x[4], x[5], x[6], tx, ty, tz);
+  out[4] = tx + dtx;
+  out[5] = ty + dty;
+  out[6] = tz + dtz;
+}
+
+__host__ __device__ constexpr int hidx(int a, int b) {   // upper-triangle row-major index, a <= b
+  return a * 6 - a * (a - 1) / 2 + (b - a);
+}
+
+// LevenbergMarquardtStrategy::ComputeStep in normal-equation form on the Jacobi-scaled system:
+// (Hs + diag(Hs)/radius) y = gs, step = -y; then TrustRegionMinimizer::ComputeTrustRegionStep's model cost change.
+// (The oracle solves the equivalent [J; sqrt(D/radius)] least-squares problem by Householder QR like Ceres'
+// DENSE_QR; the two agree to ~cond * eps.)  Returns false for an invalid step; delta = scaled step.
+__device__ __forceinline__ bool solve_step(LMState& s, double (&delta)[6]) {
+  double sc[6], gs[6], Hu[21], dg[6];
+#pragma unroll
+  for (int a = 0; a < 6; ++a) {
+    sc[a] = s.scale[a];
+    dg[a] = s.diag[a];
+  }
+#pragma unroll
+  for (int k = 0; k < 21; ++k) Hu[k] = s.H[k];
+#pragma unroll
+  for (int a = 0; a < 6; ++a) gs[a] = sc[a] * s.g[a];
+  const int reuse = s.reuse;
+  const double inv_radius = 1.0 / s.radius;
+  // packed lower triangle (row-major, l(i,j) = i(i+1)/2 + j): Hs = S H S, then A = Hs + diag/radius factored in place
+  double Hs[21], A[21];
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int j = 0; j <= i; ++j) {
+      Hs[i * (i + 1) / 2 + j] = sc[i] * Hu[hidx(j, i)] * sc[j];
+      A[i * (i + 1) / 2 + j] = Hs[i * (i + 1) / 2 + j];
+    }
+  if (!reuse) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) dg[k] = fmin(fmax(Hs[k * (k + 1) / 2 + k], 1e-6), 1e32);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) s.diag[k] = dg[k];
+  }
+  s.reuse = 1;
+  // LDL^T of A = Hs + diag / radius (no square roots on the dependent chain; one reciprocal per pivot): W[i][j] =
+  // L[i][j] D[j] is kept beside L, packed lower like A
+#pragma unroll
+  for (int k = 0; k < 6; ++k) A[k * (k + 1) / 2 + k] += dg[k] * inv_radius;
+  double W[21], rD[6];
+  bool pd = true;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    double d = A[j * (j + 1) / 2 + j];
+#pragma unroll
+    for (int k = 0; k < j; ++k) d -= A[j * (j + 1) / 2 + k] * W[j * (j + 1) / 2 + k];
+    pd = pd && (d > 0.0);
+    rD[j] = 1.0 / d;
+#pragma unroll
+    for (int i = j + 1; i < 6; ++i) {
+      double v = A[i * (i + 1) / 2 + j];
+#pragma unroll
+      for (int k = 0; k < j; ++k) v -= A[i * (i + 1) / 2 + k] * W[j * (j + 1) / 2 + k];
+      W[i * (i + 1) / 2 + j] = v;            // L[i][j] D[j]
+      A[i * (i + 1) / 2 + j] = v * rD[j];    // L[i][j]
+    }
+  }
+  if (!pd) return false;
+  double y[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {   // L z = gs
+    double v = gs[i];
+#pragma unroll
+    for (int k = 0; k < i; ++k) v -= A[i * (i + 1) / 2 + k] * y[k];
+    y[i] = v;
+  }
+#pragma unroll
+  for (int i = 5; i >= 0; --i) {   // L^T y = D^-1 z
+    double v = y[i] * rD[i];
+#pragma unroll
+    for (int k = i + 1; k < 6; ++k) v -= A[k * (k + 1) / 2 + i] * y[k];
+    y[i] = v;
+  }
+  bool finite = true;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    y[k] = -y[k];   // the step
+    finite = finite && isfinite(y[k]);
+  }
+  if (!finite) return false;
+  // model cost change -(step^T gs + step^T Hs step / 2)
+  double sg = 0.0, sHs = 0.0;
+#pragma unroll
+  for (int a = 0; a < 6; ++a) {
+    sg += y[a] * gs[a];
+    double hv = 0.0;
+#pragma unroll
+    for (int b = 0; b < 6; ++b) hv += Hs[a >= b ? a * (a + 1) / 2 + b : b * (b + 1) / 2 + a] * y[b];
+    sHs += y[a] * hv;
+  }
+  const double mcc = -(sg + 0.5 * sHs);
+  if (!(mcc > 0.0)) return false;
+  s.mcc = mcc;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) delta[k] = y[k] * sc[k];
+  return true;
+}
+
+// value of lane src (a compile-time / wave-uniform lane) to every lane: two v_readlane (no LDS round trip)
+__device__ __forceinline__ double bcast(double v, int src) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, src);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), src);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// NextStep with the gradient-norm test folded in: ComputeTrustRegionStep (+ HandleInvalidStep retries) and, when
+// check_gmax, the projected-gradient max norm at x (lane 1) computed alongside the candidate (lane 0).  If the
+// gradient test ends the solve the step is discarded, as in the sequential order (test first, then step).
+__device__ __forceinline__ void next_step_wave(LMState& s, bool check_gmax, int lane) {
+  for (;;) {
+    double delta[6];
+    const bool valid = solve_step(s, delta);
+    double d[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) d[k] = lane == 1 ? -s.g[k] : (valid ? delta[k] : 0.0);
+    double out[7];
+    se3_plus(s.x, d, out);
+    if (check_gmax) {
+      double m = 0.0;
+#pragma unroll
+      for (int i = 0; i < 7; ++i) m = fmax(m, fabs(s.x[i] - bcast(out[i], 1)));
+      s.gmax = m;
+      check_gmax = false;
+      if (s.gmax <= 1e-10) { s.done = 1; return; }   // (phase 0: before any step; phase 1: success && gmax)
+    }
+    s.iteration++;
+    if (valid) {
+#pragma unroll
+      for (int i = 0; i < 7; ++i) s.cand[i] = bcast(out[i], 0);
+      s.invalid = 0;
+      return;   // candidate pending evaluation
+    }
+    // HandleInvalidStep -> StepIsInvalid -> StepRejected(0)
+    if (++s.invalid >= 5) { s.done = 1; return; }
+    s.radius /= s.dfac;
+    s.dfac *= 2.0;
+    s.reuse = 1;
+    if (s.iteration >= 4 || s.radius < 1e-32) { s.done = 1; return; }
+  }
+}
+
+__device__ __forceinline__ double norm7(const double (&a)[7]) {
+  double v = 0.0;
+#pragma unroll
+  for (int i = 0; i < 7; ++i) v += a[i] * a[i];
+  return sqrt(v);
+}
+
+// One Ceres control step after an evaluation (sums = cost, J^T J, J^T r, count at x in phase 0, else at cand).
+// Called by all 64 lanes of one wave with identical s and sums; every lane ends with the same s.
+__device__ __forceinline__ void lm_logic(LMState& s, const double (&sums)[LM_NSUM], int lane) {
+  if (s.phase == 0) {   // IterationZero
+    s.n_res = (int)sums[28];
+    s.x_cost = sums[0];
+    s.initial_cost = sums[0];
+    if (s.n_res == 0) { s.done = 1; return; }   // no residual blocks: parameters untouched
+    if (!isfinite(s.x_cost)) { s.done = 1; return; }
+#pragma unroll
+    for (int k = 0; k < 21; ++k) s.H[k] = sums[1 + k];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) s.g[k] = sums[22 + k];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) s.scale[k] = 1.0 / (1.0 + sqrt(s.H[hidx(k, k)]));
+    s.x_norm = norm7(s.x);
+    s.radius = 1e4;
+    s.dfac = 2.0;
+    s.reuse = 0;
+    s.invalid = 0;
+    s.iteration = 0;
+    s.phase = 1;
+    next_step_wave(s, true, lane);
+    return;
+  }
+  double cand_cost = sums[0];
+  if (!isfinite(cand_cost)) cand_cost = DBL_MAX;
+  // ParameterToleranceReached (candidate not applied)
+  double sn = 0.0;
+#pragma unroll
+  for (int i = 0; i < 7; ++i) sn += (s.x[i] - s.cand[i]) * (s.x[i] - s.cand[i]);
+  sn = sqrt(sn);
+  if (sn <= 1e-8 * (s.x_norm + 1e-8)) { s.done = 1; return; }
+  // FunctionToleranceReached
+  if (fabs(s.x_cost - cand_cost) <= 1e-6 * s.x_cost) { s.done = 1; return; }
+  const double rho = (s.x_cost - cand_cost) / s.mcc;
+  bool success = false;
+  if (rho > 1e-3) {
+#pragma unroll
+    for (int i = 0; i < 7; ++i) s.x[i] = s.cand[i];
+    s.x_norm = norm7(s.x);
+    s.x_cost = cand_cost;
+#pragma unroll
+    for (int k = 0; k < 21; ++k) s.H[k] = sums[1 + k];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) s.g[k] = sums[22 + k];
+    const double t = 2.0 * rho - 1.0;
+    s.radius = fmin(1e16, s.radius / fmax(1.0 / 3.0, 1.0 - t * t * t));
+    s.dfac = 2.0;
+    s.reuse = 0;
+    s.successful++;
+    success = true;
+  } else {
+    s.radius /= s.dfac;
+    s.dfac *= 2.0;
+    s.reuse = 1;
+  }
+  if (s.iteration >= 4 || s.radius < 1e-32) { s.done = 1; return; }
+  next_step_wave(s, success, lane);
+}
+
+// the LM state without the trace fields (the register-resident copy of the control wave writes these back; the
+// trace fields of the LDS copy are written directly at iteration zero)
+__device__ __forceinline__ void store_state_core(LMState& dst, const LMState& s) {
+#pragma unroll
+  for (int k = 0; k < 7; ++k) { dst.x[k] = s.x[k]; dst.cand[k] = s.cand[k]; }
+  dst.x_cost = s.x_cost;
+#pragma unroll
+  for (int k = 0; k < 21; ++k) dst.H[k] = s.H[k];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) { dst.g[k] = s.g[k]; dst.scale[k] = s.scale[k]; dst.diag[k] = s.diag[k]; }
+  dst.radius = s.radius; dst.dfac = s.dfac; dst.mcc = s.mcc; dst.x_norm = s.x_norm; dst.gmax = s.gmax;
+  dst.initial_cost = s.initial_cost;
+  dst.phase = s.phase; dst.done = s.done; dst.iteration = s.iteration; dst.reuse = s.reuse; dst.invalid = s.invalid;
+  dst.successful = s.successful; dst.n_res = s.n_res;
+}
+
+// iteration zero's trace (x_in, J^T J, J^T r) into the LDS state, by one lane
+__device__ __forceinline__ void record_iteration_zero(LMState& dst, const LMState& s, const double (&sums)[LM_NSUM]) {
+#pragma unroll
+  for (int k = 0; k < 7; ++k) dst.x_in[k] = s.x[k];
+#pragma unroll
+  for (int k = 0; k < 21; ++k) dst.H0[k] = sums[1 + k];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) dst.g0[k] = sums[22 + k];
+}
+
+// one control step by wave 0 on its register state s, with the sums from LDS; lane 0 records iteration zero
+__device__ __forceinline__ void control_step(LMState& s, LMState& sst, const double* sums_lds, int lane) {
+  double sm[LM_NSUM];
+#pragma unroll
+  for (int k = 0; k < LM_NSUM; ++k) sm[k] = sums_lds[k];
+  if (s.phase == 0 && lane == 0) record_iteration_zero(sst, s, sm);
+  lm_logic(s, sm, lane);
+}
+
+__device__ __forceinline__ double point_component(const LMState& s, int k) {   // k wave-uniform or per lane
+  double v = 0.0;
+#pragma unroll
+  for (int j = 0; j < 7; ++j)
+    if (j == k) v = s.phase == 0 ? s.x[j] : s.cand[j];
+  return v;
+}
+
+__device__ __forceinline__ void stage_state(const LMState* __restrict__ st, LMState& sst) {
+  const unsigned* src = reinterpret_cast<const unsigned*>(st);
+  unsigned* dst = reinterpret_cast<unsigned*>(&sst);
+  for (int w = threadIdx.x; w < kStateWords; w += blockDim.x) dst[w] = src[w];
+}
+__device__ __forceinline__ void publish_state(const LMState& sst, LMState* __restrict__ st) {
+  const unsigned* src = reinterpret_cast<const unsigned*>(&sst);
+  unsigned* dst = reinterpret_cast<unsigned*>(st);
+  for (int w = threadIdx.x; w < kStateWords; w += blockDim.x) dst[w] = src[w];
+}
+
+__device__ __forceinline__ unsigned long long granule(unsigned tag, unsigned data) {
+  return ((unsigned long long)tag << 32) | data;
+}
+__device__ __forceinline__ void put_granule(unsigned long long* p, unsigned long long g) {
+  __hip_atomic_store(p, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// poll one granule until it carries `tag` (bounded); false on timeout
+__device__ __forceinline__ bool get_granule(const unsigned long long* p, unsigned tag, unsigned& data) {
+  for (long long k = 0; k < kSpin; ++k) {
+    const unsigned long long g = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((unsigned)(g >> 32) == tag) {
+      data = (unsigned)g;
+      return true;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return false;
+}
+
+// granules j0, j0 + kTB, ..., j0 + (kSweep - 1) kTB (those < n) until all carry `tag` (bounded), data into out[j]
+constexpr int kSweep = 8;
+__device__ __forceinline__ bool sweep_granules(const unsigned long long* __restrict__ g, int j0, int n, unsigned tag,
+                                               unsigned* __restrict__ out) {
+  unsigned pending = 0;
+#pragma unroll
+  for (int u = 0; u < kSweep; ++u)
+    if (j0 + u * kTB < n) pending |= 1u << u;
+  for (long long k = 0; k < kSpin && pending; ++k) {
+    unsigned long long v[kSweep];
+#pragma unroll
+    for (int u = 0; u < kSweep; ++u)   // all loads of the round issued before any is examined
+      v[u] = (pending >> u) & 1u ? __hip_atomic_load(&g[j0 + u * kTB], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                 : 0ull;
+#pragma unroll
+    for (int u = 0; u < kSweep; ++u)
+      if (((pending >> u) & 1u) && (unsigned)(v[u] >> 32) == tag) {
+        out[j0 + u * kTB] = (unsigned)v[u];
+        pending &= ~(1u << u);
+      }
+    if (pending) __builtin_amdgcn_s_sleep(1);
+  }
+  return pending == 0;
+}
+
+struct LMArgs {
+  LMState* st;
+  const double* erec;
+  const uint8_t* evalid;
+  int ecap;
+  const int* d_ne;
+  int ne_ub;
+  const double* srec;
+  const uint8_t* svalid;
+  int scap;
+  const int* d_ns;
+  int ns_ub;
+  const double* gmat;              // GRAM: G + origin (kGramWords)
+  unsigned long long* rel;         // 15 release granules
+  unsigned long long* part;        // [nblk][2 * LM_NSUM] partial granules
+  double* partials;                // sharded: [LM_NSUM][nblk]
+  double* sums;                    // sharded: 29 sums (all-reduced in place between launches)
+  unsigned* ticket;                // sharded: arrival ticket
+  unsigned long long* dbg;         // FLOAM_DEBUG_STAMPS: control-block segment times (diagnostic, normally null)
+};
+
+// ===================================================================================== the resident solve
+template <bool GRAM, bool HUBER, typename R>
+__global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
+  __shared__ double s_red[LM_NSUM * kTB];   // evaluation: thread sums; control: the partial table (as u32 halves)
+  __shared__ double s_strip[LM_NSUM * 8];
+  __shared__ double s_sums[LM_NSUM];
+  __shared__ double s_pt[7];
+  __shared__ unsigned s_rel[15];
+  __shared__ int s_flag;
+  const int nblk = (int)gridDim.x - 1;
+  const int tid = threadIdx.x;
+  if (blockIdx.x > 0) {   // ------------------------------------------------------------------ evaluation block
+    const int blk = (int)blockIdx.x - 1;
+    const unsigned ep = a.st->epoch;
+    const int ne = min(*a.d_ne, a.ne_ub);
+    const int total = ne + (GRAM ? 0 : min(*a.d_ns, a.ns_ub));
+    const int stride = nblk * kTB, i0 = blk * kTB + tid;
+    // the thread's first record stays in registers across the evaluations
+    R f0[9];
+    bool has0 = false, edge0 = true;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) f0[k] = R(0);
+    if (i0 < ne) {
+      has0 = a.evalid[i0] & 1;
+      if (has0) load_rec<R, EDGE_FIELDS>(a.erec, a.ecap, i0, f0);
+    } else if (i0 < total) {
+      edge0 = false;
+      has0 = a.svalid[i0 - ne] & 1;
+      if (has0) load_rec<R, SURF_FIELDS>(a.srec, a.scap, i0 - ne, f0);
+    }
+    for (int it = 0; it < 5; ++it) {
+      if (it == 0) {   // iteration zero evaluates at x (set by the kNN launch; kernel boundary)
+        if (tid == 0) s_flag = a.st->done;
+        if (tid < 7) s_pt[tid] = a.st->x[tid];
+      } else {         // the point the control step of evaluation it - 1 released (or the stop granule)
+        if (tid < 15) {
+          unsigned v = 0;
+          const bool ok = get_granule(&a.rel[tid], ep + (unsigned)it, v);
+          s_rel[tid] = v;
+          if (tid == 14) s_flag = ok ? (int)v : 1;   // a timeout stops this block too
+        }
+        __syncthreads();
+        if (tid < 7)
+          s_pt[tid] = __longlong_as_double((long long)(((unsigned long long)s_rel[2 * tid + 1] << 32) | s_rel[2 * tid]));
+      }
+      __syncthreads();
+      if (s_flag) return;
+      R x[7];
+#pragma unroll
+      for (int k = 0; k < 7; ++k) x[k] = (R)s_pt[k];
+      double acc[LM_NSUM];
+      eval_records<HUBER, R>(x, has0, edge0, f0, i0 + stride, stride, ne, total, a.erec, a.evalid, a.ecap, a.srec,
+                             a.svalid, a.scap, acc);
+      block_sums(acc, s_red, s_strip, s_sums);
+      if (tid < 2 * LM_NSUM) {   // 58 granules: the block's sums in 32-bit halves, tagged with this evaluation
+        const unsigned long long b = (unsigned long long)__double_as_longlong(s_sums[tid >> 1]);
+        put_granule(&a.part[blk * 2 * LM_NSUM + tid],
+                    granule(ep + (unsigned)it, (tid & 1) ? (unsigned)(b >> 32) : (unsigned)b));
+      }
+    }
+    return;
+  }
+  // ------------------------------------------------------------------------------------------------- control block
+  __shared__ LMState sst;
+  __shared__ double G[kGramW][kGramW];
+  __shared__ double o[3];
+  __shared__ double s_ssum[LM_NSUM];
+  __shared__ int s_done;
+  stage_state(a.st, sst);
+  double gv = 0.0;
+  if (GRAM && tid < kGramWords) gv = a.gmat[tid];
+  __syncthreads();
+  if (sst.done) return;   // (never after lm_reset; the evaluation blocks saw it too)
+  const unsigned ep = sst.epoch;
+  if (GRAM) gram_unpack(gv, G, o);
+  const int lane = tid & 63;
+  LMState s;   // wave 0: the whole LM state in registers for the whole solve
+  if (tid < 64) s = sst;
+  unsigned* tab = reinterpret_cast<unsigned*>(s_red);   // [nblk][2 * LM_NSUM] halves of the block partials
+  unsigned long long tm[4] = {0, 0, 0, 0};
+  int failed_at = -1;   // evaluation whose partials never arrived (never expected)
+  for (int it = 0; it < 5; ++it) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    if (tid < 7) s_pt[tid] = point_component(s, tid);   // (wave 0 holds s; lanes 0..6 write)
+    __syncthreads();
+    if (GRAM) surf_sums_from_gram(s_pt, o, G, (double)sst.corr_surf, s_ssum);   // overlaps the evaluation blocks
+    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+    // the evaluation blocks' partial granules of evaluation it: every thread keeps kSweep loads in flight per poll
+    // round (one round trip per round, not one per granule)
+    int bad = 0;
+    for (int j0 = tid; j0 < nblk * 2 * LM_NSUM; j0 += kSweep * kTB)
+      if (!sweep_granules(a.part, j0, nblk * 2 * LM_NSUM, ep + (unsigned)it, tab)) bad = 1;
+    if (__syncthreads_or(bad)) {
+      failed_at = it;
+      break;
+    }
+    const unsigned long long t2 = __builtin_amdgcn_s_memrealtime();
+    reduce_blocks([&](int c, int b) {
+      const int g = b * 2 * LM_NSUM + 2 * c;
+      return __longlong_as_double((long long)(((unsigned long long)tab[g + 1] << 32) | tab[g]));
+    }, nblk, s_strip, s_sums);
+    if (GRAM && tid < LM_NSUM) s_sums[tid] = s_sums[tid] + s_ssum[tid];   // edge + surf
+    __syncthreads();
+    const unsigned long long t3 = __builtin_amdgcn_s_memrealtime();
+    if (tid < 64) {
+      control_step(s, sst, s_sums, lane);
+      if (it + 1 < 5 && lane < 15) {   // release evaluation it + 1: the next point, or stop
+        unsigned v;
+        if (lane == 14) {
+          v = s.done ? 1u : 0u;
+        } else {
+          const unsigned long long b = (unsigned long long)__double_as_longlong(point_component(s, lane >> 1));
+          v = (lane & 1) ? (unsigned)(b >> 32) : (unsigned)b;
+        }
+        put_granule(&a.rel[lane], granule(ep + (unsigned)it + 1u, v));
+      }
+      if (lane == 0) s_done = s.done;
+    }
+    __syncthreads();
+    if (a.dbg) {
+      const unsigned long long t4 = __builtin_amdgcn_s_memrealtime();
+      tm[0] += t1 - t0; tm[1] += t2 - t1; tm[2] += t3 - t2; tm[3] += t4 - t3;
+    }
+    if (s_done) break;
+  }
+  if (failed_at >= 0 && tid < 64) {   // end the solve, report through n_res, stop the blocks still waiting
+    s.done = 1;
+    s.n_res = -1;
+    if (failed_at + 1 < 5 && lane < 15)
+      put_granule(&a.rel[lane], granule(ep + (unsigned)failed_at + 1u, lane == 14 ? 1u : 0u));
+  }
+  if (tid == 0) store_state_core(sst, s);
+  __syncthreads();
+  publish_state(sst, a.st);
+  if (a.dbg && tid == 0) {   // diagnostic stamps (100 MHz): surf sums, wait, reduce, control step + release
+    atomicAdd(&a.dbg[0], tm[0]);
+    atomicAdd(&a.dbg[1], tm[1]);
+    atomicAdd(&a.dbg[2], tm[2]);
+    atomicAdd(&a.dbg[3], tm[3]);
+    atomicAdd(&a.dbg[4], 1ull);
+  }
+}
+
+// ===================================================================================== the sharded evaluation
+// Launch k: every block stages the state, runs the control step of evaluation k - 1 on the all-reduced sums (all
+// blocks compute the same state), evaluates its records at the resulting point, and the last-arriving block reduces
+// the block partials (fixed order) + the surf half into a.sums for the all-reduce and writes the state.
+template <bool GRAM, bool HUBER, typename R>
+__global__ __launch_bounds__(kTB) void lm_shard_eval(LMArgs a, int k) {
+  __shared__ double s_red[LM_NSUM * kTB];
+  __shared__ double s_strip[LM_NSUM * 8];
+  __shared__ double s_sums[LM_NSUM];
+  __shared__ double s_ssum[LM_NSUM];
+  __shared__ double s_pt[7];
+  __shared__ LMState sst;
+  __shared__ int s_done, s_last;
+  const int nblk = (int)gridDim.x, blk = (int)blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  stage_state(a.st, sst);
+  __syncthreads();
+  LMState s;
+  if (tid < 64) {
+    s = sst;
+    if (k > 0 && !s.done) control_step(s, sst, a.sums, lane);   // a.sums: all-reduced (kernel boundary)
+    if (tid < 7) s_pt[tid] = point_component(s, tid);
+    if (lane == 0) s_done = s.done;
+  }
+  __syncthreads();
+  const bool done = s_done != 0;
+  const int ne = min(*a.d_ne, a.ne_ub);
+  const int total = ne + (GRAM ? 0 : min(*a.d_ns, a.ns_ub));
+  if (!done) {
+    R x[7];
+#pragma unroll
+    for (int q = 0; q < 7; ++q) x[q] = (R)s_pt[q];
+    const int stride = nblk * kTB, i0 = blk * kTB + tid;
+    R f0[9];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) f0[q] = R(0);
+    double acc[LM_NSUM];
+    eval_records<HUBER, R>(x, false, true, f0, i0, stride, ne, total, a.erec, a.evalid, a.ecap, a.srec, a.svalid,
+                           a.scap, acc);
+    block_sums(acc, s_red, s_strip, s_sums);
+    if (tid < LM_NSUM) a.partials[tid * nblk + blk] = s_sums[tid];
+  }
+  // arrival: producer stores -> vmcnt(0) -> barrier -> agent release -> ticket; the last block acquires
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    s_last = atomicAdd(a.ticket, 1u) == (unsigned)(nblk - 1);
+    if (s_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+  if (!s_last) return;
+  if (!done) {
+    reduce_blocks([&](int c, int b) { return a.partials[c * nblk + b]; }, nblk, s_strip, s_sums);
+    if (GRAM) {
+      __shared__ double G[kGramW][kGramW];
+      __shared__ double o[3];
+      gram_unpack(tid < kGramWords ? a.gmat[tid] : 0.0, G, o);
+      surf_sums_from_gram(s_pt, o, G, (double)sst.corr_surf, s_ssum);
+      if (tid < LM_NSUM) s_sums[tid] = s_sums[tid] + s_ssum[tid];
+      __syncthreads();
+    }
+    if (tid < LM_NSUM) a.sums[tid] = s_sums[tid];
+  } else if (tid < LM_NSUM) {
+    a.sums[tid] = 0.0;   // nothing evaluated: the all-reduce still runs on every rank (the same decision everywhere)
+  }
+  if (tid == 0) {
+    store_state_core(sst, s);
+    *a.ticket = 0u;   // every block has arrived (next launch: kernel boundary)
+  }
+  __syncthreads();
+  publish_state(sst, a.st);
+}
+
+// the control step after the last evaluation of a sharded solve
+__global__ __launch_bounds__(64) void lm_shard_final(LMState* __restrict__ st, const double* __restrict__ sums) {
+  __shared__ LMState sst;
+  stage_state(st, sst);
+  __syncthreads();
+  LMState s = sst;
+  if (!s.done) control_step(s, sst, sums, threadIdx.x);
+  __syncthreads();
+  if (threadIdx.x == 0) store_state_core(sst, s);
+  __syncthreads();
+  publish_state(sst, st);
+}
+
+__global__ void lm_trace(const LMState* __restrict__ st, const int* __restrict__ dcnt, const int* __restrict__ d_me,
+                         const int* __restrict__ d_ms, double* __restrict__ trace, unsigned* __restrict__ count,
+                         int cap) {
+  if (threadIdx.x != 0) return;
+  if (!(*d_me > 10 && *d_ms > 50)) return;   // the map-size gate (:77): no solve ran
+  const unsigned i = *count;
+  if ((int)i >= cap) return;
+  *count = i + 1;
+  double* o = trace + (size_t)i * kTraceWords;
+  int k = 0;
+  o[k++] = dcnt[0]; o[k++] = dcnt[1]; o[k++] = st->corr_edge; o[k++] = st->corr_surf;
+  o[k++] = st->iteration; o[k++] = st->successful; o[k++] = st->initial_cost; o[k++] = st->x_cost;
+  for (int j = 0; j < 7; ++j) o[k++] = st->x_in[j];
+  for (int j = 0; j < 7; ++j) o[k++] = st->x[j];
+  for (int j = 0; j < 21; ++j) o[k++] = st->H0[j];
+  for (int j = 0; j < 6; ++j) o[k++] = st->g0[j];
+}
+
+LMArgs make_args(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const CorrSet& cs, const int* d_ns,
+                 int ns_ub, LMBuffers& b, unsigned long long* dbg) {
+  return LMArgs{d_st, ce.rec.p, ce.valid.p, ce.cap, d_ne, std::max(ne_ub, 0), cs.rec.p, cs.valid.p, cs.cap, d_ns,
+                std::max(ns_ub, 0), b.gmat.p, b.rel.p, b.part.p, b.partials.p, b.sums.p, b.ticket.p, dbg};
+}
+}  // namespace
+
+void LMBuffers::reserve(hipStream_t st) {
+  if (rel.p) return;
+  rel.reserve(16);
+  part.reserve((size_t)kRecEvalBlocks * 2 * LM_NSUM);
+  partials.reserve((size_t)kRecEvalBlocks * LM_NSUM);
+  sums.reserve(LM_NSUM);
+  ticket.reserve(1);
+  gpart.reserve((size_t)(kSurfGeomBlocks + kGramGroups) * kGram);
+  gmat.reserve(kGramWords);
+  gcnt.reserve(kGramGroups + 1);
+  // tag 0 never matches (epochs start at 8), counters start at zero
+  FLOAM_HIP(hipMemsetAsync(rel.p, 0, sizeof(unsigned long long) * rel.cap, st));
+  FLOAM_HIP(hipMemsetAsync(part.p, 0, sizeof(unsigned long long) * part.cap, st));
+  FLOAM_HIP(hipMemsetAsync(ticket.p, 0, sizeof(unsigned), st));
+  FLOAM_HIP(hipMemsetAsync(gcnt.p, 0, sizeof(unsigned) * gcnt.cap, st));
+  FLOAM_HIP(hipMemsetAsync(gmat.p, 0, sizeof(double) * gmat.cap, st));
+}
+
+void lm_solve_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const CorrSet& cs,
+                     const int* d_ns, int ns_ub, int mode, LMBuffers& b, hipStream_t st, unsigned long long* dbg) {
+  b.reserve(st);
+  const LMArgs a = make_args(d_st, ce, d_ne, ne_ub, cs, d_ns, ns_ub, b, dbg);
+  // all 1 + nblk blocks are co-resident (33 or 129 blocks of 256 threads on 256 CUs)
+  if (mode & LM_GRAM) {
+    hipLaunchKernelGGL((lm_solve<true, false, double>), dim3(kEdgeEvalBlocks + 1), dim3(kTB), 0, st, a);
+  } else {
+    const dim3 g(kRecEvalBlocks + 1);
+    switch (mode & (LM_HUBER | LM_FP32)) {
+      case LM_HUBER: hipLaunchKernelGGL((lm_solve<false, true, double>), g, dim3(kTB), 0, st, a); break;
+      case LM_FP32: hipLaunchKernelGGL((lm_solve<false, false, float>), g, dim3(kTB), 0, st, a); break;
+      case LM_HUBER | LM_FP32: hipLaunchKernelGGL((lm_solve<false, true, float>), g, dim3(kTB), 0, st, a); break;
+      default: hipLaunchKernelGGL((lm_solve<false, false, double>), g, dim3(kTB), 0, st, a); break;
+    }
+  }
+  FLOAM_LAUNCH_CHECK();
+}
+
+void lm_shard_eval_launch(int k, LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const CorrSet& cs,
+                          const int* d_ns, int ns_ub, int mode, LMBuffers& b, hipStream_t st) {
+  b.reserve(st);
+  const LMArgs a = make_args(d_st, ce, d_ne, ne_ub, cs, d_ns, ns_ub, b, nullptr);
+  if (mode & LM_GRAM) {
+    hipLaunchKernelGGL((lm_shard_eval<true, false, double>), dim3(kEdgeEvalBlocks), dim3(kTB), 0, st, a, k);
+  } else {
+    const dim3 g(kRecEvalBlocks);
+    switch (mode & (LM_HUBER | LM_FP32)) {
+      case LM_HUBER: hipLaunchKernelGGL((lm_shard_eval<false, true, double>), g, dim3(kTB), 0, st, a, k); break;
+      case LM_FP32: hipLaunchKernelGGL((lm_shard_eval<false, false, float>), g, dim3(kTB), 0, st, a, k); break;
+      case LM_HUBER | LM_FP32: hipLaunchKernelGGL((lm_shard_eval<false, true, float>), g, dim3(kTB), 0, st, a, k); break;
+      default: hipLaunchKernelGGL((lm_shard_eval<false, false, double>), g, dim3(kTB), 0, st, a, k); break;
+    }
+  }
+  FLOAM_LAUNCH_CHECK();
+}
+
+void lm_shard_final_launch(LMState* d_st, LMBuffers& b, hipStream_t st) {
+  hipLaunchKernelGGL(lm_shard_final, dim3(1), dim3(64), 0, st, d_st, b.sums.p);
+  FLOAM_LAUNCH_CHECK();
+}
+
+void lm_trace_launch(const LMState* d_st, const int* dcnt, const int* d_me, const int* d_ms, double* trace,
+                     unsigned* count, int cap, hipStream_t st) {
+  hipLaunchKernelGGL(lm_trace, dim3(1), dim3(64), 0, st, d_st, dcnt, d_me, d_ms, trace, count, cap);
+  FLOAM_LAUNCH_CHECK();
+}
+
+}  // namespace floam

@@ -32,7 +32,7 @@ struct Grid {
   // occupied slots of the coarse table, per build parity: the next build clears exactly these entries
   DevBuf<int> clist[2];
   DevBuf<int> counters;      // [0] bump cursor, [1..2] coarse list sizes (by parity)
-  int bits = 0;              // table size = 1 << bits
+  int bits = 0;              // table size = 1 << bits (at least twice the map size: load <= 1/2)
   unsigned mask = 0;
   int parity = 0;
   bool fresh = true;         // tables (re)allocated: the next clear is a full one
@@ -53,15 +53,26 @@ struct CorrSet {
   DevBuf<double> rec;
   DevBuf<uint8_t> valid;   // bit 0: after the kNN pass, 5 neighbours within sqd < 1; after geometry, record accepted
                            // bit 1: the query needed the full +-1 m search (profiling byte counter)
+                           // bit 2: the search found 5 neighbours (set by the geometry pass)
   DevBuf<float> nnxyz;     // coordinates of the 5 nearest map points, nnxyz[(3 * k + axis) * cap + i]
+  // stage inspection (floam_odom_set_trace): the 5 neighbours' map indices and float squared distances, k-major
+  // (nnidx[k * cap + i]); written by the search only while tracing
+  DevBuf<int> nnidx;
+  DevBuf<float> nnsqd;
+  bool trace = false;
   int cap = 0;
   void reserve(int n, int fields) {
-    if (n <= cap) return;
-    const int c = n < 1024 ? 1024 : n + n / 4;
-    valid.reserve(c);
-    cap = (int)valid.cap;
-    rec.reserve((size_t)cap * fields);
-    nnxyz.reserve((size_t)cap * 15);
+    if (n > cap) {
+      const int c = n < 1024 ? 1024 : n + n / 4;
+      valid.reserve(c);
+      cap = (int)valid.cap;
+      rec.reserve((size_t)cap * fields);
+      nnxyz.reserve((size_t)cap * 15);
+    }
+    if (trace) {
+      nnidx.reserve((size_t)cap * 5);
+      nnsqd.reserve((size_t)cap * 5);
+    }
   }
 };
 
@@ -75,6 +86,11 @@ struct LMState {
   double scale[6];    // Jacobi scaling, fixed at iteration 0
   double diag[6];     // LM diagonal (reused after a rejected / invalid step)
   double radius, dfac, mcc, x_norm, gmax, initial_cost;
+  // the solve's iteration-zero quantities (stage inspection; oracle/odom.cpp SolveTrace): the starting point and the
+  // unscaled J^T J and J^T r there
+  double x_in[7];
+  double H0[21];
+  double g0[6];
   int phase;          // 0: evaluate x (iteration zero); 1: evaluate cand
   int done;
   int iteration;
@@ -83,15 +99,39 @@ struct LMState {
   int successful;
   int n_res;
   int corr_edge, corr_surf;   // accepted correspondences (this solve)
-  int pad;
-  // hand-off words of the resident solve (lm_solve_gram), after the state proper: the control block copies only
-  // the state (kStateWords) in and out
-  unsigned long long go;      // (done << 7) | evaluations released; zeroed with the rest of the solve state
-  double point[8];            // the evaluation point released to the evaluation blocks
+  unsigned epoch;     // hand-off tag base of the resident solve (lm.hip): advanced by 8 per solve (lm_reset)
 };
-constexpr int kStateWords = (int)(offsetof(LMState, go) / sizeof(unsigned));
+constexpr int kStateWords = (int)(sizeof(LMState) / sizeof(unsigned));
+static_assert(sizeof(LMState) % 8 == 0, "LMState is copied as whole dwords");
 
 enum { LM_NSUM = 29 };   // cost, H[21], g[6], count
+
+// Surf records as 13-vectors w = [n (x) p (9), n (3), d + n.o] (geom_kernel): the surf half of every squared-loss LM
+// evaluation is a set of quadratic forms of their Gram matrix G = sum w w^T (lm.hip)
+constexpr int kGramW = 13;
+constexpr int kGram = kGramW * (kGramW + 1) / 2;   // 91 unique entries (upper triangle, row-major)
+constexpr int kGramWords = kGram + 3;              // G + the origin o the records were recentred on
+constexpr int kSurfGeomBlocks = 256;               // fixed surf geometry grid: fixed Gram reduction order
+constexpr int kGramGroups = 8;                     // its partials are reduced in 8 groups of 32, then the groups
+constexpr int kEdgeEvalBlocks = 32;                // edge-only evaluation grid of the Gram solves (fixed order)
+constexpr int kRecEvalBlocks = 128;                // per-record evaluation grid (Huber / fp32; fixed order)
+
+// LM modes: surf half from the Gram matrix (squared loss, fp64), Huber loss, fp32 geometry + residuals / Jacobians
+enum { LM_GRAM = 1, LM_HUBER = 2, LM_FP32 = 4 };
+inline int lm_mode(bool huber, bool fp32) { return (huber || fp32) ? (huber ? LM_HUBER : 0) | (fp32 ? LM_FP32 : 0) : LM_GRAM; }
+
+// device scratch of the solves (lm.hip)
+struct LMBuffers {
+  DevBuf<unsigned long long> rel;    // resident solve: control -> evaluation release granules
+  DevBuf<unsigned long long> part;   // resident solve: evaluation -> control partial-sum granules
+  DevBuf<double> partials;           // sharded evaluation: block partials
+  DevBuf<double> sums;               // sharded evaluation: the 29 sums (all-reduced over the ranks in place)
+  DevBuf<unsigned> ticket;           // sharded evaluation: arrival ticket (zero between launches)
+  DevBuf<double> gpart;              // surf Gram matrix: per-block and per-group partials (geom_kernel)
+  DevBuf<double> gmat;               // the solve's surf Gram matrix + its origin
+  DevBuf<unsigned> gcnt;             // ticket words of the Gram reduction
+  void reserve(hipStream_t st);
+};
 
 struct QuerySet {
   const PointRec* pts;
@@ -104,9 +144,7 @@ struct X7 {
   double v[7];
   int set;
 };
-// reset the per-solve LM state; x0 (7 doubles, by value) replaces x when non-null, else x is kept
-void lm_init_launch(LMState* d_st, const double* x0, hipStream_t st);
-void lm_init_dev_launch(LMState* d_st, const double* x0_dev, hipStream_t st);   // x = x0_dev (device pointer)
+void lm_init_dev_launch(LMState* d_st, const double* x0_dev, hipStream_t st);   // reset; x = x0_dev (device pointer)
 
 // Device-resident controller state (OdomEstimationClass members odom, last_odom, the keyframe list): the pose
 // algebra between the solves runs on the device, so a whole selector is issued without a host round trip; the host
@@ -154,10 +192,14 @@ struct GatherArgs {   // a status gather carried out by another launch (deskew_b
   UpdateStatus* out = nullptr;   // null: nothing to gather
 };
 
+// KeyFrameUpdate(pose) (src/odomEstimationClass.cpp:320-343) on the device state with an explicit pose {q, t}: the
+// public method the reference's header exposes (include/odomEstimationClass.h:80); result into *flag
+void keyframe_update_launch(OdomDev* s, const double* x_dev, int first, int* flag, hipStream_t st);
+
 // Between the two updatePointsToMap calls of a deskewed UpdatePointsToMapSelector (odomEstimationClass.cpp:40-46),
 // without a host round trip: GetVelocity from the first call's result (x1 = st->x) and s->last_odom (the pose before
-// it), CompensateVelocity of both clouds in place (dataHandler.cpp:82-92, Q5); s->mid = odom1 and the second call's
-// prediction odom1 * (last_odom^-1 * odom1) into s->x0[1] (same algebra as the host, pose.hpp).
+// it), CompensateVelocity of both clouds in place (dataHandler.cpp:82-92, Q5; twice per point when edge and surf are
+// one cloud); s->mid = odom1 and the second call's prediction odom1 * (last_odom^-1 * odom1) into s->x0[1].
 // gather: the first call's status gather (mode 0: it only reads the LM state, the counts and the poses, none of
 // which this launch writes) done by block 0 instead of a launch of its own
 void deskew_bridge_launch(const LMState* st, OdomDev* s, double scan_period, PointRec* edge, const int* d_ne,
@@ -165,47 +207,35 @@ void deskew_bridge_launch(const LMState* st, OdomDev* s, double scan_period, Poi
                           const GatherArgs& gather = GatherArgs{});
 // Correspondence search for the edge and the surf query sets at the pose in st->x, in two launches:
 // knn_launch — exact 5-NN (blocks [0, nbE) edge queries against the corner map, the rest surf against the surf map);
-// geom_launch — fp64 line / plane fits and the residual records.
-// knn_launch also starts the solve (the former lm_init): LM state reset, x = x0 when x0 != null (7 doubles, by value)
-void knn_launch(LMState* d_st, const double* x0, const double* x0_dev, const QuerySet& qe, const Grid& ge, const PointRec* mapE,
-                CorrSet& ce, const QuerySet& qs, const Grid& gs, const PointRec* mapS, CorrSet& cs, const int* d_me,
-                const int* d_ms, int rank, int world, hipStream_t st, unsigned long long* dbg = nullptr);
-// gpart (nullable): per-block partial Gram matrices of the surf records for lm_step_gram ([256][91] doubles)
-// and, with gpart, the solve's surf Gram matrix into gmat (lm_gram_words() doubles) through gpart's block and group
-// partials (lm_gram_partials() doubles) and the ticket words gcnt (lm_gram_counters(), zero before the first use)
-void geom_launch(LMState* d_st, const QuerySet& qe, const Grid& ge, const PointRec* mapE, CorrSet& ce,
-                 const QuerySet& qs, const Grid& gs, const PointRec* mapS, CorrSet& cs, double* gpart, double* gmat,
-                 unsigned* gcnt, hipStream_t st);
+// geom_launch — line / plane fits and the residual records (fp64, or fp32 with fp32).
+// knn_launch also starts the solve (lm_reset): LM state reset, x = x0_dev when non-null, hand-off epoch advanced
+void knn_launch(LMState* d_st, const double* x0_dev, const QuerySet& qe, const Grid& ge, CorrSet& ce,
+                const QuerySet& qs, const Grid& gs, CorrSet& cs, const int* d_me, const int* d_ms, int rank, int world,
+                hipStream_t st);
+// gram: the squared-loss solves' surf Gram matrix of the accepted surf records into b.gmat (b.gpart's partials)
+void geom_launch(LMState* d_st, const QuerySet& qe, CorrSet& ce, const QuerySet& qs, CorrSet& cs, bool gram,
+                 bool fp32, LMBuffers& b, hipStream_t st);
 // algorithmic bytes of the correspondence pass just issued (profiling only), accumulated into *d_bytes
-void knn_traffic_launch(const LMState* d_st, const QuerySet& q, const Grid& g, const PointRec* map, CorrSet& c,
-                        int rank, int world, DevBuf<unsigned long long>& set,
-                        unsigned long long* d_bytes, hipStream_t st);
-// one LM evaluation (at x in phase 0, else at cand): block partial sums of (cost, J^T J, J^T r, count)
-int lm_eval_launch(const LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const CorrSet& cs,
-                   const int* d_ns, int ns_ub, bool huber, double* partials, hipStream_t st);
-// fused evaluation + control (single GPU): the last block reduces and runs the LM step; counter starts at 0
-void lm_step_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const CorrSet& cs,
-                    const int* d_ns, int ns_ub, bool huber, double* partials, unsigned* counter, hipStream_t st,
-                    unsigned long long* dbg = nullptr);
-// a whole Ceres solve for the squared loss (up to 5 evaluations + control steps) in one launch with resident blocks
-// (surf half from the Gram matrix of geom_launch's gpart, edge records per record); cnt (u32) is a device word,
-// zero before the first launch (the kernel leaves it at zero)
-void lm_solve_gram_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const double* gpart,
-                          double* gmat, double* partials, unsigned* cnt, hipStream_t st,
-                          unsigned long long* dbg = nullptr);
-// LM iteration for the squared loss: surf sums from the Gram matrix of the surf records (geom_launch with gpart),
-// edge records per record on a small grid.  first: this is the solve's first evaluation (reduce gpart into gmat,
-// lm_gram_words() doubles); later launches of the solve reuse gmat.
-bool lm_gram_supported(bool huber);
-void ctrl_stamps_print();   // diagnostic build (-DFLOAM_CTRL_STAMPS): control-step breakdown
-size_t lm_gram_partials();   // doubles in gpart
-int lm_gram_counters();       // ticket words of the geometry kernel's Gram reduction
-size_t lm_gram_words();      // doubles in gmat
-void lm_step_gram_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const double* gpart,
-                         double* gmat, bool first, double* partials, unsigned* counter, hipStream_t st,
-                         unsigned long long* dbg = nullptr);
-// reduce partials (nblk > 0) or read 29 pre-reduced sums (nblk == 0), then run the Ceres LM control step
-void lm_control_launch(LMState* d_st, const double* partials, int nblk, hipStream_t st);
-void lm_reduce_launch(const double* partials, int nblk, double* sums, hipStream_t st);
+void knn_traffic_launch(const LMState* d_st, const QuerySet& q, const Grid& g, CorrSet& c, int rank, int world,
+                        DevBuf<unsigned long long>& set, unsigned long long* d_bytes, hipStream_t st);
+
+// ----------------------------------------------------------------------------------------- LM solve (lm.hip)
+// A whole ceres::Solve (iteration zero + up to max_num_iterations = 4 candidates, src/odomEstimationClass.cpp:95-108)
+// in ONE launch on a single GPU: a control block keeps the LM state in registers and runs the Ceres 1.13 control
+// step; resident evaluation blocks keep their records in registers and evaluate each released point.  mode = LM_*.
+void lm_solve_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const CorrSet& cs,
+                     const int* d_ns, int ns_ub, int mode, LMBuffers& b, hipStream_t st,
+                     unsigned long long* dbg = nullptr);
+// The same solve sharded over ranks (one process per GPU): evaluation k = 0..4 in one launch each (the control step
+// of evaluation k - 1 folded in, run redundantly by every block on the all-reduced sums), leaving this rank's 29
+// sums in b.sums for the caller's all-reduce; lm_shard_final_launch runs the last control step.
+void lm_shard_eval_launch(int k, LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const CorrSet& cs,
+                          const int* d_ns, int ns_ub, int mode, LMBuffers& b, hipStream_t st);
+void lm_shard_final_launch(LMState* d_st, LMBuffers& b, hipStream_t st);
+// Stage inspection: append this solve's trace record (49 doubles, oracle/odom.cpp SolveTrace order) to trace[] at
+// *count when the map-size gate (:77) let the solve run and *count < cap.
+constexpr int kTraceWords = 49;
+void lm_trace_launch(const LMState* d_st, const int* dcnt, const int* d_me, const int* d_ms, double* trace,
+                     unsigned* count, int cap, hipStream_t st);
 
 }  // namespace floam

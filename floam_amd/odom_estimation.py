@@ -148,6 +148,67 @@ class OdomEstimationClass:
         _ffi.check(self._L.floam_odom_get_stats(self._need(), C.byref(s)))
         return {k: getattr(s, k) for k, _ in _ffi.OdomStats._fields_}
 
+    def KeyFrameUpdate(self, q_xyzw, t) -> bool:
+        """include/odomEstimationClass.h:80 (src/odomEstimationClass.cpp:320-343): pose (q, t) -> is it a keyframe."""
+        q = np.ascontiguousarray(q_xyzw, dtype=np.float64)
+        tt = np.ascontiguousarray(t, dtype=np.float64)
+        flag = C.c_int()
+        _ffi.check(self._L.floam_odom_keyframe_update(self._need(), q.ctypes.data_as(C.POINTER(C.c_double)),
+                                                      tt.ctypes.data_as(C.POINTER(C.c_double)), C.byref(flag)))
+        return bool(flag.value)
+
+    def set_precision(self, fp32: bool) -> None:
+        """fp32 geometry / residuals / Jacobians (the C5 precision sweep) or the reference's fp64 (default)."""
+        _ffi.check(self._L.floam_odom_set_precision(self._need(),
+                                                    _ffi.PRECISION_FP32 if fp32 else _ffi.PRECISION_FP64))
+
+    def set_trace(self, capacity: int) -> None:
+        """Stage inspection: record every solve (up to `capacity`) and keep the last correspondence pass."""
+        _ffi.check(self._L.floam_odom_set_trace(self._need(), int(capacity)))
+
+    def traces(self) -> list:
+        """The recorded solves since the last call (oracle.Odometry.traces() layout), then cleared."""
+        cap = 4096
+        buf = np.zeros((cap, _ffi.TRACE_WORDS))
+        n = C.c_size_t()
+        _ffi.check(self._L.floam_odom_get_traces(self._need(), buf.ctypes.data_as(C.POINTER(C.c_double)), cap,
+                                                 C.byref(n)))
+        out = []
+        for b in buf[: min(n.value, cap)]:
+            out.append(dict(n_edge_queries=int(b[0]), n_surf_queries=int(b[1]), n_edge_corr=int(b[2]),
+                            n_surf_corr=int(b[3]), iterations=int(b[4]), successful=int(b[5]),
+                            initial_cost=b[6], final_cost=b[7], x_in=b[8:15].copy(), x_out=b[15:22].copy(),
+                            H0=b[22:43].copy(), g0=b[43:49].copy()))
+        return out
+
+    def find_correspondences(self, edge_in: DeviceCloud, surf_in: DeviceCloud, q_xyzw, t) -> None:
+        """One correspondence pass at the pose (q, t) without a solve (stage inspection; needs set_trace)."""
+        q = np.ascontiguousarray(q_xyzw, dtype=np.float64)
+        tt = np.ascontiguousarray(t, dtype=np.float64)
+        _ffi.check(self._L.floam_odom_find_correspondences(self._need(), edge_in.handle, surf_in.handle,
+                                                           q.ctypes.data_as(C.POINTER(C.c_double)),
+                                                           tt.ctypes.data_as(C.POINTER(C.c_double))))
+
+    def correspondences(self, which: int) -> dict:
+        """The last correspondence pass of set `which` (0 edge, 1 surf): queries, flags, neighbour indices and
+        squared distances (n x 5), factor records (n x 9 edge / n x 7 surf)."""
+        from .synth import POINT_DTYPE
+        n = C.c_size_t()
+        _ffi.check(self._L.floam_odom_get_correspondences(self._need(), int(which), None, None, None, None, None, 0,
+                                                          C.byref(n)))
+        k = n.value
+        F = 9 if which == 0 else 7
+        q = np.zeros(max(k, 1), POINT_DTYPE)
+        fl = np.zeros(max(k, 1), np.uint8)
+        idx = np.zeros((max(k, 1), 5), np.int32)
+        sqd = np.zeros((max(k, 1), 5), np.float32)
+        rec = np.zeros((max(k, 1), F))
+        _ffi.check(self._L.floam_odom_get_correspondences(
+            self._need(), int(which), q.ctypes.data_as(C.c_void_p), fl.ctypes.data_as(C.c_void_p),
+            idx.ctypes.data_as(C.POINTER(C.c_int)), sqd.ctypes.data_as(C.POINTER(C.c_float)),
+            rec.ctypes.data_as(C.POINTER(C.c_double)), k, C.byref(n)))
+        return dict(queries=q[:k], flags=fl[:k], idx=idx[:k], sqd=sqd[:k], records=rec[:k])
+
     def set_shard(self, rank: int, world: int, unique_id: bytes | None) -> None:
         """Shard the correspondence queries over `world` ranks (one RCCL all-reduce per LM evaluation)."""
         buf = None

@@ -82,6 +82,32 @@ def lidar_model(config: str) -> LidarModel:
 MAP_PREFILL = {"c1": 0, "c2": 50_000, "c3": 200_000, "c4": 500_000, "c5": 2_000_000}
 
 
+def prefill_map(config: str, feature_extraction, target: int | None = None):
+    """The raw local map initMapWithPoints receives for ``config`` (SURVEY.md §8 d: maps prefilled to the stated
+    size): the edge / surf features of scan 0 (sensor frame == map frame) plus the features of earlier scans on the
+    ground-truth trajectory (scans -3, -6, ...) transformed into the map frame, until ``target`` points (the surf tail
+    trimmed to hit it exactly).  ``feature_extraction(raw, rings) -> (edge, surf)`` is the caller's
+    featureExtraction (the GPU operator in the bench, the CPU restatement in the tests: byte-identical outputs)."""
+    target = MAP_PREFILL.get(config, 0) if target is None else target
+    R = lidar_model(config).rings
+    e0, s0 = feature_extraction(generate_scan(config, 0), R)
+    E, S = [to_xyzi(e0)], [to_xyzi(s0)]
+    n = e0.shape[0] + s0.shape[0]
+    k = -3
+    while n < target:
+        e, s = feature_extraction(generate_scan(config, k), R)
+        T = gt_pose_matrix(k)
+        E.append(to_xyzi(transform_points(e, T)))
+        S.append(to_xyzi(transform_points(s, T)))
+        n += e.shape[0] + s.shape[0]
+        k -= 3
+    E, S = np.concatenate(E), np.concatenate(S)
+    extra = E.shape[0] + S.shape[0] - target
+    if target and extra > 0:
+        S = S[: S.shape[0] - extra]
+    return E, S
+
+
 # ----------------------------------------------------------------------------------------------- trajectory
 V_FWD = 1.0                       # m/s
 YAW_RATE = math.radians(5.0)      # rad/s

@@ -232,10 +232,44 @@ typedef struct floam_odom_stats {
 } floam_odom_stats;
 floam_status floam_odom_get_stats(const floam_odom* o, floam_odom_stats* s);
 
+/* KeyFrameUpdate(pose) (include/odomEstimationClass.h:80, src/odomEstimationClass.cpp:320-343): public in the
+ * reference's header; updatePointsToMap calls it internally (the process-wide `first` flag of Q6 is shared with
+ * those calls).  *is_keyframe = 1 when the pose moved > 0.07 m or turned > 2 deg from the last keyframe. */
+floam_status floam_odom_keyframe_update(floam_odom* o, const double q_xyzw[4], const double t[3], int* is_keyframe);
+
+/* Precision of the correspondence geometry and of the residual / Jacobian evaluation (extension: BASELINE.json
+ * configs[4], the fp32 vs fp64 tolerance sweep).  FLOAM_PRECISION_FP64 (default) is the reference's double
+ * arithmetic (src/odomEstimationClass.cpp:156-243, src/lidarOptimization.cpp:12-74); FLOAM_PRECISION_FP32 computes the
+ * line / plane fits, residuals, Jacobians and per-thread J^T J sums in float (reductions and the LM control stay in
+ * double). */
+enum { FLOAM_PRECISION_FP64 = 0, FLOAM_PRECISION_FP32 = 1 };
+floam_status floam_odom_set_precision(floam_odom* o, int precision);
+
+/* Stage inspection (extension, for parity tests against the CPU restatement).  floam_odom_set_trace(o, capacity):
+ * capacity > 0 records one 49-double record per ceres::Solve (oracle/odom.cpp SolveTrace order: edge queries, surf
+ * queries, edge factors, surf factors, iterations, successful steps, initial cost, final cost, x_in[7], x_out[7],
+ * J^T J at x_in (upper, row-major, 21), J^T r at x_in (6)) and keeps the last correspondence pass's neighbour indices
+ * and squared distances; 0 turns it off.  floam_odom_get_traces returns and clears the recorded solves. */
+floam_status floam_odom_set_trace(floam_odom* o, size_t capacity);
+floam_status floam_odom_get_traces(floam_odom* o, double* out /* capacity x 49 */, size_t capacity, size_t* n_out);
+/* One correspondence pass at an explicit pose, without a solve (the map and the odometry state are untouched):
+ * downSamplingToMap of edge / surf, pointAssociateToMap at (q, t), the 5-NN search with the sqd[4] < 1 gate and the
+ * addEdgeCostFactor / addSurfCostFactor geometry (src/odomEstimationClass.cpp:137-142, 126-135, 144-251); read the
+ * result with floam_odom_get_correspondences.  Needs tracing on. */
+floam_status floam_odom_find_correspondences(floam_odom* o, const floam_cloud* edge, const floam_cloud* surf,
+                                             const double q_xyzw[4], const double t[3]);
+/* The last correspondence pass of set `which` (0 edge / corner map, 1 surf / surf map): the downsampled queries
+ * (32-B records, sensor frame), per query flags (bit 0 accepted factor, bit 2 five neighbours with sqd < 1), the 5
+ * neighbours' map indices and float squared distances (row-major n x 5; valid when bit 2 is set) and the factor
+ * records (edge: cp, a, b = 9 doubles; surf: cp, n, d = 7 doubles; valid when bit 0 is set).  Any output may be NULL. */
+floam_status floam_odom_get_correspondences(floam_odom* o, int which, void* queries, uint8_t* flags, int* idx,
+                                            float* sqd, double* records, size_t capacity, size_t* n_out);
+
 /* Query sharding over ranks (one process per GPU): each rank runs the same calls on the same scans; the
  * correspondence queries are split into `world` contiguous ranges and the normal equations (J^T J, J^T r, cost)
  * are summed with one RCCL all-reduce per LM evaluation.  unique_id: 128 bytes from floam_comm_unique_id() on
- * rank 0, broadcast by the caller (e.g. torch.distributed). */
+ * rank 0, broadcast by the caller (e.g. torch.distributed).  world = 1 with a unique id runs the sharded path through
+ * a one-rank RCCL communicator (bit-identical to the unsharded solve). */
 floam_status floam_comm_unique_id(void* unique_id_128);
 floam_status floam_odom_set_shard(floam_odom* o, int rank, int world, const void* unique_id_128);
 /* Same sharding with a caller-supplied host all-reduce instead of RCCL (in-place sum of `count` doubles over all

@@ -69,6 +69,11 @@ def lib():
         L.oracle_odom_num_traces.restype = C.c_size_t
         L.oracle_odom_get_trace.argtypes = [C.c_void_p, C.c_size_t, c_double_p]
         L.oracle_reset_process_statics.argtypes = []
+        L.oracle_stage_correspondences.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, c_double_p,
+                                                   C.c_int, c_int_p, c_float_p, C.c_void_p, c_double_p]
+        L.oracle_stage_associate.argtypes = [C.c_void_p, C.c_size_t, c_double_p, C.c_void_p]
+        L.oracle_stage_solve.argtypes = [c_double_p, C.c_size_t, c_double_p, C.c_size_t, C.c_int, c_double_p,
+                                         c_double_p]
         L.oracle_edge_residual.argtypes = [c_double_p] * 5
         L.oracle_edge_residual.restype = C.c_double
         L.oracle_surf_residual.argtypes = [c_double_p, c_double_p, C.c_double, c_double_p, c_double_p]
@@ -244,14 +249,56 @@ class Odometry:
         for i in range(n):
             b = np.zeros(49)
             self._L.oracle_odom_get_trace(self._h, i, b.ctypes.data_as(c_double_p))
-            out.append(dict(n_edge_queries=int(b[0]), n_surf_queries=int(b[1]), n_edge_corr=int(b[2]),
-                            n_surf_corr=int(b[3]), iterations=int(b[4]), successful=int(b[5]),
-                            initial_cost=b[6], final_cost=b[7], x_in=b[8:15].copy(), x_out=b[15:22].copy(),
-                            H0=b[22:43].copy(), g0=b[43:49].copy()))
+            out.append(_trace_dict(b))
         return out
 
     def clear_traces(self):
         self._L.oracle_odom_clear_traces(self._h)
+
+
+def _trace_dict(b):
+    return dict(n_edge_queries=int(b[0]), n_surf_queries=int(b[1]), n_edge_corr=int(b[2]), n_surf_corr=int(b[3]),
+                iterations=int(b[4]), successful=int(b[5]), initial_cost=b[6], final_cost=b[7], x_in=b[8:15].copy(),
+                x_out=b[15:22].copy(), H0=b[22:43].copy(), g0=b[43:49].copy())
+
+
+def stage_correspondences(map_points: np.ndarray, queries: np.ndarray, x, edge: bool):
+    """One correspondence pass (src/odomEstimationClass.cpp:144-251): pointAssociateToMap at parameters x
+    (qx, qy, qz, qw, tx, ty, tz), KD-tree 5-NN, the sqd[4] < 1 gate, line / plane geometry.  Returns dict(idx (n, 5),
+    sqd (n, 5), flags (n,) bit 0 factor kept / bit 2 gate passed, records (n, 9 edge | 7 surf))."""
+    mp, q = _as_points(map_points), _as_points(queries)
+    n = q.shape[0]
+    F = 9 if edge else 7
+    idx = np.full((max(n, 1), 5), -1, np.int32)
+    sqd = np.full((max(n, 1), 5), np.inf, np.float32)
+    flags = np.zeros(max(n, 1), np.uint8)
+    rec = np.zeros((max(n, 1), F))
+    xx = np.ascontiguousarray(x, dtype=np.float64)
+    lib().oracle_stage_correspondences(_ptr(mp), mp.shape[0], _ptr(q), n, xx.ctypes.data_as(c_double_p), int(edge),
+                                       idx.ctypes.data_as(c_int_p), sqd.ctypes.data_as(c_float_p), _ptr(flags),
+                                       rec.ctypes.data_as(c_double_p))
+    return dict(idx=idx[:n], sqd=sqd[:n], flags=flags[:n], records=rec[:n])
+
+
+def associate_to_map(points: np.ndarray, x) -> np.ndarray:
+    """pointAssociateToMap (src/odomEstimationClass.cpp:126-135) at parameters x: double math, float result."""
+    p = _as_points(points)
+    out = np.zeros_like(p)
+    xx = np.ascontiguousarray(x, dtype=np.float64)
+    lib().oracle_stage_associate(_ptr(p), p.shape[0], xx.ctypes.data_as(c_double_p), _ptr(out))
+    return out
+
+
+def stage_solve(edge_records: np.ndarray, surf_records: np.ndarray, x, huber: bool = False):
+    """ceres::Solve (src/odomEstimationClass.cpp:95-108) on given factor records from parameters x.
+    Returns (x_out, trace dict as Odometry.traces())."""
+    e = np.ascontiguousarray(edge_records, dtype=np.float64).reshape(-1, 9)
+    s = np.ascontiguousarray(surf_records, dtype=np.float64).reshape(-1, 7)
+    xx = np.array(x, dtype=np.float64)
+    tr = np.zeros(49)
+    lib().oracle_stage_solve(e.ctypes.data_as(c_double_p), e.shape[0], s.ctypes.data_as(c_double_p), s.shape[0],
+                             int(huber), xx.ctypes.data_as(c_double_p), tr.ctypes.data_as(c_double_p))
+    return xx, _trace_dict(tr)
 
 
 def reset_process_statics():

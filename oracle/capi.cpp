@@ -115,6 +115,18 @@ void oracle_odom_get_trace(void* h, size_t i, double* out /* 49 */) {
   for (int j = 0; j < 6; ++j) out[k++] = t.g0[j];
 }
 void oracle_odom_clear_traces(void* h) { odom_clear_traces(static_cast<OdomState*>(h)); }
+void oracle_stage_correspondences(const void* map, size_t m, const void* q, size_t nq, const double* x, int edge,
+                                  int* idx, float* sqd, unsigned char* flags, double* rec) {
+  stage_correspondences(static_cast<const Pt*>(map), m, static_cast<const Pt*>(q), nq, x, edge != 0, idx, sqd, flags,
+                        rec);
+}
+void oracle_stage_associate(const void* in, size_t n, const double* x, void* out) {
+  stage_associate(static_cast<const Pt*>(in), n, x, static_cast<Pt*>(out));
+}
+void oracle_stage_solve(const double* erec, size_t ne, const double* srec, size_t ns, int huber, double* x,
+                        double* trace) {
+  stage_solve(erec, ne, srec, ns, huber != 0, x, trace);
+}
 void oracle_reset_process_statics() { reset_process_statics(); }
 
 double oracle_edge_residual(const double* cp, const double* a, const double* b, const double* x, double* J) {

@@ -361,40 +361,63 @@ Pt associate(const OdomState* s, const Pt& pi) {
   return po;
 }
 
+// addEdgeCostFactor's per-query geometry (odomEstimationClass.cpp:156-189): line through the 5 neighbours, kept iff
+// the largest eigenvalue exceeds 3x the middle one
+bool edge_factor(const std::vector<Pt>& map, const int (&ind)[5], const Pt& p, EdgeBlock* out) {
+  V3 near[5];
+  V3 center{0, 0, 0};
+  for (int j = 0; j < 5; ++j) {
+    near[j] = V3{map[ind[j]].x, map[ind[j]].y, map[ind[j]].z};
+    center = center + near[j];
+  }
+  center = center / 5.0;
+  M3 cov = M3::zero();
+  for (int j = 0; j < 5; ++j) {
+    const V3 z = near[j] - center;
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) cov.m[a][b] = cov.m[a][b] + z[a] * z[b];
+  }
+  double ev[3], evec[3][3];
+  eig_sym3(cov, ev, evec);
+  const V3 u{evec[2][0], evec[2][1], evec[2][2]};
+  if (!(ev[2] > 3 * ev[1])) return false;
+  *out = EdgeBlock{V3{p.x, p.y, p.z}, 0.1 * u + center, -0.1 * u + center};
+  return true;
+}
+
+// addSurfCostFactor's per-query geometry (odomEstimationClass.cpp:208-243): least-squares plane n.x + 1 = 0 through
+// the 5 neighbours (ColPivHouseholderQR), kept iff every neighbour is within 0.2 of it
+bool surf_factor(const std::vector<Pt>& map, const int (&ind)[5], const Pt& p, SurfBlock* out) {
+  double A[5][3], b[5];
+  for (int j = 0; j < 5; ++j) {
+    A[j][0] = map[ind[j]].x;
+    A[j][1] = map[ind[j]].y;
+    A[j][2] = map[ind[j]].z;
+    b[j] = -1.0;
+  }
+  double nv[3];
+  colpiv_qr_solve_5x3(A, b, nv);
+  V3 n{nv[0], nv[1], nv[2]};
+  const double z = sqnorm(n);
+  const double negative_OA_dot_norm = 1 / std::sqrt(z);
+  if (z > 0) n = n / std::sqrt(z);   // Eigen normalize()
+  for (int j = 0; j < 5; ++j)
+    if (std::fabs(n.x * map[ind[j]].x + n.y * map[ind[j]].y + n.z * map[ind[j]].z + negative_OA_dot_norm) > 0.2)
+      return false;
+  *out = SurfBlock{V3{p.x, p.y, p.z}, n, negative_OA_dot_norm};
+  return true;
+}
+
 // addEdgeCostFactor (odomEstimationClass.cpp:144-196)
 void add_edge(OdomState* s, const std::vector<Pt>& pc, const std::vector<Pt>& map, const KdTree& kd, Problem& P) {
-  int corner_num = 0;
   for (size_t i = 0; i < pc.size(); ++i) {
     const Pt pt = associate(s, pc[i]);
     const float q[3] = {pt.x, pt.y, pt.z};
     int ind[5];
     float sqd[5];
     kd.knn(q, 5, ind, sqd);
-    if (sqd[4] < 1.0) {
-      V3 near[5];
-      V3 center{0, 0, 0};
-      for (int j = 0; j < 5; ++j) {
-        near[j] = V3{map[ind[j]].x, map[ind[j]].y, map[ind[j]].z};
-        center = center + near[j];
-      }
-      center = center / 5.0;
-      M3 cov = M3::zero();
-      for (int j = 0; j < 5; ++j) {
-        const V3 z = near[j] - center;
-        for (int a = 0; a < 3; ++a)
-          for (int b = 0; b < 3; ++b) cov.m[a][b] = cov.m[a][b] + z[a] * z[b];
-      }
-      double ev[3], evec[3][3];
-      eig_sym3(cov, ev, evec);
-      const V3 u{evec[2][0], evec[2][1], evec[2][2]};
-      const V3 cp{pc[i].x, pc[i].y, pc[i].z};
-      if (ev[2] > 3 * ev[1]) {
-        const V3 a = 0.1 * u + center;
-        const V3 b = -0.1 * u + center;
-        P.edges.push_back(EdgeBlock{cp, a, b});
-        corner_num++;
-      }
-    }
+    EdgeBlock e;
+    if (sqd[4] < 1.0 && edge_factor(map, ind, pc[i], &e)) P.edges.push_back(e);
   }
 }
 
@@ -406,30 +429,8 @@ void add_surf(OdomState* s, const std::vector<Pt>& pc, const std::vector<Pt>& ma
     int ind[5];
     float sqd[5];
     kd.knn(q, 5, ind, sqd);
-    if (sqd[4] < 1.0) {
-      double A[5][3], b[5];
-      for (int j = 0; j < 5; ++j) {
-        A[j][0] = map[ind[j]].x;
-        A[j][1] = map[ind[j]].y;
-        A[j][2] = map[ind[j]].z;
-        b[j] = -1.0;
-      }
-      double nv[3];
-      colpiv_qr_solve_5x3(A, b, nv);
-      V3 n{nv[0], nv[1], nv[2]};
-      const double z = sqnorm(n);
-      const double negative_OA_dot_norm = 1 / std::sqrt(z);
-      if (z > 0) n = n / std::sqrt(z);   // Eigen normalize()
-      bool planeValid = true;
-      for (int j = 0; j < 5; ++j) {
-        if (std::fabs(n.x * map[ind[j]].x + n.y * map[ind[j]].y + n.z * map[ind[j]].z + negative_OA_dot_norm) >
-            0.2) {
-          planeValid = false;
-          break;
-        }
-      }
-      if (planeValid) P.surfs.push_back(SurfBlock{V3{pc[i].x, pc[i].y, pc[i].z}, n, negative_OA_dot_norm});
-    }
+    SurfBlock f;
+    if (sqd[4] < 1.0 && surf_factor(map, ind, pc[i], &f)) P.surfs.push_back(f);
   }
 }
 
@@ -596,5 +597,75 @@ const Pt* odom_map_data(const OdomState* s, int which) {
 const std::vector<SolveTrace>& odom_traces(const OdomState* s) { return s->traces; }
 void odom_clear_traces(OdomState* s) { s->traces.clear(); }
 int odom_optimization_count(const OdomState* s) { return s->optimization_count; }
+
+// stage hooks (capi.cpp): one correspondence pass — pointAssociateToMap at parameters x, the KD-tree 5-NN, the
+// sqd[4] < 1 gate and the factor geometry, per query: neighbours (index, float sq-distance), flags (bit 0 factor
+// kept, bit 2 gate passed) and the record (edge cp, a, b; surf cp, n, d)
+void stage_correspondences(const Pt* map, size_t m, const Pt* q, size_t nq, const double* x, bool edge, int* idx,
+                           float* sqd, unsigned char* flags, double* rec) {
+  OdomState s{};
+  std::copy(x, x + 7, s.parameters);
+  const std::vector<Pt> mp(map, map + m);
+  KdTree kd;
+  kd.build(mp.data(), mp.size());
+  for (size_t i = 0; i < nq; ++i) {
+    const Pt pt = associate(&s, q[i]);
+    const float qq[3] = {pt.x, pt.y, pt.z};
+    int* ind = idx + 5 * i;
+    float* d = sqd + 5 * i;
+    kd.knn(qq, 5, ind, d);
+    flags[i] = 0;
+    if (!(d[4] < 1.0)) continue;
+    flags[i] = 4;
+    int ii[5] = {ind[0], ind[1], ind[2], ind[3], ind[4]};
+    if (edge) {
+      EdgeBlock e;
+      if (edge_factor(mp, ii, q[i], &e)) {
+        flags[i] |= 1;
+        const double r[9] = {e.cp.x, e.cp.y, e.cp.z, e.a.x, e.a.y, e.a.z, e.b.x, e.b.y, e.b.z};
+        std::copy(r, r + 9, rec + 9 * i);
+      }
+    } else {
+      SurfBlock f;
+      if (surf_factor(mp, ii, q[i], &f)) {
+        flags[i] |= 1;
+        const double r[7] = {f.cp.x, f.cp.y, f.cp.z, f.n.x, f.n.y, f.n.z, f.d};
+        std::copy(r, r + 7, rec + 7 * i);
+      }
+    }
+  }
+}
+
+// pointAssociateToMap (odomEstimationClass.cpp:126-135) of n points at parameters x
+void stage_associate(const Pt* in, size_t n, const double* x, Pt* out) {
+  OdomState s{};
+  std::copy(x, x + 7, s.parameters);
+  for (size_t i = 0; i < n; ++i) out[i] = associate(&s, in[i]);
+}
+
+// ceres::Solve on given factor records (edge: 9 doubles, surf: 7) from parameters x (in: x_in, out: the solution);
+// trace: the SolveTrace layout (49 doubles)
+void stage_solve(const double* erec, size_t ne, const double* srec, size_t ns, bool huber, double* x, double* trace) {
+  Problem P;
+  P.huber = huber;
+  for (size_t i = 0; i < ne; ++i) {
+    const double* r = erec + 9 * i;
+    P.edges.push_back(EdgeBlock{V3{r[0], r[1], r[2]}, V3{r[3], r[4], r[5]}, V3{r[6], r[7], r[8]}});
+  }
+  for (size_t i = 0; i < ns; ++i) {
+    const double* r = srec + 7 * i;
+    P.surfs.push_back(SurfBlock{V3{r[0], r[1], r[2]}, V3{r[3], r[4], r[5]}, r[6]});
+  }
+  double x_in[7];
+  std::copy(x, x + 7, x_in);
+  const SolveOut so = ceres_solve(P, x);
+  int k = 0;
+  trace[k++] = 0; trace[k++] = 0; trace[k++] = (double)ne; trace[k++] = (double)ns;
+  trace[k++] = so.iterations; trace[k++] = so.successful; trace[k++] = so.initial_cost; trace[k++] = so.final_cost;
+  for (int j = 0; j < 7; ++j) trace[k++] = x_in[j];
+  for (int j = 0; j < 7; ++j) trace[k++] = x[j];
+  for (int j = 0; j < 21; ++j) trace[k++] = so.H0[j];
+  for (int j = 0; j < 6; ++j) trace[k++] = so.g0[j];
+}
 
 }  // namespace oracle

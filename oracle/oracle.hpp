@@ -114,6 +114,10 @@ const Pt* odom_map_data(const OdomState*, int which);
 const std::vector<SolveTrace>& odom_traces(const OdomState*);
 void odom_clear_traces(OdomState*);
 int odom_optimization_count(const OdomState*);
+void stage_correspondences(const Pt* map, size_t m, const Pt* q, size_t nq, const double* x, bool edge, int* idx,
+                           float* sqd, unsigned char* flags, double* rec);
+void stage_associate(const Pt* in, size_t n, const double* x, Pt* out);
+void stage_solve(const double* erec, size_t ne, const double* srec, size_t ns, bool huber, double* x, double* trace);
 // ---------------------------------------------------------------------------------------------- IMU pre-processing
 // (oracle/imu.cpp).  Quat is Eigen's (x, y, z, w) order (la.hpp).
 struct ImuHandler {                       // dmapping::ImuHandler (include/dataHandler.h:31-66), orientation only

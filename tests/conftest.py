@@ -21,6 +21,22 @@ def oracle_lib():
 
 
 @pytest.fixture(scope="session")
+def prefilled_map(oracle_lib):
+    """prefilled_map(config) -> (edge map, surf map): the raw map initMapWithPoints receives at BASELINE.json's
+    config sizes (floam_amd.synth.prefill_map with the oracle's featureExtraction, byte-identical to the GPU's),
+    built once per session."""
+    from floam_amd import synth
+    cache = {}
+
+    def get(config):
+        if config not in cache:
+            fe = lambda raw, R: oracle_lib.feature_extraction(raw, R, 0.5, 90.0, canonical=True)[:2]
+            cache[config] = synth.prefill_map(config, fe)
+        return cache[config]
+    return get
+
+
+@pytest.fixture(scope="session")
 def floam_gpu():
     """The HIP product path.  GPU tests must never pass on a fallback: fail loudly if the library or device is
     missing."""

@@ -256,3 +256,100 @@ def test_odometry_sequence_c3(floam_gpu, oracle_lib):
     res, _, _ = _run_sequence(floam_gpu, oracle_lib, "c3", 5)
     for k, dt, dr, st, _ in res:
         assert dt < 1e-3 and dr < 1e-3, (k, dt, dr, st)
+
+
+def _compare_traces(g_tr, r_tr, what):
+    """Per-solve LM traces (floam_odom_get_traces vs the oracle's SolveTrace): counts and iterations exact, costs and
+    the iteration-zero normal equations to the Gram-vs-per-record rounding (J^T J ~1e-9, J^T r ~1e-8 of its
+    largest entry: the surf half of J^T r is a difference of |p|^2-sized terms)."""
+    assert len(g_tr) == len(r_tr), (what, len(g_tr), len(r_tr))
+    for k, (g, r) in enumerate(zip(g_tr, r_tr)):
+        w = f"{what} solve {k}"
+        for f in ("n_edge_queries", "n_surf_queries", "n_edge_corr", "n_surf_corr", "iterations", "successful"):
+            assert g[f] == r[f], (w, f, g[f], r[f])
+        for f in ("initial_cost", "final_cost"):
+            assert abs(g[f] - r[f]) <= 1e-7 * abs(r[f]) + 1e-12, (w, f, g[f], r[f])
+        np.testing.assert_allclose(g["H0"], r["H0"], rtol=0, atol=1e-9 * (np.max(np.abs(r["H0"])) + 1.0), err_msg=w)
+        np.testing.assert_allclose(g["g0"], r["g0"], rtol=0, atol=1e-7 * (np.max(np.abs(r["g0"])) + 1.0), err_msg=w)
+
+
+@pytest.mark.parametrize("config,nscan", [("c2", 5), ("c3", 5), ("c4", 4), ("c5", 3)])
+def test_odometry_prefilled(floam_gpu, oracle_lib, prefilled_map, config, nscan):
+    """BASELINE.json configs C2-C5 (configs never run through odometry on the GPU): the map prefilled to
+    the config's size through initMapWithPoints (the bench's recipe), then deskewed UpdatePointsToMapSelector calls
+    on scans 1..nscan — featureExtraction on the GPU (byte-identical to the oracle's), per-scan pose vs the oracle
+    within the north star's 1e-3 m / 1e-3 rad (asserted at 1e-6), every solve's trace compared."""
+    from floam_amd.odom_estimation import reset_process_state
+    R = synth.lidar_model(config).rings
+    mapE, mapS = prefilled_map(config)
+    ref = oracle_lib.Odometry(R, 0.1, 0.5, 90.0, 0.1, "Cauchy", stable_voxel=True)
+    oracle_lib.reset_process_statics()
+    reset_process_state()
+    p = _params(R)
+    lp = floam_gpu.LaserProcessingClass()
+    lp.init(p)
+    odo = floam_gpu.OdomEstimationClass()
+    odo.init(p, 0.1, "Cauchy")
+    odo.set_trace(256)
+    odo.initMapWithPoints(floam_gpu.DeviceCloud(mapE), floam_gpu.DeviceCloud(mapS))
+    ref.init_map(mapE, mapS)
+    for k in range(1, nscan + 1):
+        raw = synth.generate_scan(config, k)
+        e_ref, s_ref, _ = oracle_lib.feature_extraction(raw, R, 0.5, 90.0, canonical=True)
+        de, ds = floam_gpu.DeviceCloud(), floam_gpu.DeviceCloud()
+        lp.featureExtraction(floam_gpu.DeviceCloud(raw), de, ds)
+        _assert_same_cloud(de.download(), e_ref, f"{config} edge {k}")
+        _assert_same_cloud(ds.download(), s_ref, f"{config} surf {k}")
+        odo.UpdatePointsToMapSelector(de, ds, True)
+        ref.update_selector(e_ref, s_ref, True)
+        (qg, tg), (qr, tr) = odo.pose(), ref.pose()
+        dt, dr = float(np.linalg.norm(tg - tr)), _angle_between(qg, qr)
+        assert dt < 1e-6 and dr < 1e-6, (config, k, dt, dr, odo.stats())
+        _compare_traces(odo.traces(), ref.traces(), f"{config} scan {k}")
+        ref.clear_traces()
+    me, ms = odo.map_sizes()
+    assert me == ref.map(0).shape[0] and ms == ref.map(1).shape[0]
+
+
+def test_odometry_aliased_selector(floam_gpu, oracle_lib):
+    """UpdatePointsToMapSelector(edge, edge, deskew): one cloud as both inputs — the reference compensates it twice,
+    one CompensateVelocity after the other (src/odomEstimationClass.cpp:42-43)."""
+    from floam_amd.odom_estimation import reset_process_state
+    R = 16
+    ref = oracle_lib.Odometry(R, 0.1, 0.5, 90.0, 0.1, "Cauchy", stable_voxel=True)
+    oracle_lib.reset_process_statics()
+    reset_process_state()
+    lp = floam_gpu.LaserProcessingClass()
+    lp.init(_params(R))
+    odo = floam_gpu.OdomEstimationClass()
+    odo.init(_params(R), 0.1, "Cauchy")
+    for k in range(5):
+        raw = synth.generate_scan("c1", k)
+        e_ref, s_ref, _ = oracle_lib.feature_extraction(raw, R, 0.5, 90.0, canonical=True)
+        de, ds = floam_gpu.DeviceCloud(), floam_gpu.DeviceCloud()
+        lp.featureExtraction(floam_gpu.DeviceCloud(raw), de, ds)
+        if k == 0:
+            odo.initMapWithPoints(de, ds)
+            ref.init_map(synth.to_xyzi(e_ref), synth.to_xyzi(s_ref))
+            continue
+        odo.UpdatePointsToMapSelector(de, de, True)
+        ref.update_selector(e_ref, e_ref, True)
+        _assert_same_cloud(de.download(), e_ref, f"twice-deskewed edge {k}")
+        (qg, tg), (qr, tr) = odo.pose(), ref.pose()
+        assert np.linalg.norm(tg - tr) < 1e-6 and _angle_between(qg, qr) < 1e-6, k
+
+
+def test_sparse_map_distinct_cells(floam_gpu):
+    """a 1024-point map with every point in its own 1-m cell fills a coarse table of 1024 slots; the
+    table is now sized for a load <= 1/2, so lookups of absent cells terminate (an update completes)."""
+    g = np.arange(1024)
+    m = np.zeros(1024, synth.POINT_DTYPE)
+    m["x"], m["y"], m["z"] = (g % 16) * 2.0 + 0.5, ((g // 16) % 8) * 2.0 + 0.5, (g // 128) * 2.0 + 0.5
+    m["pad0"] = 1.0
+    odo = floam_gpu.OdomEstimationClass()
+    odo.init(_params(16), 0.1, "Cauchy")
+    odo.initMapWithPoints(floam_gpu.DeviceCloud(m), floam_gpu.DeviceCloud(m))
+    q = m.copy()
+    q["x"] += 0.75   # every query 0.75 m from its nearest point: lookups of empty neighbour cells
+    odo.updatePointsToMap(floam_gpu.DeviceCloud(q), floam_gpu.DeviceCloud(q))
+    assert odo.stats()["optimization_count"] == 11

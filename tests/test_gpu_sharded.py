@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 NSCAN = 5
 
 
-def _run(rank, world, port, q):
+def _run(rank, world, port, q, rccl_world1=False, loss="Cauchy", fp32=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch
     import torch.distributed as dist
@@ -29,8 +29,13 @@ def _run(rank, world, port, q):
         lp = floam_amd.LaserProcessingClass(device=0)
         lp.init(p)
         odo = floam_amd.OdomEstimationClass(device=0)
-        odo.init(p, 0.1, "Cauchy")
+        odo.init(p, 0.1, loss)
+        if fp32:
+            odo.set_precision(True)
         reset_process_state()
+        if rccl_world1:   # the sharded solve through a one-rank RCCL communicator (ncclAllReduce on the stream)
+            from floam_amd.odom_estimation import comm_unique_id
+            odo.set_shard(0, 1, comm_unique_id())
         if world > 1:
             def allreduce(arr):
                 t = torch.from_numpy(arr)
@@ -78,3 +83,13 @@ def test_sharded_two_ranks_match_unsharded(floam_gpu):
         dt = np.linalg.norm(res[0][k][4:] - ref[k][4:])
         dr = 2 * math.acos(min(1.0, abs(float(np.dot(res[0][k][:4], ref[k][:4])))))
         assert dt < 1e-9 and dr < 1e-9, (k, dt, dr)
+
+
+@pytest.mark.parametrize("loss,fp32", [("Cauchy", False), ("huber", False), ("Cauchy", True)])
+def test_rccl_world1_matches_unsharded(floam_gpu, loss, fp32):
+    """The sharded solve (one launch + one ncclAllReduce of the 29 sums per LM evaluation, the control step folded
+    into the next launch) on a one-rank RCCL communicator: the same fixed-order reductions as the resident
+    single-GPU solve, so the poses are bit-identical."""
+    ref = _run(0, 1, _free_port(), None, loss=loss, fp32=fp32)
+    got = _run(0, 1, _free_port(), None, rccl_world1=True, loss=loss, fp32=fp32)
+    np.testing.assert_array_equal(got, ref)

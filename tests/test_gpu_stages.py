@@ -1,0 +1,214 @@
+"""Stage-level GPU parity (VERDICT r01 "What's weak" 1): each stage of one updatePointsToMap compared with the CPU
+oracle on identical inputs, not only through the final pose.
+
+* downSamplingToMap (src/odomEstimationClass.cpp:137-142): the downsampled queries, bit for bit;
+* the KD-tree 5-NN with the sqd[4] < 1 gate (:153-154, :206-210): neighbour index sets and float squared distances;
+* addEdgeCostFactor / addSurfCostFactor geometry (:156-243): the factor records;
+* ceres::Solve (:95-108): per-solve iterations, initial / final cost, J^T J and J^T r at iteration zero, the solution.
+
+Ties (equal float distances) are broken by map index on the GPU; FLANN keeps the first point its tree traversal finds
+(oracle/flann_kdtree.cpp).  The rule is pinned by test_knn_ties: distances always agree, index sets agree whenever
+the 5th and 6th distances differ, duplicated points give identical records (same coordinates), and boundary ties
+follow the lowest-index rule exactly.
+"""
+import numpy as np
+import pytest
+
+from floam_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+MIN_DIS, MAX_DIS = 0.5, 90.0
+
+
+def _params(R):
+    from floam_amd import LidarParams
+    return LidarParams(num_lines=R, scan_period=0.1, vertical_angle=2.0, max_distance=MAX_DIS, min_distance=MIN_DIS)
+
+
+def _sorted_pairs(idx, sqd):
+    """(sqd, idx) pairs of one query in ascending order (the GPU's tie rule)."""
+    return sorted(zip(sqd.tolist(), idx.tolist()))
+
+
+def _float_sqd(map_points, q):
+    """FLANN's L2_Simple<float> distances of query q to every map point: ((0 + dx^2) + dy^2) + dz^2 in float."""
+    dx = np.float32(q["x"]) - map_points["x"]
+    dy = np.float32(q["y"]) - map_points["y"]
+    dz = np.float32(q["z"]) - map_points["z"]
+    return ((np.float32(0) + dx * dx) + dy * dy) + dz * dz
+
+
+def _compare_pass(gpu, ref, edge, what, map_points=None, world=None):
+    """GPU correspondence pass vs the oracle's on the same queries, map and pose.  world: the queries in the map
+    frame (float), to check index-set differences against a brute-force tie test."""
+    gf, rf = gpu["flags"], ref["flags"]
+    # the gate (5 neighbours within sqd < 1) is decided identically
+    np.testing.assert_array_equal(gf & 4, rf & 4, err_msg=f"{what}: gate")
+    gated = np.nonzero(rf & 4)[0]
+    assert gated.size > 0, what
+    gs, rs = gpu["sqd"][gated], ref["sqd"][gated]
+    np.testing.assert_array_equal(gs, rs, err_msg=f"{what}: float squared distances")
+    gi, ri = gpu["idx"][gated], ref["idx"][gated]
+    same_set = np.all(np.sort(gi, axis=1) == np.sort(ri, axis=1), axis=1)
+    # any index difference must come from an exact distance tie (within the 5 or between the 5th and the 6th)
+    tied = np.zeros(gated.size, bool)
+    for k in np.nonzero(~same_set)[0]:
+        d = np.sort(_float_sqd(map_points, world[gated[k]]))
+        tied[k] = len(set(d[:5].tolist())) < 5 or d[4] == d[5]
+    assert np.all(same_set | tied), f"{what}: index sets differ without a tie ({np.sum(~same_set & ~tied)})"
+    # the factor decision and the records: bit-identical when the neighbour order matches (tie-free queries)
+    np.testing.assert_array_equal(gf[gated] & 1, rf[gated] & 1, err_msg=f"{what}: factor accepted")
+    acc = gated[(rf[gated] & 1) != 0]
+    exact = acc[np.all(gpu["idx"][acc] == ref["idx"][acc], axis=1)]
+    np.testing.assert_array_equal(gpu["records"][exact], ref["records"][exact], err_msg=f"{what}: records")
+    return int(acc.size), int(tied.sum())
+
+
+@pytest.mark.parametrize("config", ["c3", "c5"])
+def test_stages_one_update(floam_gpu, oracle_lib, prefilled_map, config):
+    """One updatePointsToMap (INITIAL_ITERATION: no map update) after initMapWithPoints: 11 solves.  The last
+    correspondence pass is compared stage by stage; every solve's trace is compared with the oracle's."""
+    from floam_amd.odom_estimation import reset_process_state
+    R = synth.lidar_model(config).rings
+    mapE, mapS = prefilled_map(config)
+    raw = synth.generate_scan(config, 1)
+    e_ref, s_ref, _ = oracle_lib.feature_extraction(raw, R, MIN_DIS, MAX_DIS, canonical=True)
+    reset_process_state()
+    odo = floam_gpu.OdomEstimationClass()
+    odo.init(_params(R), 0.1, "Cauchy")
+    odo.set_trace(64)
+    odo.initMapWithPoints(floam_gpu.DeviceCloud(mapE), floam_gpu.DeviceCloud(mapS))
+    odo.updatePointsToMap(floam_gpu.DeviceCloud(e_ref), floam_gpu.DeviceCloud(s_ref), odo.INITIAL_ITERATION)
+    g_tr = odo.traces()
+    ref = oracle_lib.Odometry(R, 0.1, MIN_DIS, MAX_DIS, 0.1, "Cauchy", stable_voxel=True)
+    ref.init_map(mapE, mapS)
+    ref.update(e_ref, s_ref, oracle_lib.Odometry.INITIAL_ITERATION)
+    r_tr = ref.traces()
+    assert len(g_tr) == len(r_tr) == 11
+    for k, (g, r) in enumerate(zip(g_tr, r_tr)):
+        what = f"{config} solve {k}"
+        for f in ("n_edge_queries", "n_surf_queries", "n_edge_corr", "n_surf_corr", "iterations", "successful"):
+            assert g[f] == r[f], (what, f, g[f], r[f])
+        np.testing.assert_allclose(g["x_in"], r["x_in"], rtol=0, atol=1e-9, err_msg=what)
+        np.testing.assert_allclose(g["x_out"], r["x_out"], rtol=0, atol=1e-9, err_msg=what)
+        for f in ("initial_cost", "final_cost"):
+            assert abs(g[f] - r[f]) <= 1e-7 * abs(r[f]) + 1e-12, (what, f, g[f], r[f])
+        scale = np.max(np.abs(r["H0"])) + 1.0
+        np.testing.assert_allclose(g["H0"], r["H0"], rtol=0, atol=1e-9 * scale, err_msg=what)
+        np.testing.assert_allclose(g["g0"], r["g0"], rtol=0, atol=1e-7 * (np.max(np.abs(r["g0"])) + 1.0),
+                                   err_msg=what)
+    # the last pass, stage by stage, at the last solve's starting point
+    x_in = g_tr[-1]["x_in"]
+    for which, leaf, mp in ((0, 0.1, mapE), (1, 0.2, mapS)):
+        gpu = odo.correspondences(which)
+        src = synth.to_xyzi(e_ref if which == 0 else s_ref)
+        vox = oracle_lib.voxel_grid(src, leaf, stable=True)
+        q = gpu["queries"]
+        assert q.shape == vox.shape
+        for f in ("x", "y", "z", "intensity"):
+            np.testing.assert_array_equal(q[f], vox[f], err_msg=f"{config} downsampled {which}.{f}")
+        ref_pass = oracle_lib.stage_correspondences(mp, vox, x_in, edge=which == 0)
+        n_acc, n_tied = _compare_pass(gpu, ref_pass, which == 0, f"{config} set {which}", mp,
+                                      oracle_lib.associate_to_map(vox, x_in))
+        assert n_acc == (g_tr[-1]["n_edge_corr"] if which == 0 else g_tr[-1]["n_surf_corr"])
+    # the last solve on the GPU's own records, restated by the oracle
+    ge, gs = odo.correspondences(0), odo.correspondences(1)
+    erec = ge["records"][(ge["flags"] & 1) != 0]
+    srec = gs["records"][(gs["flags"] & 1) != 0]
+    x_out, tr = oracle_lib.stage_solve(erec, srec, x_in)
+    assert tr["iterations"] == g_tr[-1]["iterations"]
+    np.testing.assert_allclose(g_tr[-1]["x_out"], x_out, rtol=0, atol=1e-9)
+
+
+def test_find_correspondences_explicit_pose(floam_gpu, oracle_lib, prefilled_map):
+    """floam_odom_find_correspondences: one pass at a given pose, no solve (C3 map, scan 2 features)."""
+    R = 64
+    mapE, mapS = prefilled_map("c3")
+    raw = synth.generate_scan("c3", 2)
+    e, s, _ = oracle_lib.feature_extraction(raw, R, MIN_DIS, MAX_DIS, canonical=True)
+    T = synth.gt_pose_matrix(2)
+    c, s_ = T[0, 0], T[1, 0]
+    yaw = np.arctan2(s_, c)
+    q = np.array([0.0, 0.0, np.sin(yaw / 2), np.cos(yaw / 2)])
+    t = T[:3, 3]
+    odo = floam_gpu.OdomEstimationClass()
+    odo.init(_params(R), 0.1, "Cauchy")
+    odo.set_trace(8)
+    odo.initMapWithPoints(floam_gpu.DeviceCloud(mapE), floam_gpu.DeviceCloud(mapS))
+    odo.find_correspondences(floam_gpu.DeviceCloud(e), floam_gpu.DeviceCloud(s), q, t)
+    x = np.r_[q, t]
+    for which, leaf, mp, src in ((0, 0.1, mapE, e), (1, 0.2, mapS, s)):
+        gpu = odo.correspondences(which)
+        vox = oracle_lib.voxel_grid(synth.to_xyzi(src), leaf, stable=True)
+        ref = oracle_lib.stage_correspondences(mp, vox, x, edge=which == 0)
+        _compare_pass(gpu, ref, which == 0, f"explicit pose set {which}", mp, oracle_lib.associate_to_map(vox, x))
+
+
+def test_knn_ties(floam_gpu, oracle_lib):
+    """Equal float distances.  (1) Every map point duplicated: distances agree, and the records are bit-identical
+    even where the indices differ (duplicates have the same coordinates).  (2) Queries at the centres of a 0.5-m
+    lattice's cubes: the 8 corners are exactly equidistant (sqd 0.1875), so 3 of 8 tied points are dropped; the GPU
+    keeps the 5 lowest map indices — (sqd, index) order — while FLANN keeps its traversal order."""
+    from floam_amd.odom_estimation import reset_process_state
+    reset_process_state()
+    R = 16
+    raw = synth.generate_scan("c1", 0)
+    e0, s0, _ = oracle_lib.feature_extraction(raw, R, MIN_DIS, MAX_DIS, canonical=True)
+    mapE = np.concatenate([synth.to_xyzi(e0)] * 2)
+    mapS = np.concatenate([synth.to_xyzi(s0)] * 2)
+    e1, s1, _ = oracle_lib.feature_extraction(synth.generate_scan("c1", 1), R, MIN_DIS, MAX_DIS, canonical=True)
+    odo = floam_gpu.OdomEstimationClass()
+    odo.init(_params(R), 0.1, "Cauchy")
+    odo.set_trace(8)
+    odo.initMapWithPoints(floam_gpu.DeviceCloud(mapE), floam_gpu.DeviceCloud(mapS))
+    x = np.array([0.0, 0.0, 0.0, 1.0, 0.05, 0.0, 0.0])
+    odo.find_correspondences(floam_gpu.DeviceCloud(e1), floam_gpu.DeviceCloud(s1), x[:4], x[4:])
+    for which, leaf, mp, src in ((0, 0.1, mapE, e1), (1, 0.2, mapS, s1)):
+        gpu = odo.correspondences(which)
+        vox = oracle_lib.voxel_grid(synth.to_xyzi(src), leaf, stable=True)
+        ref = oracle_lib.stage_correspondences(mp, vox, x, edge=which == 0)
+        gated = np.nonzero(ref["flags"] & 4)[0]
+        np.testing.assert_array_equal(gpu["flags"] & 5, ref["flags"] & 5)
+        np.testing.assert_array_equal(gpu["sqd"][gated], ref["sqd"][gated])
+        n = mp.shape[0] // 2
+        # the GPU takes the lower copy of every tied duplicate pair first
+        gi = gpu["idx"][gated]
+        assert np.all((gi[:, 0] < n)), "lowest index first"
+        acc = gated[(ref["flags"][gated] & 1) != 0]
+        np.testing.assert_array_equal(gpu["records"][acc], ref["records"][acc])
+    # (2) a lattice: 8 equidistant corners around each query
+    g = np.arange(-4, 4) * 0.5
+    X, Y, Z = np.meshgrid(g, g, g, indexing="ij")
+    lat = np.zeros(X.size, synth.POINT_DTYPE)
+    lat["x"], lat["y"], lat["z"] = X.ravel() + 10.0, Y.ravel(), Z.ravel()
+    lat["pad0"] = 1.0
+    rng = np.random.default_rng(3)
+    lat = lat[rng.permutation(lat.size)]          # map order unrelated to the geometry
+    c = (np.arange(-3, 3) * 0.5 + 0.25)
+    QX, QY, QZ = np.meshgrid(c, c, c, indexing="ij")
+    qs = np.zeros(QX.size, synth.POINT_DTYPE)
+    qs["x"], qs["y"], qs["z"] = QX.ravel() + 10.0, QY.ravel(), QZ.ravel()
+    qs["pad0"] = 1.0
+    odo2 = floam_gpu.OdomEstimationClass()
+    odo2.init(_params(R), 0.1, "Cauchy")
+    odo2.set_trace(8)
+    odo2.initMapWithPoints(floam_gpu.DeviceCloud(lat), floam_gpu.DeviceCloud(lat))
+    ident = np.array([0.0, 0.0, 0.0, 1.0]), np.zeros(3)
+    odo2.find_correspondences(floam_gpu.DeviceCloud(qs), floam_gpu.DeviceCloud(qs), *ident)
+    gpu = odo2.correspondences(1)
+    vox = oracle_lib.voxel_grid(qs, 0.2, stable=True)
+    ref = oracle_lib.stage_correspondences(lat, vox, np.r_[ident[0], ident[1]], edge=False)
+    gated = np.nonzero(ref["flags"] & 4)[0]
+    assert gated.size == vox.shape[0]
+    np.testing.assert_array_equal(gpu["sqd"][gated], ref["sqd"][gated])
+    assert np.all(gpu["sqd"][gated] == np.float32(0.1875))
+    # the GPU's rule: the 5 lowest map indices among the 8 tied corners (brute force, float distances)
+    for i in gated:
+        qx, qy, qz = np.float32(vox["x"][i]), np.float32(vox["y"][i]), np.float32(vox["z"][i])
+        dx, dy, dz = qx - lat["x"], qy - lat["y"], qz - lat["z"]
+        d = ((np.float32(0) + dx * dx) + dy * dy) + dz * dz
+        order = np.lexsort((np.arange(lat.size), d))[:5]
+        np.testing.assert_array_equal(gpu["idx"][i], order)
+    differs = np.sum(np.any(np.sort(gpu["idx"][gated], 1) != np.sort(ref["idx"][gated], 1), axis=1))
+    print(f"lattice: {gated.size} queries with an 8-way tie, FLANN kept a different 5 of 8 on {differs}")
