@@ -5,23 +5,28 @@ One step = one scan through the reference's two operators, exactly as the nodes 
 LaserProcessingClass::featureExtraction (src/laserProcessingNode.cpp:129) followed by
 OdomEstimationClass::UpdatePointsToMapSelector(edge, surf, deskew=true) (src/odomEstimationNode.cpp:228), with the
 launch-file defaults (launch/structor_odom.launch: map_resolution 0.1, deskew on, loss "Cauchy" -> no robust
-loss, min/max_dis 0.5/90).  The raw scans are resident in HBM before the timed region; the host reads the pose
-back after every update call like the node does.
+loss, min/max_dis 0.5/90).  The raw scans are resident in HBM before the timed region; the host collects every
+update's pose (streamed, two updates in flight).
 
-Workload (BASELINE.json configs[2], the headline): 64-ring HDL-64-style synthetic scans (~130k points), local map
-prefilled with 200k edge+surf points through initMapWithPoints, steady state (the warm-up covers the
+Workload at N = 1 (BASELINE.json configs[2], the headline): 64-ring HDL-64-style synthetic scans (~130k points),
+local map prefilled with 200k edge+surf points through initMapWithPoints, steady state (the warm-up covers the
 optimization_count 12 -> 2 ramp).
 
---gpus N > 1 (launched by torch.distributed.run), default --mode replica: every rank runs its own odometry
-pipeline (one per sensor, no collective on the data path) over a copy of the same synthetic sequence; value = scans
-of all ranks per second (weak scaling).  --mode shard is the north star's partition of ONE sequence (SURVEY.md §8 e): every rank runs the same
-sequence, shards the correspondence queries and sums the normal equations with one RCCL all-reduce per LM
-evaluation; value = scans of the one sequence per second (strong scaling).  At C3 a scan is ~0.7 ms of
-latency-bound launches, so the ~20 all-reduces per scan cost more than the sharded work saves.
+--gpus N > 1 (launched by torch.distributed.run) defaults to --mode shard on C4 (BASELINE.json configs[3]: 128-ring
+~260k-point scans, 500k map, points sharded over the GPUs with an RCCL all-reduce of J^T J): every rank runs the same
+sequence, the correspondence queries are split into N ranges, and the normal equations are summed with one RCCL
+all-reduce per LM evaluation (SURVEY.md §8 e); value = scans of the one sequence per second (strong scaling).  Rank
+0 also times the same sequence unsharded on its own GPU first ("same_config_1gpu").  --mode replica runs one
+independent pipeline per GPU (value = scans of all ranks per second, weak scaling).
 
-Prints ONE JSON line on rank 0 (contract in the task statement), with "roofline" for the dominant kernel
-(the surf correspondence kernel, HIP events on the library stream over the timed region) and "cpu_baseline"
-(the CPU oracle — the reference path restated, single-threaded — timed on this host on a bounded sample).
+Prints ONE JSON line on rank 0 (contract in the task statement) with
+  "roofline": the kNN search kernel (knn_kernel, edge + surf queries in one launch): algorithmic bytes (device-counted,
+              SURVEY.md §8 d) / its average launch time from HIP events on the library stream, measured on an
+              identical replay of the timed sequence; "traffic" = rocprofv3 FETCH/WRITE bytes per launch of the same
+              kernel and config from the committed profiles/<tag>/hbm_traffic.json;
+  "cpu_baseline": the CPU oracle (the reference path restated, single-threaded) on a bounded sample of the sequence;
+  "secondary": featureExtraction alone (scans/s) and the same sequence with loss "huber" (SURVEY.md §8 d: "a second
+              run uses loss=huber").
 """
 from __future__ import annotations
 
@@ -49,14 +54,16 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def hbm_traffic(kernel_substr):
-    """HBM bytes per launch of the dominant kernel from the newest committed rocprofv3 PMC summary
-    (profiles/<tag>/hbm_traffic.json, written by tools/prof_summary.py from separate --pmc FETCH_SIZE / WRITE_SIZE
-    runs of this bench).  (None, None) when no profile is committed."""
+def hbm_traffic(kernel_substr, config):
+    """HBM bytes per launch of the roofline kernel from the newest committed rocprofv3 PMC summary of the SAME
+    config (profiles/<tag>/hbm_traffic.json, tools/prof_summary.py, separate --pmc FETCH_SIZE / WRITE_SIZE runs of
+    this bench; summaries without a config field are C3 runs).  (None, None) when none is committed."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "hbm_traffic.json")))
     for f in reversed(files):
         d = json.load(open(f))
+        if d.get("config", "c3") != config:
+            continue
         for name, v in d.get("kernels", {}).items():
             if kernel_substr in name:
                 return round(v["total_bytes"]), os.path.relpath(f, ROOT)
@@ -68,10 +75,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--warmup", type=int, default=8)
-    ap.add_argument("--config", default="c3")
-    ap.add_argument("--mode", choices=["shard", "replica"], default="replica")
+    ap.add_argument("--config", default=None, help="c1..c5 (default: c3 at N = 1, c4 for the sharded N > 1 run)")
+    ap.add_argument("--mode", choices=["shard", "replica"], default=None, help="N > 1 only (default shard)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--json-out", default="")
     args = ap.parse_args()
 
@@ -82,6 +90,8 @@ def main():
     if world > 1:
         import torch.distributed as dist   # control plane only (barrier, id broadcast, max-time); data: RCCL
         dist.init_process_group(backend="gloo")
+    mode = (args.mode or "shard") if world > 1 else "single"
+    cfg = args.config or ("c4" if mode == "shard" else "c3")
 
     import floam_amd
     import oracle
@@ -90,17 +100,16 @@ def main():
 
     L = _ffi.load()
     dev = int(os.environ.get("FLOAM_BENCH_DEVICE", local_rank))   # override: several ranks on one GPU (testing)
-    cfg = args.config
     model = synth.lidar_model(cfg)
     R = model.rings
     target = synth.MAP_PREFILL.get(cfg, 0)
+    params = floam_amd.LidarParams(num_lines=R, scan_period=SCAN_PERIOD, vertical_angle=2.0, max_distance=MAX_DIS,
+                                   min_distance=MIN_DIS)
 
     def oracle_fe(raw, R_):   # the CPU baseline leg only
         e, s, _ = oracle.feature_extraction(raw, R_, MIN_DIS, MAX_DIS, canonical=True)
         return e, s
 
-    params = floam_amd.LidarParams(num_lines=R, scan_period=SCAN_PERIOD, vertical_angle=2.0, max_distance=MAX_DIS,
-                                   min_distance=MIN_DIS)
     fe_lp = floam_amd.LaserProcessingClass(device=dev)
     fe_lp.init(params)
 
@@ -111,10 +120,9 @@ def main():
 
     t0 = time.time()
     n_scans = args.warmup + args.steps
-    # replica ranks run independent pipelines over the same synthetic sequence (same work per rank as at N = 1;
-    # a sequence that starts elsewhere on the trajectory would not match the map prefilled around the origin)
-    scan_offset = 0
-    raws = [synth.generate_scan(cfg, scan_offset + k) for k in range(1, n_scans + 1)]
+    # every rank runs the same synthetic sequence (replicas: same work per rank as at N = 1; a sequence that starts
+    # elsewhere on the trajectory would not match the map prefilled around the origin)
+    raws = [synth.generate_scan(cfg, k) for k in range(1, n_scans + 1)]
     mapE, mapS = synth.prefill_map(cfg, gpu_fe, target)
     fe_lp.close()
     log(f"[rank {rank}] generated {n_scans} scans ({raws[0].shape[0]} pts) + map {mapE.shape[0]}+{mapS.shape[0]} "
@@ -124,19 +132,19 @@ def main():
     d_mapE, d_mapS = floam_amd.DeviceCloud(mapE, device=dev), floam_amd.DeviceCloud(mapS, device=dev)
     allreduce_impl = None
     uid = None
-    if world > 1 and args.mode == "shard":
+    if mode == "shard":
         uid = [(comm_unique_id(), comm_unique_id()) if rank == 0 else None]   # timed run, byte-count replay
         dist.broadcast_object_list(uid, src=0)
     n_pipelines = 0
 
-    def make_pipeline():
+    def make_pipeline(loss=LOSS, sharded=True):
         nonlocal allreduce_impl, n_pipelines
         reset_process_state()
-        lp = floam_amd.LaserProcessingClass(device=dev, asynchronous=True)   # one sync per scan (the pose read)
+        lp = floam_amd.LaserProcessingClass(device=dev, asynchronous=True)   # the odometry collects the counts
         lp.init(params)
         odo = floam_amd.OdomEstimationClass(device=dev)
-        odo.init(params, MAP_RES, LOSS)
-        if uid is not None:
+        odo.init(params, MAP_RES, loss)
+        if uid is not None and sharded:
             try:
                 odo.set_shard(rank, world, uid[0][n_pipelines])   # RCCL over xGMI
                 allreduce_impl = "rccl"
@@ -149,14 +157,13 @@ def main():
                     dist.all_reduce(t, op=dist.ReduceOp.SUM)
                 odo.set_shard_callback(rank, world, _allreduce)
                 allreduce_impl = "gloo-host"
+            n_pipelines += 1
         odo.initMapWithPoints(d_mapE, d_mapS)
         odo.set_async(DEPTH)
-        n_pipelines += 1
         return lp, odo
 
-    lp, odo = make_pipeline()
-    # two feature buffers: the extraction of scan k+1 (its own stream) is issued before the odometry of scan k, so
-    # the two overlap on the device, as the reference's laserProcessingNode runs beside odomEstimationNode
+    # feature buffers: the extraction of scan k+1 (its own stream) is issued before the odometry of scan k, so the
+    # two overlap on the device, as the reference's laserProcessingNode runs beside odomEstimationNode
     bufs = [(floam_amd.DeviceCloud(device=dev), floam_amd.DeviceCloud(device=dev)) for _ in range(max(2, DEPTH))]
 
     def extract(lp, k):
@@ -189,6 +196,24 @@ def main():
             dist.barrier()
         _ffi.check(L.floam_device_synchronize(dev))
 
+    def timed_sequence(loss=LOSS, sharded=True):
+        lp, odo = make_pipeline(loss, sharded)
+        poses = []
+        run(lp, odo, 0, args.warmup, poses)
+        _ffi.check(L.floam_device_synchronize(dev))
+        t_start = time.perf_counter()
+        run(lp, odo, args.warmup, n_scans, poses)
+        _ffi.check(L.floam_device_synchronize(dev))
+        dt = time.perf_counter() - t_start
+        odo.close()
+        lp.close()
+        return dt, poses
+
+    same_cfg_1gpu = None
+    if mode == "shard" and rank == 0:   # the same sequence unsharded on this GPU: the strong-scaling reference
+        dt1, _ = timed_sequence(sharded=False)
+        same_cfg_1gpu = round(args.steps / dt1, 3)
+    lp, odo = make_pipeline()
     poses = []
     run(lp, odo, 0, args.warmup, poses)
     barrier_sync()
@@ -200,7 +225,6 @@ def main():
     if os.environ.get("FLOAM_BENCH_HOST"):
         log(f"[host] per timed scan: issue {1e6 * host_split[0] / args.steps:.0f} us, "
             f"wait {1e6 * host_split[1] / args.steps:.0f} us")
-    _ffi.check(L.floam_profile_enable(dev, 0))
     if dist is not None:
         import torch
         t = torch.tensor([elapsed], dtype=torch.float64)
@@ -219,17 +243,16 @@ def main():
     if not args.no_roofline:
         odo.close()
         lp.close()
-        # The dominant kernel — the exact 5-NN search (knn_kernel, edge + surf queries in one launch) — measured on an
+        # The roofline kernel — the exact 5-NN search (knn_kernel, edge + surf queries in one launch) — measured on an
         # identical replay of the same sequence (the pipeline is deterministic; the poses are checked bit for bit):
         # HIP events on the library stream around every search launch (FLOAM_PROF_KNN_DETAIL) and the byte-counting
-        # kernel after each pass (FLOAM_PROF_KNN_BYTES, SURVEY.md §8 d).  Profiling issues the updates launch by
-        # launch: the timed run above replays each update as one hipGraph, and timing events recorded inside a graph
-        # cannot be read back on this ROCm (hipEventElapsedTime fails for them).
+        # kernel after each pass (FLOAM_PROF_KNN_BYTES, SURVEY.md §8 d).  The timed run above has no events and no
+        # byte counting inside it.
         lp, odo = make_pipeline()
         replay = []
         run(lp, odo, 0, args.warmup, replay)
         _ffi.check(L.floam_profile_reset(dev))
-        _ffi.check(L.floam_profile_enable(dev, 1 | 16 | 32))
+        _ffi.check(L.floam_profile_enable(dev, 1 | 2 | 16 | 32))
         run(lp, odo, args.warmup, n_scans, replay)
         _ffi.check(L.floam_profile_enable(dev, 0))
         timed = read_timings()
@@ -239,16 +262,39 @@ def main():
             avg_ms = kt[1] / kt[0]
             bytes_per = kt[2] / kt[0]
             ach = bytes_per / (avg_ms * 1e-3) / 1e9
-            traffic, traffic_src = hbm_traffic("knn_kernel<")
+            traffic, traffic_src = hbm_traffic("knn_kernel<", cfg)
             roof = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": traffic_src,
                     "kernel": "knn_kernel (exact 5-NN search over the hash grid, edge + surf queries)",
                     "avg_us": round(avg_ms * 1e3, 2), "launches": int(kt[0]),
                     "algorithmic_bytes_per_launch": round(bytes_per), "replay_bitwise_identical": bool(same)}
-            for sub in ("knn", "knn_geometry"):
+            for sub, key in (("knn", "correspondence_pass_avg_us"), ("knn_geometry", "knn_geometry_avg_us"),
+                             ("lm_solve", "lm_solve_avg_us"), ("lm_solve_sharded", "lm_solve_avg_us")):
                 ks = timed.get(sub)
                 if ks is not None and ks[0]:
-                    roof[("correspondence_pass" if sub == "knn" else sub) + "_avg_us"] = round(ks[1] / ks[0] * 1e3, 2)
+                    roof[key] = round(ks[1] / ks[0] * 1e3, 2)
+
+    secondary = None
+    if rank == 0 and world == 1 and not args.no_secondary:
+        odo.close()
+        lp.close()
+        # featureExtraction alone over the timed scans (its own stream, no odometry behind it)
+        fe = floam_amd.LaserProcessingClass(device=dev, asynchronous=True)
+        fe.init(params)
+        for k in range(args.warmup):
+            extract(fe, k)
+        _ffi.check(L.floam_device_synchronize(dev))
+        t1 = time.perf_counter()
+        for k in range(args.warmup, n_scans):
+            extract(fe, k)
+        _ffi.check(L.floam_device_synchronize(dev))
+        fe_dt = time.perf_counter() - t1
+        fe.close()
+        # the same sequence with loss "huber" (HuberLoss(0.1), src/odomEstimationClass.cpp:84-87)
+        hub_dt, hub_poses = timed_sequence("huber")
+        secondary = {"feature_extraction_alone": {"value": round(args.steps / fe_dt, 2), "unit": "scans/s"},
+                     "huber": {"value": round(args.steps / hub_dt, 3), "unit": "scans/s",
+                               "loss": "huber (HuberLoss(0.1))"}}
 
     cpu = None
     pose_err = None
@@ -283,26 +329,33 @@ def main():
     if rank == 0:
         gt_err = []
         for k, (q, t) in enumerate(poses):
-            T = synth.gt_pose_matrix(scan_offset + k + 1)
+            T = synth.gt_pose_matrix(k + 1)
             gt_err.append(float(np.linalg.norm(T[:3, 3] - t)))
-        total_scans = args.steps * (world if args.mode == "replica" else 1)
+        total_scans = args.steps * (world if mode == "replica" else 1)
         value = total_scans / elapsed
+        if mode == "shard":
+            par = f"query-shard x{world} ({allreduce_impl} all-reduce of J^T J per LM evaluation)"
+        else:
+            par = f"replica x{world}" if world > 1 else "single GPU"
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "scans/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,
-            "scaling": "weak" if args.mode == "replica" else "strong", "vs_baseline": None, "dtype": "fp32+fp64",
+            "scaling": "strong" if mode == "shard" else "weak", "vs_baseline": None, "dtype": "fp32+fp64",
             "data": "synthetic (seeded ring-lidar ray-cast scene, floam_amd/synth.py)",
             "config": {"workload": f"{cfg}: {R}-ring synthetic scans ({raws[0].shape[0]} pts), map prefilled "
                                    f"{target} pts, deskew on, loss {LOSS} (no robust loss, Q3), map_res {MAP_RES}",
                        "rings": R, "points_per_scan": int(raws[0].shape[0]), "map_prefill": target,
-                       "parallelism": (f"query-shard x{world} ({allreduce_impl or 'no'} all-reduce of J^T J)"
-                                       if args.mode == "shard" else f"replica x{world}")},
+                       "parallelism": par},
             "roofline": roof,
             "cpu_baseline": cpu,
             "pose_vs_oracle": pose_err,
             "pose_vs_ground_truth_rmse_m": round(math.sqrt(sum(e * e for e in gt_err) / len(gt_err)), 5),
+            "secondary": secondary,
             "last_scan_stats": {k: (int(v) if isinstance(v, int) else v) for k, v in stats.items()},
         }
+        if same_cfg_1gpu is not None:
+            out["same_config_1gpu"] = {"value": same_cfg_1gpu, "unit": "scans/s",
+                                       "note": f"{cfg} unsharded on rank 0's GPU before the sharded run"}
         line = json.dumps(out)
         print(line, flush=True)
         if args.json_out:

@@ -48,6 +48,7 @@ EXPORTS = [
     "floam_pointcloud2_fields", "floam_cloud_from_pointcloud2", "floam_transform_cloud",
     "floam_mapping_create", "floam_mapping_destroy", "floam_mapping_update", "floam_mapping_get_map",
     "floam_mapping_size",
+    "floam_save_pcd", "floam_save_odom", "floam_save_posegraph", "floam_save_poses_balm", "floam_save_merged",
 ]
 
 
@@ -137,6 +138,11 @@ def load(path: str | None = None):
         "floam_transform_cloud": [vp, dp, vp],
         "floam_mapping_create": [dbl, i32, pp], "floam_mapping_destroy": [vp], "floam_mapping_update": [vp, vp, dp, dp],
         "floam_mapping_get_map": [vp, vp], "floam_mapping_size": [vp, szp],
+        "floam_save_pcd": [C.c_char_p, vp, sz],
+        "floam_save_odom": [C.c_char_p, dp, dp, C.POINTER(C.c_void_p), szp, sz],
+        "floam_save_posegraph": [C.c_char_p, dp, dp, C.POINTER(C.c_void_p), szp, sz],
+        "floam_save_poses_balm": [C.c_char_p, dp, dp, C.POINTER(C.c_void_p), szp, sz],
+        "floam_save_merged": [C.c_char_p, dp, C.POINTER(C.c_void_p), szp, sz, dbl, i32],
     }
     for name, args in sig.items():
         f = getattr(L, name)

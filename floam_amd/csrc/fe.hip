@@ -1,21 +1,22 @@
 // Feature extraction on gfx950: LaserProcessingClass::featureExtraction (src/laserProcessingClass.cpp:72-231).
 //
 // Kernels (one scan, P points, R rings):
-//   fe_keys    grid over P     range filter + ring key + per-ring histogram            reads 32 B/pt
-//   fe_bucket  one WG / ring   stable bucketing by ring (order-preserving scan)       ring-major float4 xyz + index
-//   fe_sector  one WG / sector curvature stencil, LDS bitonic sort, greedy edge pick, surf compaction
-//   fe_output  one WG / sector gather the 32-B records of edges / surfs to their ring-major, sector-major slots
+//   fe_keys     grid over P     range filter + ring key + per-ring histogram + the radix digit histograms
+//   radix_pass  grid over P     stable bucketing by ring: ONE digit pass of the onesweep radix sort (radix.hip) for
+//                               R <= 255 rings (two for more), O(P); the ring-ordered input indices
+//   fe_sector   one WG / sector curvature stencil, LDS bitonic sort, greedy edge pick, surf compaction
+//   fe_output   one WG / sector gather the 32-B records of edges / surfs to their ring-major, sector-major slots
 // Arithmetic follows the reference bit for bit: float stencil sums in source order, double squares, no FMA
 // contraction (built with -ffp-contract=off).  Sorting is by (value, ring index), which equals the reference's
 // unstable std::sort whenever a sector has no tied curvature values (SURVEY.md §7 "Hard parts").
 #include "floam_common.hpp"
 #include "fe.hpp"
+#include "radix.hpp"
 
 namespace floam {
 
 namespace {
 
-constexpr int kBucketThreads = 1024;
 constexpr int kSectorThreads = 256;
 constexpr int kMaxEdgesPerSector = 20;
 
@@ -28,15 +29,16 @@ __device__ __forceinline__ PointRec make_out(const PointRec& p) {
   return o;
 }
 
-// RingExtractionVelodyne (src/laserProcessingClass.cpp:11-22): float x*x+y*y, float sqrt, double compare.
+// RingExtractionVelodyne (src/laserProcessingClass.cpp:11-22): float x*x+y*y, float sqrt, double compare.  Keys for
+// the stable bucketing sort: the ring, or 0xFFFF for a dropped point (sorted after every ring); values: the index.
 __global__ void fe_keys(const PointRec* __restrict__ in, int n, int num_lines, double min_d, double max_d,
-                        uint16_t* __restrict__ keys, int n_keys_padded, int* __restrict__ ring_count,
-                        int* __restrict__ status) {
+                        uint32_t* __restrict__ keys, int* __restrict__ vals, int* __restrict__ ring_count,
+                        int* __restrict__ status, unsigned* __restrict__ radix_ctl) {
   extern __shared__ int hist[];
+  __shared__ unsigned s_rhist[kRadixHistWords];
   for (int r = threadIdx.x; r < num_lines; r += blockDim.x) hist[r] = 0;
-  __syncthreads();
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) {
+  radix_hist_begin(s_rhist);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const float2 xy = *reinterpret_cast<const float2*>(&in[i].x);
     const uint16_t ring = in[i].ring;
     const float d2 = xy.x * xy.x + xy.y * xy.y;
@@ -46,11 +48,13 @@ __global__ void fe_keys(const PointRec* __restrict__ in, int n, int num_lines, d
       atomicOr(status, FE_STATUS_BAD_RING);
       keep = false;
     }
-    keys[i] = keep ? ring : (uint16_t)0xFFFF;
+    const uint32_t key = keep ? ring : 0xFFFFu;
+    keys[i] = key;
+    vals[i] = i;
+    radix_hist_add(s_rhist, key);
     if (keep) atomicAdd(&hist[ring], 1);
-  } else if (i < n_keys_padded) {
-    keys[i] = 0xFFFF;
   }
+  radix_hist_end(s_rhist, radix_ctl);
   __syncthreads();
   for (int r = threadIdx.x; r < num_lines; r += blockDim.x)
     if (hist[r]) atomicAdd(&ring_count[r], hist[r]);
@@ -90,52 +94,6 @@ __device__ __forceinline__ int ring_offset(const int* ring_count, int r) {
   return off;
 }
 
-// Stable ring bucketing: WG r scans the whole key array once to count, once to emit, in input order.
-__global__ __launch_bounds__(kBucketThreads) void fe_bucket(const PointRec* __restrict__ in, int n_padded,
-                                                            const uint16_t* __restrict__ keys,
-                                                            const int* __restrict__ ring_count,
-                                                            int* __restrict__ ring_idx, float4* __restrict__ ring_xyz) {
-  __shared__ int smem[33];
-  __shared__ int s_off;
-  const int r = blockIdx.x;
-  if (threadIdx.x == 0) s_off = ring_offset(ring_count, r);
-  __syncthreads();
-  const int off = s_off;
-  // contiguous segment of 8-key groups per thread
-  const int groups = n_padded >> 3;
-  const int per = (groups + blockDim.x - 1) / blockDim.x;
-  const int g0 = threadIdx.x * per;
-  const int g1 = min(groups, g0 + per);
-  const uint4* k4 = reinterpret_cast<const uint4*>(keys);
-  int c = 0;
-  for (int g = g0; g < g1; ++g) {
-    const uint4 v = k4[g];
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      c += ((w[h] & 0xFFFFu) == (uint32_t)r);
-      c += ((w[h] >> 16) == (uint32_t)r);
-    }
-  }
-  int total;
-  int pos = off + block_exclusive_scan_1024(c, smem, &total);
-  for (int g = g0; g < g1; ++g) {
-    const uint4 v = k4[g];
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int h = 0; h < 8; ++h) {
-      const uint32_t key = (h & 1) ? (w[h >> 1] >> 16) : (w[h >> 1] & 0xFFFFu);
-      if (key == (uint32_t)r) {
-        const int i = g * 8 + h;
-        ring_idx[pos] = i;
-        const PointRec p = in[i];
-        ring_xyz[pos] = make_float4(p.x, p.y, p.z, 0.0f);
-        ++pos;
-      }
-    }
-  }
-}
-
 __device__ __forceinline__ void sector_range(int n_r, int s, int& a, int& b) {
   // src/laserProcessingClass.cpp:103-110: T = n - 10, L = T / 6, [L*s, L*(s+1) - 1), last: [5L, T - 1)
   const int T = n_r - 10;
@@ -148,7 +106,8 @@ __device__ __forceinline__ void sector_range(int n_r, int s, int& a, int& b) {
 // picks up the (rare) longer sectors, so the common case keeps several workgroups per CU.
 template <int MINSEC, int MAXSEC, bool LAST>
 __global__ __launch_bounds__(kSectorThreads) void fe_sector(const int* __restrict__ ring_count,
-                                                            const float4* __restrict__ ring_xyz,
+                                                            const PointRec* __restrict__ in,
+                                                            const int* __restrict__ ring_idx,
                                                             int* __restrict__ sec_edge_cnt, int* __restrict__ sec_edge_pos,
                                                             int* __restrict__ sec_surf_cnt, int* __restrict__ surf_pos,
                                                             int* __restrict__ status) {
@@ -186,8 +145,8 @@ __global__ __launch_bounds__(kSectorThreads) void fe_sector(const int* __restric
   const int off = s_off;
   // stage ring points [a, b + 10) (= ids a..b+9: stencils of entries a..b-1 and all suppression neighbours)
   const int npts = m + 10;
-  for (int k = threadIdx.x; k < npts; k += blockDim.x) {
-    const float4 p = ring_xyz[off + a + k];
+  for (int k = threadIdx.x; k < npts; k += blockDim.x) {   // gathered from the input by the ring-ordered index
+    const float4 p = *reinterpret_cast<const float4*>(&in[ring_idx[off + a + k]].x);
     s_x[k] = p.x; s_y[k] = p.y; s_z[k] = p.z;
     s_picked[k] = 0;
   }
@@ -333,7 +292,8 @@ __global__ __launch_bounds__(kSectorThreads) void fe_output(const PointRec* __re
 __global__ void fe_commit(int n_sectors, const int* __restrict__ sec_edge_cnt, const int* __restrict__ sec_surf_cnt,
                           int* __restrict__ edge_count, int* __restrict__ surf_count, int* __restrict__ ring_count,
                           int num_lines, int* __restrict__ status, int* __restrict__ out3,
-                          int* __restrict__ stat_edge, int* __restrict__ stat_surf) {
+                          int* __restrict__ stat_edge, int* __restrict__ stat_surf, unsigned* __restrict__ radix_ctl) {
+  radix_ctl_zero(radix_ctl, threadIdx.x, blockDim.x);   // the next call's bucketing sort (its histograms, epoch)
   __shared__ int red[2][4];
   int pe = 0, ps = 0;
   for (int k = threadIdx.x; k < n_sectors; k += blockDim.x) {
@@ -372,17 +332,18 @@ void fe_launch(FeScratch& sc, const FeParams& prm, const PointRec* d_in, int n, 
                int* edge_count, PointRec* surf_out, int* surf_count, hipStream_t st, int* stat_edge,
                int* stat_surf) {
   const int R = prm.num_lines;
-  const int n_pad = ((n + 8191) / 8192) * 8192;   // whole uint4 groups for every bucket thread
-  sc.keys.reserve(n_pad);
+  sc.keys.reserve(n);
+  sc.keys2.reserve(n);
+  sc.vals.reserve(n);
+  sc.ring_idx.reserve(n + 16);
   if (sc.ring_count.cap < (size_t)R) sc.zeroed = false;
   sc.ring_count.reserve(R);
   sc.out3.reserve(4);
-  sc.ring_idx.reserve(n + 16);
-  sc.ring_xyz.reserve(n + 16);
   sc.sec_edge_cnt.reserve(6 * R);
   sc.sec_surf_cnt.reserve(6 * R);
   sc.sec_edge_pos.reserve(6 * R * kMaxEdgesPerSector);
   sc.surf_pos.reserve(n + 16);
+  sc.rs.reserve(n, st);   // (a fresh control block is zeroed by the allocation)
   if (!sc.zeroed || sc.zeroed_lines < R) {   // fe_commit re-zeroes the counters at the end of every call
     FLOAM_HIP(hipMemsetAsync(sc.ring_count.p, 0, sizeof(int) * sc.ring_count.cap, st));
     FLOAM_HIP(hipMemsetAsync(sc.status, 0, sizeof(int), st));
@@ -390,23 +351,30 @@ void fe_launch(FeScratch& sc, const FeParams& prm, const PointRec* d_in, int n, 
     sc.zeroed_lines = R;
   }
   const int tb = 256;
-  hipLaunchKernelGGL(fe_keys, dim3(div_up(n_pad, tb)), dim3(tb), sizeof(int) * R, st, d_in, n, R, prm.min_distance,
-                     prm.max_distance, sc.keys.p, n_pad, sc.ring_count.p, sc.status);
+  hipLaunchKernelGGL(fe_keys, dim3(std::min(div_up(n, tb), 512u)), dim3(tb), sizeof(int) * R, st, d_in, n, R,
+                     prm.min_distance, prm.max_distance, sc.keys.p, sc.vals.p, sc.ring_count.p, sc.status, sc.rs.ctl.p);
   FLOAM_LAUNCH_CHECK();
-  hipLaunchKernelGGL(fe_bucket, dim3(R), dim3(kBucketThreads), 0, st, d_in, n_pad, sc.keys.p, sc.ring_count.p,
-                     sc.ring_idx.p, sc.ring_xyz.p);
-  FLOAM_LAUNCH_CHECK();
+  // stable bucketing by ring: rings < 255 differ in the low digit only (dropped points: 0xFFFF, last)
+  if (R <= 255) {
+    radix_pass_launch(sc.rs, sc.keys.p, sc.vals.p, sc.keys2.p, sc.ring_idx.p, n, 0, st);
+  } else {
+    radix_pass_launch(sc.rs, sc.keys.p, sc.vals.p, sc.keys2.p, sc.surf_pos.p, n, 0, st);
+    radix_pass_launch(sc.rs, sc.keys2.p, sc.surf_pos.p, sc.keys.p, sc.ring_idx.p, n, 1, st);
+  }
   // the longest possible sector is (max ring size - 10) / 6 <= n / 6: the 4096 pass is only needed beyond 1024
   const bool big = n / 6 + 8 > 1024;
   if (big) {
-    hipLaunchKernelGGL((fe_sector<0, 1024, false>), dim3(6 * R), dim3(kSectorThreads), 0, st, sc.ring_count.p,
-                       sc.ring_xyz.p, sc.sec_edge_cnt.p, sc.sec_edge_pos.p, sc.sec_surf_cnt.p, sc.surf_pos.p, sc.status);
+    hipLaunchKernelGGL((fe_sector<0, 1024, false>), dim3(6 * R), dim3(kSectorThreads), 0, st, sc.ring_count.p, d_in,
+                       sc.ring_idx.p, sc.sec_edge_cnt.p, sc.sec_edge_pos.p, sc.sec_surf_cnt.p, sc.surf_pos.p,
+                       sc.status);
     FLOAM_LAUNCH_CHECK();
     hipLaunchKernelGGL((fe_sector<1024, 4096, true>), dim3(6 * R), dim3(kSectorThreads), 0, st, sc.ring_count.p,
-                       sc.ring_xyz.p, sc.sec_edge_cnt.p, sc.sec_edge_pos.p, sc.sec_surf_cnt.p, sc.surf_pos.p, sc.status);
+                       d_in, sc.ring_idx.p, sc.sec_edge_cnt.p, sc.sec_edge_pos.p, sc.sec_surf_cnt.p, sc.surf_pos.p,
+                       sc.status);
   } else {
-    hipLaunchKernelGGL((fe_sector<0, 1024, true>), dim3(6 * R), dim3(kSectorThreads), 0, st, sc.ring_count.p,
-                       sc.ring_xyz.p, sc.sec_edge_cnt.p, sc.sec_edge_pos.p, sc.sec_surf_cnt.p, sc.surf_pos.p, sc.status);
+    hipLaunchKernelGGL((fe_sector<0, 1024, true>), dim3(6 * R), dim3(kSectorThreads), 0, st, sc.ring_count.p, d_in,
+                       sc.ring_idx.p, sc.sec_edge_cnt.p, sc.sec_edge_pos.p, sc.sec_surf_cnt.p, sc.surf_pos.p,
+                       sc.status);
   }
   FLOAM_LAUNCH_CHECK();
   hipLaunchKernelGGL(fe_output, dim3(6 * R), dim3(kSectorThreads), 0, st, d_in, sc.ring_count.p, sc.ring_idx.p,
@@ -414,7 +382,7 @@ void fe_launch(FeScratch& sc, const FeParams& prm, const PointRec* d_in, int n, 
                      surf_out, surf_count);
   FLOAM_LAUNCH_CHECK();
   hipLaunchKernelGGL(fe_commit, dim3(1), dim3(256), 0, st, 6 * R, sc.sec_edge_cnt.p, sc.sec_surf_cnt.p, edge_count,
-                     surf_count, sc.ring_count.p, R, sc.status, sc.out3.p, stat_edge, stat_surf);
+                     surf_count, sc.ring_count.p, R, sc.status, sc.out3.p, stat_edge, stat_surf, sc.rs.ctl.p);
   FLOAM_LAUNCH_CHECK();
 }
 

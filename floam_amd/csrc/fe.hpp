@@ -1,5 +1,6 @@
 #pragma once
 #include "floam_common.hpp"
+#include "radix.hpp"
 
 namespace floam {
 
@@ -11,9 +12,10 @@ struct FeParams {
 };
 
 struct FeScratch {
-  DevBuf<uint16_t> keys;
+  DevBuf<uint32_t> keys, keys2;   // ring keys of the bucketing sort (and its ping-pong buffer)
+  DevBuf<int> vals;               // input indices before the sort
+  RadixScratch rs;                // the sort's control block (this extraction's own: it runs on its own stream)
   DevBuf<int> ring_count, ring_idx, sec_edge_cnt, sec_surf_cnt, sec_edge_pos, surf_pos;
-  DevBuf<float4> ring_xyz;
   DevBuf<int> out3;        // edge count, surf count, status after the call (one D2H)
   int* status = nullptr;   // device int, owned by the caller
   bool zeroed = false;

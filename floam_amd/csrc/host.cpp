@@ -781,6 +781,10 @@ void odom_velocity(const floam_odom* o, double v[3]) {
 
 }  // namespace
 
+namespace floam {
+void set_last_error(const std::string& m) { t_err = m; }
+}  // namespace floam
+
 // ============================================================================================ C ABI
 extern "C" {
 

@@ -720,6 +720,10 @@ __device__ __forceinline__ bool sweep_granules(const unsigned long long* __restr
   return pending == 0;
 }
 
+// evaluation blocks that hold records: one record slot per thread while they fit, at most nblk (a function of the
+// device count only, so the partition and the reduction order never depend on the host's upper bounds)
+__device__ __forceinline__ int active_blocks(int total, int nblk) { return max(1, min(nblk, (total + kTB - 1) / kTB)); }
+
 struct LMArgs {
   LMState* st;
   const double* erec;
@@ -757,7 +761,9 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
     const unsigned ep = a.st->epoch;
     const int ne = min(*a.d_ne, a.ne_ub);
     const int total = ne + (GRAM ? 0 : min(*a.d_ns, a.ns_ub));
-    const int stride = nblk * kTB, i0 = blk * kTB + tid;
+    const int nact = active_blocks(total, nblk);
+    if (blk >= nact) return;   // no records: the control block does not wait for this one
+    const int stride = nact * kTB, i0 = blk * kTB + tid;
     // the thread's first record stays in registers across the evaluations
     R f0[9];
     bool has0 = false, edge0 = true;
@@ -815,11 +821,12 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
   __syncthreads();
   if (sst.done) return;   // (never after lm_reset; the evaluation blocks saw it too)
   const unsigned ep = sst.epoch;
+  const int nact = active_blocks(min(*a.d_ne, a.ne_ub) + (GRAM ? 0 : min(*a.d_ns, a.ns_ub)), nblk);
   if (GRAM) gram_unpack(gv, G, o);
   const int lane = tid & 63;
   LMState s;   // wave 0: the whole LM state in registers for the whole solve
   if (tid < 64) s = sst;
-  unsigned* tab = reinterpret_cast<unsigned*>(s_red);   // [nblk][2 * LM_NSUM] halves of the block partials
+  unsigned* tab = reinterpret_cast<unsigned*>(s_red);   // [nact][2 * LM_NSUM] halves of the block partials
   unsigned long long tm[4] = {0, 0, 0, 0};
   int failed_at = -1;   // evaluation whose partials never arrived (never expected)
   for (int it = 0; it < 5; ++it) {
@@ -831,8 +838,8 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
     // the evaluation blocks' partial granules of evaluation it: every thread keeps kSweep loads in flight per poll
     // round (one round trip per round, not one per granule)
     int bad = 0;
-    for (int j0 = tid; j0 < nblk * 2 * LM_NSUM; j0 += kSweep * kTB)
-      if (!sweep_granules(a.part, j0, nblk * 2 * LM_NSUM, ep + (unsigned)it, tab)) bad = 1;
+    for (int j0 = tid; j0 < nact * 2 * LM_NSUM; j0 += kSweep * kTB)
+      if (!sweep_granules(a.part, j0, nact * 2 * LM_NSUM, ep + (unsigned)it, tab)) bad = 1;
     if (__syncthreads_or(bad)) {
       failed_at = it;
       break;
@@ -841,7 +848,7 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
     reduce_blocks([&](int c, int b) {
       const int g = b * 2 * LM_NSUM + 2 * c;
       return __longlong_as_double((long long)(((unsigned long long)tab[g + 1] << 32) | tab[g]));
-    }, nblk, s_strip, s_sums);
+    }, nact, s_strip, s_sums);
     if (GRAM && tid < LM_NSUM) s_sums[tid] = s_sums[tid] + s_ssum[tid];   // edge + surf
     __syncthreads();
     const unsigned long long t3 = __builtin_amdgcn_s_memrealtime();
@@ -911,11 +918,12 @@ __global__ __launch_bounds__(kTB) void lm_shard_eval(LMArgs a, int k) {
   const bool done = s_done != 0;
   const int ne = min(*a.d_ne, a.ne_ub);
   const int total = ne + (GRAM ? 0 : min(*a.d_ns, a.ns_ub));
-  if (!done) {
+  const int nact = active_blocks(total, nblk);   // the resident solve's partition (bit-identical on one rank)
+  if (!done && blk < nact) {
     R x[7];
 #pragma unroll
     for (int q = 0; q < 7; ++q) x[q] = (R)s_pt[q];
-    const int stride = nblk * kTB, i0 = blk * kTB + tid;
+    const int stride = nact * kTB, i0 = blk * kTB + tid;
     R f0[9];
 #pragma unroll
     for (int q = 0; q < 9; ++q) f0[q] = R(0);
@@ -923,7 +931,7 @@ __global__ __launch_bounds__(kTB) void lm_shard_eval(LMArgs a, int k) {
     eval_records<HUBER, R>(x, false, true, f0, i0, stride, ne, total, a.erec, a.evalid, a.ecap, a.srec, a.svalid,
                            a.scap, acc);
     block_sums(acc, s_red, s_strip, s_sums);
-    if (tid < LM_NSUM) a.partials[tid * nblk + blk] = s_sums[tid];
+    if (tid < LM_NSUM) a.partials[tid * nact + blk] = s_sums[tid];
   }
   // arrival: producer stores -> vmcnt(0) -> barrier -> agent release -> ticket; the last block acquires
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -936,7 +944,7 @@ __global__ __launch_bounds__(kTB) void lm_shard_eval(LMArgs a, int k) {
   __syncthreads();
   if (!s_last) return;
   if (!done) {
-    reduce_blocks([&](int c, int b) { return a.partials[c * nblk + b]; }, nblk, s_strip, s_sums);
+    reduce_blocks([&](int c, int b) { return a.partials[c * nact + b]; }, nact, s_strip, s_sums);
     if (GRAM) {
       __shared__ double G[kGramW][kGramW];
       __shared__ double o[3];

@@ -178,6 +178,16 @@ void RadixScratch::reserve(int n, hipStream_t st) {
   }
 }
 
+void radix_pass_launch(RadixScratch& sc, const uint32_t* kin, const int* vin, uint32_t* kout, int* vout, int n,
+                       int pass, hipStream_t st) {
+  if (n <= 0) return;
+  sc.reserve(n, st);
+  const int tiles = (int)div_up((unsigned)n, (unsigned)kTile);
+  hipLaunchKernelGGL(radix_pass, dim3(tiles), dim3(kTB), 0, st, kin, vin, kout, vout, n, pass, sc.ctl.p,
+                     sc.status.p + (size_t)pass * sc.tiles_cap * kRadixDigits, nullptr, nullptr);
+  FLOAM_LAUNCH_CHECK();
+}
+
 void radix_sort_launch(RadixScratch& sc, uint32_t* k0, int* v0, uint32_t* k1, int* v1, int n, hipStream_t st,
                        const int* gate, const int* n_dev) {
   if (n <= 0) return;

@@ -59,4 +59,9 @@ __device__ __forceinline__ void radix_ctl_zero(unsigned* ctl, int t, int stride)
 void radix_sort_launch(RadixScratch& sc, uint32_t* k0, int* v0, uint32_t* k1, int* v1, int n, hipStream_t st,
                        const int* gate = nullptr, const int* n_dev = nullptr);
 
+// One digit pass (pass p sorts by bits [8p, 8p + 8)) of the same sort, for keys whose high digits are known to be
+// equal (e.g. the feature extraction's ring keys: one pass for <= 255 rings)
+void radix_pass_launch(RadixScratch& sc, const uint32_t* kin, const int* vin, uint32_t* kout, int* vout, int n,
+                       int pass, hipStream_t st);
+
 }  // namespace floam

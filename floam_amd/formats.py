@@ -219,18 +219,28 @@ def loadPCDFileBinary(path: str) -> np.ndarray:
 
 
 # ------------------------------------------------------------------------------------------- exporters
+# The exporters are the library's (floam_save_*, floam_amd/csrc/exporters.cpp): the same C entry points the C++
+# nodes call.  These wrappers take numpy clouds (POINT_DTYPE / 32-B XYZI records) and 4x4 pose matrices.
+def _cloud_args(clouds):
+    arrs = [np.ascontiguousarray(c).view(POINT_DTYPE) for c in clouds]
+    ptrs = (C.c_void_p * max(1, len(arrs)))(*[a.ctypes.data for a in arrs])
+    sizes = (C.c_size_t * max(1, len(arrs)))(*[a.shape[0] for a in arrs])
+    return arrs, ptrs, sizes
+
+
+def _poses_arg(poses):
+    P = np.ascontiguousarray(np.asarray(poses, dtype=np.float64).reshape(-1, 4, 4))
+    return P, P.ctypes.data_as(C.POINTER(C.c_double))
+
+
 def SaveOdom(dump_directory: str, poses: Sequence[np.ndarray], keyframe_stamps: Sequence[float],
              clouds: Sequence[np.ndarray]) -> None:
     """SaveOdom (src/utils.cpp:78-106): per keyframe <sec>_<nsec>.pcd and .odom (4x4 pose, rows of 4)."""
-    os.makedirs(dump_directory, exist_ok=True)
-    for i in range(len(clouds)):
-        sec, nsec = ros_time(keyframe_stamps[i])
-        base = os.path.join(dump_directory, f"{sec}_{nsec}")
-        savePCDFileBinary(base + ".pcd", clouds[i])
-        m = np.asarray(poses[i], dtype=np.float64)
-        with open(base + ".odom", "w") as fh:
-            for r in range(4):
-                fh.write(" ".join(_g(m[r, c]) for c in range(4)) + "\n")
+    arrs, ptrs, sizes = _cloud_args(clouds)
+    P, pp = _poses_arg(poses)
+    st = np.ascontiguousarray(keyframe_stamps, dtype=np.float64)
+    _ffi.check(_ffi.load().floam_save_odom(dump_directory.encode(), pp, st.ctypes.data_as(C.POINTER(C.c_double)),
+                                           ptrs, sizes, len(arrs)))
 
 
 def SavePosegraph(dump_directory: str, poses: Sequence[np.ndarray], keyframe_stamps: Sequence[float],
@@ -238,44 +248,22 @@ def SavePosegraph(dump_directory: str, poses: Sequence[np.ndarray], keyframe_sta
     """SavePosegraph (src/utils.cpp:3-75): graph.g2o (VERTEX_SE3:QUAT per pose, FIX 0, EDGE_SE3:QUAT between
     consecutive poses with the diagonal information 0.01 x3, 0.001 x3) and one directory per keyframe
     (cloud.pcd + data)."""
-    os.makedirs(dump_directory, exist_ok=True)
-    P = [np.asarray(p, dtype=np.float64) for p in poses]
-    with open(os.path.join(dump_directory, "graph.g2o"), "w") as g:
-        for count, T in enumerate(P):
-            q = _quat_from_matrix(T[:3, :3])
-            t = T[:3, 3]
-            g.write(f"VERTEX_SE3:QUAT {count} " + " ".join(_g(v) for v in (*t, *q)) + "\n")
-        g.write("FIX 0\n")
-        info = np.diag([0.01, 0.01, 0.01, 0.001, 0.001, 0.001])
-        for i in range(len(P) - 1):
-            rel = _affine_inverse(P[i]) @ P[i + 1]
-            q = _quat_from_matrix(rel[:3, :3])
-            t = rel[:3, 3]
-            line = f"EDGE_SE3:QUAT {i} {i + 1} " + " ".join(_g(v) for v in (*t, *q))
-            line += "".join(" " + _g(info[r, c]) for r in range(6) for c in range(r, 6))
-            g.write(line + "\n")
-    for i, cl in enumerate(clouds):
-        d = os.path.join(dump_directory, "%06d" % i)
-        os.makedirs(d, exist_ok=True)
-        savePCDFileBinary(os.path.join(d, "cloud.pcd"), cl)
-        sec, nsec = ros_time(keyframe_stamps[i])
-        with open(os.path.join(d, "data"), "w") as fh:
-            fh.write(f"stamp {sec} {nsec}\nestimate\n{eigen_str(P[i])}\nodom\n{eigen_str(P[i])}\n"
-                     f"accum_distance -1\nid {i}\n")
+    arrs, ptrs, sizes = _cloud_args(clouds)
+    P, pp = _poses_arg(poses)
+    st = np.ascontiguousarray(keyframe_stamps, dtype=np.float64)
+    _ffi.check(_ffi.load().floam_save_posegraph(dump_directory.encode(), pp,
+                                                st.ctypes.data_as(C.POINTER(C.c_double)), ptrs, sizes, len(arrs)))
 
 
 def SavePosesHomogeneousBALM(clouds: Sequence[np.ndarray], poses: Sequence[np.ndarray],
                              stamps: Sequence[float], directory: str) -> None:
     """SavePosesHomogeneousBALM (src/odomEstimationNode.cpp:97-117): alidarPose.csv (std::fixed rows of the 4x4
     pose, the stamp in place of element (3, 3)) and full<i>.pcd."""
-    os.makedirs(directory, exist_ok=True)
-    with open(os.path.join(directory, "alidarPose.csv"), "w") as fh:
-        for i, T in enumerate(poses):
-            m = np.asarray(T, dtype=np.float64)
-            rows = [list(m[r]) for r in range(3)] + [[m[3, 0], m[3, 1], m[3, 2], float(stamps[i])]]
-            for row in rows:
-                fh.write(",".join("%.6f" % v for v in row) + ",\n")
-            savePCDFileBinary(os.path.join(directory, f"full{i}.pcd"), clouds[i])
+    arrs, ptrs, sizes = _cloud_args(clouds)
+    P, pp = _poses_arg(poses)
+    st = np.ascontiguousarray(stamps, dtype=np.float64)
+    _ffi.check(_ffi.load().floam_save_poses_balm(directory.encode(), pp, st.ctypes.data_as(C.POINTER(C.c_double)),
+                                                 ptrs, sizes, len(arrs)))
 
 
 def SaveMerged(clouds: Sequence[np.ndarray], poses: Sequence[np.ndarray], directory: str, downsample_size: float,
@@ -283,16 +271,7 @@ def SaveMerged(clouds: Sequence[np.ndarray], poses: Sequence[np.ndarray], direct
     """SaveMerged (src/odomEstimationNode.cpp:66-96): every keyframe cloud transformed by its pose and concatenated
     (floam_merged.pcd), then VoxelGrid(downsample_size) (floam_merged_downsampled_leaf_<size>.pcd); the transforms
     and the voxel grid run on the device."""
-    os.makedirs(directory, exist_ok=True)
-    parts = []
-    d_in, d_out = DeviceCloud(device=device), DeviceCloud(device=device)
-    for cl, T in zip(clouds, poses):
-        d_in.upload(np.ascontiguousarray(cl).view(POINT_DTYPE))
-        transformPointCloud(d_in, d_out, T)
-        parts.append(d_out.download())
-    merged = np.concatenate(parts) if parts else np.zeros(0, POINT_DTYPE)
-    d_m = DeviceCloud(merged, device=device) if merged.shape[0] else DeviceCloud(device=device)
-    down = d_m.voxel_grid(float(downsample_size)).download() if merged.shape[0] else merged
-    savePCDFileBinary(directory + "floam_merged.pcd", merged)
-    if down.shape[0]:
-        savePCDFileBinary(directory + "floam_merged_downsampled_leaf_" + ("%f" % downsample_size) + ".pcd", down)
+    arrs, ptrs, sizes = _cloud_args(clouds)
+    P, pp = _poses_arg(poses)
+    _ffi.check(_ffi.load().floam_save_merged(directory.encode(), pp, ptrs, sizes, len(arrs), float(downsample_size),
+                                             int(device)))

@@ -167,6 +167,26 @@ floam_status floam_cloud_from_pointcloud2(floam_cloud* out, int point_type, cons
  * SaveMerged's per-keyframe transform (src/odomEstimationNode.cpp:72-76). */
 floam_status floam_transform_cloud(const floam_cloud* in, const double m[16], floam_cloud* out);
 
+/* Disk exporters of the odometry node (src/utils.cpp:3-106, src/odomEstimationNode.cpp:66-117), for the C++ nodes.
+ * poses: n row-major 4x4 Eigen::Affine3d matrices; clouds: n host arrays of pcl::PointXYZI-compatible 32-B records
+ * (cloud_sizes points each); stamps in seconds (ros::Time::toSec()).  Text is written through std::ostream exactly
+ * as the reference does; PCD files are pcl::io::savePCDFileBinary of pcl::PointXYZI (v0.7, x y z intensity). */
+floam_status floam_save_pcd(const char* path, const floam_point* points, size_t n);
+/* SaveOdom (src/utils.cpp:80-106): <dir>/<sec>_<nsec>.pcd and .odom per keyframe */
+floam_status floam_save_odom(const char* dump_directory, const double* poses, const double* keyframe_stamps,
+                             const floam_point* const* clouds, const size_t* cloud_sizes, size_t n);
+/* SavePosegraph (src/utils.cpp:3-75): graph.g2o + <dir>/%06d/{cloud.pcd, data} */
+floam_status floam_save_posegraph(const char* dump_directory, const double* poses, const double* keyframe_stamps,
+                                  const floam_point* const* clouds, const size_t* cloud_sizes, size_t n);
+/* SavePosesHomogeneousBALM (src/odomEstimationNode.cpp:97-117): <dir>alidarPose.csv + <dir>full<i>.pcd (the
+ * directory string is concatenated as the reference does: pass a trailing '/') */
+floam_status floam_save_poses_balm(const char* directory, const double* poses, const double* stamps,
+                                   const floam_point* const* clouds, const size_t* cloud_sizes, size_t n);
+/* SaveMerged (src/odomEstimationNode.cpp:66-96): every cloud transformed by its pose (on the device), concatenated to
+ * <dir>floam_merged.pcd, VoxelGrid(downsample_size) to <dir>floam_merged_downsampled_leaf_<size>.pcd */
+floam_status floam_save_merged(const char* directory, const double* poses, const floam_point* const* clouds,
+                               const size_t* cloud_sizes, size_t n, double downsample_size, int device);
+
 /* ------------------------------------------------------------------------------- LaserMappingClass */
 /* The mapping node's global map (src/laserMappingClass.cpp): 50-m cells of pcl::PointXYZI,
  * VoxelGrid(map_resolution) of the 5 x 5 x 5 cells around the pose after every update. */

@@ -50,6 +50,7 @@ def main():
     ap.add_argument("--last", type=int, default=240,
                     help="dispatches per kernel averaged for hbm_traffic.json (the timed tail; default = 60 scans x 4 "
                          "solves)")
+    ap.add_argument("--config", default="c3", help="bench config the profiled run used (bench.py keys traffic by it)")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles"))
     args = ap.parse_args()
     out = os.path.join(args.out, args.tag)
@@ -68,7 +69,7 @@ def main():
 
     traffic = {}
     lines = [f"# rocprofv3 summary — {args.tag}", "",
-             "Command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --cpu-baseline-seconds 0` (C3, 8 warm-up + "
+             f"Command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --cpu-baseline-seconds 0` ({args.config}, 8 warm-up + "
              "60 timed scans, then the same 68 scans replayed with per-launch events for the roofline; all dispatches of the run, map prefill included).  HBM bytes: separate "
              "`--pmc FETCH_SIZE` and `--pmc WRITE_SIZE` runs of the same command; FETCH_SIZE doubled (gfx950 16-B/lane "
              "read correction), KiB → bytes.", "",
@@ -90,7 +91,7 @@ def main():
     if bench:
         lines += ["", "## bench line of the same session (un-profiled run)", "", "```json", json.dumps(bench), "```"]
     open(os.path.join(out, "summary.md"), "w").write("\n".join(lines) + "\n")
-    json.dump({"source": f"profiles/{args.tag}", "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate runs; "
+    json.dump({"source": f"profiles/{args.tag}", "config": args.config, "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate runs; "
                f"FETCH_SIZE x2 (gfx950), KiB->B; average over the kernel's last {args.last} dispatches (timed tail)",
                "kernels": traffic},
               open(os.path.join(out, "hbm_traffic.json"), "w"), indent=1)
