@@ -681,7 +681,13 @@ __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArg
       stencil_scan<G, U, false>(A, qx - 1, qx + 1, qy - 1, qy + 1, qz - 1, qz + 1, wx, wy, wz, lane, s_pre, s_start,
                                 t, cnt, s_cc);
       group_merge<G>(t, cnt);
-      const bool complete = cnt >= 5 && __uint_as_float((unsigned)(t.k[4] >> 32)) < 0.25f;
+      // exact early exit: a map point outside the fine block [lo, hi) (lo = (f - 1) / 2, hi = (f + 2) / 2 per axis,
+      // exact in float) lies beyond a face, so on that axis |fl(q - p)| >= fl(q - lo) or fl(hi - q) (monotone
+      // rounding) and its float sq-distance is >= fl(b^2), b the query's smallest face distance (>= 0.5)
+      const float b = fminf(fminf(fminf(wx - 0.5f * (float)(qx - 1), 0.5f * (float)(qx + 2) - wx),
+                                  fminf(wy - 0.5f * (float)(qy - 1), 0.5f * (float)(qy + 2) - wy)),
+                            fminf(wz - 0.5f * (float)(qz - 1), 0.5f * (float)(qz + 2) - wz));
+      const bool complete = cnt >= 5 && __uint_as_float((unsigned)(t.k[4] >> 32)) < b * b;
       if (!complete) {   // coarse cells floor(q - 1) .. floor(q + 1) per axis (exact in double)
 #pragma unroll
         for (int k = 0; k < 5; ++k) t.k[k] = ~0ull;
