@@ -80,6 +80,9 @@ def main():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
+    ap.add_argument("--precision", choices=["fp64", "fp32", "fp32g"], default="fp64",
+                    help="residual / Jacobian precision (floam_odom_set_precision): fp64 = the reference's (default); "
+                         "fp32 = float residuals / Jacobians; fp32g = float line / plane fits too (C5 sweep)")
     ap.add_argument("--json-out", default="")
     args = ap.parse_args()
 
@@ -144,6 +147,8 @@ def main():
         lp.init(params)
         odo = floam_amd.OdomEstimationClass(device=dev)
         odo.init(params, MAP_RES, loss)
+        if args.precision != "fp64":
+            odo.set_precision(True, geometry=args.precision == "fp32g")
         if uid is not None and sharded:
             try:
                 odo.set_shard(rank, world, uid[0][n_pipelines])   # RCCL over xGMI
@@ -302,7 +307,7 @@ def main():
         # the reference path restated (oracle), single-threaded, same scans from scan 1 and the same prefilled
         # map; warm-up scans (optimization_count ramp) untimed, then steady-state scans for ~N seconds.
         oracle.reset_process_statics()
-        ref = oracle.Odometry(R, SCAN_PERIOD, MIN_DIS, MAX_DIS, MAP_RES, LOSS, stable_voxel=True)
+        ref = oracle.Odometry(R, SCAN_PERIOD, MIN_DIS, MAX_DIS, MAP_RES, LOSS, stable_voxel=True)   # fp64 always
         ref.init_map(mapE, mapS)
         t_cpu, n_cpu, errs = 0.0, 0, []
         for k in range(n_scans):
@@ -340,12 +345,13 @@ def main():
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "scans/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,
-            "scaling": "strong" if mode == "shard" else "weak", "vs_baseline": None, "dtype": "fp32+fp64",
+            "scaling": "strong" if mode == "shard" else "weak", "vs_baseline": None,
+            "dtype": "fp32+fp64" if args.precision == "fp64" else "fp32",
             "data": "synthetic (seeded ring-lidar ray-cast scene, floam_amd/synth.py)",
             "config": {"workload": f"{cfg}: {R}-ring synthetic scans ({raws[0].shape[0]} pts), map prefilled "
                                    f"{target} pts, deskew on, loss {LOSS} (no robust loss, Q3), map_res {MAP_RES}",
                        "rings": R, "points_per_scan": int(raws[0].shape[0]), "map_prefill": target,
-                       "parallelism": par},
+                       "parallelism": par, "precision": args.precision},
             "roofline": roof,
             "cpu_baseline": cpu,
             "pose_vs_oracle": pose_err,

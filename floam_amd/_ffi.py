@@ -70,7 +70,7 @@ class OdomStats(C.Structure):
                 ("surf_map", C.c_size_t), ("final_cost", C.c_double)]
 
 
-PRECISION_FP64, PRECISION_FP32 = 0, 1
+PRECISION_FP64, PRECISION_FP32, PRECISION_FP32_GEOMETRY = 0, 1, 2
 TRACE_WORDS = 49   # per-solve trace record (include/floam_c.h floam_odom_set_trace)
 
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.c_int, C.c_void_p)

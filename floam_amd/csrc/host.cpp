@@ -247,7 +247,8 @@ struct floam_odom {
   Grid gE, gS;
   bool grid_dirty = true;
   CorrSet ce, cs;
-  bool fp32 = false;                       // floam_odom_set_precision: fp32 geometry + residuals (C5 sweep)
+  bool fp32 = false;                       // floam_odom_set_precision: fp32 residuals / Jacobians (C5 sweep)
+  bool fp32_geom = false;                  // ... and fp32 line / plane fits (FLOAM_PRECISION_FP32_GEOMETRY)
   LMBuffers lmb;                           // the solves' scratch (lm.hip)
   DevBuf<unsigned long long> dbg_stamps;   // FLOAM_DEBUG_STAMPS=1: the resident solve's segment times (diagnostic)
   int qhint[2] = {0, 0};                   // recent downsampled edge / surf query counts (search grid sizing)
@@ -467,7 +468,7 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
                    o->mapS.count.p, o->rank, o->world, st);
       }
       ProfScope ps2(ctx, "knn_geometry", FLOAM_PROF_KNN_DETAIL);
-      geom_launch(o->lm.p, qe, o->ce, qs, o->cs, gram, o->fp32, o->lmb, st);
+      geom_launch(o->lm.p, qe, o->ce, qs, o->cs, gram, o->fp32_geom, o->lmb, st);
     }
     if (ctx.profile & FLOAM_PROF_KNN_BYTES) {   // replay only: algorithmic bytes of the two launches above
       knn_traffic_launch(o->lm.p, qe, o->gE, o->ce, o->rank, o->world, o->traffic_set, o->prof_bytes.p + 0, st);
@@ -1344,10 +1345,12 @@ floam_status floam_odom_set_shard_callback(floam_odom* o, int rank, int world, f
 
 floam_status floam_odom_set_precision(floam_odom* o, int precision) {
   return guarded([&] {
-    if (!o || (precision != FLOAM_PRECISION_FP64 && precision != FLOAM_PRECISION_FP32))
+    if (!o || (precision != FLOAM_PRECISION_FP64 && precision != FLOAM_PRECISION_FP32 &&
+               precision != FLOAM_PRECISION_FP32_GEOMETRY))
       throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null handle or unknown precision");
     odom_collect(o, ctx_for(o->device), 0);
-    o->fp32 = precision == FLOAM_PRECISION_FP32;
+    o->fp32 = precision != FLOAM_PRECISION_FP64;
+    o->fp32_geom = precision == FLOAM_PRECISION_FP32_GEOMETRY;
     return FLOAM_OK;
   });
 }
@@ -1422,7 +1425,7 @@ floam_status floam_odom_find_correspondences(floam_odom* o, const floam_cloud* e
     o->ce.trace = o->cs.trace = true;
     QuerySet qe{o->dE.p, o->cnt.p + 0, ne_ub}, qs{o->dS.p, o->cnt.p + 1, ns_ub};
     knn_launch(o->lm.p, o->kf_io.p, qe, o->gE, o->ce, qs, o->gS, o->cs, o->mapE.count.p, o->mapS.count.p, 0, 1, st);
-    geom_launch(o->lm.p, qe, o->ce, qs, o->cs, false, o->fp32, o->lmb, st);
+    geom_launch(o->lm.p, qe, o->ce, qs, o->cs, false, o->fp32_geom, o->lmb, st);
     o->last_q[0] = o->dE.p;
     o->last_q[1] = o->dS.p;
     o->last_qn = o->cnt.p;

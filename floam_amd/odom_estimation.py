@@ -157,10 +157,14 @@ class OdomEstimationClass:
                                                       tt.ctypes.data_as(C.POINTER(C.c_double)), C.byref(flag)))
         return bool(flag.value)
 
-    def set_precision(self, fp32: bool) -> None:
-        """fp32 geometry / residuals / Jacobians (the C5 precision sweep) or the reference's fp64 (default)."""
-        _ffi.check(self._L.floam_odom_set_precision(self._need(),
-                                                    _ffi.PRECISION_FP32 if fp32 else _ffi.PRECISION_FP64))
+    def set_precision(self, fp32, geometry: bool = False) -> None:
+        """Residual / Jacobian precision (the C5 sweep, BASELINE.json configs[4]): fp32=False is the reference's fp64;
+        fp32=True evaluates residuals, Jacobians and per-thread sums in float (fits and LM control in double);
+        geometry=True also runs the line / plane fits in float."""
+        level = _ffi.PRECISION_FP64
+        if fp32:
+            level = _ffi.PRECISION_FP32_GEOMETRY if geometry else _ffi.PRECISION_FP32
+        _ffi.check(self._L.floam_odom_set_precision(self._need(), level))
 
     def set_trace(self, capacity: int) -> None:
         """Stage inspection: record every solve (up to `capacity`) and keep the last correspondence pass."""

@@ -257,12 +257,13 @@ floam_status floam_odom_get_stats(const floam_odom* o, floam_odom_stats* s);
  * those calls).  *is_keyframe = 1 when the pose moved > 0.07 m or turned > 2 deg from the last keyframe. */
 floam_status floam_odom_keyframe_update(floam_odom* o, const double q_xyzw[4], const double t[3], int* is_keyframe);
 
-/* Precision of the correspondence geometry and of the residual / Jacobian evaluation (extension: BASELINE.json
- * configs[4], the fp32 vs fp64 tolerance sweep).  FLOAM_PRECISION_FP64 (default) is the reference's double
- * arithmetic (src/odomEstimationClass.cpp:156-243, src/lidarOptimization.cpp:12-74); FLOAM_PRECISION_FP32 computes the
- * line / plane fits, residuals, Jacobians and per-thread J^T J sums in float (reductions and the LM control stay in
- * double). */
-enum { FLOAM_PRECISION_FP64 = 0, FLOAM_PRECISION_FP32 = 1 };
+/* Precision of the residual / Jacobian evaluation and of the correspondence geometry (extension: BASELINE.json
+ * configs[4], the fp32 vs fp64 Jacobian tolerance sweep).  FLOAM_PRECISION_FP64 (default) is the reference's double
+ * arithmetic throughout (src/odomEstimationClass.cpp:156-243, src/lidarOptimization.cpp:12-74).
+ * FLOAM_PRECISION_FP32: residuals, Jacobians and the per-thread J^T J / J^T r sums in float; the line / plane fits,
+ * the cross-thread reductions and the LM control stay in double.  FLOAM_PRECISION_FP32_GEOMETRY: additionally the
+ * line (eigen) and plane (QR) fits in float.  Measured deviations from the fp64 solution: DESIGN.md §4. */
+enum { FLOAM_PRECISION_FP64 = 0, FLOAM_PRECISION_FP32 = 1, FLOAM_PRECISION_FP32_GEOMETRY = 2 };
 floam_status floam_odom_set_precision(floam_odom* o, int precision);
 
 /* Stage inspection (extension, for parity tests against the CPU restatement).  floam_odom_set_trace(o, capacity):
