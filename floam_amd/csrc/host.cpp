@@ -1110,12 +1110,12 @@ floam_status floam_odom_destroy(floam_odom* o) {
       for (auto& row : o->graph_exec)
         for (auto& ex : row)
           if (ex) FLOAM_HIP(hipGraphExecDestroy(ex));
-      if (o->dbg_stamps.p) {   // FLOAM_DEBUG_STAMPS: the resident solve's control-block segments (100 MHz ticks)
+      if (o->dbg_stamps.p) {   // FLOAM_DEBUG_STAMPS: the resident solve's segments in block 0 (100 MHz ticks)
         unsigned long long h[8];
         FLOAM_HIP(hipMemcpy(h, o->dbg_stamps.p, sizeof(h), hipMemcpyDeviceToHost));
         const double n = h[4] ? (double)h[4] : 1.0;
-        std::fprintf(stderr, "[floam stamps] %llu solves (control block, per solve): surf sums %.2f us, wait for the "
-                     "evaluation blocks %.2f us, reduce %.2f us, control step + release %.2f us\n", h[4],
+        std::fprintf(stderr, "[floam stamps] %llu solves (block 0, per solve): evaluate + publish %.2f us, all-gather "
+                     "%.2f us, reduce %.2f us, control step %.2f us\n", h[4],
                      h[0] / n / 100.0, h[1] / n / 100.0, h[2] / n / 100.0, h[3] / n / 100.0);
       }
       if (o->side) {

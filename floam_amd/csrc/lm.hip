@@ -4,27 +4,27 @@
 // Ceres 1.13 TrustRegionMinimizer + LevenbergMarquardtStrategy control is restated in lm_logic (SURVEY.md §8 a-12;
 // oracle/odom.cpp ceres_solve is the CPU restatement).
 //
-// Single GPU — lm_solve, ONE launch per solve.  Block 0 (control) keeps the LM state in the registers of its first
-// wave and runs the control step; blocks 1..nblk (evaluation) keep their records in registers across the up to five
-// evaluations.  The hand-offs are data-tagged 8-byte granules (MI355X_MICROARCH.md "handoff-1to1": one sc1 store per
-// granule, {tag, 32 data bits}, the consumer polls until every granule carries the tag it expects; no flag words,
-// no counters, no drains):
-//   control -> evaluation: the next evaluation point as 14 granules (7 doubles in halves) + a stop granule;
-//   evaluation -> control: each block's 29 partial sums as 58 granules.
-// Tags are epoch + evaluation index, with the epoch advanced by 8 at every solve (lm_reset), so a granule of an
-// earlier evaluation or solve never matches and nothing is ever cleared.  Every poll is bounded (~0.5 s); a timeout
-// ends the solve with n_res = -1, which the host reports as FLOAM_ERR_DEVICE.
+// Single GPU — lm_solve, ONE launch per solve, no control block.  Every active block (256 threads) keeps its records
+// in registers across the up to five evaluations, evaluates them at the current point, publishes its 29 partial sums
+// as data-tagged 8-byte granules (MI355X_MICROARCH.md "handoff-1to1": one sc1 store per granule, {tag, 32 data
+// bits}; the consumer polls until every granule carries the tag it expects; no flags, counters or drains), then
+// gathers every active block's granules, reduces them in a fixed order and runs the Ceres control step on its wave 0
+// with the LM state in registers.  All blocks compute the same bits, so the next point is known everywhere without a
+// control -> evaluation hop: one hand-off per evaluation.  Tags are epoch + evaluation index, with the epoch advanced
+// by 8 at every solve (lm_reset), so a granule of an earlier evaluation or solve never matches and nothing is ever
+// cleared.  Every poll is bounded (~0.3 s); a timeout ends the solve with n_res = -1 (FLOAM_ERR_DEVICE on the host).
 //
 // Modes (LM_*): GRAM — squared loss (the launch default, Q3): the surf half of every evaluation comes from the Gram
-// matrix of the surf records (exact in real arithmetic, see surf_sums_from_gram) and 32 evaluation blocks evaluate the
-// edge records; otherwise (Huber, fp32) 128 evaluation blocks evaluate every record.  FP32: residuals, Jacobians and
-// the per-thread sums in float (the C5 precision sweep, BASELINE.json configs[4]); reductions and control in double.
+// matrix of the surf records (exact in real arithmetic, see surf_sums_wave), formed by wave 3 of every block beside
+// the edge records of waves 0..2; otherwise (Huber, fp32) all 4 waves evaluate records of both kinds.  FP32:
+// residuals, Jacobians and the per-thread sums in float (the C5 precision sweep, BASELINE.json configs[4]);
+// reductions and control in double.
 //
 // Multi-GPU — lm_shard_eval: one launch per evaluation, the control step of the previous evaluation (on the
 // all-reduced sums) run redundantly by every block, then this rank's block partials reduced in fixed order by the
 // last-arriving block into the 29 sums the host all-reduces (RCCL) between the launches.
 //
-// Fixed reduction orders throughout (thread -> 8 strips of 32 -> block; blocks -> 8 strips -> total), so the result
+// Fixed reduction orders throughout (thread -> 8 strips -> block; blocks -> 8 strips -> total), so the result
 // does not depend on timing; the sharded path on one rank reproduces the single-GPU solve bit for bit.
 #include <cfloat>
 #include <climits>
@@ -34,13 +34,33 @@
 namespace floam {
 
 namespace {
-constexpr int kTB = 256;
+constexpr int kTB = 256;     // solve blocks: 4 waves, one per SIMD (the control wave keeps the LM state in 512 registers)
+constexpr int kStrips = 8;   // block_sums strips
 constexpr long long kSpin = 1ll << 23;   // bounded polls (s_sleep 1 each): ~0.3 s
+
+// LDS written by some lanes of a wave and read by others of the same wave: DS ops of one wave execute in order, so
+// only the compiler has to be kept from reordering
+__device__ __forceinline__ void wave_lds_order() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 template <typename R>
 __device__ __forceinline__ R real_min() { return DBL_MIN; }
 template <>
 __device__ __forceinline__ float real_min<float>() { return FLT_MIN; }
+
+// 1 / d for the dependent chains of the solve: v_rcp_f64 + two Newton steps (within an ulp of the division, a third of
+// its instructions); the float variant is the plain division
+__device__ __forceinline__ double recip(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  double e = fma(-d, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-d, r, 1.0);
+  return fma(r, e, r);
+}
+__device__ __forceinline__ float recip(float d) { return 1.0f / d; }
 
 // ===================================================================================== residuals (R = double | float)
 // Eigen's q * v: uv = 2 q.vec x v; v + w uv + q.vec x uv
@@ -56,6 +76,7 @@ __device__ __forceinline__ void rot(const R* x, R vx, R vy, R vz, R& ox, R& oy, 
 }
 
 // EdgeAnalyticCostFunction::Evaluate (src/lidarOptimization.cpp:12-43): J = -(nu/|nu|)^T [de]x [-[lp]x, I] / |de|
+// (the divisions by |nu| and |de| as products with their reciprocals: the same values to an ulp)
 template <typename R>
 __device__ __forceinline__ R edge_residual(const R* x, const R* r9, R J[6]) {
   R lx, ly, lz;
@@ -67,19 +88,20 @@ __device__ __forceinline__ R edge_residual(const R* x, const R* r9, R J[6]) {
   const R dex = r9[3] - r9[6], dey = r9[4] - r9[7], dez = r9[5] - r9[8];
   const R de_norm = sqrt(dex * dex + dey * dey + dez * dez);
   const R nn = sqrt(nux * nux + nuy * nuy + nuz * nuz);
-  const R r = nn / de_norm;
-  const R w0 = -nux / nn, w1 = -nuy / nn, w2 = -nuz / nn;
+  const R ide = recip(de_norm), inn = recip(nn);   // one reciprocal each instead of ten divisions
+  const R r = nn * ide;
+  const R w0 = -nux * inn, w1 = -nuy * inn, w2 = -nuz * inn;
   // r1 = w * skew(de): skew(de) = [[0,-dz,dy],[dz,0,-dx],[-dy,dx,0]]
   const R r10 = w1 * dez + w2 * (-dey);
   const R r11 = w0 * (-dez) + w2 * dex;
   const R r12 = w0 * dey + w1 * (-dex);
   // dp = [-skew(lp), I]; -skew(lp) = [[0,lz,-ly],[-lz,0,lx],[ly,-lx,0]]
-  J[0] = (r11 * (-lz) + r12 * ly) / de_norm;
-  J[1] = (r10 * lz + r12 * (-lx)) / de_norm;
-  J[2] = (r10 * (-ly) + r11 * lx) / de_norm;
-  J[3] = r10 / de_norm;
-  J[4] = r11 / de_norm;
-  J[5] = r12 / de_norm;
+  J[0] = (r11 * (-lz) + r12 * ly) * ide;
+  J[1] = (r10 * lz + r12 * (-lx)) * ide;
+  J[2] = (r10 * (-ly) + r11 * lx) * ide;
+  J[3] = r10 * ide;
+  J[4] = r11 * ide;
+  J[5] = r12 * ide;
   return r;
 }
 
@@ -140,27 +162,37 @@ __device__ __forceinline__ void load_rec(const double* __restrict__ rec, int cap
   for (int k = 0; k < 9; ++k) f[k] = k < N ? (R)rec[k * cap + i] : R(0);
 }
 
-// thread sums -> the block's 29 sums in out (LDS), fixed order: 8 strips of 32 threads, then the strips
-__device__ __forceinline__ void block_sums(const double (&acc)[LM_NSUM], double* red /* LDS [LM_NSUM][kTB] */,
-                                           double* strip /* LDS [LM_NSUM][8] */, double* out /* LDS [LM_NSUM] */) {
+// thread sums of the record threads [0, NR) -> the block's 29 sums, fixed order: strip p of component c (8 strips,
+// 29 x 8 = 232 threads) adds threads p, p + 8, p + 16, ... (the strip threads read consecutive LDS words: no bank
+// conflicts), then the 8 strips are added in order.  Returns, to thread t < 58, the sum of component t >> 1 (the
+// caller publishes it in two halves); no barrier after the last LDS read of `strip`.
+template <int NR>
+constexpr int red_stride() { return NR + 1; }   // odd row stride (in doubles): the 8 rows a wave reads hit 8 bank sets
+template <int NR>
+__device__ __forceinline__ double block_sums(const double (&acc)[LM_NSUM], double* red /* LDS [LM_NSUM][NR + 1] */,
+                                             double* strip /* LDS [LM_NSUM][kStrips] */) {
+  static_assert(NR % kStrips == 0 && LM_NSUM * kStrips <= kTB, "strip layout");
+  constexpr int RS = red_stride<NR>();
   const int t = threadIdx.x;
+  if (t < NR)
 #pragma unroll
-  for (int k = 0; k < LM_NSUM; ++k) red[k * kTB + t] = acc[k];
+    for (int k = 0; k < LM_NSUM; ++k) red[k * RS + t] = acc[k];
   __syncthreads();
-  if (t < LM_NSUM * 8) {
-    const int c = t >> 3, p = t & 7;
+  if (t < LM_NSUM * kStrips) {
+    const int c = t / kStrips, p = t % kStrips;
     double v = 0.0;
-#pragma unroll
-    for (int j = 0; j < kTB / 8; ++j) v += red[c * kTB + p * (kTB / 8) + j];
-    strip[c * 8 + p] = v;
+#pragma unroll 4
+    for (int j = 0; j < NR / kStrips; ++j) v += red[c * RS + j * kStrips + p];
+    strip[c * kStrips + p] = v;
   }
   __syncthreads();
-  if (t < LM_NSUM) {
-    double v = 0.0;
-    for (int p = 0; p < 8; ++p) v += strip[t * 8 + p];
-    out[t] = v;
+  double v = 0.0;
+  if (t < 2 * LM_NSUM) {
+    const int c = t >> 1;
+#pragma unroll
+    for (int p = 0; p < kStrips; ++p) v += strip[c * kStrips + p];
   }
-  __syncthreads();
+  return v;
 }
 
 // block partials P(c, b) (c < 29, b < nblk) -> 29 sums in out (LDS), fixed order: component c sums 8 strips of
@@ -231,93 +263,104 @@ __device__ __forceinline__ void eval_records(const R (&x)[7], bool has0, bool ed
 // nu/|nu|, which depends on the pose).  Recentring c on o keeps the cancellation inside G c independent of how far the
 // pose is from the map origin.  Same function values as the per-residual evaluation in exact arithmetic; the rounding
 // differs (~|G| eps in c^T G c, ~1e-9 of the cost at C3; poses agree with the per-record path to ~1e-14).
-__device__ void surf_sums_from_gram(const double* x /* LDS [7] */, const double* o /* LDS [3] */,
-                                    const double (*G)[kGramW] /* LDS */, double n_surf, double* out /* LDS [29] */) {
+// One wave (lane = 0..63) computes the surf half; the other waves of the block are not involved (no block barrier).
+// Lane 0 forms M and the translations (LDS); V = [K_0..K_5, c] is filled branch-free from a constant table (entry =
+// sign x one of M, t', t, 1); only Y = G [K_0, K_1, K_2, c] is formed, because K_3..K_5 are the unit vectors
+// e_9..e_11: every output is one 13-term dot product of two rows of V, Y or G (a row of G for G K_{3+a} = G e_{9+a},
+// G symmetric) — the same products and sums, in the same order, as the full quadratic forms (the unit vectors only
+// contribute exact zeros).
+struct SurfTable {
+  signed char sgn[7][kGramW];   // -1, 0, +1
+  unsigned char idx[7][kGramW]; // into Mt: M (0..8), t' (9..11), t (12..14), 1 (15)
+  unsigned char ra[LM_NSUM], rb[LM_NSUM];   // output rows: 0..6 V, 7..10 Y(K_0, K_1, K_2, c), 11..23 G
+};
+constexpr SurfTable make_surf_table() {
+  SurfTable T{};
+  for (int m = 0; m < kGramW; ++m) {   // c = [M, t', 1]
+    T.sgn[6][m] = 1;
+    T.idx[6][m] = (unsigned char)(m < 12 ? m : 15);
+  }
+  for (int i = 0; i < 3; ++i) {        // K_i: sum_b eps_ibc M_be (w index 3c + e), sum_b eps_ibc t_b
+    const int b1 = (i + 1) % 3, b2 = (i + 2) % 3;
+    for (int m = 0; m < kGramW; ++m) {
+      if (m < 9) {
+        const int c = m / 3, e = m % 3;
+        if (c == b2) { T.sgn[i][m] = 1; T.idx[i][m] = (unsigned char)(3 * b1 + e); }
+        else if (c == b1) { T.sgn[i][m] = -1; T.idx[i][m] = (unsigned char)(3 * b2 + e); }
+      } else if (m < 12) {
+        const int c = m - 9;
+        if (c == b2) { T.sgn[i][m] = 1; T.idx[i][m] = (unsigned char)(12 + b1); }
+        else if (c == b1) { T.sgn[i][m] = -1; T.idx[i][m] = (unsigned char)(12 + b2); }
+      }
+    }
+  }
+  for (int a = 0; a < 3; ++a) { T.sgn[3 + a][9 + a] = 1; T.idx[3 + a][9 + a] = 15; }   // K_{3+a} = e_{9+a}
+  // outputs: cost = c.Gc; J^T J (a <= b): a, b < 3: K_a.(G K_b); a < 3 <= b: K_a.(row 9+b-3 of G);
+  // 3 <= a, b: e_{9+a-3}.(row 9+b-3 of G); J^T r: a < 3: K_a.(G c); a >= 3: e_{9+a-3}.(G c)
+  auto yrow = [](int v) { return v < 3 ? 7 + v : 10; };   // Y row of K_v (v < 3) or c (v = 6)
+  T.ra[0] = 6; T.rb[0] = 10;
+  int h = 1;
+  for (int a = 0; a < 6; ++a)
+    for (int b = a; b < 6; ++b, ++h) {
+      T.ra[h] = (unsigned char)a;   // V row K_a (the unit vectors for a >= 3)
+      T.rb[h] = (unsigned char)(b < 3 ? yrow(b) : 11 + 9 + b - 3);
+    }
+  for (int a = 0; a < 6; ++a) { T.ra[22 + a] = (unsigned char)a; T.rb[22 + a] = 10; }
+  T.ra[28] = 6; T.rb[28] = 6;   // (count: not a dot product)
+  return T;
+}
+__constant__ SurfTable c_surf = make_surf_table();
+
+__device__ void surf_sums_wave(const double* x /* LDS [7] */, const double* o /* LDS [3] */,
+                               const double (*G)[kGramW] /* LDS */, double n_surf, double* out /* LDS [29] */,
+                               int t /* lane */) {
   __shared__ double V[7][kGramW];   // K_0..K_5, c
-  __shared__ double Y[7][kGramW];   // G V
-  const int t = threadIdx.x;
-  if (t < kGramW) {   // lanes 0..12 build one component of all 7 vectors
+  __shared__ double Y[4][kGramW];   // G K_0, G K_1, G K_2, G c
+  __shared__ double Mt[16];         // M (row-major), t' = t - o, t, 1
+  if (t == 0) {
     const double qx = x[0], qy = x[1], qz = x[2], qw = x[3];
     const double U[3][3] = {{0, -qz, qy}, {qz, 0, -qx}, {-qy, qx, 0}};
-    double Mm[3][3];
 #pragma unroll
     for (int a = 0; a < 3; ++a)
 #pragma unroll
       for (int b = 0; b < 3; ++b) {
         const double u2 = U[a][0] * U[0][b] + U[a][1] * U[1][b] + U[a][2] * U[2][b];
-        Mm[a][b] = ((a == b) ? 1.0 : 0.0) + 2.0 * qw * U[a][b] + 2.0 * u2;
+        Mt[3 * a + b] = ((a == b) ? 1.0 : 0.0) + 2.0 * qw * U[a][b] + 2.0 * u2;
       }
-    const double tp[3] = {x[4] - o[0], x[5] - o[1], x[6] - o[2]};   // c: recentred (d absorbed n.o)
-    const double tf[3] = {x[4], x[5], x[6]};                        // K: the Jacobian's lp = M p + t itself
-    const int m = t;   // component of w
-    // register-resident selects instead of run-time array indexing (no scratch)
-    auto Msel = [&](int r, int c) {
-      double v = 0.0;
 #pragma unroll
-      for (int a = 0; a < 3; ++a)
-#pragma unroll
-        for (int b = 0; b < 3; ++b)
-          if (a == r && b == c) v = Mm[a][b];
-      return v;
-    };
-    auto vsel = [&](const double (&vv)[3], int k) { return k == 0 ? vv[0] : (k == 1 ? vv[1] : vv[2]); };
-    double cm = 1.0;
-    if (m < 9) cm = Msel(m / 3, m % 3);
-    else if (m < 12) cm = vsel(tp, m - 9);
-    V[6][m] = cm;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {   // K_i for i = 0..2 (lp x n)
-      const int b1 = (i + 1) % 3, b2 = (i + 2) % 3;   // eps_{i b1 b2} = +1, eps_{i b2 b1} = -1
-      double km = 0.0;
-      if (m < 9) {
-        const int c = m / 3, e = m % 3;   // w index 3c + e: sum_b eps_{ibc} M_be
-        if (c == b2) km = Msel(b1, e);
-        else if (c == b1) km = -Msel(b2, e);
-      } else if (m < 12) {
-        const int c = m - 9;              // sum_b eps_{ibc} t_b
-        if (c == b2) km = vsel(tf, b1);
-        else if (c == b1) km = -vsel(tf, b2);
-      }
-      V[i][m] = km;
+    for (int k = 0; k < 3; ++k) {
+      Mt[9 + k] = x[4 + k] - o[k];   // c: recentred (d absorbed n.o)
+      Mt[12 + k] = x[4 + k];         // K: the Jacobian's lp = M p + t itself
     }
-#pragma unroll
-    for (int a = 0; a < 3; ++a) V[3 + a][m] = (m == 9 + a) ? 1.0 : 0.0;   // K_{3+a} = e_{9+a}
+    Mt[15] = 1.0;
   }
-  __syncthreads();
-  if (t < 7 * kGramW) {   // Y = G V
+  wave_lds_order();
+  for (int e = t; e < 7 * kGramW; e += 64) {
+    const int v = e / kGramW, m = e % kGramW;
+    const int sg = c_surf.sgn[v][m];
+    const double mv = Mt[c_surf.idx[v][m]];
+    V[v][m] = sg > 0 ? mv : (sg < 0 ? -mv : 0.0);
+  }
+  wave_lds_order();
+  if (t < 4 * kGramW) {   // Y = G [K_0, K_1, K_2, c]
     const int v = t / kGramW, i = t % kGramW;
+    const double* vv = V[v == 3 ? 6 : v];
     double a = 0.0;
 #pragma unroll
-    for (int j = 0; j < kGramW; ++j) a += G[i][j] * V[v][j];
+    for (int j = 0; j < kGramW; ++j) a += G[i][j] * vv[j];
     Y[v][i] = a;
   }
-  __syncthreads();
+  wave_lds_order();
   if (t < LM_NSUM) {   // cost, J^T J upper (row-major), J^T r, count
-    double s;
-    if (t == 0) {
-      double a = 0.0;
+    const int ra = c_surf.ra[t], rb = c_surf.rb[t];
+    const double* A = V[ra];
+    const double* B = rb < 7 ? V[rb] : (rb < 11 ? Y[rb - 7] : G[rb - 11]);
+    double a = 0.0;
 #pragma unroll
-      for (int i = 0; i < kGramW; ++i) a += V[6][i] * Y[6][i];
-      s = 0.5 * a;
-    } else if (t < 22) {
-      int hh = t - 1, ja = 0;
-      while (hh >= 6 - ja) { hh -= 6 - ja; ++ja; }
-      const int jb = ja + hh;
-      double a = 0.0;
-#pragma unroll
-      for (int i = 0; i < kGramW; ++i) a += V[ja][i] * Y[jb][i];
-      s = a;
-    } else if (t < 28) {
-      double a = 0.0;
-#pragma unroll
-      for (int i = 0; i < kGramW; ++i) a += V[t - 22][i] * Y[6][i];
-      s = a;
-    } else {
-      s = n_surf;
-    }
-    out[t] = s;
+    for (int i = 0; i < kGramW; ++i) a += A[i] * B[i];
+    out[t] = t == 28 ? n_surf : (t == 0 ? 0.5 * a : a);
   }
-  __syncthreads();
+  wave_lds_order();
 }
 
 __device__ __forceinline__ void gram_pair(int e, int& i, int& j) {   // upper-triangle entry e -> (i, j), i <= j
@@ -361,11 +404,12 @@ __device__ __forceinline__ void se3_plus(const double (&x)[7], const double (&d)
   const double real_factor = ch;
   double imag;
   const bool small = theta < 1e-10;
+  const double rt = recip(theta);   // beside the sincos, off the dependent chain
   if (small) {
     const double t2 = theta * theta, t4 = t2 * t2;
     imag = 0.5 - 0.0208333 * t2 + 0.000260417 * t4;
   } else {
-    imag = sh / theta;
+    imag = sh * rt;
   }
   const double dq[4] = {imag * wx, imag * wy, imag * wz, real_factor};   // x, y, z, w
   double Jm[3][3];
@@ -386,8 +430,8 @@ __device__ __forceinline__ void se3_plus(const double (&x)[7], const double (&d)
       for (int j = 0; j < 3; ++j) O2[i][j] = O[i][0] * O[0][j] + O[i][1] * O[1][j] + O[i][2] * O[2][j];
     double st, ct;
     sincos(theta, &st, &ct);
-    const double c1 = (1 - ct) / (theta * theta);
-    const double c2 = (theta - st) / (theta * theta * theta);
+    const double c1 = (1 - ct) * (rt * rt);
+    const double c2 = (theta - st) * (rt * rt * rt);
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -430,7 +474,7 @@ __device__ __forceinline__ bool solve_step(LMState& s, double (&delta)[6]) {
 #pragma unroll
   for (int a = 0; a < 6; ++a) gs[a] = sc[a] * s.g[a];
   const int reuse = s.reuse;
-  const double inv_radius = 1.0 / s.radius;
+  const double inv_radius = recip(s.radius);
   // packed lower triangle (row-major, l(i,j) = i(i+1)/2 + j): Hs = S H S, then A = Hs + diag/radius factored in place
   double Hs[21], A[21];
 #pragma unroll
@@ -459,7 +503,7 @@ __device__ __forceinline__ bool solve_step(LMState& s, double (&delta)[6]) {
 #pragma unroll
     for (int k = 0; k < j; ++k) d -= A[j * (j + 1) / 2 + k] * W[j * (j + 1) / 2 + k];
     pd = pd && (d > 0.0);
-    rD[j] = 1.0 / d;
+    rD[j] = recip(d);
 #pragma unroll
     for (int i = j + 1; i < 6; ++i) {
       double v = A[i * (i + 1) / 2 + j];
@@ -682,19 +726,6 @@ __device__ __forceinline__ unsigned long long granule(unsigned tag, unsigned dat
 __device__ __forceinline__ void put_granule(unsigned long long* p, unsigned long long g) {
   __hip_atomic_store(p, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// poll one granule until it carries `tag` (bounded); false on timeout
-__device__ __forceinline__ bool get_granule(const unsigned long long* p, unsigned tag, unsigned& data) {
-  for (long long k = 0; k < kSpin; ++k) {
-    const unsigned long long g = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if ((unsigned)(g >> 32) == tag) {
-      data = (unsigned)g;
-      return true;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-  return false;
-}
-
 // granules j0, j0 + kTB, ..., j0 + (kSweep - 1) kTB (those < n) until all carry `tag` (bounded), data into out[j]
 constexpr int kSweep = 8;
 __device__ __forceinline__ bool sweep_granules(const unsigned long long* __restrict__ g, int j0, int n, unsigned tag,
@@ -720,9 +751,15 @@ __device__ __forceinline__ bool sweep_granules(const unsigned long long* __restr
   return pending == 0;
 }
 
-// evaluation blocks that hold records: one record slot per thread while they fit, at most nblk (a function of the
-// device count only, so the partition and the reduction order never depend on the host's upper bounds)
-__device__ __forceinline__ int active_blocks(int total, int nblk) { return max(1, min(nblk, (total + kTB - 1) / kTB)); }
+// evaluation blocks that hold records: one record slot per record thread while they fit, at most nblk (a function of
+// the device count only, so the partition and the reduction order never depend on the host's upper bounds)
+template <int NR>
+__device__ __forceinline__ int active_blocks(int total, int nblk) { return max(1, min(nblk, (total + NR - 1) / NR)); }
+
+// record threads of a solve block: GRAM — waves 0..2 hold edge records and wave 3 forms the surf half from G;
+// otherwise every thread holds records
+template <bool GRAM>
+constexpr int rec_threads() { return GRAM ? kTB - 64 : kTB; }
 
 struct LMArgs {
   LMState* st;
@@ -737,109 +774,103 @@ struct LMArgs {
   const int* d_ns;
   int ns_ub;
   const double* gmat;              // GRAM: G + origin (kGramWords)
-  unsigned long long* rel;         // 15 release granules
-  unsigned long long* part;        // [nblk][2 * LM_NSUM] partial granules
+  unsigned long long* part;        // [2][kRecEvalBlocks][2 * LM_NSUM] partial granules (by evaluation parity)
   double* partials;                // sharded: [LM_NSUM][nblk]
   double* sums;                    // sharded: 29 sums (all-reduced in place between launches)
   unsigned* ticket;                // sharded: arrival ticket
-  unsigned long long* dbg;         // FLOAM_DEBUG_STAMPS: control-block segment times (diagnostic, normally null)
+  unsigned long long* dbg;         // FLOAM_DEBUG_STAMPS: block 0's segment times (diagnostic, normally null)
 };
 
+// the block's first record (the one kept in registers across the evaluations) of record thread i0
+template <typename R>
+__device__ __forceinline__ void first_record(const LMArgs& a, int i0, int ne, int total, R (&f0)[9], bool& has0,
+                                             bool& edge0) {
+#pragma unroll
+  for (int k = 0; k < 9; ++k) f0[k] = R(0);
+  has0 = false;
+  edge0 = true;
+  if (i0 < ne) {
+    has0 = a.evalid[i0] & 1;
+    if (has0) load_rec<R, EDGE_FIELDS>(a.erec, a.ecap, i0, f0);
+  } else if (i0 < total) {
+    edge0 = false;
+    has0 = a.svalid[i0 - ne] & 1;
+    if (has0) load_rec<R, SURF_FIELDS>(a.srec, a.scap, i0 - ne, f0);
+  }
+}
+
 // ===================================================================================== the resident solve
+// Every active block runs the whole solve: it evaluates its records at the current point, publishes its 29 partial
+// sums as tagged granules, gathers every active block's granules (all-gather: one hand-off per evaluation, no
+// control -> evaluation release hop), reduces them in a fixed block order and runs the Ceres control step on wave 0
+// — every block computes the same bits, so every block knows the next point and whether the solve ended.  Block 0
+// writes the state back.  Granule slots alternate with the evaluation's parity: a block overwrites its slot of
+// evaluation k only in evaluation k + 2, after it has seen every block's granule of evaluation k + 1, which each block
+// publishes only after it has seen every granule of evaluation k.
 template <bool GRAM, bool HUBER, typename R>
 __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
-  __shared__ double s_red[LM_NSUM * kTB];   // evaluation: thread sums; control: the partial table (as u32 halves)
-  __shared__ double s_strip[LM_NSUM * 8];
+  constexpr int NR = rec_threads<GRAM>();
+  __shared__ double s_buf[LM_NSUM * red_stride<NR>()];   // thread sums; then the all-gathered partial table (u32)
+  __shared__ double s_strip[LM_NSUM * kStrips];
   __shared__ double s_sums[LM_NSUM];
+  __shared__ double s_ssum[LM_NSUM];
   __shared__ double s_pt[7];
-  __shared__ unsigned s_rel[15];
-  __shared__ int s_flag;
-  const int nblk = (int)gridDim.x - 1;
-  const int tid = threadIdx.x;
-  if (blockIdx.x > 0) {   // ------------------------------------------------------------------ evaluation block
-    const int blk = (int)blockIdx.x - 1;
-    const unsigned ep = a.st->epoch;
-    const int ne = min(*a.d_ne, a.ne_ub);
-    const int total = ne + (GRAM ? 0 : min(*a.d_ns, a.ns_ub));
-    const int nact = active_blocks(total, nblk);
-    if (blk >= nact) return;   // no records: the control block does not wait for this one
-    const int stride = nact * kTB, i0 = blk * kTB + tid;
-    // the thread's first record stays in registers across the evaluations
-    R f0[9];
-    bool has0 = false, edge0 = true;
-#pragma unroll
-    for (int k = 0; k < 9; ++k) f0[k] = R(0);
-    if (i0 < ne) {
-      has0 = a.evalid[i0] & 1;
-      if (has0) load_rec<R, EDGE_FIELDS>(a.erec, a.ecap, i0, f0);
-    } else if (i0 < total) {
-      edge0 = false;
-      has0 = a.svalid[i0 - ne] & 1;
-      if (has0) load_rec<R, SURF_FIELDS>(a.srec, a.scap, i0 - ne, f0);
-    }
-    for (int it = 0; it < 5; ++it) {
-      if (it == 0) {   // iteration zero evaluates at x (set by the kNN launch; kernel boundary)
-        if (tid == 0) s_flag = a.st->done;
-        if (tid < 7) s_pt[tid] = a.st->x[tid];
-      } else {         // the point the control step of evaluation it - 1 released (or the stop granule)
-        if (tid < 15) {
-          unsigned v = 0;
-          const bool ok = get_granule(&a.rel[tid], ep + (unsigned)it, v);
-          s_rel[tid] = v;
-          if (tid == 14) s_flag = ok ? (int)v : 1;   // a timeout stops this block too
-        }
-        __syncthreads();
-        if (tid < 7)
-          s_pt[tid] = __longlong_as_double((long long)(((unsigned long long)s_rel[2 * tid + 1] << 32) | s_rel[2 * tid]));
-      }
-      __syncthreads();
-      if (s_flag) return;
-      R x[7];
-#pragma unroll
-      for (int k = 0; k < 7; ++k) x[k] = (R)s_pt[k];
-      double acc[LM_NSUM];
-      eval_records<HUBER, R>(x, has0, edge0, f0, i0 + stride, stride, ne, total, a.erec, a.evalid, a.ecap, a.srec,
-                             a.svalid, a.scap, acc);
-      block_sums(acc, s_red, s_strip, s_sums);
-      if (tid < 2 * LM_NSUM) {   // 58 granules: the block's sums in 32-bit halves, tagged with this evaluation
-        const unsigned long long b = (unsigned long long)__double_as_longlong(s_sums[tid >> 1]);
-        put_granule(&a.part[blk * 2 * LM_NSUM + tid],
-                    granule(ep + (unsigned)it, (tid & 1) ? (unsigned)(b >> 32) : (unsigned)b));
-      }
-    }
-    return;
-  }
-  // ------------------------------------------------------------------------------------------------- control block
   __shared__ LMState sst;
   __shared__ double G[kGramW][kGramW];
   __shared__ double o[3];
-  __shared__ double s_ssum[LM_NSUM];
   __shared__ int s_done;
+  const int nblk = (int)gridDim.x, blk = (int)blockIdx.x, tid = (int)threadIdx.x, lane = tid & 63;
+  const int ne = min(*a.d_ne, a.ne_ub);
+  const int total = ne + (GRAM ? 0 : min(*a.d_ns, a.ns_ub));
+  const int nact = active_blocks<NR>(total, nblk);
+  if (blk >= nact) return;   // no records: nobody waits for this block
   stage_state(a.st, sst);
-  double gv = 0.0;
-  if (GRAM && tid < kGramWords) gv = a.gmat[tid];
+  const double gv = (GRAM && tid < kGramWords) ? a.gmat[tid] : 0.0;
+  const int stride = nact * NR, i0 = blk * NR + tid;
+  R f0[9];
+  bool has0 = false, edge0 = true;
+  if (tid < NR) first_record<R>(a, i0, ne, total, f0, has0, edge0);
   __syncthreads();
-  if (sst.done) return;   // (never after lm_reset; the evaluation blocks saw it too)
-  const unsigned ep = sst.epoch;
-  const int nact = active_blocks(min(*a.d_ne, a.ne_ub) + (GRAM ? 0 : min(*a.d_ns, a.ns_ub)), nblk);
+  if (sst.done) return;   // (never after lm_reset)
   if (GRAM) gram_unpack(gv, G, o);
-  const int lane = tid & 63;
+  const unsigned ep = sst.epoch;
   LMState s;   // wave 0: the whole LM state in registers for the whole solve
   if (tid < 64) s = sst;
-  unsigned* tab = reinterpret_cast<unsigned*>(s_red);   // [nact][2 * LM_NSUM] halves of the block partials
+  if (tid < 7) s_pt[tid] = sst.x[tid];   // iteration zero evaluates at x (set by the kNN launch; kernel boundary)
+  if (tid == 0) s_done = 0;
+  unsigned* tab = reinterpret_cast<unsigned*>(s_buf);   // [nact][2 * LM_NSUM]
+  const int ngr = nact * 2 * LM_NSUM;
   unsigned long long tm[4] = {0, 0, 0, 0};
-  int failed_at = -1;   // evaluation whose partials never arrived (never expected)
+  int failed_at = -1;   // evaluation whose granules never arrived (never expected)
   for (int it = 0; it < 5; ++it) {
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    if (tid < 7) s_pt[tid] = point_component(s, tid);   // (wave 0 holds s; lanes 0..6 write)
-    __syncthreads();
-    if (GRAM) surf_sums_from_gram(s_pt, o, G, (double)sst.corr_surf, s_ssum);   // overlaps the evaluation blocks
+    __syncthreads();   // s_pt and s_done of this evaluation
+    if (s_done) break;
+    double acc[LM_NSUM];
+    if (tid < NR) {
+      R x[7];
+#pragma unroll
+      for (int k = 0; k < 7; ++k) x[k] = (R)s_pt[k];
+      eval_records<HUBER, R>(x, has0, edge0, f0, i0 + stride, stride, ne, total, a.erec, a.evalid, a.ecap, a.srec,
+                             a.svalid, a.scap, acc);
+    } else {
+#pragma unroll
+      for (int k = 0; k < LM_NSUM; ++k) acc[k] = 0.0;
+      if (GRAM) surf_sums_wave(s_pt, o, G, (double)sst.corr_surf, s_ssum, lane);   // beside the edge records
+    }
+    const double v = block_sums<NR>(acc, s_buf, s_strip);
+    unsigned long long* slot = a.part + (size_t)(it & 1) * kRecEvalBlocks * 2 * LM_NSUM;
+    const unsigned tag = ep + (unsigned)it;
+    if (tid < 2 * LM_NSUM) {   // 58 granules: the block's sums in 32-bit halves, tagged with this evaluation
+      const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+      put_granule(&slot[blk * 2 * LM_NSUM + tid], granule(tag, (tid & 1) ? (unsigned)(b >> 32) : (unsigned)b));
+    }
     const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
-    // the evaluation blocks' partial granules of evaluation it: every thread keeps kSweep loads in flight per poll
-    // round (one round trip per round, not one per granule)
+    // every active block's granules of this evaluation (this block's own included): kSweep loads in flight per
+    // thread and poll round
     int bad = 0;
-    for (int j0 = tid; j0 < nact * 2 * LM_NSUM; j0 += kSweep * kTB)
-      if (!sweep_granules(a.part, j0, nact * 2 * LM_NSUM, ep + (unsigned)it, tab)) bad = 1;
+    for (int j0 = tid; j0 < ngr; j0 += kSweep * kTB)
+      if (!sweep_granules(slot, j0, ngr, tag, tab)) bad = 1;
     if (__syncthreads_or(bad)) {
       failed_at = it;
       break;
@@ -854,35 +885,23 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
     const unsigned long long t3 = __builtin_amdgcn_s_memrealtime();
     if (tid < 64) {
       control_step(s, sst, s_sums, lane);
-      if (it + 1 < 5 && lane < 15) {   // release evaluation it + 1: the next point, or stop
-        unsigned v;
-        if (lane == 14) {
-          v = s.done ? 1u : 0u;
-        } else {
-          const unsigned long long b = (unsigned long long)__double_as_longlong(point_component(s, lane >> 1));
-          v = (lane & 1) ? (unsigned)(b >> 32) : (unsigned)b;
-        }
-        put_granule(&a.rel[lane], granule(ep + (unsigned)it + 1u, v));
-      }
+      if (tid < 7) s_pt[tid] = point_component(s, tid);   // the next point (if the solve goes on)
       if (lane == 0) s_done = s.done;
     }
-    __syncthreads();
-    if (a.dbg) {
+    if (a.dbg && blk == 0) {
       const unsigned long long t4 = __builtin_amdgcn_s_memrealtime();
       tm[0] += t1 - t0; tm[1] += t2 - t1; tm[2] += t3 - t2; tm[3] += t4 - t3;
     }
-    if (s_done) break;
   }
-  if (failed_at >= 0 && tid < 64) {   // end the solve, report through n_res, stop the blocks still waiting
+  if (blk != 0) return;
+  if (failed_at >= 0 && tid < 64) {   // end the solve, report through n_res
     s.done = 1;
     s.n_res = -1;
-    if (failed_at + 1 < 5 && lane < 15)
-      put_granule(&a.rel[lane], granule(ep + (unsigned)failed_at + 1u, lane == 14 ? 1u : 0u));
   }
   if (tid == 0) store_state_core(sst, s);
   __syncthreads();
   publish_state(sst, a.st);
-  if (a.dbg && tid == 0) {   // diagnostic stamps (100 MHz): surf sums, wait, reduce, control step + release
+  if (a.dbg && tid == 0) {   // diagnostic stamps (100 MHz): evaluate + publish, all-gather, reduce, control step
     atomicAdd(&a.dbg[0], tm[0]);
     atomicAdd(&a.dbg[1], tm[1]);
     atomicAdd(&a.dbg[2], tm[2]);
@@ -893,18 +912,20 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
 
 // ===================================================================================== the sharded evaluation
 // Launch k: every block stages the state, runs the control step of evaluation k - 1 on the all-reduced sums (all
-// blocks compute the same state), evaluates its records at the resulting point, and the last-arriving block reduces
-// the block partials (fixed order) + the surf half into a.sums for the all-reduce and writes the state.
+// blocks compute the same state), evaluates its records at the resulting point with the resident solve's partition
+// and reduction order, and the last-arriving block reduces the block partials (fixed order) + the surf half into
+// a.sums for the all-reduce and writes the state (on one rank: the resident solve's bits).
 template <bool GRAM, bool HUBER, typename R>
 __global__ __launch_bounds__(kTB) void lm_shard_eval(LMArgs a, int k) {
-  __shared__ double s_red[LM_NSUM * kTB];
-  __shared__ double s_strip[LM_NSUM * 8];
+  constexpr int NR = rec_threads<GRAM>();
+  __shared__ double s_buf[LM_NSUM * red_stride<NR>()];
+  __shared__ double s_strip[LM_NSUM * kStrips];
   __shared__ double s_sums[LM_NSUM];
   __shared__ double s_ssum[LM_NSUM];
   __shared__ double s_pt[7];
   __shared__ LMState sst;
   __shared__ int s_done, s_last;
-  const int nblk = (int)gridDim.x, blk = (int)blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  const int nblk = (int)gridDim.x, blk = (int)blockIdx.x, tid = (int)threadIdx.x, lane = tid & 63;
   stage_state(a.st, sst);
   __syncthreads();
   LMState s;
@@ -918,20 +939,25 @@ __global__ __launch_bounds__(kTB) void lm_shard_eval(LMArgs a, int k) {
   const bool done = s_done != 0;
   const int ne = min(*a.d_ne, a.ne_ub);
   const int total = ne + (GRAM ? 0 : min(*a.d_ns, a.ns_ub));
-  const int nact = active_blocks(total, nblk);   // the resident solve's partition (bit-identical on one rank)
-  if (!done && blk < nact) {
-    R x[7];
-#pragma unroll
-    for (int q = 0; q < 7; ++q) x[q] = (R)s_pt[q];
-    const int stride = nact * kTB, i0 = blk * kTB + tid;
-    R f0[9];
-#pragma unroll
-    for (int q = 0; q < 9; ++q) f0[q] = R(0);
+  const int nact = active_blocks<NR>(total, nblk);
+  if (!done && blk < nact) {   // block-uniform
     double acc[LM_NSUM];
-    eval_records<HUBER, R>(x, false, true, f0, i0, stride, ne, total, a.erec, a.evalid, a.ecap, a.srec, a.svalid,
-                           a.scap, acc);
-    block_sums(acc, s_red, s_strip, s_sums);
-    if (tid < LM_NSUM) a.partials[tid * nact + blk] = s_sums[tid];
+    if (tid < NR) {
+      R x[7];
+#pragma unroll
+      for (int q = 0; q < 7; ++q) x[q] = (R)s_pt[q];
+      const int stride = nact * NR, i0 = blk * NR + tid;
+      R f0[9];
+      bool has0, edge0;
+      first_record<R>(a, i0, ne, total, f0, has0, edge0);
+      eval_records<HUBER, R>(x, has0, edge0, f0, i0 + stride, stride, ne, total, a.erec, a.evalid, a.ecap, a.srec,
+                             a.svalid, a.scap, acc);
+    } else {
+#pragma unroll
+      for (int q = 0; q < LM_NSUM; ++q) acc[q] = 0.0;
+    }
+    const double v = block_sums<NR>(acc, s_buf, s_strip);
+    if (tid < 2 * LM_NSUM && !(tid & 1)) a.partials[(tid >> 1) * nact + blk] = v;
   }
   // arrival: producer stores -> vmcnt(0) -> barrier -> agent release -> ticket; the last block acquires
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -949,7 +975,8 @@ __global__ __launch_bounds__(kTB) void lm_shard_eval(LMArgs a, int k) {
       __shared__ double G[kGramW][kGramW];
       __shared__ double o[3];
       gram_unpack(tid < kGramWords ? a.gmat[tid] : 0.0, G, o);
-      surf_sums_from_gram(s_pt, o, G, (double)sst.corr_surf, s_ssum);
+      if (tid < 64) surf_sums_wave(s_pt, o, G, (double)sst.corr_surf, s_ssum, lane);
+      __syncthreads();
       if (tid < LM_NSUM) s_sums[tid] = s_sums[tid] + s_ssum[tid];
       __syncthreads();
     }
@@ -999,14 +1026,13 @@ __global__ void lm_trace(const LMState* __restrict__ st, const int* __restrict__
 LMArgs make_args(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const CorrSet& cs, const int* d_ns,
                  int ns_ub, LMBuffers& b, unsigned long long* dbg) {
   return LMArgs{d_st, ce.rec.p, ce.valid.p, ce.cap, d_ne, std::max(ne_ub, 0), cs.rec.p, cs.valid.p, cs.cap, d_ns,
-                std::max(ns_ub, 0), b.gmat.p, b.rel.p, b.part.p, b.partials.p, b.sums.p, b.ticket.p, dbg};
+                std::max(ns_ub, 0), b.gmat.p, b.part.p, b.partials.p, b.sums.p, b.ticket.p, dbg};
 }
 }  // namespace
 
 void LMBuffers::reserve(hipStream_t st) {
-  if (rel.p) return;
-  rel.reserve(16);
-  part.reserve((size_t)kRecEvalBlocks * 2 * LM_NSUM);
+  if (part.p) return;
+  part.reserve((size_t)2 * kRecEvalBlocks * 2 * LM_NSUM);
   partials.reserve((size_t)kRecEvalBlocks * LM_NSUM);
   sums.reserve(LM_NSUM);
   ticket.reserve(1);
@@ -1014,7 +1040,6 @@ void LMBuffers::reserve(hipStream_t st) {
   gmat.reserve(kGramWords);
   gcnt.reserve(kGramGroups + 1);
   // tag 0 never matches (epochs start at 8), counters start at zero
-  FLOAM_HIP(hipMemsetAsync(rel.p, 0, sizeof(unsigned long long) * rel.cap, st));
   FLOAM_HIP(hipMemsetAsync(part.p, 0, sizeof(unsigned long long) * part.cap, st));
   FLOAM_HIP(hipMemsetAsync(ticket.p, 0, sizeof(unsigned), st));
   FLOAM_HIP(hipMemsetAsync(gcnt.p, 0, sizeof(unsigned) * gcnt.cap, st));
@@ -1025,11 +1050,11 @@ void lm_solve_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_u
                      const int* d_ns, int ns_ub, int mode, LMBuffers& b, hipStream_t st, unsigned long long* dbg) {
   b.reserve(st);
   const LMArgs a = make_args(d_st, ce, d_ne, ne_ub, cs, d_ns, ns_ub, b, dbg);
-  // all 1 + nblk blocks are co-resident (33 or 129 blocks of 256 threads on 256 CUs)
+  // the active blocks (at most 32 or 128 blocks of 256 threads on 256 CUs) are co-resident
   if (mode & LM_GRAM) {
-    hipLaunchKernelGGL((lm_solve<true, false, double>), dim3(kEdgeEvalBlocks + 1), dim3(kTB), 0, st, a);
+    hipLaunchKernelGGL((lm_solve<true, false, double>), dim3(kEdgeEvalBlocks), dim3(kTB), 0, st, a);
   } else {
-    const dim3 g(kRecEvalBlocks + 1);
+    const dim3 g(kRecEvalBlocks);
     switch (mode & (LM_HUBER | LM_FP32)) {
       case LM_HUBER: hipLaunchKernelGGL((lm_solve<false, true, double>), g, dim3(kTB), 0, st, a); break;
       case LM_FP32: hipLaunchKernelGGL((lm_solve<false, false, float>), g, dim3(kTB), 0, st, a); break;

@@ -113,7 +113,7 @@ constexpr int kGram = kGramW * (kGramW + 1) / 2;   // 91 unique entries (upper t
 constexpr int kGramWords = kGram + 3;              // G + the origin o the records were recentred on
 constexpr int kSurfGeomBlocks = 256;               // fixed surf geometry grid: fixed Gram reduction order
 constexpr int kGramGroups = 8;                     // its partials are reduced in 8 groups of 32, then the groups
-constexpr int kEdgeEvalBlocks = 32;                // edge-only evaluation grid of the Gram solves (fixed order)
+constexpr int kEdgeEvalBlocks = 64;                // edge-only evaluation grid of the Gram solves (fixed order)
 constexpr int kRecEvalBlocks = 128;                // per-record evaluation grid (Huber / fp32; fixed order)
 
 // LM modes: surf half from the Gram matrix (squared loss, fp64), Huber loss, fp32 geometry + residuals / Jacobians
@@ -122,8 +122,7 @@ inline int lm_mode(bool huber, bool fp32) { return (huber || fp32) ? (huber ? LM
 
 // device scratch of the solves (lm.hip)
 struct LMBuffers {
-  DevBuf<unsigned long long> rel;    // resident solve: control -> evaluation release granules
-  DevBuf<unsigned long long> part;   // resident solve: evaluation -> control partial-sum granules
+  DevBuf<unsigned long long> part;   // resident solve: every block's partial-sum granules (two parity slots)
   DevBuf<double> partials;           // sharded evaluation: block partials
   DevBuf<double> sums;               // sharded evaluation: the 29 sums (all-reduced over the ranks in place)
   DevBuf<unsigned> ticket;           // sharded evaluation: arrival ticket (zero between launches)
@@ -221,8 +220,8 @@ void knn_traffic_launch(const LMState* d_st, const QuerySet& q, const Grid& g, C
 
 // ----------------------------------------------------------------------------------------- LM solve (lm.hip)
 // A whole ceres::Solve (iteration zero + up to max_num_iterations = 4 candidates, src/odomEstimationClass.cpp:95-108)
-// in ONE launch on a single GPU: a control block keeps the LM state in registers and runs the Ceres 1.13 control
-// step; resident evaluation blocks keep their records in registers and evaluate each released point.  mode = LM_*.
+// in ONE launch on a single GPU: every block keeps its records in registers, evaluates them, all-gathers the blocks'
+// partial sums and runs the Ceres 1.13 control step itself (the same bits in every block).  mode = LM_*.
 void lm_solve_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const CorrSet& cs,
                      const int* d_ns, int ns_ub, int mode, LMBuffers& b, hipStream_t st,
                      unsigned long long* dbg = nullptr);

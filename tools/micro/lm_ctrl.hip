@@ -1,19 +1,27 @@
-// Latency of the LM control step (lm_logic_wave0) and of the Gram surf sums (surf_sums_from_gram) inside one block,
-// measured with s_memrealtime (100 MHz) over repeated calls on a synthetic, well-conditioned state (diagnostic).
-// Build: hipcc -O3 -std=c++17 -ffp-contract=off --offload-arch=gfx950 -I floam_amd/csrc tools/micro/lm_ctrl.hip
-#include "../../floam_amd/csrc/odom_kernels.hip"
+// Latency of the pieces of one resident-solve evaluation (lm.hip), inside one 256-thread block, measured with
+// s_memrealtime (100 MHz) over repeated calls on a synthetic, well-conditioned state (diagnostic):
+//   control step (iteration zero + step; accepted candidate + step), solve_step, se3_plus, the surf half from G
+//   (one wave), one edge record's residual + Jacobian + accumulation, block_sums over 192 record threads.
+// Build + run (GPU box): hipcc -O3 -std=c++17 -ffp-contract=fast --offload-arch=gfx950 tools/micro/lm_ctrl.hip
+//                        -o /tmp/lm_ctrl && /tmp/lm_ctrl
+#include "../../floam_amd/csrc/lm.hip"
 
 #include <cstdio>
 
 namespace floam {
+namespace {
 __global__ __launch_bounds__(256) void ctrl_bench(unsigned long long* out, double* sink) {
   __shared__ LMState sst;
   __shared__ double sums[LM_NSUM];
   __shared__ double G[kGramW][kGramW];
   __shared__ double o[3];
   __shared__ double ssum[LM_NSUM];
-  const int t = threadIdx.x;
-  unsigned long long acc[4] = {0, 0, 0, 0};
+  __shared__ double red[LM_NSUM * 193];
+  __shared__ double strip[LM_NSUM * kStrips];
+  __shared__ double pt[7];
+  const int t = threadIdx.x, lane = t & 63;
+  unsigned long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const unsigned long long c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
   for (int rep = 0; rep < 64; ++rep) {
     if (t == 0) {
       LMState s{};
@@ -35,53 +43,88 @@ __global__ __launch_bounds__(256) void ctrl_bench(unsigned long long* out, doubl
     if (t < kGramW * kGramW) G[t / kGramW][t % kGramW] = (t / kGramW == t % kGramW) ? 100.0 : 0.5;
     if (t < 3) o[t] = 0.0;
     __syncthreads();
+    LMState s;
+    if (t < 64) s = sst;
     unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    lm_logic_wave0(sst, sums);   // IterationZero + the first step
+    if (t < 64) control_step(s, sst, sums, lane);   // IterationZero + the first step
     __syncthreads();
     unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
     if (t < LM_NSUM) sums[t] = t == 0 ? 49.0 : sums[t];
     __syncthreads();
     unsigned long long t2 = __builtin_amdgcn_s_memrealtime();
-    lm_logic_wave0(sst, sums);   // candidate accepted + the next step
+    if (t < 64) control_step(s, sst, sums, lane);   // candidate accepted + the next step
     __syncthreads();
     unsigned long long t3 = __builtin_amdgcn_s_memrealtime();
-    double x[7];
-#pragma unroll
-    for (int k = 0; k < 7; ++k) x[k] = sst.x[k];
-    surf_sums_from_gram(x, o, G, 20000.0, ssum);
+    if (t < 7) pt[t] = s.x[t];
+    __syncthreads();
     unsigned long long t4 = __builtin_amdgcn_s_memrealtime();
+    if (t < 64) surf_sums_wave(pt, o, G, 20000.0, ssum, lane);
+    __syncthreads();
+    unsigned long long t5 = __builtin_amdgcn_s_memrealtime();
+    double delta[6];
+    bool ok = false;
+    if (t < 64) ok = solve_step(s, delta);
+    __syncthreads();
+    unsigned long long t6 = __builtin_amdgcn_s_memrealtime();
+    double xo[7];
+    if (t < 64) {
+      double d[6];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) d[k] = ok ? delta[k] : 1e-3 * (k + 1);
+      se3_plus(s.x, d, xo);
+    }
+    __syncthreads();
+    unsigned long long t7 = __builtin_amdgcn_s_memrealtime();
+    double accd[LM_NSUM];
+    {
+      double x[7], f[9];
+#pragma unroll
+      for (int k = 0; k < 7; ++k) x[k] = pt[k];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) f[k] = 0.3 * k + 0.01 * t + (k == 3 ? 1.0 : 0.0);
+      eval_records<false, double>(x, true, true, f, 1 << 30, 1, 0, 0, nullptr, nullptr, 0, nullptr, nullptr, 0, accd);
+    }
+    __syncthreads();
+    unsigned long long t8 = __builtin_amdgcn_s_memrealtime();
+    const double v = block_sums<192>(accd, red, strip);
+    __syncthreads();
+    unsigned long long t9 = __builtin_amdgcn_s_memrealtime();
     acc[0] += t1 - t0;
     acc[1] += t3 - t2;
-    acc[2] += t4 - t3;
-    acc[3] += sst.iteration;
-    if (t == 0) sink[rep] = sst.cand[4] + ssum[3];
+    acc[2] += t5 - t4;
+    acc[3] += t6 - t5;
+    acc[4] += t7 - t6;
+    acc[5] += t8 - t7;
+    acc[6] += t9 - t8;
+    acc[7] += s.iteration;
+    if (t < 58) sink[rep * 64 + t] = s.cand[4] + ssum[3] + xo[t % 7] + v;
     __syncthreads();
   }
-  if (t == 0)
-    for (int k = 0; k < 4; ++k) out[k] = acc[k];
+  const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  if (t == 0) {
+    for (int k = 0; k < 8; ++k) out[k] = acc[k];
+    out[8] = c1 - c0;
+    out[9] = r1 - r0;
+  }
 }
+}  // namespace
 }  // namespace floam
 
 int main() {
   unsigned long long* d;
   double* sink;
-  hipMalloc(&d, 32);
-  hipMalloc(&sink, 64 * sizeof(double));
+  hipMalloc(&d, 80);
+  hipMalloc(&sink, 64 * 64 * sizeof(double));
   for (int r = 0; r < 3; ++r) {
     hipLaunchKernelGGL(floam::ctrl_bench, dim3(1), dim3(256), 0, 0, d, sink);
     hipDeviceSynchronize();
   }
-  unsigned long long h[4];
-  hipMemcpy(h, d, 32, hipMemcpyDeviceToHost);
-#ifdef FLOAM_CTRL_STAMPS
-  unsigned long long c[8];
-  hipMemcpyFromSymbol(c, HIP_SYMBOL(floam::g_ctrl_stamps), sizeof(c));
-  const double n = c[3] ? (double)c[3] : 1.0;
-  std::printf("control stamps over %llu steps: solve_step %.2f us, se3_plus %.2f us, gmax+cand %.2f us, whole step %.2f us;"
-              " per phase-0 prologue %.2f us, per phase-1 prologue %.2f us\n", c[3], c[0] / n / 100.0, c[1] / n / 100.0,
-              c[5] / n / 100.0, c[2] / n / 100.0, c[4] / (n / 2) / 100.0, c[6] / (n / 2) / 100.0);
-#endif
-  std::printf("control step: iteration zero + step %.2f us, accept + step %.2f us; surf sums from G %.2f us "
-              "(iterations %llu)\n", h[0] / 64.0 / 100.0, h[1] / 64.0 / 100.0, h[2] / 64.0 / 100.0, h[3]);
+  unsigned long long h[10];
+  hipMemcpy(h, d, 80, hipMemcpyDeviceToHost);
+  std::printf("shader clock during the run: %.0f MHz (s_memtime / s_memrealtime)\n", 100.0 * h[8] / (double)h[9]);
+  const char* names[7] = {"control step (iteration zero + step)", "control step (accept + step)", "surf half (one wave)",
+                          "solve_step", "se3_plus", "edge record eval + accumulate", "block_sums<192>"};
+  for (int k = 0; k < 7; ++k) std::printf("%-40s %6.2f us\n", names[k], h[k] / 64.0 / 100.0);
+  std::printf("(iterations %llu)\n", h[7]);
   return 0;
 }
