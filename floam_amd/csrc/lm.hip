@@ -168,53 +168,52 @@ __device__ __forceinline__ void load_rec(const double* __restrict__ rec, int cap
 // caller publishes it in two halves); no barrier after the last LDS read of `strip`.
 template <int NR>
 constexpr int red_stride() { return NR + 1; }   // odd row stride (in doubles): the 8 rows a wave reads hit 8 bank sets
+
+// the 8 strip sums of component c live in lanes 8c .. 8c + 7 of one wave: a fixed butterfly gives every one of them
+// the same total (each step adds two values, commutatively, so all eight lanes compute the same bits)
+__device__ __forceinline__ double strip8_total(double v) {
+  v += __shfl_xor(v, 1, 8);
+  v += __shfl_xor(v, 2, 8);
+  v += __shfl_xor(v, 4, 8);
+  return v;
+}
+
+// thread sums of the record threads [0, NR) -> the block's 29 sums, fixed order: strip p of component c (8 strips,
+// threads 8c + p) adds threads p, p + 8, p + 16, ... (the strip threads read consecutive LDS words: no bank
+// conflicts), then the 8 strips by strip8_total.  Returns, to threads 8c and 8c + 1 (c < 29), the sum of component c
+// (the caller publishes it in two halves); one block barrier.
 template <int NR>
-__device__ __forceinline__ double block_sums(const double (&acc)[LM_NSUM], double* red /* LDS [LM_NSUM][NR + 1] */,
-                                             double* strip /* LDS [LM_NSUM][kStrips] */) {
-  static_assert(NR % kStrips == 0 && LM_NSUM * kStrips <= kTB, "strip layout");
+__device__ __forceinline__ double block_sums(const double (&acc)[LM_NSUM], double* red /* LDS [LM_NSUM][NR + 1] */) {
+  static_assert(NR % kStrips == 0 && LM_NSUM * kStrips <= kTB && kStrips == 8, "strip layout");
   constexpr int RS = red_stride<NR>();
   const int t = threadIdx.x;
   if (t < NR)
 #pragma unroll
     for (int k = 0; k < LM_NSUM; ++k) red[k * RS + t] = acc[k];
   __syncthreads();
+  double v = 0.0;
   if (t < LM_NSUM * kStrips) {
     const int c = t / kStrips, p = t % kStrips;
-    double v = 0.0;
 #pragma unroll 4
     for (int j = 0; j < NR / kStrips; ++j) v += red[c * RS + j * kStrips + p];
-    strip[c * kStrips + p] = v;
   }
-  __syncthreads();
-  double v = 0.0;
-  if (t < 2 * LM_NSUM) {
-    const int c = t >> 1;
-#pragma unroll
-    for (int p = 0; p < kStrips; ++p) v += strip[c * kStrips + p];
-  }
-  return v;
+  return strip8_total(v);   // (threads >= 232 hold zeros)
 }
 
 // block partials P(c, b) (c < 29, b < nblk) -> 29 sums in out (LDS), fixed order: component c sums 8 strips of
-// consecutive blocks in block order, then the strip totals in order
+// consecutive blocks in block order, then the strip totals by strip8_total
 template <typename Load>
-__device__ __forceinline__ void reduce_blocks(Load P, int nblk, double* strip /* LDS [LM_NSUM][8] */,
-                                              double* out /* LDS [LM_NSUM] */) {
+__device__ __forceinline__ void reduce_blocks(Load P, int nblk, double* out /* LDS [LM_NSUM] */) {
   const int t = threadIdx.x;
+  double v = 0.0;
   if (t < LM_NSUM * 8) {
     const int c = t >> 3, p = t & 7;
     const int per = (nblk + 7) / 8;
     const int b0 = p * per, b1 = min(nblk, b0 + per);
-    double v = 0.0;
     for (int b = b0; b < b1; ++b) v += P(c, b);
-    strip[c * 8 + p] = v;
   }
-  __syncthreads();
-  if (t < LM_NSUM) {
-    double v = 0.0;
-    for (int p = 0; p < 8; ++p) v += strip[t * 8 + p];
-    out[t] = v;
-  }
+  v = strip8_total(v);
+  if (t < LM_NSUM * 8 && (t & 7) == 0) out[t >> 3] = v;
   __syncthreads();
 }
 
@@ -810,8 +809,8 @@ __device__ __forceinline__ void first_record(const LMArgs& a, int i0, int ne, in
 template <bool GRAM, bool HUBER, typename R>
 __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
   constexpr int NR = rec_threads<GRAM>();
-  __shared__ double s_buf[LM_NSUM * red_stride<NR>()];   // thread sums; then the all-gathered partial table (u32)
-  __shared__ double s_strip[LM_NSUM * kStrips];
+  __shared__ double s_buf[LM_NSUM * red_stride<NR>()];   // thread sums
+  __shared__ unsigned s_tab[kRecEvalBlocks * 2 * LM_NSUM];   // the all-gathered block partials (u32 halves)
   __shared__ double s_sums[LM_NSUM];
   __shared__ double s_ssum[LM_NSUM];
   __shared__ double s_pt[7];
@@ -820,16 +819,33 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
   __shared__ double o[3];
   __shared__ int s_done;
   const int nblk = (int)gridDim.x, blk = (int)blockIdx.x, tid = (int)threadIdx.x, lane = tid & 63;
-  const int ne = min(*a.d_ne, a.ne_ub);
-  const int total = ne + (GRAM ? 0 : min(*a.d_ns, a.ns_ub));
-  const int nact = active_blocks<NR>(total, nblk);
-  if (blk >= nact) return;   // no records: nobody waits for this block
-  stage_state(a.st, sst);
+  // the counts, the LM state, G and (GRAM) this thread's edge record — speculatively, for i0 < ne_ub, which is
+  // inside the record arrays — all issued before any is waited on: one memory round trip before the first evaluation
+  static_assert(kStateWords <= kTB, "one state word per thread");
+  const int i0 = blk * NR + tid;
+  const int ne_dev = *a.d_ne;
+  const int ns_dev = GRAM ? 0 : *a.d_ns;
+  const unsigned sw = tid < kStateWords ? reinterpret_cast<const unsigned*>(a.st)[tid] : 0u;
   const double gv = (GRAM && tid < kGramWords) ? a.gmat[tid] : 0.0;
-  const int stride = nact * NR, i0 = blk * NR + tid;
   R f0[9];
   bool has0 = false, edge0 = true;
-  if (tid < NR) first_record<R>(a, i0, ne, total, f0, has0, edge0);
+  uint8_t v0 = 0;
+  if (GRAM) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) f0[k] = R(0);
+    if (tid < NR && i0 < a.ne_ub) {
+      v0 = a.evalid[i0];
+      load_rec<R, EDGE_FIELDS>(a.erec, a.ecap, i0, f0);
+    }
+  }
+  const int ne = min(ne_dev, a.ne_ub);
+  const int total = ne + (GRAM ? 0 : min(ns_dev, a.ns_ub));
+  const int nact = active_blocks<NR>(total, nblk);
+  if (blk >= nact) return;   // no records: nobody waits for this block
+  if (tid < kStateWords) reinterpret_cast<unsigned*>(&sst)[tid] = sw;
+  const int stride = nact * NR;
+  if (GRAM) has0 = tid < NR && i0 < ne && (v0 & 1);
+  else if (tid < NR) first_record<R>(a, i0, ne, total, f0, has0, edge0);
   __syncthreads();
   if (sst.done) return;   // (never after lm_reset)
   if (GRAM) gram_unpack(gv, G, o);
@@ -838,7 +854,7 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
   if (tid < 64) s = sst;
   if (tid < 7) s_pt[tid] = sst.x[tid];   // iteration zero evaluates at x (set by the kNN launch; kernel boundary)
   if (tid == 0) s_done = 0;
-  unsigned* tab = reinterpret_cast<unsigned*>(s_buf);   // [nact][2 * LM_NSUM]
+  unsigned* tab = s_tab;   // [nact][2 * LM_NSUM]
   const int ngr = nact * 2 * LM_NSUM;
   unsigned long long tm[4] = {0, 0, 0, 0};
   int failed_at = -1;   // evaluation whose granules never arrived (never expected)
@@ -858,12 +874,13 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
       for (int k = 0; k < LM_NSUM; ++k) acc[k] = 0.0;
       if (GRAM) surf_sums_wave(s_pt, o, G, (double)sst.corr_surf, s_ssum, lane);   // beside the edge records
     }
-    const double v = block_sums<NR>(acc, s_buf, s_strip);
+    const double v = block_sums<NR>(acc, s_buf);
     unsigned long long* slot = a.part + (size_t)(it & 1) * kRecEvalBlocks * 2 * LM_NSUM;
     const unsigned tag = ep + (unsigned)it;
-    if (tid < 2 * LM_NSUM) {   // 58 granules: the block's sums in 32-bit halves, tagged with this evaluation
+    if (tid < LM_NSUM * kStrips && (tid & 7) < 2) {   // 58 granules: component c in 32-bit halves (lanes 8c, 8c + 1)
+      const int c = tid >> 3, h = tid & 1;
       const unsigned long long b = (unsigned long long)__double_as_longlong(v);
-      put_granule(&slot[blk * 2 * LM_NSUM + tid], granule(tag, (tid & 1) ? (unsigned)(b >> 32) : (unsigned)b));
+      put_granule(&slot[blk * 2 * LM_NSUM + 2 * c + h], granule(tag, h ? (unsigned)(b >> 32) : (unsigned)b));
     }
     const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
     // every active block's granules of this evaluation (this block's own included): kSweep loads in flight per
@@ -879,7 +896,7 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
     reduce_blocks([&](int c, int b) {
       const int g = b * 2 * LM_NSUM + 2 * c;
       return __longlong_as_double((long long)(((unsigned long long)tab[g + 1] << 32) | tab[g]));
-    }, nact, s_strip, s_sums);
+    }, nact, s_sums);
     if (GRAM && tid < LM_NSUM) s_sums[tid] = s_sums[tid] + s_ssum[tid];   // edge + surf
     __syncthreads();
     const unsigned long long t3 = __builtin_amdgcn_s_memrealtime();
@@ -919,7 +936,6 @@ template <bool GRAM, bool HUBER, typename R>
 __global__ __launch_bounds__(kTB) void lm_shard_eval(LMArgs a, int k) {
   constexpr int NR = rec_threads<GRAM>();
   __shared__ double s_buf[LM_NSUM * red_stride<NR>()];
-  __shared__ double s_strip[LM_NSUM * kStrips];
   __shared__ double s_sums[LM_NSUM];
   __shared__ double s_ssum[LM_NSUM];
   __shared__ double s_pt[7];
@@ -956,8 +972,8 @@ __global__ __launch_bounds__(kTB) void lm_shard_eval(LMArgs a, int k) {
 #pragma unroll
       for (int q = 0; q < LM_NSUM; ++q) acc[q] = 0.0;
     }
-    const double v = block_sums<NR>(acc, s_buf, s_strip);
-    if (tid < 2 * LM_NSUM && !(tid & 1)) a.partials[(tid >> 1) * nact + blk] = v;
+    const double v = block_sums<NR>(acc, s_buf);
+    if (tid < LM_NSUM * kStrips && (tid & 7) == 0) a.partials[(tid >> 3) * nact + blk] = v;
   }
   // arrival: producer stores -> vmcnt(0) -> barrier -> agent release -> ticket; the last block acquires
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -970,7 +986,7 @@ __global__ __launch_bounds__(kTB) void lm_shard_eval(LMArgs a, int k) {
   __syncthreads();
   if (!s_last) return;
   if (!done) {
-    reduce_blocks([&](int c, int b) { return a.partials[c * nact + b]; }, nact, s_strip, s_sums);
+    reduce_blocks([&](int c, int b) { return a.partials[c * nact + b]; }, nact, s_sums);
     if (GRAM) {
       __shared__ double G[kGramW][kGramW];
       __shared__ double o[3];

@@ -17,7 +17,6 @@ __global__ __launch_bounds__(256) void ctrl_bench(unsigned long long* out, doubl
   __shared__ double o[3];
   __shared__ double ssum[LM_NSUM];
   __shared__ double red[LM_NSUM * 193];
-  __shared__ double strip[LM_NSUM * kStrips];
   __shared__ double pt[7];
   const int t = threadIdx.x, lane = t & 63;
   unsigned long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -86,7 +85,7 @@ __global__ __launch_bounds__(256) void ctrl_bench(unsigned long long* out, doubl
     }
     __syncthreads();
     unsigned long long t8 = __builtin_amdgcn_s_memrealtime();
-    const double v = block_sums<192>(accd, red, strip);
+    const double v = block_sums<192>(accd, red);
     __syncthreads();
     unsigned long long t9 = __builtin_amdgcn_s_memrealtime();
     acc[0] += t1 - t0;
