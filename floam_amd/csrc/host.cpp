@@ -1115,8 +1115,9 @@ floam_status floam_odom_destroy(floam_odom* o) {
         FLOAM_HIP(hipMemcpy(h, o->dbg_stamps.p, sizeof(h), hipMemcpyDeviceToHost));
         const double n = h[4] ? (double)h[4] : 1.0;
         std::fprintf(stderr, "[floam stamps] %llu solves (block 0, per solve): evaluate + publish %.2f us, all-gather "
-                     "%.2f us, reduce %.2f us, control step %.2f us\n", h[4],
-                     h[0] / n / 100.0, h[1] / n / 100.0, h[2] / n / 100.0, h[3] / n / 100.0);
+                     "%.2f us, reduce %.2f us, control step %.2f us; prologue %.2f us, block 0 first instruction to "
+                     "state written %.2f us\n", h[4], h[0] / n / 100.0, h[1] / n / 100.0, h[2] / n / 100.0,
+                     h[3] / n / 100.0, h[5] / n / 100.0, h[6] / n / 100.0);
       }
       if (o->side) {
         (void)hipStreamSynchronize(o->side);

@@ -427,9 +427,10 @@ __device__ __forceinline__ void se3_plus(const double (&x)[7], const double (&d)
     for (int i = 0; i < 3; ++i)
 #pragma unroll
       for (int j = 0; j < 3; ++j) O2[i][j] = O[i][0] * O[0][j] + O[i][1] * O[1][j] + O[i][2] * O[2][j];
-    double st, ct;
-    sincos(theta, &st, &ct);
-    const double c1 = (1 - ct) * (rt * rt);
+    // sin(theta), 1 - cos(theta) from the half angle (one sincos per exponential instead of two: the control step is
+    // a single wave's fp64 instruction stream, 4 cycles an instruction)
+    const double st = 2.0 * sh * ch, omc = 2.0 * sh * sh;
+    const double c1 = omc * (rt * rt);
     const double c2 = (theta - st) * (rt * rt * rt);
 #pragma unroll
     for (int i = 0; i < 3; ++i)
@@ -819,6 +820,7 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
   __shared__ double o[3];
   __shared__ int s_done;
   const int nblk = (int)gridDim.x, blk = (int)blockIdx.x, tid = (int)threadIdx.x, lane = tid & 63;
+  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
   // the counts, the LM state, G and (GRAM) this thread's edge record — speculatively, for i0 < ne_ub, which is
   // inside the record arrays — all issued before any is waited on: one memory round trip before the first evaluation
   static_assert(kStateWords <= kTB, "one state word per thread");
@@ -857,6 +859,7 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
   unsigned* tab = s_tab;   // [nact][2 * LM_NSUM]
   const int ngr = nact * 2 * LM_NSUM;
   unsigned long long tm[4] = {0, 0, 0, 0};
+  const unsigned long long t_loop = __builtin_amdgcn_s_memrealtime();
   int failed_at = -1;   // evaluation whose granules never arrived (never expected)
   for (int it = 0; it < 5; ++it) {
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -918,12 +921,14 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
   if (tid == 0) store_state_core(sst, s);
   __syncthreads();
   publish_state(sst, a.st);
-  if (a.dbg && tid == 0) {   // diagnostic stamps (100 MHz): evaluate + publish, all-gather, reduce, control step
-    atomicAdd(&a.dbg[0], tm[0]);
+  if (a.dbg && tid == 0) {   // diagnostic stamps (100 MHz): evaluate + publish, all-gather, reduce, control step,
+    atomicAdd(&a.dbg[0], tm[0]);   // then the prologue (first instruction -> loop) and the write-back
     atomicAdd(&a.dbg[1], tm[1]);
     atomicAdd(&a.dbg[2], tm[2]);
     atomicAdd(&a.dbg[3], tm[3]);
     atomicAdd(&a.dbg[4], 1ull);
+    atomicAdd(&a.dbg[5], t_loop - t_start);
+    atomicAdd(&a.dbg[6], __builtin_amdgcn_s_memrealtime() - t_start);
   }
 }
 
