@@ -440,6 +440,16 @@ __device__ __forceinline__ void wave_lds_order() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// agent-scope relaxed 8-B store / load (global_store / global_load ... sc1): the hand-off forms of the Gram reduction
+__device__ __forceinline__ void sc1_store(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double sc1_load(const double* p) {
+  return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
+                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
 struct CorrArgs {
   const PointRec* q;       // downsampled scan points (sensor frame)
   const int* d_n;          // device count
@@ -909,20 +919,20 @@ __global__ __launch_bounds__(kTB) void geom_kernel(LMState* __restrict__ st, Cor
     double v = s_part[0][threadIdx.x];
 #pragma unroll
     for (int k = 1; k < kTB / 64; ++k) v += s_part[k][threadIdx.x];
-    gpart[sb * kGram + threadIdx.x] = v;
+    sc1_store(&gpart[sb * kGram + threadIdx.x], v);
   }
-  // G of the solve, reduced by the last-arriving blocks (fixed order: the 32 blocks of a group, then the 8 groups):
-  // producer stores -> vmcnt(0) -> barrier -> agent release -> ticket; the block whose ticket is last acquires
+  // G of the solve, reduced by the last-arriving blocks (fixed order: the 32 blocks of a group, then the 8 groups),
+  // without agent fences (MI355X_MICROARCH.md "Hand-offs measured with sc1 loads in place of the acquire", first
+  // row): every partial is stored sc1 and loaded sc1; each storing wave drains its stores (vmcnt(0)) before the
+  // block barrier behind which one lane adds to the group's ticket; the block whose add comes last reads the group
+  // after its add has returned (its other waves after the barrier).  (Two release / acquire fence pairs on the
+  // chain cost ~1.7 us each.)
   constexpr int per = kSurfGeomBlocks / kGramGroups;
   __shared__ int s_last;
   const int grp = sb / per;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    s_last = atomicAdd(&gcnt[grp], 1u) == (unsigned)(per - 1);
-    if (s_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  }
+  if (threadIdx.x == 0) s_last = atomicAdd(&gcnt[grp], 1u) == (unsigned)(per - 1);
   __syncthreads();
   if (!s_last) return;
   double* gpart2 = gpart + kSurfGeomBlocks * kGram;   // [8][91] group partials
@@ -930,24 +940,26 @@ __global__ __launch_bounds__(kTB) void geom_kernel(LMState* __restrict__ st, Cor
     double v = 0.0;
     double gp[per];   // all loads in flight before the in-order sum
 #pragma unroll
-    for (int k = 0; k < per; ++k) gp[k] = gpart[(grp * per + k) * kGram + threadIdx.x];
+    for (int k = 0; k < per; ++k) gp[k] = sc1_load(&gpart[(grp * per + k) * kGram + threadIdx.x]);
 #pragma unroll
     for (int k = 0; k < per; ++k) v += gp[k];
-    gpart2[grp * kGram + threadIdx.x] = v;
+    sc1_store(&gpart2[grp * kGram + threadIdx.x], v);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
     gcnt[grp] = 0u;   // every block of the group has arrived (next launch: kernel boundary)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     s_last = atomicAdd(&gcnt[kGramGroups], 1u) == (unsigned)(kGramGroups - 1);
-    if (s_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
   __syncthreads();
   if (!s_last) return;
   if (threadIdx.x < kGram) {
-    double v = gpart2[threadIdx.x];
-    for (int k = 1; k < kGramGroups; ++k) v += gpart2[k * kGram + threadIdx.x];
+    double gp[kGramGroups];
+#pragma unroll
+    for (int k = 0; k < kGramGroups; ++k) gp[k] = sc1_load(&gpart2[k * kGram + threadIdx.x]);
+    double v = gp[0];
+#pragma unroll
+    for (int k = 1; k < kGramGroups; ++k) v += gp[k];
     gmat[threadIdx.x] = v;
   } else if (threadIdx.x < kGram + 3) {
     gmat[threadIdx.x] = o[threadIdx.x - kGram];   // the origin the records were recentred on
