@@ -71,6 +71,11 @@ def hbm_traffic(kernel_substr, config):
 
 
 def main():
+    # stdout carries exactly the one JSON line: the libraries' own stdout chatter (gloo's peer-connection notice,
+    # RCCL's version banner) is sent to stderr at the file-descriptor level, before any of them initialises
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=60)
@@ -363,7 +368,7 @@ def main():
             out["same_config_1gpu"] = {"value": same_cfg_1gpu, "unit": "scans/s",
                                        "note": f"{cfg} unsharded on rank 0's GPU before the sharded run"}
         line = json.dumps(out)
-        print(line, flush=True)
+        print(line, file=json_out, flush=True)
         if args.json_out:
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
