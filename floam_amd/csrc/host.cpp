@@ -264,6 +264,7 @@ struct floam_odom {
   // side stream as soon as the scan's features exist, overlapped with the previous update (double-buffered by parity)
   hipStream_t side = nullptr;
   hipEvent_t side_ev[2] = {nullptr, nullptr};     // call-1 buffers of a parity consumed (recorded on the main stream)
+  hipEvent_t pre_ev = nullptr;                    // the side stream's call-1 VoxelGrids done (both clouds' producers)
   bool side_ev_rec[2] = {false, false};
   DevBuf<PointRec> pE[2], pS[2];
   DevBuf<int> pcnt[2];
@@ -429,11 +430,16 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
                       predict ? o->ds.p : nullptr);
     o->grid_dirty = false;
   }
-  for (const floam_cloud*& c : o->late_wait)
-    if (c) {
-      cloud_on_main(c);
+  if (o->late_wait[0]) {   // one wait orders the main stream after the side stream's VoxelGrids and, through them,
+    FLOAM_HIP(hipStreamWaitEvent(st, o->pre_ev, 0));   // after both clouds' producers (odom_prevoxel)
+    for (const floam_cloud*& c : o->late_wait) {
+      if (!c) continue;
+      auto* cc = const_cast<floam_cloud*>(c);
+      cc->last_stream = st;
+      cc->ev_valid = false;
       c = nullptr;
     }
+  }
   o->lm.reserve(1);
   o->lmb.reserve(st);
   if (!o->dbg_stamps.p && std::getenv("FLOAM_DEBUG_STAMPS")) {
@@ -716,11 +722,12 @@ floam_status odom_update(floam_odom* o, const floam_cloud* edge, const floam_clo
 // Call 1's VoxelGrids (edge cloud at the edge and the surf leaf, Q4) on the side stream, ordered after the cloud's
 // producer (the feature extraction) and after the update that last used this parity's buffers; the main stream
 // orders itself after it through the cloud (cloud_on_main).  Not used while an update is captured into a graph.
-void odom_prevoxel(floam_odom* o, floam_cloud* edge) {
+void odom_prevoxel(floam_odom* o, floam_cloud* edge, floam_cloud* surf) {
   if (o->use_graph) return;
   if (!o->side) {
     FLOAM_HIP(hipStreamCreateWithFlags(&o->side, hipStreamNonBlocking));
     for (auto& e : o->side_ev) FLOAM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    FLOAM_HIP(hipEventCreateWithFlags(&o->pre_ev, hipEventDisableTiming));
   }
   const int par = o->pre_par;
   o->pre_par ^= 1;
@@ -730,12 +737,14 @@ void odom_prevoxel(floam_odom* o, floam_cloud* edge) {
   o->pcnt[par].reserve(2);
   if (o->side_ev_rec[par]) FLOAM_HIP(hipStreamWaitEvent(o->side, o->side_ev[par], 0));
   cloud_on(edge, o->side);
+  cloud_on(surf, o->side);   // (not used here: so that one event below orders the main stream after both producers)
   VoxelJob je, js;
   je.part0 = edge->pts.p; je.d_n0 = edge->count.p; je.n0_ub = ne_ub; je.leaf = o->leafE;
   je.out = o->pE[par].p; je.d_out = o->pcnt[par].p + 0;
   js.part0 = edge->pts.p; js.d_n0 = edge->count.p; js.n0_ub = ne_ub; js.leaf = o->leafS;
   js.out = o->pS[par].p; js.d_out = o->pcnt[par].p + 1;
   voxel2_launch(o->vs1, je, js, o->side);
+  FLOAM_HIP(hipEventRecord(o->pre_ev, o->side));
   o->pre_valid = par;
 }
 
@@ -759,15 +768,15 @@ floam_status odom_update_deskew(floam_odom* o, floam_cloud* edge, floam_cloud* s
       deskew_bridge_launch(o->lm.p, o->ds.p, o->lp.scan_period, edge->pts.p, edge->count.p, ne_ub, surf->pts.p,
                            surf->count.p, ns_ub, ctx.stream, g1);
     }
-    if (pre >= 0) {   // the side stream may refill this parity's buffers once call 1 has run, including the deferred
-      FLOAM_HIP(hipEventRecord(o->side_ev[pre], ctx.stream));   // status gather in deskew_bridge (reads pcnt[pre])
-      o->side_ev_rec[pre] = true;
-    }
     if (o->optimization_count > 2) o->optimization_count--;
     odom_issue(o, ctx, edge, surf, ne_ub, ns_ub, o->ds.p->x0[1], 2 * ring + 1,
                GATHER_FINISH | GATHER_AFTER_MID | gather_keyframe_mode());
     size_t addE = 0, addS = 0;
     odom_map_update(o, ctx, ne_ub, ns_ub, addE, addS);
+    if (pre >= 0) {   // the side stream may refill this parity's buffers once this update has run: recorded at its
+      FLOAM_HIP(hipEventRecord(o->side_ev[pre], ctx.stream));   // end (an event record between two launches of
+      o->side_ev_rec[pre] = true;                               // the chain costs the stream a few us)
+    }
     return odom_end(o, ctx, ring, 2, 1, addE, addS, captured, 1);
   } catch (...) {
     odom_capture_abort(ctx);
@@ -1122,6 +1131,7 @@ floam_status floam_odom_destroy(floam_odom* o) {
       if (o->side) {
         (void)hipStreamSynchronize(o->side);
         for (auto& e : o->side_ev) (void)hipEventDestroy(e);
+        if (o->pre_ev) (void)hipEventDestroy(o->pre_ev);
         (void)hipStreamDestroy(o->side);
       }
       if (o->comm) ncclCommDestroy(o->comm);
@@ -1169,7 +1179,7 @@ floam_status floam_odom_update(floam_odom* o, const floam_cloud* edge, const flo
 floam_status floam_odom_update_selector(floam_odom* o, floam_cloud* edge, floam_cloud* surf, int deskew) {
   return guarded([&] {
     if (!o || !edge || !surf) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
-    if (deskew && edge != surf) odom_prevoxel(o, edge);
+    if (deskew && edge != surf) odom_prevoxel(o, edge, surf);
     if (deskew && o->pre_valid >= 0) {   // ordered after the grid rebuild (odom_issue)
       o->late_wait[0] = edge;
       o->late_wait[1] = surf;
