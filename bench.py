@@ -283,6 +283,12 @@ def main():
                 ks = timed.get(sub)
                 if ks is not None and ks[0]:
                     roof[key] = round(ks[1] / ks[0] * 1e3, 2)
+            # the north star prices the kNN search against HBM; the largest kernel by time per scan is the LM solve
+            # (4 launches of ~36 us at C3), which moves < 1 MB per launch and is bound by its serial chain (one
+            # hand-off + one fp64 control step per LM evaluation), not by a roofline
+            roof["largest_kernel_by_time"] = {"kernel": "lm_solve", "avg_us": roof.get("lm_solve_avg_us"),
+                                              "bound": "latency (serial fp64 control step + one inter-block "
+                                                       "hand-off per LM evaluation)"}
 
     secondary = None
     if rank == 0 and world == 1 and not args.no_secondary:
