@@ -58,21 +58,9 @@ __device__ __forceinline__ void list_append(int* __restrict__ list, int* __restr
   if (take) list[base + __popcll(b & ((1ull << lane) - 1ull))] = slot;
 }
 
-__global__ __launch_bounds__(kTB) void grid_clear(GridJob E, GridJob S) {
-  const GridJob& J = blockIdx.y == 0 ? E : S;
-  const int stride = gridDim.x * blockDim.x;
-  const int t0 = blockIdx.x * blockDim.x + threadIdx.x;
-  if (J.full_clear) {
-    const int size = (int)J.mask + 1;
-    for (int t = t0; t < size; t += stride) J.coarse[t] = empty_coarse();
-  } else {
-    const int nc = J.counters[1 + (J.parity ^ 1)];
-    for (int t = t0; t < nc; t += stride) J.coarse[J.clist_old[t]] = empty_coarse();
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    J.counters[0] = 0;
-    J.counters[1 + J.parity] = 0;
-  }
+__global__ __launch_bounds__(kTB) void grid_clear(GridClearDev E, GridClearDev S) {
+  grid_clear_part(blockIdx.y == 0 ? E : S, blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x,
+                  blockIdx.x == 0 && threadIdx.x == 0);
 }
 
 // Map points are in voxel order, so a wave's 64 points fall in a handful of coarse cells: the wave groups its lanes
@@ -213,6 +201,10 @@ void reserve_grid(Grid& g, int ub) {
   }
 }
 
+GridClearDev clear_job(const Grid& g) {
+  return GridClearDev{g.coarse.p, g.clist[g.parity ^ 1].p, g.counters.p, g.parity, g.fresh ? 1 : 0, g.mask};
+}
+
 GridJob make_job(Grid& g, const PointRec* map, const int* d_m, int m_ub) {
   const int p = g.parity;
   return GridJob{map, d_m, m_ub, g.pts.p, g.coarse.p, g.where.p, g.xyz.p, g.clist[p].p, g.clist[p ^ 1].p,
@@ -220,21 +212,38 @@ GridJob make_job(Grid& g, const PointRec* map, const int* d_m, int m_ub) {
 }
 }  // namespace
 
+GridClearDev grid_clear_prepare(Grid& g, int ub, hipStream_t st) {
+  reserve_grid(g, std::max(ub, 1));
+  if (g.fresh) FLOAM_HIP(hipMemsetAsync(g.counters.p, 0, sizeof(int) * 8, st));
+  const GridClearDev c = clear_job(g);
+  g.fresh = false;
+  g.precleared = true;
+  return c;
+}
+
 void grid_build_launch(Grid& gE, const PointRec* mapE, const int* d_mE, int mE_ub, Grid& gS, const PointRec* mapS,
-                       const int* d_mS, int mS_ub, hipStream_t st, OdomDev* predict) {
+                       const int* d_mS, int mS_ub, hipStream_t st, OdomDev* predict, bool precleared) {
   mE_ub = std::max(mE_ub, 1);
   mS_ub = std::max(mS_ub, 1);
-  reserve_grid(gE, mE_ub);
-  reserve_grid(gS, mS_ub);
-  if (gE.fresh) FLOAM_HIP(hipMemsetAsync(gE.counters.p, 0, sizeof(int) * 8, st));
-  if (gS.fresh) FLOAM_HIP(hipMemsetAsync(gS.counters.p, 0, sizeof(int) * 8, st));
+  // a build cleared in advance was sized for at least this map (the upper bounds only shrink once the update that
+  // added the points is collected); otherwise the clear runs here (again: clearing the same entries is idempotent)
+  precleared = precleared && gE.precleared && gS.precleared && (1 << gE.bits) >= 2 * mE_ub &&
+               (1 << gS.bits) >= 2 * mS_ub;
+  if (!precleared) {
+    reserve_grid(gE, mE_ub);
+    reserve_grid(gS, mS_ub);
+    if (gE.fresh) FLOAM_HIP(hipMemsetAsync(gE.counters.p, 0, sizeof(int) * 8, st));
+    if (gS.fresh) FLOAM_HIP(hipMemsetAsync(gS.counters.p, 0, sizeof(int) * 8, st));
+  }
   const GridJob E = make_job(gE, mapE, d_mE, mE_ub), S = make_job(gS, mapS, d_mS, mS_ub);
-  const bool full = gE.fresh || gS.fresh;
-  const int tmax = (int)std::max(gE.mask, gS.mask) + 1;
-  const unsigned tb = full ? std::min(div_up(tmax, kTB), 2048u) : std::min(div_up(std::max(mE_ub, mS_ub), kTB), 512u);
+  if (!precleared) {
+    const bool full = gE.fresh || gS.fresh;
+    const int tmax = (int)std::max(gE.mask, gS.mask) + 1;
+    const unsigned tb = full ? std::min(div_up(tmax, kTB), 2048u) : std::min(div_up(std::max(mE_ub, mS_ub), kTB), 512u);
+    hipLaunchKernelGGL(grid_clear, dim3(tb, 2), dim3(kTB), 0, st, clear_job(gE), clear_job(gS));
+    FLOAM_LAUNCH_CHECK();
+  }
   const unsigned pb = std::min(div_up(std::max(mE_ub, mS_ub), kTB), 2048u);
-  hipLaunchKernelGGL(grid_clear, dim3(tb, 2), dim3(kTB), 0, st, E, S);
-  FLOAM_LAUNCH_CHECK();
   hipLaunchKernelGGL(grid_count, dim3(pb, 2), dim3(kTB), 0, st, E, S, predict);
   FLOAM_LAUNCH_CHECK();
   hipLaunchKernelGGL(grid_alloc, dim3(std::min(pb, 512u), 2), dim3(kTB), 0, st, E, S);
@@ -243,6 +252,7 @@ void grid_build_launch(Grid& gE, const PointRec* mapE, const int* d_mE, int mE_u
   FLOAM_LAUNCH_CHECK();
   for (Grid* g : {&gE, &gS}) {
     g->fresh = false;
+    g->precleared = false;
     g->parity ^= 1;
   }
 }

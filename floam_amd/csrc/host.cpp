@@ -402,9 +402,29 @@ void allreduce_sums(floam_odom* o, DeviceCtx& ctx) {
 // pre >= 0: the call's clouds were downsampled on the side stream into the parity-`pre` buffers (odom_prevoxel)
 // predict: the update's prediction (odom_predict) is issued here — inside the grid rebuild's first launch when the
 // maps changed, else as a launch of its own — before anything reads x0_dev
+struct MapUpdatePlan {
+  VoxelJob je, js;
+  int ne_ub = 0, ns_ub = 0;
+  VoxelFused vf;   // the bounding-box stage, run by the status gather before the update
+};
+
+// downSamplingToMap's two VoxelGrids of one call (:137-142): edge cloud at the edge leaf, surf cloud at the surf leaf
+void call_voxel_jobs(floam_odom* o, const floam_cloud* edge, const floam_cloud* surf, int ne_ub, int ns_ub, VoxelJob& je,
+                     VoxelJob& js) {
+  o->dE.reserve(std::max(ne_ub, 1));
+  o->dS.reserve(std::max(ns_ub, 1));
+  o->cnt.reserve(4);
+  je.part0 = edge->pts.p; je.d_n0 = edge->count.p; je.n0_ub = ne_ub; je.leaf = o->leafE;
+  je.out = o->dE.p; je.d_out = o->cnt.p + 0;
+  js.part0 = surf->pts.p; js.d_n0 = surf->count.p; js.n0_ub = ns_ub; js.leaf = o->leafS;
+  js.out = o->dS.p; js.d_out = o->cnt.p + 1;
+}
+
+// vox_fused: the call's VoxelGrids' bounding-box stage already ran (deskew_bridge); map: the map update that follows
+// this call (its bounding-box stage and the next grid builds' clears run in the status gather)
 void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const floam_cloud* surf, int ne_ub, int ns_ub,
                 const double* x0_dev, int slot, int gather_mode, int pre = -1, bool predict = false,
-                GatherArgs* defer_gather = nullptr) {
+                GatherArgs* defer_gather = nullptr, bool vox_fused = false, const MapUpdatePlan* map = nullptr) {
   hipStream_t st = ctx.stream;
   if (predict && !o->grid_dirty) odom_predict_launch(o->ds.p, st);
   o->dE.reserve(std::max(ne_ub, 1));
@@ -417,17 +437,14 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
     ProfScope ps(ctx, "voxel_downsample", FLOAM_PROF_CLOUD);
     // VelToIntensityCopy + downSamplingToMap (:53-54, :75, :137-142): both grids in one pipeline
     VoxelJob je, js;
-    je.part0 = edge->pts.p; je.d_n0 = edge->count.p; je.n0_ub = ne_ub; je.leaf = o->leafE;
-    je.out = o->dE.p; je.d_out = o->cnt.p + 0;
-    js.part0 = surf->pts.p; js.d_n0 = surf->count.p; js.n0_ub = ns_ub; js.leaf = o->leafS;
-    js.out = o->dS.p; js.d_out = o->cnt.p + 1;
-    voxel2_launch(o->vs, je, js, st);
+    call_voxel_jobs(o, edge, surf, ne_ub, ns_ub, je, js);
+    voxel2_launch(o->vs, je, js, st, nullptr, vox_fused);
   }
   const int mE_ub = (int)o->mapE_n, mS_ub = (int)o->mapS_n;   // exact or upper bounds
   if (o->grid_dirty) {
     ProfScope ps(ctx, "grid_build", FLOAM_PROF_CLOUD);
     grid_build_launch(o->gE, o->mapE.pts.p, o->mapE.count.p, mE_ub, o->gS, o->mapS.pts.p, o->mapS.count.p, mS_ub, st,
-                      predict ? o->ds.p : nullptr);
+                      predict ? o->ds.p : nullptr, true);
     o->grid_dirty = false;
   }
   if (o->late_wait[0]) {   // one wait orders the main stream after the side stream's VoxelGrids and, through them,
@@ -501,8 +518,14 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
     *defer_gather = GatherArgs{dcnt, o->mapE.count.p, o->mapS.count.p, edge->fe_status, o->h_ustat.p + slot};
     return;
   }
+  GridClearDev gc[2];
+  if (map) {   // (the grids' last readers, this call's kNN launches, are issued: the tables may be resized now)
+    gc[0] = grid_clear_prepare(o->gE, (int)o->mapE_n + map->ne_ub, st);
+    gc[1] = grid_clear_prepare(o->gS, (int)o->mapS_n + map->ns_ub, st);
+  }
   gather_status_launch(o->lm.p, dcnt, o->mapE.count.p, o->mapS.count.p, edge->fe_status,
-                       prof_knn ? o->prof_bytes.p : nullptr, o->h_ustat.p + slot, o->ds.p, gather_mode, st);
+                       prof_knn ? o->prof_bytes.p : nullptr, o->h_ustat.p + slot, o->ds.p, gather_mode, st,
+                       map ? &map->vf : nullptr, map ? gc : nullptr);
   if (prof_knn) FLOAM_HIP(hipMemsetAsync(o->prof_bytes.p, 0, sizeof(unsigned long long) * 2, st));
 }
 
@@ -671,24 +694,43 @@ int gather_keyframe_mode() {   // KeyFrameUpdate's process-wide `first` flag (Q6
 // addPointsToMap (:253-294), issued unconditionally and gated on the device by the keyframe decision (a skipped
 // update copies the maps unchanged): transform + append + CropBox + VoxelGrid of both maps with the optimised pose
 // (lm->x), one pipeline.  Returns the upper bounds of the points it may add.
-void odom_map_update(floam_odom* o, DeviceCtx& ctx, int ne_ub, int ns_ub, size_t& addE, size_t& addS) {
+MapUpdatePlan odom_map_plan(floam_odom* o, DeviceCtx& ctx, int ne_ub, int ns_ub) {
   hipStream_t st = ctx.stream;
-  ProfScope ps(ctx, "map_update", FLOAM_PROF_CLOUD);
+  MapUpdatePlan P;
+  P.ne_ub = ne_ub;
+  P.ns_ub = ns_ub;
   const int ubS = (int)o->mapS_n + ns_ub, ubE = (int)o->mapE_n + ne_ub;
   cloud_reserve(&o->mapS_next, std::max(ubS, 1), 0, st);
   cloud_reserve(&o->mapE_next, std::max(ubE, 1), 0, st);
-  VoxelJob je, js;
+  o->dE.reserve(std::max(ne_ub, 1));
+  o->dS.reserve(std::max(ns_ub, 1));
+  o->cnt.reserve(4);
+  o->lm.reserve(1);
+  VoxelJob& je = P.je;
+  VoxelJob& js = P.js;
   je.part0 = o->mapE.pts.p; je.d_n0 = o->mapE.count.p; je.n0_ub = (int)o->mapE_n;
   je.part1 = o->dE.p; je.d_n1 = o->cnt.p + 0; je.n1_ub = ne_ub;
   je.pose = o->lm.p->x; je.leaf = o->leafE; je.out = o->mapE_next.pts.p; je.d_out = o->mapE_next.count.p;
   js.part0 = o->mapS.pts.p; js.d_n0 = o->mapS.count.p; js.n0_ub = (int)o->mapS_n;
   js.part1 = o->dS.p; js.d_n1 = o->cnt.p + 1; js.n1_ub = ns_ub;
   js.pose = o->lm.p->x; js.leaf = o->leafS; js.out = o->mapS_next.pts.p; js.d_out = o->mapS_next.count.p;
-  voxel2_launch(o->vs, je, js, st, &o->ds.p->kf_flag);
+  P.vf = voxel2_prepare(o->vs, je, js, st);
+  return P;
+}
+
+// addPointsToMap (:253-294), issued unconditionally and gated on the device by the keyframe decision (a skipped
+// update copies the maps unchanged): transform + append + CropBox + VoxelGrid of both maps with the optimised pose
+// (lm->x), one pipeline whose bounding-box stage ran in the status gather (P.vf).  Returns the upper bounds of the
+// points it may add.
+void odom_map_update(floam_odom* o, DeviceCtx& ctx, const MapUpdatePlan& P, size_t& addE, size_t& addS) {
+  hipStream_t st = ctx.stream;
+  ProfScope ps(ctx, "map_update", FLOAM_PROF_CLOUD);
+  const int ubS = (int)o->mapS_n + P.ns_ub, ubE = (int)o->mapE_n + P.ne_ub;
+  voxel2_launch(o->vs, P.je, P.js, st, &o->ds.p->kf_flag, true);
   cloud_swap(&o->mapE, &o->mapE_next);
   cloud_swap(&o->mapS, &o->mapS_next);
-  addE = (size_t)ne_ub;
-  addS = (size_t)ns_ub;
+  addE = (size_t)P.ne_ub;
+  addS = (size_t)P.ns_ub;
   o->mapS_n = (size_t)ubS;   // upper bounds until the update is collected
   o->mapE_n = (size_t)ubE;
   o->mapS.host_count_valid = false;
@@ -708,10 +750,13 @@ floam_status odom_update(floam_odom* o, const floam_cloud* edge, const floam_clo
   try {
     if (o->optimization_count > 2) o->optimization_count--;
     const bool update_map = type == FLOAM_VANILLA || type == FLOAM_REFINEMENT_AND_UPDATE;
+    MapUpdatePlan mp;
+    if (update_map) mp = odom_map_plan(o, ctx, ne_ub, ns_ub);
     odom_issue(o, ctx, edge, surf, ne_ub, ns_ub, o->ds.p->x0[0], 2 * ring,
-               GATHER_FINISH | (update_map ? gather_keyframe_mode() : 0), -1, true);
+               GATHER_FINISH | (update_map ? gather_keyframe_mode() : 0), -1, true, nullptr, false,
+               update_map ? &mp : nullptr);
     size_t addE = 0, addS = 0;
-    if (update_map) odom_map_update(o, ctx, ne_ub, ns_ub, addE, addS);
+    if (update_map) odom_map_update(o, ctx, mp, addE, addS);
     return odom_end(o, ctx, ring, 1, update_map ? 0 : -1, addE, addS, captured, 0);
   } catch (...) {
     odom_capture_abort(ctx);
@@ -763,16 +808,26 @@ floam_status odom_update_deskew(floam_odom* o, floam_cloud* edge, floam_cloud* s
     if (o->optimization_count > 2) o->optimization_count--;
     GatherArgs g1;
     odom_issue(o, ctx, edge, edge, ne_ub, ne_ub, o->ds.p->x0[0], 2 * ring, 0, pre, true, &g1);
+    // the second call's VoxelGrids get their bounding boxes from deskew_bridge, which writes their input (distinct
+    // clouds; aliased ones are shifted twice per point by one thread and keep the separate stage)
+    const bool fuse = edge != surf;
+    VoxelFused vf2{};
+    if (fuse) {
+      VoxelJob je, js;
+      call_voxel_jobs(o, edge, surf, ne_ub, ns_ub, je, js);
+      vf2 = voxel2_prepare(o->vs, je, js, ctx.stream);
+    }
     {
       ProfScope ps(ctx, "deskew", FLOAM_PROF_CLOUD);
       deskew_bridge_launch(o->lm.p, o->ds.p, o->lp.scan_period, edge->pts.p, edge->count.p, ne_ub, surf->pts.p,
-                           surf->count.p, ns_ub, ctx.stream, g1);
+                           surf->count.p, ns_ub, ctx.stream, g1, fuse ? &vf2 : nullptr);
     }
     if (o->optimization_count > 2) o->optimization_count--;
+    MapUpdatePlan mp = odom_map_plan(o, ctx, ne_ub, ns_ub);
     odom_issue(o, ctx, edge, surf, ne_ub, ns_ub, o->ds.p->x0[1], 2 * ring + 1,
-               GATHER_FINISH | GATHER_AFTER_MID | gather_keyframe_mode());
+               GATHER_FINISH | GATHER_AFTER_MID | gather_keyframe_mode(), -1, false, nullptr, fuse, &mp);
     size_t addE = 0, addS = 0;
-    odom_map_update(o, ctx, ne_ub, ns_ub, addE, addS);
+    odom_map_update(o, ctx, mp, addE, addS);
     if (pre >= 0) {   // the side stream may refill this parity's buffers once this update has run: recorded at its
       FLOAM_HIP(hipEventRecord(o->side_ev[pre], ctx.stream));   // end (an event record between two launches of
       o->side_ev_rec[pre] = true;                               // the chain costs the stream a few us)

@@ -1039,31 +1039,55 @@ __global__ __launch_bounds__(kTB) void deskew_bridge(const LMState* __restrict__
                                                      double period, PointRec* __restrict__ edge,
                                                      const int* __restrict__ d_ne, int ne_ub,
                                                      PointRec* __restrict__ surf, const int* __restrict__ d_ns,
-                                                     int ns_ub, int aliased, GatherArgs g) {
-  if (g.out && blockIdx.x == 0) gather_block(st, g.dcnt, g.mapE_count, g.mapS_count, g.fe_status, nullptr, g.out, s, 0);
+                                                     int ns_ub, int aliased, GatherArgs g, float* __restrict__ vpart,
+                                                     unsigned* __restrict__ vctl) {
+  const bool lead = blockIdx.x == 0 && blockIdx.y == 0;
+  if (g.out && lead) gather_block(st, g.dcnt, g.mapE_count, g.mapS_count, g.fe_status, nullptr, g.out, s, 0);
   double x1[7];
 #pragma unroll
   for (int k = 0; k < 7; ++k) x1[k] = st->x[k];
   const double* t0 = s->last_odom.t;   // the pose before the first call (read-only in this launch)
   // GetVelocity (include/odomEstimationClass.h:78): (odom.translation() - last_odom.translation()) / scan_period
   const double vx = (x1[4] - t0[0]) / period, vy = (x1[5] - t0[1]) / period, vz = (x1[6] - t0[2]) / period;
-  // aliased (edge and surf are one cloud): the reference's two CompensateVelocity calls (src/odomEstimationClass.cpp:
-  // 42-43) shift every point twice, one after the other, so one thread applies both shifts to its point
-  const int ne = min(*d_ne, ne_ub), ns = aliased ? 0 : min(*d_ns, ns_ub);
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < ne + ns; i += gridDim.x * blockDim.x) {
-    PointRec& p = i < ne ? edge[i] : surf[i - ne];   // CompensateVelocity: p += v * time, double -> float
-    const double t = p.time;
-    float x = (float)((double)p.x + vx * t), y = (float)((double)p.y + vy * t), z = (float)((double)p.z + vz * t);
-    if (aliased) {
-      x = (float)((double)x + vx * t);
-      y = (float)((double)y + vy * t);
-      z = (float)((double)z + vz * t);
+  const int ne = min(*d_ne, ne_ub);
+  if (vpart) {
+    // fused with the next VoxelGrids' bounding-box stage: blockIdx.y = the cloud (0 edge, 1 surf), partial
+    // blockIdx.x of its min / max over the compensated coordinates (edge != surf)
+    const int job = (int)blockIdx.y;
+    PointRec* __restrict__ c = job ? surf : edge;
+    const int n = job ? min(*d_ns, ns_ub) : ne;
+    float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+      PointRec& p = c[i];   // CompensateVelocity: p += v * time, double -> float
+      const double t = p.time;
+      const float x = (float)((double)p.x + vx * t), y = (float)((double)p.y + vy * t), z = (float)((double)p.z + vz * t);
+      p.x = x;
+      p.y = y;
+      p.z = z;
+      mn[0] = fminf(mn[0], x); mn[1] = fminf(mn[1], y); mn[2] = fminf(mn[2], z);
+      mx[0] = fmaxf(mx[0], x); mx[1] = fmaxf(mx[1], y); mx[2] = fmaxf(mx[2], z);
     }
-    p.x = x;
-    p.y = y;
-    p.z = z;
+    vox_partial_store(mn, mx, job, (int)blockIdx.x, vpart);
+    if (lead) radix_ctl_zero(vctl, threadIdx.x, blockDim.x);
+  } else {
+    // aliased (edge and surf are one cloud): the reference's two CompensateVelocity calls (src/odomEstimationClass.cpp:
+    // 42-43) shift every point twice, one after the other, so one thread applies both shifts to its point
+    const int ns = aliased ? 0 : min(*d_ns, ns_ub);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < ne + ns; i += gridDim.x * blockDim.x) {
+      PointRec& p = i < ne ? edge[i] : surf[i - ne];   // CompensateVelocity: p += v * time, double -> float
+      const double t = p.time;
+      float x = (float)((double)p.x + vx * t), y = (float)((double)p.y + vy * t), z = (float)((double)p.z + vz * t);
+      if (aliased) {
+        x = (float)((double)x + vx * t);
+        y = (float)((double)y + vy * t);
+        z = (float)((double)z + vz * t);
+      }
+      p.x = x;
+      p.y = y;
+      p.z = z;
+    }
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+  if (lead && threadIdx.x == 0) {
     // the first call's writeback (:114-116) and the second call's prediction (:62-71): odom1 (last^-1 odom1)
     const Pose odom1 = params_to_pose(x1);
     const Pose pred = pose_mul(odom1, pose_mul(pose_inverse(s->last_odom), odom1));
@@ -1093,11 +1117,16 @@ __global__ void odom_predict(OdomDev* s) {
 // ===================================================================================== launchers
 void deskew_bridge_launch(const LMState* d_st, OdomDev* s, double scan_period, PointRec* edge, const int* d_ne,
                           int ne_ub, PointRec* surf, const int* d_ns, int ns_ub, hipStream_t stream,
-                          const GatherArgs& gather) {
+                          const GatherArgs& gather, const VoxelFused* vf) {
   const int aliased = edge == surf ? 1 : 0;
-  const unsigned nb = std::max(1u, std::min(div_up(std::max(ne_ub + ns_ub, 1), kTB), 1024u));
-  hipLaunchKernelGGL(deskew_bridge, dim3(nb), dim3(kTB), 0, stream, d_st, s, scan_period, edge, d_ne, ne_ub, surf,
-                     d_ns, ns_ub, aliased, gather);
+  if (vf && !aliased) {
+    hipLaunchKernelGGL(deskew_bridge, dim3(kVoxMinMaxBlocks, 2), dim3(kTB), 0, stream, d_st, s, scan_period, edge, d_ne,
+                       ne_ub, surf, d_ns, ns_ub, 0, gather, vf->partials, vf->ctl);
+  } else {
+    const unsigned nb = std::max(1u, std::min(div_up(std::max(ne_ub + ns_ub, 1), kTB), 1024u));
+    hipLaunchKernelGGL(deskew_bridge, dim3(nb), dim3(kTB), 0, stream, d_st, s, scan_period, edge, d_ne, ne_ub, surf,
+                       d_ns, ns_ub, aliased, gather, nullptr, nullptr);
+  }
   FLOAM_LAUNCH_CHECK();
 }
 
@@ -1153,15 +1182,32 @@ __device__ __forceinline__ void gather_block(const LMState* __restrict__ lm, con
 __global__ void gather_status(const LMState* __restrict__ lm, const int* __restrict__ dcnt,
                               const int* __restrict__ mapE_count, const int* __restrict__ mapS_count,
                               const int* __restrict__ fe_status, const unsigned long long* __restrict__ prof,
-                              UpdateStatus* __restrict__ out, OdomDev* __restrict__ s, int mode) {
-  gather_block(lm, dcnt, mapE_count, mapS_count, fe_status, prof, out, s, mode);
+                              UpdateStatus* __restrict__ out, OdomDev* __restrict__ s, int mode, VoxelJobDev A,
+                              VoxelJobDev B, float* __restrict__ vpart, unsigned* __restrict__ vctl,
+                              GridClearDev gcE, GridClearDev gcS) {
+  const bool lead = blockIdx.x == 0 && blockIdx.y == 0;
+  if (lead) gather_block(lm, dcnt, mapE_count, mapS_count, fe_status, prof, out, s, mode);
+  if (vpart) {   // the map update's bounding-box stage (its keyframe gate is applied by the launches after this one)
+    if (lead) radix_ctl_zero(vctl, threadIdx.x, blockDim.x);
+    vox_minmax_block(blockIdx.y == 0 ? A : B, (int)blockIdx.y, (int)blockIdx.x, (int)gridDim.x, vpart);
+    if (gcE.coarse)   // the next grid builds' clears (this update's kNN launches are done)
+      grid_clear_part(blockIdx.y == 0 ? gcE : gcS, blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x,
+                      blockIdx.x == 0 && threadIdx.x == 0);
+  }
 }
 
 void gather_status_launch(const LMState* lm, const int* dcnt, const int* mapE_count, const int* mapS_count,
                           const int* fe_status, const unsigned long long* prof, UpdateStatus* out, OdomDev* s,
-                          int mode, hipStream_t st) {
-  hipLaunchKernelGGL(gather_status, dim3(1), dim3(256), 0, st, lm, dcnt, mapE_count, mapS_count, fe_status, prof,
-                     out, s, mode);
+                          int mode, hipStream_t st, const VoxelFused* vf, const GridClearDev* gc) {
+  const GridClearDev none{};
+  if (vf) {
+    hipLaunchKernelGGL(gather_status, dim3(kVoxMinMaxBlocks, 2), dim3(256), 0, st, lm, dcnt, mapE_count, mapS_count,
+                       fe_status, prof, out, s, mode, vf->A, vf->B, vf->partials, vf->ctl, gc ? gc[0] : none,
+                       gc ? gc[1] : none);
+  } else {
+    hipLaunchKernelGGL(gather_status, dim3(1), dim3(256), 0, st, lm, dcnt, mapE_count, mapS_count, fe_status, prof,
+                       out, s, mode, VoxelJobDev{}, VoxelJobDev{}, nullptr, nullptr, none, none);
+  }
   FLOAM_LAUNCH_CHECK();
 }
 

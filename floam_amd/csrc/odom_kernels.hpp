@@ -2,6 +2,7 @@
 #include "cloud_ops.hpp"
 #include "floam_common.hpp"
 #include "pose.hpp"
+#include "voxel.hpp"
 
 namespace floam {
 
@@ -36,13 +37,49 @@ struct Grid {
   unsigned mask = 0;
   int parity = 0;
   bool fresh = true;         // tables (re)allocated: the next clear is a full one
+  bool precleared = false;   // the next build's clear was issued in advance (grid_clear_prepare)
 };
 
+// The first step of a grid build — empty the table entries the previous build occupied (its slot list; the whole
+// table after a reallocation) and reset the cursors — as a device job, so that it can run inside an earlier launch
+// once the previous grid's last reader (the kNN) is done.
+struct GridClearDev {
+  CoarseCell* coarse;
+  const int* clist_old;
+  int* counters;
+  int parity;
+  int full_clear;
+  unsigned mask;
+};
+__device__ __forceinline__ void grid_clear_part(const GridClearDev& J, int t0, int stride, bool lead) {
+  CoarseCell e;
+  e.key = kEmptyKey;
+  e.start = 0;
+  e.total = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) e.sub[k] = 0;
+  if (J.full_clear) {
+    const int size = (int)J.mask + 1;
+    for (int t = t0; t < size; t += stride) J.coarse[t] = e;
+  } else {
+    const int nc = J.counters[1 + (J.parity ^ 1)];
+    for (int t = t0; t < nc; t += stride) J.coarse[J.clist_old[t]] = e;
+  }
+  if (lead) {
+    J.counters[0] = 0;
+    J.counters[1 + J.parity] = 0;
+  }
+}
+// sizes the grid for a map of up to ub points and returns its next build's clear (the build is then issued with
+// precleared = true).  Must not be called while a launch that reads the grid is still to be issued.
+GridClearDev grid_clear_prepare(Grid& g, int ub, hipStream_t st);
+
 struct OdomDev;
-// Rebuild the grids of both local maps (corner and surf) in four launches.  predict (nullable): the update's
-// constant-velocity prediction (odom_predict_step) runs in the first of them instead of a launch of its own.
+// Rebuild the grids of both local maps (corner and surf) in four launches (three when precleared).  predict
+// (nullable): the update's constant-velocity prediction (odom_predict_step) runs in the first of them instead of a
+// launch of its own.
 void grid_build_launch(Grid& gE, const PointRec* mapE, const int* d_mE, int mE_ub, Grid& gS, const PointRec* mapS,
-                       const int* d_mS, int mS_ub, hipStream_t st, OdomDev* predict = nullptr);
+                       const int* d_mS, int mS_ub, hipStream_t st, OdomDev* predict = nullptr, bool precleared = false);
 
 // ----------------------------------------------------------------------------------------- correspondences
 // Edge record (EdgeAnalyticCostFunction inputs): cp (sensor point), a, b.  Surf: cp, unit normal n, d.
@@ -182,7 +219,11 @@ struct UpdateStatus {
 enum { GATHER_FINISH = 1, GATHER_AFTER_MID = 2, GATHER_KEYFRAME = 4, GATHER_KEYFRAME_FIRST = 8 };
 void gather_status_launch(const LMState* lm, const int* dcnt, const int* mapE_count, const int* mapS_count,
                           const int* fe_status, const unsigned long long* prof, UpdateStatus* out, OdomDev* s,
-                          int mode, hipStream_t st);
+                          int mode, hipStream_t st, const VoxelFused* vf = nullptr,
+                          const GridClearDev* gc = nullptr);
+// vf (non-null): the launch also runs the bounding-box stage of the voxel2_launch that follows it (the map update,
+// whose pose is the solve's result): grid (kVoxMinMaxBlocks, 2), block (0, 0) gathers first; gc (with vf, nullable):
+// the clears of the next builds of the two grids (gc[0] corner, gc[1] surf), after the last kNN of this update
 struct GatherArgs {   // a status gather carried out by another launch (deskew_bridge for the first call's slot)
   const int* dcnt = nullptr;
   const int* mapE_count = nullptr;
@@ -203,7 +244,9 @@ void keyframe_update_launch(OdomDev* s, const double* x_dev, int first, int* fla
 // which this launch writes) done by block 0 instead of a launch of its own
 void deskew_bridge_launch(const LMState* st, OdomDev* s, double scan_period, PointRec* edge, const int* d_ne,
                           int ne_ub, PointRec* surf, const int* d_ns, int ns_ub, hipStream_t stream,
-                          const GatherArgs& gather = GatherArgs{});
+                          const GatherArgs& gather = GatherArgs{}, const VoxelFused* vf = nullptr);
+// vf (non-null, edge != surf): the bounding-box stage of the second call's VoxelGrids (deskewed edge at the edge
+// leaf, deskewed surf at the surf leaf) over the coordinates this launch writes; grid (kVoxMinMaxBlocks, 2)
 // Correspondence search for the edge and the surf query sets at the pose in st->x, in two launches:
 // knn_launch — exact 5-NN (blocks [0, nbE) edge queries against the corner map, the rest surf against the surf map);
 // geom_launch — line / plane fits and the residual records (fp64, or fp32 with fp32).

@@ -26,81 +26,15 @@ namespace floam {
 
 namespace {
 constexpr int kTB = 256;
-constexpr int kMinMaxBlocks = 64;       // partials per cloud
+constexpr int kMinMaxBlocks = kVoxMinMaxBlocks;   // partials per cloud
 constexpr int kPerThread = 4;
 constexpr int kTile = kTB * kPerThread;   // elements per compaction tile
-
-struct VoxelJobDev {
-  const PointRec* part0;
-  const int* d_n0;
-  int n0_ub;
-  const PointRec* part1;
-  const int* d_n1;
-  int n1_ub;
-  const double* pose;   // non-null: part1 -> map frame, CropBox(t +- 100) over both parts
-  float inv;
-  PointRec* out;
-  int* d_out;
-  int base;             // first element of this cloud in the combined key array
-};
-
-// element i of the (virtual) concatenation; false if it does not exist or is cropped away
-__device__ __forceinline__ bool vox_fetch(const VoxelJobDev& J, int n0, int n1, int i, PointRec& p) {
-  if (i < n0) {
-    p = J.part0[i];
-  } else if (i < n0 + n1) {
-    const PointRec s = J.part1[i - n0];
-    if (J.pose) {   // pointAssociateToMap (:126-135) into an XYZI record
-      float x, y, z;
-      associate_to_map(J.pose, s.x, s.y, s.z, x, y, z);
-      p.x = x; p.y = y; p.z = z; p.pad0 = 1.0f;
-      p.intensity = s.intensity;
-      p.ring = 0; p.pad1 = 0; p.time = 0.0f; p.pad2 = 0.0f;
-    } else {
-      p = s;
-    }
-  } else {
-    return false;
-  }
-  if (J.pose) {   // CropBox min/max = Vector4f(t -+ 100) (double -> float), inclusive (:270-287)
-    const double* t = J.pose + 4;
-    const float mnx = (float)(t[0] - 100), mny = (float)(t[1] - 100), mnz = (float)(t[2] - 100);
-    const float mxx = (float)(t[0] + 100), mxy = (float)(t[1] + 100), mxz = (float)(t[2] + 100);
-    if (p.x < mnx || p.y < mny || p.z < mnz || p.x > mxx || p.y > mxy || p.z > mxz) return false;
-  }
-  return true;
-}
 
 __global__ __launch_bounds__(kTB) void vox_minmax(VoxelJobDev A, VoxelJobDev B, float* __restrict__ partials,
                                                   unsigned* __restrict__ radix_ctl, const int* __restrict__ gate) {
   if (gate && !*gate) return;
-  const VoxelJobDev& J = blockIdx.y == 0 ? A : B;
   if (blockIdx.x == 0 && blockIdx.y == 0) radix_ctl_zero(radix_ctl, threadIdx.x, blockDim.x);   // for vox_keys
-  const int n0 = *J.d_n0, n1 = J.d_n1 ? *J.d_n1 : 0;
-  float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n0 + n1; i += gridDim.x * blockDim.x) {
-    PointRec p;
-    if (!vox_fetch(J, n0, n1, i, p)) continue;
-    mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
-    mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1)
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-      mn[d] = fminf(mn[d], __shfl_down(mn[d], o, 64));
-      mx[d] = fmaxf(mx[d], __shfl_down(mx[d], o, 64));
-    }
-  __shared__ float s[6][kTB / 64];
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0)
-    for (int d = 0; d < 3; ++d) { s[d][w] = mn[d]; s[3 + d][w] = mx[d]; }
-  __syncthreads();
-  if (threadIdx.x < 6) {
-    float v = s[threadIdx.x][0];
-    for (int k = 1; k < kTB / 64; ++k) v = threadIdx.x < 3 ? fminf(v, s[threadIdx.x][k]) : fmaxf(v, s[threadIdx.x][k]);
-    partials[(blockIdx.y * kMinMaxBlocks + blockIdx.x) * 6 + threadIdx.x] = v;
-  }
+  vox_minmax_block(blockIdx.y == 0 ? A : B, (int)blockIdx.y, (int)blockIdx.x, (int)gridDim.x, partials);
 }
 
 struct VoxelGeom {
@@ -399,13 +333,22 @@ __global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B,
   }
 }
 
+}  // namespace
+
 VoxelJobDev to_dev(const VoxelJob& j, int base) {
   return VoxelJobDev{j.part0, j.d_n0, j.n0_ub, j.part1, j.d_n1, j.part1 ? j.n1_ub : 0, j.pose, 1.0f / j.leaf,
                      j.out, j.d_out, base};
 }
-}  // namespace
 
-void voxel2_launch(VoxelScratch2& sc, const VoxelJob& a, const VoxelJob& b, hipStream_t st, const int* gate) {
+VoxelFused voxel2_prepare(VoxelScratch2& sc, const VoxelJob& a, const VoxelJob& b, hipStream_t st) {
+  const int total = a.n0_ub + (a.part1 ? a.n1_ub : 0) + b.n0_ub + (b.part1 ? b.n1_ub : 0);
+  sc.partials.reserve(2 * kMinMaxBlocks * 6);
+  sc.rs.reserve(std::max(total, 1), st);
+  return VoxelFused{to_dev(a, 0), to_dev(b, a.n0_ub + (a.part1 ? a.n1_ub : 0)), sc.partials.p, sc.rs.ctl.p};
+}
+
+void voxel2_launch(VoxelScratch2& sc, const VoxelJob& a, const VoxelJob& b, hipStream_t st, const int* gate,
+                   bool minmax_done) {
   const VoxelJobDev A = to_dev(a, 0);
   const VoxelJobDev B = to_dev(b, a.n0_ub + (a.part1 ? a.n1_ub : 0));
   const int total = B.base + b.n0_ub + (b.part1 ? b.n1_ub : 0);
@@ -423,8 +366,10 @@ void voxel2_launch(VoxelScratch2& sc, const VoxelJob& a, const VoxelJob& b, hipS
   sc.ticket.reserve(1);
   const int umax = std::max(A.n0_ub + A.n1_ub, b.n0_ub + (b.part1 ? b.n1_ub : 0));
   sc.rs.reserve(n, st);
-  hipLaunchKernelGGL(vox_minmax, dim3(kMinMaxBlocks, 2), dim3(kTB), 0, st, A, B, sc.partials.p, sc.rs.ctl.p, gate);
-  FLOAM_LAUNCH_CHECK();
+  if (!minmax_done) {   // else the producer of the clouds ran the stage (voxel2_prepare)
+    hipLaunchKernelGGL(vox_minmax, dim3(kMinMaxBlocks, 2), dim3(kTB), 0, st, A, B, sc.partials.p, sc.rs.ctl.p, gate);
+    FLOAM_LAUNCH_CHECK();
+  }
   // few blocks: each folds its LDS digit histograms into the global ones with one atomic per non-zero bin
   const unsigned kb = std::max(1u, std::min(div_up(std::max(umax, 1), kTB), 64u));
   hipLaunchKernelGGL(vox_keys, dim3(kb, 2), dim3(kTB), 0, st, A, B, sc.partials.p, sc.s.k0.p, sc.s.v0.p,

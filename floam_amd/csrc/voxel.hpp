@@ -1,5 +1,7 @@
 // Batched pcl::VoxelGrid (+ the map-side half of addPointsToMap) — see voxel.hip.
 #pragma once
+#include <cfloat>
+
 #include "cloud_ops.hpp"
 #include "floam_common.hpp"
 #include "radix.hpp"
@@ -23,6 +25,98 @@ struct VoxelJob {
   int* d_out = nullptr;
 };
 
+// ---- device side of the pipeline, shared with kernels that produce a voxel grid's input (stage fusion)
+
+// the device view of a VoxelJob (base: first element of this cloud in the combined key array)
+struct VoxelJobDev {
+  const PointRec* part0;
+  const int* d_n0;
+  int n0_ub;
+  const PointRec* part1;
+  const int* d_n1;
+  int n1_ub;
+  const double* pose;   // non-null: part1 -> map frame, CropBox(t +- 100) over both parts
+  float inv;
+  PointRec* out;
+  int* d_out;
+  int base;             // first element of this cloud in the combined key array
+};
+
+// element i of the (virtual) concatenation; false if it does not exist or is cropped away
+__device__ __forceinline__ bool vox_fetch(const VoxelJobDev& J, int n0, int n1, int i, PointRec& p) {
+  if (i < n0) {
+    p = J.part0[i];
+  } else if (i < n0 + n1) {
+    const PointRec s = J.part1[i - n0];
+    if (J.pose) {   // pointAssociateToMap (:126-135) into an XYZI record
+      float x, y, z;
+      associate_to_map(J.pose, s.x, s.y, s.z, x, y, z);
+      p.x = x; p.y = y; p.z = z; p.pad0 = 1.0f;
+      p.intensity = s.intensity;
+      p.ring = 0; p.pad1 = 0; p.time = 0.0f; p.pad2 = 0.0f;
+    } else {
+      p = s;
+    }
+  } else {
+    return false;
+  }
+  if (J.pose) {   // CropBox min/max = Vector4f(t -+ 100) (double -> float), inclusive (:270-287)
+    const double* t = J.pose + 4;
+    const float mnx = (float)(t[0] - 100), mny = (float)(t[1] - 100), mnz = (float)(t[2] - 100);
+    const float mxx = (float)(t[0] + 100), mxy = (float)(t[1] + 100), mxz = (float)(t[2] + 100);
+    if (p.x < mnx || p.y < mny || p.z < mnz || p.x > mxx || p.y > mxy || p.z > mxz) return false;
+  }
+  return true;
+}
+
+constexpr int kVoxMinMaxBlocks = 64;   // bounding-box partials per cloud
+
+// The bounding-box stage for one cloud: min / max over the elements i = b * blockDim.x + threadIdx.x (+ k * nblocks *
+// blockDim.x) that vox_fetch keeps, reduced over the block and stored as partial b of cloud `job`.  Called by every
+// thread of a block; blocks b = 0 .. nblocks - 1 (nblocks = kVoxMinMaxBlocks) of each job must all run.
+__device__ __forceinline__ void vox_partial_store(float (&mn)[3], float (&mx)[3], int job, int b,
+                                                  float* __restrict__ partials) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      mn[d] = fminf(mn[d], __shfl_down(mn[d], o, 64));
+      mx[d] = fmaxf(mx[d], __shfl_down(mx[d], o, 64));
+    }
+  __shared__ float s[6][16];
+  const int w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  if ((threadIdx.x & 63) == 0)
+    for (int d = 0; d < 3; ++d) { s[d][w] = mn[d]; s[3 + d][w] = mx[d]; }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    float v = s[threadIdx.x][0];
+    for (int k = 1; k < nw; ++k) v = threadIdx.x < 3 ? fminf(v, s[threadIdx.x][k]) : fmaxf(v, s[threadIdx.x][k]);
+    partials[(job * kVoxMinMaxBlocks + b) * 6 + threadIdx.x] = v;
+  }
+}
+
+__device__ __forceinline__ void vox_minmax_block(const VoxelJobDev& J, int job, int b, int nblocks,
+                                                 float* __restrict__ partials) {
+  const int n0 = *J.d_n0, n1 = J.d_n1 ? *J.d_n1 : 0;
+  float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+  for (int i = b * blockDim.x + threadIdx.x; i < n0 + n1; i += nblocks * blockDim.x) {
+    PointRec p;
+    if (!vox_fetch(J, n0, n1, i, p)) continue;
+    mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
+    mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
+  }
+  vox_partial_store(mn, mx, job, b, partials);
+}
+
+// What a producer kernel needs to run the bounding-box stage of a voxel2_launch issued after it (minmax_done):
+// both clouds' device jobs, the partials, and the sort's control words, which block (0, 0) zeroes
+// (radix_ctl_zero) once its previous sort is complete in stream order.
+struct VoxelFused {
+  VoxelJobDev A, B;
+  float* partials;
+  unsigned* ctl;
+};
+
 struct VoxelScratch2 {
   SortScratch s;
   DevBuf<float> partials;
@@ -35,7 +129,11 @@ struct VoxelScratch2 {
 // Two independent voxel grids in one pipeline (3 kernels + the 4 radix passes).  *d_out of each job receives the
 // voxel count (-1 if the single-pass compaction failed, never expected).  gate (device int, nullable): when it reads
 // 0 the pipeline does nothing but copy each job's part0 to its output (a map update skipped on the device).
+// minmax_done: a producer kernel already ran the bounding-box stage with voxel2_prepare's VoxelFused (same jobs).
 void voxel2_launch(VoxelScratch2& sc, const VoxelJob& a, const VoxelJob& b, hipStream_t st,
-                   const int* gate = nullptr);
+                   const int* gate = nullptr, bool minmax_done = false);
+// reserves the scratch of a voxel2_launch of the same jobs and returns the producer's view of it
+VoxelFused voxel2_prepare(VoxelScratch2& sc, const VoxelJob& a, const VoxelJob& b, hipStream_t st);
+VoxelJobDev to_dev(const VoxelJob& j, int base);
 
 }  // namespace floam

@@ -1,33 +1,59 @@
-#!/usr/bin/env python3
-"""Per-scan kernel timeline from a rocprofv3 kernel trace (run_kernel_trace.csv): one steady-state scan of the
-bench (between two fe_keys launches), with the GPU idle gaps, grouped into phases."""
+"""Main-stream timeline of steady-state scans from a rocprofv3 --kernel-trace CSV.
+
+Usage: python tools/timeline.py gpurun_out/tl/p/.../run_kernel_trace.csv [scans]
+Prints, for one steady-state scan of the stream that runs knn_kernel, every kernel with its duration and the idle
+gap before it, then the per-scan period / busy / idle totals averaged over the last `scans` scans.
+"""
 import csv
 import sys
 
-rows = list(csv.DictReader(open(sys.argv[1])))
-rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-which = int(sys.argv[2]) if len(sys.argv) > 2 else 20
-fk = [i for i, r in enumerate(rows) if "fe_keys" in r["Kernel_Name"]]
-a, b = fk[which], fk[which + 1]
-t0 = int(rows[a]["Start_Timestamp"])
-prev = t0
-busy = 0
-groups = {}
-for r in rows[a:b]:
-    s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
-    busy += e - s
-    name = r["Kernel_Name"].replace("floam::(anonymous namespace)::", "")
-    name = name.split("(")[0].replace("void ", "")
-    if "rocprim" in name:
-        name = "rocprim::" + name.split("detail::")[-1][:40]
-    if "-v" in sys.argv:
-        print(f"{(s - t0) / 1e3:8.1f} gap {(s - prev) / 1e3:6.1f} dur {(e - s) / 1e3:6.1f} {name[:70]}")
-    g = groups.setdefault(name, [0, 0.0, 0.0])
-    g[0] += 1
-    g[1] += (e - s) / 1e3
-    g[2] += (s - prev) / 1e3
-    prev = e
-wall = (int(rows[b]["Start_Timestamp"]) - t0) / 1e3
-print(f"scan wall {wall:.1f} us, kernels {b - a}, busy {busy / 1e3:.1f} us, idle {wall - busy / 1e3:.1f} us")
-for k, v in sorted(groups.items(), key=lambda kv: -kv[1][1]):
-    print(f"  {k[:60]:60s} x{v[0]:3d} {v[1]:8.1f} us (+gaps {v[2]:6.1f})")
+
+def short(name):
+    n = name.replace("floam::(anonymous namespace)::", "").replace("floam::", "").replace("void ", "")
+    return n.split("(")[0][:34]
+
+
+def main():
+    path = sys.argv[1]
+    nscan = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+    rows = list(csv.DictReader(open(path)))
+    sid = "Stream_Id" if "Stream_Id" in rows[0] else "Queue_Id"
+    for r in rows:
+        r["s"] = int(r["Start_Timestamp"])
+        r["e"] = int(r["End_Timestamp"])
+        r["n"] = short(r["Kernel_Name"])
+    main_stream = next(r[sid] for r in rows if r["n"].startswith("knn_kernel"))
+    ms = sorted((r for r in rows if r[sid] == main_stream), key=lambda r: r["s"])
+    # a scan ends with gather_status (writeback + KeyFrameUpdate) followed by the map update
+    ends = [i for i, r in enumerate(ms) if r["n"] == "gather_status"]
+    if len(ends) < nscan + 2:
+        nscan = max(1, len(ends) - 2)
+    # timed scans sit before the replay; take the last nscan full scans of the first half of the run
+    half = ends[: len(ends) // 2] if len(ends) > 2 * nscan + 4 else ends
+    sel = half[-nscan - 1:]
+    periods, busy = [], []
+    for a, b in zip(sel[:-1], sel[1:]):
+        seg = ms[a + 1: b + 1]
+        t0, t1 = ms[a]["e"], ms[b]["e"]
+        periods.append((t1 - t0) / 1e3)
+        busy.append(sum(r["e"] - r["s"] for r in seg) / 1e3)
+    a, b = sel[-2], sel[-1]
+    prev = ms[a]["e"]
+    print(f"{'kernel':36s} {'dur us':>8s} {'gap us':>8s}")
+    for r in ms[a + 1: b + 1]:
+        print(f"{r['n']:36s} {(r['e'] - r['s']) / 1e3:8.2f} {(r['s'] - prev) / 1e3:8.2f}")
+        prev = r["e"]
+    others = {}
+    for r in rows:
+        if r[sid] != main_stream and ms[a]["e"] <= r["s"] <= ms[b]["e"]:
+            others.setdefault(r[sid], []).append((r["n"], (r["e"] - r["s"]) / 1e3))
+    for s, ks in others.items():
+        print(f"stream {s}: {len(ks)} kernels, {sum(k[1] for k in ks):.1f} us: " +
+              ", ".join(f"{n} {d:.1f}" for n, d in ks))
+    n = len(periods)
+    print(f"scans {n}: period {sum(periods) / n:.1f} us, main-stream busy {sum(busy) / n:.1f} us, "
+          f"idle {(sum(periods) - sum(busy)) / n:.1f} us, launches {b - a}")
+
+
+if __name__ == "__main__":
+    main()
