@@ -371,7 +371,7 @@ __device__ __forceinline__ void gram_pair(int e, int& i, int& j) {   // upper-tr
   j = i + e;
 }
 
-// G (full symmetric) and its origin o into LDS from the geometry launch's gmat (gv = gmat[threadIdx.x])
+// G (full symmetric) and its origin o into LDS from the geometry launch's gmat (gv = gram_load(gmat, threadIdx.x))
 __device__ __forceinline__ void gram_unpack(double gv, double (*G)[kGramW], double* o) {
   const int t = threadIdx.x;
   if (t < kGram) {
@@ -828,7 +828,7 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
   const int ne_dev = *a.d_ne;
   const int ns_dev = GRAM ? 0 : *a.d_ns;
   const unsigned sw = tid < kStateWords ? reinterpret_cast<const unsigned*>(a.st)[tid] : 0u;
-  const double gv = (GRAM && tid < kGramWords) ? a.gmat[tid] : 0.0;
+  const double gv = GRAM ? gram_load(a.gmat, tid) : 0.0;
   R f0[9];
   bool has0 = false, edge0 = true;
   uint8_t v0 = 0;
@@ -998,7 +998,7 @@ __global__ __launch_bounds__(kTB) void lm_shard_eval(LMArgs a, int k) {
     if (GRAM) {
       __shared__ double G[kGramW][kGramW];
       __shared__ double o[3];
-      gram_unpack(tid < kGramWords ? a.gmat[tid] : 0.0, G, o);
+      gram_unpack(gram_load(a.gmat, tid), G, o);
       if (tid < 64) surf_sums_wave(s_pt, o, G, (double)sst.corr_surf, s_ssum, lane);
       __syncthreads();
       if (tid < LM_NSUM) s_sums[tid] = s_sums[tid] + s_ssum[tid];
@@ -1060,8 +1060,8 @@ void LMBuffers::reserve(hipStream_t st) {
   partials.reserve((size_t)kRecEvalBlocks * LM_NSUM);
   sums.reserve(LM_NSUM);
   ticket.reserve(1);
-  gpart.reserve((size_t)(kSurfGeomBlocks + kGramGroups) * kGram);
-  gmat.reserve(kGramWords);
+  gpart.reserve((size_t)kSurfGeomBlocks * kGram);
+  gmat.reserve(kGramMatWords);
   gcnt.reserve(kGramGroups + 1);
   // tag 0 never matches (epochs start at 8), counters start at zero
   FLOAM_HIP(hipMemsetAsync(part.p, 0, sizeof(unsigned long long) * part.cap, st));

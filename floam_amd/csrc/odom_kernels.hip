@@ -921,7 +921,8 @@ __global__ __launch_bounds__(kTB) void geom_kernel(LMState* __restrict__ st, Cor
     for (int k = 1; k < kTB / 64; ++k) v += s_part[k][threadIdx.x];
     sc1_store(&gpart[sb * kGram + threadIdx.x], v);
   }
-  // G of the solve, reduced by the last-arriving blocks (fixed order: the 32 blocks of a group, then the 8 groups),
+  // G of the solve, reduced by the last-arriving block of each group (fixed order: the 32 blocks of a group here; the
+  // 8 groups in the solve's prologue, gram_load),
   // without agent fences (MI355X_MICROARCH.md "Hand-offs measured with sc1 loads in place of the acquire", first
   // row): every partial is stored sc1 and loaded sc1; each storing wave drains its stores (vmcnt(0)) before the
   // block barrier behind which one lane adds to the group's ticket; the block whose add comes last reads the group
@@ -935,36 +936,18 @@ __global__ __launch_bounds__(kTB) void geom_kernel(LMState* __restrict__ st, Cor
   if (threadIdx.x == 0) s_last = atomicAdd(&gcnt[grp], 1u) == (unsigned)(per - 1);
   __syncthreads();
   if (!s_last) return;
-  double* gpart2 = gpart + kSurfGeomBlocks * kGram;   // [8][91] group partials
-  if (threadIdx.x < kGram) {
+  if (threadIdx.x < kGram) {   // the group's partial of G into gmat[grp] (the solve adds the groups, gram_load)
     double v = 0.0;
     double gp[per];   // all loads in flight before the in-order sum
 #pragma unroll
     for (int k = 0; k < per; ++k) gp[k] = sc1_load(&gpart[(grp * per + k) * kGram + threadIdx.x]);
 #pragma unroll
     for (int k = 0; k < per; ++k) v += gp[k];
-    sc1_store(&gpart2[grp * kGram + threadIdx.x], v);
+    gmat[grp * kGram + threadIdx.x] = v;
+  } else if (grp == 0 && threadIdx.x < kGram + 3) {
+    gmat[kGramGroups * kGram + threadIdx.x - kGram] = o[threadIdx.x - kGram];   // the origin the records use
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    gcnt[grp] = 0u;   // every block of the group has arrived (next launch: kernel boundary)
-    s_last = atomicAdd(&gcnt[kGramGroups], 1u) == (unsigned)(kGramGroups - 1);
-  }
-  __syncthreads();
-  if (!s_last) return;
-  if (threadIdx.x < kGram) {
-    double gp[kGramGroups];
-#pragma unroll
-    for (int k = 0; k < kGramGroups; ++k) gp[k] = sc1_load(&gpart2[k * kGram + threadIdx.x]);
-    double v = gp[0];
-#pragma unroll
-    for (int k = 1; k < kGramGroups; ++k) v += gp[k];
-    gmat[threadIdx.x] = v;
-  } else if (threadIdx.x < kGram + 3) {
-    gmat[threadIdx.x] = o[threadIdx.x - kGram];   // the origin the records were recentred on
-  }
-  if (threadIdx.x == 0) gcnt[kGramGroups] = 0u;
+  if (threadIdx.x == 0) gcnt[grp] = 0u;   // every block of the group has arrived (next launch: kernel boundary)
 }
 
 // Algorithmic traffic of one launch of the search kernel (knn_kernel; SURVEY.md §8 d): every map

@@ -150,6 +150,21 @@ constexpr int kGram = kGramW * (kGramW + 1) / 2;   // 91 unique entries (upper t
 constexpr int kGramWords = kGram + 3;              // G + the origin o the records were recentred on
 constexpr int kSurfGeomBlocks = 256;               // fixed surf geometry grid: fixed Gram reduction order
 constexpr int kGramGroups = 8;                     // its partials are reduced in 8 groups of 32, then the groups
+// gmat as the geometry launch leaves it: the 8 group partials of G, then o; the solve's prologue adds the groups up
+// in order (gram_load), so the geometry launch needs no second level of hand-offs
+constexpr int kGramMatWords = kGramGroups * kGram + 3;
+__device__ __forceinline__ double gram_load(const double* __restrict__ gmat, int t) {
+  if (t < kGram) {
+    double gp[kGramGroups];   // all loads in flight before the in-order sum
+#pragma unroll
+    for (int k = 0; k < kGramGroups; ++k) gp[k] = gmat[k * kGram + t];
+    double v = gp[0];
+#pragma unroll
+    for (int k = 1; k < kGramGroups; ++k) v += gp[k];
+    return v;
+  }
+  return t < kGramWords ? gmat[kGramGroups * kGram + (t - kGram)] : 0.0;
+}
 constexpr int kEdgeEvalBlocks = 64;                // edge-only evaluation grid of the Gram solves (fixed order)
 constexpr int kRecEvalBlocks = 128;                // per-record evaluation grid (Huber / fp32; fixed order)
 
