@@ -341,6 +341,9 @@ def main():
                              f"single thread, {os.cpu_count()} host cores present"}
         pose_err = {"scans_compared": len(errs), "max_dt_m": max(e[0] for e in errs),
                     "max_drot_rad": max(e[1] for e in errs)}
+        if os.environ.get("FLOAM_BENCH_POSE_LOG"):   # per-scan agreement (diagnostic)
+            for k, (et, er) in enumerate(errs):
+                log(f"[pose] scan {k + 1}: {et:.3e} m {er:.3e} rad")
 
     if rank == 0:
         gt_err = []

@@ -74,14 +74,20 @@ __global__ __launch_bounds__(kTB) void vox_keys(VoxelJobDev A, VoxelJobDev B, co
   __shared__ float s_mm[6];
   __shared__ unsigned s_hist[kRadixHistWords];
   radix_hist_begin(s_hist);
-  if (threadIdx.x < 6) {
-    const bool is_min = threadIdx.x < 3;
+  if (threadIdx.x < 6 * 32) {   // component c = t / 32 (two per wave), 32 lanes over the partials, then a 32-lane min/max
+    const int c = threadIdx.x >> 5, l = threadIdx.x & 31;
+    const bool is_min = c < 3;
     float v = is_min ? FLT_MAX : -FLT_MAX;
-    for (int b = 0; b < kMinMaxBlocks; ++b) {
-      const float u = partials[(job * kMinMaxBlocks + b) * 6 + threadIdx.x];
+    for (int b = l; b < kMinMaxBlocks; b += 32) {
+      const float u = partials[(job * kMinMaxBlocks + b) * 6 + c];
       v = is_min ? fminf(v, u) : fmaxf(v, u);
     }
-    s_mm[threadIdx.x] = v;
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) {
+      const float u = __shfl_xor(v, o, 64);
+      v = is_min ? fminf(v, u) : fmaxf(v, u);
+    }
+    if (l == 0) s_mm[c] = v;
   }
   // lookback state of the compaction launch that follows this one
   for (int t = (job * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x; t < ntiles; t += 2 * gridDim.x * blockDim.x)
