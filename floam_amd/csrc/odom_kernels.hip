@@ -1170,12 +1170,13 @@ __global__ void gather_status(const LMState* __restrict__ lm, const int* __restr
                               GridClearDev gcE, GridClearDev gcS) {
   const bool lead = blockIdx.x == 0 && blockIdx.y == 0;
   if (lead) gather_block(lm, dcnt, mapE_count, mapS_count, fe_status, prof, out, s, mode);
-  if (vpart) {   // the map update's bounding-box stage (its keyframe gate is applied by the launches after this one)
+  if (!vpart) return;
+  if (blockIdx.y < 2) {   // the map update's bounding-box stage (its keyframe gate is applied by the launches after)
     if (lead) radix_ctl_zero(vctl, threadIdx.x, blockDim.x);
     vox_minmax_block(blockIdx.y == 0 ? A : B, (int)blockIdx.y, (int)blockIdx.x, (int)gridDim.x, vpart);
-    if (gcE.coarse)   // the next grid builds' clears (this update's kNN launches are done)
-      grid_clear_part(blockIdx.y == 0 ? gcE : gcS, blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x,
-                      blockIdx.x == 0 && threadIdx.x == 0);
+  } else if (gcE.coarse) {   // blocks of their own: the next grid builds' clears (this update's kNN launches are done)
+    grid_clear_part(blockIdx.y == 2 ? gcE : gcS, blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x,
+                    blockIdx.x == 0 && threadIdx.x == 0);
   }
 }
 
@@ -1184,7 +1185,7 @@ void gather_status_launch(const LMState* lm, const int* dcnt, const int* mapE_co
                           int mode, hipStream_t st, const VoxelFused* vf, const GridClearDev* gc) {
   const GridClearDev none{};
   if (vf) {
-    hipLaunchKernelGGL(gather_status, dim3(kVoxMinMaxBlocks, 2), dim3(256), 0, st, lm, dcnt, mapE_count, mapS_count,
+    hipLaunchKernelGGL(gather_status, dim3(kVoxMinMaxBlocks, gc ? 4 : 2), dim3(256), 0, st, lm, dcnt, mapE_count, mapS_count,
                        fe_status, prof, out, s, mode, vf->A, vf->B, vf->partials, vf->ctl, gc ? gc[0] : none,
                        gc ? gc[1] : none);
   } else {
