@@ -366,7 +366,7 @@ __device__ __forceinline__ void lm_reset(LMState* st, const X7& x0) {
 // top-5 of 64-bit keys (float sq-distance bits << 32 | map index: ascending distance, ties by map index) and a
 // butterfly merge over the group gives the exact 5-NN; lane 0 then runs the fp64 line / plane geometry.
 constexpr int kGroupDefault = 16;   // lanes per query (template parameter G below)
-constexpr int kUnrollDefault = 4;   // candidate loads in flight per lane (U)
+constexpr int kUnrollDefault = 2;   // candidate loads in flight per lane (U; 2 beat 4 and 8 at C3)
 
 // (start, count) of a coarse cell, or (0, 0): the entry's {key, start, total} head (one 16-B load)
 template <typename Cell>
