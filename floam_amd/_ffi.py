@@ -36,7 +36,8 @@ EXPORTS = [
     "floam_odom_create", "floam_odom_destroy", "floam_odom_init_map", "floam_odom_update_selector",
     "floam_odom_update", "floam_odom_get_pose", "floam_odom_get_last_pose", "floam_odom_get_velocity",
     "floam_odom_get_map", "floam_odom_get_map_sizes", "floam_odom_download_maps", "floam_odom_get_stats",
-    "floam_odom_set_async", "floam_odom_wait", "floam_odom_keyframe_update", "floam_odom_set_precision",
+    "floam_odom_set_async", "floam_odom_wait", "floam_odom_keyframe_update", "floam_odom_get_keyframe",
+    "floam_odom_set_precision",
     "floam_odom_set_trace", "floam_odom_get_traces", "floam_odom_get_correspondences",
     "floam_odom_find_correspondences",
     "floam_comm_unique_id", "floam_odom_set_shard", "floam_odom_set_shard_callback",
@@ -119,7 +120,8 @@ def load(path: str | None = None):
         "floam_odom_get_map": [vp, vp], "floam_odom_get_map_sizes": [vp, szp, szp],
         "floam_odom_download_maps": [vp, vp, sz, vp, sz], "floam_odom_get_stats": [vp, C.POINTER(OdomStats)],
         "floam_odom_set_async": [vp, i32], "floam_odom_wait": [vp, sz, dp, sz, szp],
-        "floam_odom_keyframe_update": [vp, dp, dp, ip], "floam_odom_set_precision": [vp, i32],
+        "floam_odom_keyframe_update": [vp, vp, vp, dp, dp, ip],
+        "floam_odom_get_keyframe": [vp, sz, dp, dp, vp, vp, szp], "floam_odom_set_precision": [vp, i32],
         "floam_odom_set_trace": [vp, sz], "floam_odom_get_traces": [vp, dp, sz, szp],
         "floam_odom_get_correspondences": [vp, i32, vp, vp, ip, C.POINTER(C.c_float), dp, sz, szp],
         "floam_odom_find_correspondences": [vp, vp, vp, dp, dp],

@@ -258,7 +258,20 @@ struct floam_odom {
   DevBuf<unsigned> trace_count;
   const PointRec* last_q[2] = {nullptr, nullptr};   // the last pass's query clouds (downsampled, sensor frame)
   const int* last_qn = nullptr;                     // their device counts
+  bool last_traced = false;                         // that pass wrote neighbour indices / distances (tracing on)
   DevBuf<double> kf_io;                             // floam_odom_keyframe_update: pose in, flag out
+  // keyframes_ (include/odomEstimationClass.h:116-117, 3 deep): the pose of every keyframe and, for the public
+  // KeyFrameUpdate, device copies of the clouds it was given.  The updates' own keyframes keep the pose only (their
+  // downsampled clouds are private in the reference and never read back); the decision itself reads the last
+  // keyframe pose from the device state (OdomDev)
+  struct Keyframe {
+    Pose pose;
+    floam_cloud* surf = nullptr;
+    floam_cloud* edge = nullptr;
+  };
+  std::deque<Keyframe> keyframes;
+  std::vector<floam_cloud*> kf_spare;               // clouds of dropped history entries, reused
+  bool next_kf_first = false;                       // the update being issued consumed the process-wide `first`
   DevBuf<LMState> lm;
   // call 1 of a deskewed selector downsamples the edge cloud only (Q4), in the sensor frame: that VoxelGrid runs on a
   // side stream as soon as the scan's features exist, overlapped with the previous update (double-buffered by parity)
@@ -287,6 +300,7 @@ struct floam_odom {
     size_t addE, addS;            // upper bounds of the points the map update may add
     hipEvent_t ev;
     std::vector<void*> graveyard; // device buffers replaced while the update was captured (freed once it ran)
+    bool kf_first;                // its keyframe decision took KeyFrameUpdate's `first` branch (no history trim)
   };
   std::deque<Pending> inflight;
   int depth = 0;                  // floam_odom_set_async: 0 = every update synchronises (the reference's contract)
@@ -313,6 +327,7 @@ struct floam_odom {
   void* ar_user = nullptr;
   HostBuf<double> h_sums;
   bool sharded() const { return world > 1 || comm != nullptr; }
+  int coresident[16] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};   // lm_resident, per mode
   floam_odom_stats stats{};
   floam_status last_warning = FLOAM_OK;
 };
@@ -368,6 +383,11 @@ floam_status guarded(F&& f) {
   }
 }
 
+// an ABI call made from inside another one: its failure propagates with its own status and message
+void chk(floam_status s) {
+  if (s != FLOAM_OK && s < 100) throw Error(s, t_err);
+}
+
 void check_params(const floam_lidar_params* p) {
   if (!p) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null lidar params");
   if (p->num_lines <= 0 || p->num_lines > 4096) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "num_lines out of range");
@@ -390,6 +410,18 @@ void allreduce_sums(floam_odom* o, DeviceCtx& ctx) {
   if (o->ar_fn(o->h_sums.p, LM_NSUM, o->ar_user) != 0) throw Error(FLOAM_ERR_COMM, "host all-reduce callback failed");
   FLOAM_HIP(hipMemcpyAsync(sums, o->h_sums.p, sizeof(double) * LM_NSUM, hipMemcpyHostToDevice, ctx.stream));
   FLOAM_HIP(hipStreamSynchronize(ctx.stream));
+}
+
+// The resident solve needs its whole grid on the device at once (its blocks poll each other): checked once per mode
+// from the kernel's occupancy (a partitioned or smaller device falls back to one launch per evaluation, the sharded
+// path on one rank).  FLOAM_LM_PER_EVAL=1 forces the fallback (tests).
+bool lm_resident(floam_odom* o, int mode) {
+  int& c = o->coresident[mode & 15];
+  if (c < 0) {
+    const char* f = std::getenv("FLOAM_LM_PER_EVAL");
+    c = (f && f[0] == '1') ? 0 : (lm_solve_coresident(mode, o->device) ? 1 : 0);
+  }
+  return c == 1;
 }
 
 // updatePointsToMap (src/odomEstimationClass.cpp:52-124) runs on the device end to end, the controller included:
@@ -475,6 +507,7 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
   if (o->qhint[0] > 0) qe.grid_hint = std::min(ne_ub, o->qhint[0] + o->qhint[0] / 4 + 256);
   if (o->qhint[1] > 0) qs.grid_hint = std::min(ns_ub, o->qhint[1] + o->qhint[1] / 4 + 256);
   o->ce.trace = o->cs.trace = o->trace_cap > 0;
+  o->last_traced = o->ce.trace;   // the neighbour indices / distances of this pass are written only while tracing
   o->last_q[0] = dE;
   o->last_q[1] = dS;
   o->last_qn = dcnt;
@@ -498,14 +531,14 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
       knn_traffic_launch(o->lm.p, qs, o->gS, o->cs, o->rank, o->world, o->traffic_set, o->prof_bytes.p + 1, st);
     }
     // ceres::Solve: iteration zero + at most max_num_iterations = 4 candidates (odomEstimationClass.cpp:102)
-    if (!sharded) {
+    if (!sharded && lm_resident(o, mode)) {
       ProfScope ps(ctx, "lm_solve", FLOAM_PROF_LM);
       lm_solve_launch(o->lm.p, o->ce, dcnt + 0, ne_ub, o->cs, dcnt + 1, ns_ub, mode, o->lmb, st, o->dbg_stamps.p);
-    } else {   // one launch + one all-reduce of the 29 sums per evaluation, all on the stream
+    } else {   // one launch (+ one all-reduce of the 29 sums when sharded) per evaluation, all on the stream
       ProfScope ps(ctx, "lm_solve_sharded", FLOAM_PROF_LM);
       for (int ev = 0; ev < 5; ++ev) {
         lm_shard_eval_launch(ev, o->lm.p, o->ce, dcnt + 0, ne_ub, o->cs, dcnt + 1, ns_ub, mode, o->lmb, st);
-        allreduce_sums(o, ctx);
+        if (sharded) allreduce_sums(o, ctx);
       }
       lm_shard_final_launch(o->lm.p, o->lmb, st);
     }
@@ -527,6 +560,17 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
                        prof_knn ? o->prof_bytes.p : nullptr, o->h_ustat.p + slot, o->ds.p, gather_mode, st,
                        map ? &map->vf : nullptr, map ? gc : nullptr);
   if (prof_knn) FLOAM_HIP(hipMemsetAsync(o->prof_bytes.p, 0, sizeof(unsigned long long) * 2, st));
+}
+
+// keyframes_.push_back + the history trim of KeyFrameUpdate (src/odomEstimationClass.cpp:326, 334-337): the `first`
+// branch appends without trimming, the others keep the newest keyframe_history_ = 3
+void keyframe_push(floam_odom* o, const floam_odom::Keyframe& k, bool first) {
+  o->keyframes.push_back(k);
+  if (!first && o->keyframes.size() > 3) {
+    for (floam_cloud* c : {o->keyframes.front().surf, o->keyframes.front().edge})
+      if (c) o->kf_spare.push_back(c);
+    o->keyframes.pop_front();
+  }
 }
 
 // stats and warning of one call from its status slot (the gate :77 and the warnings :112, :193, :248)
@@ -588,7 +632,10 @@ floam_status odom_collect_one(floam_odom* o, DeviceCtx& ctx) {
   const UpdateStatus& last = slots[P.nslots - 1];
   o->odom = last.odom;
   o->last_odom = last.last_odom;
-  if (P.map_slot >= 0) o->stats.map_updated = slots[P.map_slot].kf_flag;
+  if (P.map_slot >= 0) {
+    o->stats.map_updated = slots[P.map_slot].kf_flag;
+    if (o->stats.map_updated) keyframe_push(o, floam_odom::Keyframe{slots[P.map_slot].odom}, P.kf_first);
+  }
   // map sizes: exact before this update's map update, plus what the later in-flight updates may add
   const UpdateStatus& M = slots[P.map_slot >= 0 ? P.map_slot : P.nslots - 1];
   o->mapE_n = (size_t)M.counts[2] + P.addE + o->pendE;
@@ -678,15 +725,18 @@ floam_status odom_end(floam_odom* o, DeviceCtx& ctx, int ring, int nslots, int m
   hipEvent_t ev;
   FLOAM_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   FLOAM_HIP(hipEventRecord(ev, ctx.stream));
-  o->inflight.push_back(floam_odom::Pending{ring, nslots, map_slot, addE, addS, ev, std::move(graveyard)});
+  o->inflight.push_back(
+      floam_odom::Pending{ring, nslots, map_slot, addE, addS, ev, std::move(graveyard), o->next_kf_first});
+  o->next_kf_first = false;
   o->pendE += addE;
   o->pendS += addS;
   if (o->depth == 0) return odom_collect(o, ctx, 0);
   return FLOAM_OK;
 }
 
-int gather_keyframe_mode() {   // KeyFrameUpdate's process-wide `first` flag (Q6) is consumed by this call
+int gather_keyframe_mode(floam_odom* o) {   // KeyFrameUpdate's process-wide `first` flag (Q6) is consumed here
   const int m = GATHER_KEYFRAME | (g_keyframe_first ? GATHER_KEYFRAME_FIRST : 0);
+  o->next_kf_first = g_keyframe_first;
   g_keyframe_first = false;
   return m;
 }
@@ -753,7 +803,7 @@ floam_status odom_update(floam_odom* o, const floam_cloud* edge, const floam_clo
     MapUpdatePlan mp;
     if (update_map) mp = odom_map_plan(o, ctx, ne_ub, ns_ub);
     odom_issue(o, ctx, edge, surf, ne_ub, ns_ub, o->ds.p->x0[0], 2 * ring,
-               GATHER_FINISH | (update_map ? gather_keyframe_mode() : 0), -1, true, nullptr, false,
+               GATHER_FINISH | (update_map ? gather_keyframe_mode(o) : 0), -1, true, nullptr, false,
                update_map ? &mp : nullptr);
     size_t addE = 0, addS = 0;
     if (update_map) odom_map_update(o, ctx, mp, addE, addS);
@@ -825,7 +875,7 @@ floam_status odom_update_deskew(floam_odom* o, floam_cloud* edge, floam_cloud* s
     if (o->optimization_count > 2) o->optimization_count--;
     MapUpdatePlan mp = odom_map_plan(o, ctx, ne_ub, ns_ub);
     odom_issue(o, ctx, edge, surf, ne_ub, ns_ub, o->ds.p->x0[1], 2 * ring + 1,
-               GATHER_FINISH | GATHER_AFTER_MID | gather_keyframe_mode(), -1, false, nullptr, fuse, &mp);
+               GATHER_FINISH | GATHER_AFTER_MID | gather_keyframe_mode(o), -1, false, nullptr, fuse, &mp);
     size_t addE = 0, addS = 0;
     odom_map_update(o, ctx, mp, addE, addS);
     if (pre >= 0) {   // the side stream may refill this parity's buffers once this update has run: recorded at its
@@ -1190,6 +1240,9 @@ floam_status floam_odom_destroy(floam_odom* o) {
         (void)hipStreamDestroy(o->side);
       }
       if (o->comm) ncclCommDestroy(o->comm);
+      for (const auto& k : o->keyframes)
+        for (floam_cloud* c : {k.surf, k.edge}) floam_cloud_destroy(c);
+      for (floam_cloud* c : o->kf_spare) floam_cloud_destroy(c);
       delete o;
     }
     return FLOAM_OK;
@@ -1445,7 +1498,7 @@ floam_status floam_odom_get_traces(floam_odom* o, double* out, size_t capacity, 
     unsigned n = 0;
     FLOAM_HIP(hipMemcpyAsync(&n, o->trace_count.p, sizeof(unsigned), hipMemcpyDeviceToHost, ctx.stream));
     FLOAM_HIP(hipStreamSynchronize(ctx.stream));
-    const size_t k = std::min((size_t)n, capacity);
+    const size_t k = std::min({(size_t)n, capacity, (size_t)o->trace_cap});
     if (k) {
       if (!out) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null output");
       FLOAM_HIP(hipMemcpy(out, o->trace.p, k * kTraceWords * sizeof(double), hipMemcpyDeviceToHost));
@@ -1489,6 +1542,7 @@ floam_status floam_odom_find_correspondences(floam_odom* o, const floam_cloud* e
     const double x[7] = {q[0], q[1], q[2], q[3], t[0], t[1], t[2]};
     FLOAM_HIP(hipMemcpyAsync(o->kf_io.p, x, sizeof(x), hipMemcpyHostToDevice, st));
     o->ce.trace = o->cs.trace = true;
+    o->last_traced = true;
     QuerySet qe{o->dE.p, o->cnt.p + 0, ne_ub}, qs{o->dS.p, o->cnt.p + 1, ns_ub};
     knn_launch(o->lm.p, o->kf_io.p, qe, o->gE, o->ce, qs, o->gS, o->cs, o->mapE.count.p, o->mapS.count.p, 0, 1, st);
     geom_launch(o->lm.p, qe, o->ce, qs, o->cs, false, o->fp32_geom, o->lmb, st);
@@ -1504,7 +1558,10 @@ floam_status floam_odom_get_correspondences(floam_odom* o, int which, void* quer
                                             float* sqd, double* records, size_t capacity, size_t* n_out) {
   return guarded([&] {
     if (!o || (which != 0 && which != 1)) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null handle or bad set");
-    if (o->trace_cap <= 0 || !o->last_qn) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "tracing off or no update yet");
+    if (!o->last_qn) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "no correspondence pass yet");
+    if ((idx || sqd) && !o->last_traced)   // (stale indices of an earlier traced pass are never returned)
+      throw Error(FLOAM_ERR_INVALID_ARGUMENT, "the last correspondence pass ran untraced: no neighbour indices / "
+                                              "distances (floam_odom_set_trace before the pass)");
     DeviceCtx& ctx = ctx_for(o->device);
     odom_collect(o, ctx, 0);
     FLOAM_HIP(hipStreamSynchronize(ctx.stream));
@@ -1541,9 +1598,12 @@ floam_status floam_odom_get_correspondences(floam_odom* o, int which, void* quer
   });
 }
 
-floam_status floam_odom_keyframe_update(floam_odom* o, const double q[4], const double t[3], int* is_keyframe) {
+floam_status floam_odom_keyframe_update(floam_odom* o, const floam_cloud* surf_cloud, const floam_cloud* edge_cloud,
+                                        const double q[4], const double t[3], int* is_keyframe) {
   return guarded([&] {
     if (!o || !q || !t) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
+    for (const floam_cloud* c : {surf_cloud, edge_cloud})
+      if (c && c->device != o->device) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "cloud on another device");
     DeviceCtx& ctx = ctx_for(o->device);
     FLOAM_HIP(hipSetDevice(o->device));
     odom_collect(o, ctx, 0);
@@ -1556,7 +1616,50 @@ floam_status floam_odom_keyframe_update(floam_odom* o, const double q[4], const 
     int flag = 0;
     FLOAM_HIP(hipMemcpyAsync(&flag, o->kf_io.p + 8, sizeof(int), hipMemcpyDeviceToHost, ctx.stream));
     FLOAM_HIP(hipStreamSynchronize(ctx.stream));
+    if (flag) {   // currentFrame{pose, edge_cloud, surf_cloud} joins the history (:322, :326, :334): the clouds are
+      floam_odom::Keyframe k;   // copied on the device (the reference keeps the caller's shared pointers)
+      k.pose = params_to_pose(x);
+      floam_cloud** dst[2] = {&k.surf, &k.edge};
+      const floam_cloud* src[2] = {surf_cloud, edge_cloud};
+      for (int i = 0; i < 2; ++i) {
+        if (!src[i]) continue;
+        floam_cloud* c = nullptr;
+        if (!o->kf_spare.empty()) {
+          c = o->kf_spare.back();
+          o->kf_spare.pop_back();
+        } else {
+          chk(floam_cloud_create(o->device, 0, &c));
+        }
+        *dst[i] = c;
+        chk(floam_cloud_copy(c, src[i]));
+      }
+      keyframe_push(o, k, first);
+    }
     if (is_keyframe) *is_keyframe = flag;
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_odom_get_keyframe(floam_odom* o, size_t index, double q[4], double t[3], floam_cloud* surf_out,
+                                     floam_cloud* edge_out, size_t* n_keyframes) {
+  return guarded([&] {
+    if (!o) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null handle");
+    DeviceCtx& ctx = ctx_for(o->device);
+    odom_collect(o, ctx, 0);
+    if (n_keyframes) *n_keyframes = o->keyframes.size();
+    if (!q && !t && !surf_out && !edge_out) return FLOAM_OK;
+    if (index >= o->keyframes.size()) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "keyframe index out of range");
+    const floam_odom::Keyframe& k = o->keyframes[index];
+    if (q) mat_to_quat(k.pose.R, q);
+    if (t)
+      for (int i = 0; i < 3; ++i) t[i] = k.pose.t[i];
+    floam_cloud* outs[2] = {surf_out, edge_out};
+    const floam_cloud* src[2] = {k.surf, k.edge};
+    for (int i = 0; i < 2; ++i) {
+      if (!outs[i]) continue;
+      if (src[i]) chk(floam_cloud_copy(outs[i], src[i]));
+      else chk(floam_cloud_clear(outs[i]));
+    }
     return FLOAM_OK;
   });
 }

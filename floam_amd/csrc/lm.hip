@@ -25,7 +25,9 @@
 // last-arriving block into the 29 sums the host all-reduces (RCCL) between the launches.
 //
 // Fixed reduction orders throughout (thread -> 8 strips -> block; blocks -> 8 strips -> total), so the result
-// does not depend on timing; the sharded path on one rank reproduces the single-GPU solve bit for bit.
+// does not depend on timing.  The sharded path on one rank agrees with the resident solve to a few ulps (lm.o is built
+// with FMA contraction, and the compiler may contract the two kernels' evaluations differently); its LM decisions are
+// identical.
 #include <cfloat>
 #include <climits>
 
@@ -1035,8 +1037,8 @@ __global__ void lm_trace(const LMState* __restrict__ st, const int* __restrict__
   if (threadIdx.x != 0) return;
   if (!(*d_me > 10 && *d_ms > 50)) return;   // the map-size gate (:77): no solve ran
   const unsigned i = *count;
+  *count = i + 1;   // counts every solve: a count above the capacity tells the reader that records were dropped
   if ((int)i >= cap) return;
-  *count = i + 1;
   double* o = trace + (size_t)i * kTraceWords;
   int k = 0;
   o[k++] = dcnt[0]; o[k++] = dcnt[1]; o[k++] = st->corr_edge; o[k++] = st->corr_surf;
@@ -1074,7 +1076,8 @@ void lm_solve_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_u
                      const int* d_ns, int ns_ub, int mode, LMBuffers& b, hipStream_t st, unsigned long long* dbg) {
   b.reserve(st);
   const LMArgs a = make_args(d_st, ce, d_ne, ne_ub, cs, d_ns, ns_ub, b, dbg);
-  // the active blocks (at most 32 or 128 blocks of 256 threads on 256 CUs) are co-resident
+  // the active blocks (at most 64 or 128 blocks of 256 threads on 256 CUs) are co-resident: checked by the caller
+  // through lm_solve_coresident before it chooses this path
   if (mode & LM_GRAM) {
     hipLaunchKernelGGL((lm_solve<true, false, double>), dim3(kEdgeEvalBlocks), dim3(kTB), 0, st, a);
   } else {
@@ -1087,6 +1090,24 @@ void lm_solve_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_u
     }
   }
   FLOAM_LAUNCH_CHECK();
+}
+
+template <typename K>
+static bool fits(K kernel, int blocks, int device) {
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kTB, 0) != hipSuccess) return false;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return false;
+  return (long long)per_cu * cus >= blocks;
+}
+
+bool lm_solve_coresident(int mode, int device) {
+  if (mode & LM_GRAM) return fits(lm_solve<true, false, double>, kEdgeEvalBlocks, device);
+  switch (mode & (LM_HUBER | LM_FP32)) {
+    case LM_HUBER: return fits(lm_solve<false, true, double>, kRecEvalBlocks, device);
+    case LM_FP32: return fits(lm_solve<false, false, float>, kRecEvalBlocks, device);
+    case LM_HUBER | LM_FP32: return fits(lm_solve<false, true, float>, kRecEvalBlocks, device);
+    default: return fits(lm_solve<false, false, double>, kRecEvalBlocks, device);
+  }
 }
 
 void lm_shard_eval_launch(int k, LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const CorrSet& cs,

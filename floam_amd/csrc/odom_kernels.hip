@@ -1087,6 +1087,7 @@ __global__ void odom_dev_init(OdomDev* s) {
   s->kf = pose_identity();
   s->kf_count = 0;
   s->kf_flag = 0;
+  s->failed = 0;
   pose_to_params(pose_identity(), s->x0[0]);
   pose_to_params(pose_identity(), s->x0[1]);
 }
@@ -1152,11 +1153,15 @@ __device__ __forceinline__ void gather_block(const LMState* __restrict__ lm, con
     out->prof[0] = prof ? prof[0] : 0ull;
     out->prof[1] = prof ? prof[1] : 0ull;
     out->kf_flag = 0;
-    if (mode & GATHER_FINISH) {
-      if (mode & GATHER_AFTER_MID) s->last_odom = s->mid;
-      s->odom = params_to_pose(lm->x);   // x == the prediction when the solve did not run (gate, no residuals)
+    s->kf_flag = 0;   // (the map update's gate)
+    if (lm->n_res < 0) s->failed = 1;   // an abandoned solve: its pose is not taken, no keyframe, no
+    if (!s->failed) {                   // map update — for this update and every later one; the host raises it
+      if (mode & GATHER_FINISH) {
+        if (mode & GATHER_AFTER_MID) s->last_odom = s->mid;
+        s->odom = params_to_pose(lm->x);   // x == the prediction when the solve did not run (gate, no residuals)
+      }
+      if (mode & GATHER_KEYFRAME) out->kf_flag = keyframe_decide(s, s->odom, (mode & GATHER_KEYFRAME_FIRST) != 0);
     }
-    if (mode & GATHER_KEYFRAME) out->kf_flag = keyframe_decide(s, s->odom, (mode & GATHER_KEYFRAME_FIRST) != 0);
     out->odom = s->odom;
     out->last_odom = s->last_odom;
   }

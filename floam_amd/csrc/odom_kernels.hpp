@@ -206,6 +206,8 @@ struct OdomDev {
   Pose kf;                 // keyframes.back()
   int kf_count;            // keyframes.size() (0..3)
   int kf_flag;             // the last KeyFrameUpdate result: gates the map update
+  int failed;              // a solve ended without its blocks' hand-offs (n_res < 0): from then on the status
+                           // gathers leave the pose, the keyframe and the maps untouched (the host raises the error)
   double x0[2][7];         // parameters {q, t} of the predictions of the first / second call
 };
 void odom_dev_init_launch(OdomDev* s, hipStream_t st);   // identity poses, no keyframes
@@ -289,6 +291,10 @@ void lm_solve_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_u
 void lm_shard_eval_launch(int k, LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const CorrSet& cs,
                           const int* d_ns, int ns_ub, int mode, LMBuffers& b, hipStream_t st);
 void lm_shard_final_launch(LMState* d_st, LMBuffers& b, hipStream_t st);
+// lm_solve's blocks poll each other's partial sums, so the whole grid must be resident at once: true when the
+// occupancy of the instance `mode` selects times the device's CU count covers its grid.  Otherwise the caller runs
+// the per-evaluation path (lm_shard_eval + lm_shard_final on one rank, no spin between blocks).
+bool lm_solve_coresident(int mode, int device);
 // Stage inspection: append this solve's trace record (49 doubles, oracle/odom.cpp SolveTrace order) to trace[] at
 // *count when the map-size gate (:77) let the solve run and *count < cap.
 constexpr int kTraceWords = 49;

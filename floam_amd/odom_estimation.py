@@ -148,14 +148,32 @@ class OdomEstimationClass:
         _ffi.check(self._L.floam_odom_get_stats(self._need(), C.byref(s)))
         return {k: getattr(s, k) for k, _ in _ffi.OdomStats._fields_}
 
-    def KeyFrameUpdate(self, q_xyzw, t) -> bool:
-        """include/odomEstimationClass.h:80 (src/odomEstimationClass.cpp:320-343): pose (q, t) -> is it a keyframe."""
-        q = np.ascontiguousarray(q_xyzw, dtype=np.float64)
-        tt = np.ascontiguousarray(t, dtype=np.float64)
+    def KeyFrameUpdate(self, surf_cloud: DeviceCloud | None, edge_cloud: DeviceCloud | None, pose) -> bool:
+        """include/odomEstimationClass.h:80 (src/odomEstimationClass.cpp:320-343): KeyFrameUpdate(surf_cloud,
+        edge_cloud, pose) -> is `pose` a new keyframe; a keyframe joins the 3-deep history with copies of the clouds.
+        `pose` is (q_xyzw, t) or a 4x4 matrix."""
+        q, tt = _pose_qt(pose)
         flag = C.c_int()
-        _ffi.check(self._L.floam_odom_keyframe_update(self._need(), q.ctypes.data_as(C.POINTER(C.c_double)),
-                                                      tt.ctypes.data_as(C.POINTER(C.c_double)), C.byref(flag)))
+        _ffi.check(self._L.floam_odom_keyframe_update(
+            self._need(), surf_cloud.handle if surf_cloud is not None else None,
+            edge_cloud.handle if edge_cloud is not None else None, q.ctypes.data_as(C.POINTER(C.c_double)),
+            tt.ctypes.data_as(C.POINTER(C.c_double)), C.byref(flag)))
         return bool(flag.value)
+
+    def keyframes(self) -> list:
+        """The keyframe history keyframes_ (private in the reference, include/odomEstimationClass.h:117), oldest
+        first: (q_xyzw, t, surf points, edge points); entries of the updates themselves have empty clouds."""
+        n = C.c_size_t()
+        _ffi.check(self._L.floam_odom_get_keyframe(self._need(), 0, None, None, None, None, C.byref(n)))
+        out = []
+        for i in range(n.value):
+            q, t = np.zeros(4), np.zeros(3)
+            s, e = DeviceCloud(device=self.device), DeviceCloud(device=self.device)
+            _ffi.check(self._L.floam_odom_get_keyframe(self._need(), i, q.ctypes.data_as(C.POINTER(C.c_double)),
+                                                       t.ctypes.data_as(C.POINTER(C.c_double)), s.handle, e.handle,
+                                                       None))
+            out.append((q, t, s.download(), e.download()))
+        return out
 
     def set_precision(self, fp32, geometry: bool = False) -> None:
         """Residual / Jacobian precision (the C5 sweep, BASELINE.json configs[4]): fp32=False is the reference's fp64;
@@ -169,6 +187,7 @@ class OdomEstimationClass:
     def set_trace(self, capacity: int) -> None:
         """Stage inspection: record every solve (up to `capacity`) and keep the last correspondence pass."""
         _ffi.check(self._L.floam_odom_set_trace(self._need(), int(capacity)))
+        self._trace_cap = int(capacity)
 
     def traces(self) -> list:
         """The recorded solves since the last call (oracle.Odometry.traces() layout), then cleared."""
@@ -177,6 +196,8 @@ class OdomEstimationClass:
         n = C.c_size_t()
         _ffi.check(self._L.floam_odom_get_traces(self._need(), buf.ctypes.data_as(C.POINTER(C.c_double)), cap,
                                                  C.byref(n)))
+        if n.value > min(cap, getattr(self, "_trace_cap", cap)):
+            raise _ffi.FloamError(_ffi.ERR_INVALID_ARGUMENT, f"{n.value} solves since the last call: trace truncated")
         out = []
         for b in buf[: min(n.value, cap)]:
             out.append(dict(n_edge_queries=int(b[0]), n_surf_queries=int(b[1]), n_edge_corr=int(b[2]),
@@ -243,6 +264,21 @@ class OdomEstimationClass:
             self.close()
         except Exception:
             pass
+
+
+def _pose_qt(pose):
+    """(q_xyzw, t) from a (q, t) pair or a 4x4 isometry."""
+    if isinstance(pose, np.ndarray) and pose.shape == (4, 4):
+        R = pose[:3, :3]
+        w = np.sqrt(max(0.0, 1.0 + R[0, 0] + R[1, 1] + R[2, 2])) / 2.0
+        if w > 1e-6:
+            q = np.array([(R[2, 1] - R[1, 2]) / (4 * w), (R[0, 2] - R[2, 0]) / (4 * w), (R[1, 0] - R[0, 1]) / (4 * w), w])
+        else:
+            from scipy.spatial.transform import Rotation
+            q = Rotation.from_matrix(R).as_quat()
+        return np.ascontiguousarray(q, dtype=np.float64), np.ascontiguousarray(pose[:3, 3], dtype=np.float64)
+    q, t = pose
+    return np.ascontiguousarray(q, dtype=np.float64), np.ascontiguousarray(t, dtype=np.float64)
 
 
 def comm_unique_id() -> bytes:

@@ -252,14 +252,24 @@ typedef struct floam_odom_stats {
 } floam_odom_stats;
 floam_status floam_odom_get_stats(const floam_odom* o, floam_odom_stats* s);
 
-/* KeyFrameUpdate(pose) (include/odomEstimationClass.h:80, src/odomEstimationClass.cpp:320-343): public in the
- * reference's header; updatePointsToMap calls it internally (the process-wide `first` flag of Q6 is shared with
- * those calls).  *is_keyframe = 1 when the pose moved > 0.07 m or turned > 2 deg from the last keyframe. */
-floam_status floam_odom_keyframe_update(floam_odom* o, const double q_xyzw[4], const double t[3], int* is_keyframe);
+/* bool KeyFrameUpdate(PointCloud<PointXYZI>::Ptr surf_cloud, PointCloud<PointXYZI>::Ptr edge_cloud,
+ *                     const Eigen::Isometry3d& pose)   (include/odomEstimationClass.h:80, src/odomEstimationClass.cpp:320-343)
+ * Public in the reference's header; updatePointsToMap calls it internally (:118), and the process-wide `first` flag
+ * of Q6 is shared with those calls.  *is_keyframe = 1 when the pose moved > 0.07 m or turned > 2 deg from the last
+ * keyframe (or on the process's first call).  A keyframe joins the 3-deep history keyframes_ (:326, :334-337) with
+ * device copies of surf_cloud / edge_cloud (either may be NULL, a null Ptr in the reference). */
+floam_status floam_odom_keyframe_update(floam_odom* o, const floam_cloud* surf_cloud, const floam_cloud* edge_cloud,
+                                        const double q_xyzw[4], const double t[3], int* is_keyframe);
+/* Inspection of the keyframe history keyframes_ (private in the reference, include/odomEstimationClass.h:117; for
+ * tests): *n_keyframes = its size; entry `index` (0 = oldest): pose and copies of its clouds.  Entries made by the
+ * updates themselves carry the pose only (their clouds come back empty). Every output may be NULL. */
+floam_status floam_odom_get_keyframe(floam_odom* o, size_t index, double q_xyzw[4], double t[3], floam_cloud* surf_out,
+                                     floam_cloud* edge_out, size_t* n_keyframes);
 
 /* Precision of the residual / Jacobian evaluation and of the correspondence geometry (extension: BASELINE.json
- * configs[4], the fp32 vs fp64 Jacobian tolerance sweep).  FLOAM_PRECISION_FP64 (default) is the reference's double
- * arithmetic throughout (src/odomEstimationClass.cpp:156-243, src/lidarOptimization.cpp:12-74).
+ * configs[4], the fp32 vs fp64 Jacobian tolerance sweep).  FLOAM_PRECISION_FP64 (default) computes in double like
+ * the reference (src/odomEstimationClass.cpp:156-243, src/lidarOptimization.cpp:12-74); the solve's residuals,
+ * Jacobians and control step use fused multiply-adds, so they differ from the reference's unfused arithmetic by ulps.
  * FLOAM_PRECISION_FP32: residuals, Jacobians and the per-thread J^T J / J^T r sums in float; the line / plane fits,
  * the cross-thread reductions and the LM control stay in double.  FLOAM_PRECISION_FP32_GEOMETRY: additionally the
  * line (eigen) and plane (QR) fits in float.  Measured deviations from the fp64 solution: DESIGN.md §4. */
@@ -270,7 +280,9 @@ floam_status floam_odom_set_precision(floam_odom* o, int precision);
  * capacity > 0 records one 49-double record per ceres::Solve (oracle/odom.cpp SolveTrace order: edge queries, surf
  * queries, edge factors, surf factors, iterations, successful steps, initial cost, final cost, x_in[7], x_out[7],
  * J^T J at x_in (upper, row-major, 21), J^T r at x_in (6)) and keeps the last correspondence pass's neighbour indices
- * and squared distances; 0 turns it off.  floam_odom_get_traces returns and clears the recorded solves. */
+ * and squared distances; 0 turns it off.  floam_odom_get_traces copies min(n, capacity, trace capacity) records and
+ * clears them; *n_out = n, the number of solves since the last call, so n_out > capacity (or > the set_trace
+ * capacity) signals that records were dropped. */
 floam_status floam_odom_set_trace(floam_odom* o, size_t capacity);
 floam_status floam_odom_get_traces(floam_odom* o, double* out /* capacity x 49 */, size_t capacity, size_t* n_out);
 /* One correspondence pass at an explicit pose, without a solve (the map and the odometry state are untouched):
@@ -282,7 +294,9 @@ floam_status floam_odom_find_correspondences(floam_odom* o, const floam_cloud* e
 /* The last correspondence pass of set `which` (0 edge / corner map, 1 surf / surf map): the downsampled queries
  * (32-B records, sensor frame), per query flags (bit 0 accepted factor, bit 2 five neighbours with sqd < 1), the 5
  * neighbours' map indices and float squared distances (row-major n x 5; valid when bit 2 is set) and the factor
- * records (edge: cp, a, b = 9 doubles; surf: cp, n, d = 7 doubles; valid when bit 0 is set).  Any output may be NULL. */
+ * records (edge: cp, a, b = 9 doubles; surf: cp, n, d = 7 doubles; valid when bit 0 is set).  Any output may be NULL.
+ * The indices / distances exist only for a pass that ran with tracing on: asking for them after an untraced pass
+ * fails with FLOAM_ERR_INVALID_ARGUMENT (no stale values of an earlier pass). */
 floam_status floam_odom_get_correspondences(floam_odom* o, int which, void* queries, uint8_t* flags, int* idx,
                                             float* sqd, double* records, size_t capacity, size_t* n_out);
 
@@ -290,7 +304,7 @@ floam_status floam_odom_get_correspondences(floam_odom* o, int which, void* quer
  * correspondence queries are split into `world` contiguous ranges and the normal equations (J^T J, J^T r, cost)
  * are summed with one RCCL all-reduce per LM evaluation.  unique_id: 128 bytes from floam_comm_unique_id() on
  * rank 0, broadcast by the caller (e.g. torch.distributed).  world = 1 with a unique id runs the sharded path through
- * a one-rank RCCL communicator (bit-identical to the unsharded solve). */
+ * a one-rank RCCL communicator (agrees with the unsharded solve to a few ulps; identical LM decisions). */
 floam_status floam_comm_unique_id(void* unique_id_128);
 floam_status floam_odom_set_shard(floam_odom* o, int rank, int world, const void* unique_id_128);
 /* Same sharding with a caller-supplied host all-reduce instead of RCCL (in-place sum of `count` doubles over all

@@ -55,6 +55,16 @@ int main(int argc, char** argv) {
   CHECK(floam_odom_get_pose(nullptr, q, t) == FLOAM_ERR_INVALID_ARGUMENT);
   CHECK(floam_odom_update_selector(nullptr, nullptr, nullptr, 1) == FLOAM_ERR_INVALID_ARGUMENT);
   CHECK(floam_odom_set_precision(nullptr, FLOAM_PRECISION_FP32) == FLOAM_ERR_INVALID_ARGUMENT);
+  // KeyFrameUpdate(surf_cloud, edge_cloud, pose) (include/odomEstimationClass.h:80): the reference's argument order,
+  // the clouds as device clouds (either may be null), the pose as (q, t)
+  {
+    floam_status (*kfu)(floam_odom*, const floam_cloud*, const floam_cloud*, const double*, const double*, int*) =
+        &floam_odom_keyframe_update;
+    int kf = -1;
+    CHECK(kfu(nullptr, nullptr, nullptr, q, t, &kf) == FLOAM_ERR_INVALID_ARGUMENT && kf == -1);
+    size_t nk = 7;
+    CHECK(floam_odom_get_keyframe(nullptr, 0, q, t, nullptr, nullptr, &nk) == FLOAM_ERR_INVALID_ARGUMENT);
+  }
 
   // device calls fail loudly without a gfx950 device (no CPU fallback)
   if (expect_no_device) {

@@ -1,0 +1,67 @@
+"""Control-path guards of the odometry handle on the GPU: the per-evaluation fallback of the LM solve (taken when the
+resident solve's grid cannot be co-resident), trace overflow reporting, and the refusal of neighbour indices from an
+untraced correspondence pass."""
+import numpy as np
+import pytest
+
+from floam_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _params(R):
+    from floam_amd import LidarParams
+    return LidarParams(num_lines=R, scan_period=0.1, vertical_angle=2.0, max_distance=90.0, min_distance=0.5)
+
+
+def _run(floam_gpu, n, loss="Cauchy", trace=0):
+    from floam_amd.odom_estimation import reset_process_state
+    reset_process_state()
+    lp = floam_gpu.LaserProcessingClass()
+    lp.init(_params(16))
+    odo = floam_gpu.OdomEstimationClass()
+    odo.init(_params(16), 0.1, loss)
+    if trace:
+        odo.set_trace(trace)
+    poses = []
+    for k in range(n):
+        de, ds = floam_gpu.DeviceCloud(), floam_gpu.DeviceCloud()
+        lp.featureExtraction(floam_gpu.DeviceCloud(synth.generate_scan("c1", k)), de, ds)
+        if k == 0:
+            odo.initMapWithPoints(de, ds)
+        else:
+            odo.UpdatePointsToMapSelector(de, ds, True)
+        poses.append(odo.pose())
+    return poses, odo
+
+
+@pytest.mark.parametrize("loss", ["Cauchy", "huber"])
+def test_per_evaluation_fallback_matches_resident_solve(floam_gpu, monkeypatch, loss):
+    """the resident lm_solve needs its whole grid co-resident; where the occupancy check fails the handle
+    runs one launch per evaluation (lm_shard_eval on one rank).  Forced here: same LM decisions, poses to ulps."""
+    ref, _ = _run(floam_gpu, 6, loss)
+    monkeypatch.setenv("FLOAM_LM_PER_EVAL", "1")
+    alt, _ = _run(floam_gpu, 6, loss)
+    for k, ((qa, ta), (qb, tb)) in enumerate(zip(ref, alt)):
+        np.testing.assert_allclose(tb, ta, rtol=0, atol=1e-12, err_msg=f"scan {k}")
+        np.testing.assert_allclose(qb, qa, rtol=0, atol=1e-12, err_msg=f"scan {k}")
+
+
+def test_trace_overflow_is_reported(floam_gpu):
+    """a trace capacity below the number of solves is reported (n_out > capacity), not hidden."""
+    from floam_amd import FloamError
+    _, odo = _run(floam_gpu, 2, trace=1)   # one deskewed update with optimization_count 11 + 10 solves
+    with pytest.raises(FloamError, match="truncated"):
+        odo.traces()
+    _, odo = _run(floam_gpu, 2, trace=64)
+    assert len(odo.traces()) == 21
+
+
+def test_untraced_pass_has_no_neighbour_indices(floam_gpu):
+    """neighbour indices / distances exist only for a traced pass; switching tracing on after an
+    untraced update does not hand out stale ones."""
+    from floam_amd import FloamError
+    _, odo = _run(floam_gpu, 2)
+    odo.set_trace(16)
+    with pytest.raises(FloamError, match="untraced"):
+        odo.correspondences(0)
