@@ -173,8 +173,10 @@ def main():
         return lp, odo
 
     # feature buffers: the extraction of scan k+1 (its own stream) is issued before the odometry of scan k, so the
-    # two overlap on the device, as the reference's laserProcessingNode runs beside odomEstimationNode
-    bufs = [(floam_amd.DeviceCloud(device=dev), floam_amd.DeviceCloud(device=dev)) for _ in range(max(2, DEPTH))]
+    # two overlap on the device, as the reference's laserProcessingNode runs beside odomEstimationNode.  DEPTH + 1
+    # buffers: the extraction into a buffer is issued once the update that last read it has been collected, so it
+    # needs no cross-stream wait on the odometry stream
+    bufs = [(floam_amd.DeviceCloud(device=dev), floam_amd.DeviceCloud(device=dev)) for _ in range(max(3, DEPTH + 1))]
 
     def extract(lp, k):
         e, s = bufs[k % len(bufs)]
@@ -184,6 +186,8 @@ def main():
 
     host_split = [0.0, 0.0]   # host seconds issuing / waiting (diagnostic, FLOAM_BENCH_HOST=1)
 
+    host_trace = [] if os.environ.get("FLOAM_BENCH_HOST_TRACE") else None   # (diagnostic) monotonic ns per scan
+
     def run(lp, odo, a, b, poses):
         """scans [a, b): featureExtraction + UpdatePointsToMapSelector each, extraction one scan ahead; the odometry
         streams (floam_odom_set_async): scan k's pose is collected after scan k+1 has been issued"""
@@ -191,14 +195,19 @@ def main():
             extract(lp, a)
         for k in range(a, b):
             t0 = time.perf_counter()
+            m0 = time.monotonic_ns()
             if k + 1 < b:
                 extract(lp, k + 1)
+            m1 = time.monotonic_ns()
             e, s = bufs[k % len(bufs)]
             odo.UpdatePointsToMapSelector(e, s, True)
             t1 = time.perf_counter()
+            m2 = time.monotonic_ns()
             poses.extend(odo.wait(DEPTH - 1))
             host_split[0] += t1 - t0
             host_split[1] += time.perf_counter() - t1
+            if host_trace is not None:
+                host_trace.append((k, m0, m1, m2, time.monotonic_ns()))
         poses.extend(odo.wait(0))
 
     def barrier_sync():
@@ -227,11 +236,16 @@ def main():
     poses = []
     run(lp, odo, 0, args.warmup, poses)
     barrier_sync()
+    _ffi.check(L.floam_profile_mark(dev, 1))   # trace marker: the timed region starts (tools/prof_summary.py)
+    barrier_sync()
     host_split[:] = [0.0, 0.0]
     t_start = time.perf_counter()
     run(lp, odo, args.warmup, n_scans, poses)
     barrier_sync()
     elapsed = time.perf_counter() - t_start
+    _ffi.check(L.floam_profile_mark(dev, 2))   # ... and ends
+    if host_trace is not None:
+        json.dump(host_trace, open(os.environ["FLOAM_BENCH_HOST_TRACE"], "w"))
     if os.environ.get("FLOAM_BENCH_HOST"):
         log(f"[host] per timed scan: issue {1e6 * host_split[0] / args.steps:.0f} us, "
             f"wait {1e6 * host_split[1] / args.steps:.0f} us")

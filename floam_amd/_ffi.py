@@ -42,7 +42,7 @@ EXPORTS = [
     "floam_odom_find_correspondences",
     "floam_comm_unique_id", "floam_odom_set_shard", "floam_odom_set_shard_callback",
     "floam_last_error", "floam_version", "floam_reset_process_state", "floam_device_synchronize",
-    "floam_profile_enable", "floam_profile_read", "floam_profile_reset",
+    "floam_profile_enable", "floam_profile_read", "floam_profile_reset", "floam_profile_mark",
     "floam_imu_create", "floam_imu_destroy", "floam_imu_add_msg", "floam_imu_add_msgs", "floam_imu_size",
     "floam_imu_get", "floam_imu_time_contained", "floam_euler_to_quaternion", "floam_center_time",
     "floam_imu_compensate", "floam_imu_preprocess",
@@ -128,7 +128,7 @@ def load(path: str | None = None):
         "floam_comm_unique_id": [vp], "floam_odom_set_shard": [vp, i32, i32, vp],
         "floam_odom_set_shard_callback": [vp, i32, i32, ALLREDUCE_FN, vp],
         "floam_device_synchronize": [i32], "floam_profile_enable": [i32, i32],
-        "floam_profile_read": [i32, C.POINTER(KernelTiming), i32, C.POINTER(C.c_int)], "floam_profile_reset": [i32],
+        "floam_profile_read": [i32, C.POINTER(KernelTiming), i32, C.POINTER(C.c_int)], "floam_profile_reset": [i32], "floam_profile_mark": [i32, i32],
         "floam_imu_create": [i32, pp], "floam_imu_destroy": [vp], "floam_imu_add_msg": [vp, dbl, dp, ip],
         "floam_imu_add_msgs": [vp, dp, dp, sz, szp], "floam_imu_size": [vp, szp],
         "floam_imu_get": [vp, dbl, dp, ip], "floam_imu_time_contained": [vp, dbl, ip],

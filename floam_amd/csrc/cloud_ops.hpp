@@ -24,6 +24,9 @@ struct SortScratch {   // (key, value) ping-pong buffers of the voxel sort
   void reserve(int n);
 };
 
+// one marker dispatch (kernel floam_profile_marker) on the stream: tools/prof_summary.py slices traces by it
+void profile_marker_launch(int id, hipStream_t st);
+
 // dmapping::CompensateVelocity (src/dataHandler.cpp:82-92), in place
 void compensate_velocity_launch(PointRec* pts, const int* d_n, int n_ub, double vx, double vy, double vz,
                                 hipStream_t st);

@@ -250,7 +250,8 @@ __global__ __launch_bounds__(kSectorThreads) void fe_output(const PointRec* __re
                                                             const int* __restrict__ sec_surf_cnt,
                                                             const int* __restrict__ surf_pos,
                                                             PointRec* __restrict__ edge_out, const int* __restrict__ edge_count,
-                                                            PointRec* __restrict__ surf_out, const int* __restrict__ surf_count) {
+                                                            PointRec* __restrict__ surf_out, const int* __restrict__ surf_count,
+                                                            int clear) {
   __shared__ int red[2][kSectorThreads / 64];
   __shared__ int s_off;
   const int sec = blockIdx.x;
@@ -277,7 +278,7 @@ __global__ __launch_bounds__(kSectorThreads) void fe_output(const PointRec* __re
     surf_prefix += red[1][w];
   }
   const int ne = sec_edge_cnt[sec], ns = sec_surf_cnt[sec];
-  const int be = edge_count[0] + edge_prefix, bs = surf_count[0] + surf_prefix;
+  const int be = ((clear & 1) ? 0 : edge_count[0]) + edge_prefix, bs = ((clear & 2) ? 0 : surf_count[0]) + surf_prefix;
   if ((int)threadIdx.x < ne) edge_out[be + threadIdx.x] = make_out(in[ring_idx[sec_edge_pos[sec * kMaxEdgesPerSector + threadIdx.x]]]);
   if (ns > 0) {
     int a, b;
@@ -292,7 +293,8 @@ __global__ __launch_bounds__(kSectorThreads) void fe_output(const PointRec* __re
 __global__ void fe_commit(int n_sectors, const int* __restrict__ sec_edge_cnt, const int* __restrict__ sec_surf_cnt,
                           int* __restrict__ edge_count, int* __restrict__ surf_count, int* __restrict__ ring_count,
                           int num_lines, int* __restrict__ status, int* __restrict__ out3,
-                          int* __restrict__ stat_edge, int* __restrict__ stat_surf, unsigned* __restrict__ radix_ctl) {
+                          int* __restrict__ stat_edge, int* __restrict__ stat_surf, unsigned* __restrict__ radix_ctl,
+                          int clear) {
   radix_ctl_zero(radix_ctl, threadIdx.x, blockDim.x);   // the next call's bucketing sort (its histograms, epoch)
   __shared__ int red[2][4];
   int pe = 0, ps = 0;
@@ -313,8 +315,8 @@ __global__ void fe_commit(int n_sectors, const int* __restrict__ sec_edge_cnt, c
   if (threadIdx.x == 0) {
     int te = 0, ts = 0;
     for (int w = 0; w < (int)(blockDim.x >> 6); ++w) { te += red[0][w]; ts += red[1][w]; }
-    edge_count[0] += te;
-    surf_count[0] += ts;
+    edge_count[0] = ((clear & 1) ? 0 : edge_count[0]) + te;   // clear: the outputs were emptied before this call
+    surf_count[0] = ((clear & 2) ? 0 : surf_count[0]) + ts;    // (floam_cloud_clear, folded in: no fill launch)
     out3[0] = edge_count[0];
     out3[1] = surf_count[0];
     const int sv = *status;
@@ -330,7 +332,7 @@ __global__ void fe_commit(int n_sectors, const int* __restrict__ sec_edge_cnt, c
 
 void fe_launch(FeScratch& sc, const FeParams& prm, const PointRec* d_in, int n, PointRec* edge_out,
                int* edge_count, PointRec* surf_out, int* surf_count, hipStream_t st, int* stat_edge,
-               int* stat_surf) {
+               int* stat_surf, int clear) {
   const int R = prm.num_lines;
   sc.keys.reserve(n);
   sc.keys2.reserve(n);
@@ -379,10 +381,10 @@ void fe_launch(FeScratch& sc, const FeParams& prm, const PointRec* d_in, int n, 
   FLOAM_LAUNCH_CHECK();
   hipLaunchKernelGGL(fe_output, dim3(6 * R), dim3(kSectorThreads), 0, st, d_in, sc.ring_count.p, sc.ring_idx.p,
                      sc.sec_edge_cnt.p, sc.sec_edge_pos.p, sc.sec_surf_cnt.p, sc.surf_pos.p, edge_out, edge_count,
-                     surf_out, surf_count);
+                     surf_out, surf_count, clear);
   FLOAM_LAUNCH_CHECK();
   hipLaunchKernelGGL(fe_commit, dim3(1), dim3(256), 0, st, 6 * R, sc.sec_edge_cnt.p, sc.sec_surf_cnt.p, edge_count,
-                     surf_count, sc.ring_count.p, R, sc.status, sc.out3.p, stat_edge, stat_surf, sc.rs.ctl.p);
+                     surf_count, sc.ring_count.p, R, sc.status, sc.out3.p, stat_edge, stat_surf, sc.rs.ctl.p, clear);
   FLOAM_LAUNCH_CHECK();
 }
 

@@ -23,8 +23,9 @@ struct FeScratch {
 };
 
 // Appends edge/surf features of d_in[0, n) to edge_out/surf_out at their device counts (which are advanced).
+// clear: bit 0 / bit 1 — the edge / surf output counts are taken as 0 (a pending floam_cloud_clear, folded in).
 void fe_launch(FeScratch& sc, const FeParams& prm, const PointRec* d_in, int n, PointRec* edge_out, int* edge_count,
                PointRec* surf_out, int* surf_count, hipStream_t st, int* stat_edge = nullptr,
-               int* stat_surf = nullptr);
+               int* stat_surf = nullptr, int clear = 0);
 
 }  // namespace floam

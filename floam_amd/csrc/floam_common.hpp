@@ -1,5 +1,6 @@
 // Shared host/device definitions of the MI355X-native FLOAM core (gfx950, CDNA4).
 #pragma once
+#include <memory>
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
@@ -127,6 +128,12 @@ struct floam_cloud {
   hipStream_t last_stream = nullptr;
   hipEvent_t ev = nullptr;
   bool ev_valid = false;            // ev recorded after the last operation (else recorded lazily when needed)
+  hipEvent_t ext_ev = nullptr;      // with ev_valid: a borrowed event (the end of an odometry update, shared with
+                                    // the update's other consumers) used instead of ev
+  // the last operation was odometry update `done_seq` of a handle whose collected serial number is *done_ctr: once
+  // it has been collected the operation is complete and a consumer on another stream needs no wait at all
+  std::shared_ptr<const unsigned long long> done_ctr;
+  unsigned long long done_seq = 0;
   bool clear_pending = false;       // floam_cloud_clear: the device count is zeroed by the cloud's next operation,
                                     // on that operation's stream
 };

@@ -56,6 +56,18 @@ struct DeviceCtx {
   std::vector<PendingTiming> pending;
   std::vector<hipEvent_t> free_events;
   std::map<std::string, floam_kernel_timing> totals;
+  // end-of-update events, recycled round-robin: one record per update serves every consumer of that point of the
+  // stream (the host's collection, the next extraction into the update's clouds, the side stream's buffer reuse).
+  // A record is a barrier packet that costs the stream several us, so it is issued once.  An event re-recorded by a
+  // later update only makes a late waiter wait for a later point of the same stream (never too early); 64 updates
+  // separate two records of one event (the deepest asynchronous ring is 16).
+  hipEvent_t update_ev[64] = {};
+  unsigned update_ev_next = 0;
+  hipEvent_t next_update_event() {
+    hipEvent_t& e = update_ev[update_ev_next++ % 64];
+    if (!e) FLOAM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return e;
+  }
 
   hipEvent_t get_event() {
     if (!free_events.empty()) {
@@ -140,13 +152,20 @@ struct ProfScope {
 // issued so far, the cloud's last operation included).
 static void cloud_on(const floam_cloud* cc, hipStream_t s) {
   auto* c = const_cast<floam_cloud*>(cc);
-  if (c->last_stream && c->last_stream != s) {
-    if (!c->ev) FLOAM_HIP(hipEventCreateWithFlags(&c->ev, hipEventDisableTiming));
-    if (!c->ev_valid) FLOAM_HIP(hipEventRecord(c->ev, c->last_stream));
-    FLOAM_HIP(hipStreamWaitEvent(s, c->ev, 0));
+  const bool complete = c->done_ctr && *c->done_ctr >= c->done_seq;   // its last update has been collected
+  if (c->last_stream && c->last_stream != s && !complete) {
+    hipEvent_t e = c->ev_valid ? c->ext_ev : nullptr;
+    if (!e) {
+      if (!c->ev) FLOAM_HIP(hipEventCreateWithFlags(&c->ev, hipEventDisableTiming));
+      if (!c->ev_valid) FLOAM_HIP(hipEventRecord(c->ev, c->last_stream));
+      e = c->ev;
+    }
+    FLOAM_HIP(hipStreamWaitEvent(s, e, 0));
   }
   c->last_stream = s;
   c->ev_valid = false;
+  c->ext_ev = nullptr;
+  c->done_ctr.reset();
   if (c->clear_pending) {
     FLOAM_HIP(hipMemsetAsync(c->count.p, 0, sizeof(int), s));
     c->clear_pending = false;
@@ -159,6 +178,19 @@ static void cloud_publish(const floam_cloud* cc, hipStream_t s) {   // after an 
   FLOAM_HIP(hipEventRecord(c->ev, s));
   c->last_stream = s;
   c->ev_valid = true;
+  c->ext_ev = nullptr;
+}
+// after odometry update `seq` of a handle with collection counter ctr: a consumer on another stream skips the wait
+// once the update has been collected; before that it waits on `recorded` (the update's end event) if there is one,
+// else on an event recorded then on s (a later point of the same stream: correct, only later than needed)
+static void cloud_publish_update(const floam_cloud* cc, hipStream_t s, hipEvent_t recorded,
+                                 const std::shared_ptr<unsigned long long>& ctr, unsigned long long seq) {
+  auto* c = const_cast<floam_cloud*>(cc);
+  c->last_stream = s;
+  c->ev_valid = recorded != nullptr;
+  c->ext_ev = recorded;
+  c->done_ctr = ctr;
+  c->done_seq = seq;
 }
 
 static size_t cloud_count_sync(const floam_cloud* c) {
@@ -276,7 +308,13 @@ struct floam_odom {
   // call 1 of a deskewed selector downsamples the edge cloud only (Q4), in the sensor frame: that VoxelGrid runs on a
   // side stream as soon as the scan's features exist, overlapped with the previous update (double-buffered by parity)
   hipStream_t side = nullptr;
-  hipEvent_t side_ev[2] = {nullptr, nullptr};     // call-1 buffers of a parity consumed (recorded on the main stream)
+  hipEvent_t side_ev[2] = {nullptr, nullptr};     // call-1 buffers of a parity consumed: the end of the update that
+                                                  // used them (a shared end-of-update event, DeviceCtx::update_ev)
+  hipEvent_t end_ev = nullptr;                    // the end-of-update event of the last issued update (if recorded)
+  unsigned long long collected_seq = 0;           // serial number of the last collected update (updates complete in
+                                                  // order: every update up to it is done); shared with the clouds
+  std::shared_ptr<unsigned long long> done_ctr = std::make_shared<unsigned long long>(0);
+  unsigned long long side_seq[2] = {0, 0};        // the update that last read each parity's call-1 buffers
   hipEvent_t pre_ev = nullptr;                    // the side stream's call-1 VoxelGrids done (both clouds' producers)
   bool side_ev_rec[2] = {false, false};
   DevBuf<PointRec> pE[2], pS[2];
@@ -301,6 +339,7 @@ struct floam_odom {
     hipEvent_t ev;
     std::vector<void*> graveyard; // device buffers replaced while the update was captured (freed once it ran)
     bool kf_first;                // its keyframe decision took KeyFrameUpdate's `first` branch (no history trim)
+    unsigned long long seq;       // its serial number (o->issued), stored last in each of its status slots
   };
   std::deque<Pending> inflight;
   int depth = 0;                  // floam_odom_set_async: 0 = every update synchronises (the reference's contract)
@@ -548,7 +587,8 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
   if (o->optimization_count <= 0) lm_init_dev_launch(o->lm.p, x0_dev, st);
   const bool prof_knn = (ctx.profile & FLOAM_PROF_KNN_BYTES) != 0;
   if (defer_gather && !prof_knn && gather_mode == 0) {   // carried out by the next launch (deskew_bridge)
-    *defer_gather = GatherArgs{dcnt, o->mapE.count.p, o->mapS.count.p, edge->fe_status, o->h_ustat.p + slot};
+    *defer_gather = GatherArgs{dcnt, o->mapE.count.p, o->mapS.count.p, edge->fe_status, o->h_ustat.p + slot,
+                               (unsigned)o->issued};
     return;
   }
   GridClearDev gc[2];
@@ -557,7 +597,8 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
     gc[1] = grid_clear_prepare(o->gS, (int)o->mapS_n + map->ns_ub, st);
   }
   gather_status_launch(o->lm.p, dcnt, o->mapE.count.p, o->mapS.count.p, edge->fe_status,
-                       prof_knn ? o->prof_bytes.p : nullptr, o->h_ustat.p + slot, o->ds.p, gather_mode, st,
+                       prof_knn ? o->prof_bytes.p : nullptr, o->h_ustat.p + slot, o->ds.p, gather_mode,
+                       (unsigned)o->issued, st,
                        map ? &map->vf : nullptr, map ? gc : nullptr);
   if (prof_knn) FLOAM_HIP(hipMemsetAsync(o->prof_bytes.p, 0, sizeof(unsigned long long) * 2, st));
 }
@@ -596,6 +637,30 @@ floam_status odom_call_status(floam_odom* o, const UpdateStatus& U) {
   return w;
 }
 
+// Wait until every status slot of update P carries its serial number (the gather kernels store it last, at system
+// scope, into coherent pinned host memory).  A stream that went idle or failed without the number is a device error.
+void wait_status(floam_odom* o, DeviceCtx& ctx, const floam_odom::Pending& P) {
+  const UpdateStatus* slots = o->h_ustat.p + 2 * P.ring;
+  const unsigned want = (unsigned)P.seq;
+  auto done = [&] {
+    for (int k = 0; k < P.nslots; ++k)
+      if (__atomic_load_n(&slots[k].seq, __ATOMIC_ACQUIRE) != want) return false;
+    return true;
+  };
+  static const bool query = !std::getenv("FLOAM_NOQUERY");   // (diagnostic knob)
+  for (long long spin = 0; !done(); ++spin) {
+    if (query && (spin & 1023) == 1023) {   // now and then: has the stream stopped without the status?
+      const hipError_t q = hipStreamQuery(ctx.stream);
+      if (q == hipSuccess) {
+        if (done()) break;
+        throw Error(FLOAM_ERR_DEVICE, "the update's status gather did not run (stream idle)");
+      }
+      if (q != hipErrorNotReady) throw Error(FLOAM_ERR_DEVICE, std::string("HIP: ") + hipGetErrorString(q));
+    }
+    __builtin_ia32_pause();
+  }
+}
+
 // Collect the oldest in-flight update: wait for its status copy, raise its device errors, take its warning, stats,
 // poses and (exact) map sizes.  Returns the update's warning (the second call's, else the first call's).
 floam_status odom_collect_one(floam_odom* o, DeviceCtx& ctx) {
@@ -603,8 +668,10 @@ floam_status odom_collect_one(floam_odom* o, DeviceCtx& ctx) {
   o->inflight.pop_front();
   o->pendE -= P.addE;
   o->pendS -= P.addS;
-  FLOAM_HIP(hipEventSynchronize(P.ev));
-  FLOAM_HIP(hipEventDestroy(P.ev));
+  if (P.ev) FLOAM_HIP(hipEventSynchronize(P.ev));   // (a recycled event: not destroyed)
+  wait_status(o, ctx, P);
+  o->collected_seq = P.seq;
+  *o->done_ctr = P.seq;
   for (void* b : P.graveyard) (void)hipFree(b);
   ctx.drain();
   const UpdateStatus* slots = o->h_ustat.p + 2 * P.ring;
@@ -722,11 +789,19 @@ floam_status odom_end(floam_odom* o, DeviceCtx& ctx, int ring, int nslots, int m
     graveyard.swap(capture_state().graveyard);
     odom_capture_end(o, ctx, kind);
   }
-  hipEvent_t ev;
-  FLOAM_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-  FLOAM_HIP(hipEventRecord(ev, ctx.stream));
-  o->inflight.push_back(
-      floam_odom::Pending{ring, nslots, map_slot, addE, addS, ev, std::move(graveyard), o->next_kf_first});
+  // The host learns that an update is done by polling its status slots (their serial number is stored last), and
+  // the consumers of its buffers on other streams check the collected serial number (cloud_on, odom_prevoxel), so
+  // no event is recorded per update (profiles r03a/r03b: the device idled 30 us between two updates with four
+  // records there, 14 us with one).  Only a ring deeper than 2 records one, for the side stream's buffer reuse (its
+  // parity buffers may not be collected yet).
+  hipEvent_t ev = nullptr;
+  if (o->depth > 2 || captured) {
+    ev = ctx.next_update_event();
+    FLOAM_HIP(hipEventRecord(ev, ctx.stream));
+  }
+  o->end_ev = ev;
+  o->inflight.push_back(floam_odom::Pending{ring, nslots, map_slot, addE, addS, ev, std::move(graveyard),
+                                            o->next_kf_first, o->issued});
   o->next_kf_first = false;
   o->pendE += addE;
   o->pendS += addS;
@@ -821,7 +896,6 @@ void odom_prevoxel(floam_odom* o, floam_cloud* edge, floam_cloud* surf) {
   if (o->use_graph) return;
   if (!o->side) {
     FLOAM_HIP(hipStreamCreateWithFlags(&o->side, hipStreamNonBlocking));
-    for (auto& e : o->side_ev) FLOAM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     FLOAM_HIP(hipEventCreateWithFlags(&o->pre_ev, hipEventDisableTiming));
   }
   const int par = o->pre_par;
@@ -830,7 +904,14 @@ void odom_prevoxel(floam_odom* o, floam_cloud* edge, floam_cloud* surf) {
   o->pE[par].reserve(std::max(ne_ub, 1));
   o->pS[par].reserve(std::max(ne_ub, 1));
   o->pcnt[par].reserve(2);
-  if (o->side_ev_rec[par]) FLOAM_HIP(hipStreamWaitEvent(o->side, o->side_ev[par], 0));
+  if (o->side_ev_rec[par] && o->side_seq[par] > o->collected_seq) {   // the update that read them still runs
+    hipEvent_t e = o->side_ev[par];
+    if (!e) {   // (no end event was recorded for it: the main stream's tail, a later point)
+      e = ctx_for(o->device).next_update_event();
+      FLOAM_HIP(hipEventRecord(e, ctx_for(o->device).stream));
+    }
+    FLOAM_HIP(hipStreamWaitEvent(o->side, e, 0));
+  }
   cloud_on(edge, o->side);
   cloud_on(surf, o->side);   // (not used here: so that one event below orders the main stream after both producers)
   VoxelJob je, js;
@@ -878,11 +959,13 @@ floam_status odom_update_deskew(floam_odom* o, floam_cloud* edge, floam_cloud* s
                GATHER_FINISH | GATHER_AFTER_MID | gather_keyframe_mode(o), -1, false, nullptr, fuse, &mp);
     size_t addE = 0, addS = 0;
     odom_map_update(o, ctx, mp, addE, addS);
-    if (pre >= 0) {   // the side stream may refill this parity's buffers once this update has run: recorded at its
-      FLOAM_HIP(hipEventRecord(o->side_ev[pre], ctx.stream));   // end (an event record between two launches of
-      o->side_ev_rec[pre] = true;                               // the chain costs the stream a few us)
+    const floam_status r = odom_end(o, ctx, ring, 2, 1, addE, addS, captured, 1);
+    if (pre >= 0) {   // the side stream may refill this parity's buffers once this update has run (its end event)
+      o->side_ev[pre] = o->end_ev;
+      o->side_seq[pre] = o->issued;
+      o->side_ev_rec[pre] = true;
     }
-    return odom_end(o, ctx, ring, 2, 1, addE, addS, captured, 1);
+    return r;
   } catch (...) {
     odom_capture_abort(ctx);
     throw;
@@ -932,8 +1015,9 @@ floam_status floam_cloud_destroy(floam_cloud* c) {
     if (c) {
       DeviceCtx& ctx = ctx_for(c->device);
       FLOAM_HIP(hipStreamSynchronize(ctx.stream));
+      if (c->ev_valid && c->ext_ev) FLOAM_HIP(hipEventSynchronize(c->ext_ev));
       if (c->ev) {
-        if (c->ev_valid) FLOAM_HIP(hipEventSynchronize(c->ev));
+        if (c->ev_valid && !c->ext_ev) FLOAM_HIP(hipEventSynchronize(c->ev));
         FLOAM_HIP(hipEventDestroy(c->ev));
       }
       delete c;
@@ -1126,6 +1210,10 @@ floam_status floam_lp_feature_extraction(floam_lp* lp, const floam_cloud* in, fl
     const size_t ns0 = lp->async ? cloud_ub(surf) : cloud_count_sync(surf);
     const size_t ne_add = std::min(n, (size_t)lp->prm.num_lines * 6 * 20);
     cloud_on(in, st);
+    // a pending clear of an output is folded into the extraction's kernels (no fill launch of its own)
+    const int clear = n > 0 ? (edge->clear_pending ? 1 : 0) | (surf->clear_pending ? 2 : 0) : 0;
+    if (clear & 1) edge->clear_pending = false;
+    if (clear & 2) surf->clear_pending = false;
     cloud_on(edge, st);
     cloud_on(surf, st);
     cloud_reserve(edge, ne0 + ne_add + 1, ne0, st);
@@ -1135,7 +1223,7 @@ floam_status floam_lp_feature_extraction(floam_lp* lp, const floam_cloud* in, fl
     if (n > 0) {
       ProfScope ps(ctx, "feature_extraction", FLOAM_PROF_FE, 64.0 * (double)n, st);
       fe_launch(lp->sc, lp->prm, in->pts.p, (int)n, edge->pts.p, edge->count.p, surf->pts.p, surf->count.p, st,
-                edge->fe_stat.p, surf->fe_stat.p);
+                edge->fe_stat.p, surf->fe_stat.p, clear);
     }
     cloud_publish(in, st);
     cloud_publish(edge, st);
@@ -1216,10 +1304,8 @@ floam_status floam_odom_destroy(floam_odom* o) {
     if (o) {
       DeviceCtx& ctx = ctx_for(o->device);
       FLOAM_HIP(hipStreamSynchronize(ctx.stream));
-      for (auto& P : o->inflight) {
-        FLOAM_HIP(hipEventDestroy(P.ev));
+      for (auto& P : o->inflight)
         for (void* b : P.graveyard) (void)hipFree(b);
-      }
       o->inflight.clear();
       for (auto& row : o->graph_exec)
         for (auto& ex : row)
@@ -1235,10 +1321,10 @@ floam_status floam_odom_destroy(floam_odom* o) {
       }
       if (o->side) {
         (void)hipStreamSynchronize(o->side);
-        for (auto& e : o->side_ev) (void)hipEventDestroy(e);
         if (o->pre_ev) (void)hipEventDestroy(o->pre_ev);
         (void)hipStreamDestroy(o->side);
       }
+      *o->done_ctr = ~0ull;   // (the stream is idle: clouds that still point here never wait)
       if (o->comm) ncclCommDestroy(o->comm);
       for (const auto& k : o->keyframes)
         for (floam_cloud* c : {k.surf, k.edge}) floam_cloud_destroy(c);
@@ -1302,10 +1388,10 @@ floam_status floam_odom_update_selector(floam_odom* o, floam_cloud* edge, floam_
       o->late_wait[0] = o->late_wait[1] = nullptr;
       throw;
     }
-    if (!o->use_graph) {   // an event right after the update's last use: a later producer on another stream (the
-      hipStream_t st = ctx_for(o->device).stream;   // next extraction into these buffers) waits for exactly this
-      cloud_publish(edge, st);                       // update, not for whatever the host has issued since
-      if (surf != edge) cloud_publish(surf, st);
+    if (!o->use_graph) {   // a later producer on another stream (the next extraction into these buffers) waits for
+      hipStream_t st = ctx_for(o->device).stream;   // exactly this update, and not at all once it is collected
+      cloud_publish_update(edge, st, o->end_ev, o->done_ctr, o->issued);
+      if (surf != edge) cloud_publish_update(surf, st, o->end_ev, o->done_ctr, o->issued);
     }
     return r;
   });
@@ -1668,6 +1754,16 @@ floam_status floam_profile_enable(int device, int enable) {
   return guarded([&] {
     DeviceCtx& c = ctx_for(device);
     c.profile = enable;
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_profile_mark(int device, int id) {
+  return guarded([&] {
+    if (id < 0) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "marker id must be >= 0");
+    DeviceCtx& c = ctx_for(device);
+    FLOAM_HIP(hipSetDevice(device));
+    profile_marker_launch(id, c.stream);
     return FLOAM_OK;
   });
 }

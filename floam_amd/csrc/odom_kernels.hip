@@ -385,34 +385,52 @@ __device__ __forceinline__ int2 grid_lookup(const Cell* __restrict__ tab, unsign
 // points in the fine (0.5-m) cell (fx, fy, fz): its sub-cell count in the entry of the coarse cell that holds it
 __device__ __forceinline__ int fine_count(const struct CorrArgs& A, int fx, int fy, int fz);
 
-__device__ __forceinline__ void cswap(unsigned long long& a, unsigned long long& b) {
-  const unsigned long long lo = a < b ? a : b, hi = a < b ? b : a;
+// a (key, slot) compare-exchange: the slot of a candidate is its position in the cell-grouped point array (A.gpts),
+// carried beside its (distance, map index) key so the winners' coordinates are re-read from the lines the search
+// itself just fetched, not gathered from the by-index array
+__device__ __forceinline__ void cswap(unsigned long long& a, unsigned long long& b, int& sa, int& sb) {
+  const bool sw = b < a;
+  const unsigned long long lo = sw ? b : a, hi = sw ? a : b;
+  const int slo = sw ? sb : sa, shi = sw ? sa : sb;
   a = lo;
   b = hi;
+  sa = slo;
+  sb = shi;
 }
 
 struct Top5 {
-  unsigned long long k[5];
+  unsigned long long k[5];   // (float distance bits << 32) | map index, ascending
+  int s[5];                  // their slots in A.gpts
 };
 
-__device__ __forceinline__ void top5_insert(Top5& t, unsigned long long key) {
+__device__ __forceinline__ void top5_insert(Top5& t, unsigned long long key, int slot) {
   if (key >= t.k[4]) return;
   t.k[4] = key;
-  cswap(t.k[3], t.k[4]);
-  cswap(t.k[2], t.k[3]);
-  cswap(t.k[1], t.k[2]);
-  cswap(t.k[0], t.k[1]);
+  t.s[4] = slot;
+  cswap(t.k[3], t.k[4], t.s[3], t.s[4]);
+  cswap(t.k[2], t.k[3], t.s[2], t.s[3]);
+  cswap(t.k[1], t.k[2], t.s[1], t.s[2]);
+  cswap(t.k[0], t.k[1], t.s[0], t.s[1]);
 }
 
 // 5 smallest of two ascending 5-lists: bitonic split min(a[i], b[4-i]), then a 5-input sorting network
 __device__ __forceinline__ void top5_merge(Top5& a, const Top5& b) {
   unsigned long long m[5];
+  int ms[5];
 #pragma unroll
-  for (int i = 0; i < 5; ++i) m[i] = a.k[i] < b.k[4 - i] ? a.k[i] : b.k[4 - i];
-  cswap(m[0], m[1]); cswap(m[3], m[4]); cswap(m[2], m[4]); cswap(m[2], m[3]); cswap(m[0], m[3]);
-  cswap(m[0], m[2]); cswap(m[1], m[4]); cswap(m[1], m[3]); cswap(m[1], m[2]);
+  for (int i = 0; i < 5; ++i) {
+    const bool ta = a.k[i] < b.k[4 - i];
+    m[i] = ta ? a.k[i] : b.k[4 - i];
+    ms[i] = ta ? a.s[i] : b.s[4 - i];
+  }
+  cswap(m[0], m[1], ms[0], ms[1]); cswap(m[3], m[4], ms[3], ms[4]); cswap(m[2], m[4], ms[2], ms[4]);
+  cswap(m[2], m[3], ms[2], ms[3]); cswap(m[0], m[3], ms[0], ms[3]); cswap(m[0], m[2], ms[0], ms[2]);
+  cswap(m[1], m[4], ms[1], ms[4]); cswap(m[1], m[3], ms[1], ms[3]); cswap(m[1], m[2], ms[1], ms[2]);
 #pragma unroll
-  for (int i = 0; i < 5; ++i) a.k[i] = m[i];
+  for (int i = 0; i < 5; ++i) {
+    a.k[i] = m[i];
+    a.s[i] = ms[i];
+  }
 }
 
 template <int G>
@@ -604,9 +622,11 @@ __device__ __forceinline__ void stencil_scan(const CorrArgs& A, int x0, int x1, 
   int c = 0, c_lo = 0, c_hi = s_pre[1], c_start = s_start[0];   // cursor: cell c = [c_lo, c_hi)
   for (int tb = 0; tb < tot; tb += G * U) {
     float4 m[U];
+    int sl[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int tt = tb + u * G + lane;
+      sl[u] = 0;
       if (tt < tot) {
         while (tt >= c_hi) {
           ++c;
@@ -614,7 +634,8 @@ __device__ __forceinline__ void stencil_scan(const CorrArgs& A, int x0, int x1, 
           c_hi = s_pre[c + 1];
           c_start = s_start[c];
         }
-        m[u] = A.gpts[c_start + (tt - c_lo)];
+        sl[u] = c_start + (tt - c_lo);
+        m[u] = A.gpts[sl[u]];
       } else {
         m[u] = make_float4(1e30f, 1e30f, 1e30f, 0.0f);
       }
@@ -630,7 +651,7 @@ __device__ __forceinline__ void stencil_scan(const CorrArgs& A, int x0, int x1, 
       dd += df * df;
       if (dd < 1.0f) {
         ++cnt;
-        top5_insert(t, ((unsigned long long)__float_as_uint(dd) << 32) | (unsigned)__float_as_int(m[u].w));
+        top5_insert(t, ((unsigned long long)__float_as_uint(dd) << 32) | (unsigned)__float_as_int(m[u].w), sl[u]);
       }
     }
   }
@@ -644,7 +665,10 @@ __device__ __forceinline__ void group_merge(Top5& t, int& cnt) {
   for (int mm = G / 2; mm > 0; mm >>= 1) {
     Top5 o;
 #pragma unroll
-    for (int k = 0; k < 5; ++k) o.k[k] = shfl_xor_u64<G>(t.k[k], mm);
+    for (int k = 0; k < 5; ++k) {
+      o.k[k] = shfl_xor_u64<G>(t.k[k], mm);
+      o.s[k] = __shfl_xor(t.s[k], mm, G);
+    }
     top5_merge(t, o);
     cnt += __shfl_xor(cnt, mm, G);
   }
@@ -686,7 +710,7 @@ __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArg
       fine_cell(wx, wy, wz, qx, qy, qz);
       Top5 t;
 #pragma unroll
-      for (int k = 0; k < 5; ++k) t.k[k] = ~0ull;
+      for (int k = 0; k < 5; ++k) { t.k[k] = ~0ull; t.s[k] = 0; }
       int cnt = 0;
       stencil_scan<G, U, false>(A, qx - 1, qx + 1, qy - 1, qy + 1, qz - 1, qz + 1, wx, wy, wz, lane, s_pre, s_start,
                                 t, cnt, s_cc);
@@ -700,7 +724,7 @@ __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArg
       const bool complete = cnt >= 5 && __uint_as_float((unsigned)(t.k[4] >> 32)) < b * b;
       if (!complete) {   // coarse cells floor(q - 1) .. floor(q + 1) per axis (exact in double)
 #pragma unroll
-        for (int k = 0; k < 5; ++k) t.k[k] = ~0ull;
+        for (int k = 0; k < 5; ++k) { t.k[k] = ~0ull; t.s[k] = 0; }
         cnt = 0;
         stencil_scan<G, U, true>(A, (int)floor((double)wx - 1.0), (int)floor((double)wx + 1.0),
                                  (int)floor((double)wy - 1.0), (int)floor((double)wy + 1.0),
@@ -711,12 +735,16 @@ __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArg
       }
       if (cnt >= 5) {   // sqd[4] < 1 (:154, :210)
         flags |= 1;
-        if (lane < 5) {   // lane k writes the coordinates of neighbour k
+        if (lane < 5) {   // lane k writes the coordinates of neighbour k (re-read from its slot in A.gpts)
           unsigned long long kk = t.k[0];
+          int slot = t.s[0];
 #pragma unroll
           for (int k = 1; k < 5; ++k)
-            if (lane == k) kk = t.k[k];
-          const float4 m = A.map[(int)(kk & 0xFFFFFFFFull)];
+            if (lane == k) {
+              kk = t.k[k];
+              slot = t.s[k];
+            }
+          const float4 m = A.gpts[slot];
           A.nnxyz[(3 * lane + 0) * A.cap + i] = m.x;
           A.nnxyz[(3 * lane + 1) * A.cap + i] = m.y;
           A.nnxyz[(3 * lane + 2) * A.cap + i] = m.z;
@@ -1015,7 +1043,8 @@ __device__ __forceinline__ void gather_block(const LMState* __restrict__ lm, con
                                              const int* __restrict__ mapE_count, const int* __restrict__ mapS_count,
                                              const int* __restrict__ fe_status,
                                              const unsigned long long* __restrict__ prof,
-                                             UpdateStatus* __restrict__ out, OdomDev* __restrict__ s, int mode);
+                                             UpdateStatus* __restrict__ out, OdomDev* __restrict__ s, int mode,
+                                             unsigned seq);
 namespace {
 
 __global__ __launch_bounds__(kTB) void deskew_bridge(const LMState* __restrict__ st, OdomDev* __restrict__ s,
@@ -1025,7 +1054,7 @@ __global__ __launch_bounds__(kTB) void deskew_bridge(const LMState* __restrict__
                                                      int ns_ub, int aliased, GatherArgs g, float* __restrict__ vpart,
                                                      unsigned* __restrict__ vctl) {
   const bool lead = blockIdx.x == 0 && blockIdx.y == 0;
-  if (g.out && lead) gather_block(st, g.dcnt, g.mapE_count, g.mapS_count, g.fe_status, nullptr, g.out, s, 0);
+  if (g.out && lead) gather_block(st, g.dcnt, g.mapE_count, g.mapS_count, g.fe_status, nullptr, g.out, s, 0, g.seq);
   double x1[7];
 #pragma unroll
   for (int k = 0; k < 7; ++k) x1[k] = st->x[k];
@@ -1139,7 +1168,8 @@ __device__ __forceinline__ void gather_block(const LMState* __restrict__ lm, con
                                              const int* __restrict__ mapE_count, const int* __restrict__ mapS_count,
                                              const int* __restrict__ fe_status,
                                              const unsigned long long* __restrict__ prof,
-                                             UpdateStatus* __restrict__ out, OdomDev* __restrict__ s, int mode) {
+                                             UpdateStatus* __restrict__ out, OdomDev* __restrict__ s, int mode,
+                                             unsigned seq) {
   constexpr int kWords = kStateWords;
   const unsigned* src = reinterpret_cast<const unsigned*>(lm);
   unsigned* dst = reinterpret_cast<unsigned*>(&out->lm);
@@ -1165,16 +1195,24 @@ __device__ __forceinline__ void gather_block(const LMState* __restrict__ lm, con
     out->odom = s->odom;
     out->last_odom = s->last_odom;
   }
+  // the serial number last, after every other word of the slot is visible to the host: the host polls it instead
+  // of waiting on an event (an event record is a barrier packet that costs the stream ~10 us per update)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    __hip_atomic_store(&out->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 __global__ void gather_status(const LMState* __restrict__ lm, const int* __restrict__ dcnt,
                               const int* __restrict__ mapE_count, const int* __restrict__ mapS_count,
                               const int* __restrict__ fe_status, const unsigned long long* __restrict__ prof,
-                              UpdateStatus* __restrict__ out, OdomDev* __restrict__ s, int mode, VoxelJobDev A,
+                              UpdateStatus* __restrict__ out, OdomDev* __restrict__ s, int mode, unsigned seq,
+                              VoxelJobDev A,
                               VoxelJobDev B, float* __restrict__ vpart, unsigned* __restrict__ vctl,
                               GridClearDev gcE, GridClearDev gcS) {
   const bool lead = blockIdx.x == 0 && blockIdx.y == 0;
-  if (lead) gather_block(lm, dcnt, mapE_count, mapS_count, fe_status, prof, out, s, mode);
+  if (lead) gather_block(lm, dcnt, mapE_count, mapS_count, fe_status, prof, out, s, mode, seq);
   if (!vpart) return;
   if (blockIdx.y < 2) {   // the map update's bounding-box stage (its keyframe gate is applied by the launches after)
     if (lead) radix_ctl_zero(vctl, threadIdx.x, blockDim.x);
@@ -1187,15 +1225,15 @@ __global__ void gather_status(const LMState* __restrict__ lm, const int* __restr
 
 void gather_status_launch(const LMState* lm, const int* dcnt, const int* mapE_count, const int* mapS_count,
                           const int* fe_status, const unsigned long long* prof, UpdateStatus* out, OdomDev* s,
-                          int mode, hipStream_t st, const VoxelFused* vf, const GridClearDev* gc) {
+                          int mode, unsigned seq, hipStream_t st, const VoxelFused* vf, const GridClearDev* gc) {
   const GridClearDev none{};
   if (vf) {
     hipLaunchKernelGGL(gather_status, dim3(kVoxMinMaxBlocks, gc ? 4 : 2), dim3(256), 0, st, lm, dcnt, mapE_count, mapS_count,
-                       fe_status, prof, out, s, mode, vf->A, vf->B, vf->partials, vf->ctl, gc ? gc[0] : none,
+                       fe_status, prof, out, s, mode, seq, vf->A, vf->B, vf->partials, vf->ctl, gc ? gc[0] : none,
                        gc ? gc[1] : none);
   } else {
     hipLaunchKernelGGL(gather_status, dim3(1), dim3(256), 0, st, lm, dcnt, mapE_count, mapS_count, fe_status, prof,
-                       out, s, mode, VoxelJobDev{}, VoxelJobDev{}, nullptr, nullptr, none, none);
+                       out, s, mode, seq, VoxelJobDev{}, VoxelJobDev{}, nullptr, nullptr, none, none);
   }
   FLOAM_LAUNCH_CHECK();
 }

@@ -229,6 +229,8 @@ struct UpdateStatus {
   int kf_flag;                    // KeyFrameUpdate result of this call (when it ran)
   unsigned long long prof[2];     // algorithmic bytes of the kNN launches (profiling)
   Pose odom, last_odom;           // controller poses after this call
+  unsigned seq;                   // the update's serial number, stored last (system scope): the host polls it
+  unsigned seq_pad;
 };
 // status gather; with finish: the call's writeback odom = Isometry(q(x), t(x)) (:114-116; x is the prediction when
 // the gate (:77) kept the solve from running), after a deskewed first call last_odom = the first call's result, and
@@ -236,7 +238,7 @@ struct UpdateStatus {
 enum { GATHER_FINISH = 1, GATHER_AFTER_MID = 2, GATHER_KEYFRAME = 4, GATHER_KEYFRAME_FIRST = 8 };
 void gather_status_launch(const LMState* lm, const int* dcnt, const int* mapE_count, const int* mapS_count,
                           const int* fe_status, const unsigned long long* prof, UpdateStatus* out, OdomDev* s,
-                          int mode, hipStream_t st, const VoxelFused* vf = nullptr,
+                          int mode, unsigned seq, hipStream_t st, const VoxelFused* vf = nullptr,
                           const GridClearDev* gc = nullptr);
 // vf (non-null): the launch also runs the bounding-box stage of the voxel2_launch that follows it (the map update,
 // whose pose is the solve's result): grid (kVoxMinMaxBlocks, 2), block (0, 0) gathers first; gc (with vf, nullable):
@@ -247,6 +249,7 @@ struct GatherArgs {   // a status gather carried out by another launch (deskew_b
   const int* mapS_count = nullptr;
   const int* fe_status = nullptr;
   UpdateStatus* out = nullptr;   // null: nothing to gather
+  unsigned seq = 0;
 };
 
 // KeyFrameUpdate(pose) (src/odomEstimationClass.cpp:320-343) on the device state with an explicit pose {q, t}: the

@@ -337,6 +337,9 @@ typedef struct floam_kernel_timing {
 floam_status floam_profile_enable(int device, int enable);
 floam_status floam_profile_read(int device, floam_kernel_timing* out, int max_entries, int* n_out);
 floam_status floam_profile_reset(int device);
+/* One do-nothing dispatch (kernel `floam_profile_marker`) on the device's library stream: brackets a region of a
+ * rocprofv3 kernel trace (bench.py marks its timed region; tools/prof_summary.py keeps the dispatches between). */
+floam_status floam_profile_mark(int device, int id);
 
 #ifdef __cplusplus
 }

@@ -85,6 +85,103 @@ def test_sharded_two_ranks_match_unsharded(floam_gpu):
         assert dt < 1e-9 and dr < 1e-9, (k, dt, dr)
 
 
+C4_SCANS = 2
+
+
+def _run_c4(rank, world, port, q, mapE, mapS, rccl_world1=False):
+    """BASELINE.json configs[3] (C4: 128 rings, ~262k-point scans, 500k prefill): the sharded path on scans
+    1..C4_SCANS, extraction on the GPU, the map prefilled through initMapWithPoints."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import floam_amd
+        from floam_amd import synth
+        from floam_amd.odom_estimation import comm_unique_id, reset_process_state
+        p = floam_amd.LidarParams(num_lines=128, scan_period=0.1, max_distance=90.0, min_distance=0.5)
+        lp = floam_amd.LaserProcessingClass(device=0)
+        lp.init(p)
+        odo = floam_amd.OdomEstimationClass(device=0)
+        odo.init(p, 0.1, "Cauchy")
+        reset_process_state()
+        if rccl_world1:
+            odo.set_shard(0, 1, comm_unique_id())
+        if world > 1:
+            def allreduce(arr):
+                t = torch.from_numpy(arr)
+                dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            odo.set_shard_callback(rank, world, allreduce)
+        odo.initMapWithPoints(floam_amd.DeviceCloud(mapE, device=0), floam_amd.DeviceCloud(mapS, device=0))
+        poses = []
+        for k in range(1, C4_SCANS + 1):
+            de, ds = floam_amd.DeviceCloud(device=0), floam_amd.DeviceCloud(device=0)
+            lp.featureExtraction(floam_amd.DeviceCloud(synth.generate_scan("c4", k), device=0), de, ds)
+            odo.UpdatePointsToMapSelector(de, ds, True)
+            q_, t_ = odo.pose()
+            poses.append(np.r_[q_, t_])
+        out = (np.array(poses), odo.map_sizes())
+        if q is not None:
+            q.put((rank, out))
+        return out
+    finally:
+        if world > 1:
+            dist.destroy_process_group()
+
+
+def _c4_oracle(oracle_lib, mapE, mapS):
+    from floam_amd import synth
+    ref = oracle_lib.Odometry(128, 0.1, 0.5, 90.0, 0.1, "Cauchy", stable_voxel=True)
+    oracle_lib.reset_process_statics()
+    ref.init_map(mapE, mapS)
+    poses = []
+    for k in range(1, C4_SCANS + 1):
+        e, s, _ = oracle_lib.feature_extraction(synth.generate_scan("c4", k), 128, 0.5, 90.0, canonical=True)
+        ref.update_selector(e, s, True)
+        q_, t_ = ref.pose()
+        poses.append(np.r_[q_, t_])
+    return np.array(poses), (ref.map(0).shape[0], ref.map(1).shape[0])
+
+
+def _assert_close_to_oracle(got, ref, what, tol=1e-6):
+    for k in range(len(ref)):
+        dt = float(np.linalg.norm(got[k][4:] - ref[k][4:]))
+        dr = 2 * math.acos(min(1.0, abs(float(np.dot(got[k][:4], ref[k][:4])))))
+        assert dt < tol and dr < tol, (what, k + 1, dt, dr)
+
+
+def test_sharded_two_ranks_c4_match_oracle(floam_gpu, oracle_lib, prefilled_map):
+    """the query-sharded path at the config the north star shards (C4, 500k prefill): two ranks on
+    one GPU (the host all-reduce over gloo stands in for RCCL, which refuses two ranks on one device), poses
+    identical on both ranks and within 1e-6 m / rad of the oracle; map sizes equal to the oracle's."""
+    import torch.multiprocessing as mp
+    mapE, mapS = prefilled_map("c4")
+    ref, ref_sizes = _c4_oracle(oracle_lib, mapE, mapS)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_run_c4, args=(r, 2, port, q, mapE, mapS)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    res = dict(q.get(timeout=300) for _ in range(2))
+    for pr in procs:
+        pr.join(timeout=120)
+        assert pr.exitcode == 0
+    assert np.array_equal(res[0][0], res[1][0])   # every rank takes the same LM decisions
+    assert res[0][1] == res[1][1] == ref_sizes, (res[0][1], res[1][1], ref_sizes)
+    _assert_close_to_oracle(res[0][0], ref, "2-rank shard")
+
+
+def test_rccl_world1_c4_matches_oracle(floam_gpu, oracle_lib, prefilled_map):
+    """The sharded solve through a one-rank RCCL communicator (ncclAllReduce on the library stream) at C4."""
+    mapE, mapS = prefilled_map("c4")
+    ref, ref_sizes = _c4_oracle(oracle_lib, mapE, mapS)
+    got, sizes = _run_c4(0, 1, _free_port(), None, mapE, mapS, rccl_world1=True)
+    assert sizes == ref_sizes
+    _assert_close_to_oracle(got, ref, "RCCL world 1")
+
+
 @pytest.mark.parametrize("loss,fp32", [("Cauchy", False), ("huber", False), ("Cauchy", True)])
 def test_rccl_world1_matches_unsharded(floam_gpu, loss, fp32):
     """The sharded solve (one launch + one ncclAllReduce of the 29 sums per LM evaluation, the control step folded

@@ -1,16 +1,22 @@
 #!/usr/bin/env python3
 """Condense one GPU session's rocprofv3 output into files worth committing under profiles/<tag>/.
 
-Inputs (written by tools/gpu_round.sh on the GPU box):
-  <run>/prof_trace/run_kernel_stats.csv     rocprofv3 --kernel-trace --stats (no counters)
-  <run>/prof_trace/run_kernel_trace.csv     per-dispatch trace of the same command
+Inputs (written by tools/gpu_prof.sh on the GPU box):
+  <run>/prof_trace/run_kernel_trace.csv     rocprofv3 --kernel-trace --stats (no counters), per dispatch
+  <run>/prof_trace/run_kernel_stats.csv     the --stats summary of the same run (whole process)
   <run>/prof_fetch/run_counter_collection.csv   --pmc FETCH_SIZE pass (own run)
   <run>/prof_write/run_counter_collection.csv   --pmc WRITE_SIZE pass (own run)
 
+The bench marks its timed region with two `floam_profile_marker` dispatches on the library stream
+(floam_profile_mark, bench.py).  Every table here is restricted to that region: kernel-trace dispatches that start
+after the first marker ends and end before the second starts (all streams), and counter rows whose Dispatch_Id lies
+between the two markers' dispatch ids.  Runs without markers fall back to the whole trace (noted in the summary).
+
 Outputs:
-  profiles/<tag>/kernel_stats.csv   the rocprofv3 --stats summary, verbatim
-  profiles/<tag>/summary.md         per-kernel table (calls, avg us, HBM bytes per launch) + bench line
-  profiles/<tag>/hbm_traffic.json   per-kernel PMC bytes per launch, read by bench.py for roofline.traffic
+  profiles/<tag>/kernel_stats.csv   per-kernel calls / total / avg / min / max over the timed region
+  profiles/<tag>/kernel_stats_whole_run.csv   the rocprofv3 --stats summary, verbatim (prefill, replay included)
+  profiles/<tag>/summary.md         per-kernel table (calls per scan, avg us, HBM bytes per launch) + bench line
+  profiles/<tag>/hbm_traffic.json   per-kernel PMC bytes per launch (timed region), read by bench.py's roofline
 
 HBM bytes per launch follow /opt/skills/guides/MI355X_MICROARCH.md § HBM: FETCH_SIZE and WRITE_SIZE are KiB;
 on gfx950 FETCH_SIZE reports half the bytes of a wide (16 B/lane) coalesced read, so it is doubled; WRITE_SIZE
@@ -24,78 +30,106 @@ import json
 import os
 import shutil
 
+MARKER = "floam_profile_marker"
+
 
 def short(name, n=64):
     name = name.replace("floam::(anonymous namespace)::", "").replace("rocprim::ROCPRIM_400200_NS::detail::", "rocprim::")
     return name if len(name) <= n else name[: n - 1] + "…"
 
 
-def counters(path, counter, last=0):
-    """Average KiB per dispatch of each kernel; with last > 0, over its last `last` dispatches only (the bench's
-    timed region is the tail of the run)."""
-    per = collections.defaultdict(list)
-    if not os.path.exists(path):
-        return {}
-    rows = [r for r in csv.DictReader(open(path)) if r["Counter_Name"] == counter]
-    rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+def trace_region(path):
+    """(rows in the timed region, marked?) of a kernel_trace.csv."""
+    rows = list(csv.DictReader(open(path)))
     for r in rows:
+        r["_s"], r["_e"] = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+    rows.sort(key=lambda r: r["_s"])
+    marks = [r for r in rows if MARKER in r["Kernel_Name"]]
+    if len(marks) < 2:
+        return rows, False, None
+    t0, t1 = marks[0]["_e"], marks[1]["_s"]
+    return [r for r in rows if r["_s"] >= t0 and r["_e"] <= t1 and MARKER not in r["Kernel_Name"]], True, (t0, t1)
+
+
+def counters(path, counter):
+    """Average KiB per dispatch of each kernel over the timed region (between the markers' dispatch ids)."""
+    if not os.path.exists(path):
+        return {}, False
+    rows = [r for r in csv.DictReader(open(path)) if r["Counter_Name"] == counter]
+    marks = sorted(int(r["Dispatch_Id"]) for r in rows if MARKER in r["Kernel_Name"])
+    marked = len(marks) >= 2
+    per = collections.defaultdict(list)
+    for r in rows:
+        d = int(r["Dispatch_Id"])
+        if MARKER in r["Kernel_Name"] or (marked and not marks[0] < d < marks[1]):
+            continue
         per[r["Kernel_Name"]].append(float(r["Counter_Value"]))
-    return {k: sum(v[-last:] if last else v) / len(v[-last:] if last else v) for k, v in per.items()}
+    return {k: sum(v) / len(v) for k, v in per.items()}, marked
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("run", help="gpurun_out/<tag> directory")
     ap.add_argument("tag")
-    ap.add_argument("--last", type=int, default=240,
-                    help="dispatches per kernel averaged for hbm_traffic.json (the timed tail; default = 60 scans x 4 "
-                         "solves)")
     ap.add_argument("--config", default="c3", help="bench config the profiled run used (bench.py keys traffic by it)")
+    ap.add_argument("--steps", type=int, default=60, help="timed scans of the profiled bench run")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles"))
     args = ap.parse_args()
     out = os.path.join(args.out, args.tag)
     os.makedirs(out, exist_ok=True)
-    stats_csv = os.path.join(args.run, "prof_trace", "run_kernel_stats.csv")
-    shutil.copy(stats_csv, os.path.join(out, "kernel_stats.csv"))
-    stats = list(csv.DictReader(open(stats_csv)))
-    fetch = counters(os.path.join(args.run, "prof_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
-    write = counters(os.path.join(args.run, "prof_write", "run_counter_collection.csv"), "WRITE_SIZE")
-    fetch_t = counters(os.path.join(args.run, "prof_fetch", "run_counter_collection.csv"), "FETCH_SIZE", args.last)
-    write_t = counters(os.path.join(args.run, "prof_write", "run_counter_collection.csv"), "WRITE_SIZE", args.last)
+    shutil.copy(os.path.join(args.run, "prof_trace", "run_kernel_stats.csv"),
+                os.path.join(out, "kernel_stats_whole_run.csv"))
+    rows, marked, span = trace_region(os.path.join(args.run, "prof_trace", "run_kernel_trace.csv"))
+    per = collections.defaultdict(list)
+    for r in rows:
+        per[r["Kernel_Name"]].append((r["_e"] - r["_s"]) / 1e3)
+    total = sum(sum(v) for v in per.values())
+    stats = sorted(per.items(), key=lambda kv: -sum(kv[1]))
+    with open(os.path.join(out, "kernel_stats.csv"), "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Name", "Calls", "CallsPerScan", "TotalUs", "AvgUs", "MinUs", "MaxUs", "Percentage"])
+        for name, d in stats:
+            w.writerow([name, len(d), f"{len(d) / args.steps:.2f}", f"{sum(d):.1f}", f"{sum(d) / len(d):.2f}",
+                        f"{min(d):.2f}", f"{max(d):.2f}", f"{100 * sum(d) / total:.2f}"])
+    fetch, fm = counters(os.path.join(args.run, "prof_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
+    write, wm = counters(os.path.join(args.run, "prof_write", "run_counter_collection.csv"), "WRITE_SIZE")
     bench = None
     bpath = os.path.join(args.run, "bench.json")
     if os.path.exists(bpath) and os.path.getsize(bpath):
         bench = json.loads(open(bpath).read().strip().splitlines()[-1])
-
-    traffic = {}
+    region = (f"the timed region only ({args.steps} scans between the bench's two `{MARKER}` dispatches, "
+              f"{(span[1] - span[0]) / 1e6:.2f} ms of trace)" if marked else
+              "the WHOLE run (no markers found: prefill and replay included)")
     lines = [f"# rocprofv3 summary — {args.tag}", "",
-             f"Command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --cpu-baseline-seconds 0` ({args.config}, 8 warm-up + "
-             "60 timed scans, then the same 68 scans replayed with per-launch events for the roofline; all dispatches of the run, map prefill included).  HBM bytes: separate "
-             "`--pmc FETCH_SIZE` and `--pmc WRITE_SIZE` runs of the same command; FETCH_SIZE doubled (gfx950 16-B/lane "
-             "read correction), KiB → bytes.", "",
-             "| kernel | calls | total us | avg us | % | HBM read B/launch | HBM write B/launch |",
-             "|---|---|---|---|---|---|---|"]
-    for r in stats:
-        name = r["Name"]
+             f"Command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --cpu-baseline-seconds 0 --no-secondary` "
+             f"({args.config}).  Dispatches of {region}.  HBM bytes: separate `--pmc FETCH_SIZE` and `--pmc WRITE_SIZE` "
+             "runs of the same command, restricted the same way by dispatch id "
+             f"({'marked' if fm and wm else 'unmarked'}); FETCH_SIZE doubled (gfx950 16-B/lane read correction), "
+             "KiB → bytes.  Kernel time sums over all streams (the feature extraction overlaps the odometry).", "",
+             "| kernel | calls | per scan | total us | avg us | min us | max us | % | HBM read B/launch | HBM write B/launch |",
+             "|---|---|---|---|---|---|---|---|---|---|"]
+    traffic = {}
+    for name, d in stats:
         f = fetch.get(name)
-        w = write.get(name)
+        wv = write.get(name)
         rd = None if f is None else 2.0 * f * 1024.0
-        wr = None if w is None else w * 1024.0
-        if name in fetch_t or name in write_t:
-            rt = 2.0 * fetch_t.get(name, 0.0) * 1024.0
-            wt = write_t.get(name, 0.0) * 1024.0
-            traffic[name] = {"read_bytes": rt, "write_bytes": wt, "total_bytes": rt + wt}
-        lines.append(f"| `{short(name)}` | {r['Calls']} | {float(r['TotalDurationNs']) / 1e3:.1f} | "
-                     f"{float(r['AverageNs']) / 1e3:.2f} | {float(r['Percentage']):.2f} | "
+        wr = None if wv is None else wv * 1024.0
+        if rd is not None or wr is not None:
+            traffic[name] = {"read_bytes": rd or 0.0, "write_bytes": wr or 0.0, "total_bytes": (rd or 0.0) + (wr or 0.0)}
+        lines.append(f"| `{short(name)}` | {len(d)} | {len(d) / args.steps:.2f} | {sum(d):.1f} | {sum(d) / len(d):.2f} | "
+                     f"{min(d):.2f} | {max(d):.2f} | {100 * sum(d) / total:.2f} | "
                      f"{'' if rd is None else f'{rd:,.0f}'} | {'' if wr is None else f'{wr:,.0f}'} |")
+    lines += ["", f"Kernel time per scan (all streams): {total / args.steps:.1f} us; dispatches per scan: "
+              f"{sum(len(d) for d in per.values()) / args.steps:.2f}"]
     if bench:
         lines += ["", "## bench line of the same session (un-profiled run)", "", "```json", json.dumps(bench), "```"]
     open(os.path.join(out, "summary.md"), "w").write("\n".join(lines) + "\n")
-    json.dump({"source": f"profiles/{args.tag}", "config": args.config, "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate runs; "
-               f"FETCH_SIZE x2 (gfx950), KiB->B; average over the kernel's last {args.last} dispatches (timed tail)",
+    json.dump({"source": f"profiles/{args.tag}", "config": args.config,
+               "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate runs; FETCH_SIZE x2 (gfx950), KiB->B; "
+                         "average over the dispatches of the timed region (between the bench's marker dispatches)",
                "kernels": traffic},
               open(os.path.join(out, "hbm_traffic.json"), "w"), indent=1)
-    print("\n".join(lines[:40]))
+    print("\n".join(lines[:50]))
 
 
 if __name__ == "__main__":
