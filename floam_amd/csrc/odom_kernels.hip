@@ -385,52 +385,34 @@ __device__ __forceinline__ int2 grid_lookup(const Cell* __restrict__ tab, unsign
 // points in the fine (0.5-m) cell (fx, fy, fz): its sub-cell count in the entry of the coarse cell that holds it
 __device__ __forceinline__ int fine_count(const struct CorrArgs& A, int fx, int fy, int fz);
 
-// a (key, slot) compare-exchange: the slot of a candidate is its position in the cell-grouped point array (A.gpts),
-// carried beside its (distance, map index) key so the winners' coordinates are re-read from the lines the search
-// itself just fetched, not gathered from the by-index array
-__device__ __forceinline__ void cswap(unsigned long long& a, unsigned long long& b, int& sa, int& sb) {
-  const bool sw = b < a;
-  const unsigned long long lo = sw ? b : a, hi = sw ? a : b;
-  const int slo = sw ? sb : sa, shi = sw ? sa : sb;
+__device__ __forceinline__ void cswap(unsigned long long& a, unsigned long long& b) {
+  const unsigned long long lo = a < b ? a : b, hi = a < b ? b : a;
   a = lo;
   b = hi;
-  sa = slo;
-  sb = shi;
 }
 
 struct Top5 {
-  unsigned long long k[5];   // (float distance bits << 32) | map index, ascending
-  int s[5];                  // their slots in A.gpts
+  unsigned long long k[5];
 };
 
-__device__ __forceinline__ void top5_insert(Top5& t, unsigned long long key, int slot) {
+__device__ __forceinline__ void top5_insert(Top5& t, unsigned long long key) {
   if (key >= t.k[4]) return;
   t.k[4] = key;
-  t.s[4] = slot;
-  cswap(t.k[3], t.k[4], t.s[3], t.s[4]);
-  cswap(t.k[2], t.k[3], t.s[2], t.s[3]);
-  cswap(t.k[1], t.k[2], t.s[1], t.s[2]);
-  cswap(t.k[0], t.k[1], t.s[0], t.s[1]);
+  cswap(t.k[3], t.k[4]);
+  cswap(t.k[2], t.k[3]);
+  cswap(t.k[1], t.k[2]);
+  cswap(t.k[0], t.k[1]);
 }
 
 // 5 smallest of two ascending 5-lists: bitonic split min(a[i], b[4-i]), then a 5-input sorting network
 __device__ __forceinline__ void top5_merge(Top5& a, const Top5& b) {
   unsigned long long m[5];
-  int ms[5];
 #pragma unroll
-  for (int i = 0; i < 5; ++i) {
-    const bool ta = a.k[i] < b.k[4 - i];
-    m[i] = ta ? a.k[i] : b.k[4 - i];
-    ms[i] = ta ? a.s[i] : b.s[4 - i];
-  }
-  cswap(m[0], m[1], ms[0], ms[1]); cswap(m[3], m[4], ms[3], ms[4]); cswap(m[2], m[4], ms[2], ms[4]);
-  cswap(m[2], m[3], ms[2], ms[3]); cswap(m[0], m[3], ms[0], ms[3]); cswap(m[0], m[2], ms[0], ms[2]);
-  cswap(m[1], m[4], ms[1], ms[4]); cswap(m[1], m[3], ms[1], ms[3]); cswap(m[1], m[2], ms[1], ms[2]);
+  for (int i = 0; i < 5; ++i) m[i] = a.k[i] < b.k[4 - i] ? a.k[i] : b.k[4 - i];
+  cswap(m[0], m[1]); cswap(m[3], m[4]); cswap(m[2], m[4]); cswap(m[2], m[3]); cswap(m[0], m[3]);
+  cswap(m[0], m[2]); cswap(m[1], m[4]); cswap(m[1], m[3]); cswap(m[1], m[2]);
 #pragma unroll
-  for (int i = 0; i < 5; ++i) {
-    a.k[i] = m[i];
-    a.s[i] = ms[i];
-  }
+  for (int i = 0; i < 5; ++i) a.k[i] = m[i];
 }
 
 template <int G>
@@ -622,11 +604,9 @@ __device__ __forceinline__ void stencil_scan(const CorrArgs& A, int x0, int x1, 
   int c = 0, c_lo = 0, c_hi = s_pre[1], c_start = s_start[0];   // cursor: cell c = [c_lo, c_hi)
   for (int tb = 0; tb < tot; tb += G * U) {
     float4 m[U];
-    int sl[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int tt = tb + u * G + lane;
-      sl[u] = 0;
       if (tt < tot) {
         while (tt >= c_hi) {
           ++c;
@@ -634,8 +614,7 @@ __device__ __forceinline__ void stencil_scan(const CorrArgs& A, int x0, int x1, 
           c_hi = s_pre[c + 1];
           c_start = s_start[c];
         }
-        sl[u] = c_start + (tt - c_lo);
-        m[u] = A.gpts[sl[u]];
+        m[u] = A.gpts[c_start + (tt - c_lo)];
       } else {
         m[u] = make_float4(1e30f, 1e30f, 1e30f, 0.0f);
       }
@@ -651,7 +630,7 @@ __device__ __forceinline__ void stencil_scan(const CorrArgs& A, int x0, int x1, 
       dd += df * df;
       if (dd < 1.0f) {
         ++cnt;
-        top5_insert(t, ((unsigned long long)__float_as_uint(dd) << 32) | (unsigned)__float_as_int(m[u].w), sl[u]);
+        top5_insert(t, ((unsigned long long)__float_as_uint(dd) << 32) | (unsigned)__float_as_int(m[u].w));
       }
     }
   }
@@ -665,10 +644,7 @@ __device__ __forceinline__ void group_merge(Top5& t, int& cnt) {
   for (int mm = G / 2; mm > 0; mm >>= 1) {
     Top5 o;
 #pragma unroll
-    for (int k = 0; k < 5; ++k) {
-      o.k[k] = shfl_xor_u64<G>(t.k[k], mm);
-      o.s[k] = __shfl_xor(t.s[k], mm, G);
-    }
+    for (int k = 0; k < 5; ++k) o.k[k] = shfl_xor_u64<G>(t.k[k], mm);
     top5_merge(t, o);
     cnt += __shfl_xor(cnt, mm, G);
   }
@@ -710,7 +686,7 @@ __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArg
       fine_cell(wx, wy, wz, qx, qy, qz);
       Top5 t;
 #pragma unroll
-      for (int k = 0; k < 5; ++k) { t.k[k] = ~0ull; t.s[k] = 0; }
+      for (int k = 0; k < 5; ++k) t.k[k] = ~0ull;
       int cnt = 0;
       stencil_scan<G, U, false>(A, qx - 1, qx + 1, qy - 1, qy + 1, qz - 1, qz + 1, wx, wy, wz, lane, s_pre, s_start,
                                 t, cnt, s_cc);
@@ -724,7 +700,7 @@ __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArg
       const bool complete = cnt >= 5 && __uint_as_float((unsigned)(t.k[4] >> 32)) < b * b;
       if (!complete) {   // coarse cells floor(q - 1) .. floor(q + 1) per axis (exact in double)
 #pragma unroll
-        for (int k = 0; k < 5; ++k) { t.k[k] = ~0ull; t.s[k] = 0; }
+        for (int k = 0; k < 5; ++k) t.k[k] = ~0ull;
         cnt = 0;
         stencil_scan<G, U, true>(A, (int)floor((double)wx - 1.0), (int)floor((double)wx + 1.0),
                                  (int)floor((double)wy - 1.0), (int)floor((double)wy + 1.0),
@@ -735,16 +711,12 @@ __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArg
       }
       if (cnt >= 5) {   // sqd[4] < 1 (:154, :210)
         flags |= 1;
-        if (lane < 5) {   // lane k writes the coordinates of neighbour k (re-read from its slot in A.gpts)
+        if (lane < 5) {   // lane k writes the coordinates of neighbour k
           unsigned long long kk = t.k[0];
-          int slot = t.s[0];
 #pragma unroll
           for (int k = 1; k < 5; ++k)
-            if (lane == k) {
-              kk = t.k[k];
-              slot = t.s[k];
-            }
-          const float4 m = A.gpts[slot];
+            if (lane == k) kk = t.k[k];
+          const float4 m = A.map[(int)(kk & 0xFFFFFFFFull)];
           A.nnxyz[(3 * lane + 0) * A.cap + i] = m.x;
           A.nnxyz[(3 * lane + 1) * A.cap + i] = m.y;
           A.nnxyz[(3 * lane + 2) * A.cap + i] = m.z;
