@@ -29,6 +29,7 @@
 #include "floam_common.hpp"
 #include "formats.hpp"
 #include "imu.hpp"
+#include "mapmerge.hpp"
 #include "mapping.hpp"
 #include "odom_kernels.hpp"
 #include "pose.hpp"
@@ -271,6 +272,15 @@ struct floam_odom {
   // local map (device) and host-known exact sizes (valid as of the last synchronisation)
   floam_cloud mapE, mapS;
   floam_cloud mapE_next, mapS_next;   // double buffers: the map update writes here, then the two swap
+  // the maps' cell keys (mapmerge.hpp: the incremental map update), double-buffered with the maps: [map][buffer],
+  // buffer mkcur the current one; mmeta: what the keys are worth (invalid after initMapWithPoints: a raw map)
+  DevBuf<unsigned long long> mkeys[2][2];
+  DevBuf<MapMeta> mmeta[2][2];
+  int mkcur = 0;
+  MapMergeScratch mms;
+  bool map_merge = true;          // FLOAM_MAP_MERGE=0: the whole-map VoxelGrid of round 2 (A/B)
+  bool map_force_full = false;    // FLOAM_MAP_FULL=1: the merge pipeline always takes its full-sort path (tests)
+  int map_violate_mod = 0;        // FLOAM_MM_VIOLATE=n: every n-th merge reports its keys out of order (tests)
   size_t mapE_n = 0, mapS_n = 0;   // map sizes: exact after a synchronisation, else upper bounds
   // scratch
   DevBuf<PointRec> dE, dS, tmp;
@@ -477,6 +487,7 @@ struct MapUpdatePlan {
   VoxelJob je, js;
   int ne_ub = 0, ns_ub = 0;
   VoxelFused vf;   // the bounding-box stage, run by the status gather before the update
+  MapKeys ke, ks;  // the incremental merge (o->map_merge)
 };
 
 // downSamplingToMap's two VoxelGrids of one call (:137-142): edge cloud at the edge leaf, surf cloud at the surf leaf
@@ -670,6 +681,14 @@ floam_status odom_collect_one(floam_odom* o, DeviceCtx& ctx) {
   o->pendS -= P.addS;
   if (P.ev) FLOAM_HIP(hipEventSynchronize(P.ev));   // (a recycled event: not destroyed)
   wait_status(o, ctx, P);
+  static const bool mm_debug = std::getenv("FLOAM_MM_DEBUG") != nullptr;   // (diagnostic: the merge's modes)
+  if (mm_debug && o->map_merge && o->mms.ctl.p) {
+    FLOAM_HIP(hipStreamSynchronize(ctx.stream));
+    int c[kMergeCtlWords];
+    FLOAM_HIP(hipMemcpy(c, o->mms.ctl.p, sizeof(c), hipMemcpyDeviceToHost));
+    std::fprintf(stderr, "[floam mm] update %llu: set %d / %d, full %d / %d, overflow %d / %d\n", P.seq, c[0], c[1], c[2],
+                 c[3], c[4], c[5]);
+  }
   o->collected_seq = P.seq;
   *o->done_ctr = P.seq;
   for (void* b : P.graveyard) (void)hipFree(b);
@@ -840,6 +859,22 @@ MapUpdatePlan odom_map_plan(floam_odom* o, DeviceCtx& ctx, int ne_ub, int ns_ub)
   js.part1 = o->dS.p; js.d_n1 = o->cnt.p + 1; js.n1_ub = ns_ub;
   js.pose = o->lm.p->x; js.leaf = o->leafS; js.out = o->mapS_next.pts.p; js.d_out = o->mapS_next.count.p;
   P.vf = voxel2_prepare(o->vs, je, js, st);
+  if (o->map_merge) {
+    const int cur = o->mkcur, nxt = cur ^ 1;
+    for (int m = 0; m < 2; ++m) {
+      o->mkeys[m][cur].reserve(std::max(m ? (int)o->mapS_n : (int)o->mapE_n, 1));
+      o->mkeys[m][nxt].reserve(std::max(m ? ubS : ubE, 1));
+      for (int b = 0; b < 2; ++b)
+        if (!o->mmeta[m][b].p) {
+          o->mmeta[m][b].reserve(1);
+          FLOAM_HIP(hipMemsetAsync(o->mmeta[m][b].p, 0, sizeof(MapMeta), st));
+        }
+    }
+    o->mms.reserve(1, st);
+    P.ke = MapKeys{o->mkeys[0][cur].p, o->mmeta[0][cur].p, o->mkeys[0][nxt].p, o->mmeta[0][nxt].p};
+    P.ks = MapKeys{o->mkeys[1][cur].p, o->mmeta[1][cur].p, o->mkeys[1][nxt].p, o->mmeta[1][nxt].p};
+    P.vf.mc = merge_check(o->mms, (unsigned)o->issued);
+  }
   return P;
 }
 
@@ -851,7 +886,13 @@ void odom_map_update(floam_odom* o, DeviceCtx& ctx, const MapUpdatePlan& P, size
   hipStream_t st = ctx.stream;
   ProfScope ps(ctx, "map_update", FLOAM_PROF_CLOUD);
   const int ubS = (int)o->mapS_n + P.ns_ub, ubE = (int)o->mapE_n + P.ne_ub;
-  voxel2_launch(o->vs, P.je, P.js, st, &o->ds.p->kf_flag, true);
+  if (o->map_merge) {   // the new scan voxels merged into the voxel-ordered maps (mapmerge.hip)
+    map_merge_launch(o->vs, o->mms, P.je, P.js, P.ke, P.ks, &o->ds.p->kf_flag, (unsigned)o->issued,
+                     o->map_force_full, o->map_violate_mod, st);
+    o->mkcur ^= 1;
+  } else {
+    voxel2_launch(o->vs, P.je, P.js, st, &o->ds.p->kf_flag, true);
+  }
   cloud_swap(&o->mapE, &o->mapE_next);
   cloud_swap(&o->mapS, &o->mapS_next);
   addE = (size_t)P.ne_ub;
@@ -1275,6 +1316,9 @@ floam_status floam_odom_create(const floam_lidar_params* p, double map_resolutio
     o->device = device;
     o->lp = *p;
     o->map_resolution = map_resolution;
+    if (const char* e = std::getenv("FLOAM_MAP_MERGE")) o->map_merge = e[0] != '0';
+    if (const char* e = std::getenv("FLOAM_MAP_FULL")) o->map_force_full = e[0] == '1';
+    if (const char* e = std::getenv("FLOAM_MM_VIOLATE")) o->map_violate_mod = std::atoi(e);
     std::string l = loss ? loss : "";
     std::transform(l.begin(), l.end(), l.begin(), [](unsigned char c) { return (char)std::tolower(c); });
     o->huber = (l == "huber");   // any other string: no robust loss (Q3)
@@ -1354,6 +1398,10 @@ floam_status floam_odom_init_map(floam_odom* o, const floam_cloud* edge, const f
     o->mapE.host_count = o->mapE_n; o->mapE.host_count_valid = true;
     o->mapS.host_count = o->mapS_n; o->mapS.host_count_valid = true;
     o->grid_dirty = true;
+    for (int m = 0; m < 2; ++m) {   // a raw map (Q8): no cell keys until a map update has voxelised it
+      o->mmeta[m][o->mkcur].reserve(1);
+      FLOAM_HIP(hipMemsetAsync(o->mmeta[m][o->mkcur].p, 0, sizeof(MapMeta), st));
+    }
     o->optimization_count = 12;   // (:31)
     FLOAM_HIP(hipStreamSynchronize(st));
     return FLOAM_OK;

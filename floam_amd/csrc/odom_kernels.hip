@@ -1182,13 +1182,19 @@ __global__ void gather_status(const LMState* __restrict__ lm, const int* __restr
                               UpdateStatus* __restrict__ out, OdomDev* __restrict__ s, int mode, unsigned seq,
                               VoxelJobDev A,
                               VoxelJobDev B, float* __restrict__ vpart, unsigned* __restrict__ vctl,
-                              GridClearDev gcE, GridClearDev gcS) {
+                              GridClearDev gcE, GridClearDev gcS, MergeCheck mc) {
   const bool lead = blockIdx.x == 0 && blockIdx.y == 0;
   if (lead) gather_block(lm, dcnt, mapE_count, mapS_count, fe_status, prof, out, s, mode, seq);
   if (!vpart) return;
   if (blockIdx.y < 2) {   // the map update's bounding-box stage (its keyframe gate is applied by the launches after)
-    if (lead) radix_ctl_zero(vctl, threadIdx.x, blockDim.x);
-    vox_minmax_block(blockIdx.y == 0 ? A : B, (int)blockIdx.y, (int)blockIdx.x, (int)gridDim.x, vpart);
+    if (lead) {
+      radix_ctl_zero(vctl, threadIdx.x, blockDim.x);
+      if (mc.ctl && threadIdx.x < kMergeCtlWords) mc.ctl[threadIdx.x] = 0;
+    }
+    if (mc.flags)   // + the incremental merge's checks (mapmerge.hip)
+      mm_minmax_block(blockIdx.y == 0 ? A : B, (int)blockIdx.y, (int)blockIdx.x, (int)gridDim.x, vpart, mc);
+    else
+      vox_minmax_block(blockIdx.y == 0 ? A : B, (int)blockIdx.y, (int)blockIdx.x, (int)gridDim.x, vpart);
   } else if (gcE.coarse) {   // blocks of their own: the next grid builds' clears (this update's kNN launches are done)
     grid_clear_part(blockIdx.y == 2 ? gcE : gcS, blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x,
                     blockIdx.x == 0 && threadIdx.x == 0);
@@ -1202,10 +1208,10 @@ void gather_status_launch(const LMState* lm, const int* dcnt, const int* mapE_co
   if (vf) {
     hipLaunchKernelGGL(gather_status, dim3(kVoxMinMaxBlocks, gc ? 4 : 2), dim3(256), 0, st, lm, dcnt, mapE_count, mapS_count,
                        fe_status, prof, out, s, mode, seq, vf->A, vf->B, vf->partials, vf->ctl, gc ? gc[0] : none,
-                       gc ? gc[1] : none);
+                       gc ? gc[1] : none, vf->mc);
   } else {
     hipLaunchKernelGGL(gather_status, dim3(1), dim3(256), 0, st, lm, dcnt, mapE_count, mapS_count, fe_status, prof,
-                       out, s, mode, seq, VoxelJobDev{}, VoxelJobDev{}, nullptr, nullptr, none, none);
+                       out, s, mode, seq, VoxelJobDev{}, VoxelJobDev{}, nullptr, nullptr, none, none, MergeCheck{});
   }
   FLOAM_LAUNCH_CHECK();
 }

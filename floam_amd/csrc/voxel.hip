@@ -37,31 +37,6 @@ __global__ __launch_bounds__(kTB) void vox_minmax(VoxelJobDev A, VoxelJobDev B, 
   vox_minmax_block(blockIdx.y == 0 ? A : B, (int)blockIdx.y, (int)blockIdx.x, (int)gridDim.x, partials);
 }
 
-struct VoxelGeom {
-  int min_b[3];
-  int divb_mul[3];
-  bool overflow;
-};
-
-// PCL 1.8.1 VoxelGrid::applyFilter index arithmetic (float leaf inverse, int min/max boxes)
-__device__ __forceinline__ VoxelGeom voxel_geom(const float (&mn)[3], const float (&mx)[3], float inv) {
-  VoxelGeom g;
-  const long long dx = (long long)((mx[0] - mn[0]) * inv) + 1;
-  const long long dy = (long long)((mx[1] - mn[1]) * inv) + 1;
-  const long long dz = (long long)((mx[2] - mn[2]) * inv) + 1;
-  g.overflow = (dx * dy * dz) > (long long)INT_MAX;
-  int div_b[3];
-  for (int d = 0; d < 3; ++d) {
-    g.min_b[d] = (int)floorf(mn[d] * inv);
-    const int max_b = (int)floorf(mx[d] * inv);
-    div_b[d] = max_b - g.min_b[d] + 1;
-  }
-  g.divb_mul[0] = 1;
-  g.divb_mul[1] = div_b[0];
-  g.divb_mul[2] = div_b[0] * div_b[1];
-  return g;
-}
-
 __global__ __launch_bounds__(kTB) void vox_keys(VoxelJobDev A, VoxelJobDev B, const float* __restrict__ partials,
                                                 uint32_t* __restrict__ keys, int* __restrict__ vals,
                                                 int* __restrict__ overflow, unsigned long long* __restrict__ status,
@@ -111,10 +86,7 @@ __global__ __launch_bounds__(kTB) void vox_keys(VoxelJobDev A, VoxelJobDev B, co
       if (g.overflow) {
         idx = (uint32_t)i;   // output = input unchanged (Q9): identity order, one "voxel" per point
       } else {
-        const int ijk0 = (int)(floorf(p.x * J.inv) - (float)g.min_b[0]);
-        const int ijk1 = (int)(floorf(p.y * J.inv) - (float)g.min_b[1]);
-        const int ijk2 = (int)(floorf(p.z * J.inv) - (float)g.min_b[2]);
-        idx = (uint32_t)(ijk0 * g.divb_mul[0] + ijk1 * g.divb_mul[1] + ijk2 * g.divb_mul[2]);
+        idx = voxel_idx(g, J.inv, p);
       }
       key = ((uint32_t)job << 31) | idx;
     }

@@ -1,6 +1,7 @@
 // Batched pcl::VoxelGrid (+ the map-side half of addPointsToMap) — see voxel.hip.
 #pragma once
 #include <cfloat>
+#include <climits>
 
 #include "cloud_ops.hpp"
 #include "floam_common.hpp"
@@ -71,6 +72,39 @@ __device__ __forceinline__ bool vox_fetch(const VoxelJobDev& J, int n0, int n1, 
 
 constexpr int kVoxMinMaxBlocks = 64;   // bounding-box partials per cloud
 
+struct VoxelGeom {
+  int min_b[3];
+  int divb_mul[3];
+  bool overflow;
+};
+
+// PCL 1.8.1 VoxelGrid::applyFilter index arithmetic (float leaf inverse, int min/max boxes)
+__device__ __forceinline__ VoxelGeom voxel_geom(const float (&mn)[3], const float (&mx)[3], float inv) {
+  VoxelGeom g;
+  const long long dx = (long long)((mx[0] - mn[0]) * inv) + 1;
+  const long long dy = (long long)((mx[1] - mn[1]) * inv) + 1;
+  const long long dz = (long long)((mx[2] - mn[2]) * inv) + 1;
+  g.overflow = (dx * dy * dz) > (long long)INT_MAX;
+  int div_b[3];
+  for (int d = 0; d < 3; ++d) {
+    g.min_b[d] = (int)floorf(mn[d] * inv);
+    const int max_b = (int)floorf(mx[d] * inv);
+    div_b[d] = max_b - g.min_b[d] + 1;
+  }
+  g.divb_mul[0] = 1;
+  g.divb_mul[1] = div_b[0];
+  g.divb_mul[2] = div_b[0] * div_b[1];
+  return g;
+}
+
+// the voxel index of a point inside the grid's box (vox_keys; 32 bits with the cloud in bit 31)
+__device__ __forceinline__ uint32_t voxel_idx(const VoxelGeom& g, float inv, const PointRec& p) {
+  const int ijk0 = (int)(floorf(p.x * inv) - (float)g.min_b[0]);
+  const int ijk1 = (int)(floorf(p.y * inv) - (float)g.min_b[1]);
+  const int ijk2 = (int)(floorf(p.z * inv) - (float)g.min_b[2]);
+  return (uint32_t)(ijk0 * g.divb_mul[0] + ijk1 * g.divb_mul[1] + ijk2 * g.divb_mul[2]);
+}
+
 // The bounding-box stage for one cloud: min / max over the elements i = b * blockDim.x + threadIdx.x (+ k * nblocks *
 // blockDim.x) that vox_fetch keeps, reduced over the block and stored as partial b of cloud `job`.  Called by every
 // thread of a block; blocks b = 0 .. nblocks - 1 (nblocks = kVoxMinMaxBlocks) of each job must all run.
@@ -108,6 +142,51 @@ __device__ __forceinline__ void vox_minmax_block(const VoxelJobDev& J, int job, 
   vox_partial_store(mn, mx, job, b, partials);
 }
 
+// The map's voxel order key: the cell (floor(z inv), floor(y inv), floor(x inv)) packed lexicographically, 21 bits a
+// component (offset 2^20).  For points inside a VoxelGrid's bounding box this orders exactly as PCL's
+// idx = i + j dx + k dx dy (ijk = floor(p inv) - min_b: a translation), whatever min_b is.  ok = false for
+// non-finite coordinates or cells beyond +-2^20 (the merge then falls back to the full sort).
+__device__ __forceinline__ unsigned long long mm_cell_key(float x, float y, float z, float inv, bool& ok) {
+  const float fx = floorf(x * inv), fy = floorf(y * inv), fz = floorf(z * inv);
+  constexpr float kLim = 1048575.0f;   // 2^20 - 1
+  ok = fabsf(fx) <= kLim && fabsf(fy) <= kLim && fabsf(fz) <= kLim;   // (false for NaN)
+  if (!ok) return ~0ull;
+  const unsigned long long cx = (unsigned long long)((int)fx + (1 << 20));
+  const unsigned long long cy = (unsigned long long)((int)fy + (1 << 20));
+  const unsigned long long cz = (unsigned long long)((int)fz + (1 << 20));
+  return (cz << 42) | (cy << 21) | cx;
+}
+
+// What the map update's bounding-box stage (run inside the status gather) checks for the merge: a non-finite scan
+// point (part1) of job j stores `seq` into flags[j] (the update then takes the full sort; the map's own points are
+// covered by its stored cell keys, mapmerge.hip).  ctl: the merge's per-update words, zeroed by the same launch.
+struct MergeCheck {
+  unsigned* flags = nullptr;   // [2]
+  int* ctl = nullptr;          // [kMergeCtlWords]
+  unsigned seq = 0;
+};
+// [0, 1] kept set elements of job A / B, [2, 3] mode (1 full), [4, 5] overflow, [6 + 6j .. 11 + 6j] job j's min_b[3],
+// div_b[3]
+constexpr int kMergeCtlWords = 18;
+
+// bounding box of one cloud (as vox_minmax_block) + the MergeCheck test of its scan points
+__device__ __forceinline__ void mm_minmax_block(const VoxelJobDev& J, int job, int b, int nblocks,
+                                                float* __restrict__ partials, const MergeCheck& mc) {
+  const int n0 = *J.d_n0, n1 = J.d_n1 ? *J.d_n1 : 0;
+  float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+  bool bad = false;
+  for (int i = b * blockDim.x + threadIdx.x; i < n0 + n1; i += nblocks * blockDim.x) {
+    PointRec p;
+    const bool kept = vox_fetch(J, n0, n1, i, p);
+    if (i >= n0 && !(isfinite(p.x) && isfinite(p.y) && isfinite(p.z))) bad = true;   // (cropped ones too)
+    if (!kept) continue;
+    mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
+    mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
+  }
+  if (__any(bad) && (threadIdx.x & 63) == 0) mc.flags[job] = mc.seq;
+  vox_partial_store(mn, mx, job, b, partials);
+}
+
 // What a producer kernel needs to run the bounding-box stage of a voxel2_launch issued after it (minmax_done):
 // both clouds' device jobs, the partials, and the sort's control words, which block (0, 0) zeroes
 // (radix_ctl_zero) once its previous sort is complete in stream order.
@@ -115,6 +194,7 @@ struct VoxelFused {
   VoxelJobDev A, B;
   float* partials;
   unsigned* ctl;
+  MergeCheck mc;   // the map update (mapmerge.hpp): the merge's checks run in the same stage (mc.flags != null)
 };
 
 struct VoxelScratch2 {
