@@ -5,7 +5,8 @@
 // the same four launches:
 //   grid_clear   empty the table entries the previous build occupied (its slot lists; everything after a resize)
 //   grid_count   per point: insert its coarse cell (1 m, absolute coordinates -> 64-bit key; new cells appended to
-//                the occupied list), count it in its fine sub-cell (0.5 m) and keep its rank there
+//                the occupied list), count it in its fine sub-cell (0.5 m) and keep its rank there — run by the map
+//                update's last launch instead, as it writes the map (grid_count_job, mapmerge.hip)
 //   grid_alloc   per occupied coarse cell (from the list): a contiguous range of the cell-grouped array (one atomic
 //                per block on a bump cursor), fine sub-cells consecutive inside it
 //   grid_scatter per point: its slot = coarse start + preceding sub-cells + rank
@@ -46,87 +47,34 @@ __device__ __forceinline__ CoarseCell empty_coarse() {
   return c;
 }
 
-// wave-aggregated append of `slot` (lanes with take) to list[*count ...]
-__device__ __forceinline__ void list_append(int* __restrict__ list, int* __restrict__ count, bool take, int slot) {
-  const unsigned long long b = __ballot(take);
-  if (!b) return;
-  const int lane = threadIdx.x & 63;
-  const int leader = __ffsll((long long)b) - 1;
-  int base = 0;
-  if (lane == leader) base = atomicAdd(count, __popcll(b));
-  base = __shfl(base, leader, 64);
-  if (take) list[base + __popcll(b & ((1ull << lane) - 1ull))] = slot;
-}
-
 __global__ __launch_bounds__(kTB) void grid_clear(GridClearDev E, GridClearDev S) {
   grid_clear_part(blockIdx.y == 0 ? E : S, blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x,
                   blockIdx.x == 0 && threadIdx.x == 0);
 }
 
-// Map points are in voxel order, so a wave's 64 points fall in a handful of coarse cells: the wave groups its lanes
-// by cell key (ballots, no memory traffic), one leader per cell inserts it, and one leader per (cell, sub-cell) adds
-// the group's count — a few atomics per wave on each cache line instead of two per point.  Ranks inside a group
-// follow lane order (the order inside a cell is not deterministic across waves either way; the kNN breaks distance
-// ties by map index).
+__host__ __device__ inline GridCountDev count_dev(const GridJob& J) {
+  return GridCountDev{J.coarse, J.where, J.clist_new, J.counters, J.parity, J.bits, J.mask};
+}
+
+// (grid_count_point, grid.hpp)
 __global__ __launch_bounds__(kTB) void grid_count(GridJob E, GridJob S, OdomDev* __restrict__ predict) {
   const GridJob& J = blockIdx.y == 0 ? E : S;
   if (predict && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) odom_predict_step(predict);
   const int m = min(*J.d_m, J.m_ub);
-  const int lane = threadIdx.x & 63;
-  const unsigned long long below = (1ull << lane) - 1ull;
+  const GridCountDev C = count_dev(J);
   for (int i0 = blockIdx.x * blockDim.x; i0 < m; i0 += gridDim.x * blockDim.x) {   // wave-uniform trip count
     const int i = i0 + threadIdx.x;
     const bool valid = i < m;
-    unsigned long long key = kEmptyKey;
-    int sub = 0;
-    if (valid) {
-      const float4 p = *reinterpret_cast<const float4*>(&J.map[i].x);
-      int fx, fy, fz;
-      fine_cell(p.x, p.y, p.z, fx, fy, fz);
-      key = cell_key(fx >> 1, fy >> 1, fz >> 1);
-      sub = (fx & 1) | ((fy & 1) << 1) | ((fz & 1) << 2);
-    }
-    // lanes grouped by key: my_grp = the lanes sharing my cell, leader = its lowest lane
-    unsigned long long pending = __ballot(valid), my_grp = 0ull;
-    while (pending) {
-      const int l = __ffsll((long long)pending) - 1;
-      const unsigned lo = (unsigned)__shfl((int)(unsigned)key, l, 64);
-      const unsigned hi = (unsigned)__shfl((int)(unsigned)(key >> 32), l, 64);
-      const unsigned long long grp = __ballot(valid && key == (((unsigned long long)hi << 32) | lo)) & pending;
-      if ((grp >> lane) & 1ull) my_grp = grp;
-      pending &= ~grp;
-    }
-    const int leader = valid ? __ffsll((long long)my_grp) - 1 : lane;
-    bool fresh = false;
-    unsigned h = 0;
-    if (valid && leader == lane) {
-      h = hash_slot64(key, J.bits);
-      for (;;) {
-        const unsigned long long prev = atomicCAS(&J.coarse[h].key, kEmptyKey, key);
-        if (prev == kEmptyKey) fresh = true;
-        if (prev == kEmptyKey || prev == key) break;
-        h = (h + 1) & J.mask;
-      }
-    }
-    h = (unsigned)__shfl((int)h, leader, 64);
-    // lanes of my cell with my sub-cell: one add per (cell, sub-cell) group, ranks in lane order
-    unsigned long long sub_grp = 0ull;
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const unsigned long long b = __ballot(valid && sub == s);
-      if (sub == s) sub_grp = b & my_grp;
-    }
-    const int leader2 = valid ? __ffsll((long long)sub_grp) - 1 : lane;
-    int base = 0;
-    if (valid && leader2 == lane) base = atomicAdd(&J.coarse[h].sub[sub], __popcll(sub_grp));
-    base = __shfl(base, leader2, 64);
-    if (valid) J.where[i] = make_uint2(h, ((unsigned)sub << 28) | (unsigned)(base + __popcll(sub_grp & below)));
-    list_append(J.clist_new, &J.counters[1 + J.parity], fresh, (int)h);
+    float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (valid) p = *reinterpret_cast<const float4*>(&J.map[i].x);
+    grid_count_point(C, i, valid, p.x, p.y, p.z);
   }
 }
 
-__global__ __launch_bounds__(kTB) void grid_alloc(GridJob E, GridJob S) {
+// predict: as grid_count's, when the count ran in the map update (grid_count_job)
+__global__ __launch_bounds__(kTB) void grid_alloc(GridJob E, GridJob S, OdomDev* __restrict__ predict) {
   const GridJob& J = blockIdx.y == 0 ? E : S;
+  if (predict && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) odom_predict_step(predict);
   const int nc = J.counters[1 + J.parity];
   __shared__ int s_wave[kTB / 64];
   __shared__ int s_base;
@@ -212,6 +160,11 @@ GridJob make_job(Grid& g, const PointRec* map, const int* d_m, int m_ub) {
 }
 }  // namespace
 
+GridCountDev grid_count_job(Grid& g) {
+  g.counted = true;
+  return count_dev(make_job(g, nullptr, nullptr, 0));
+}
+
 GridClearDev grid_clear_prepare(Grid& g, int ub, hipStream_t st) {
   reserve_grid(g, std::max(ub, 1));
   if (g.fresh) FLOAM_HIP(hipMemsetAsync(g.counters.p, 0, sizeof(int) * 8, st));
@@ -229,6 +182,13 @@ void grid_build_launch(Grid& gE, const PointRec* mapE, const int* d_mE, int mE_u
   // added the points is collected); otherwise the clear runs here (again: clearing the same entries is idempotent)
   precleared = precleared && gE.precleared && gS.precleared && (1 << gE.bits) >= 2 * mE_ub &&
                (1 << gS.bits) >= 2 * mS_ub;
+  // counted in advance (grid_count_job) into a cleared table of this size; otherwise the counts of such a pass are in
+  // entries the clear below does not know of: the whole tables are cleared and counted again
+  bool counted = gE.counted && gS.counted;
+  if ((gE.counted || gS.counted) && !(precleared && counted)) {
+    gE.fresh = gS.fresh = true;
+    precleared = counted = false;
+  }
   if (!precleared) {
     reserve_grid(gE, mE_ub);
     reserve_grid(gS, mS_ub);
@@ -244,15 +204,18 @@ void grid_build_launch(Grid& gE, const PointRec* mapE, const int* d_mE, int mE_u
     FLOAM_LAUNCH_CHECK();
   }
   const unsigned pb = std::min(div_up(std::max(mE_ub, mS_ub), kTB), 2048u);
-  hipLaunchKernelGGL(grid_count, dim3(pb, 2), dim3(kTB), 0, st, E, S, predict);
-  FLOAM_LAUNCH_CHECK();
-  hipLaunchKernelGGL(grid_alloc, dim3(std::min(pb, 512u), 2), dim3(kTB), 0, st, E, S);
+  if (!counted) {
+    hipLaunchKernelGGL(grid_count, dim3(pb, 2), dim3(kTB), 0, st, E, S, predict);
+    FLOAM_LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(grid_alloc, dim3(std::min(pb, 512u), 2), dim3(kTB), 0, st, E, S, counted ? predict : nullptr);
   FLOAM_LAUNCH_CHECK();
   hipLaunchKernelGGL(grid_scatter, dim3(pb, 2), dim3(kTB), 0, st, E, S);
   FLOAM_LAUNCH_CHECK();
   for (Grid* g : {&gE, &gS}) {
     g->fresh = false;
     g->precleared = false;
+    g->counted = false;
     g->parity ^= 1;
   }
 }

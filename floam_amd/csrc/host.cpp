@@ -280,6 +280,10 @@ struct floam_odom {
   MapMergeScratch mms;
   bool map_merge = true;          // FLOAM_MAP_MERGE=0: the whole-map VoxelGrid of round 2 (A/B)
   bool map_force_full = false;    // FLOAM_MAP_FULL=1: the merge pipeline always takes its full-sort path (tests)
+  // FLOAM_GRID_COUNT_FUSED=1: the merge also counts its output into the next kNN grids (grid_count_job) instead of
+  // the grid build's own count launch — measured slower (r03g/r03h: mm_merge 27.6 -> 46 us, grid_scatter 6.5 -> 14 us
+  // against grid_count's 16.5 us), so off by default
+  bool grid_count_off = true;
   int map_violate_mod = 0;        // FLOAM_MM_VIOLATE=n: every n-th merge reports its keys out of order (tests)
   size_t mapE_n = 0, mapS_n = 0;   // map sizes: exact after a synchronisation, else upper bounds
   // scratch
@@ -887,8 +891,15 @@ void odom_map_update(floam_odom* o, DeviceCtx& ctx, const MapUpdatePlan& P, size
   ProfScope ps(ctx, "map_update", FLOAM_PROF_CLOUD);
   const int ubS = (int)o->mapS_n + P.ns_ub, ubE = (int)o->mapE_n + P.ne_ub;
   if (o->map_merge) {   // the new scan voxels merged into the voxel-ordered maps (mapmerge.hip)
+    // (the next grid builds' clears ran in the status gather: the merge also counts the points it writes into them)
+    GridCountDev gcount[2];
+    const bool fuse = o->gE.precleared && o->gS.precleared && !o->grid_count_off;
+    if (fuse) {
+      gcount[0] = grid_count_job(o->gE);
+      gcount[1] = grid_count_job(o->gS);
+    }
     map_merge_launch(o->vs, o->mms, P.je, P.js, P.ke, P.ks, &o->ds.p->kf_flag, (unsigned)o->issued,
-                     o->map_force_full, o->map_violate_mod, st);
+                     o->map_force_full, o->map_violate_mod, fuse ? gcount : nullptr, st);
     o->mkcur ^= 1;
   } else {
     voxel2_launch(o->vs, P.je, P.js, st, &o->ds.p->kf_flag, true);
@@ -1319,6 +1330,7 @@ floam_status floam_odom_create(const floam_lidar_params* p, double map_resolutio
     if (const char* e = std::getenv("FLOAM_MAP_MERGE")) o->map_merge = e[0] != '0';
     if (const char* e = std::getenv("FLOAM_MAP_FULL")) o->map_force_full = e[0] == '1';
     if (const char* e = std::getenv("FLOAM_MM_VIOLATE")) o->map_violate_mod = std::atoi(e);
+    if (const char* e = std::getenv("FLOAM_GRID_COUNT_FUSED")) o->grid_count_off = std::atoi(e) == 0;
     std::string l = loss ? loss : "";
     std::transform(l.begin(), l.end(), l.begin(), [](unsigned char c) { return (char)std::tolower(c); });
     o->huber = (l == "huber");   // any other string: no robust loss (Q3)
@@ -1354,6 +1366,7 @@ floam_status floam_odom_destroy(floam_odom* o) {
       for (auto& row : o->graph_exec)
         for (auto& ex : row)
           if (ex) FLOAM_HIP(hipGraphExecDestroy(ex));
+      radix_stamps_print();
       if (o->dbg_stamps.p) {   // FLOAM_DEBUG_STAMPS: the resident solve's segments in block 0 (100 MHz ticks)
         unsigned long long h[8];
         FLOAM_HIP(hipMemcpy(h, o->dbg_stamps.p, sizeof(h), hipMemcpyDeviceToHost));
@@ -1398,6 +1411,11 @@ floam_status floam_odom_init_map(floam_odom* o, const floam_cloud* edge, const f
     o->mapE.host_count = o->mapE_n; o->mapE.host_count_valid = true;
     o->mapS.host_count = o->mapS_n; o->mapS.host_count_valid = true;
     o->grid_dirty = true;
+    for (Grid* g : {&o->gE, &o->gS})
+      if (g->counted) {   // a map update counted its points into the next grids: those tables are cleared whole
+        g->counted = g->precleared = false;
+        g->fresh = true;
+      }
     for (int m = 0; m < 2; ++m) {   // a raw map (Q8): no cell keys until a map update has voxelised it
       o->mmeta[m][o->mkcur].reserve(1);
       FLOAM_HIP(hipMemsetAsync(o->mmeta[m][o->mkcur].p, 0, sizeof(MapMeta), st));

@@ -17,7 +17,8 @@
 // Launches per update (both maps at once): mm_keys (the sort set's 32-bit voxel keys + digit histograms, the
 // VoxelGrid's own key arithmetic), the four radix passes (radix.hip) — over the scan voxels only on the merge path —
 // and mm_merge (merge-path tiles: partition by a 128-ary search of the two index sequences, the tile's elements
-// merged in LDS, runs -> centroids, decoupled-lookback output positions, the new map's cell keys and verdict).
+// merged in LDS, runs -> centroids, decoupled-lookback output positions, the new map's cell keys and verdict, and
+// the kNN grid's per-point count of the new map: grid_count_point, so that the grid build skips that launch).
 // Merge comparisons run on voxel indices: the set's sort keys, and the map's stored cell keys mapped into the same
 // grid — a cropped map point may lie outside it and is saturated to the first / last cell of its row, plane or grid,
 // which keeps the order (it takes part in the order only: a cropped point adds nothing to a centroid).
@@ -25,6 +26,7 @@
 #include <climits>
 
 #include "cloud_ops.hpp"
+#include "grid.hpp"
 #include "lookback.hpp"
 #include "mapmerge.hpp"
 #include "radix.hpp"
@@ -44,26 +46,50 @@ __global__ __launch_bounds__(kTB) void mm_keys(VoxelJobDev A, VoxelJobDev B, con
                                                int* __restrict__ n_dev, int* __restrict__ ctl,
                                                const MapMeta* __restrict__ metaA, const MapMeta* __restrict__ metaB,
                                                const unsigned* __restrict__ flags, unsigned seq, int force_full) {
-  if (gate && !*gate) return;
+  // the prologue's loads are all issued before any is waited on (one round trip instead of four in a row): the gate,
+  // the bounding-box partials, the metas, the flags, the counts and — for the merge path, where element e is scan
+  // point e — this thread's first scan record and the pose (the host bound n1_ub keeps the load inside the array)
   const int job = blockIdx.y;
+  const int gv = gate ? *gate : 1;
+  const MapMeta mA = *metaA, mB = *metaB;
+  const unsigned flA = flags[0], flB = flags[1];
+  const int dA0 = *A.d_n0, dA1 = *A.d_n1, dB0 = *B.d_n0, dB1 = *B.d_n1;
+  float pv[2][kVoxMinMaxBlocks / 32];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {   // partial q = threadIdx.x + 256 h of the 384 (2 jobs x 6 components x 32 lanes)
+    const int q = threadIdx.x + kTB * h;
+    const int jb = q / 192, c = (q / 32) % 6, l = q & 31;
+#pragma unroll
+    for (int u = 0; u < kVoxMinMaxBlocks / 32; ++u)
+      pv[h][u] = q < 2 * 6 * 32 ? partials[(jb * kVoxMinMaxBlocks + l + 32 * u) * 6 + c] : 0.f;
+  }
+  const VoxelJobDev& J0 = job ? B : A;
+  const int e0 = blockIdx.x * blockDim.x + threadIdx.x;
+  PointRec sp0;
+  if (e0 < J0.n1_ub) sp0 = J0.part1[e0];
+  double pose0[7];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) pose0[k] = J0.pose[k];
+  if (!gv) return;
   __shared__ float s_mm[2][6];
   __shared__ unsigned s_hist[kRadixHistWords];
   __shared__ int s_kept;
   radix_hist_begin(s_hist);
   if (threadIdx.x == 0) s_kept = 0;
   // both maps' bounding boxes (job B's elements are packed after job A's, whose count depends on A's mode)
-  for (int q = threadIdx.x; q < 2 * 6 * 32; q += kTB) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int q = threadIdx.x + kTB * h;
+    if (q >= 2 * 6 * 32) continue;   // (wave-uniform: 384 = 6 waves)
     const int jb = q / 192, c = (q / 32) % 6, l = q & 31;
     const bool is_min = c < 3;
     float v = is_min ? FLT_MAX : -FLT_MAX;
-    for (int b = l; b < kVoxMinMaxBlocks; b += 32) {
-      const float u = partials[(jb * kVoxMinMaxBlocks + b) * 6 + c];
-      v = is_min ? fminf(v, u) : fmaxf(v, u);
-    }
+#pragma unroll
+    for (int u = 0; u < kVoxMinMaxBlocks / 32; ++u) v = is_min ? fminf(v, pv[h][u]) : fmaxf(v, pv[h][u]);
 #pragma unroll
     for (int o = 16; o > 0; o >>= 1) {
-      const float u = __shfl_xor(v, o, 64);
-      v = is_min ? fminf(v, u) : fmaxf(v, u);
+      const float w = __shfl_xor(v, o, 64);
+      v = is_min ? fminf(v, w) : fmaxf(v, w);
     }
     if (l == 0) s_mm[jb][c] = v;
   }
@@ -84,10 +110,10 @@ __global__ __launch_bounds__(kTB) void mm_keys(VoxelJobDev A, VoxelJobDev B, con
     dzB = (int)floorf(mx[2] * B.inv) - gB.min_b[2] + 1;
   }
   // the full sort if forced, the map's keys are absent or out of order, a scan point is not finite, or overflow
-  const bool fullA = force_full || !metaA->valid || metaA->violation == metaA->seq || flags[0] == seq || gA.overflow;
-  const bool fullB = force_full || !metaB->valid || metaB->violation == metaB->seq || flags[1] == seq || gB.overflow;
-  const int nA0 = min(*A.d_n0, A.n0_ub), nA1 = min(*A.d_n1, A.n1_ub);
-  const int nB0 = min(*B.d_n0, B.n0_ub), nB1 = min(*B.d_n1, B.n1_ub);
+  const bool fullA = force_full || !mA.valid || mA.violation == mA.seq || flA == seq || gA.overflow;
+  const bool fullB = force_full || !mB.valid || mB.violation == mB.seq || flB == seq || gB.overflow;
+  const int nA0 = min(dA0, A.n0_ub), nA1 = min(dA1, A.n1_ub);
+  const int nB0 = min(dB0, B.n0_ub), nB1 = min(dB1, B.n1_ub);
   const int sizeA = (fullA ? nA0 : 0) + nA1, sizeB = (fullB ? nB0 : 0) + nB1;
   if (job == 0 && blockIdx.x == 0 && threadIdx.x == 0) {
     *n_dev = sizeA + sizeB;
@@ -110,11 +136,22 @@ __global__ __launch_bounds__(kTB) void mm_keys(VoxelJobDev A, VoxelJobDev B, con
   const int n0 = job ? nB0 : nA0, n1 = job ? nB1 : nA1;
   const int start = full ? 0 : n0, count = job ? sizeB : sizeA, base = job ? sizeA : 0;
   int kept = 0;
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < count; e += gridDim.x * blockDim.x) {
+  for (int e = e0; e < count; e += gridDim.x * blockDim.x) {
     const int i = start + e;   // index into the job's [map ; scan] concatenation
     uint32_t key = 0xFFFFFFFFu;
     PointRec p;
-    if (vox_fetch(J, n0, n1, i, p)) {
+    bool in;
+    if (!full && e == e0) {   // the prefetched scan record: vox_fetch's transform and CropBox, on registers
+      float x, y, z;
+      associate_to_map(pose0, sp0.x, sp0.y, sp0.z, x, y, z);
+      p.x = x; p.y = y; p.z = z;
+      const float mnx = (float)(pose0[4] - 100), mny = (float)(pose0[5] - 100), mnz = (float)(pose0[6] - 100);
+      const float mxx = (float)(pose0[4] + 100), mxy = (float)(pose0[5] + 100), mxz = (float)(pose0[6] + 100);
+      in = !(x < mnx || y < mny || z < mnz || x > mxx || y > mxy || z > mxz);
+    } else {
+      in = vox_fetch(J, n0, n1, i, p);
+    }
+    if (in) {
       key = ((uint32_t)job << 31) | (G.overflow ? (uint32_t)i : voxel_idx(G, J.inv, p));
       ++kept;
     }
@@ -226,7 +263,8 @@ __global__ __launch_bounds__(kTB) void mm_merge(VoxelJobDev A, VoxelJobDev B, Ma
                                                 const int* __restrict__ ctl, unsigned long long* __restrict__ mstatus,
                                                 int tiles_cap, int tilesA,
                                                 const unsigned* __restrict__ radix_ctl, const int* __restrict__ gate,
-                                                unsigned seq, int violate_mod) {
+                                                unsigned seq, int violate_mod, GridCountDev GA, GridCountDev GB,
+                                                int count_grid) {
   const int job = (int)blockIdx.x < tilesA ? 0 : 1;
   const int tile = job ? (int)blockIdx.x - tilesA : (int)blockIdx.x;
   const int njb = job ? (int)gridDim.x - tilesA : tilesA;   // this job's blocks
@@ -236,10 +274,18 @@ __global__ __launch_bounds__(kTB) void mm_merge(VoxelJobDev A, VoxelJobDev B, Ma
   V.n0 = min(*V.J.d_n0, V.J.n0_ub);
   V.n1 = min(*V.J.d_n1, V.J.n1_ub);
   const int t = threadIdx.x;
+  const GridCountDev& G = job ? GB : GA;
   if (gate && !*gate) {   // no keyframe: the map, its keys and their verdict stay as they are
-    for (int i = tile * kTB + t; i < V.n0; i += njb * kTB) {
-      V.J.out[i] = V.J.part0[i];
-      V.K.out[i] = V.K.in[i];
+    for (int i0 = tile * kTB; i0 < V.n0; i0 += njb * kTB) {   // (wave-uniform trip count: the grid count)
+      const int i = i0 + t;
+      const bool valid = i < V.n0;
+      PointRec p;
+      if (valid) {
+        p = V.J.part0[i];
+        V.J.out[i] = p;
+        V.K.out[i] = V.K.in[i];
+      }
+      if (count_grid) grid_count_point(G, i, valid, p.x, p.y, p.z);
     }
     if (tile == 0 && t == 0) {
       *V.J.d_out = V.n0;
@@ -517,14 +563,27 @@ __global__ __launch_bounds__(kTB) void mm_merge(VoxelJobDev A, VoxelJobDev B, Ma
   }
   if (violate_mod > 0 && seq % (unsigned)violate_mod == 0) bad = true;   // (test knob: exercise the fallback)
   if (__syncthreads_or(bad) && t == 0) V.K.meta_out->violation = seq;
-  for (int k = t; k < nloc; k += kTB) {
-    const float4 c = s_pt[k];
-    PointRec o;
-    if (V.ovf) mv_fetch(V, __float_as_int(c.x), o);
-    else o = centroid_rec(c);
-    V.J.out[pre.a + k] = o;
-    V.K.out[pre.a + k] = s_key[k];
+  int gi[kPer];
+  bool gv[kPer];
+  float gx[kPer], gy[kPer], gz[kPer];
+#pragma unroll
+  for (int r = 0; r < kPer; ++r) {   // (nloc <= kTile: every output in one of the kPer rounds)
+    const int k = r * kTB + t;
+    gv[r] = k < nloc;
+    gi[r] = pre.a + k;
+    gx[r] = gy[r] = gz[r] = 0.f;
+    if (gv[r]) {
+      const float4 c = s_pt[k];
+      PointRec o;
+      if (V.ovf) mv_fetch(V, __float_as_int(c.x), o);
+      else o = centroid_rec(c);
+      V.J.out[pre.a + k] = o;
+      V.K.out[pre.a + k] = s_key[k];
+      gx[r] = o.x; gy[r] = o.y; gz[r] = o.z;
+    }
   }
+  // the next kNN grid's per-point step (grid_count_job) for the map's points pre.a + k, all rounds at once
+  if (count_grid) grid_count_points<kPer>(G, gi, gv, gx, gy, gz);
   if (tile == ntiles - 1 && t == 0) {
     const bool sort_failed = radix_ctl[kRadixHistWords + 4] != 0u;   // a sort lookback timed out (never expected)
     *V.J.d_out = sort_failed ? -1 : pre.a + nloc;
@@ -559,7 +618,7 @@ MergeCheck merge_check(MapMergeScratch& ms, unsigned seq) {
 
 void map_merge_launch(VoxelScratch2& vs, MapMergeScratch& ms, const VoxelJob& a, const VoxelJob& b, const MapKeys& ka,
                       const MapKeys& kb, const int* gate, unsigned seq, bool force_full, int violate_mod,
-                      hipStream_t st) {
+                      const GridCountDev* grids, hipStream_t st) {
   const VoxelJobDev A = to_dev(a, 0);
   const VoxelJobDev B = to_dev(b, a.n0_ub + a.n1_ub);
   const int nA = a.n0_ub + a.n1_ub, nB = b.n0_ub + b.n1_ub, n = std::max(nA + nB, 1);
@@ -579,7 +638,8 @@ void map_merge_launch(VoxelScratch2& vs, MapMergeScratch& ms, const VoxelJob& a,
   FLOAM_LAUNCH_CHECK();
   radix_sort_launch(vs.rs, vs.s.k0.p, vs.s.v0.p, vs.s.k1.p, vs.s.v1.p, n, st, gate, vs.overflow.p + 2);
   hipLaunchKernelGGL(mm_merge, dim3(tilesA + tilesB), dim3(kTB), 0, st, A, B, ka, kb, vs.s.k0.p, vs.s.v0.p, ms.ctl.p,
-                     ms.status.p, ms.tiles_cap, tilesA, vs.rs.ctl.p, gate, seq, violate_mod);
+                     ms.status.p, ms.tiles_cap, tilesA, vs.rs.ctl.p, gate, seq, violate_mod,
+                     grids ? grids[0] : GridCountDev{}, grids ? grids[1] : GridCountDev{}, grids ? 1 : 0);
   FLOAM_LAUNCH_CHECK();
 }
 

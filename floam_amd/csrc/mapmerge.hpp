@@ -1,6 +1,7 @@
 // Incremental map update of addPointsToMap (src/odomEstimationClass.cpp:253-294): merge the sorted new scan voxels
 // into the voxel-ordered map instead of re-sorting the whole map — see mapmerge.hip.
 #pragma once
+#include "grid.hpp"
 #include "voxel.hpp"
 
 namespace floam {
@@ -42,9 +43,10 @@ MergeCheck merge_check(MapMergeScratch& ms, unsigned seq);
 // join the sort (the full VoxelGrid of map + scan, PCL semantics incl. the overflow pass-through).  gate: as
 // voxel2_launch (0 = no keyframe: the maps, keys and metas are copied unchanged).  Test knobs: force_full: always the
 // full sort; violate_mod > 0: the merges of updates seq % violate_mod == 0 report their keys out of order (the next
-// update then takes the full sort).
+// update then takes the full sort).  grids (nullable): [corner, surf] grid_count_job of the maps' next kNN grids — the
+// merge counts the points it writes.
 void map_merge_launch(VoxelScratch2& vs, MapMergeScratch& ms, const VoxelJob& a, const VoxelJob& b, const MapKeys& ka,
                       const MapKeys& kb, const int* gate, unsigned seq, bool force_full, int violate_mod,
-                      hipStream_t st);
+                      const GridCountDev* grids, hipStream_t st);
 
 }  // namespace floam

@@ -1,6 +1,7 @@
 #pragma once
 #include "cloud_ops.hpp"
 #include "floam_common.hpp"
+#include "grid.hpp"
 #include "pose.hpp"
 #include "voxel.hpp"
 
@@ -15,15 +16,6 @@ namespace floam {
 // from which the kNN derives every fine cell's range (no fine-cell table).
 // Layout order inside a cell is not deterministic; the kNN breaks distance ties by map index, so results are.
 // Exact replacement of the 5-NN KD-tree under the reference's sqd[4] < 1 gate (knn_group).
-constexpr double kFineCell = 0.5;
-
-struct alignas(64) CoarseCell {   // 64 B, one per half cache line: a probe never straddles two lines
-  unsigned long long key;
-  int start, total;
-  int sub[8];                // points per fine sub-cell (x bit 0, y bit 1, z bit 2)
-  int pad[4];
-};
-constexpr unsigned long long kEmptyKey = ~0ull;
 
 struct Grid {
   DevBuf<float4> pts;        // {x, y, z, map index bits}, grouped by coarse cell then fine sub-cell
@@ -38,6 +30,7 @@ struct Grid {
   int parity = 0;
   bool fresh = true;         // tables (re)allocated: the next clear is a full one
   bool precleared = false;   // the next build's clear was issued in advance (grid_clear_prepare)
+  bool counted = false;      // the next build's per-point count was issued in advance (grid_count_job)
 };
 
 // The first step of a grid build — empty the table entries the previous build occupied (its slot list; the whole
@@ -73,6 +66,11 @@ __device__ __forceinline__ void grid_clear_part(const GridClearDev& J, int t0, i
 // sizes the grid for a map of up to ub points and returns its next build's clear (the build is then issued with
 // precleared = true).  Must not be called while a launch that reads the grid is still to be issued.
 GridClearDev grid_clear_prepare(Grid& g, int ub, hipStream_t st);
+
+// The next build's per-point count (grid_count_point) as a device job, for the launch that writes the map; issued
+// after grid_clear_prepare, for a map of at most its ub points.  The build then skips its count (a build that finds
+// the clear not prepared clears and counts the whole tables again).
+GridCountDev grid_count_job(Grid& g);
 
 struct OdomDev;
 // Rebuild the grids of both local maps (corner and surf) in four launches (three when precleared).  predict

@@ -17,6 +17,11 @@
 
 namespace floam {
 
+// FLOAM_RADIX_STAMPS=1 (diagnostic): per-block phase times of every pass (100 MHz ticks) and per-launch first block
+// start / last block end, printed by radix_stamps_print
+constexpr int kStampSlots = 4096;
+__device__ unsigned long long g_radix_stamps[8 + 2 * kStampSlots];
+
 namespace {
 constexpr int kTB = 256;
 constexpr int kItems = 8;
@@ -42,25 +47,18 @@ __global__ __launch_bounds__(kTB) void radix_pass(const uint32_t* __restrict__ k
                                                   uint32_t* __restrict__ kout, int* __restrict__ vout, int n,
                                                   int pass, unsigned* __restrict__ ctl,
                                                   unsigned long long* __restrict__ status,
-                                                  const int* __restrict__ gate, const int* __restrict__ n_dev) {
-  if (gate && !*gate) return;
-  const unsigned epoch = ctl[kRadixEpochWord];
-  if (n_dev) n = min(n, *n_dev);
-  __shared__ unsigned s_wcnt[kTB / 64][kRadixDigits];
-  __shared__ unsigned s_off[kRadixDigits];
-  __shared__ unsigned s_wsum[kTB / 64];
-  __shared__ int s_tile;
+                                                  const int* __restrict__ gate, const int* __restrict__ n_dev,
+                                                  int stamps) {
+  const unsigned long long ts0 = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  // every load of the prologue is issued at once (one memory round trip, not three in a row): the gate, the epoch,
+  // the device count, this digit's histogram count and the tile's elements up to the host bound n (allocated; the
+  // ones past the device count are dropped below)
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int shift = 8 * pass;
-  // the tile is the block index: workgroups are dispatched in index order and a launch has at most a few hundred
-  // tiles, so a tile only waits on tiles that are running or done (no ticket round trip)
-  if (t == 0) s_tile = (int)blockIdx.x;
-  const unsigned h = ctl[pass * kRadixDigits + t];   // digit t's histogram count, loaded with the keys
-#pragma unroll
-  for (int k = 0; k < kTB / 64; ++k) s_wcnt[k][t] = 0u;
-  __syncthreads();
-  const int tile = s_tile;
-  if (tile * kTile >= n) return;   // beyond the elements (block-uniform); nobody waits on a later tile
+  const int tile = (int)blockIdx.x;
+  const int gv = gate ? *gate : 1;
+  const unsigned epoch = ctl[kRadixEpochWord];
+  const int nd = n_dev ? *n_dev : n;
+  const unsigned h = ctl[pass * kRadixDigits + t];   // digit t's histogram count
   const int base = tile * kTile + w * 64 * kItems;
   uint32_t key[kItems];
   int val[kItems];
@@ -70,6 +68,18 @@ __global__ __launch_bounds__(kTB) void radix_pass(const uint32_t* __restrict__ k
     key[r] = i < n ? kin[i] : 0u;
     val[r] = i < n ? vin[i] : 0;
   }
+  if (!gv) return;
+  n = min(n, nd);
+  // the tile is the block index: workgroups are dispatched in index order and a launch has at most a few hundred
+  // tiles, so a tile only waits on tiles that are running or done (no ticket round trip)
+  if (tile * kTile >= n) return;   // beyond the elements (block-uniform); nobody waits on a later tile
+  __shared__ unsigned s_wcnt[kTB / 64][kRadixDigits];
+  __shared__ unsigned s_off[kRadixDigits];
+  __shared__ unsigned s_wsum[kTB / 64];
+  const int shift = 8 * pass;
+#pragma unroll
+  for (int k = 0; k < kTB / 64; ++k) s_wcnt[k][t] = 0u;
+  __syncthreads();
   // 2. stable rank within (wave, digit)
   unsigned rank[kItems];
   const unsigned long long lt = (1ull << lane) - 1ull;
@@ -83,6 +93,7 @@ __global__ __launch_bounds__(kTB) void radix_pass(const uint32_t* __restrict__ k
     if (valid && lane == 63 - __clzll((long long)peers)) s_wcnt[w][d] = before + (unsigned)__popcll(peers);
   }
   __syncthreads();
+  const unsigned long long ts1 = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
   // 3. thread t = digit t: wave offsets, tile count, bucket start, lookback over the earlier tiles
   unsigned c[kTB / 64], cnt = 0;
 #pragma unroll
@@ -149,6 +160,7 @@ __global__ __launch_bounds__(kTB) void radix_pass(const uint32_t* __restrict__ k
     if (k < w) wb += s_wsum[k];
   s_off[t] = wb + incl - h + prefix;
   __syncthreads();
+  const unsigned long long ts2 = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
   // 4. scatter
 #pragma unroll
   for (int r = 0; r < kItems; ++r) {
@@ -159,8 +171,54 @@ __global__ __launch_bounds__(kTB) void radix_pass(const uint32_t* __restrict__ k
       vout[dst] = val[r];
     }
   }
+  if (stamps) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) {
+      const unsigned long long ts3 = __builtin_amdgcn_s_memrealtime();
+      atomicAdd(&g_radix_stamps[0], ts1 - ts0);
+      atomicAdd(&g_radix_stamps[1], ts2 - ts1);
+      atomicAdd(&g_radix_stamps[2], ts3 - ts2);
+      atomicAdd(&g_radix_stamps[3], 1ull);
+      const int slot = stamps - 1;   // the host's launch counter
+      atomicMin(&g_radix_stamps[8 + 2 * slot], ts0);
+      atomicMax(&g_radix_stamps[8 + 2 * slot + 1], ts3);
+    }
+  }
 }
+
 }  // namespace
+
+static int stamps_on() {
+  static unsigned launches = 0;
+  static const int on = std::getenv("FLOAM_RADIX_STAMPS") ? 1 : 0;
+  static bool init = false;
+  if (on && !init) {
+    init = true;
+    static unsigned long long h[8 + 2 * kStampSlots];
+    for (int k = 0; k < 8 + 2 * kStampSlots; ++k) h[k] = (k >= 8 && (k & 1) == 0) ? ~0ull : 0ull;
+    FLOAM_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_radix_stamps), h, sizeof(h)));
+  }
+  return on ? (int)(launches++ % (unsigned)kStampSlots) + 1 : 0;   // per launch: its slot + 1
+}
+
+void radix_stamps_print() {
+  if (!std::getenv("FLOAM_RADIX_STAMPS")) return;
+  static unsigned long long h[8 + 2 * kStampSlots];
+  FLOAM_HIP(hipDeviceSynchronize());
+  FLOAM_HIP(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_radix_stamps), sizeof(h)));
+  const double nb = h[3] ? (double)h[3] : 1.0;
+  double span = 0.0;
+  int nl = 0;
+  for (int k = 0; k < kStampSlots; ++k)
+    if (h[8 + 2 * k + 1] != 0ull) {
+      span += (double)(h[8 + 2 * k + 1] - h[8 + 2 * k]);
+      ++nl;
+    }
+  std::fprintf(stderr, "[radix stamps] %llu blocks: load + rank %.2f us, lookback %.2f us, scatter + drain %.2f us per "
+               "block; %d launches: first block start -> last block end %.2f us\n", h[3], h[0] / nb / 100.0,
+               h[1] / nb / 100.0, h[2] / nb / 100.0, nl, nl ? span / nl / 100.0 : 0.0);
+}
 
 void RadixScratch::reserve(int n, hipStream_t st) {
   if (!ctl.p) {
@@ -184,7 +242,7 @@ void radix_pass_launch(RadixScratch& sc, const uint32_t* kin, const int* vin, ui
   sc.reserve(n, st);
   const int tiles = (int)div_up((unsigned)n, (unsigned)kTile);
   hipLaunchKernelGGL(radix_pass, dim3(tiles), dim3(kTB), 0, st, kin, vin, kout, vout, n, pass, sc.ctl.p,
-                     sc.status.p + (size_t)pass * sc.tiles_cap * kRadixDigits, nullptr, nullptr);
+                     sc.status.p + (size_t)pass * sc.tiles_cap * kRadixDigits, nullptr, nullptr, stamps_on());
   FLOAM_LAUNCH_CHECK();
 }
 
@@ -197,7 +255,7 @@ void radix_sort_launch(RadixScratch& sc, uint32_t* k0, int* v0, uint32_t* k1, in
     const bool even = (p & 1) == 0;
     hipLaunchKernelGGL(radix_pass, dim3(tiles), dim3(kTB), 0, st, even ? k0 : k1, even ? v0 : v1, even ? k1 : k0,
                        even ? v1 : v0, n, p, sc.ctl.p, sc.status.p + (size_t)p * sc.tiles_cap * kRadixDigits,
-                       gate, n_dev);
+                       gate, n_dev, stamps_on());
     FLOAM_LAUNCH_CHECK();
   }
 }

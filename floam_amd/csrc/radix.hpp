@@ -61,6 +61,9 @@ void radix_sort_launch(RadixScratch& sc, uint32_t* k0, int* v0, uint32_t* k1, in
 
 // One digit pass (pass p sorts by bits [8p, 8p + 8)) of the same sort, for keys whose high digits are known to be
 // equal (e.g. the feature extraction's ring keys: one pass for <= 255 rings)
+// FLOAM_RADIX_STAMPS=1: print the passes' in-kernel phase times (diagnostic; synchronises the device)
+void radix_stamps_print();
+
 void radix_pass_launch(RadixScratch& sc, const uint32_t* kin, const int* vin, uint32_t* kout, int* vout, int n,
                        int pass, hipStream_t st);
 

@@ -43,24 +43,33 @@ __global__ __launch_bounds__(kTB) void vox_keys(VoxelJobDev A, VoxelJobDev B, co
                                                 int ntiles, unsigned* __restrict__ ticket,
                                                 unsigned* __restrict__ radix_ctl, const int* __restrict__ gate,
                                                 int* __restrict__ n_dev) {
-  if (gate && !*gate) return;
+  // the prologue's loads are issued together (one round trip instead of three in a row): the gate, the partials,
+  // the counts and this thread's first record of the first part (inside the array by the host bound n0_ub)
   const int job = blockIdx.y;
   const VoxelJobDev& J = job == 0 ? A : B;
+  const int gv = gate ? *gate : 1;
+  const int dA0 = *A.d_n0, dA1 = A.d_n1 ? *A.d_n1 : 0, dB0 = *B.d_n0, dB1 = B.d_n1 ? *B.d_n1 : 0;
+  const int c = threadIdx.x >> 5, l = threadIdx.x & 31;   // component c = t / 32 (two per wave), 32 lanes
+  float pv[kMinMaxBlocks / 32];
+#pragma unroll
+  for (int u = 0; u < kMinMaxBlocks / 32; ++u)
+    pv[u] = threadIdx.x < 6 * 32 ? partials[(job * kMinMaxBlocks + l + 32 * u) * 6 + c] : 0.f;
+  const int i0 = blockIdx.x * blockDim.x + threadIdx.x;
+  PointRec p0;
+  if (i0 < J.n0_ub) p0 = J.part0[i0];
+  if (!gv) return;
   __shared__ float s_mm[6];
   __shared__ unsigned s_hist[kRadixHistWords];
   radix_hist_begin(s_hist);
-  if (threadIdx.x < 6 * 32) {   // component c = t / 32 (two per wave), 32 lanes over the partials, then a 32-lane min/max
-    const int c = threadIdx.x >> 5, l = threadIdx.x & 31;
+  if (threadIdx.x < 6 * 32) {   // the partials' min / max per component: 32 lanes, then a 32-lane reduction
     const bool is_min = c < 3;
     float v = is_min ? FLT_MAX : -FLT_MAX;
-    for (int b = l; b < kMinMaxBlocks; b += 32) {
-      const float u = partials[(job * kMinMaxBlocks + b) * 6 + c];
-      v = is_min ? fminf(v, u) : fmaxf(v, u);
-    }
+#pragma unroll
+    for (int u = 0; u < kMinMaxBlocks / 32; ++u) v = is_min ? fminf(v, pv[u]) : fmaxf(v, pv[u]);
 #pragma unroll
     for (int o = 16; o > 0; o >>= 1) {
-      const float u = __shfl_xor(v, o, 64);
-      v = is_min ? fminf(v, u) : fmaxf(v, u);
+      const float w = __shfl_xor(v, o, 64);
+      v = is_min ? fminf(v, w) : fmaxf(v, w);
     }
     if (l == 0) s_mm[c] = v;
   }
@@ -73,15 +82,22 @@ __global__ __launch_bounds__(kTB) void vox_keys(VoxelJobDev A, VoxelJobDev B, co
   const VoxelGeom g = voxel_geom(mn, mx, J.inv);
   if (blockIdx.x == 0 && threadIdx.x == 0) overflow[job] = g.overflow ? 1 : 0;
   // the elements the device holds, packed: cloud A at [0, nA), cloud B at [nA, nA + nB) (no upper-bound padding)
-  const int nA0 = min(*A.d_n0, A.n0_ub), nA1 = A.d_n1 ? min(*A.d_n1, A.n1_ub) : 0;
-  const int nB0 = min(*B.d_n0, B.n0_ub), nB1 = B.d_n1 ? min(*B.d_n1, B.n1_ub) : 0;
+  const int nA0 = min(dA0, A.n0_ub), nA1 = A.d_n1 ? min(dA1, A.n1_ub) : 0;
+  const int nB0 = min(dB0, B.n0_ub), nB1 = B.d_n1 ? min(dB1, B.n1_ub) : 0;
   const int n0 = job ? nB0 : nA0, n1 = job ? nB1 : nA1;
   const int base = job ? nA0 + nA1 : 0;
   if (job == 0 && blockIdx.x == 0 && threadIdx.x == 0) *n_dev = nA0 + nA1 + nB0 + nB1;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n0 + n1; i += gridDim.x * blockDim.x) {
+  for (int i = i0; i < n0 + n1; i += gridDim.x * blockDim.x) {
     uint32_t key = 0xFFFFFFFFu;
     PointRec p;
-    if (vox_fetch(J, n0, n1, i, p)) {
+    bool in;
+    if (i == i0 && i < n0 && !J.pose) {   // the prefetched record (no transform, no crop: vox_fetch's first part)
+      p = p0;
+      in = true;
+    } else {
+      in = vox_fetch(J, n0, n1, i, p);
+    }
+    if (in) {
       uint32_t idx;
       if (g.overflow) {
         idx = (uint32_t)i;   // output = input unchanged (Q9): identity order, one "voxel" per point
@@ -102,30 +118,55 @@ __global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B,
                                                    const int* __restrict__ vals, const int* __restrict__ overflow,
                                                    const int* __restrict__ n_dev, unsigned long long* __restrict__ status,
                                                    unsigned* __restrict__ ticket, const unsigned* __restrict__ radix_ctl,
-                                                   const int* __restrict__ gate) {
-  if (gate && !*gate) {   // gated off (no keyframe): the output is the unchanged first part (the map)
+                                                   const int* __restrict__ gate, int n_cap) {
+  // the prologue's loads are issued together (one round trip instead of four in a row): the gate, the device
+  // counts, and the tile's keys and values up to the host bound n_cap (allocated; entries past the device count are
+  // masked below)
+  const int gv = gate ? *gate : 1;
+  const int tile = (int)blockIdx.x;   // (workgroups dispatch in index order: a tile only waits on earlier tiles)
+  const int t0 = tile * kTile;
+  const int total_d = *n_dev;   // packed elements (vox_keys)
+  const int nA0 = *A.d_n0, nA1 = A.d_n1 ? *A.d_n1 : 0, nB0 = *B.d_n0, nB1 = B.d_n1 ? *B.d_n1 : 0;
+  const int ovf[2] = {overflow[0], overflow[1]};
+  // s_key[k] = key of element t0 - 1 + k, k in [0, kTile + 1]
+  __shared__ uint32_t s_key[kTile + 2];
+  uint32_t kr[(kTile + 2 + kTB - 1) / kTB];
+#pragma unroll
+  for (int r = 0; r < (kTile + 2 + kTB - 1) / kTB; ++r) {
+    const int k = r * kTB + threadIdx.x;
+    const int i = t0 - 1 + k;
+    kr[r] = (k <= kTile + 1 && i >= 0 && i < n_cap) ? keys[i] : 0xFFFFFFFFu;
+  }
+  const int4* __restrict__ vals4 = reinterpret_cast<const int4*>(vals);
+  const int k0 = threadIdx.x * kPerThread;
+  int v[kPerThread];
+  if (t0 + k0 + kPerThread <= n_cap) {
+    const int4 vv = vals4[(t0 + k0) / kPerThread];
+    v[0] = vv.x; v[1] = vv.y; v[2] = vv.z; v[3] = vv.w;
+  } else {
+#pragma unroll
+    for (int u = 0; u < kPerThread; ++u) v[u] = t0 + k0 + u < n_cap ? vals[t0 + k0 + u] : 0;
+  }
+  if (!gv) {   // gated off (no keyframe): the output is the unchanged first part (the map)
     for (int job = 0; job < 2; ++job) {
       const VoxelJobDev& J = job == 0 ? A : B;
-      const int n0 = *J.d_n0;
+      const int n0 = job ? nB0 : nA0;
       for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n0; i += gridDim.x * blockDim.x) J.out[i] = J.part0[i];
       if (blockIdx.x == 0 && threadIdx.x == 0) *J.d_out = n0;
     }
     return;
   }
-  // the tile is the block index (workgroups dispatch in index order: a tile only waits on running or finished tiles)
-  const int tile = (int)blockIdx.x;
-  const int total = *n_dev;   // packed elements (vox_keys)
+  const int total = total_d;
   const int ntiles = (total + kTile - 1) / kTile;
   if (tile >= ntiles) {   // beyond the device's elements (the grid is sized by the host's upper bounds)
     if (tile == 0 && threadIdx.x == 0) { *A.d_out = 0; *B.d_out = 0; }   // no elements at all
     return;
   }
-  const int t0 = tile * kTile;
-  // s_key[k] = key of element t0 - 1 + k, k in [0, kTile + 1]
-  __shared__ uint32_t s_key[kTile + 2];
-  for (int k = threadIdx.x; k <= kTile + 1; k += blockDim.x) {
+#pragma unroll
+  for (int r = 0; r < (kTile + 2 + kTB - 1) / kTB; ++r) {
+    const int k = r * kTB + threadIdx.x;
     const int i = t0 - 1 + k;
-    s_key[k] = (i >= 0 && i < total) ? keys[i] : 0xFFFFFFFFu;
+    if (k <= kTile + 1) s_key[k] = i < total ? kr[r] : 0xFFFFFFFFu;
   }
   __syncthreads();
   // run tails of the tile as a bitmask: bit k set if element t0 + k is the last of its run
@@ -145,18 +186,7 @@ __global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B,
   // gather every element's point (x, y, z, intensity) of the tile into LDS: one parallel round trip, issued
   // before the lookback wait so the two latencies overlap; the runs are then summed from LDS
   __shared__ float4 s_pt[kTile];
-  const int nA0 = *A.d_n0, nA1 = A.d_n1 ? *A.d_n1 : 0, nB0 = *B.d_n0, nB1 = B.d_n1 ? *B.d_n1 : 0;
-  const int4* __restrict__ vals4 = reinterpret_cast<const int4*>(vals);
   {
-    const int k0 = threadIdx.x * kPerThread;
-    int v[kPerThread];
-    if (t0 + k0 + kPerThread <= total) {
-      const int4 vv = vals4[(t0 + k0) / kPerThread];
-      v[0] = vv.x; v[1] = vv.y; v[2] = vv.z; v[3] = vv.w;
-    } else {
-#pragma unroll
-      for (int u = 0; u < kPerThread; ++u) v[u] = t0 + k0 + u < total ? vals[t0 + k0 + u] : 0;
-    }
 #pragma unroll
     for (int u = 0; u < kPerThread; ++u) {
       const uint32_t key = s_key[k0 + u + 1];
@@ -212,7 +242,6 @@ __global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B,
     return;
   }
   int pos[2] = {pre.a + wb[0] + inc[0] - cnt[0], pre.b + wb[1] + inc[1] - cnt[1]};
-  const int ovf[2] = {overflow[0], overflow[1]};
   // the run that crosses the tile end (at most one): its head's partial sums, finished cooperatively below
   __shared__ float s_cross[4];
   __shared__ int s_cross_pos, s_cross_head, s_cross_job;
@@ -228,7 +257,7 @@ __global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B,
     const VoxelJobDev& J = job == 0 ? A : B;
     if (ovf[job]) {   // input returned unchanged: the whole record
       PointRec o;
-      vox_fetch(J, job ? nB0 : nA0, job ? nB1 : nA1, vals[i], o);
+      vox_fetch(J, job ? nB0 : nA0, job ? nB1 : nA1, v[u], o);
       J.out[pos[job]++] = o;
       continue;
     }
@@ -356,7 +385,7 @@ void voxel2_launch(VoxelScratch2& sc, const VoxelJob& a, const VoxelJob& b, hipS
   // sorted pairs in k0 / v0; the passes and the compaction work on the packed device count
   radix_sort_launch(sc.rs, sc.s.k0.p, sc.s.v0.p, sc.s.k1.p, sc.s.v1.p, n, st, gate, sc.overflow.p + 2);
   hipLaunchKernelGGL(vox_compact, dim3(ntiles), dim3(kTB), 0, st, A, B, sc.s.k0.p, sc.s.v0.p, sc.overflow.p,
-                     sc.overflow.p + 2, sc.status.p, sc.ticket.p, sc.rs.ctl.p, gate);
+                     sc.overflow.p + 2, sc.status.p, sc.ticket.p, sc.rs.ctl.p, gate, n);
   FLOAM_LAUNCH_CHECK();
 }
 

@@ -11,6 +11,7 @@ timeout -k 10 400 python bench.py "$@" > $OUT/bench.json 2> $OUT/bench.err || { 
 cut -c1-400 $OUT/bench.json
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_trace -o run -- \
     python3 bench.py --cpu-baseline-seconds 0 --no-secondary "$@" > $OUT/prof_trace.log 2>&1 || { tail -30 $OUT/prof_trace.log; exit 1; }
+[ -n "$PROF_TRACE_ONLY" ] && { echo done; exit 0; }
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $OUT/prof_fetch -o run -- \
     python3 bench.py --cpu-baseline-seconds 0 --no-roofline --no-secondary "$@" > $OUT/prof_fetch.log 2>&1 || { tail -30 $OUT/prof_fetch.log; exit 1; }
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $OUT/prof_write -o run -- \
