@@ -81,7 +81,11 @@ def main():
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--config", default=None, help="c1..c5 (default: c3 at N = 1, c4 for the sharded N > 1 run)")
-    ap.add_argument("--mode", choices=["shard", "replica"], default=None, help="N > 1 only (default shard)")
+    ap.add_argument("--mode", choices=["shard", "replica"], default=None,
+                    help="N > 1: shard (default) or replica; N = 1: shard runs the sharded solve through a one-rank "
+                         "RCCL communicator (the per-evaluation all-reduce measured on one GPU)")
+    ap.add_argument("--oracle-scans", type=int, default=12,
+                    help="N > 1: scans of the sequence the oracle replays for pose_vs_oracle (untimed)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
@@ -98,7 +102,7 @@ def main():
     if world > 1:
         import torch.distributed as dist   # control plane only (barrier, id broadcast, max-time); data: RCCL
         dist.init_process_group(backend="gloo")
-    mode = (args.mode or "shard") if world > 1 else "single"
+    mode = (args.mode or "shard") if world > 1 else ("shard" if args.mode == "shard" else "single")
     cfg = args.config or ("c4" if mode == "shard" else "c3")
 
     import floam_amd
@@ -142,7 +146,8 @@ def main():
     uid = None
     if mode == "shard":
         uid = [(comm_unique_id(), comm_unique_id()) if rank == 0 else None]   # timed run, byte-count replay
-        dist.broadcast_object_list(uid, src=0)
+        if dist is not None:
+            dist.broadcast_object_list(uid, src=0)
     n_pipelines = 0
 
     def make_pipeline(loss=LOSS, sharded=True):
@@ -328,7 +333,22 @@ def main():
 
     cpu = None
     pose_err = None
-    if rank == 0 and args.cpu_baseline_seconds > 0:
+    if rank == 0 and world > 1 and args.oracle_scans > 0:
+        # N > 1: the poses of the sharded (or replicated) run against the oracle over the first scans of the same
+        # sequence (untimed; the CPU baseline itself is an N = 1 figure)
+        oracle.reset_process_statics()
+        ref = oracle.Odometry(R, SCAN_PERIOD, MIN_DIS, MAX_DIS, MAP_RES, LOSS, stable_voxel=True)
+        ref.init_map(mapE, mapS)
+        errs = []
+        for k in range(min(n_scans, args.oracle_scans)):
+            e, s = oracle_fe(raws[k], R)
+            ref.update_selector(e, s, True)
+            qr, tr = ref.pose()
+            qg, tg = poses[k]
+            errs.append((float(np.linalg.norm(tr - tg)), 2 * math.acos(min(1.0, abs(float(np.dot(qr, qg)))))))
+        pose_err = {"scans_compared": len(errs), "max_dt_m": max(e[0] for e in errs),
+                    "max_drot_rad": max(e[1] for e in errs)}
+    elif rank == 0 and args.cpu_baseline_seconds > 0:
         # the reference path restated (oracle), single-threaded, same scans from scan 1 and the same prefilled
         # map; warm-up scans (optimization_count ramp) untimed, then steady-state scans for ~N seconds.
         oracle.reset_process_statics()

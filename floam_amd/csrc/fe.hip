@@ -3,9 +3,13 @@
 // Kernels (one scan, P points, R rings):
 //   fe_keys     grid over P     range filter + ring key + per-ring histogram + the radix digit histograms
 //   radix_pass  grid over P     stable bucketing by ring: ONE digit pass of the onesweep radix sort (radix.hip) for
-//                               R <= 255 rings (two for more), O(P); the ring-ordered input indices
-//   fe_sector   one WG / sector curvature stencil, LDS bitonic sort, greedy edge pick, surf compaction
-//   fe_output   one WG / sector gather the 32-B records of edges / surfs to their ring-major, sector-major slots
+//                               R <= 255 rings, O(P), which stages the scan ring-major as it goes: every point's
+//                               coordinates (16 B) and record (32 B) written once to its ring-major slot (more rings:
+//                               two key-only passes, then fe_stage gathers by the ring-ordered indices)
+//   fe_sector   one WG / sector curvature stencil over the contiguous ring-major coordinates, LDS bitonic sort,
+//                               greedy edge pick, surf compaction
+//   fe_output   one WG / sector copy the 32-B ring-major records of edges / surfs to their sector-major slots; the
+//                               last block to finish advances the output counts (the commit)
 // Arithmetic follows the reference bit for bit: float stencil sums in source order, double squares, no FMA
 // contraction (built with -ffp-contract=off).  Sorting is by (value, ring index), which equals the reference's
 // unstable std::sort whenever a sector has no tied curvature values (SURVEY.md §7 "Hard parts").
@@ -31,13 +35,22 @@ __device__ __forceinline__ PointRec make_out(const PointRec& p) {
 
 // RingExtractionVelodyne (src/laserProcessingClass.cpp:11-22): float x*x+y*y, float sqrt, double compare.  Keys for
 // the stable bucketing sort: the ring, or 0xFFFF for a dropped point (sorted after every ring); values: the index.
+// ONE_DIGIT (R <= 255 rings, one bucketing pass): the per-ring counts ARE the pass's digit histogram (a dropped
+// point's low digit 0xFF is no ring), so one 256-bin LDS histogram serves both; otherwise the ring histogram and
+// the four digit histograms separately.
+template <bool ONE_DIGIT>
 __global__ void fe_keys(const PointRec* __restrict__ in, int n, int num_lines, double min_d, double max_d,
                         uint32_t* __restrict__ keys, int* __restrict__ vals, int* __restrict__ ring_count,
                         int* __restrict__ status, unsigned* __restrict__ radix_ctl) {
   extern __shared__ int hist[];
-  __shared__ unsigned s_rhist[kRadixHistWords];
-  for (int r = threadIdx.x; r < num_lines; r += blockDim.x) hist[r] = 0;
-  radix_hist_begin(s_rhist);
+  __shared__ unsigned s_rhist[ONE_DIGIT ? kRadixDigits : kRadixHistWords];
+  if (ONE_DIGIT) {
+    for (int k = threadIdx.x; k < kRadixDigits; k += blockDim.x) s_rhist[k] = 0u;
+    __syncthreads();
+  } else {
+    for (int r = threadIdx.x; r < num_lines; r += blockDim.x) hist[r] = 0;
+    radix_hist_begin(s_rhist);
+  }
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const float2 xy = *reinterpret_cast<const float2*>(&in[i].x);
     const uint16_t ring = in[i].ring;
@@ -50,14 +63,29 @@ __global__ void fe_keys(const PointRec* __restrict__ in, int n, int num_lines, d
     }
     const uint32_t key = keep ? ring : 0xFFFFu;
     keys[i] = key;
-    vals[i] = i;
-    radix_hist_add(s_rhist, key);
-    if (keep) atomicAdd(&hist[ring], 1);
+    if (ONE_DIGIT) {
+      atomicAdd(&s_rhist[key & 255u], 1u);
+    } else {
+      vals[i] = i;
+      radix_hist_add(s_rhist, key);
+      if (keep) atomicAdd(&hist[ring], 1);
+    }
   }
-  radix_hist_end(s_rhist, radix_ctl);
-  __syncthreads();
-  for (int r = threadIdx.x; r < num_lines; r += blockDim.x)
-    if (hist[r]) atomicAdd(&ring_count[r], hist[r]);
+  if (ONE_DIGIT) {
+    __syncthreads();
+    for (int k = threadIdx.x; k < kRadixDigits; k += blockDim.x) {
+      const unsigned v = s_rhist[k];
+      if (v) {
+        atomicAdd(&radix_ctl[k], v);   // pass 0's digit histogram
+        if (k < num_lines) atomicAdd(&ring_count[k], (int)v);
+      }
+    }
+  } else {
+    radix_hist_end(s_rhist, radix_ctl);
+    __syncthreads();
+    for (int r = threadIdx.x; r < num_lines; r += blockDim.x)
+      if (hist[r]) atomicAdd(&ring_count[r], hist[r]);
+  }
 }
 
 __device__ __forceinline__ int block_exclusive_scan_1024(int v, int* smem /* >= 32 ints */, int* total) {
@@ -88,10 +116,18 @@ __device__ __forceinline__ int block_exclusive_scan_1024(int v, int* smem /* >= 
   return excl;
 }
 
-__device__ __forceinline__ int ring_offset(const int* ring_count, int r) {
-  int off = 0;
-  for (int k = 0; k < r; ++k) off += ring_count[k];
-  return off;
+// points in rings [0, r): the first wave loads the counts together (one round trip, not one per ring) and sums
+// them in a fixed order; called by every thread, the result in every thread (one block barrier)
+__device__ __forceinline__ int ring_offset(const int* ring_count, int r, int* s_red) {
+  if (threadIdx.x < 64) {
+    int v = 0;
+    for (int k = threadIdx.x; k < r; k += 64) v += ring_count[k];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (threadIdx.x == 0) *s_red = v;
+  }
+  __syncthreads();
+  return *s_red;
 }
 
 __device__ __forceinline__ void sector_range(int n_r, int s, int& a, int& b) {
@@ -106,8 +142,7 @@ __device__ __forceinline__ void sector_range(int n_r, int s, int& a, int& b) {
 // picks up the (rare) longer sectors, so the common case keeps several workgroups per CU.
 template <int MINSEC, int MAXSEC, bool LAST>
 __global__ __launch_bounds__(kSectorThreads) void fe_sector(const int* __restrict__ ring_count,
-                                                            const PointRec* __restrict__ in,
-                                                            const int* __restrict__ ring_idx,
+                                                            const float4* __restrict__ ring_xyz,
                                                             int* __restrict__ sec_edge_cnt, int* __restrict__ sec_edge_pos,
                                                             int* __restrict__ sec_surf_cnt, int* __restrict__ surf_pos,
                                                             int* __restrict__ status) {
@@ -140,13 +175,11 @@ __global__ __launch_bounds__(kSectorThreads) void fe_sector(const int* __restric
     }
     return;
   }
-  if (threadIdx.x == 0) s_off = ring_offset(ring_count, r);
-  __syncthreads();
-  const int off = s_off;
+  const int off = ring_offset(ring_count, r, &s_off);
   // stage ring points [a, b + 10) (= ids a..b+9: stencils of entries a..b-1 and all suppression neighbours)
   const int npts = m + 10;
-  for (int k = threadIdx.x; k < npts; k += blockDim.x) {   // gathered from the input by the ring-ordered index
-    const float4 p = *reinterpret_cast<const float4*>(&in[ring_idx[off + a + k]].x);
+  for (int k = threadIdx.x; k < npts; k += blockDim.x) {   // contiguous ring-major coordinates
+    const float4 p = ring_xyz[off + a + k];
     s_x[k] = p.x; s_y[k] = p.y; s_z[k] = p.z;
     s_picked[k] = 0;
   }
@@ -173,9 +206,12 @@ __global__ __launch_bounds__(kSectorThreads) void fe_sector(const int* __restric
     }
   }
   __syncthreads();
-  // bitonic sort ascending by (key, id)
+  // bitonic sort ascending by (key, id).  A stage with stride <= 64 pairs positions inside one 128-entry chunk, and
+  // every chunk belongs to one wave (thread t's pairs lie in chunk t / 64 and t / 64 + 4, ...): those stages need
+  // only the wave's own LDS ordering; block barriers surround the stages with longer strides
   for (int size = 2; size <= P2; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      if (stride >= 128) __syncthreads();
       for (int t = threadIdx.x; t < (P2 >> 1); t += blockDim.x) {
         const int lo = 2 * t - (t & (stride - 1));
         const int hi = lo + stride;
@@ -188,39 +224,75 @@ __global__ __launch_bounds__(kSectorThreads) void fe_sector(const int* __restric
           s_id[lo] = ib; s_id[hi] = ia;
         }
       }
-      __syncthreads();
+      if (stride >= 128) {   // (its pairs crossed chunks: the next stage's chunks were written by other waves)
+        __syncthreads();
+      } else {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
     }
   }
-  // greedy edge pick (src/laserProcessingClass.cpp:129-170), one lane, LDS only
-  if (threadIdx.x == 0) {
+  __syncthreads();
+  // greedy edge pick (src/laserProcessingClass.cpp:129-170) by wave 0: the candidates in descending order, 64 at a
+  // time (lane order = the reference's order).  Per chunk every lane reads whether its point was picked by an earlier
+  // chunk; then, pick by pick, the first unsuppressed lane is the next candidate the reference examines (the ones
+  // before it are skipped as picked): its curvature ends the loop at <= 0.1, otherwise it is picked, lanes 1..10
+  // evaluate its +-5 neighbour gaps together (the same float differences and double squares as the reference), and
+  // its picked run is marked in LDS and in the chunk's suppression mask.  One step per pick, not per candidate.
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
     int picked_num = 0, nedge = 0;
-    for (int i = m - 1; i >= 0; --i) {
-      const int ind = s_id[i] + 5;                      // local point index
-      if (s_picked[ind]) continue;
-      if (__longlong_as_double((long long)s_key[i]) <= 0.1) break;
-      ++picked_num;
-      s_picked[ind] = 1;
-      if (picked_num <= kMaxEdgesPerSector) {
-        s_edges[nedge++] = ind;
-      } else {
-        break;
+    bool stop = false;
+    for (int c0 = m - 1; c0 >= 0 && !stop; c0 -= 64) {   // (wave-uniform)
+      const int i = c0 - lane;
+      const bool valid = i >= 0;
+      int ind = 0;
+      double key = 0.0;
+      if (valid) {
+        ind = s_id[i] + 5;   // local point index
+        key = __longlong_as_double((long long)s_key[i]);
       }
-      for (int k = 1; k <= 5; ++k) {
-        const double dX = s_x[ind + k] - s_x[ind + k - 1];
-        const double dY = s_y[ind + k] - s_y[ind + k - 1];
-        const double dZ = s_z[ind + k] - s_z[ind + k - 1];
-        if (dX * dX + dY * dY + dZ * dZ > 0.05) break;
-        s_picked[ind + k] = 1;
+      bool supp = !valid || s_picked[ind];
+      unsigned long long pending = __ballot(valid);
+      for (;;) {
+        const unsigned long long cand = __ballot(!supp) & pending;
+        if (!cand) break;   // the rest of the chunk was picked: the next chunk
+        const int l = __ffsll((long long)cand) - 1;
+        const double kl = __shfl(key, l, 64);
+        const int il = __shfl(ind, l, 64);
+        if (kl <= 0.1) { stop = true; break; }
+        ++picked_num;
+        if (picked_num > 20) {   // picked, not kept, and the loop ends
+          if (lane == 0) s_picked[il] = 1;
+          stop = true;
+          break;
+        }
+        if (lane == 0) s_edges[nedge] = il;
+        ++nedge;
+        // neighbour gaps: lane k (1..5) between il + k and il + k - 1, lane 5 + k between il - k and il - k + 1
+        bool gap = false;
+        if (lane >= 1 && lane <= 10) {
+          const int k = lane <= 5 ? lane : -(lane - 5);
+          const int q0 = il + k, q1 = k > 0 ? il + k - 1 : il + k + 1;
+          const double dX = s_x[q0] - s_x[q1];
+          const double dY = s_y[q0] - s_y[q1];
+          const double dZ = s_z[q0] - s_z[q1];
+          gap = dX * dX + dY * dY + dZ * dZ > 0.05;
+        }
+        const unsigned long long g = __ballot(gap);
+        const unsigned long long gr = (g >> 1) & 0x1Full, gl = (g >> 6) & 0x1Full;
+        const int rr = gr ? __ffsll((long long)gr) - 1 : 5;   // neighbours marked to the right
+        const int ll = gl ? __ffsll((long long)gl) - 1 : 5;   // and to the left
+        if (lane <= rr + ll) s_picked[il - ll + lane] = 1;
+        supp = supp || (valid && ind >= il - ll && ind <= il + rr);
+        pending &= ~((2ull << l) - 1ull);   // candidates up to l examined
       }
-      for (int k = -1; k >= -5; --k) {
-        const double dX = s_x[ind + k] - s_x[ind + k + 1];
-        const double dY = s_y[ind + k] - s_y[ind + k + 1];
-        const double dZ = s_z[ind + k] - s_z[ind + k + 1];
-        if (dX * dX + dY * dY + dZ * dZ > 0.05) break;
-        s_picked[ind + k] = 1;
-      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // (this wave's picked marks: the next chunk's reads)
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    s_nedge = nedge;
+    if (lane == 0) s_nedge = nedge;
   }
   __syncthreads();
   const int nedge = s_nedge;
@@ -242,55 +314,10 @@ __global__ __launch_bounds__(kSectorThreads) void fe_sector(const int* __restric
   }
 }
 
-__global__ __launch_bounds__(kSectorThreads) void fe_output(const PointRec* __restrict__ in,
-                                                            const int* __restrict__ ring_count,
-                                                            const int* __restrict__ ring_idx,
-                                                            const int* __restrict__ sec_edge_cnt,
-                                                            const int* __restrict__ sec_edge_pos,
-                                                            const int* __restrict__ sec_surf_cnt,
-                                                            const int* __restrict__ surf_pos,
-                                                            PointRec* __restrict__ edge_out, const int* __restrict__ edge_count,
-                                                            PointRec* __restrict__ surf_out, const int* __restrict__ surf_count,
-                                                            int clear) {
-  __shared__ int red[2][kSectorThreads / 64];
-  __shared__ int s_off;
-  const int sec = blockIdx.x;
-  const int r = sec / 6, s = sec % 6;
-  int pe = 0, ps = 0;
-  for (int k = threadIdx.x; k < sec; k += blockDim.x) {
-    pe += sec_edge_cnt[k];
-    ps += sec_surf_cnt[k];
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    pe += __shfl_down(pe, o, 64);
-    ps += __shfl_down(ps, o, 64);
-  }
-  if ((threadIdx.x & 63) == 0) {
-    red[0][threadIdx.x >> 6] = pe;
-    red[1][threadIdx.x >> 6] = ps;
-  }
-  if (threadIdx.x == 0) s_off = ring_offset(ring_count, r);
-  __syncthreads();
-  int edge_prefix = 0, surf_prefix = 0;
-  for (int w = 0; w < kSectorThreads / 64; ++w) {
-    edge_prefix += red[0][w];
-    surf_prefix += red[1][w];
-  }
-  const int ne = sec_edge_cnt[sec], ns = sec_surf_cnt[sec];
-  const int be = ((clear & 1) ? 0 : edge_count[0]) + edge_prefix, bs = ((clear & 2) ? 0 : surf_count[0]) + surf_prefix;
-  if ((int)threadIdx.x < ne) edge_out[be + threadIdx.x] = make_out(in[ring_idx[sec_edge_pos[sec * kMaxEdgesPerSector + threadIdx.x]]]);
-  if (ns > 0) {
-    int a, b;
-    sector_range(ring_count[r], s, a, b);
-    const int base = s_off + a;
-    for (int k = threadIdx.x; k < ns; k += blockDim.x) surf_out[bs + k] = make_out(in[ring_idx[surf_pos[base + k]]]);
-  }
-}
-
 // Advances the output counts, publishes (edge count, surf count, status) for one D2H copy and re-zeroes the
-// per-call counters for the next call (so no memset nodes are needed).
-__global__ void fe_commit(int n_sectors, const int* __restrict__ sec_edge_cnt, const int* __restrict__ sec_surf_cnt,
+// per-call counters for the next call (so no memset nodes are needed).  Run by the last block of fe_output to
+// arrive (every other block has read the counts and ring sizes it needs), not as a launch of its own.
+__device__ __forceinline__ void fe_commit_block(int n_sectors, const int* __restrict__ sec_edge_cnt, const int* __restrict__ sec_surf_cnt,
                           int* __restrict__ edge_count, int* __restrict__ surf_count, int* __restrict__ ring_count,
                           int num_lines, int* __restrict__ status, int* __restrict__ out3,
                           int* __restrict__ stat_edge, int* __restrict__ stat_surf, unsigned* __restrict__ radix_ctl,
@@ -328,6 +355,73 @@ __global__ void fe_commit(int n_sectors, const int* __restrict__ sec_edge_cnt, c
   for (int r = threadIdx.x; r < num_lines; r += blockDim.x) ring_count[r] = 0;
 }
 
+__global__ __launch_bounds__(kSectorThreads) void fe_output(const PointRec* __restrict__ ring_pts,
+                                                            const int* __restrict__ ring_count,
+                                                            const int* __restrict__ sec_edge_cnt,
+                                                            const int* __restrict__ sec_edge_pos,
+                                                            const int* __restrict__ sec_surf_cnt,
+                                                            const int* __restrict__ surf_pos,
+                                                            PointRec* __restrict__ edge_out, int* __restrict__ edge_count,
+                                                            PointRec* __restrict__ surf_out, int* __restrict__ surf_count,
+                                                            int clear, int* __restrict__ ring_count_w, int num_lines,
+                                                            int* __restrict__ status, int* __restrict__ out3,
+                                                            int* __restrict__ stat_edge, int* __restrict__ stat_surf,
+                                                            unsigned* __restrict__ radix_ctl,
+                                                            unsigned* __restrict__ ticket) {
+  __shared__ int red[2][kSectorThreads / 64];
+  __shared__ int s_off;
+  const int sec = blockIdx.x;
+  const int r = sec / 6, s = sec % 6;
+  int pe = 0, ps = 0;
+  for (int k = threadIdx.x; k < sec; k += blockDim.x) {
+    pe += sec_edge_cnt[k];
+    ps += sec_surf_cnt[k];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    pe += __shfl_down(pe, o, 64);
+    ps += __shfl_down(ps, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = pe;
+    red[1][threadIdx.x >> 6] = ps;
+  }
+  const int roff = ring_offset(ring_count, r, &s_off);   // (its barrier also orders red[][])
+  int edge_prefix = 0, surf_prefix = 0;
+  for (int w = 0; w < kSectorThreads / 64; ++w) {
+    edge_prefix += red[0][w];
+    surf_prefix += red[1][w];
+  }
+  const int ne = sec_edge_cnt[sec], ns = sec_surf_cnt[sec];
+  const int be = ((clear & 1) ? 0 : edge_count[0]) + edge_prefix, bs = ((clear & 2) ? 0 : surf_count[0]) + surf_prefix;
+  if ((int)threadIdx.x < ne) edge_out[be + threadIdx.x] = make_out(ring_pts[sec_edge_pos[sec * kMaxEdgesPerSector + threadIdx.x]]);
+  if (ns > 0) {
+    int a, b;
+    sector_range(ring_count[r], s, a, b);
+    const int base = roff + a;
+    for (int k = threadIdx.x; k < ns; k += blockDim.x) surf_out[bs + k] = make_out(ring_pts[surf_pos[base + k]]);
+  }
+  // the commit by the last block to arrive (its add returns nblocks - 1: every block has read what it needs)
+  __shared__ int s_last;
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  fe_commit_block((int)gridDim.x, sec_edge_cnt, sec_surf_cnt, edge_count, surf_count, ring_count_w, num_lines, status,
+                  out3, stat_edge, stat_surf, radix_ctl, clear);
+  if (threadIdx.x == 0) *ticket = 0u;
+}
+
+// more than 255 rings: the ring-major staging by the ring-ordered input indices (the key-only passes' output)
+__global__ void fe_stage(const PointRec* __restrict__ in, const int* __restrict__ ring_idx, int n,
+                         float4* __restrict__ ring_xyz, PointRec* __restrict__ ring_pts) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const PointRec p = in[ring_idx[i]];
+    ring_xyz[i] = make_float4(p.x, p.y, p.z, 0.0f);
+    ring_pts[i] = p;
+  }
+}
+
 }  // namespace
 
 void fe_launch(FeScratch& sc, const FeParams& prm, const PointRec* d_in, int n, PointRec* edge_out,
@@ -338,6 +432,8 @@ void fe_launch(FeScratch& sc, const FeParams& prm, const PointRec* d_in, int n, 
   sc.keys2.reserve(n);
   sc.vals.reserve(n);
   sc.ring_idx.reserve(n + 16);
+  sc.ring_xyz.reserve(n + 16);
+  sc.ring_pts.reserve(n + 16);
   if (sc.ring_count.cap < (size_t)R) sc.zeroed = false;
   sc.ring_count.reserve(R);
   sc.out3.reserve(4);
@@ -346,46 +442,60 @@ void fe_launch(FeScratch& sc, const FeParams& prm, const PointRec* d_in, int n, 
   sc.sec_edge_pos.reserve(6 * R * kMaxEdgesPerSector);
   sc.surf_pos.reserve(n + 16);
   sc.rs.reserve(n, st);   // (a fresh control block is zeroed by the allocation)
-  if (!sc.zeroed || sc.zeroed_lines < R) {   // fe_commit re-zeroes the counters at the end of every call
+  if (!sc.ticket.p) {
+    sc.ticket.reserve(1);
+    FLOAM_HIP(hipMemsetAsync(sc.ticket.p, 0, sizeof(unsigned), st));   // (reset by the last block of every call)
+  }
+  if (!sc.zeroed || sc.zeroed_lines < R) {   // the commit re-zeroes the counters at the end of every call
     FLOAM_HIP(hipMemsetAsync(sc.ring_count.p, 0, sizeof(int) * sc.ring_count.cap, st));
     FLOAM_HIP(hipMemsetAsync(sc.status, 0, sizeof(int), st));
     sc.zeroed = true;
     sc.zeroed_lines = R;
   }
   const int tb = 256;
-  hipLaunchKernelGGL(fe_keys, dim3(std::min(div_up(n, tb), 512u)), dim3(tb), sizeof(int) * R, st, d_in, n, R,
-                     prm.min_distance, prm.max_distance, sc.keys.p, sc.vals.p, sc.ring_count.p, sc.status, sc.rs.ctl.p);
+  if (R <= 255) {   // few blocks, 4+ points per thread: each block folds <= 256 bins with global atomics
+    hipLaunchKernelGGL(fe_keys<true>, dim3(std::max(1u, std::min(div_up(n, 4 * tb), 256u))), dim3(tb), 0, st, d_in,
+                       n, R, prm.min_distance, prm.max_distance, sc.keys.p, sc.vals.p, sc.ring_count.p, sc.status,
+                       sc.rs.ctl.p);
+  } else {
+    hipLaunchKernelGGL(fe_keys<false>, dim3(std::min(div_up(n, tb), 512u)), dim3(tb), sizeof(int) * R, st, d_in, n,
+                       R, prm.min_distance, prm.max_distance, sc.keys.p, sc.vals.p, sc.ring_count.p, sc.status,
+                       sc.rs.ctl.p);
+  }
   FLOAM_LAUNCH_CHECK();
-  // stable bucketing by ring: rings < 255 differ in the low digit only (dropped points: 0xFFFF, last)
+  // stable bucketing by ring: rings < 255 differ in the low digit only (dropped points: 0xFFFF, last); the pass
+  // stages the scan ring-major
   if (R <= 255) {
-    radix_pass_launch(sc.rs, sc.keys.p, sc.vals.p, sc.keys2.p, sc.ring_idx.p, n, 0, st);
+    radix_pass_payload_launch(sc.rs, sc.keys.p, nullptr, nullptr, n, d_in, sc.ring_xyz.p, sc.ring_pts.p, st);
   } else {
     radix_pass_launch(sc.rs, sc.keys.p, sc.vals.p, sc.keys2.p, sc.surf_pos.p, n, 0, st);
     radix_pass_launch(sc.rs, sc.keys2.p, sc.surf_pos.p, sc.keys.p, sc.ring_idx.p, n, 1, st);
+    hipLaunchKernelGGL(fe_stage, dim3(std::min(div_up(n, 256u), 1024u)), dim3(256), 0, st, d_in, sc.ring_idx.p, n,
+                       sc.ring_xyz.p, sc.ring_pts.p);
+    FLOAM_LAUNCH_CHECK();
   }
   // the longest possible sector is (max ring size - 10) / 6 <= n / 6: the 4096 pass is only needed beyond 1024
   const bool big = n / 6 + 8 > 1024;
   if (big) {
-    hipLaunchKernelGGL((fe_sector<0, 1024, false>), dim3(6 * R), dim3(kSectorThreads), 0, st, sc.ring_count.p, d_in,
-                       sc.ring_idx.p, sc.sec_edge_cnt.p, sc.sec_edge_pos.p, sc.sec_surf_cnt.p, sc.surf_pos.p,
+    hipLaunchKernelGGL((fe_sector<0, 1024, false>), dim3(6 * R), dim3(kSectorThreads), 0, st, sc.ring_count.p,
+                       sc.ring_xyz.p, sc.sec_edge_cnt.p, sc.sec_edge_pos.p, sc.sec_surf_cnt.p, sc.surf_pos.p,
                        sc.status);
     FLOAM_LAUNCH_CHECK();
     hipLaunchKernelGGL((fe_sector<1024, 4096, true>), dim3(6 * R), dim3(kSectorThreads), 0, st, sc.ring_count.p,
-                       d_in, sc.ring_idx.p, sc.sec_edge_cnt.p, sc.sec_edge_pos.p, sc.sec_surf_cnt.p, sc.surf_pos.p,
+                       sc.ring_xyz.p, sc.sec_edge_cnt.p, sc.sec_edge_pos.p, sc.sec_surf_cnt.p, sc.surf_pos.p,
                        sc.status);
   } else {
-    hipLaunchKernelGGL((fe_sector<0, 1024, true>), dim3(6 * R), dim3(kSectorThreads), 0, st, sc.ring_count.p, d_in,
-                       sc.ring_idx.p, sc.sec_edge_cnt.p, sc.sec_edge_pos.p, sc.sec_surf_cnt.p, sc.surf_pos.p,
+    hipLaunchKernelGGL((fe_sector<0, 1024, true>), dim3(6 * R), dim3(kSectorThreads), 0, st, sc.ring_count.p,
+                       sc.ring_xyz.p, sc.sec_edge_cnt.p, sc.sec_edge_pos.p, sc.sec_surf_cnt.p, sc.surf_pos.p,
                        sc.status);
   }
   FLOAM_LAUNCH_CHECK();
-  hipLaunchKernelGGL(fe_output, dim3(6 * R), dim3(kSectorThreads), 0, st, d_in, sc.ring_count.p, sc.ring_idx.p,
+  hipLaunchKernelGGL(fe_output, dim3(6 * R), dim3(kSectorThreads), 0, st, sc.ring_pts.p, sc.ring_count.p,
                      sc.sec_edge_cnt.p, sc.sec_edge_pos.p, sc.sec_surf_cnt.p, sc.surf_pos.p, edge_out, edge_count,
-                     surf_out, surf_count, clear);
+                     surf_out, surf_count, clear, sc.ring_count.p, R, sc.status, sc.out3.p, stat_edge, stat_surf,
+                     sc.rs.ctl.p, sc.ticket.p);
   FLOAM_LAUNCH_CHECK();
-  hipLaunchKernelGGL(fe_commit, dim3(1), dim3(256), 0, st, 6 * R, sc.sec_edge_cnt.p, sc.sec_surf_cnt.p, edge_count,
-                     surf_count, sc.ring_count.p, R, sc.status, sc.out3.p, stat_edge, stat_surf, sc.rs.ctl.p, clear);
-  FLOAM_LAUNCH_CHECK();
+
 }
 
 }  // namespace floam

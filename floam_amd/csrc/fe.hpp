@@ -16,7 +16,11 @@ struct FeScratch {
   DevBuf<int> vals;               // input indices before the sort
   RadixScratch rs;                // the sort's control block (this extraction's own: it runs on its own stream)
   DevBuf<int> ring_count, ring_idx, sec_edge_cnt, sec_surf_cnt, sec_edge_pos, surf_pos;
+  // the scan staged ring-major once, by the bucketing pass: the sectors stream contiguous coordinates and records
+  DevBuf<float4> ring_xyz;
+  DevBuf<PointRec> ring_pts;
   DevBuf<int> out3;        // edge count, surf count, status after the call (one D2H)
+  DevBuf<unsigned> ticket; // fe_output's arrival counter (its last block commits)
   int* status = nullptr;   // device int, owned by the caller
   bool zeroed = false;
   int zeroed_lines = 0;

@@ -43,12 +43,17 @@ __device__ __forceinline__ unsigned long long match_digit(unsigned d, bool valid
   return m;
 }
 
+// PAYLOAD: the values are the element positions (a first pass over the original order), and each element's
+// record pin[i] travels with it: its 16-B coordinates to pxyz[dst], the whole 32-B record to prec[dst] (loaded
+// coalesced with the keys, written where the element lands); the sorted keys / values only if kout != null
+template <bool PAYLOAD>
 __global__ __launch_bounds__(kTB) void radix_pass(const uint32_t* __restrict__ kin, const int* __restrict__ vin,
                                                   uint32_t* __restrict__ kout, int* __restrict__ vout, int n,
                                                   int pass, unsigned* __restrict__ ctl,
                                                   unsigned long long* __restrict__ status,
                                                   const int* __restrict__ gate, const int* __restrict__ n_dev,
-                                                  int stamps) {
+                                                  int stamps, const PointRec* __restrict__ pin,
+                                                  float4* __restrict__ pxyz, PointRec* __restrict__ prec) {
   const unsigned long long ts0 = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
   // every load of the prologue is issued at once (one memory round trip, not three in a row): the gate, the epoch,
   // the device count, this digit's histogram count and the tile's elements up to the host bound n (allocated; the
@@ -66,7 +71,15 @@ __global__ __launch_bounds__(kTB) void radix_pass(const uint32_t* __restrict__ k
   for (int r = 0; r < kItems; ++r) {
     const int i = base + r * 64 + lane;
     key[r] = i < n ? kin[i] : 0u;
-    val[r] = i < n ? vin[i] : 0;
+    val[r] = PAYLOAD ? i : (i < n ? vin[i] : 0);
+  }
+  PointRec rec[PAYLOAD ? kItems : 1];
+  if (PAYLOAD) {
+#pragma unroll
+    for (int r = 0; r < kItems; ++r) {
+      const int i = base + r * 64 + lane;
+      if (i < n) rec[r] = pin[i];
+    }
   }
   if (!gv) return;
   n = min(n, nd);
@@ -113,6 +126,17 @@ __global__ __launch_bounds__(kTB) void radix_pass(const uint32_t* __restrict__ k
     if (lane >= o) incl += u;
   }
   if (lane == 63) s_wsum[w] = incl;
+  // PAYLOAD: the tile-local start of digit t (exclusive scan of the tile's digit counts) for the LDS staging
+  __shared__ unsigned s_twsum[kTB / 64];
+  unsigned tincl = cnt;
+  if (PAYLOAD) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned u = __shfl_up(tincl, o, 64);
+      if (lane >= o) tincl += u;
+    }
+    if (lane == 63) s_twsum[w] = tincl;
+  }
   unsigned prefix = 0;
   if (tile > 0) {
     // windowed lookback: the words of the kLbWin nearest unconsumed predecessors are loaded together (one round
@@ -159,16 +183,52 @@ __global__ __launch_bounds__(kTB) void radix_pass(const uint32_t* __restrict__ k
   for (int k = 0; k < kTB / 64; ++k)
     if (k < w) wb += s_wsum[k];
   s_off[t] = wb + incl - h + prefix;
+  __shared__ unsigned s_tstart[PAYLOAD ? kRadixDigits : 1];
+  if (PAYLOAD) {
+    unsigned twb = 0;
+#pragma unroll
+    for (int k = 0; k < kTB / 64; ++k)
+      if (k < w) twb += s_twsum[k];
+    s_tstart[t] = twb + tincl - cnt;
+  }
   __syncthreads();
   const unsigned long long ts2 = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
   // 4. scatter
+  if (PAYLOAD) {   // keys / values as below; the records through LDS in tile-sorted order, then written as runs
+    __shared__ PointRec s_rec[PAYLOAD ? kTile : 1];
+    __shared__ unsigned char s_dig[PAYLOAD ? kTile : 1];
 #pragma unroll
-  for (int r = 0; r < kItems; ++r) {
-    if (base + r * 64 + lane < n) {
-      const unsigned d = (key[r] >> shift) & 255u;
-      const unsigned dst = s_off[d] + s_wcnt[w][d] + rank[r];
-      kout[dst] = key[r];
-      vout[dst] = val[r];
+    for (int r = 0; r < kItems; ++r) {
+      if (base + r * 64 + lane < n) {
+        const unsigned d = (key[r] >> shift) & 255u;
+        const unsigned loc = s_tstart[d] + s_wcnt[w][d] + rank[r];
+        s_rec[loc] = rec[r];
+        s_dig[loc] = (unsigned char)d;
+        if (kout) {
+          const unsigned dst = s_off[d] + s_wcnt[w][d] + rank[r];
+          kout[dst] = key[r];
+          vout[dst] = val[r];
+        }
+      }
+    }
+    __syncthreads();
+    const int nloc = min(kTile, n - tile * kTile);
+    for (int j = t; j < nloc; j += kTB) {   // consecutive j of one digit land on consecutive slots
+      const unsigned d = s_dig[j];
+      const unsigned dst = s_off[d] + ((unsigned)j - s_tstart[d]);
+      const PointRec q = s_rec[j];
+      prec[dst] = q;
+      pxyz[dst] = make_float4(q.x, q.y, q.z, 0.0f);
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < kItems; ++r) {
+      if (base + r * 64 + lane < n) {
+        const unsigned d = (key[r] >> shift) & 255u;
+        const unsigned dst = s_off[d] + s_wcnt[w][d] + rank[r];
+        kout[dst] = key[r];
+        vout[dst] = val[r];
+      }
     }
   }
   if (stamps) {
@@ -241,8 +301,19 @@ void radix_pass_launch(RadixScratch& sc, const uint32_t* kin, const int* vin, ui
   if (n <= 0) return;
   sc.reserve(n, st);
   const int tiles = (int)div_up((unsigned)n, (unsigned)kTile);
-  hipLaunchKernelGGL(radix_pass, dim3(tiles), dim3(kTB), 0, st, kin, vin, kout, vout, n, pass, sc.ctl.p,
-                     sc.status.p + (size_t)pass * sc.tiles_cap * kRadixDigits, nullptr, nullptr, stamps_on());
+  hipLaunchKernelGGL(radix_pass<false>, dim3(tiles), dim3(kTB), 0, st, kin, vin, kout, vout, n, pass, sc.ctl.p,
+                     sc.status.p + (size_t)pass * sc.tiles_cap * kRadixDigits, nullptr, nullptr, stamps_on(), nullptr,
+                     nullptr, nullptr);
+  FLOAM_LAUNCH_CHECK();
+}
+
+void radix_pass_payload_launch(RadixScratch& sc, const uint32_t* kin, uint32_t* kout, int* vout, int n,
+                               const PointRec* pin, float4* pxyz, PointRec* prec, hipStream_t st) {
+  if (n <= 0) return;
+  sc.reserve(n, st);
+  const int tiles = (int)div_up((unsigned)n, (unsigned)kTile);
+  hipLaunchKernelGGL(radix_pass<true>, dim3(tiles), dim3(kTB), 0, st, kin, nullptr, kout, vout, n, 0, sc.ctl.p,
+                     sc.status.p, nullptr, nullptr, stamps_on(), pin, pxyz, prec);
   FLOAM_LAUNCH_CHECK();
 }
 
@@ -253,9 +324,10 @@ void radix_sort_launch(RadixScratch& sc, uint32_t* k0, int* v0, uint32_t* k1, in
   const int tiles = (int)div_up((unsigned)n, (unsigned)kTile);
   for (int p = 0; p < kRadixPasses; ++p) {
     const bool even = (p & 1) == 0;
-    hipLaunchKernelGGL(radix_pass, dim3(tiles), dim3(kTB), 0, st, even ? k0 : k1, even ? v0 : v1, even ? k1 : k0,
-                       even ? v1 : v0, n, p, sc.ctl.p, sc.status.p + (size_t)p * sc.tiles_cap * kRadixDigits,
-                       gate, n_dev, stamps_on());
+    hipLaunchKernelGGL(radix_pass<false>, dim3(tiles), dim3(kTB), 0, st, even ? k0 : k1, even ? v0 : v1,
+                       even ? k1 : k0, even ? v1 : v0, n, p, sc.ctl.p,
+                       sc.status.p + (size_t)p * sc.tiles_cap * kRadixDigits, gate, n_dev, stamps_on(), nullptr,
+                       nullptr, nullptr);
     FLOAM_LAUNCH_CHECK();
   }
 }

@@ -61,6 +61,12 @@ void radix_sort_launch(RadixScratch& sc, uint32_t* k0, int* v0, uint32_t* k1, in
 
 // One digit pass (pass p sorts by bits [8p, 8p + 8)) of the same sort, for keys whose high digits are known to be
 // equal (e.g. the feature extraction's ring keys: one pass for <= 255 rings)
+// The first digit pass (pass 0) over elements in their original order (values = positions, not read) carrying each
+// element's record: its coordinates to pxyz[dst] and the record to prec[dst] (the feature extraction's ring-major
+// staging of the scan); kout / vout (nullable): the sorted keys and positions
+void radix_pass_payload_launch(RadixScratch& sc, const uint32_t* kin, uint32_t* kout, int* vout, int n,
+                               const PointRec* pin, float4* pxyz, PointRec* prec, hipStream_t st);
+
 // FLOAM_RADIX_STAMPS=1: print the passes' in-kernel phase times (diagnostic; synchronises the device)
 void radix_stamps_print();
 
