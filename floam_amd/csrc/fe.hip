@@ -6,7 +6,8 @@
 //                               R <= 255 rings, O(P), which stages the scan ring-major as it goes: every point's
 //                               coordinates (16 B) and record (32 B) written once to its ring-major slot (more rings:
 //                               two key-only passes, then fe_stage gathers by the ring-ordered indices)
-//   fe_sector   one WG / sector curvature stencil over the contiguous ring-major coordinates, LDS bitonic sort,
+//   fe_sector   one WG / sector curvature stencil over the contiguous ring-major coordinates, LDS bitonic
+//                               sort (block barriers only around the strides that cross waves), wave-parallel
 //                               greedy edge pick, surf compaction
 //   fe_output   one WG / sector copy the 32-B ring-major records of edges / surfs to their sector-major slots; the
 //                               last block to finish advances the output counts (the commit)
@@ -18,6 +19,10 @@
 #include "radix.hpp"
 
 namespace floam {
+
+// FLOAM_FE_STAMPS=1 (diagnostic): fe_sector's per-block phase times (100 MHz ticks): [0] staging, [1] curvature +
+// sort, [2] greedy pick, [3] surf compaction + writes, [4] blocks, [5] sum of launch spans, [6] launches
+__device__ unsigned long long g_fe_stamps[8];
 
 namespace {
 
@@ -145,7 +150,8 @@ __global__ __launch_bounds__(kSectorThreads) void fe_sector(const int* __restric
                                                             const float4* __restrict__ ring_xyz,
                                                             int* __restrict__ sec_edge_cnt, int* __restrict__ sec_edge_pos,
                                                             int* __restrict__ sec_surf_cnt, int* __restrict__ surf_pos,
-                                                            int* __restrict__ status) {
+                                                            int* __restrict__ status, int stamps) {
+  const unsigned long long T0 = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
   constexpr int kPts = MAXSEC + 10;
   __shared__ unsigned long long s_key[MAXSEC];
   __shared__ uint16_t s_id[MAXSEC];      // ring index - a - 5 (the curvature entry offset)
@@ -184,56 +190,63 @@ __global__ __launch_bounds__(kSectorThreads) void fe_sector(const int* __restric
     s_picked[k] = 0;
   }
   __syncthreads();
+  const unsigned long long T1 = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
   // curvature (src/laserProcessingClass.cpp:95-101), entry e = a + k, point j = e + 5 -> local k + 5
-  int P2 = 1;
-  while (P2 < m) P2 <<= 1;
-  for (int k = threadIdx.x; k < P2; k += blockDim.x) {
-    if (k < m) {
-      const int c = k + 5;
-      const float fx = s_x[c - 5] + s_x[c - 4] + s_x[c - 3] + s_x[c - 2] + s_x[c - 1] - 10 * s_x[c] + s_x[c + 1] +
-                       s_x[c + 2] + s_x[c + 3] + s_x[c + 4] + s_x[c + 5];
-      const float fy = s_y[c - 5] + s_y[c - 4] + s_y[c - 3] + s_y[c - 2] + s_y[c - 1] - 10 * s_y[c] + s_y[c + 1] +
-                       s_y[c + 2] + s_y[c + 3] + s_y[c + 4] + s_y[c + 5];
-      const float fz = s_z[c - 5] + s_z[c - 4] + s_z[c - 3] + s_z[c - 2] + s_z[c - 1] - 10 * s_z[c] + s_z[c + 1] +
-                       s_z[c + 2] + s_z[c + 3] + s_z[c + 4] + s_z[c + 5];
-      const double dX = fx, dY = fy, dZ = fz;
-      const double v = dX * dX + dY * dY + dZ * dZ;
-      s_key[k] = (unsigned long long)__double_as_longlong(v);   // v >= +0: bit pattern is order-preserving
-      s_id[k] = (uint16_t)k;
-    } else {
-      s_key[k] = ~0ull;
-      s_id[k] = 0xFFFF;
+  auto curvature = [&](int k) -> unsigned long long {
+    const int c = k + 5;
+    const float fx = s_x[c - 5] + s_x[c - 4] + s_x[c - 3] + s_x[c - 2] + s_x[c - 1] - 10 * s_x[c] + s_x[c + 1] +
+                     s_x[c + 2] + s_x[c + 3] + s_x[c + 4] + s_x[c + 5];
+    const float fy = s_y[c - 5] + s_y[c - 4] + s_y[c - 3] + s_y[c - 2] + s_y[c - 1] - 10 * s_y[c] + s_y[c + 1] +
+                     s_y[c + 2] + s_y[c + 3] + s_y[c + 4] + s_y[c + 5];
+    const float fz = s_z[c - 5] + s_z[c - 4] + s_z[c - 3] + s_z[c - 2] + s_z[c - 1] - 10 * s_z[c] + s_z[c + 1] +
+                     s_z[c + 2] + s_z[c + 3] + s_z[c + 4] + s_z[c + 5];
+    const double dX = fx, dY = fy, dZ = fz;
+    const double v = dX * dX + dY * dY + dZ * dZ;
+    return (unsigned long long)__double_as_longlong(v);   // v >= +0: the bit pattern is order-preserving
+  };
+  {   // (a register / lane-shuffle bitonic and an O(m^2) rank sort both measured slower: 17.3 and 27.3 us a block)
+    int P2 = 1;
+    while (P2 < m) P2 <<= 1;
+    for (int k = threadIdx.x; k < P2; k += blockDim.x) {
+      if (k < m) {
+        s_key[k] = curvature(k);
+        s_id[k] = (uint16_t)k;
+      } else {
+        s_key[k] = ~0ull;
+        s_id[k] = 0xFFFF;
+      }
     }
-  }
-  __syncthreads();
-  // bitonic sort ascending by (key, id).  A stage with stride <= 64 pairs positions inside one 128-entry chunk, and
-  // every chunk belongs to one wave (thread t's pairs lie in chunk t / 64 and t / 64 + 4, ...): those stages need
-  // only the wave's own LDS ordering; block barriers surround the stages with longer strides
-  for (int size = 2; size <= P2; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      if (stride >= 128) __syncthreads();
-      for (int t = threadIdx.x; t < (P2 >> 1); t += blockDim.x) {
-        const int lo = 2 * t - (t & (stride - 1));
-        const int hi = lo + stride;
-        const bool up = ((lo & size) == 0);
-        const unsigned long long ka = s_key[lo], kb = s_key[hi];
-        const uint16_t ia = s_id[lo], ib = s_id[hi];
-        const bool gt = (ka > kb) || (ka == kb && ia > ib);
-        if (gt == up) {
-          s_key[lo] = kb; s_key[hi] = ka;
-          s_id[lo] = ib; s_id[hi] = ia;
+    __syncthreads();
+    // bitonic sort ascending by (key, id).  A stage with stride <= 64 pairs positions inside one 128-entry chunk,
+    // and every chunk belongs to one wave (thread t's pairs lie in chunk t / 64 and t / 64 + 4, ...): those stages
+    // need only the wave's own LDS ordering; block barriers surround the stages with longer strides
+    for (int size = 2; size <= P2; size <<= 1) {
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        if (stride >= 128) __syncthreads();
+        for (int t = threadIdx.x; t < (P2 >> 1); t += blockDim.x) {
+          const int lo = 2 * t - (t & (stride - 1));
+          const int hi = lo + stride;
+          const bool up = ((lo & size) == 0);
+          const unsigned long long ka = s_key[lo], kb = s_key[hi];
+          const uint16_t ia = s_id[lo], ib = s_id[hi];
+          const bool gt = (ka > kb) || (ka == kb && ia > ib);
+          if (gt == up) {
+            s_key[lo] = kb; s_key[hi] = ka;
+            s_id[lo] = ib; s_id[hi] = ia;
+          }
+        }
+        if (stride >= 128) {   // (its pairs crossed chunks: the next stage's chunks were written by other waves)
+          __syncthreads();
+        } else {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
       }
-      if (stride >= 128) {   // (its pairs crossed chunks: the next stage's chunks were written by other waves)
-        __syncthreads();
-      } else {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      }
     }
   }
   __syncthreads();
+  const unsigned long long T2 = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
   // greedy edge pick (src/laserProcessingClass.cpp:129-170) by wave 0: the candidates in descending order, 64 at a
   // time (lane order = the reference's order).  Per chunk every lane reads whether its point was picked by an earlier
   // chunk; then, pick by pick, the first unsuppressed lane is the next candidate the reference examines (the ones
@@ -295,6 +308,7 @@ __global__ __launch_bounds__(kSectorThreads) void fe_sector(const int* __restric
     if (lane == 0) s_nedge = nedge;
   }
   __syncthreads();
+  const unsigned long long T3 = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
   const int nedge = s_nedge;
   if (threadIdx.x < nedge) sec_edge_pos[sec * kMaxEdgesPerSector + threadIdx.x] = off + a + s_edges[threadIdx.x];
   // surf = unpicked entries in ascending order (src/laserProcessingClass.cpp:220-227): contiguous chunk per thread
@@ -311,6 +325,19 @@ __global__ __launch_bounds__(kSectorThreads) void fe_sector(const int* __restric
   if (threadIdx.x == 0) {
     sec_edge_cnt[sec] = nedge;
     sec_surf_cnt[sec] = total;
+  }
+  if (stamps) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned long long T4 = __builtin_amdgcn_s_memrealtime();
+      atomicAdd(&g_fe_stamps[0], T1 - T0);
+      atomicAdd(&g_fe_stamps[1], T2 - T1);
+      atomicAdd(&g_fe_stamps[2], T3 - T2);
+      atomicAdd(&g_fe_stamps[3], T4 - T3);
+      atomicAdd(&g_fe_stamps[4], 1ull);
+      atomicMax(&g_fe_stamps[7], T4 - T0);   // the longest block
+    }
   }
 }
 
@@ -424,6 +451,22 @@ __global__ void fe_stage(const PointRec* __restrict__ in, const int* __restrict_
 
 }  // namespace
 
+static int fe_stamps_on() {
+  static const int on = std::getenv("FLOAM_FE_STAMPS") ? 1 : 0;
+  return on;
+}
+
+void fe_stamps_print() {
+  if (!fe_stamps_on()) return;
+  unsigned long long h[8];
+  FLOAM_HIP(hipDeviceSynchronize());
+  FLOAM_HIP(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_fe_stamps), sizeof(h)));
+  const double nb = h[4] ? (double)h[4] : 1.0;
+  std::fprintf(stderr, "[fe stamps] %llu sector blocks: staging %.2f us, curvature + sort %.2f us, greedy pick %.2f us, "
+               "surf compaction %.2f us per block; longest block %.2f us\n", h[4], h[0] / nb / 100.0,
+               h[1] / nb / 100.0, h[2] / nb / 100.0, h[3] / nb / 100.0, h[7] / 100.0);
+}
+
 void fe_launch(FeScratch& sc, const FeParams& prm, const PointRec* d_in, int n, PointRec* edge_out,
                int* edge_count, PointRec* surf_out, int* surf_count, hipStream_t st, int* stat_edge,
                int* stat_surf, int clear) {
@@ -479,15 +522,15 @@ void fe_launch(FeScratch& sc, const FeParams& prm, const PointRec* d_in, int n, 
   if (big) {
     hipLaunchKernelGGL((fe_sector<0, 1024, false>), dim3(6 * R), dim3(kSectorThreads), 0, st, sc.ring_count.p,
                        sc.ring_xyz.p, sc.sec_edge_cnt.p, sc.sec_edge_pos.p, sc.sec_surf_cnt.p, sc.surf_pos.p,
-                       sc.status);
+                       sc.status, fe_stamps_on());
     FLOAM_LAUNCH_CHECK();
     hipLaunchKernelGGL((fe_sector<1024, 4096, true>), dim3(6 * R), dim3(kSectorThreads), 0, st, sc.ring_count.p,
                        sc.ring_xyz.p, sc.sec_edge_cnt.p, sc.sec_edge_pos.p, sc.sec_surf_cnt.p, sc.surf_pos.p,
-                       sc.status);
+                       sc.status, fe_stamps_on());
   } else {
     hipLaunchKernelGGL((fe_sector<0, 1024, true>), dim3(6 * R), dim3(kSectorThreads), 0, st, sc.ring_count.p,
                        sc.ring_xyz.p, sc.sec_edge_cnt.p, sc.sec_edge_pos.p, sc.sec_surf_cnt.p, sc.surf_pos.p,
-                       sc.status);
+                       sc.status, fe_stamps_on());
   }
   FLOAM_LAUNCH_CHECK();
   hipLaunchKernelGGL(fe_output, dim3(6 * R), dim3(kSectorThreads), 0, st, sc.ring_pts.p, sc.ring_count.p,

@@ -26,6 +26,9 @@ struct FeScratch {
   int zeroed_lines = 0;
 };
 
+// FLOAM_FE_STAMPS=1: print fe_sector's in-kernel phase times (diagnostic; synchronises the device)
+void fe_stamps_print();
+
 // Appends edge/surf features of d_in[0, n) to edge_out/surf_out at their device counts (which are advanced).
 // clear: bit 0 / bit 1 — the edge / surf output counts are taken as 0 (a pending floam_cloud_clear, folded in).
 void fe_launch(FeScratch& sc, const FeParams& prm, const PointRec* d_in, int n, PointRec* edge_out, int* edge_count,

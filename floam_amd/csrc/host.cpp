@@ -1238,6 +1238,7 @@ floam_status floam_lp_wait(floam_lp* lp) {
 floam_status floam_lp_destroy(floam_lp* lp) {
   return guarded([&] {
     if (lp) {
+      fe_stamps_print();
       if (lp->stream) {
         FLOAM_HIP(hipStreamSynchronize(lp->stream));
         FLOAM_HIP(hipStreamDestroy(lp->stream));
