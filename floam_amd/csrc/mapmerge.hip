@@ -35,8 +35,6 @@ namespace floam {
 
 namespace {
 constexpr int kTB = 256;
-constexpr int kPer = 4;
-constexpr int kTile = kTB * kPer;   // merged elements per tile
 constexpr unsigned long long kNone = ~0ull;   // no element (never an index or a sort key: both < 2^32)
 
 __global__ __launch_bounds__(kTB) void mm_keys(VoxelJobDev A, VoxelJobDev B, const float* __restrict__ partials,
@@ -258,6 +256,7 @@ __device__ __forceinline__ PointRec centroid_rec(float4 c) {   // VoxelGrid's ou
   return o;
 }
 
+template <int PER>
 __global__ __launch_bounds__(kTB) void mm_merge(VoxelJobDev A, VoxelJobDev B, MapKeys KA, MapKeys KB,
                                                 const uint32_t* __restrict__ skeys, const int* __restrict__ svals,
                                                 const int* __restrict__ ctl, unsigned long long* __restrict__ mstatus,
@@ -304,7 +303,7 @@ __global__ __launch_bounds__(kTB) void mm_merge(VoxelJobDev A, VoxelJobDev B, Ma
   V.skeys = skeys;
   V.svals = svals;
   const int L = V.full ? V.nset : V.n0 + V.nset;   // merged elements
-  const int ntiles = (L + kTile - 1) / kTile;
+  const int ntiles = (L + (PER * kTB) - 1) / (PER * kTB);
   if (tile >= ntiles) {   // (block-uniform; nobody waits on a tile beyond the last)
     if (tile == 0 && t == 0) {
       *V.J.d_out = 0;
@@ -313,13 +312,13 @@ __global__ __launch_bounds__(kTB) void mm_merge(VoxelJobDev A, VoxelJobDev B, Ma
     }
     return;
   }
-  const int d0 = tile * kTile, d1 = min(L, d0 + kTile), cnt = d1 - d0;
+  const int d0 = tile * (PER * kTB), d1 = min(L, d0 + (PER * kTB)), cnt = d1 - d0;
   // the tile's merged elements in LDS: key (s_key[k + 1] for element k; s_key[0] the previous element, s_key[cnt + 1]
   // the next one), point, source index (concatenation), kept flag
-  __shared__ unsigned long long s_key[kTile + 2];
-  __shared__ float4 s_pt[kTile];
-  __shared__ int s_src[kTile];
-  __shared__ unsigned char s_live[kTile];
+  __shared__ unsigned long long s_key[(PER * kTB) + 2];
+  __shared__ float4 s_pt[(PER * kTB)];
+  __shared__ int s_src[(PER * kTB)];
+  __shared__ unsigned char s_live[(PER * kTB)];
   __shared__ int s_split[2], s_first[2], s_open[2];
   int j1 = d1;   // first set element after the tile (sorted order)
   if (V.full) {
@@ -349,12 +348,12 @@ __global__ __launch_bounds__(kTB) void mm_merge(VoxelJobDev A, VoxelJobDev B, Ma
     }
     const int na = i1 - i0, nb = j1 - j0;
     // the two runs' indices in LDS (points, sources, kept flags stay in registers: element k = t + r kTB)
-    __shared__ unsigned long long s_ak[kTile], s_bk[kTile];
-    float4 rp[kPer];
-    int rs[kPer];
-    bool rl[kPer];
+    __shared__ unsigned long long s_ak[(PER * kTB)], s_bk[(PER * kTB)];
+    float4 rp[PER];
+    int rs[PER];
+    bool rl[PER];
 #pragma unroll
-    for (int r = 0; r < kPer; ++r) {
+    for (int r = 0; r < PER; ++r) {
       const int k = t + r * kTB;
       rs[r] = 0;
       rl[r] = false;
@@ -395,7 +394,7 @@ __global__ __launch_bounds__(kTB) void mm_merge(VoxelJobDev A, VoxelJobDev B, Ma
     }
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < kPer; ++r) {   // merged position: own rank + the other run's elements before it
+    for (int r = 0; r < PER; ++r) {   // merged position: own rank + the other run's elements before it
       const int k = t + r * kTB;
       if (k >= na + nb) continue;
       int pos;
@@ -433,16 +432,16 @@ __global__ __launch_bounds__(kTB) void mm_merge(VoxelJobDev A, VoxelJobDev B, Ma
   // the new map's keys are strictly increasing when every centroid lies in its run's voxel; on an index overflow the
   // map leaves voxel order altogether (both: the next update takes the full sort)
   bool bad = V.ovf;
-  float4 ov[kPer];      // this thread's outputs: centroid (or, on overflow, the source index in ov.x's bits)
+  float4 ov[PER];      // this thread's outputs: centroid (or, on overflow, the source index in ov.x's bits)
   int cross_u = -1;     // which of them continues past the tile (summed so far into s_cross*)
   __shared__ float s_cross[4];
   __shared__ int s_cross_n, s_cross_local;
   __shared__ unsigned long long s_cross_key;
   if (t == 0) s_cross_local = -1;
 #pragma unroll
-  for (int u = 0; u < kPer; ++u) {
+  for (int u = 0; u < PER; ++u) {
     ov[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-    const int k = t * kPer + u;
+    const int k = t * PER + u;
     if (k >= cnt || s_key[k + 1] == s_key[k]) continue;
     const unsigned long long key = s_key[k + 1];
     int e = k + 1;
@@ -533,7 +532,7 @@ __global__ __launch_bounds__(kTB) void mm_merge(VoxelJobDev A, VoxelJobDev B, Ma
   }
   // stage the outputs in tile order (s_pt, s_src are free now) and their cell keys (s_key)
 #pragma unroll
-  for (int u = 0; u < kPer; ++u) {
+  for (int u = 0; u < PER; ++u) {
     if (u >= nout || u == cross_u) continue;
     s_pt[lbase + u] = ov[u];
   }
@@ -563,11 +562,11 @@ __global__ __launch_bounds__(kTB) void mm_merge(VoxelJobDev A, VoxelJobDev B, Ma
   }
   if (violate_mod > 0 && seq % (unsigned)violate_mod == 0) bad = true;   // (test knob: exercise the fallback)
   if (__syncthreads_or(bad) && t == 0) V.K.meta_out->violation = seq;
-  int gi[kPer];
-  bool gv[kPer];
-  float gx[kPer], gy[kPer], gz[kPer];
+  int gi[PER];
+  bool gv[PER];
+  float gx[PER], gy[PER], gz[PER];
 #pragma unroll
-  for (int r = 0; r < kPer; ++r) {   // (nloc <= kTile: every output in one of the kPer rounds)
+  for (int r = 0; r < PER; ++r) {   // (nloc <= (PER * kTB): every output in one of the PER rounds)
     const int k = r * kTB + t;
     gv[r] = k < nloc;
     gi[r] = pre.a + k;
@@ -583,7 +582,7 @@ __global__ __launch_bounds__(kTB) void mm_merge(VoxelJobDev A, VoxelJobDev B, Ma
     }
   }
   // the next kNN grid's per-point step (grid_count_job) for the map's points pre.a + k, all rounds at once
-  if (count_grid) grid_count_points<kPer>(G, gi, gv, gx, gy, gz);
+  if (count_grid) grid_count_points<PER>(G, gi, gv, gx, gy, gz);
   if (tile == ntiles - 1 && t == 0) {
     const bool sort_failed = radix_ctl[kRadixHistWords + 4] != 0u;   // a sort lookback timed out (never expected)
     *V.J.d_out = sort_failed ? -1 : pre.a + nloc;
@@ -622,8 +621,14 @@ void map_merge_launch(VoxelScratch2& vs, MapMergeScratch& ms, const VoxelJob& a,
   const VoxelJobDev A = to_dev(a, 0);
   const VoxelJobDev B = to_dev(b, a.n0_ub + a.n1_ub);
   const int nA = a.n0_ub + a.n1_ub, nB = b.n0_ub + b.n1_ub, n = std::max(nA + nB, 1);
-  const int tilesA = std::max(1, (int)div_up(std::max(nA, 1), kTile));
-  const int tilesB = std::max(1, (int)div_up(std::max(nB, 1), kTile));
+  // merged elements per tile: 256 threads x PER (FLOAM_MM_PER = 2 or 4, default 4)
+  static const int per = [] {
+    const char* e = std::getenv("FLOAM_MM_PER");
+    return e && std::atoi(e) == 2 ? 2 : 4;
+  }();
+  const int tile = kTB * per;
+  const int tilesA = std::max(1, (int)div_up(std::max(nA, 1), tile));
+  const int tilesB = std::max(1, (int)div_up(std::max(nB, 1), tile));
   ms.reserve(std::max(tilesA, tilesB), st);
   vs.s.reserve(n);
   vs.partials.reserve(2 * kVoxMinMaxBlocks * 6);
@@ -637,9 +642,14 @@ void map_merge_launch(VoxelScratch2& vs, MapMergeScratch& ms, const VoxelJob& a,
                      kb.meta_in, ms.flags.p, seq, force_full ? 1 : 0);
   FLOAM_LAUNCH_CHECK();
   radix_sort_launch(vs.rs, vs.s.k0.p, vs.s.v0.p, vs.s.k1.p, vs.s.v1.p, n, st, gate, vs.overflow.p + 2);
-  hipLaunchKernelGGL(mm_merge, dim3(tilesA + tilesB), dim3(kTB), 0, st, A, B, ka, kb, vs.s.k0.p, vs.s.v0.p, ms.ctl.p,
-                     ms.status.p, ms.tiles_cap, tilesA, vs.rs.ctl.p, gate, seq, violate_mod,
-                     grids ? grids[0] : GridCountDev{}, grids ? grids[1] : GridCountDev{}, grids ? 1 : 0);
+  if (per == 2)
+    hipLaunchKernelGGL(mm_merge<2>, dim3(tilesA + tilesB), dim3(kTB), 0, st, A, B, ka, kb, vs.s.k0.p, vs.s.v0.p,
+                       ms.ctl.p, ms.status.p, ms.tiles_cap, tilesA, vs.rs.ctl.p, gate, seq, violate_mod,
+                       grids ? grids[0] : GridCountDev{}, grids ? grids[1] : GridCountDev{}, grids ? 1 : 0);
+  else
+    hipLaunchKernelGGL(mm_merge<4>, dim3(tilesA + tilesB), dim3(kTB), 0, st, A, B, ka, kb, vs.s.k0.p, vs.s.v0.p,
+                       ms.ctl.p, ms.status.p, ms.tiles_cap, tilesA, vs.rs.ctl.p, gate, seq, violate_mod,
+                       grids ? grids[0] : GridCountDev{}, grids ? grids[1] : GridCountDev{}, grids ? 1 : 0);
   FLOAM_LAUNCH_CHECK();
 }
 
