@@ -22,11 +22,13 @@ namespace floam {
 
 // FLOAM_FE_STAMPS=1 (diagnostic): fe_sector's per-block phase times (100 MHz ticks): [0] staging, [1] curvature +
 // sort, [2] greedy pick, [3] surf compaction + writes, [4] blocks, [5] sum of launch spans, [6] launches
-__device__ unsigned long long g_fe_stamps[8];
+__device__ unsigned long long g_fe_stamps[8 + 3 * 1024];   // + per launch: first start, last start, last end
 
 namespace {
 
-constexpr int kSectorThreads = 256;
+constexpr int kSectorThreads = 256;   // fe_output
+// fe_sector's block (128 threads measured slower: 32 vs 25 us from the first block's start to the last one's end)
+constexpr int kSortThreads = 256;
 constexpr int kMaxEdgesPerSector = 20;
 
 __device__ __forceinline__ PointRec make_out(const PointRec& p) {
@@ -143,10 +145,87 @@ __device__ __forceinline__ void sector_range(int n_r, int s, int& a, int& b) {
   b = (s == 5) ? T - 1 : L * (s + 1) - 1;
 }
 
+// ---- register bitonic sort of a sector's (curvature bits, entry) pairs: N = kSortThreads E entries, E per thread (position
+// p = E t + e), every stage's stride a compile-time constant, so a lane exchange inside a wave is one ds_swizzle
+// (xor of the lane bits, no memory) or, across the wave halves, one ds_bpermute; only strides >= 64 E go through LDS.
+template <int M>
+__device__ __forceinline__ unsigned xor_lane(unsigned v) {
+  if constexpr (M < 32) return (unsigned)__builtin_amdgcn_ds_swizzle((int)v, (M << 10) | 0x1F);   // bitmask mode
+  else return (unsigned)__builtin_amdgcn_ds_bpermute((int)((((threadIdx.x & 63) ^ M)) << 2), (int)v);
+}
+template <int M>
+__device__ __forceinline__ unsigned long long xor_lane64(unsigned long long v) {
+  return ((unsigned long long)xor_lane<M>((unsigned)(v >> 32)) << 32) | xor_lane<M>((unsigned)v);
+}
+
+// one stage (size, stride) of the network on the thread's E registers
+template <int E, int SIZE, int STRIDE>
+__device__ __forceinline__ void bitonic_stage(unsigned long long (&k)[E], unsigned (&id)[E],
+                                              unsigned long long* s_key, uint16_t* s_id) {
+  const int t = threadIdx.x;
+  unsigned long long ok[E];
+  unsigned oi[E];
+  if constexpr (STRIDE < E) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) { ok[e] = k[e ^ STRIDE]; oi[e] = id[e ^ STRIDE]; }
+  } else if constexpr (STRIDE < 64 * E) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) { ok[e] = xor_lane64<STRIDE / E>(k[e]); oi[e] = xor_lane<STRIDE / E>(id[e]); }
+  } else {
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < E; ++e) { s_key[E * t + e] = k[e]; s_id[E * t + e] = (uint16_t)id[e]; }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < E; ++e) { ok[e] = s_key[(E * t + e) ^ STRIDE]; oi[e] = s_id[(E * t + e) ^ STRIDE]; }
+  }
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int pp = E * t + e;
+    const bool lower = (pp & STRIDE) == 0, asc = (pp & SIZE) == 0;
+    const bool other_less = ok[e] < k[e] || (ok[e] == k[e] && oi[e] < id[e]);
+    if (other_less == (asc == lower)) {   // the lower slot of an ascending pair keeps the smaller, and so on
+      k[e] = ok[e];
+      id[e] = oi[e];
+    }
+  }
+}
+template <int E, int SIZE, int STRIDE>
+__device__ __forceinline__ void bitonic_strides(unsigned long long (&k)[E], unsigned (&id)[E],
+                                                unsigned long long* s_key, uint16_t* s_id) {
+  bitonic_stage<E, SIZE, STRIDE>(k, id, s_key, s_id);
+  if constexpr (STRIDE > 1) bitonic_strides<E, SIZE, STRIDE / 2>(k, id, s_key, s_id);
+}
+template <int E, int SIZE>
+__device__ __forceinline__ void bitonic_sizes(unsigned long long (&k)[E], unsigned (&id)[E],
+                                              unsigned long long* s_key, uint16_t* s_id) {
+  bitonic_strides<E, SIZE, SIZE / 2>(k, id, s_key, s_id);
+  if constexpr (SIZE < kSortThreads * E) bitonic_sizes<E, SIZE * 2>(k, id, s_key, s_id);
+}
+// the m curvature values (entries 0..m-1, padded with +inf keys) sorted ascending by (value, entry) into s_key/s_id
+template <int E, typename Curv>
+__device__ __forceinline__ void sector_sort(int m, Curv curvature, unsigned long long* s_key, uint16_t* s_id) {
+  unsigned long long k[E];
+  unsigned id[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int q = E * threadIdx.x + e;
+    k[e] = q < m ? curvature(q) : ~0ull;
+    id[e] = q < m ? (unsigned)q : 0xFFFFu;
+  }
+  bitonic_sizes<E, 2>(k, id, s_key, s_id);
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    s_key[E * threadIdx.x + e] = k[e];
+    s_id[E * threadIdx.x + e] = (uint16_t)id[e];
+  }
+}
+
 // Sectors with MINSEC < m <= MAXSEC are processed; the small-LDS instantiation runs first and the large one only
 // picks up the (rare) longer sectors, so the common case keeps several workgroups per CU.
 template <int MINSEC, int MAXSEC, bool LAST>
-__global__ __launch_bounds__(kSectorThreads) void fe_sector(const int* __restrict__ ring_count,
+__global__ __launch_bounds__(kSortThreads) void fe_sector(const int* __restrict__ ring_count,
                                                             const float4* __restrict__ ring_xyz,
                                                             int* __restrict__ sec_edge_cnt, int* __restrict__ sec_edge_pos,
                                                             int* __restrict__ sec_surf_cnt, int* __restrict__ surf_pos,
@@ -204,7 +283,12 @@ __global__ __launch_bounds__(kSectorThreads) void fe_sector(const int* __restric
     const double v = dX * dX + dY * dY + dZ * dZ;
     return (unsigned long long)__double_as_longlong(v);   // v >= +0: the bit pattern is order-preserving
   };
-  {   // (a register / lane-shuffle bitonic and an O(m^2) rank sort both measured slower: 17.3 and 27.3 us a block)
+  if (MAXSEC <= 1024 && m <= 1024) {   // (block-uniform) the register network, E = 1, 2, 4 or 8 entries a thread
+    if (m <= kSortThreads) sector_sort<1>(m, curvature, s_key, s_id);
+    else if (m <= 2 * kSortThreads) sector_sort<2>(m, curvature, s_key, s_id);
+    else if (m <= 4 * kSortThreads) sector_sort<4>(m, curvature, s_key, s_id);
+    else sector_sort<8>(m, curvature, s_key, s_id);
+  } else {   // longer sectors (the 4096 instantiation): the network in LDS
     int P2 = 1;
     while (P2 < m) P2 <<= 1;
     for (int k = threadIdx.x; k < P2; k += blockDim.x) {
@@ -272,8 +356,11 @@ __global__ __launch_bounds__(kSectorThreads) void fe_sector(const int* __restric
         const unsigned long long cand = __ballot(!supp) & pending;
         if (!cand) break;   // the rest of the chunk was picked: the next chunk
         const int l = __ffsll((long long)cand) - 1;
-        const double kl = __shfl(key, l, 64);
-        const int il = __shfl(ind, l, 64);
+        const unsigned long long kb = (unsigned long long)__double_as_longlong(key);
+        const double kl = __longlong_as_double((long long)(((unsigned long long)(unsigned)__builtin_amdgcn_readlane(
+                                                               (int)(kb >> 32), l) << 32) |
+                                                           (unsigned)__builtin_amdgcn_readlane((int)kb, l)));
+        const int il = __builtin_amdgcn_readlane(ind, l);
         if (kl <= 0.1) { stop = true; break; }
         ++picked_num;
         if (picked_num > 20) {   // picked, not kept, and the loop ends
@@ -337,6 +424,10 @@ __global__ __launch_bounds__(kSectorThreads) void fe_sector(const int* __restric
       atomicAdd(&g_fe_stamps[3], T4 - T3);
       atomicAdd(&g_fe_stamps[4], 1ull);
       atomicMax(&g_fe_stamps[7], T4 - T0);   // the longest block
+      unsigned long long* L = &g_fe_stamps[8 + 3 * ((stamps - 1) % 1024)];
+      atomicMin(&L[0], T0);
+      atomicMax(&L[1], T0);
+      atomicMax(&L[2], T4);
     }
   }
 }
@@ -453,15 +544,34 @@ __global__ void fe_stage(const PointRec* __restrict__ in, const int* __restrict_
 
 static int fe_stamps_on() {
   static const int on = std::getenv("FLOAM_FE_STAMPS") ? 1 : 0;
-  return on;
+  static unsigned launches = 0;
+  static bool init = false;
+  if (on && !init) {
+    init = true;
+    static unsigned long long h[8 + 3 * 1024];
+    for (int k = 0; k < 8 + 3 * 1024; ++k) h[k] = (k >= 8 && (k - 8) % 3 == 0) ? ~0ull : 0ull;
+    FLOAM_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_fe_stamps), h, sizeof(h)));
+  }
+  return on ? (int)(launches++ % 1024u) + 1 : 0;   // per launch: its slot + 1
 }
 
 void fe_stamps_print() {
-  if (!fe_stamps_on()) return;
-  unsigned long long h[8];
+  if (!std::getenv("FLOAM_FE_STAMPS")) return;
+  static unsigned long long h[8 + 3 * 1024];
   FLOAM_HIP(hipDeviceSynchronize());
   FLOAM_HIP(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_fe_stamps), sizeof(h)));
   const double nb = h[4] ? (double)h[4] : 1.0;
+  double skew = 0.0, span = 0.0;
+  int nl = 0;
+  for (int k = 0; k < 1024; ++k) {
+    const unsigned long long* L = &h[8 + 3 * k];
+    if (L[2] == 0ull) continue;
+    skew += (double)(L[1] - L[0]);
+    span += (double)(L[2] - L[0]);
+    ++nl;
+  }
+  if (nl) std::fprintf(stderr, "[fe stamps] %d launches with work: first -> last block start %.2f us, first start -> "
+                       "last end %.2f us\n", nl, skew / nl / 100.0, span / nl / 100.0);
   std::fprintf(stderr, "[fe stamps] %llu sector blocks: staging %.2f us, curvature + sort %.2f us, greedy pick %.2f us, "
                "surf compaction %.2f us per block; longest block %.2f us\n", h[4], h[0] / nb / 100.0,
                h[1] / nb / 100.0, h[2] / nb / 100.0, h[3] / nb / 100.0, h[7] / 100.0);
@@ -520,15 +630,15 @@ void fe_launch(FeScratch& sc, const FeParams& prm, const PointRec* d_in, int n, 
   // the longest possible sector is (max ring size - 10) / 6 <= n / 6: the 4096 pass is only needed beyond 1024
   const bool big = n / 6 + 8 > 1024;
   if (big) {
-    hipLaunchKernelGGL((fe_sector<0, 1024, false>), dim3(6 * R), dim3(kSectorThreads), 0, st, sc.ring_count.p,
+    hipLaunchKernelGGL((fe_sector<0, 1024, false>), dim3(6 * R), dim3(kSortThreads), 0, st, sc.ring_count.p,
                        sc.ring_xyz.p, sc.sec_edge_cnt.p, sc.sec_edge_pos.p, sc.sec_surf_cnt.p, sc.surf_pos.p,
                        sc.status, fe_stamps_on());
     FLOAM_LAUNCH_CHECK();
-    hipLaunchKernelGGL((fe_sector<1024, 4096, true>), dim3(6 * R), dim3(kSectorThreads), 0, st, sc.ring_count.p,
+    hipLaunchKernelGGL((fe_sector<1024, 4096, true>), dim3(6 * R), dim3(kSortThreads), 0, st, sc.ring_count.p,
                        sc.ring_xyz.p, sc.sec_edge_cnt.p, sc.sec_edge_pos.p, sc.sec_surf_cnt.p, sc.surf_pos.p,
                        sc.status, fe_stamps_on());
   } else {
-    hipLaunchKernelGGL((fe_sector<0, 1024, true>), dim3(6 * R), dim3(kSectorThreads), 0, st, sc.ring_count.p,
+    hipLaunchKernelGGL((fe_sector<0, 1024, true>), dim3(6 * R), dim3(kSortThreads), 0, st, sc.ring_count.p,
                        sc.ring_xyz.p, sc.sec_edge_cnt.p, sc.sec_edge_pos.p, sc.sec_surf_cnt.p, sc.surf_pos.p,
                        sc.status, fe_stamps_on());
   }
