@@ -225,11 +225,11 @@ __device__ __forceinline__ void sector_sort(int m, Curv curvature, unsigned long
 // Sectors with MINSEC < m <= MAXSEC are processed; the small-LDS instantiation runs first and the large one only
 // picks up the (rare) longer sectors, so the common case keeps several workgroups per CU.
 template <int MINSEC, int MAXSEC, bool LAST>
-__global__ __launch_bounds__(kSortThreads) void fe_sector(const int* __restrict__ ring_count,
-                                                            const float4* __restrict__ ring_xyz,
-                                                            int* __restrict__ sec_edge_cnt, int* __restrict__ sec_edge_pos,
-                                                            int* __restrict__ sec_surf_cnt, int* __restrict__ surf_pos,
-                                                            int* __restrict__ status, int stamps) {
+__device__ __forceinline__ void fe_sector_body(int sec, const int* __restrict__ ring_count,
+                                               const float4* __restrict__ ring_xyz, int* __restrict__ sec_edge_cnt,
+                                               int* __restrict__ sec_edge_pos, int* __restrict__ sec_surf_cnt,
+                                               int* __restrict__ surf_pos, int* __restrict__ status, int stamps,
+                                               int* __restrict__ long_list, int* __restrict__ long_count) {
   const unsigned long long T0 = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
   constexpr int kPts = MAXSEC + 10;
   __shared__ unsigned long long s_key[MAXSEC];
@@ -241,8 +241,7 @@ __global__ __launch_bounds__(kSortThreads) void fe_sector(const int* __restrict_
   __shared__ int smem[33];
   __shared__ int s_off;
 
-  const int r = blockIdx.x / 6, s = blockIdx.x % 6;
-  const int sec = blockIdx.x;
+  const int r = sec / 6, s = sec % 6;
   const int n_r = ring_count[r];
   if (n_r < 131) {                                    // :89
     if (MINSEC == 0 && threadIdx.x == 0) { sec_edge_cnt[sec] = 0; sec_surf_cnt[sec] = 0; }
@@ -258,6 +257,7 @@ __global__ __launch_bounds__(kSortThreads) void fe_sector(const int* __restrict_
       sec_edge_cnt[sec] = 0;
       sec_surf_cnt[sec] = 0;
     }
+    if (!LAST && long_list && threadIdx.x == 0) long_list[atomicAdd(long_count, 1)] = sec;   // for fe_sector_long
     return;
   }
   const int off = ring_offset(ring_count, r, &s_off);
@@ -432,10 +432,40 @@ __global__ __launch_bounds__(kSortThreads) void fe_sector(const int* __restrict_
   }
 }
 
+// one sector per block; with long_list: a sector longer than MAXSEC is listed for fe_sector_long
+template <int MINSEC, int MAXSEC, bool LAST>
+__global__ __launch_bounds__(kSortThreads) void fe_sector(const int* __restrict__ ring_count,
+                                                          const float4* __restrict__ ring_xyz,
+                                                          int* __restrict__ sec_edge_cnt, int* __restrict__ sec_edge_pos,
+                                                          int* __restrict__ sec_surf_cnt, int* __restrict__ surf_pos,
+                                                          int* __restrict__ status, int stamps,
+                                                          int* __restrict__ long_list, int* __restrict__ long_count) {
+  fe_sector_body<MINSEC, MAXSEC, LAST>((int)blockIdx.x, ring_count, ring_xyz, sec_edge_cnt, sec_edge_pos, sec_surf_cnt,
+                                       surf_pos, status, stamps, long_list, long_count);
+}
+
+// the listed long sectors (1024 < m <= 4096; longer: FE_STATUS_SECTOR_TOO_LONG), a few blocks looping over the list
+// (a grid of one block per sector would cost a launch of 6 R blocks that nearly all find nothing to do)
+__global__ __launch_bounds__(kSortThreads) void fe_sector_long(const int* __restrict__ ring_count,
+                                                               const float4* __restrict__ ring_xyz,
+                                                               int* __restrict__ sec_edge_cnt,
+                                                               int* __restrict__ sec_edge_pos,
+                                                               int* __restrict__ sec_surf_cnt,
+                                                               int* __restrict__ surf_pos, int* __restrict__ status,
+                                                               const int* __restrict__ long_list,
+                                                               const int* __restrict__ long_count) {
+  const int nl = *long_count;
+  for (int j = blockIdx.x; j < nl; j += gridDim.x) {
+    fe_sector_body<1024, 4096, true>(long_list[j], ring_count, ring_xyz, sec_edge_cnt, sec_edge_pos, sec_surf_cnt,
+                                     surf_pos, status, 0, nullptr, nullptr);
+    __syncthreads();   // (the body's LDS is reused by the next listed sector)
+  }
+}
+
 // Advances the output counts, publishes (edge count, surf count, status) for one D2H copy and re-zeroes the
 // per-call counters for the next call (so no memset nodes are needed).  Run by the last block of fe_output to
 // arrive (every other block has read the counts and ring sizes it needs), not as a launch of its own.
-__device__ __forceinline__ void fe_commit_block(int n_sectors, const int* __restrict__ sec_edge_cnt, const int* __restrict__ sec_surf_cnt,
+__device__ __forceinline__ void fe_commit_block(int* __restrict__ long_count, int n_sectors, const int* __restrict__ sec_edge_cnt, const int* __restrict__ sec_surf_cnt,
                           int* __restrict__ edge_count, int* __restrict__ surf_count, int* __restrict__ ring_count,
                           int num_lines, int* __restrict__ status, int* __restrict__ out3,
                           int* __restrict__ stat_edge, int* __restrict__ stat_surf, unsigned* __restrict__ radix_ctl,
@@ -471,6 +501,7 @@ __device__ __forceinline__ void fe_commit_block(int n_sectors, const int* __rest
     *status = 0;
   }
   for (int r = threadIdx.x; r < num_lines; r += blockDim.x) ring_count[r] = 0;
+  if (threadIdx.x == 0) *long_count = 0;   // fe_sector's long-sector list, for the next call
 }
 
 __global__ __launch_bounds__(kSectorThreads) void fe_output(const PointRec* __restrict__ ring_pts,
@@ -485,7 +516,7 @@ __global__ __launch_bounds__(kSectorThreads) void fe_output(const PointRec* __re
                                                             int* __restrict__ status, int* __restrict__ out3,
                                                             int* __restrict__ stat_edge, int* __restrict__ stat_surf,
                                                             unsigned* __restrict__ radix_ctl,
-                                                            unsigned* __restrict__ ticket) {
+                                                            unsigned* __restrict__ ticket, int* __restrict__ long_count) {
   __shared__ int red[2][kSectorThreads / 64];
   __shared__ int s_off;
   const int sec = blockIdx.x;
@@ -525,7 +556,7 @@ __global__ __launch_bounds__(kSectorThreads) void fe_output(const PointRec* __re
   if (threadIdx.x == 0) s_last = atomicAdd(ticket, 1u) == gridDim.x - 1;
   __syncthreads();
   if (!s_last) return;
-  fe_commit_block((int)gridDim.x, sec_edge_cnt, sec_surf_cnt, edge_count, surf_count, ring_count_w, num_lines, status,
+  fe_commit_block(long_count, (int)gridDim.x, sec_edge_cnt, sec_surf_cnt, edge_count, surf_count, ring_count_w, num_lines, status,
                   out3, stat_edge, stat_surf, radix_ctl, clear);
   if (threadIdx.x == 0) *ticket = 0u;
 }
@@ -599,6 +630,11 @@ void fe_launch(FeScratch& sc, const FeParams& prm, const PointRec* d_in, int n, 
     sc.ticket.reserve(1);
     FLOAM_HIP(hipMemsetAsync(sc.ticket.p, 0, sizeof(unsigned), st));   // (reset by the last block of every call)
   }
+  if (sc.long_sec.cap < (size_t)(6 * R + 1)) {   // [0] count (reset by the commit), [1..] long sectors
+    sc.long_sec.release();
+    sc.long_sec.reserve(6 * R + 1);
+    FLOAM_HIP(hipMemsetAsync(sc.long_sec.p, 0, sizeof(int), st));
+  }
   if (!sc.zeroed || sc.zeroed_lines < R) {   // the commit re-zeroes the counters at the end of every call
     FLOAM_HIP(hipMemsetAsync(sc.ring_count.p, 0, sizeof(int) * sc.ring_count.cap, st));
     FLOAM_HIP(hipMemsetAsync(sc.status, 0, sizeof(int), st));
@@ -629,24 +665,24 @@ void fe_launch(FeScratch& sc, const FeParams& prm, const PointRec* d_in, int n, 
   }
   // the longest possible sector is (max ring size - 10) / 6 <= n / 6: the 4096 pass is only needed beyond 1024
   const bool big = n / 6 + 8 > 1024;
-  if (big) {
+  if (big) {   // sectors beyond 1024 entries (rare) are listed by the first launch and run by a small second one
     hipLaunchKernelGGL((fe_sector<0, 1024, false>), dim3(6 * R), dim3(kSortThreads), 0, st, sc.ring_count.p,
                        sc.ring_xyz.p, sc.sec_edge_cnt.p, sc.sec_edge_pos.p, sc.sec_surf_cnt.p, sc.surf_pos.p,
-                       sc.status, fe_stamps_on());
+                       sc.status, fe_stamps_on(), sc.long_sec.p + 1, sc.long_sec.p + 0);
     FLOAM_LAUNCH_CHECK();
-    hipLaunchKernelGGL((fe_sector<1024, 4096, true>), dim3(6 * R), dim3(kSortThreads), 0, st, sc.ring_count.p,
-                       sc.ring_xyz.p, sc.sec_edge_cnt.p, sc.sec_edge_pos.p, sc.sec_surf_cnt.p, sc.surf_pos.p,
-                       sc.status, fe_stamps_on());
+    hipLaunchKernelGGL(fe_sector_long, dim3(16), dim3(kSortThreads), 0, st, sc.ring_count.p, sc.ring_xyz.p,
+                       sc.sec_edge_cnt.p, sc.sec_edge_pos.p, sc.sec_surf_cnt.p, sc.surf_pos.p, sc.status,
+                       sc.long_sec.p + 1, sc.long_sec.p + 0);
   } else {
     hipLaunchKernelGGL((fe_sector<0, 1024, true>), dim3(6 * R), dim3(kSortThreads), 0, st, sc.ring_count.p,
                        sc.ring_xyz.p, sc.sec_edge_cnt.p, sc.sec_edge_pos.p, sc.sec_surf_cnt.p, sc.surf_pos.p,
-                       sc.status, fe_stamps_on());
+                       sc.status, fe_stamps_on(), nullptr, nullptr);
   }
   FLOAM_LAUNCH_CHECK();
   hipLaunchKernelGGL(fe_output, dim3(6 * R), dim3(kSectorThreads), 0, st, sc.ring_pts.p, sc.ring_count.p,
                      sc.sec_edge_cnt.p, sc.sec_edge_pos.p, sc.sec_surf_cnt.p, sc.surf_pos.p, edge_out, edge_count,
                      surf_out, surf_count, clear, sc.ring_count.p, R, sc.status, sc.out3.p, stat_edge, stat_surf,
-                     sc.rs.ctl.p, sc.ticket.p);
+                     sc.rs.ctl.p, sc.ticket.p, sc.long_sec.p + 0);
   FLOAM_LAUNCH_CHECK();
 
 }

@@ -21,6 +21,7 @@ struct FeScratch {
   DevBuf<PointRec> ring_pts;
   DevBuf<int> out3;        // edge count, surf count, status after the call (one D2H)
   DevBuf<unsigned> ticket; // fe_output's arrival counter (its last block commits)
+  DevBuf<int> long_sec;    // [0] count, [1..] sectors longer than 1024 entries (fe_sector -> fe_sector_long)
   int* status = nullptr;   // device int, owned by the caller
   bool zeroed = false;
   int zeroed_lines = 0;

@@ -82,6 +82,35 @@ def test_feature_extraction_edge_cases(floam_gpu, oracle_lib):
     assert len(de2) == 0 and len(ds2) == 0
 
 
+def test_feature_extraction_long_sectors(floam_gpu, oracle_lib):
+    """Sectors of more than 1024 entries take fe_sector's second path (listed by the first launch, run by
+    fe_sector_long): ring 0 seven times as dense (~1190-entry sectors) stays byte-identical to the oracle; a ring
+    whose sectors exceed 4096 entries is refused (FLOAM_ERR_UNSUPPORTED) rather than truncated."""
+    raw = synth.generate_scan("c1", 1)
+    r0 = raw[raw["ring"] == 0]
+    rng = np.random.default_rng(5)
+
+    def copies(k):
+        out = []
+        for _ in range(k):
+            c = r0.copy()
+            for f in ("x", "y", "z"):
+                c[f] = (c[f] + rng.normal(0.0, 2e-3, len(c))).astype(np.float32)
+            out.append(c)
+        return out
+
+    dense = np.concatenate([raw] + copies(6))
+    assert (len(r0) * 7 - 10) // 6 > 1024
+    e_ref, s_ref, _ = oracle_lib.feature_extraction(dense, 16, 0.5, 90.0, canonical=True)
+    e, s, _ = _gpu_fe(floam_gpu, dense, 16)
+    _assert_same_cloud(e, e_ref, "edge")
+    _assert_same_cloud(s, s_ref, "surf")
+    huge = np.concatenate([raw] + copies(24))   # sectors of ~4260 entries
+    assert (len(r0) * 25 - 10) // 6 > 4096
+    with pytest.raises(floam_gpu.FloamError):
+        _gpu_fe(floam_gpu, huge, 16)
+
+
 def _angle_between(q1, q2):
     d = abs(float(np.dot(q1, q2)))
     return 2.0 * math.acos(min(1.0, d))
