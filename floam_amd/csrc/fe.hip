@@ -14,6 +14,8 @@
 // Arithmetic follows the reference bit for bit: float stencil sums in source order, double squares, no FMA
 // contraction (built with -ffp-contract=off).  Sorting is by (value, ring index), which equals the reference's
 // unstable std::sort whenever a sector has no tied curvature values (SURVEY.md §7 "Hard parts").
+#include <vector>
+
 #include "floam_common.hpp"
 #include "fe.hpp"
 #include "radix.hpp"
@@ -23,6 +25,7 @@ namespace floam {
 // FLOAM_FE_STAMPS=1 (diagnostic): fe_sector's per-block phase times (100 MHz ticks): [0] staging, [1] curvature +
 // sort, [2] greedy pick, [3] surf compaction + writes, [4] blocks, [5] sum of launch spans, [6] launches
 __device__ unsigned long long g_fe_stamps[8 + 3 * 1024];   // + per launch: first start, last start, last end
+__device__ unsigned g_fe_sec[1024][12];   // per sector, the last launch: m, phases (10-ns ticks), start vs first
 
 namespace {
 
@@ -404,20 +407,26 @@ __device__ __forceinline__ void fe_sector_body(int sec, const int* __restrict__ 
   int c = 0;
   for (int i = i0; i < i1; ++i) c += !s_picked[s_id[i] + 5];
   int total;
+  const unsigned long long T3a = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
   int pos = block_exclusive_scan_1024(c, smem, &total);
+  const unsigned long long T3b = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
   for (int i = i0; i < i1; ++i) {
     const int ind = s_id[i] + 5;
     if (!s_picked[ind]) surf_pos[off + a + pos++] = off + a + ind;
   }
+  const unsigned long long T3c = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
   if (threadIdx.x == 0) {
     sec_edge_cnt[sec] = nedge;
     sec_surf_cnt[sec] = total;
   }
   if (stamps) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned long long T3d = __builtin_amdgcn_s_memrealtime();
     __syncthreads();
+    const unsigned long long T3e = __builtin_amdgcn_s_memrealtime();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (threadIdx.x == 0) {
       const unsigned long long T4 = __builtin_amdgcn_s_memrealtime();
+      if (sec < 1024) g_fe_sec[sec][11] = (unsigned)(((T3e - T3d) & 0xFFFF) | ((T4 - T3e) << 16));
       atomicAdd(&g_fe_stamps[0], T1 - T0);
       atomicAdd(&g_fe_stamps[1], T2 - T1);
       atomicAdd(&g_fe_stamps[2], T3 - T2);
@@ -428,6 +437,13 @@ __device__ __forceinline__ void fe_sector_body(int sec, const int* __restrict__ 
       atomicMin(&L[0], T0);
       atomicMax(&L[1], T0);
       atomicMax(&L[2], T4);
+      if (sec < 1024) {
+        unsigned* q = g_fe_sec[sec];
+        q[0] = (unsigned)m; q[1] = (unsigned)(T1 - T0); q[2] = (unsigned)(T2 - T1); q[3] = (unsigned)(T3 - T2);
+        q[4] = (unsigned)(T4 - T3); q[5] = (unsigned)(T0 & 0xFFFFFFFFu); q[6] = (unsigned)r;
+        q[7] = (unsigned)(((T3a - T3) & 0x3FF) | (((T3b - T3a) & 0x3FF) << 10) | (((T3c - T3b) & 0x3FF) << 20));
+        q[8] = (unsigned)nedge; q[9] = (unsigned)total; q[10] = (unsigned)(off + a);
+      }
     }
   }
 }
@@ -603,6 +619,30 @@ void fe_stamps_print() {
   }
   if (nl) std::fprintf(stderr, "[fe stamps] %d launches with work: first -> last block start %.2f us, first start -> "
                        "last end %.2f us\n", nl, skew / nl / 100.0, span / nl / 100.0);
+  {
+    static unsigned q[1024][12];
+    FLOAM_HIP(hipMemcpyFromSymbol(q, HIP_SYMBOL(g_fe_sec), sizeof(q)));
+    unsigned t0 = ~0u;
+    for (int k = 0; k < 1024; ++k)
+      if (q[k][0]) t0 = std::min(t0, q[k][5]);
+    std::vector<std::pair<unsigned, int>> d;
+    for (int k = 0; k < 1024; ++k)
+      if (q[k][0]) d.push_back({q[k][1] + q[k][2] + q[k][3] + q[k][4], k});
+    std::sort(d.begin(), d.end());
+    const int nd = (int)d.size();
+    for (int j = 0; j < nd; ++j) {
+      if (j >= 6 && j < nd - 10) continue;   // the fastest and the slowest blocks of the last launch
+      const unsigned* x = q[d[j].second];
+      std::fprintf(stderr, "[fe sector %3d ring %2u] m %4u start +%.2f us: staging %.2f sort %.2f pick %.2f "
+                   "compaction %.2f us (count %.2f, scan %.2f, writes %.2f, drain %.2f: barrier %.2f, stores %.2f) edges %u surf %u "
+                   "at %u\n",
+                   d[j].second, x[6], x[0],
+                   (x[5] - t0) / 100.0, x[1] / 100.0, x[2] / 100.0, x[3] / 100.0, x[4] / 100.0,
+                   (x[7] & 0x3FF) / 100.0, ((x[7] >> 10) & 0x3FF) / 100.0, ((x[7] >> 20) & 0x3FF) / 100.0,
+                   (x[4] - (x[7] & 0x3FF) - ((x[7] >> 10) & 0x3FF) - ((x[7] >> 20) & 0x3FF)) / 100.0,
+                   (x[11] & 0xFFFF) / 100.0, (x[11] >> 16) / 100.0, x[8], x[9], x[10]);
+    }
+  }
   std::fprintf(stderr, "[fe stamps] %llu sector blocks: staging %.2f us, curvature + sort %.2f us, greedy pick %.2f us, "
                "surf compaction %.2f us per block; longest block %.2f us\n", h[4], h[0] / nb / 100.0,
                h[1] / nb / 100.0, h[2] / nb / 100.0, h[3] / nb / 100.0, h[7] / 100.0);
