@@ -637,107 +637,6 @@ __device__ __forceinline__ void stencil_scan(const CorrArgs& A, int x0, int x1, 
   wave_lds_order();   // the group's LDS slot is rewritten by its next scan
 }
 
-// Stage 2 as the SHELL around stage 1's block: the fine cells (edge 0.5 m) qx - 2 .. qx + 2 per axis hold every
-// point within 1 m of a query in fine cell (qx, qy, qz) (floor(2 (q - 1)) >= qx - 2 and floor(2 (q + 1)) <= qx + 2,
-// exact in double), and the inner 3 x 3 x 3 of them were scanned completely by stage 1, so stage 2 scans the other 98
-// (12.25 m^3 instead of the 27 m^3 of the 3 x 3 x 3 coarse cells around q) and continues stage 1's top-5 and count.
-// The 125 cells lie in exactly 3 x 3 x 3 coarse cells, probed by the lanes (start + the 8 sub-cell counts each) into
-// LDS; every fine cell's range is its coarse start + the counts of the sub-cells before it (inner cells: empty).
-constexpr int kShell = 125;
-constexpr int kShellCoarse = 27;
-template <int G, int U>
-__device__ __forceinline__ void shell_scan(const CorrArgs& A, int qx, int qy, int qz, float wx, float wy, float wz,
-                                           int lane, int* __restrict__ s_pre, int* __restrict__ s_start,
-                                           int* __restrict__ s_cc, Top5& t, int& cnt) {
-  const int cx0 = (qx - 2) >> 1, cy0 = (qy - 2) >> 1, cz0 = (qz - 2) >> 1;   // floor division by 2
-#pragma unroll 1
-  for (int ci = lane; ci < kShellCoarse; ci += G) {   // (27 probes over the group's lanes)
-    const unsigned long long key = cell_key(cx0 + ci % 3, cy0 + (ci / 3) % 3, cz0 + ci / 9);
-    unsigned slot = hash_slot64(key, A.bits);
-    const int4* e = reinterpret_cast<const int4*>(&A.coarse[slot]);
-    int4 h = e[0], s0 = e[1], s1 = e[2];
-    unsigned long long k = ((unsigned long long)(unsigned)h.y << 32) | (unsigned)h.x;
-    while (k != key && k != kEmptyKey) {   // collision chain (rare)
-      slot = (slot + 1) & A.mask;
-      e = reinterpret_cast<const int4*>(&A.coarse[slot]);
-      h = e[0];
-      s0 = e[1];
-      s1 = e[2];
-      k = ((unsigned long long)(unsigned)h.y << 32) | (unsigned)h.x;
-    }
-    const bool hit = k == key;
-    int* cc = s_cc + 9 * ci;
-    cc[0] = hit ? h.z : 0;
-    cc[1] = hit ? s0.x : 0; cc[2] = hit ? s0.y : 0; cc[3] = hit ? s0.z : 0; cc[4] = hit ? s0.w : 0;
-    cc[5] = hit ? s1.x : 0; cc[6] = hit ? s1.y : 0; cc[7] = hit ? s1.z : 0; cc[8] = hit ? s1.w : 0;
-  }
-  wave_lds_order();
-  constexpr int P = (kShell + G - 1) / G;   // fine cells per lane
-  const int cb = min(kShell, lane * P), ce = min(kShell, cb + P);
-  int local = 0;
-#pragma unroll 1
-  for (int j = 0; j < P; ++j) {
-    const int c = cb + j;
-    if (c < ce) {
-      const int ox = c % 5, oy = (c / 5) % 5, oz = c / 25;
-      const int fx = qx - 2 + ox, fy = qy - 2 + oy, fz = qz - 2 + oz;
-      const int ci = ((fx >> 1) - cx0) + 3 * ((fy >> 1) - cy0) + 9 * ((fz >> 1) - cz0);
-      const int sub = (fx & 1) | ((fy & 1) << 1) | ((fz & 1) << 2);
-      const int* cc = s_cc + 9 * ci;
-      int start = cc[0];
-#pragma unroll
-      for (int k = 0; k < 8; ++k)
-        if (k < sub) start += cc[1 + k];
-      const bool inner = ox >= 1 && ox <= 3 && oy >= 1 && oy <= 3 && oz >= 1 && oz <= 3;
-      s_start[c] = start;
-      s_pre[c] = local;
-      local += inner ? 0 : cc[1 + sub];
-    }
-  }
-  const int incl = group_incl_scan<G>(local, lane);
-  const int excl = incl - local;
-#pragma unroll 1
-  for (int j = 0; j < P; ++j)
-    if (cb + j < ce) s_pre[cb + j] += excl;
-  const int tot = __shfl(incl, G - 1, G);
-  if (lane == G - 1) s_pre[kShell] = incl;
-  wave_lds_order();
-  int c = 0, c_lo = 0, c_hi = s_pre[1], c_start = s_start[0];   // cursor: cell c = [c_lo, c_hi)
-  for (int tb = 0; tb < tot; tb += G * U) {
-    float4 m[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int tt = tb + u * G + lane;
-      if (tt < tot) {
-        while (tt >= c_hi) {
-          ++c;
-          c_lo = c_hi;
-          c_hi = s_pre[c + 1];
-          c_start = s_start[c];
-        }
-        m[u] = A.gpts[c_start + (tt - c_lo)];
-      } else {
-        m[u] = make_float4(1e30f, 1e30f, 1e30f, 0.0f);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      float dd = 0.0f;   // flann::L2_Simple<float>: ((0 + dx*dx) + dy*dy) + dz*dz
-      float df = wx - m[u].x;
-      dd += df * df;
-      df = wy - m[u].y;
-      dd += df * df;
-      df = wz - m[u].z;
-      dd += df * df;
-      if (dd < 1.0f) {
-        ++cnt;
-        top5_insert(t, ((unsigned long long)__float_as_uint(dd) << 32) | (unsigned)__float_as_int(m[u].w));
-      }
-    }
-  }
-  wave_lds_order();   // the group's LDS slot is rewritten by its next scan
-}
-
 // group-wide top-5 (every lane ends with the merged list) and count
 template <int G>
 __device__ __forceinline__ void group_merge(Top5& t, int& cnt) {
@@ -799,13 +698,14 @@ __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArg
                                   fminf(wy - 0.5f * (float)(qy - 1), 0.5f * (float)(qy + 2) - wy)),
                             fminf(wz - 0.5f * (float)(qz - 1), 0.5f * (float)(qz + 2) - wz));
       const bool complete = cnt >= 5 && __uint_as_float((unsigned)(t.k[4] >> 32)) < b * b;
-      if (!complete) {   // the shell of fine cells around the block: together every cell within 1 m
-        if (lane != 0) {   // stage 1's merged top-5 and count continue in lane 0 only
+      if (!complete) {   // coarse cells floor(q - 1) .. floor(q + 1) per axis (exact in double)
 #pragma unroll
-          for (int k = 0; k < 5; ++k) t.k[k] = ~0ull;
-          cnt = 0;
-        }
-        shell_scan<G, U>(A, qx, qy, qz, wx, wy, wz, lane, s_pre, s_start, s_cc, t, cnt);
+        for (int k = 0; k < 5; ++k) t.k[k] = ~0ull;
+        cnt = 0;
+        stencil_scan<G, U, true>(A, (int)floor((double)wx - 1.0), (int)floor((double)wx + 1.0),
+                                 (int)floor((double)wy - 1.0), (int)floor((double)wy + 1.0),
+                                 (int)floor((double)wz - 1.0), (int)floor((double)wz + 1.0), wx, wy, wz, lane, s_pre,
+                                 s_start, t, cnt);
         group_merge<G>(t, cnt);
         flags |= 2;
       }
@@ -839,9 +739,9 @@ __global__ __launch_bounds__(kTB, W) void knn_kernel(LMState* __restrict__ st, c
                                                   CorrArgs E, CorrArgs S, int nbE,
                                                   const int* __restrict__ d_me, const int* __restrict__ d_ms,
                                                   int rank, int world) {
-  __shared__ int s_pre[kTB / G][kShell + 1];   // (stage 1 uses the first kMaxStencil + 1 of each group's rows)
-  __shared__ int s_start[kTB / G][kShell];
-  __shared__ int s_cc[kTB / G][kShellCoarse * 9];
+  __shared__ int s_pre[kTB / G][kMaxStencil + 1];
+  __shared__ int s_start[kTB / G][kMaxStencil];
+  __shared__ int s_cc[kTB / G][8 * 9];
   const int lane = threadIdx.x & (G - 1);
   const int g = threadIdx.x / G;
   double pose[7];   // wave-uniform: kept in SGPRs (readfirstlane), not in 14 VGPRs of every lane
@@ -1072,17 +972,21 @@ __global__ __launch_bounds__(kTB) void knn_traffic(const LMState* __restrict__ s
   // the search kernel's own bytes: query (16 B) + flag (1 B) + the neighbours' coordinates it hands to the
   // geometry pass (5 x 12 B, for the queries with 5 neighbours: bit 2 after the geometry pass)
   unsigned long long bytes = level ? 0ull : 16ull + 1ull + ((f & 4) ? 60ull : 0ull);
-  // level 0: the 3 x 3 x 3 fine block around the query's fine cell; level 1 (stage-2 queries): the shell of fine
-  // cells around it out to +-2 (shell_scan)
-  int qx, qy, qz;
-  fine_cell(wx, wy, wz, qx, qy, qz);
-  const int r = level ? 2 : 1;
-  for (int z = qz - r; z <= qz + r; ++z)
-    for (int y = qy - r; y <= qy + r; ++y)
-      for (int x = qx - r; x <= qx + r; ++x) {
-        if (level && abs(x - qx) <= 1 && abs(y - qy) <= 1 && abs(z - qz) <= 1) continue;   // (stage 1's block)
+  int x0, y0, z0, x1, y1, z1;
+  if (level) {
+    x0 = (int)floor((double)wx - 1.0); x1 = (int)floor((double)wx + 1.0);
+    y0 = (int)floor((double)wy - 1.0); y1 = (int)floor((double)wy + 1.0);
+    z0 = (int)floor((double)wz - 1.0); z1 = (int)floor((double)wz + 1.0);
+  } else {
+    fine_cell(wx, wy, wz, x0, y0, z0);
+    --x0; --y0; --z0;
+    x1 = x0 + 2; y1 = y0 + 2; z1 = z0 + 2;
+  }
+  for (int z = z0; z <= z1; ++z)
+    for (int y = y0; y <= y1; ++y)
+      for (int x = x0; x <= x1; ++x) {
         const unsigned long long k = cell_key(x, y, z);
-        const int cnt = fine_count(A, x, y, z);
+        const int cnt = level ? grid_lookup(A.coarse, k, A.bits, A.mask).y : fine_count(A, x, y, z);
         if (cnt == 0) continue;
         unsigned h = hash_slot64(k, set_bits);
         for (;;) {
@@ -1393,7 +1297,7 @@ void knn_traffic_launch(const LMState* d_st, const QuerySet& q, const Grid& g, C
                         DevBuf<unsigned long long>& set, unsigned long long* d_bytes, hipStream_t st) {
   if (q.n_ub <= 0) return;
   int bits = 10;
-  while ((1 << bits) < 256 * q.n_ub) ++bits;   // distinct occupied cells scanned (<= 98 per query)
+  while ((1 << bits) < 64 * q.n_ub) ++bits;   // distinct occupied cells scanned (<= 27 per query)
   set.reserve((size_t)1 << bits);
   CorrArgs A, B;
   corr_args(q, g, c, q, g, c, A, B);
