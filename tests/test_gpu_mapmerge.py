@@ -77,3 +77,13 @@ def test_merge_after_skipped_keyframe(floam_gpu, monkeypatch):
     runs = {v: _run(floam_gpu, monkeypatch, v, "c1", 7, repeat=(4,)) for v in ("merge", "voxelgrid")}
     assert not all(r[3] for r in runs["merge"]), "every update was a keyframe: the copy path never ran"
     _same(runs["merge"], runs["voxelgrid"], "c1 with a repeated scan")
+
+
+def test_merge_long_sequence(floam_gpu, monkeypatch, prefilled_map):
+    """20 C2 updates from the prefilled map: every map after every update byte-identical to the whole-map VoxelGrid's
+    (the merge's order invariant checked on the device all along; a violation would take the full sort, which is
+    also exact)."""
+    prefill = prefilled_map("c2")
+    runs = {v: _run(floam_gpu, monkeypatch, v, "c2", 20, prefill) for v in ("merge", "voxelgrid")}
+    assert sum(r[3] for r in runs["merge"]) >= 10, "too few keyframes to exercise the merge"
+    _same(runs["merge"], runs["voxelgrid"], "c2 x 20 merge vs whole-map VoxelGrid")
