@@ -410,10 +410,15 @@ __device__ __forceinline__ void fe_sector_body(int sec, const int* __restrict__ 
   const unsigned long long T3a = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
   int pos = block_exclusive_scan_1024(c, smem, &total);
   const unsigned long long T3b = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  // the sector's surf positions are one contiguous range: staged in LDS (the curvature keys are free now), then
+  // written as whole lines
+  int* s_out = reinterpret_cast<int*>(s_key);
   for (int i = i0; i < i1; ++i) {
     const int ind = s_id[i] + 5;
-    if (!s_picked[ind]) surf_pos[off + a + pos++] = off + a + ind;
+    if (!s_picked[ind]) s_out[pos++] = off + a + ind;
   }
+  __syncthreads();
+  for (int k = threadIdx.x; k < total; k += blockDim.x) surf_pos[off + a + k] = s_out[k];
   const unsigned long long T3c = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
   if (threadIdx.x == 0) {
     sec_edge_cnt[sec] = nedge;
