@@ -239,6 +239,7 @@ __device__ __forceinline__ void fe_sector_body(int sec, const int* __restrict__ 
   __shared__ uint16_t s_id[MAXSEC];      // ring index - a - 5 (the curvature entry offset)
   __shared__ float s_x[kPts], s_y[kPts], s_z[kPts];
   __shared__ uint8_t s_picked[kPts];
+  __shared__ unsigned s_gapw[(kPts + 63) / 64 * 2];   // bit j: points j and j + 1 farther apart than 0.05 (sq.)
   __shared__ int s_edges[kMaxEdgesPerSector];
   __shared__ int s_nedge;
   __shared__ int smem[33];
@@ -273,6 +274,23 @@ __device__ __forceinline__ void fe_sector_body(int sec, const int* __restrict__ 
   }
   __syncthreads();
   const unsigned long long T1 = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  // the reference's neighbour test (:151-166) between consecutive points, once per pair, as a bitmask: float
+  // differences, double squares (the left-side test of a pair computes the same numbers negated: the same result)
+  for (int j0 = (threadIdx.x & ~63); j0 < npts; j0 += blockDim.x) {   // (wave-uniform: a word pair per wave)
+    const int j = j0 + (threadIdx.x & 63);
+    bool gap = false;
+    if (j + 1 < npts) {
+      const double dX = s_x[j + 1] - s_x[j];
+      const double dY = s_y[j + 1] - s_y[j];
+      const double dZ = s_z[j + 1] - s_z[j];
+      gap = dX * dX + dY * dY + dZ * dZ > 0.05;
+    }
+    const unsigned long long b = __ballot(gap);
+    if ((threadIdx.x & 63) == 0) {
+      s_gapw[j0 >> 5] = (unsigned)b;
+      s_gapw[(j0 >> 5) + 1] = (unsigned)(b >> 32);
+    }
+  }
   // curvature (src/laserProcessingClass.cpp:95-101), entry e = a + k, point j = e + 5 -> local k + 5
   auto curvature = [&](int k) -> unsigned long long {
     const int c = k + 5;
@@ -337,8 +355,8 @@ __device__ __forceinline__ void fe_sector_body(int sec, const int* __restrict__ 
   // greedy edge pick (src/laserProcessingClass.cpp:129-170) by wave 0: the candidates in descending order, 64 at a
   // time (lane order = the reference's order).  Per chunk every lane reads whether its point was picked by an earlier
   // chunk; then, pick by pick, the first unsuppressed lane is the next candidate the reference examines (the ones
-  // before it are skipped as picked): its curvature ends the loop at <= 0.1, otherwise it is picked, lanes 1..10
-  // evaluate its +-5 neighbour gaps together (the same float differences and double squares as the reference), and
+  // before it are skipped as picked): its curvature ends the loop at <= 0.1, otherwise it is picked, its +-5
+  // neighbour runs come from the pair-gap bitmask (one broadcast LDS read, no arithmetic on the pick's chain), and
   // its picked run is marked in LDS and in the chunk's suppression mask.  One step per pick, not per candidate.
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
@@ -373,20 +391,14 @@ __device__ __forceinline__ void fe_sector_body(int sec, const int* __restrict__ 
         }
         if (lane == 0) s_edges[nedge] = il;
         ++nedge;
-        // neighbour gaps: lane k (1..5) between il + k and il + k - 1, lane 5 + k between il - k and il - k + 1
-        bool gap = false;
-        if (lane >= 1 && lane <= 10) {
-          const int k = lane <= 5 ? lane : -(lane - 5);
-          const int q0 = il + k, q1 = k > 0 ? il + k - 1 : il + k + 1;
-          const double dX = s_x[q0] - s_x[q1];
-          const double dY = s_y[q0] - s_y[q1];
-          const double dZ = s_z[q0] - s_z[q1];
-          gap = dX * dX + dY * dY + dZ * dZ > 0.05;
-        }
-        const unsigned long long g = __ballot(gap);
-        const unsigned long long gr = (g >> 1) & 0x1Full, gl = (g >> 6) & 0x1Full;
-        const int rr = gr ? __ffsll((long long)gr) - 1 : 5;   // neighbours marked to the right
-        const int ll = gl ? __ffsll((long long)gl) - 1 : 5;   // and to the left
+        // its suppression runs from the pair gaps: right, pairs (il + k - 1, il + k) = bits il .. il + 4; left, pairs
+        // (il - k, il - k + 1) = bits il - 1 down to il - 5
+        const int wb = (il - 5) >> 5;
+        const unsigned long long win = (unsigned long long)s_gapw[wb] | ((unsigned long long)s_gapw[wb + 1] << 32);
+        const unsigned bits10 = (unsigned)(win >> ((il - 5) & 31)) & 0x3FFu;   // bits il - 5 .. il + 4
+        const unsigned gr = bits10 >> 5, gl = bits10 & 0x1Fu;
+        const int rr = gr ? __builtin_ctz(gr) : 5;                 // neighbours marked to the right
+        const int ll = gl ? 4 - (31 - __builtin_clz(gl)) : 5;      // and to the left
         if (lane <= rr + ll) s_picked[il - ll + lane] = 1;
         supp = supp || (valid && ind >= il - ll && ind <= il + rr);
         pending &= ~((2ull << l) - 1ull);   // candidates up to l examined
@@ -432,16 +444,8 @@ __device__ __forceinline__ void fe_sector_body(int sec, const int* __restrict__ 
     if (threadIdx.x == 0) {
       const unsigned long long T4 = __builtin_amdgcn_s_memrealtime();
       if (sec < 1024) g_fe_sec[sec][11] = (unsigned)(((T3e - T3d) & 0xFFFF) | ((T4 - T3e) << 16));
-      atomicAdd(&g_fe_stamps[0], T1 - T0);
-      atomicAdd(&g_fe_stamps[1], T2 - T1);
-      atomicAdd(&g_fe_stamps[2], T3 - T2);
-      atomicAdd(&g_fe_stamps[3], T4 - T3);
-      atomicAdd(&g_fe_stamps[4], 1ull);
-      atomicMax(&g_fe_stamps[7], T4 - T0);   // the longest block
-      unsigned long long* L = &g_fe_stamps[8 + 3 * ((stamps - 1) % 1024)];
-      atomicMin(&L[0], T0);
-      atomicMax(&L[1], T0);
-      atomicMax(&L[2], T4);
+      // (plain per-sector records only: 384 blocks' atomics on a few shared words would queue behind one another
+      // and delay the stores being timed)
       if (sec < 1024) {
         unsigned* q = g_fe_sec[sec];
         q[0] = (unsigned)m; q[1] = (unsigned)(T1 - T0); q[2] = (unsigned)(T2 - T1); q[3] = (unsigned)(T3 - T2);
@@ -612,18 +616,6 @@ void fe_stamps_print() {
   static unsigned long long h[8 + 3 * 1024];
   FLOAM_HIP(hipDeviceSynchronize());
   FLOAM_HIP(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_fe_stamps), sizeof(h)));
-  const double nb = h[4] ? (double)h[4] : 1.0;
-  double skew = 0.0, span = 0.0;
-  int nl = 0;
-  for (int k = 0; k < 1024; ++k) {
-    const unsigned long long* L = &h[8 + 3 * k];
-    if (L[2] == 0ull) continue;
-    skew += (double)(L[1] - L[0]);
-    span += (double)(L[2] - L[0]);
-    ++nl;
-  }
-  if (nl) std::fprintf(stderr, "[fe stamps] %d launches with work: first -> last block start %.2f us, first start -> "
-                       "last end %.2f us\n", nl, skew / nl / 100.0, span / nl / 100.0);
   {
     static unsigned q[1024][12];
     FLOAM_HIP(hipMemcpyFromSymbol(q, HIP_SYMBOL(g_fe_sec), sizeof(q)));
@@ -631,10 +623,20 @@ void fe_stamps_print() {
     for (int k = 0; k < 1024; ++k)
       if (q[k][0]) t0 = std::min(t0, q[k][5]);
     std::vector<std::pair<unsigned, int>> d;
+    double ph[4] = {0, 0, 0, 0};
+    unsigned tend = 0;
     for (int k = 0; k < 1024; ++k)
-      if (q[k][0]) d.push_back({q[k][1] + q[k][2] + q[k][3] + q[k][4], k});
+      if (q[k][0]) {
+        d.push_back({q[k][1] + q[k][2] + q[k][3] + q[k][4], k});
+        for (int j = 0; j < 4; ++j) ph[j] += q[k][1 + j];
+        tend = std::max(tend, q[k][5] - t0 + q[k][1] + q[k][2] + q[k][3] + q[k][4]);
+      }
     std::sort(d.begin(), d.end());
     const int nd = (int)d.size();
+    if (nd)
+      std::fprintf(stderr, "[fe stamps] last launch, %d sector blocks: staging %.2f, curvature + sort %.2f, greedy "
+                   "pick %.2f, compaction %.2f us per block; first start -> last end %.2f us\n", nd,
+                   ph[0] / nd / 100.0, ph[1] / nd / 100.0, ph[2] / nd / 100.0, ph[3] / nd / 100.0, tend / 100.0);
     for (int j = 0; j < nd; ++j) {
       if (j >= 6 && j < nd - 10) continue;   // the fastest and the slowest blocks of the last launch
       const unsigned* x = q[d[j].second];
@@ -648,9 +650,6 @@ void fe_stamps_print() {
                    (x[11] & 0xFFFF) / 100.0, (x[11] >> 16) / 100.0, x[8], x[9], x[10]);
     }
   }
-  std::fprintf(stderr, "[fe stamps] %llu sector blocks: staging %.2f us, curvature + sort %.2f us, greedy pick %.2f us, "
-               "surf compaction %.2f us per block; longest block %.2f us\n", h[4], h[0] / nb / 100.0,
-               h[1] / nb / 100.0, h[2] / nb / 100.0, h[3] / nb / 100.0, h[7] / 100.0);
 }
 
 void fe_launch(FeScratch& sc, const FeParams& prm, const PointRec* d_in, int n, PointRec* edge_out,
