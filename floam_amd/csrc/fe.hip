@@ -356,8 +356,8 @@ __device__ __forceinline__ void fe_sector_body(int sec, const int* __restrict__ 
   // time (lane order = the reference's order).  Per chunk every lane reads whether its point was picked by an earlier
   // chunk; then, pick by pick, the first unsuppressed lane is the next candidate the reference examines (the ones
   // before it are skipped as picked): its curvature ends the loop at <= 0.1, otherwise it is picked, its +-5
-  // neighbour runs come from the pair-gap bitmask (one broadcast LDS read, no arithmetic on the pick's chain), and
-  // its picked run is marked in LDS and in the chunk's suppression mask.  One step per pick, not per candidate.
+  // neighbour runs (every lane's, from the pair-gap bitmask at the chunk's start: one read-lane on the pick's chain),
+  // and its picked run is marked in LDS and in the chunk's suppression mask.  One step per pick, not per candidate.
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
     int picked_num = 0, nedge = 0;
@@ -366,23 +366,33 @@ __device__ __forceinline__ void fe_sector_body(int sec, const int* __restrict__ 
       const int i = c0 - lane;
       const bool valid = i >= 0;
       int ind = 0;
-      double key = 0.0;
+      bool over = false;   // not curvature <= 0.1 (the reference's loop continues)
       if (valid) {
         ind = s_id[i] + 5;   // local point index
-        key = __longlong_as_double((long long)s_key[i]);
+        over = !(__longlong_as_double((long long)s_key[i]) <= 0.1);
       }
       bool supp = !valid || s_picked[ind];
+      // each lane's suppression run if its point is picked, from the pair-gap bitmask: right, pairs
+      // (ind + k - 1, ind + k) = bits ind .. ind + 4; left, pairs (ind - k, ind - k + 1) = bits ind - 1 down to ind - 5
+      int run = 0;   // ind | rr << 16 | ll << 20
+      if (valid) {
+        const int wb = (ind - 5) >> 5;
+        const unsigned long long win = (unsigned long long)s_gapw[wb] | ((unsigned long long)s_gapw[wb + 1] << 32);
+        const unsigned bits10 = (unsigned)(win >> ((ind - 5) & 31)) & 0x3FFu;   // bits ind - 5 .. ind + 4
+        const unsigned gr = bits10 >> 5, gl = bits10 & 0x1Fu;
+        const int rr = gr ? __builtin_ctz(gr) : 5;              // neighbours marked to the right
+        const int ll = gl ? 4 - (31 - __builtin_clz(gl)) : 5;   // and to the left
+        run = ind | rr << 16 | ll << 20;
+      }
+      const unsigned long long ends = __ballot(valid && !over);   // candidates that end the loop
       unsigned long long pending = __ballot(valid);
       for (;;) {
         const unsigned long long cand = __ballot(!supp) & pending;
         if (!cand) break;   // the rest of the chunk was picked: the next chunk
         const int l = __ffsll((long long)cand) - 1;
-        const unsigned long long kb = (unsigned long long)__double_as_longlong(key);
-        const double kl = __longlong_as_double((long long)(((unsigned long long)(unsigned)__builtin_amdgcn_readlane(
-                                                               (int)(kb >> 32), l) << 32) |
-                                                           (unsigned)__builtin_amdgcn_readlane((int)kb, l)));
-        const int il = __builtin_amdgcn_readlane(ind, l);
-        if (kl <= 0.1) { stop = true; break; }
+        if ((ends >> l) & 1ull) { stop = true; break; }
+        const int rl = __builtin_amdgcn_readlane(run, l);
+        const int il = rl & 0xFFFF;
         ++picked_num;
         if (picked_num > 20) {   // picked, not kept, and the loop ends
           if (lane == 0) s_picked[il] = 1;
@@ -391,14 +401,7 @@ __device__ __forceinline__ void fe_sector_body(int sec, const int* __restrict__ 
         }
         if (lane == 0) s_edges[nedge] = il;
         ++nedge;
-        // its suppression runs from the pair gaps: right, pairs (il + k - 1, il + k) = bits il .. il + 4; left, pairs
-        // (il - k, il - k + 1) = bits il - 1 down to il - 5
-        const int wb = (il - 5) >> 5;
-        const unsigned long long win = (unsigned long long)s_gapw[wb] | ((unsigned long long)s_gapw[wb + 1] << 32);
-        const unsigned bits10 = (unsigned)(win >> ((il - 5) & 31)) & 0x3FFu;   // bits il - 5 .. il + 4
-        const unsigned gr = bits10 >> 5, gl = bits10 & 0x1Fu;
-        const int rr = gr ? __builtin_ctz(gr) : 5;                 // neighbours marked to the right
-        const int ll = gl ? 4 - (31 - __builtin_clz(gl)) : 5;      // and to the left
+        const int rr = (rl >> 16) & 0xF, ll = rl >> 20;
         if (lane <= rr + ll) s_picked[il - ll + lane] = 1;
         supp = supp || (valid && ind >= il - ll && ind <= il + rr);
         pending &= ~((2ull << l) - 1ull);   // candidates up to l examined
