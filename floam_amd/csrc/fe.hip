@@ -148,80 +148,104 @@ __device__ __forceinline__ void sector_range(int n_r, int s, int& a, int& b) {
   b = (s == 5) ? T - 1 : L * (s + 1) - 1;
 }
 
-// ---- register bitonic sort of a sector's (curvature bits, entry) pairs: N = kSortThreads E entries, E per thread (position
-// p = E t + e), every stage's stride a compile-time constant, so a lane exchange inside a wave is one ds_swizzle
-// (xor of the lane bits, no memory) or, across the wave halves, one ds_bpermute; only strides >= 64 E go through LDS.
+// ---- register bitonic sort of a sector's entries by (curvature, entry): the network sorts one 32-bit word per entry,
+// the top 21 bits of the curvature's bit pattern above the 11-bit entry (unique words: a compare-exchange is one
+// min / max), N = kSortThreads E words, E per thread (position p = E t + e), every stage's stride a compile-time
+// constant, so a lane exchange inside a wave is one ds_swizzle (xor of the lane bits, no memory) or, across the wave
+// halves, one ds_bpermute; only strides >= 64 E go through LDS.  Entries whose prefixes tie are then re-ordered by
+// their full value (rare, short runs).
 template <int M>
 __device__ __forceinline__ unsigned xor_lane(unsigned v) {
   if constexpr (M < 32) return (unsigned)__builtin_amdgcn_ds_swizzle((int)v, (M << 10) | 0x1F);   // bitmask mode
   else return (unsigned)__builtin_amdgcn_ds_bpermute((int)((((threadIdx.x & 63) ^ M)) << 2), (int)v);
 }
-template <int M>
-__device__ __forceinline__ unsigned long long xor_lane64(unsigned long long v) {
-  return ((unsigned long long)xor_lane<M>((unsigned)(v >> 32)) << 32) | xor_lane<M>((unsigned)v);
-}
 
-// one stage (size, stride) of the network on the thread's E registers
+// one stage (size, stride) of the network on the thread's E words
 template <int E, int SIZE, int STRIDE>
-__device__ __forceinline__ void bitonic_stage(unsigned long long (&k)[E], unsigned (&id)[E],
-                                              unsigned long long* s_key, uint16_t* s_id) {
+__device__ __forceinline__ void bitonic_stage(unsigned (&k)[E], unsigned* s_pk) {
   const int t = threadIdx.x;
-  unsigned long long ok[E];
-  unsigned oi[E];
+  unsigned ok[E];
   if constexpr (STRIDE < E) {
 #pragma unroll
-    for (int e = 0; e < E; ++e) { ok[e] = k[e ^ STRIDE]; oi[e] = id[e ^ STRIDE]; }
+    for (int e = 0; e < E; ++e) ok[e] = k[e ^ STRIDE];
   } else if constexpr (STRIDE < 64 * E) {
 #pragma unroll
-    for (int e = 0; e < E; ++e) { ok[e] = xor_lane64<STRIDE / E>(k[e]); oi[e] = xor_lane<STRIDE / E>(id[e]); }
+    for (int e = 0; e < E; ++e) ok[e] = xor_lane<STRIDE / E>(k[e]);
   } else {
     __syncthreads();
 #pragma unroll
-    for (int e = 0; e < E; ++e) { s_key[E * t + e] = k[e]; s_id[E * t + e] = (uint16_t)id[e]; }
+    for (int e = 0; e < E; ++e) s_pk[E * t + e] = k[e];
     __syncthreads();
 #pragma unroll
-    for (int e = 0; e < E; ++e) { ok[e] = s_key[(E * t + e) ^ STRIDE]; oi[e] = s_id[(E * t + e) ^ STRIDE]; }
+    for (int e = 0; e < E; ++e) ok[e] = s_pk[(E * t + e) ^ STRIDE];
   }
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const int pp = E * t + e;
     const bool lower = (pp & STRIDE) == 0, asc = (pp & SIZE) == 0;
-    const bool other_less = ok[e] < k[e] || (ok[e] == k[e] && oi[e] < id[e]);
-    if (other_less == (asc == lower)) {   // the lower slot of an ascending pair keeps the smaller, and so on
-      k[e] = ok[e];
-      id[e] = oi[e];
-    }
+    // the lower slot of an ascending pair keeps the smaller, and so on
+    k[e] = asc == lower ? min(k[e], ok[e]) : max(k[e], ok[e]);
   }
 }
 template <int E, int SIZE, int STRIDE>
-__device__ __forceinline__ void bitonic_strides(unsigned long long (&k)[E], unsigned (&id)[E],
-                                                unsigned long long* s_key, uint16_t* s_id) {
-  bitonic_stage<E, SIZE, STRIDE>(k, id, s_key, s_id);
-  if constexpr (STRIDE > 1) bitonic_strides<E, SIZE, STRIDE / 2>(k, id, s_key, s_id);
+__device__ __forceinline__ void bitonic_strides(unsigned (&k)[E], unsigned* s_pk) {
+  bitonic_stage<E, SIZE, STRIDE>(k, s_pk);
+  if constexpr (STRIDE > 1) bitonic_strides<E, SIZE, STRIDE / 2>(k, s_pk);
 }
 template <int E, int SIZE>
-__device__ __forceinline__ void bitonic_sizes(unsigned long long (&k)[E], unsigned (&id)[E],
-                                              unsigned long long* s_key, uint16_t* s_id) {
-  bitonic_strides<E, SIZE, SIZE / 2>(k, id, s_key, s_id);
-  if constexpr (SIZE < kSortThreads * E) bitonic_sizes<E, SIZE * 2>(k, id, s_key, s_id);
+__device__ __forceinline__ void bitonic_sizes(unsigned (&k)[E], unsigned* s_pk) {
+  bitonic_strides<E, SIZE, SIZE / 2>(k, s_pk);
+  if constexpr (SIZE < kSortThreads * E) bitonic_sizes<E, SIZE * 2>(k, s_pk);
 }
-// the m curvature values (entries 0..m-1, padded with +inf keys) sorted ascending by (value, entry) into s_key/s_id
+// the m curvature values (entries 0..m-1 <= 1024): s_key[q] = the value of entry q, s_id = the entries in ascending
+// (value, entry) order
 template <int E, typename Curv>
-__device__ __forceinline__ void sector_sort(int m, Curv curvature, unsigned long long* s_key, uint16_t* s_id) {
-  unsigned long long k[E];
-  unsigned id[E];
+__device__ __forceinline__ void sector_sort(int m, Curv curvature, unsigned long long* s_key, uint16_t* s_id,
+                                            unsigned* s_pk) {
+  unsigned k[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const int q = E * threadIdx.x + e;
-    k[e] = q < m ? curvature(q) : ~0ull;
-    id[e] = q < m ? (unsigned)q : 0xFFFFu;
+    if (q < m) {
+      const unsigned long long v = curvature(q);   // v >= +0 (bit 63 clear): 21 bits below it
+      s_key[q] = v;
+      k[e] = (unsigned)(v >> 42) << 11 | (unsigned)q;   // < 0xFFFFFFFF: the padding sorts last
+    } else {
+      k[e] = ~0u;
+    }
   }
-  bitonic_sizes<E, 2>(k, id, s_key, s_id);
+  bitonic_sizes<E, 2>(k, s_pk);
   __syncthreads();
 #pragma unroll
+  for (int e = 0; e < E; ++e) s_pk[E * threadIdx.x + e] = k[e];
+  __syncthreads();
+  // a position that starts a prefix (its predecessor's differs) writes its entry; if its successors share the
+  // prefix, it orders that run by (value, entry) — insertion sort, a run of tied prefixes being short and rare
+#pragma unroll
   for (int e = 0; e < E; ++e) {
-    s_key[E * threadIdx.x + e] = k[e];
-    s_id[E * threadIdx.x + e] = (uint16_t)id[e];
+    const int p = E * threadIdx.x + e;
+    if (p >= m) continue;
+    const unsigned pre = k[e] >> 11;
+    if (p > 0 && (s_pk[p - 1] >> 11) == pre) continue;   // inside a run: its first position orders it
+    if (p + 1 < m && (s_pk[p + 1] >> 11) == pre) {
+      int end = p + 2;
+      while (end < m && (s_pk[end] >> 11) == pre) ++end;
+      for (int i = p; i < end; ++i) {
+        const int q = (int)(s_pk[i] & 0x7FFu);
+        const unsigned long long v = s_key[q];
+        int j = i;
+        while (j > p) {
+          const int qj = s_id[j - 1];
+          const unsigned long long vj = s_key[qj];
+          if (vj < v || (vj == v && qj < q)) break;
+          s_id[j] = (uint16_t)qj;
+          --j;
+        }
+        s_id[j] = (uint16_t)q;
+      }
+    } else {
+      s_id[p] = (uint16_t)(k[e] & 0x7FFu);
+    }
   }
 }
 
@@ -237,6 +261,7 @@ __device__ __forceinline__ void fe_sector_body(int sec, const int* __restrict__ 
   constexpr int kPts = MAXSEC + 10;
   __shared__ unsigned long long s_key[MAXSEC];
   __shared__ uint16_t s_id[MAXSEC];      // ring index - a - 5 (the curvature entry offset)
+  __shared__ unsigned s_pk[MAXSEC <= 1024 ? MAXSEC : 1];   // the register network's LDS exchanges
   __shared__ float s_x[kPts], s_y[kPts], s_z[kPts];
   __shared__ uint8_t s_picked[kPts];
   __shared__ unsigned s_gapw[(kPts + 63) / 64 * 2];   // bit j: points j and j + 1 farther apart than 0.05 (sq.)
@@ -304,11 +329,12 @@ __device__ __forceinline__ void fe_sector_body(int sec, const int* __restrict__ 
     const double v = dX * dX + dY * dY + dZ * dZ;
     return (unsigned long long)__double_as_longlong(v);   // v >= +0: the bit pattern is order-preserving
   };
-  if (MAXSEC <= 1024 && m <= 1024) {   // (block-uniform) the register network, E = 1, 2, 4 or 8 entries a thread
-    if (m <= kSortThreads) sector_sort<1>(m, curvature, s_key, s_id);
-    else if (m <= 2 * kSortThreads) sector_sort<2>(m, curvature, s_key, s_id);
-    else if (m <= 4 * kSortThreads) sector_sort<4>(m, curvature, s_key, s_id);
-    else sector_sort<8>(m, curvature, s_key, s_id);
+  // s_key by entry (the register network) or by sorted position (the LDS network)
+  const bool by_entry = MAXSEC <= 1024 && m <= 1024;
+  if (by_entry) {   // (block-uniform) the register network, E = 1, 2 or 4 entries a thread
+    if (m <= kSortThreads) sector_sort<1>(m, curvature, s_key, s_id, s_pk);
+    else if (m <= 2 * kSortThreads) sector_sort<2>(m, curvature, s_key, s_id, s_pk);
+    else sector_sort<4>(m, curvature, s_key, s_id, s_pk);
   } else {   // longer sectors (the 4096 instantiation): the network in LDS
     int P2 = 1;
     while (P2 < m) P2 <<= 1;
@@ -369,7 +395,7 @@ __device__ __forceinline__ void fe_sector_body(int sec, const int* __restrict__ 
       bool over = false;   // not curvature <= 0.1 (the reference's loop continues)
       if (valid) {
         ind = s_id[i] + 5;   // local point index
-        over = !(__longlong_as_double((long long)s_key[i]) <= 0.1);
+        over = !(__longlong_as_double((long long)s_key[by_entry ? ind - 5 : i]) <= 0.1);
       }
       bool supp = !valid || s_picked[ind];
       // each lane's suppression run if its point is picked, from the pair-gap bitmask: right, pairs
