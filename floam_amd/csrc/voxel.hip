@@ -24,6 +24,10 @@
 
 namespace floam {
 
+// FLOAM_VOX_STAMPS=1 (diagnostic): vox_compact's per-tile phase times of the last launch over >= 32 tiles (10-ns
+// ticks): [0] start (low bits), [1] keys staged, [2] points gathered + heads, [3] lookback done, [4] end (drained)
+__device__ unsigned g_vox_st[1024][5];
+
 namespace {
 constexpr int kTB = 256;
 constexpr int kMinMaxBlocks = kVoxMinMaxBlocks;   // partials per cloud
@@ -118,7 +122,8 @@ __global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B,
                                                    const int* __restrict__ vals, const int* __restrict__ overflow,
                                                    const int* __restrict__ n_dev, unsigned long long* __restrict__ status,
                                                    unsigned* __restrict__ ticket, const unsigned* __restrict__ radix_ctl,
-                                                   const int* __restrict__ gate, int n_cap) {
+                                                   const int* __restrict__ gate, int n_cap, int stamps) {
+  const unsigned long long T0 = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
   // the prologue's loads are issued together (one round trip instead of four in a row): the gate, the device
   // counts, and the tile's keys and values up to the host bound n_cap (allocated; entries past the device count are
   // masked below)
@@ -169,6 +174,7 @@ __global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B,
     if (k <= kTile + 1) s_key[k] = i < total ? kr[r] : 0xFFFFFFFFu;
   }
   __syncthreads();
+  const unsigned long long T1 = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
   // run tails of the tile as a bitmask: bit k set if element t0 + k is the last of its run
   __shared__ unsigned s_tail[kTile / 32];
   {
@@ -236,7 +242,13 @@ __global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B,
       if (k < w) wb[c] += s_w[c][k];
       agg[c] += s_w[c][k];
     }
+  unsigned long long T2 = 0ull;
+  if (stamps) {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    T2 = __builtin_amdgcn_s_memrealtime();
+  }
   const Prefix2 pre = lookback_prefix(status, tile, Prefix2{agg[0], agg[1]});
+  const unsigned long long T3 = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
   if (pre.a < 0) {   // lookback timed out (never expected): report through the output counts
     if (threadIdx.x == 0) { *A.d_out = -1; *B.d_out = -1; }
     return;
@@ -338,9 +350,50 @@ __global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B,
     *A.d_out = sort_failed ? -1 : pre.a + agg[0];
     *B.d_out = sort_failed ? -1 : pre.b + agg[1];
   }
+  if (stamps && ntiles >= 32 && tile < 1024) {   // plain per-tile records (no shared atomics: they would queue)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned long long T4 = __builtin_amdgcn_s_memrealtime();
+      unsigned* q = g_vox_st[tile];
+      q[0] = (unsigned)T0; q[1] = (unsigned)(T1 - T0); q[2] = (unsigned)(T2 - T1); q[3] = (unsigned)(T3 - T2);
+      q[4] = (unsigned)(T4 - T3);
+    }
+  }
 }
 
 }  // namespace
+
+static int vox_stamps_on() {
+  static const int on = std::getenv("FLOAM_VOX_STAMPS") ? 1 : 0;
+  return on;
+}
+
+void vox_stamps_print() {
+  if (!vox_stamps_on()) return;
+  static unsigned q[1024][5];
+  FLOAM_HIP(hipDeviceSynchronize());
+  FLOAM_HIP(hipMemcpyFromSymbol(q, HIP_SYMBOL(g_vox_st), sizeof(q)));
+  int nt = 0;
+  double ph[4] = {0, 0, 0, 0};
+  int smin = 0, emax = 0;   // relative to tile 0's start
+  for (int t = 0; t < 1024; ++t) {
+    if (q[t][1] == 0 && q[t][4] == 0) continue;
+    ++nt;
+    for (int k = 0; k < 4; ++k) ph[k] += q[t][1 + k];
+    const int st = (int)(q[t][0] - q[0][0]);
+    smin = std::min(smin, st);
+    emax = std::max(emax, st + (int)(q[t][1] + q[t][2] + q[t][3] + q[t][4]));
+  }
+  const int last_end = emax - smin;
+  if (!nt) return;
+  std::fprintf(stderr, "[vox stamps] last launch, %d tiles: keys staged %.2f, gather + heads %.2f, lookback %.2f, "
+               "sums + stores + drain %.2f us per tile; first start -> last end %.2f us\n", nt, ph[0] / nt / 100.0,
+               ph[1] / nt / 100.0, ph[2] / nt / 100.0, ph[3] / nt / 100.0, last_end / 100.0);
+  for (int t = 0; t < nt; t += std::max(1, nt / 8))
+    std::fprintf(stderr, "[vox tile %4d] start +%.2f: %.2f %.2f %.2f %.2f us\n", t, (int)(q[t][0] - q[0][0]) / 100.0,
+                 q[t][1] / 100.0, q[t][2] / 100.0, q[t][3] / 100.0, q[t][4] / 100.0);
+}
 
 VoxelJobDev to_dev(const VoxelJob& j, int base) {
   return VoxelJobDev{j.part0, j.d_n0, j.n0_ub, j.part1, j.d_n1, j.part1 ? j.n1_ub : 0, j.pose, 1.0f / j.leaf,
@@ -385,7 +438,7 @@ void voxel2_launch(VoxelScratch2& sc, const VoxelJob& a, const VoxelJob& b, hipS
   // sorted pairs in k0 / v0; the passes and the compaction work on the packed device count
   radix_sort_launch(sc.rs, sc.s.k0.p, sc.s.v0.p, sc.s.k1.p, sc.s.v1.p, n, st, gate, sc.overflow.p + 2);
   hipLaunchKernelGGL(vox_compact, dim3(ntiles), dim3(kTB), 0, st, A, B, sc.s.k0.p, sc.s.v0.p, sc.overflow.p,
-                     sc.overflow.p + 2, sc.status.p, sc.ticket.p, sc.rs.ctl.p, gate, n);
+                     sc.overflow.p + 2, sc.status.p, sc.ticket.p, sc.rs.ctl.p, gate, n, vox_stamps_on());
   FLOAM_LAUNCH_CHECK();
 }
 

@@ -210,6 +210,9 @@ struct VoxelScratch2 {
 // voxel count (-1 if the single-pass compaction failed, never expected).  gate (device int, nullable): when it reads
 // 0 the pipeline does nothing but copy each job's part0 to its output (a map update skipped on the device).
 // minmax_done: a producer kernel already ran the bounding-box stage with voxel2_prepare's VoxelFused (same jobs).
+// FLOAM_VOX_STAMPS=1: print vox_compact's in-kernel phase times (diagnostic; synchronises the device)
+void vox_stamps_print();
+
 void voxel2_launch(VoxelScratch2& sc, const VoxelJob& a, const VoxelJob& b, hipStream_t st,
                    const int* gate = nullptr, bool minmax_done = false);
 // reserves the scratch of a voxel2_launch of the same jobs and returns the producer's view of it
