@@ -133,15 +133,19 @@ __global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B,
   const int total_d = *n_dev;   // packed elements (vox_keys)
   const int nA0 = *A.d_n0, nA1 = A.d_n1 ? *A.d_n1 : 0, nB0 = *B.d_n0, nB1 = B.d_n1 ? *B.d_n1 : 0;
   const int ovf[2] = {overflow[0], overflow[1]};
-  // s_key[k] = key of element t0 - 1 + k, k in [0, kTile + 1]
-  __shared__ uint32_t s_key[kTile + 2];
-  uint32_t kr[(kTile + 2 + kTB - 1) / kTB];
+  // s_key[k] = key of element t0 - 1 + k, k in [0, kTile + 1 + kHalo]: the rounds of the prologue's key loads
+  // also cover kHalo elements past the tile (the continuation of a run that crosses the tile end, usually short)
+  constexpr int kRounds = (kTile + 2 + kTB - 1) / kTB;
+  constexpr int kHalo = kRounds * kTB - (kTile + 2);
+  __shared__ uint32_t s_key[kTile + 2 + kHalo];
+  uint32_t kr[kRounds];
 #pragma unroll
-  for (int r = 0; r < (kTile + 2 + kTB - 1) / kTB; ++r) {
+  for (int r = 0; r < kRounds; ++r) {
     const int k = r * kTB + threadIdx.x;
     const int i = t0 - 1 + k;
-    kr[r] = (k <= kTile + 1 && i >= 0 && i < n_cap) ? keys[i] : 0xFFFFFFFFu;
+    kr[r] = (i >= 0 && i < n_cap) ? keys[i] : 0xFFFFFFFFu;
   }
+  const int vh = threadIdx.x < kHalo && t0 + kTile + (int)threadIdx.x < n_cap ? vals[t0 + kTile + threadIdx.x] : 0;
   const int4* __restrict__ vals4 = reinterpret_cast<const int4*>(vals);
   const int k0 = threadIdx.x * kPerThread;
   int v[kPerThread];
@@ -168,10 +172,10 @@ __global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B,
     return;
   }
 #pragma unroll
-  for (int r = 0; r < (kTile + 2 + kTB - 1) / kTB; ++r) {
+  for (int r = 0; r < kRounds; ++r) {
     const int k = r * kTB + threadIdx.x;
     const int i = t0 - 1 + k;
-    if (k <= kTile + 1) s_key[k] = i < total ? kr[r] : 0xFFFFFFFFu;
+    s_key[k] = i < total ? kr[r] : 0xFFFFFFFFu;
   }
   __syncthreads();
   const unsigned long long T1 = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
@@ -204,6 +208,17 @@ __global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B,
         q = make_float4(p.x, p.y, p.z, p.intensity);
       }
       s_pt[k0 + u] = q;
+    }
+  }
+  // ... and the halo elements that continue the tile's last run (sorted: the elements equal to it are contiguous)
+  __shared__ float4 s_halo[kHalo];
+  if (threadIdx.x < kHalo) {
+    const uint32_t key = s_key[kTile + 1 + threadIdx.x];   // element t0 + kTile + threadIdx.x
+    if (key != 0xFFFFFFFFu && key == s_key[kTile]) {
+      PointRec p;
+      if (key >> 31) vox_fetch(B, nB0, nB1, vh, p);
+      else vox_fetch(A, nA0, nA1, vh, p);
+      s_halo[threadIdx.x] = make_float4(p.x, p.y, p.z, p.intensity);
     }
   }
   // heads in this thread's 4 consecutive elements
@@ -290,7 +305,23 @@ __global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B,
       c0 += p.x; c1 += p.y; c2 += p.z; c3 += p.w;
     }
     const bool crosses = end == kTile && t0 + kTile < total && s_key[kTile + 1] == key;
-    if (crosses) {
+    if (crosses) {   // its continuation in the halo, in order (elements past the count read 0xFFFFFFFF)
+      int h = 0;
+      while (h < kHalo && s_key[kTile + 1 + h] == key) {
+        const float4 p = s_halo[h];
+        c0 += p.x; c1 += p.y; c2 += p.z; c3 += p.w;
+        ++h;
+      }
+      if (h < kHalo) {   // it ends there
+        const float cn = (float)(t0 + kTile + h - i);
+        PointRec o;
+        o.x = c0 / cn; o.y = c1 / cn; o.z = c2 / cn; o.pad0 = 1.0f;
+        o.intensity = c3 / cn;
+        o.ring = 0; o.pad1 = 0; o.time = 0.0f; o.pad2 = 0.0f;
+        J.out[pos[job]++] = o;
+        continue;
+      }
+      // longer than the halo: finished cooperatively below, from element t0 + kTile + kHalo
       s_cross[0] = c0; s_cross[1] = c1; s_cross[2] = c2; s_cross[3] = c3;
       s_cross_pos = pos[job]++;
       s_cross_head = i;
@@ -311,7 +342,7 @@ __global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B,
     const uint32_t key = s_key[kTile];   // the tile's last element belongs to the crossing run
     const int n0 = job ? nB0 : nA0, n1 = job ? nB1 : nA1;
     __shared__ int s_done;
-    int j0 = t0 + kTile;
+    int j0 = t0 + kTile + kHalo;
     for (;;) {
       const int j = j0 + threadIdx.x;
       const bool in = j < total && keys[j] == key;
