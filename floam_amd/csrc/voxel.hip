@@ -300,7 +300,17 @@ __global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B,
     }
     const float4 f = s_pt[k];
     float c0 = f.x, c1 = f.y, c2 = f.z, c3 = f.w;
-    for (int j = k + 1; j < end; ++j) {   // sequential sum in sorted (= input) order
+    // sequential sum in sorted (= input) order; a long run (dense near-range voxels: tens to hundreds of points)
+    // reads 8 points per LDS round trip, the additions staying in order
+    int j = k + 1;
+    for (; j + 8 <= end; j += 8) {
+      float4 p[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) p[q] = s_pt[j + q];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) { c0 += p[q].x; c1 += p[q].y; c2 += p[q].z; c3 += p[q].w; }
+    }
+    for (; j < end; ++j) {
       const float4 p = s_pt[j];
       c0 += p.x; c1 += p.y; c2 += p.z; c3 += p.w;
     }
