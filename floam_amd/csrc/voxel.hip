@@ -25,8 +25,9 @@
 namespace floam {
 
 // FLOAM_VOX_STAMPS=1 (diagnostic): vox_compact's per-tile phase times of the last launch over >= 32 tiles (10-ns
-// ticks): [0] start (low bits), [1] keys staged, [2] points gathered + heads, [3] lookback done, [4] end (drained)
-__device__ unsigned g_vox_st[1024][5];
+// ticks): [0] start (low bits), [1] keys staged, [2] points gathered + heads, [3] lookback done, [4] end (drained),
+// [5] the longest run with its head in the tile
+__device__ unsigned g_vox_st[1024][6];
 
 namespace {
 constexpr int kTB = 256;
@@ -272,7 +273,8 @@ __global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B,
   // the run that crosses the tile end (at most one): its head's partial sums, finished cooperatively below
   __shared__ float s_cross[4];
   __shared__ int s_cross_pos, s_cross_head, s_cross_job;
-  if (threadIdx.x == 0) s_cross_head = -1;
+  __shared__ int s_maxrun;
+  if (threadIdx.x == 0) { s_cross_head = -1; s_maxrun = 0; }
   __syncthreads();
 #pragma unroll
   for (int u = 0; u < kPerThread; ++u) {
@@ -298,6 +300,7 @@ __global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B,
         break;
       }
     }
+    if (stamps) s_maxrun = max(s_maxrun, end - k);   // (diagnostic; racy max is fine)
     const float4 f = s_pt[k];
     float c0 = f.x, c1 = f.y, c2 = f.z, c3 = f.w;
     // sequential sum in sorted (= input) order; a long run (dense near-range voxels: tens to hundreds of points)
@@ -398,7 +401,7 @@ __global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B,
       const unsigned long long T4 = __builtin_amdgcn_s_memrealtime();
       unsigned* q = g_vox_st[tile];
       q[0] = (unsigned)T0; q[1] = (unsigned)(T1 - T0); q[2] = (unsigned)(T2 - T1); q[3] = (unsigned)(T3 - T2);
-      q[4] = (unsigned)(T4 - T3);
+      q[4] = (unsigned)(T4 - T3); q[5] = (unsigned)s_maxrun;
     }
   }
 }
@@ -412,7 +415,7 @@ static int vox_stamps_on() {
 
 void vox_stamps_print() {
   if (!vox_stamps_on()) return;
-  static unsigned q[1024][5];
+  static unsigned q[1024][6];
   FLOAM_HIP(hipDeviceSynchronize());
   FLOAM_HIP(hipMemcpyFromSymbol(q, HIP_SYMBOL(g_vox_st), sizeof(q)));
   int nt = 0;
@@ -432,8 +435,9 @@ void vox_stamps_print() {
                "sums + stores + drain %.2f us per tile; first start -> last end %.2f us\n", nt, ph[0] / nt / 100.0,
                ph[1] / nt / 100.0, ph[2] / nt / 100.0, ph[3] / nt / 100.0, last_end / 100.0);
   for (int t = 0; t < nt; t += std::max(1, nt / 8))
-    std::fprintf(stderr, "[vox tile %4d] start +%.2f: %.2f %.2f %.2f %.2f us\n", t, (int)(q[t][0] - q[0][0]) / 100.0,
-                 q[t][1] / 100.0, q[t][2] / 100.0, q[t][3] / 100.0, q[t][4] / 100.0);
+    std::fprintf(stderr, "[vox tile %4d] start +%.2f: %.2f %.2f %.2f %.2f us, longest run %u\n", t,
+                 (int)(q[t][0] - q[0][0]) / 100.0, q[t][1] / 100.0, q[t][2] / 100.0, q[t][3] / 100.0, q[t][4] / 100.0,
+                 q[t][5]);
 }
 
 VoxelJobDev to_dev(const VoxelJob& j, int base) {
