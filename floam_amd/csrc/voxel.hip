@@ -349,6 +349,8 @@ __global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B,
     J.out[pos[job]++] = o;
   }
   __syncthreads();
+  const unsigned long long T3b = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  const bool had_cross = s_cross_head >= 0;
   if (s_cross_head >= 0) {   // block-uniform: gather the run's continuation chunk by chunk, thread 0 sums in order
     const int job = s_cross_job;
     const VoxelJobDev& J = job == 0 ? A : B;
@@ -401,7 +403,7 @@ __global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B,
       const unsigned long long T4 = __builtin_amdgcn_s_memrealtime();
       unsigned* q = g_vox_st[tile];
       q[0] = (unsigned)T0; q[1] = (unsigned)(T1 - T0); q[2] = (unsigned)(T2 - T1); q[3] = (unsigned)(T3 - T2);
-      q[4] = (unsigned)(T4 - T3); q[5] = (unsigned)s_maxrun;
+      q[4] = (unsigned)(T4 - T3); q[5] = (unsigned)s_maxrun | (unsigned)(T3b - T3) << 16 | (had_cross ? 1u << 31 : 0u);
     }
   }
 }
@@ -435,9 +437,9 @@ void vox_stamps_print() {
                "sums + stores + drain %.2f us per tile; first start -> last end %.2f us\n", nt, ph[0] / nt / 100.0,
                ph[1] / nt / 100.0, ph[2] / nt / 100.0, ph[3] / nt / 100.0, last_end / 100.0);
   for (int t = 0; t < nt; t += std::max(1, nt / 8))
-    std::fprintf(stderr, "[vox tile %4d] start +%.2f: %.2f %.2f %.2f %.2f us, longest run %u\n", t,
+    std::fprintf(stderr, "[vox tile %4d] start +%.2f: %.2f %.2f %.2f %.2f us (heads %.2f us%s), longest run %u\n", t,
                  (int)(q[t][0] - q[0][0]) / 100.0, q[t][1] / 100.0, q[t][2] / 100.0, q[t][3] / 100.0, q[t][4] / 100.0,
-                 q[t][5]);
+                 ((q[t][5] >> 16) & 0x7FFF) / 100.0, (q[t][5] >> 31) ? ", deferred crossing run" : "", q[t][5] & 0xFFFF);
 }
 
 VoxelJobDev to_dev(const VoxelJob& j, int base) {
