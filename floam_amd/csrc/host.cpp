@@ -100,6 +100,20 @@ struct DeviceCtx {
 static std::mutex g_ctx_mu;
 static std::map<int, std::unique_ptr<DeviceCtx>> g_ctx;
 
+// Stream creation.  FLOAM_STREAM_PRIO=1 (experiment): the odometry stream at the highest priority, the side and
+// feature-extraction streams at the lowest, so that the command processor prefers the odometry's workgroups.
+static void make_stream(hipStream_t* s, bool high) {
+  static const bool prio = std::getenv("FLOAM_STREAM_PRIO") != nullptr;
+  if (!prio) {
+    FLOAM_HIP(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
+    return;
+  }
+  int least = 0, greatest = 0;
+  FLOAM_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+  FLOAM_HIP(hipStreamCreateWithPriority(s, hipStreamNonBlocking, high ? greatest : least));
+}
+
+
 static DeviceCtx& ctx_for(int device) {
   std::lock_guard<std::mutex> lk(g_ctx_mu);
   auto it = g_ctx.find(device);
@@ -115,7 +129,7 @@ static DeviceCtx& ctx_for(int device) {
     throw Error(FLOAM_ERR_DEVICE, std::string("device is ") + prop.gcnArchName + ", this build targets gfx950");
   auto c = std::make_unique<DeviceCtx>();
   c->device = device;
-  FLOAM_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  make_stream(&c->stream, true);
   DeviceCtx& ref = *c;
   g_ctx[device] = std::move(c);
   return ref;
@@ -947,7 +961,7 @@ floam_status odom_update(floam_odom* o, const floam_cloud* edge, const floam_clo
 void odom_prevoxel(floam_odom* o, floam_cloud* edge, floam_cloud* surf) {
   if (o->use_graph) return;
   if (!o->side) {
-    FLOAM_HIP(hipStreamCreateWithFlags(&o->side, hipStreamNonBlocking));
+    make_stream(&o->side, false);
     FLOAM_HIP(hipEventCreateWithFlags(&o->pre_ev, hipEventDisableTiming));
   }
   const int par = o->pre_par;
@@ -1207,7 +1221,7 @@ floam_status floam_lp_create(const floam_lidar_params* p, int device, floam_lp**
     lp->status.reserve(1);
     lp->h_out.reserve(4);
     lp->sc.status = lp->status.p;
-    FLOAM_HIP(hipStreamCreateWithFlags(&lp->stream, hipStreamNonBlocking));
+    make_stream(&lp->stream, false);
     *out = lp.release();
     return FLOAM_OK;
   });
