@@ -698,13 +698,20 @@ __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArg
                                   fminf(wy - 0.5f * (float)(qy - 1), 0.5f * (float)(qy + 2) - wy)),
                             fminf(wz - 0.5f * (float)(qz - 1), 0.5f * (float)(qz + 2) - wz));
       const bool complete = cnt >= 5 && __uint_as_float((unsigned)(t.k[4] >> 32)) < b * b;
-      if (!complete) {   // coarse cells floor(q - 1) .. floor(q + 1) per axis (exact in double)
+      if (!complete) {
+        // coarse cells floor(q - r) .. floor(q + r) per axis (exact in double).  r = 1 (every point within 1 m)
+        // unless stage 1 already holds 5 points within 1 m: then the 5-NN and every point tied with the 5th lie in
+        // the ball of its float sq-distance d5, and r = sqrt(d5) (1 + 1e-6) covers that ball with margin — a point
+        // outside the box is more than r away along one axis, so its float sq-distance is >= r^2 (1 - 2^-24)^5 > d5
+        // (monotone rounding of the 3 squares and 2 adds) and it can neither enter nor tie the top-5
+        double r = 1.0;
+        if (cnt >= 5) r = fmin(1.0, sqrt((double)__uint_as_float((unsigned)(t.k[4] >> 32))) * (1.0 + 1e-6));
 #pragma unroll
         for (int k = 0; k < 5; ++k) t.k[k] = ~0ull;
         cnt = 0;
-        stencil_scan<G, U, true>(A, (int)floor((double)wx - 1.0), (int)floor((double)wx + 1.0),
-                                 (int)floor((double)wy - 1.0), (int)floor((double)wy + 1.0),
-                                 (int)floor((double)wz - 1.0), (int)floor((double)wz + 1.0), wx, wy, wz, lane, s_pre,
+        stencil_scan<G, U, true>(A, (int)floor((double)wx - r), (int)floor((double)wx + r),
+                                 (int)floor((double)wy - r), (int)floor((double)wy + r),
+                                 (int)floor((double)wz - r), (int)floor((double)wz + r), wx, wy, wz, lane, s_pre,
                                  s_start, t, cnt);
         group_merge<G>(t, cnt);
         flags |= 2;
@@ -955,6 +962,47 @@ __global__ __launch_bounds__(kTB) void geom_kernel(LMState* __restrict__ st, Cor
 // the query's cell — level 0 — and of the coarse +-1 m stencil for the queries whose bit 1 says they needed stage 2
 // — level 1), every query is read once (16 B) and writes its flag (1 B) and, with 5 neighbours, their coordinates
 // (60 B) (counted at level 0).  Runs untimed, on a replay, only when profiling.
+//
+// The radius of a query's stage 2 (knn_group): 1, or with 5 points within 1 m in the fine block around the query's
+// cell, sqrt of the 5th-smallest float sq-distance among them times (1 + 1e-6) — recomputed here serially over the
+// same 27 fine cells with the same float arithmetic
+__device__ double stage2_radius(const CorrArgs& A, float wx, float wy, float wz) {
+  int qx, qy, qz;
+  fine_cell(wx, wy, wz, qx, qy, qz);
+  float best[5] = {2.f, 2.f, 2.f, 2.f, 2.f};   // ascending
+  int cnt = 0;
+  for (int fz = qz - 1; fz <= qz + 1; ++fz)
+    for (int fy = qy - 1; fy <= qy + 1; ++fy)
+      for (int fx = qx - 1; fx <= qx + 1; ++fx) {
+        const unsigned long long key = cell_key(fx >> 1, fy >> 1, fz >> 1);
+        unsigned h = hash_slot64(key, A.bits);
+        while (A.coarse[h].key != key && A.coarse[h].key != kEmptyKey) h = (h + 1) & A.mask;
+        const CoarseCell& c = A.coarse[h];
+        if (c.key != key) continue;
+        const int sub = (fx & 1) | ((fy & 1) << 1) | ((fz & 1) << 2);
+        int start = c.start;
+        for (int k = 0; k < sub; ++k) start += c.sub[k];
+        for (int j = 0; j < c.sub[sub]; ++j) {
+          const float4 m = A.gpts[start + j];
+          float dd = 0.0f, df = wx - m.x;
+          dd += df * df;
+          df = wy - m.y;
+          dd += df * df;
+          df = wz - m.z;
+          dd += df * df;
+          if (!(dd < 1.0f)) continue;
+          ++cnt;
+          for (int k = 0; k < 5; ++k)
+            if (dd < best[k]) {
+              const float tmp = best[k];
+              best[k] = dd;
+              dd = tmp;
+            }
+        }
+      }
+  return cnt >= 5 ? fmin(1.0, sqrt((double)best[4]) * (1.0 + 1e-6)) : 1.0;
+}
+
 __global__ __launch_bounds__(kTB) void knn_traffic(const LMState* __restrict__ st, CorrArgs A, int rank,
                                                    int world, int level, unsigned long long* __restrict__ set,
                                                    unsigned set_mask, int set_bits,
@@ -974,9 +1022,10 @@ __global__ __launch_bounds__(kTB) void knn_traffic(const LMState* __restrict__ s
   unsigned long long bytes = level ? 0ull : 16ull + 1ull + ((f & 4) ? 60ull : 0ull);
   int x0, y0, z0, x1, y1, z1;
   if (level) {
-    x0 = (int)floor((double)wx - 1.0); x1 = (int)floor((double)wx + 1.0);
-    y0 = (int)floor((double)wy - 1.0); y1 = (int)floor((double)wy + 1.0);
-    z0 = (int)floor((double)wz - 1.0); z1 = (int)floor((double)wz + 1.0);
+    const double r = stage2_radius(A, wx, wy, wz);
+    x0 = (int)floor((double)wx - r); x1 = (int)floor((double)wx + r);
+    y0 = (int)floor((double)wy - r); y1 = (int)floor((double)wy + r);
+    z0 = (int)floor((double)wz - r); z1 = (int)floor((double)wz + r);
   } else {
     fine_cell(wx, wy, wz, x0, y0, z0);
     --x0; --y0; --z0;
