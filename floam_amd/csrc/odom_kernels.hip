@@ -490,13 +490,23 @@ constexpr int kMaxStencil = 27;
 // start and the point count of each of their 8 fine sub-cells (sub-cells are consecutive inside the range, in sub
 // order: grid.hip).  Lanes 0..7 probe the 8 coarse cells (head and sub counts of a slot in one round trip) into LDS
 // (s_cc[8][9]: start, 8 counts), then every fine cell's range is start + the counts of the sub-cells before it.
-template <int G>
-__device__ __forceinline__ void fine_block_ranges(const CorrArgs& A, int qx, int qy, int qz, int lane,
+// NB = 2: the 2x2x2 fine block with low corner (lx, ly, lz) (the query's cell and its nearer neighbour per axis),
+// whose cells lie in 1 or 2 coarse cells per axis (only those are probed).
+template <int G, int NB = 3>
+__device__ __forceinline__ void fine_block_ranges(const CorrArgs& A, int lx, int ly, int lz, int lane,
                                                   int* __restrict__ s_pre, int* __restrict__ s_start,
                                                   int* __restrict__ s_cc) {
   static_assert(G >= 8, "one coarse probe per lane");
-  const int cx0 = (qx - 1) >> 1, cy0 = (qy - 1) >> 1, cz0 = (qz - 1) >> 1;   // floor division by 2
-  if (lane < 8) {
+  const int cx0 = lx >> 1, cy0 = ly >> 1, cz0 = lz >> 1;   // floor division by 2
+  // (NB = 3: three consecutive fine indices always span two coarse indices; NB = 2: two when lx is odd)
+  const bool need = NB == 3 || (((lane & 1) == 0 || (lx & 1)) && (((lane >> 1) & 1) == 0 || (ly & 1)) &&
+                                ((lane >> 2) == 0 || (lz & 1)));
+  if (lane < 8 && !need) {
+    int* cc = s_cc + 9 * lane;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) cc[k] = 0;
+  }
+  if (lane < 8 && need) {
     const unsigned long long key = cell_key(cx0 + (lane & 1), cy0 + ((lane >> 1) & 1), cz0 + (lane >> 2));
     unsigned slot = hash_slot64(key, A.bits);
     const int4* e = reinterpret_cast<const int4*>(&A.coarse[slot]);
@@ -517,14 +527,15 @@ __device__ __forceinline__ void fine_block_ranges(const CorrArgs& A, int qx, int
     cc[5] = hit ? s1.x : 0; cc[6] = hit ? s1.y : 0; cc[7] = hit ? s1.z : 0; cc[8] = hit ? s1.w : 0;
   }
   wave_lds_order();
-  constexpr int P = (kMaxStencil + G - 1) / G;   // fine cells per lane
-  const int cb = min(kMaxStencil, lane * P), ce = min(kMaxStencil, cb + P);
+  constexpr int NC = NB * NB * NB;
+  constexpr int P = (NC + G - 1) / G;   // fine cells per lane
+  const int cb = min(NC, lane * P), ce = min(NC, cb + P);
   int local = 0;
 #pragma unroll
   for (int j = 0; j < P; ++j) {
     const int c = cb + j;
     if (c < ce) {
-      const int fx = qx - 1 + c % 3, fy = qy - 1 + (c / 3) % 3, fz = qz - 1 + c / 9;
+      const int fx = lx + c % NB, fy = ly + (c / NB) % NB, fz = lz + c / (NB * NB);
       const int ci = ((fx >> 1) - cx0) | (((fy >> 1) - cy0) << 1) | (((fz >> 1) - cz0) << 2);
       const int sub = (fx & 1) | ((fy & 1) << 1) | ((fz & 1) << 2);
       const int* cc = s_cc + 9 * ci;
@@ -542,11 +553,11 @@ __device__ __forceinline__ void fine_block_ranges(const CorrArgs& A, int qx, int
 #pragma unroll
   for (int j = 0; j < P; ++j)
     if (cb + j < ce) s_pre[cb + j] += excl;
-  if (lane == G - 1) s_pre[kMaxStencil] = incl;
+  if (lane == G - 1) s_pre[NC] = incl;
   wave_lds_order();
 }
 
-template <int G, int U, bool COARSE>
+template <int G, int U, bool COARSE, int NB = 3>
 __device__ __forceinline__ void stencil_scan(const CorrArgs& A, int x0, int x1, int y0, int y1, int z0, int z1,
                                              float wx, float wy, float wz, int lane, int* __restrict__ s_pre,
                                              int* __restrict__ s_start, Top5& t, int& cnt,
@@ -555,9 +566,9 @@ __device__ __forceinline__ void stencil_scan(const CorrArgs& A, int x0, int x1, 
   const int nxr = x1 - x0 + 1, nyr = y1 - y0 + 1, nzr = z1 - z0 + 1;
   const int ncell = nxr * nyr * nzr;
   int tot;
-  if constexpr (!COARSE) {   // the fine block around (x0 + 1, y0 + 1, z0 + 1), ranges from the coarse entries
-    fine_block_ranges<G>(A, x0 + 1, y0 + 1, z0 + 1, lane, s_pre, s_start, s_cc);
-    tot = s_pre[kMaxStencil];
+  if constexpr (!COARSE) {   // the fine block with low corner (x0, y0, z0), ranges from the coarse entries
+    fine_block_ranges<G, NB>(A, x0, y0, z0, lane, s_pre, s_start, s_cc);
+    tot = s_pre[NB * NB * NB];
   } else {
   const int per = (ncell + G - 1) / G;
   const int cb = min(ncell, lane * per), ce = min(ncell, cb + per);
@@ -667,7 +678,22 @@ __device__ __forceinline__ int xcd_block(int p, int nactive) {
 // which contain every point within 1 m.  Ties at equal float distance go to the lower map index (FLANN's own order
 // depends on its tree traversal; tie-free data is identical).
 // Output: valid bit 0 = 5 neighbours within sqd < 1 (their coordinates in nnxyz), bit 1 = stage 2 was needed.
-template <int G, int U>
+// Low fine corner of a query's stage-1 block: nb = 3, the cells around the query's (qx, qy, qz); nb = 2, the
+// query's cell and the neighbour on the nearer side per axis (2 w - f is exact: f = floor(2 w) and 2 w are floats
+// within a factor 2)
+__device__ __forceinline__ void knn_block_corner(int nb, float wx, float wy, float wz, int qx, int qy, int qz, int& lx,
+                                                 int& ly, int& lz) {
+  lx = qx - 1;
+  ly = qy - 1;
+  lz = qz - 1;
+  if (nb == 2) {
+    if (2.0f * wx - (float)qx >= 0.5f) ++lx;
+    if (2.0f * wy - (float)qy >= 0.5f) ++ly;
+    if (2.0f * wz - (float)qz >= 0.5f) ++lz;
+  }
+}
+
+template <int G, int U, int NB>
 __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArgs& A, int gid, int ngroups,
                                           int lane, bool gate, int rank, int world, int* __restrict__ s_pre,
                                           int* __restrict__ s_start, int* __restrict__ s_cc) {
@@ -688,15 +714,18 @@ __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArg
 #pragma unroll
       for (int k = 0; k < 5; ++k) t.k[k] = ~0ull;
       int cnt = 0;
-      stencil_scan<G, U, false>(A, qx - 1, qx + 1, qy - 1, qy + 1, qz - 1, qz + 1, wx, wy, wz, lane, s_pre, s_start,
-                                t, cnt, s_cc);
+      int lx, ly, lz;
+      knn_block_corner(NB, wx, wy, wz, qx, qy, qz, lx, ly, lz);
+      stencil_scan<G, U, false, NB>(A, lx, lx + NB - 1, ly, ly + NB - 1, lz, lz + NB - 1, wx, wy, wz, lane, s_pre,
+                                    s_start, t, cnt, s_cc);
       group_merge<G>(t, cnt);
-      // exact early exit: a map point outside the fine block [lo, hi) (lo = (f - 1) / 2, hi = (f + 2) / 2 per axis,
-      // exact in float) lies beyond a face, so on that axis |fl(q - p)| >= fl(q - lo) or fl(hi - q) (monotone
-      // rounding) and its float sq-distance is >= fl(b^2), b the query's smallest face distance (>= 0.5)
-      const float b = fminf(fminf(fminf(wx - 0.5f * (float)(qx - 1), 0.5f * (float)(qx + 2) - wx),
-                                  fminf(wy - 0.5f * (float)(qy - 1), 0.5f * (float)(qy + 2) - wy)),
-                            fminf(wz - 0.5f * (float)(qz - 1), 0.5f * (float)(qz + 2) - wz));
+      // exact early exit: a map point outside the fine block [lo, hi) (lo = l / 2, hi = (l + NB) / 2 per axis, exact
+      // in float) lies beyond a face, so on that axis |fl(q - p)| >= fl(q - lo) or fl(hi - q) (monotone rounding)
+      // and its float sq-distance is >= fl(b^2), b the query's smallest face distance (>= 0.5 for NB = 3, >= 0.25
+      // for NB = 2)
+      const float b = fminf(fminf(fminf(wx - 0.5f * (float)lx, 0.5f * (float)(lx + NB) - wx),
+                                  fminf(wy - 0.5f * (float)ly, 0.5f * (float)(ly + NB) - wy)),
+                            fminf(wz - 0.5f * (float)lz, 0.5f * (float)(lz + NB) - wz));
       const bool complete = cnt >= 5 && __uint_as_float((unsigned)(t.k[4] >> 32)) < b * b;
       if (!complete) {
         // coarse cells floor(q - r) .. floor(q + r) per axis (exact in double).  r = 1 (every point within 1 m)
@@ -741,7 +770,7 @@ __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArg
 // Edge and surf kNN in one launch: blocks [0, nbE) run edge groups, the others surf groups.  The launch also starts
 // the solve (lm_init folded in): block 0 resets the LM state and, for the first solve of an update, stores the
 // prediction x0 that every block uses for its transforms (the others never read st->x in that case).
-template <int G, int U, int W>
+template <int G, int U, int W, int NB>
 __global__ __launch_bounds__(kTB, W) void knn_kernel(LMState* __restrict__ st, const double* __restrict__ x0_dev,
                                                   CorrArgs E, CorrArgs S, int nbE,
                                                   const int* __restrict__ d_me, const int* __restrict__ d_ms,
@@ -776,7 +805,7 @@ __global__ __launch_bounds__(kTB, W) void knn_kernel(LMState* __restrict__ st, c
   const int nq = min(*A.d_n, A.n_ub);
   const int nact = min(nb, (int)(((long long)nq * G + kTB - 1) / kTB));
   if (p < nact) p = xcd_block(p, nact);
-  knn_group<G, U>(pose, A, (p * kTB + (int)threadIdx.x) / G, nb * (kTB / G), lane, gate, rank, world, s_pre[g],
+  knn_group<G, U, NB>(pose, A, (p * kTB + (int)threadIdx.x) / G, nb * (kTB / G), lane, gate, rank, world, s_pre[g],
                   s_start[g], s_cc[g]);
 }
 
@@ -964,16 +993,17 @@ __global__ __launch_bounds__(kTB) void geom_kernel(LMState* __restrict__ st, Cor
 // (60 B) (counted at level 0).  Runs untimed, on a replay, only when profiling.
 //
 // The radius of a query's stage 2 (knn_group): 1, or with 5 points within 1 m in the fine block around the query's
-// cell, sqrt of the 5th-smallest float sq-distance among them times (1 + 1e-6) — recomputed here serially over the
-// same 27 fine cells with the same float arithmetic
-__device__ double stage2_radius(const CorrArgs& A, float wx, float wy, float wz) {
-  int qx, qy, qz;
+// block (nb^3 fine cells), sqrt of the 5th-smallest float sq-distance among them times (1 + 1e-6) — recomputed here
+// serially over the same fine cells with the same float arithmetic
+__device__ double stage2_radius(const CorrArgs& A, int nb, float wx, float wy, float wz) {
+  int qx, qy, qz, lx, ly, lz;
   fine_cell(wx, wy, wz, qx, qy, qz);
+  knn_block_corner(nb, wx, wy, wz, qx, qy, qz, lx, ly, lz);
   float best[5] = {2.f, 2.f, 2.f, 2.f, 2.f};   // ascending
   int cnt = 0;
-  for (int fz = qz - 1; fz <= qz + 1; ++fz)
-    for (int fy = qy - 1; fy <= qy + 1; ++fy)
-      for (int fx = qx - 1; fx <= qx + 1; ++fx) {
+  for (int fz = lz; fz < lz + nb; ++fz)
+    for (int fy = ly; fy < ly + nb; ++fy)
+      for (int fx = lx; fx < lx + nb; ++fx) {
         const unsigned long long key = cell_key(fx >> 1, fy >> 1, fz >> 1);
         unsigned h = hash_slot64(key, A.bits);
         while (A.coarse[h].key != key && A.coarse[h].key != kEmptyKey) h = (h + 1) & A.mask;
@@ -1004,7 +1034,8 @@ __device__ double stage2_radius(const CorrArgs& A, float wx, float wy, float wz)
 }
 
 __global__ __launch_bounds__(kTB) void knn_traffic(const LMState* __restrict__ st, CorrArgs A, int rank,
-                                                   int world, int level, unsigned long long* __restrict__ set,
+                                                   int world, int level, int nb,
+                                                   unsigned long long* __restrict__ set,
                                                    unsigned set_mask, int set_bits,
                                                    unsigned long long* __restrict__ out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1022,14 +1053,15 @@ __global__ __launch_bounds__(kTB) void knn_traffic(const LMState* __restrict__ s
   unsigned long long bytes = level ? 0ull : 16ull + 1ull + ((f & 4) ? 60ull : 0ull);
   int x0, y0, z0, x1, y1, z1;
   if (level) {
-    const double r = stage2_radius(A, wx, wy, wz);
+    const double r = stage2_radius(A, nb, wx, wy, wz);
     x0 = (int)floor((double)wx - r); x1 = (int)floor((double)wx + r);
     y0 = (int)floor((double)wy - r); y1 = (int)floor((double)wy + r);
     z0 = (int)floor((double)wz - r); z1 = (int)floor((double)wz + r);
   } else {
-    fine_cell(wx, wy, wz, x0, y0, z0);
-    --x0; --y0; --z0;
-    x1 = x0 + 2; y1 = y0 + 2; z1 = z0 + 2;
+    int qx, qy, qz;
+    fine_cell(wx, wy, wz, qx, qy, qz);
+    knn_block_corner(nb, wx, wy, wz, qx, qy, qz, x0, y0, z0);
+    x1 = x0 + nb - 1; y1 = y0 + nb - 1; z1 = z0 + nb - 1;
   }
   for (int z = z0; z <= z1; ++z)
     for (int y = y0; y <= y1; ++y)
@@ -1303,6 +1335,15 @@ static void corr_args(const QuerySet& qe, const Grid& ge, CorrSet& ce, const Que
                cs.valid.p, cs.nnxyz.p, cs.trace ? cs.nnidx.p : nullptr, cs.trace ? cs.nnsqd.p : nullptr, cs.cap};
 }
 
+// stage-1 block edge in fine cells (FLOAM_KNN_BLOCK=2|3)
+static int knn_block() {
+  static const int nb = [] {
+    const char* e = std::getenv("FLOAM_KNN_BLOCK");
+    return e && std::atoi(e) == 2 ? 2 : 3;
+  }();
+  return nb;
+}
+
 void knn_launch(LMState* d_st, const double* x0_dev, const QuerySet& qe, const Grid& ge, CorrSet& ce,
                 const QuerySet& qs, const Grid& gs, CorrSet& cs, const int* d_me, const int* d_ms, int rank, int world,
                 hipStream_t st) {
@@ -1318,8 +1359,12 @@ void knn_launch(LMState* d_st, const double* x0_dev, const QuerySet& qe, const G
   const int nS = qs.grid_hint > 0 ? std::min(qs.grid_hint, qs.n_ub) : qs.n_ub;
   const unsigned nbE = std::min(div_up((size_t)std::max(nE, 1) * G, kTB), 4096u);
   const unsigned nbS = std::min(div_up((size_t)std::max(nS, 1) * G, kTB), 8192u);
-  hipLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6>), dim3(nbE + nbS), dim3(kTB), 0, st, d_st, x0_dev, E, S,
-                     (int)nbE, d_me, d_ms, rank, world);
+  if (knn_block() == 2)
+    hipLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6, 2>), dim3(nbE + nbS), dim3(kTB), 0, st, d_st, x0_dev, E, S,
+                       (int)nbE, d_me, d_ms, rank, world);
+  else
+    hipLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6, 3>), dim3(nbE + nbS), dim3(kTB), 0, st, d_st, x0_dev, E, S,
+                       (int)nbE, d_me, d_ms, rank, world);
   FLOAM_LAUNCH_CHECK();
 }
 
@@ -1353,7 +1398,7 @@ void knn_traffic_launch(const LMState* d_st, const QuerySet& q, const Grid& g, C
   for (int level = 0; level < 2; ++level) {
     FLOAM_HIP(hipMemsetAsync(set.p, 0xFF, sizeof(unsigned long long) << bits, st));
     hipLaunchKernelGGL(knn_traffic, dim3(div_up(q.n_ub, kTB)), dim3(kTB), 0, st, d_st, A, rank, world,
-                       level, set.p, (1u << bits) - 1u, bits, d_bytes);
+                       level, knn_block(), set.p, (1u << bits) - 1u, bits, d_bytes);
     FLOAM_LAUNCH_CHECK();
   }
 }
