@@ -212,3 +212,77 @@ def test_knn_ties(floam_gpu, oracle_lib):
         np.testing.assert_array_equal(gpu["idx"][i], order)
     differs = np.sum(np.any(np.sort(gpu["idx"][gated], 1) != np.sort(ref["idx"][gated], 1), axis=1))
     print(f"lattice: {gated.size} queries with an 8-way tie, FLANN kept a different 5 of 8 on {differs}")
+
+
+def _brute_top5(map_points, qx, qy, qz):
+    """(float sq-distances, map indices) of the exact 5-NN under the GPU's rule — FLANN's float L2_Simple order, ties
+    by map index — and the count within sqd < 1."""
+    dx = np.float32(qx) - map_points["x"]
+    dy = np.float32(qy) - map_points["y"]
+    dz = np.float32(qz) - map_points["z"]
+    d = ((np.float32(0) + dx * dx) + dy * dy) + dz * dz
+    order = np.lexsort((np.arange(d.size), d))[:5]
+    return d[order], order, int(np.sum(d < np.float32(1)))
+
+
+def test_knn_stage2_radius(floam_gpu, oracle_lib):
+    """Stage 2 of the search (odom_kernels.hip knn_group): when the 3x3x3 fine block around the query's cell already
+    holds 5 points within 1 m but the 5th is farther than the block's nearest face, only the coarse cells of the ball
+    of that 5th distance (with a rounding margin) are scanned.  (1) A boundary tie: 5 points inside the block and one
+    outside it at exactly the same float distance (0.625^2) with the lowest map index — the GPU must keep it (ties by
+    map index), so the ball must reach it.  (2) A sparse random map (2.5 points / m^3: most queries need stage 2, with
+    r < 1 or r = 1): every gated query's indices and float distances equal the brute-force 5-NN exactly."""
+    from floam_amd.odom_estimation import reset_process_state
+    reset_process_state()
+    R = 16
+    ident = np.array([0.0, 0.0, 0.0, 1.0]), np.zeros(3)
+
+    def run(map_pts, queries, leaf_set):
+        odo = floam_gpu.OdomEstimationClass()
+        odo.init(_params(R), 0.1, "Cauchy")
+        odo.set_trace(8)
+        odo.initMapWithPoints(floam_gpu.DeviceCloud(map_pts), floam_gpu.DeviceCloud(map_pts))
+        odo.find_correspondences(floam_gpu.DeviceCloud(queries), floam_gpu.DeviceCloud(queries), *ident)
+        out = odo.correspondences(leaf_set)
+        odo.close()
+        return out
+
+    def pts(xyz):
+        a = np.zeros(len(xyz), synth.POINT_DTYPE)
+        a["x"], a["y"], a["z"] = np.asarray(xyz, np.float32).T
+        a["pad0"] = 1.0
+        return a
+
+    # (1) query (10, 0.25, 0.25): fine block x in [9.5, 11), y, z in [-0.5, 1); nearest face 0.5 m (b^2 = 0.25)
+    tied_out = [(9.375, 0.25, 0.25)]                                     # outside the block, index 0
+    inside = [(10.625, 0.25, 0.25), (10.0, 0.875, 0.25), (10.0, 0.25, 0.875), (10.0, -0.375, 0.25),
+              (10.0, 0.25, -0.375)]                                      # sqd 0.390625 each
+    filler = [(10.0 + 3.0 * k, 40.0, 40.0) for k in range(60)]          # far away: the map-size gate (> 50 points)
+    mp = pts(tied_out + inside + filler)
+    q = pts([(10.0, 0.25, 0.25)])
+    g = run(mp, q, 1)
+    assert g["flags"][0] & 4, "gated"
+    assert g["flags"][0] & 2, "stage 2 ran"
+    np.testing.assert_array_equal(g["sqd"][0], np.full(5, 0.390625, np.float32))
+    np.testing.assert_array_equal(g["idx"][0], [0, 1, 2, 3, 4])         # the 5 lowest of the 6 tied indices
+
+    # (2) sparse random map
+    rng = np.random.default_rng(11)
+    mp = pts(rng.uniform(-10.0, 10.0, size=(20000, 3)))
+    qs = pts(rng.uniform(-9.0, 9.0, size=(3000, 3)))
+    g = run(mp, qs, 1)
+    vox = oracle_lib.voxel_grid(qs, 0.2, stable=True)
+    assert g["queries"].shape == vox.shape
+    n_gated = n_stage2 = 0
+    for i in range(vox.shape[0]):
+        d, idx, cnt = _brute_top5(mp, vox["x"][i], vox["y"][i], vox["z"][i])
+        gated = cnt >= 5
+        assert bool(g["flags"][i] & 4) == gated, i
+        if not gated:
+            continue
+        n_gated += 1
+        n_stage2 += bool(g["flags"][i] & 2)
+        np.testing.assert_array_equal(g["sqd"][i], d, err_msg=f"query {i}")
+        np.testing.assert_array_equal(g["idx"][i], idx, err_msg=f"query {i}")
+    assert n_gated > 500 and n_stage2 > 200, (n_gated, n_stage2)
+    print(f"sparse map: {vox.shape[0]} queries, {n_gated} gated, {n_stage2} of them through stage 2")
