@@ -309,6 +309,85 @@ def main():
                                               "bound": "latency (serial fp64 control step + one inter-block "
                                                        "hand-off per LM evaluation)"}
 
+    def dropin_sync(ref_poses):
+        """The drop-in contract: host-resident PointXYZIRT scans through exactly the INTEGRATION.md
+        adapters' calls, one scan per callback, everything synchronous (src/laserProcessingNode.cpp:129,
+        src/odomEstimationNode.cpp:205-244): featureExtraction = raw upload + extraction + edge / surf download (the
+        processing node publishes host clouds); UpdatePointsToMapSelector = edge / surf upload + the update (async
+        off) + the Q5 write-back downloads (size + download each, as the adapter's download()) + get_pose +
+        get_last_pose.  Same scans and prefilled map as the headline run; the poses must equal the resident run's."""
+        reset_process_state()
+        lp_ = floam_amd.LaserProcessingClass(device=dev)
+        lp_.init(params)
+        odo_ = floam_amd.OdomEstimationClass(device=dev)
+        odo_.init(params, MAP_RES, LOSS)
+        odo_.initMapWithPoints(d_mapE, d_mapS)
+        hL, h_lp, h_odo = L, lp_._h, odo_._h
+        c_in, c_e, c_s = (floam_amd.DeviceCloud(device=dev) for _ in range(3))   # processing node
+        o_e, o_s = floam_amd.DeviceCloud(device=dev), floam_amd.DeviceCloud(device=dev)   # odometry node
+        he = np.zeros(max(64 * 1024, raws[0].shape[0]), synth.POINT_DTYPE)
+        hs = np.zeros(raws[0].shape[0] + 1024, synth.POINT_DTYPE)
+        vp = C.c_void_p
+        q, t, q2, t2 = np.zeros(4), np.zeros(3), np.zeros(4), np.zeros(3)
+        qp, tp = q.ctypes.data_as(C.POINTER(C.c_double)), t.ctypes.data_as(C.POINTER(C.c_double))
+        q2p, t2p = q2.ctypes.data_as(C.POINTER(C.c_double)), t2.ctypes.data_as(C.POINTER(C.c_double))
+        n_ = C.c_size_t()
+        seg = np.zeros(6)   # seconds: raw upload, extraction, FE downloads, odometry uploads, update, write-back + poses
+        got = []
+
+        def download(c, buf):
+            _ffi.check(hL.floam_cloud_size(c.handle, C.byref(n_)))
+            n = n_.value
+            _ffi.check(hL.floam_cloud_download(c.handle, vp(buf.ctypes.data), n, C.byref(n_)))
+            return n
+
+        def one(k):
+            raw = raws[k]
+            t0 = time.perf_counter()
+            _ffi.check(hL.floam_cloud_upload(c_in.handle, vp(raw.ctypes.data), raw.shape[0], 32))
+            t1 = time.perf_counter()
+            _ffi.check(hL.floam_cloud_clear(c_e.handle))
+            _ffi.check(hL.floam_cloud_clear(c_s.handle))
+            _ffi.check(hL.floam_lp_feature_extraction(h_lp, c_in.handle, c_e.handle, c_s.handle))
+            t2 = time.perf_counter()
+            ne, ns = download(c_e, he), download(c_s, hs)
+            t3 = time.perf_counter()
+            _ffi.check(hL.floam_cloud_upload(o_e.handle, vp(he.ctypes.data), ne, 32))
+            _ffi.check(hL.floam_cloud_upload(o_s.handle, vp(hs.ctypes.data), ns, 32))
+            t4 = time.perf_counter()
+            _ffi.check(hL.floam_odom_update_selector(h_odo, o_e.handle, o_s.handle, 1))
+            t5 = time.perf_counter()
+            download(o_e, he)
+            download(o_s, hs)
+            _ffi.check(hL.floam_odom_get_pose(h_odo, qp, tp))
+            _ffi.check(hL.floam_odom_get_last_pose(h_odo, q2p, t2p))
+            t6 = time.perf_counter()
+            return np.array([t1 - t0, t2 - t1, t3 - t2, t4 - t3, t5 - t4, t6 - t5])
+
+        for k in range(args.warmup):
+            one(k)
+            got.append((q.copy(), t.copy()))
+        t_start = time.perf_counter()
+        for k in range(args.warmup, n_scans):
+            seg += one(k)
+            got.append((q.copy(), t.copy()))
+        dt = time.perf_counter() - t_start
+        same = all(np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) for a, b in zip(ref_poses, got))
+        for c in (c_in, c_e, c_s, o_e, o_s):
+            c.close()
+        odo_.close()
+        lp_.close()
+        us = 1e6 / args.steps
+        return {"value": round(args.steps / dt, 2), "unit": "scans/s", "ms_per_scan": round(1e3 * dt / args.steps, 3),
+                "poses_equal_resident_run": bool(same),
+                "segments_us_per_scan": {"raw_upload": round(seg[0] * us, 1), "feature_extraction": round(seg[1] * us, 1),
+                                         "fe_downloads": round(seg[2] * us, 1),
+                                         "odom_uploads": round(seg[3] * us, 1), "update": round(seg[4] * us, 1),
+                                         "writeback_downloads_and_poses": round(seg[5] * us, 1)},
+                "calls": "per scan: floam_cloud_upload(raw), floam_lp_feature_extraction (sync), size+download x2, "
+                         "floam_cloud_upload x2, floam_odom_update_selector (async off, deskew), size+download x2 (Q5), "
+                         "floam_odom_get_pose, floam_odom_get_last_pose (INTEGRATION.md adapters)"}
+
     secondary = None
     if rank == 0 and world == 1 and not args.no_secondary:
         odo.close()
@@ -329,7 +408,8 @@ def main():
         hub_dt, hub_poses = timed_sequence("huber")
         secondary = {"feature_extraction_alone": {"value": round(args.steps / fe_dt, 2), "unit": "scans/s"},
                      "huber": {"value": round(args.steps / hub_dt, 3), "unit": "scans/s",
-                               "loss": "huber (HuberLoss(0.1))"}}
+                               "loss": "huber (HuberLoss(0.1))"},
+                     "dropin_sync": dropin_sync(poses)}
 
     cpu = None
     pose_err = None

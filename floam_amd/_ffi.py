@@ -12,6 +12,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libfloam_amd.so")
 
 # floam_status (include/floam_c.h)
+ABI_VERSION = 2   # FLOAM_ABI_VERSION of include/floam_c.h this package binds
 OK = 0
 ERR_INVALID_ARGUMENT = 1
 ERR_DEVICE = 2
@@ -41,7 +42,7 @@ EXPORTS = [
     "floam_odom_set_trace", "floam_odom_get_traces", "floam_odom_get_correspondences",
     "floam_odom_find_correspondences",
     "floam_comm_unique_id", "floam_odom_set_shard", "floam_odom_set_shard_callback",
-    "floam_last_error", "floam_version", "floam_reset_process_state", "floam_device_synchronize",
+    "floam_last_error", "floam_version", "floam_abi_version", "floam_reset_process_state", "floam_device_synchronize",
     "floam_profile_enable", "floam_profile_read", "floam_profile_reset", "floam_profile_mark",
     "floam_imu_create", "floam_imu_destroy", "floam_imu_add_msg", "floam_imu_add_msgs", "floam_imu_size",
     "floam_imu_get", "floam_imu_time_contained", "floam_euler_to_quaternion", "floam_center_time",
@@ -156,6 +157,11 @@ def load(path: str | None = None):
     L.floam_last_error.restype = C.c_char_p
     L.floam_version.argtypes = []
     L.floam_version.restype = C.c_char_p
+    L.floam_abi_version.argtypes = []
+    L.floam_abi_version.restype = C.c_int
+    if L.floam_abi_version() != ABI_VERSION:   # a library built from another revision of include/floam_c.h
+        raise FloamError(ERR_UNSUPPORTED, f"libfloam_amd ABI {L.floam_abi_version()}, this package expects "
+                                          f"{ABI_VERSION} (rebuild floam_amd/csrc)")
     L.floam_reset_process_state.argtypes = []
     L.floam_reset_process_state.restype = None
     if path is None:

@@ -299,6 +299,7 @@ struct floam_odom {
   // against grid_count's 16.5 us), so off by default
   bool grid_count_off = true;
   int map_violate_mod = 0;        // FLOAM_MM_VIOLATE=n: every n-th merge reports its keys out of order (tests)
+  int mm_per = 4;                 // FLOAM_MM_PER=2: 512-element merge tiles instead of 1024 (tests, A/B)
   size_t mapE_n = 0, mapS_n = 0;   // map sizes: exact after a synchronisation, else upper bounds
   // scratch
   DevBuf<PointRec> dE, dS, tmp;
@@ -397,6 +398,10 @@ struct floam_odom {
   int coresident[16] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};   // lm_resident, per mode
   floam_odom_stats stats{};
   floam_status last_warning = FLOAM_OK;
+  // a device failure of an update (a solve abandoned, a compaction lookback timed out) leaves the device controller
+  // frozen (OdomDev::failed: no pose taken, no keyframe, no map update from then on): every later update of the
+  // handle fails with the first failure's message instead of returning stale odometry
+  std::string poisoned;
 };
 
 // dmapping::ImuHandler (include/dataHandler.h:31-66): the stamped orientation stream, host-side (AddMsg / Get /
@@ -712,6 +717,10 @@ floam_status odom_collect_one(floam_odom* o, DeviceCtx& ctx) {
   for (void* b : P.graveyard) (void)hipFree(b);
   ctx.drain();
   const UpdateStatus* slots = o->h_ustat.p + 2 * P.ring;
+  auto poison = [&](const char* m) {
+    o->poisoned = m;
+    throw Error(FLOAM_ERR_DEVICE, m);
+  };
   for (int k = 0; k < P.nslots; ++k) {
     const UpdateStatus& U = slots[k];
     if (ctx.profile & FLOAM_PROF_KNN_BYTES) {
@@ -719,10 +728,9 @@ floam_status odom_collect_one(floam_odom* o, DeviceCtx& ctx) {
       std::strncpy(t.name, "knn_search", sizeof(t.name) - 1);
       t.algorithmic_bytes += (double)U.prof[0] + (double)U.prof[1];
     }
-    if (U.lm.n_res < 0)
-      throw Error(FLOAM_ERR_DEVICE, "LM evaluation blocks did not arrive at the control block (timeout)");
+    if (U.lm.n_res < 0) poison("LM evaluation blocks did not arrive at the control block (timeout)");
     if (U.counts[0] < 0 || U.counts[1] < 0 || U.counts[2] < 0 || U.counts[3] < 0)
-      throw Error(FLOAM_ERR_DEVICE, "voxel-grid compaction failed (lookback timeout)");
+      poison("voxel-grid compaction failed (lookback timeout)");
     if (U.fe_status & FE_STATUS_SECTOR_TOO_LONG)
       throw Error(FLOAM_ERR_UNSUPPORTED, "a ring sector exceeds 4096 points (ring longer than ~24k points)");
     if (U.fe_status & FE_STATUS_BAD_RING)
@@ -768,6 +776,9 @@ floam_status odom_collect(floam_odom* o, DeviceCtx& ctx, size_t max_pending) {
 
 // status slots for the next update (collecting the oldest in-flight update if the ring is full)
 int odom_begin(floam_odom* o, DeviceCtx& ctx) {
+  if (!o->poisoned.empty())
+    throw Error(FLOAM_ERR_DEVICE, "an earlier update of this handle failed on the device (" + o->poisoned +
+                                      "); its odometry is frozen: create a new handle");
   const int ring_n = std::max(o->depth, 1);
   if (o->inflight.size() >= (size_t)ring_n) {
     const floam_status w = odom_collect(o, ctx, (size_t)ring_n - 1);
@@ -913,7 +924,7 @@ void odom_map_update(floam_odom* o, DeviceCtx& ctx, const MapUpdatePlan& P, size
       gcount[1] = grid_count_job(o->gS);
     }
     map_merge_launch(o->vs, o->mms, P.je, P.js, P.ke, P.ks, &o->ds.p->kf_flag, (unsigned)o->issued,
-                     o->map_force_full, o->map_violate_mod, fuse ? gcount : nullptr, st);
+                     o->map_force_full, o->map_violate_mod, fuse ? gcount : nullptr, st, o->mm_per);
     o->mkcur ^= 1;
   } else {
     voxel2_launch(o->vs, P.je, P.js, st, &o->ds.p->kf_flag, true);
@@ -1053,7 +1064,8 @@ void set_last_error(const std::string& m) { t_err = m; }
 extern "C" {
 
 const char* floam_last_error(void) { return t_err.c_str(); }
-const char* floam_version(void) { return "floam_amd 0.1.0 (gfx950)"; }
+const char* floam_version(void) { return "floam_amd 0.2.0 (gfx950, ABI 2)"; }
+int floam_abi_version(void) { return FLOAM_ABI_VERSION; }
 void floam_reset_process_state(void) { g_keyframe_first = true; }
 
 floam_status floam_device_synchronize(int device) {
@@ -1345,6 +1357,8 @@ floam_status floam_odom_create(const floam_lidar_params* p, double map_resolutio
     if (const char* e = std::getenv("FLOAM_MAP_MERGE")) o->map_merge = e[0] != '0';
     if (const char* e = std::getenv("FLOAM_MAP_FULL")) o->map_force_full = e[0] == '1';
     if (const char* e = std::getenv("FLOAM_MM_VIOLATE")) o->map_violate_mod = std::atoi(e);
+    if (const char* e = std::getenv("FLOAM_MM_PER")) o->mm_per = std::atoi(e) == 2 ? 2 : 4;
+    if (const char* e = std::getenv("FLOAM_LM_FAIL_TEST")) o->lmb.fail_test = std::atoi(e) != 0;
     if (const char* e = std::getenv("FLOAM_GRID_COUNT_FUSED")) o->grid_count_off = std::atoi(e) == 0;
     std::string l = loss ? loss : "";
     std::transform(l.begin(), l.end(), l.begin(), [](unsigned char c) { return (char)std::tolower(c); });

@@ -781,6 +781,7 @@ struct LMArgs {
   double* sums;                    // sharded: 29 sums (all-reduced in place between launches)
   unsigned* ticket;                // sharded: arrival ticket
   unsigned long long* dbg;         // FLOAM_DEBUG_STAMPS: block 0's segment times (diagnostic, normally null)
+  int fail_test;                   // LMBuffers::fail_test: report the first hand-off as timed out (tests)
 };
 
 // the block's first record (the one kept in registers across the evaluations) of record thread i0
@@ -893,6 +894,7 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
     int bad = 0;
     for (int j0 = tid; j0 < ngr; j0 += kSweep * kTB)
       if (!sweep_granules(slot, j0, ngr, tag, tab)) bad = 1;
+    if (a.fail_test) bad = 1;
     if (__syncthreads_or(bad)) {
       failed_at = it;
       break;
@@ -1052,7 +1054,7 @@ __global__ void lm_trace(const LMState* __restrict__ st, const int* __restrict__
 LMArgs make_args(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const CorrSet& cs, const int* d_ns,
                  int ns_ub, LMBuffers& b, unsigned long long* dbg) {
   return LMArgs{d_st, ce.rec.p, ce.valid.p, ce.cap, d_ne, std::max(ne_ub, 0), cs.rec.p, cs.valid.p, cs.cap, d_ns,
-                std::max(ns_ub, 0), b.gmat.p, b.part.p, b.partials.p, b.sums.p, b.ticket.p, dbg};
+                std::max(ns_ub, 0), b.gmat.p, b.part.p, b.partials.p, b.sums.p, b.ticket.p, dbg, b.fail_test};
 }
 }  // namespace
 

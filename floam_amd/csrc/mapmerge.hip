@@ -320,7 +320,10 @@ __global__ __launch_bounds__(kTB) void mm_merge(VoxelJobDev A, VoxelJobDev B, Ma
   __shared__ int s_src[(PER * kTB)];
   __shared__ unsigned char s_live[(PER * kTB)];
   __shared__ int s_split[2], s_first[2], s_open[2];
-  int j1 = d1;   // first set element after the tile (sorted order)
+  __shared__ int s_has_cross;   // a run of this tile continues past it (finished cooperatively below)
+  int j1 = d1;       // first set element after the tile (sorted order)
+  int i1m = V.n0;    // first map element after the tile (the merge path; none on the full path: the map is in the set)
+  if (t == 0) s_has_cross = 0;
   if (V.full) {
     for (int k = t; k < cnt; k += kTB) {
       const int pos = V.base + d0 + k;
@@ -345,6 +348,7 @@ __global__ __launch_bounds__(kTB) void mm_merge(VoxelJobDev A, VoxelJobDev B, Ma
       i1 = s_split[1];
       j0 = d0 - i0;
       j1 = d1 - i1;
+      i1m = i1;
     }
     const int na = i1 - i0, nb = j1 - j0;
     // the two runs' indices in LDS (points, sources, kept flags stay in registers: element k = t + r kTB)
@@ -425,8 +429,10 @@ __global__ __launch_bounds__(kTB) void mm_merge(VoxelJobDev A, VoxelJobDev B, Ma
   }
   __syncthreads();
   // runs: element k heads a run when its key differs from the previous element's; a run is output when one of its
-  // elements is kept (a cropped map point takes part in the order only) or it continues past the tile (the
-  // continuation is set elements, all kept); its centroid sums the kept points in merged order
+  // elements is kept (a cropped map point takes part in the order only); its centroid sums the kept points in merged
+  // order.  A run that continues past the tile is finished by the whole block: its continuation is the merged
+  // sequence after the tile — map elements first (within a voxel the map precedes the scan; cropped map points that
+  // map_idx saturated into this voxel among them, summed only when kept), then set elements (all kept)
   const unsigned long long next_key = s_key[cnt + 1];
   int nout = 0;
   // the new map's keys are strictly increasing when every centroid lies in its run's voxel; on an index overflow the
@@ -437,7 +443,6 @@ __global__ __launch_bounds__(kTB) void mm_merge(VoxelJobDev A, VoxelJobDev B, Ma
   __shared__ float s_cross[4];
   __shared__ int s_cross_n, s_cross_local;
   __shared__ unsigned long long s_cross_key;
-  if (t == 0) s_cross_local = -1;
 #pragma unroll
   for (int u = 0; u < PER; ++u) {
     ov[u] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -460,11 +465,12 @@ __global__ __launch_bounds__(kTB) void mm_merge(VoxelJobDev A, VoxelJobDev B, Ma
       else { c0 += p.x; c1 += p.y; c2 += p.z; c3 += p.w; }
       ++n;
     }
-    if (crosses) {   // finished cooperatively below
+    if (crosses) {   // finished cooperatively below (output only if a kept point is found)
       s_cross[0] = c0; s_cross[1] = c1; s_cross[2] = c2; s_cross[3] = c3;
       s_cross_n = n;
       s_cross_key = key;
-      cross_u = nout++;
+      s_has_cross = 1;
+      cross_u = nout;
       continue;
     }
     if (n == 0) continue;   // only cropped map points
@@ -472,6 +478,63 @@ __global__ __launch_bounds__(kTB) void mm_merge(VoxelJobDev A, VoxelJobDev B, Ma
     ov[nout++] = make_float4(c0 / cn, c1 / cn, c2 / cn, c3 / cn);
     if (mv_idx(V, c0 / cn, c1 / cn, c2 / cn) != (key & 0x7FFFFFFFull)) bad = true;
   }
+  __syncthreads();
+  if (s_has_cross) {   // block-uniform: the crossing run's continuation, chunk by chunk
+    const unsigned long long key = s_cross_key;
+    __shared__ int s_done;
+    __shared__ float4 s_cp[kTB];
+    __shared__ unsigned char s_cl[kTB];
+    // part 0: map elements i1m.. with the run's index (a prefix of each chunk: map indices never decrease); part 1:
+    // set elements j1.. (likewise a prefix)
+    for (int part = 0; part < 2; ++part) {
+      int jn = part ? j1 : i1m;
+      const int jend = part ? (V.full ? L : V.nset) : V.n0;
+      for (;;) {
+        const int j = jn + t;
+        bool in = false, live = false;
+        float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (j < jend) {
+          PointRec p;
+          if (part == 0) {
+            in = map_idx(V, j) == key;
+            if (in) live = mv_fetch(V, j, p);
+          } else {
+            in = (V.full ? (unsigned long long)skeys[V.base + j] : set_idx(V, j)) == key;
+            if (in) {
+              mv_fetch(V, svals[V.base + j], p);
+              live = true;
+            }
+          }
+          if (live) q = make_float4(p.x, p.y, p.z, p.intensity);
+        }
+        s_cp[t] = q;
+        s_cl[t] = live ? 1 : 0;
+        const int nin = __syncthreads_count(in);   // the run is a prefix of the chunk
+        if (t == 0) {
+          float c0 = s_cross[0], c1 = s_cross[1], c2 = s_cross[2], c3 = s_cross[3];
+          int n = s_cross_n;
+          for (int r = 0; r < nin; ++r) {
+            if (!s_cl[r]) continue;
+            const float4 p = s_cp[r];
+            if (n == 0) { c0 = p.x; c1 = p.y; c2 = p.z; c3 = p.w; }
+            else { c0 += p.x; c1 += p.y; c2 += p.z; c3 += p.w; }
+            ++n;
+          }
+          s_cross[0] = c0; s_cross[1] = c1; s_cross[2] = c2; s_cross[3] = c3;
+          s_cross_n = n;
+          s_done = nin < kTB;
+        }
+        __syncthreads();
+        jn += nin;
+        if (s_done) break;
+      }
+    }
+    if (cross_u >= 0) {
+      if (s_cross_n > 0) ++nout;   // (cross_u == the old nout: the crossing run is this thread's last)
+      else cross_u = -1;            // only cropped map points: no output (as a run inside a tile)
+    }
+  }
+  if (t == 0) s_cross_local = -1;
   // the tile's output order: block exclusive scan of the per-thread counts
   __shared__ int s_w[kTB / 64];
   const int lane = t & 63, w = t >> 6;
@@ -492,44 +555,6 @@ __global__ __launch_bounds__(kTB) void mm_merge(VoxelJobDev A, VoxelJobDev B, Ma
   const int lbase = wb + inc - nout;   // this thread's first output in the tile
   if (cross_u >= 0) s_cross_local = lbase + cross_u;
   __syncthreads();
-  if (s_cross_local >= 0) {   // block-uniform: the crossing run's continuation, chunk by chunk (set elements)
-    const unsigned long long key = s_cross_key;
-    __shared__ int s_done;
-    __shared__ float4 s_cp[kTB];
-    int jn = j1;   // the next set element (sorted order)
-    const int jend = V.full ? L : V.nset;
-    for (;;) {
-      const int j = jn + t;
-      bool in = false;
-      float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (j < jend) {
-        in = (V.full ? (unsigned long long)skeys[V.base + j] : set_idx(V, j)) == key;
-        if (in) {
-          PointRec p;
-          mv_fetch(V, svals[V.base + j], p);
-          q = make_float4(p.x, p.y, p.z, p.intensity);
-        }
-      }
-      s_cp[t] = q;
-      const int nin = __syncthreads_count(in);   // the run is a prefix of the chunk
-      if (t == 0) {
-        float c0 = s_cross[0], c1 = s_cross[1], c2 = s_cross[2], c3 = s_cross[3];
-        int n = s_cross_n;
-        for (int r = 0; r < nin; ++r) {
-          const float4 p = s_cp[r];
-          if (n == 0) { c0 = p.x; c1 = p.y; c2 = p.z; c3 = p.w; }
-          else { c0 += p.x; c1 += p.y; c2 += p.z; c3 += p.w; }
-          ++n;
-        }
-        s_cross[0] = c0; s_cross[1] = c1; s_cross[2] = c2; s_cross[3] = c3;
-        s_cross_n = n;
-        s_done = nin < kTB;
-      }
-      __syncthreads();
-      jn += nin;
-      if (s_done) break;
-    }
-  }
   // stage the outputs in tile order (s_pt, s_src are free now) and their cell keys (s_key)
 #pragma unroll
   for (int u = 0; u < PER; ++u) {
@@ -617,15 +642,11 @@ MergeCheck merge_check(MapMergeScratch& ms, unsigned seq) {
 
 void map_merge_launch(VoxelScratch2& vs, MapMergeScratch& ms, const VoxelJob& a, const VoxelJob& b, const MapKeys& ka,
                       const MapKeys& kb, const int* gate, unsigned seq, bool force_full, int violate_mod,
-                      const GridCountDev* grids, hipStream_t st) {
+                      const GridCountDev* grids, hipStream_t st, int per) {
   const VoxelJobDev A = to_dev(a, 0);
   const VoxelJobDev B = to_dev(b, a.n0_ub + a.n1_ub);
   const int nA = a.n0_ub + a.n1_ub, nB = b.n0_ub + b.n1_ub, n = std::max(nA + nB, 1);
-  // merged elements per tile: 256 threads x PER (FLOAM_MM_PER = 2 or 4, default 4)
-  static const int per = [] {
-    const char* e = std::getenv("FLOAM_MM_PER");
-    return e && std::atoi(e) == 2 ? 2 : 4;
-  }();
+  per = per == 2 ? 2 : 4;   // merged elements per tile: 256 threads x per
   const int tile = kTB * per;
   const int tilesA = std::max(1, (int)div_up(std::max(nA, 1), tile));
   const int tilesB = std::max(1, (int)div_up(std::max(nB, 1), tile));

@@ -179,6 +179,8 @@ struct LMBuffers {
   DevBuf<double> gpart;              // surf Gram matrix: per-block and per-group partials (geom_kernel)
   DevBuf<double> gmat;               // the solve's surf Gram matrix + its origin
   DevBuf<unsigned> gcnt;             // ticket words of the Gram reduction
+  int fail_test = 0;                 // FLOAM_LM_FAIL_TEST=1 (tests): every resident solve reports its hand-off as
+                                     // timed out (n_res < 0), the path a lost block would take
   void reserve(hipStream_t st);
 };
 

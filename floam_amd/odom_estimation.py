@@ -267,16 +267,27 @@ class OdomEstimationClass:
 
 
 def _pose_qt(pose):
-    """(q_xyzw, t) from a (q, t) pair or a 4x4 isometry."""
+    """(q_xyzw, t) from a (q, t) pair or a 4x4 isometry (numpy only: the branch on the largest of the trace and the
+    diagonal keeps the division away from zero for any rotation, then the quaternion is normalised)."""
     if isinstance(pose, np.ndarray) and pose.shape == (4, 4):
-        R = pose[:3, :3]
-        w = np.sqrt(max(0.0, 1.0 + R[0, 0] + R[1, 1] + R[2, 2])) / 2.0
-        if w > 1e-6:
-            q = np.array([(R[2, 1] - R[1, 2]) / (4 * w), (R[0, 2] - R[2, 0]) / (4 * w), (R[1, 0] - R[0, 1]) / (4 * w), w])
+        R = np.asarray(pose[:3, :3], dtype=np.float64)
+        tr = R[0, 0] + R[1, 1] + R[2, 2]
+        k = int(np.argmax([tr, R[0, 0], R[1, 1], R[2, 2]]))
+        if k == 0:
+            s = 2.0 * np.sqrt(1.0 + tr)
+            q = [(R[2, 1] - R[1, 2]) / s, (R[0, 2] - R[2, 0]) / s, (R[1, 0] - R[0, 1]) / s, s / 4.0]
+        elif k == 1:
+            s = 2.0 * np.sqrt(1.0 + R[0, 0] - R[1, 1] - R[2, 2])
+            q = [s / 4.0, (R[0, 1] + R[1, 0]) / s, (R[0, 2] + R[2, 0]) / s, (R[2, 1] - R[1, 2]) / s]
+        elif k == 2:
+            s = 2.0 * np.sqrt(1.0 + R[1, 1] - R[0, 0] - R[2, 2])
+            q = [(R[0, 1] + R[1, 0]) / s, s / 4.0, (R[1, 2] + R[2, 1]) / s, (R[0, 2] - R[2, 0]) / s]
         else:
-            from scipy.spatial.transform import Rotation
-            q = Rotation.from_matrix(R).as_quat()
-        return np.ascontiguousarray(q, dtype=np.float64), np.ascontiguousarray(pose[:3, 3], dtype=np.float64)
+            s = 2.0 * np.sqrt(1.0 + R[2, 2] - R[0, 0] - R[1, 1])
+            q = [(R[0, 2] + R[2, 0]) / s, (R[1, 2] + R[2, 1]) / s, s / 4.0, (R[1, 0] - R[0, 1]) / s]
+        q = np.asarray(q, dtype=np.float64)
+        q /= np.linalg.norm(q)
+        return np.ascontiguousarray(q), np.ascontiguousarray(pose[:3, 3], dtype=np.float64)
     q, t = pose
     return np.ascontiguousarray(q, dtype=np.float64), np.ascontiguousarray(t, dtype=np.float64)
 

@@ -17,6 +17,14 @@
 #ifndef FLOAM_C_H
 #define FLOAM_C_H
 
+/* ABI revision of this header.  Bumped whenever an entry point's parameter list changes, so that a caller compiled
+ * against an older header can refuse the library instead of passing arguments in the wrong slots:
+ *   1  round 1-2 entry points
+ *   2  floam_odom_keyframe_update gained the (surf, edge) cloud parameters of KeyFrameUpdate
+ *      (include/odomEstimationClass.h:80); floam_abi_version added
+ * A caller checks `floam_abi_version() == FLOAM_ABI_VERSION` once after loading the library. */
+#define FLOAM_ABI_VERSION 2
+
 #include <stddef.h>
 #include <stdint.h>
 
@@ -316,6 +324,7 @@ floam_status floam_odom_set_shard_callback(floam_odom* o, int rank, int world, f
 /* ------------------------------------------------------------------------------------------ misc */
 const char* floam_last_error(void);
 const char* floam_version(void);
+int floam_abi_version(void);   /* FLOAM_ABI_VERSION the library was built with */
 /* KeyFrameUpdate keeps a function-static `first` flag shared by every instance in the process
  * (src/odomEstimationClass.cpp:323, quirk Q6); this resets it (tests/bench only). */
 void floam_reset_process_state(void);

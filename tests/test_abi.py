@@ -3,6 +3,7 @@ product path fails loudly (no CPU fallback) when no gfx950 device is present."""
 import os
 import re
 
+import numpy as np
 import pytest
 
 from floam_amd import _ffi
@@ -52,3 +53,33 @@ def test_null_arguments_are_rejected():
     assert L.floam_lp_create(None, 0, C.byref(C.c_void_p())) == _ffi.ERR_INVALID_ARGUMENT
     assert L.floam_odom_get_pose(None, None, None) == _ffi.ERR_INVALID_ARGUMENT
     assert b"null" in L.floam_last_error()
+
+
+def test_abi_version_matches_header():
+    """floam_odom_keyframe_update's parameter list changed; the header carries FLOAM_ABI_VERSION and the
+    library reports the one it was built with, which the loader checks."""
+    import re
+    hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "floam_c.h")).read()
+    v = int(re.search(r"#define FLOAM_ABI_VERSION (\d+)", hdr).group(1))
+    assert _ffi.load().floam_abi_version() == v == _ffi.ABI_VERSION
+
+
+def test_pose_qt_any_rotation():
+    """the 4x4 -> quaternion conversion of the keyframe wrapper needs no scipy and is exact near 180 deg."""
+    from floam_amd.odom_estimation import _pose_qt
+    rng = np.random.default_rng(3)
+    for ang in [0.0, 1e-3, 1.0, np.pi - 1e-9, np.pi]:
+        for _ in range(20):
+            ax = rng.normal(size=3)
+            ax /= np.linalg.norm(ax)
+            K = np.array([[0, -ax[2], ax[1]], [ax[2], 0, -ax[0]], [-ax[1], ax[0], 0]])
+            R = np.eye(3) + np.sin(ang) * K + (1 - np.cos(ang)) * K @ K
+            T = np.eye(4)
+            T[:3, :3] = R
+            q, _ = _pose_qt(T)
+            x, y, z, w = q
+            R2 = np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                           [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                           [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
+            assert abs(np.linalg.norm(q) - 1.0) < 1e-12
+            np.testing.assert_allclose(R2, R, atol=1e-12)

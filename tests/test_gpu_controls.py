@@ -65,3 +65,34 @@ def test_untraced_pass_has_no_neighbour_indices(floam_gpu):
     odo.set_trace(16)
     with pytest.raises(FloamError, match="untraced"):
         odo.correspondences(0)
+
+
+def test_device_failure_poisons_the_handle(floam_gpu, monkeypatch):
+    """ADVICE r03: a solve whose blocks' hand-off timed out freezes the device controller (OdomDev::failed: no pose,
+    no keyframe, no map update from then on).  The update that failed raises FLOAM_ERR_DEVICE, and so must every later
+    update of the same handle — never a silent FLOAM_OK with stale odometry.  FLOAM_LM_FAIL_TEST=1 makes every resident
+    solve report its first hand-off as timed out."""
+    from floam_amd import FloamError
+    from floam_amd.odom_estimation import reset_process_state
+    monkeypatch.setenv("FLOAM_LM_FAIL_TEST", "1")
+    reset_process_state()
+    lp = floam_gpu.LaserProcessingClass()
+    lp.init(_params(16))
+    odo = floam_gpu.OdomEstimationClass()
+    odo.init(_params(16), 0.1, "Cauchy")
+    monkeypatch.delenv("FLOAM_LM_FAIL_TEST")   # (read once, when the handle is created)
+    clouds = []
+    for k in range(3):
+        de, ds = floam_gpu.DeviceCloud(), floam_gpu.DeviceCloud()
+        lp.featureExtraction(floam_gpu.DeviceCloud(synth.generate_scan("c1", k)), de, ds)
+        clouds.append((de, ds))
+    odo.initMapWithPoints(*clouds[0])
+    with pytest.raises(FloamError) as e1:
+        odo.UpdatePointsToMapSelector(*clouds[1], True)
+    assert "did not arrive" in str(e1.value)
+    with pytest.raises(FloamError) as e2:
+        odo.UpdatePointsToMapSelector(*clouds[2], True)
+    assert "earlier update" in str(e2.value) and "did not arrive" in str(e2.value)
+    # a fresh handle is unaffected
+    poses, _ = _run(floam_gpu, 3)
+    assert np.all(np.isfinite(poses[-1][1]))

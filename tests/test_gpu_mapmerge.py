@@ -11,8 +11,10 @@ pytestmark = pytest.mark.gpu
 
 VARIANTS = {"merge": {}, "full": {"FLOAM_MAP_FULL": "1"}, "voxelgrid": {"FLOAM_MAP_MERGE": "0"},
             # every other merge reports its keys out of order: the next update takes the full sort, then merges again
-            "fallback": {"FLOAM_MM_VIOLATE": "2"}}
-KNOBS = ("FLOAM_MAP_FULL", "FLOAM_MAP_MERGE", "FLOAM_MM_VIOLATE")
+            "fallback": {"FLOAM_MM_VIOLATE": "2"},
+            # 512-element merge tiles: more runs cross a tile edge
+            "merge512": {"FLOAM_MM_PER": "2"}}
+KNOBS = ("FLOAM_MAP_FULL", "FLOAM_MAP_MERGE", "FLOAM_MM_VIOLATE", "FLOAM_MM_PER")
 
 
 def _params(R):
@@ -87,3 +89,42 @@ def test_merge_long_sequence(floam_gpu, monkeypatch, prefilled_map):
     runs = {v: _run(floam_gpu, monkeypatch, v, "c2", 20, prefill) for v in ("merge", "voxelgrid")}
     assert sum(r[3] for r in runs["merge"]) >= 10, "too few keyframes to exercise the merge"
     _same(runs["merge"], runs["voxelgrid"], "c2 x 20 merge vs whole-map VoxelGrid")
+
+
+def _slab(x, y, z):
+    """map records on the grid x (outer) * y * z (inner): one per 0.1-m cell centre"""
+    from floam_amd.synth import POINT_DTYPE
+    X, Y, Z = np.meshgrid(np.asarray(x, np.float32), np.asarray(y, np.float32), np.asarray(z, np.float32),
+                          indexing="ij")
+    out = np.zeros(X.size, POINT_DTYPE)
+    out["x"], out["y"], out["z"] = X.ravel(), Y.ravel(), Z.ravel()
+    out["pad0"] = 1.0
+    out["intensity"] = (np.arange(X.size) % 251).astype(np.float32)
+    return out
+
+
+@pytest.mark.parametrize("variant", ["merge", "merge512"])
+def test_merge_crops_map_points(floam_gpu, monkeypatch, prefilled_map, variant):
+    """CropBox [t - 100, t + 100] removes map points once the sensor has moved; the merge saturates
+    a cropped point's index to the first / last cell of its row or plane (map_idx), so runs of several cropped points
+    — and a cropped point sharing its voxel index with a kept map point — occur and cross tile edges.  The C2 map is
+    prefilled with two slabs right inside the first update's crop box: one behind the sensor's direction of travel
+    (+x: a 0.1-m slice per scan leaves the box; its cropped points share a row's first index with the next kept
+    slice) and one at y = -100 (the trajectory drifts +y: whole slices leave at once and all of a z plane's cropped
+    points share one index).  Maps after every update byte-identical to the whole-map VoxelGrid's, never a NaN."""
+    E, S = prefilled_map("c2")
+    zs = np.arange(-1.45, 2.5, 0.1)
+    xslab = _slab(np.arange(-99.85, -97.9, 0.1), np.arange(-9.95, 10.0, 0.1), zs)
+    yslab = _slab(np.arange(-19.95, 20.0, 0.1), [-99.98, -99.94, -99.9, -99.86, -99.82], zs)
+    prefill = (np.concatenate([E, xslab, yslab]), np.concatenate([S, xslab, yslab]))
+    nscan = 20
+    runs = {v: _run(floam_gpu, monkeypatch, v, "c2", nscan, prefill) for v in (variant, "voxelgrid")}
+    assert sum(r[3] for r in runs[variant]) >= 10, "too few keyframes to exercise the merge"
+    for (_, e, s, _) in runs[variant]:
+        for m in (e, s):
+            assert np.all(np.isfinite(m["x"]) & np.isfinite(m["y"]) & np.isfinite(m["z"])), "NaN in the merged map"
+    # the slabs really were cropped along the way (the run's last map lost most of both)
+    e_last = runs[variant][-1][1]
+    assert np.count_nonzero(e_last["x"] < -97.8) < xslab.size // 4, "the x slab was not cropped"
+    assert np.count_nonzero(e_last["y"] < -99.8) < yslab.size // 2, "the y slab was not cropped"
+    _same(runs[variant], runs["voxelgrid"], f"c2 cropping slabs {variant} vs whole-map VoxelGrid")

@@ -338,6 +338,25 @@ def test_odometry_prefilled(floam_gpu, oracle_lib, prefilled_map, config, nscan)
         ref.clear_traces()
     me, ms = odo.map_sizes()
     assert me == ref.map(0).shape[0] and ms == ref.map(1).shape[0]
+    # map CONTENTS vs the oracle: the same voxels in the same order, coordinates within 1 ulp
+    # (the poses agree to ~1e-14, so a scan point's float transform can round differently by an ulp; the stable
+    # voxelisation sums in the same order on both sides)
+    _assert_map_close(odo.laserCloudCornerMap, ref.map(0), f"{config} corner map")
+    _assert_map_close(odo.laserCloudSurfMap, ref.map(1), f"{config} surf map")
+
+
+def _assert_map_close(g, r, what, ulps=1):
+    assert g.shape == r.shape, (what, g.shape, r.shape)
+    exact = 0
+    for f in ("x", "y", "z", "intensity"):
+        a, b = g[f].astype(np.float32), r[f].astype(np.float32)
+        assert np.all(np.isfinite(a)), (what, f, "non-finite map coordinate")
+        d = np.abs(a.astype(np.float64) - b.astype(np.float64))
+        tol = ulps * np.spacing(np.maximum(np.abs(a), np.abs(b))).astype(np.float64)
+        bad = np.flatnonzero(d > tol)
+        assert bad.size == 0, (what, f, int(bad.size), bad[:5].tolist(), a[bad[:5]].tolist(), b[bad[:5]].tolist())
+        exact += int(np.count_nonzero(a.view(np.uint32) == b.view(np.uint32)))
+    return exact
 
 
 @pytest.mark.parametrize("config,nscan", [("c3", 3), ("c5", 3)])
