@@ -92,6 +92,11 @@ def main():
     ap.add_argument("--precision", choices=["fp64", "fp32", "fp32g"], default="fp64",
                     help="residual / Jacobian precision (floam_odom_set_precision): fp64 = the reference's (default); "
                          "fp32 = float residuals / Jacobians; fp32g = float line / plane fits too (C5 sweep)")
+    ap.add_argument("--shard-comm", choices=["peer", "rccl"], default=os.environ.get("FLOAM_SHARD_COMM", "peer"),
+                    help="sharded solve: peer = one resident LM launch per solve exchanging the ranks' sums through "
+                         "IPC-mapped buffers (floam_odom_set_shard_peers; default), rccl = one launch + one "
+                         "ncclAllReduce per LM evaluation (floam_odom_set_shard)")
+    ap.add_argument("--no-c3-shard", action="store_true", help="N > 1 shard mode: skip the extra C3 sharded line")
     ap.add_argument("--json-out", default="")
     args = ap.parse_args()
 
@@ -150,15 +155,49 @@ def main():
             dist.broadcast_object_list(uid, src=0)
     n_pipelines = 0
 
-    def make_pipeline(loss=LOSS, sharded=True):
+    peer_ok = [args.shard_comm == "peer"]
+
+    def set_peers(odo):
+        """peer sharding: every rank's exchange-buffer IPC handle, gathered over the control plane (gloo); False
+        (RCCL instead) when any rank cannot map the others' buffers"""
+        ok = True
+        try:
+            h, _ = odo.shard_exchange()
+        except floam_amd.FloamError as e:
+            log(f"[rank {rank}] peer exchange buffer unavailable ({e})")
+            ok, h = False, b""
+        handles = [None] * world
+        dist.all_gather_object(handles, h)
+        if ok and all(len(x) == 64 for x in handles):
+            try:
+                odo.set_shard_peers(rank, world, handles=handles)
+            except floam_amd.FloamError as e:
+                log(f"[rank {rank}] peer mapping failed ({e})")
+                ok = False
+        import torch
+        t = torch.tensor([0 if ok else 1], dtype=torch.int32)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return int(t.item()) == 0
+
+    def make_pipeline(loss=LOSS, sharded=True, params_=None, maps=None):
         nonlocal allreduce_impl, n_pipelines
+        params_ = params_ or params
+        joint = uid is not None and sharded and dist is not None   # every rank builds this pipeline together
         reset_process_state()
         lp = floam_amd.LaserProcessingClass(device=dev, asynchronous=True)   # the odometry collects the counts
-        lp.init(params)
+        lp.init(params_)
         odo = floam_amd.OdomEstimationClass(device=dev)
-        odo.init(params, MAP_RES, loss)
+        odo.init(params_, MAP_RES, loss)
         if args.precision != "fp64":
             odo.set_precision(True, geometry=args.precision == "fp32g")
+        if uid is not None and sharded and world > 1 and peer_ok[0]:
+            if set_peers(odo):
+                allreduce_impl = "peer"
+                n_pipelines += 1
+                sharded = False   # (configured)
+            else:
+                log(f"[rank {rank}] peer sharding unavailable: RCCL all-reduce instead")
+                peer_ok[0] = False
         if uid is not None and sharded:
             try:
                 odo.set_shard(rank, world, uid[0][n_pipelines])   # RCCL over xGMI
@@ -173,8 +212,11 @@ def main():
                 odo.set_shard_callback(rank, world, _allreduce)
                 allreduce_impl = "gloo-host"
             n_pipelines += 1
-        odo.initMapWithPoints(d_mapE, d_mapS)
+        m = maps or (d_mapE, d_mapS)
+        odo.initMapWithPoints(m[0], m[1])
         odo.set_async(DEPTH)
+        if joint:
+            dist.barrier()   # (sharded ranks start their solves together: a peer waits for the others' sums)
         return lp, odo
 
     # feature buffers: the extraction of scan k+1 (its own stream) is issued before the odometry of scan k, so the
@@ -183,26 +225,26 @@ def main():
     # needs no cross-stream wait on the odometry stream
     bufs = [(floam_amd.DeviceCloud(device=dev), floam_amd.DeviceCloud(device=dev)) for _ in range(max(3, DEPTH + 1))]
 
-    def extract(lp, k):
+    def extract(lp, k, src=None):
         e, s = bufs[k % len(bufs)]
         e.clear()
         s.clear()
-        lp.featureExtraction(d_raw[k], e, s)
+        lp.featureExtraction((src or d_raw)[k], e, s)
 
     host_split = [0.0, 0.0]   # host seconds issuing / waiting (diagnostic, FLOAM_BENCH_HOST=1)
 
     host_trace = [] if os.environ.get("FLOAM_BENCH_HOST_TRACE") else None   # (diagnostic) monotonic ns per scan
 
-    def run(lp, odo, a, b, poses):
+    def run(lp, odo, a, b, poses, src=None):
         """scans [a, b): featureExtraction + UpdatePointsToMapSelector each, extraction one scan ahead; the odometry
         streams (floam_odom_set_async): scan k's pose is collected after scan k+1 has been issued"""
         if a < b:
-            extract(lp, a)
+            extract(lp, a, src)
         for k in range(a, b):
             t0 = time.perf_counter()
             m0 = time.monotonic_ns()
             if k + 1 < b:
-                extract(lp, k + 1)
+                extract(lp, k + 1, src)
             m1 = time.monotonic_ns()
             e, s = bufs[k % len(bufs)]
             odo.UpdatePointsToMapSelector(e, s, True)
@@ -388,6 +430,63 @@ def main():
                          "floam_cloud_upload x2, floam_odom_update_selector (async off, deskew), size+download x2 (Q5), "
                          "floam_odom_get_pose, floam_odom_get_last_pose (INTEGRATION.md adapters)"}
 
+    def dropin_host(ref_poses):
+        """The drop-in contract through the one-call host entry points the INTEGRATION.md adapters use when built
+        against ABI 2 (floam_lp_feature_extraction_host, floam_odom_update_selector_host): per scan one upload + the
+        extraction + both downloads with one synchronisation, then both uploads + the synchronous update with the
+        deskewed records copied back (Q5) on a copy stream while the update's second call runs, + the two pose reads."""
+        reset_process_state()
+        lp_ = floam_amd.LaserProcessingClass(device=dev)
+        lp_.init(params)
+        odo_ = floam_amd.OdomEstimationClass(device=dev)
+        odo_.init(params, MAP_RES, LOSS)
+        odo_.initMapWithPoints(d_mapE, d_mapS)
+        hL, h_lp, h_odo = L, lp_._h, odo_._h
+        he = np.zeros(R * 120 + 1, synth.POINT_DTYPE)
+        hs = np.zeros(raws[0].shape[0] + 1024, synth.POINT_DTYPE)
+        vp = C.c_void_p
+        q, t, q2, t2 = np.zeros(4), np.zeros(3), np.zeros(4), np.zeros(3)
+        qp, tp = q.ctypes.data_as(C.POINTER(C.c_double)), t.ctypes.data_as(C.POINTER(C.c_double))
+        q2p, t2p = q2.ctypes.data_as(C.POINTER(C.c_double)), t2.ctypes.data_as(C.POINTER(C.c_double))
+        ne, ns = C.c_size_t(), C.c_size_t()
+        seg = np.zeros(3)
+        got = []
+
+        def one(k):
+            raw = raws[k]
+            t0 = time.perf_counter()
+            _ffi.check(hL.floam_lp_feature_extraction_host(h_lp, vp(raw.ctypes.data), raw.shape[0], 32,
+                                                           vp(he.ctypes.data), he.shape[0], C.byref(ne),
+                                                           vp(hs.ctypes.data), hs.shape[0], C.byref(ns)))
+            t1 = time.perf_counter()
+            _ffi.check(hL.floam_odom_update_selector_host(h_odo, vp(he.ctypes.data), ne.value, vp(hs.ctypes.data),
+                                                          ns.value, 32, 1))
+            t2_ = time.perf_counter()
+            _ffi.check(hL.floam_odom_get_pose(h_odo, qp, tp))
+            _ffi.check(hL.floam_odom_get_last_pose(h_odo, q2p, t2p))
+            t3 = time.perf_counter()
+            return np.array([t1 - t0, t2_ - t1, t3 - t2_])
+
+        for k in range(args.warmup):
+            one(k)
+            got.append((q.copy(), t.copy()))
+        t_start = time.perf_counter()
+        for k in range(args.warmup, n_scans):
+            seg += one(k)
+            got.append((q.copy(), t.copy()))
+        dt = time.perf_counter() - t_start
+        same = all(np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) for a, b in zip(ref_poses, got))
+        odo_.close()
+        lp_.close()
+        us = 1e6 / args.steps
+        return {"value": round(args.steps / dt, 2), "unit": "scans/s", "ms_per_scan": round(1e3 * dt / args.steps, 3),
+                "poses_equal_resident_run": bool(same),
+                "segments_us_per_scan": {"feature_extraction_host": round(seg[0] * us, 1),
+                                         "update_selector_host": round(seg[1] * us, 1),
+                                         "poses": round(seg[2] * us, 1)},
+                "calls": "per scan: floam_lp_feature_extraction_host, floam_odom_update_selector_host (deskew), "
+                         "floam_odom_get_pose, floam_odom_get_last_pose"}
+
     secondary = None
     if rank == 0 and world == 1 and not args.no_secondary:
         odo.close()
@@ -409,7 +508,7 @@ def main():
         secondary = {"feature_extraction_alone": {"value": round(args.steps / fe_dt, 2), "unit": "scans/s"},
                      "huber": {"value": round(args.steps / hub_dt, 3), "unit": "scans/s",
                                "loss": "huber (HuberLoss(0.1))"},
-                     "dropin_sync": dropin_sync(poses)}
+                     "dropin_sync": dropin_sync(poses), "dropin_host": dropin_host(poses)}
 
     cpu = None
     pose_err = None
@@ -459,6 +558,60 @@ def main():
             for k, (et, er) in enumerate(errs):
                 log(f"[pose] scan {k + 1}: {et:.3e} m {er:.3e} rad")
 
+    c3_line = None
+    if mode == "shard" and world > 1 and cfg != "c3" and not args.no_c3_shard:
+        # the headline config sharded too, beside the C4 line (same scheme: max over ranks of the
+        # timed region; rank 0 first times it unsharded on its own GPU)
+        odo.close()
+        lp.close()
+        m3 = synth.lidar_model("c3")
+        p3 = floam_amd.LidarParams(num_lines=m3.rings, scan_period=SCAN_PERIOD, vertical_angle=2.0,
+                                   max_distance=MAX_DIS, min_distance=MIN_DIS)
+        fe3 = floam_amd.LaserProcessingClass(device=dev)
+        fe3.init(p3)
+
+        def gpu_fe3(raw, R_):
+            de, ds = floam_amd.DeviceCloud(device=dev), floam_amd.DeviceCloud(device=dev)
+            fe3.featureExtraction(floam_amd.DeviceCloud(raw, device=dev), de, ds)
+            return de.download(), ds.download()
+
+        raws3 = [synth.generate_scan("c3", k) for k in range(1, n_scans + 1)]
+        mE3, mS3 = synth.prefill_map("c3", gpu_fe3, synth.MAP_PREFILL.get("c3", 0))
+        fe3.close()
+        d_raw3 = [floam_amd.DeviceCloud(r, device=dev) for r in raws3]
+        maps3 = (floam_amd.DeviceCloud(mE3, device=dev), floam_amd.DeviceCloud(mS3, device=dev))
+        c3_1gpu = None
+        if rank == 0:
+            lp3, odo3 = make_pipeline(sharded=False, params_=p3, maps=maps3)
+            ps3 = []
+            run(lp3, odo3, 0, args.warmup, ps3, d_raw3)
+            _ffi.check(L.floam_device_synchronize(dev))
+            t1 = time.perf_counter()
+            run(lp3, odo3, args.warmup, n_scans, ps3, d_raw3)
+            _ffi.check(L.floam_device_synchronize(dev))
+            c3_1gpu = round(args.steps / (time.perf_counter() - t1), 3)
+            odo3.close()
+            lp3.close()
+        lp3, odo3 = make_pipeline(params_=p3, maps=maps3)
+        ps3 = []
+        run(lp3, odo3, 0, args.warmup, ps3, d_raw3)
+        barrier_sync()
+        t1 = time.perf_counter()
+        run(lp3, odo3, args.warmup, n_scans, ps3, d_raw3)
+        barrier_sync()
+        import torch
+        t = torch.tensor([time.perf_counter() - t1], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        odo3.close()
+        lp3.close()
+        c3_line = {"value": round(args.steps / float(t.item()), 3), "unit": "scans/s",
+                   "config": f"c3: {m3.rings}-ring synthetic scans ({raws3[0].shape[0]} pts), map prefilled "
+                             f"{synth.MAP_PREFILL.get('c3', 0)} pts, sharded like the main line ({allreduce_impl})",
+                   "same_config_1gpu": c3_1gpu}
+        for c in list(d_raw3) + list(maps3):
+            c.close()
+        lp, odo = None, None
+
     if rank == 0:
         gt_err = []
         for k, (q, t) in enumerate(poses):
@@ -466,7 +619,10 @@ def main():
             gt_err.append(float(np.linalg.norm(T[:3, 3] - t)))
         total_scans = args.steps * (world if mode == "replica" else 1)
         value = total_scans / elapsed
-        if mode == "shard":
+        if mode == "shard" and allreduce_impl == "peer":
+            par = (f"query-shard x{world} (resident LM solve: the ranks' J^T J / J^T r / cost exchanged through "
+                   f"IPC-mapped peer buffers once per LM evaluation, no collective launch)")
+        elif mode == "shard":
             par = f"query-shard x{world} ({allreduce_impl} all-reduce of J^T J per LM evaluation)"
         else:
             par = f"replica x{world}" if world > 1 else "single GPU"
@@ -487,6 +643,8 @@ def main():
             "secondary": secondary,
             "last_scan_stats": {k: (int(v) if isinstance(v, int) else v) for k, v in stats.items()},
         }
+        if c3_line is not None:
+            out["c3_sharded"] = c3_line
         if same_cfg_1gpu is not None:
             out["same_config_1gpu"] = {"value": same_cfg_1gpu, "unit": "scans/s",
                                        "note": f"{cfg} unsharded on rank 0's GPU before the sharded run"}
@@ -495,8 +653,9 @@ def main():
         if args.json_out:
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
-    odo.close()
-    lp.close()
+    if odo is not None:
+        odo.close()
+        lp.close()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

@@ -12,7 +12,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libfloam_amd.so")
 
 # floam_status (include/floam_c.h)
-ABI_VERSION = 2   # FLOAM_ABI_VERSION of include/floam_c.h this package binds
+ABI_VERSION = 3   # FLOAM_ABI_VERSION of include/floam_c.h this package binds
 OK = 0
 ERR_INVALID_ARGUMENT = 1
 ERR_DEVICE = 2
@@ -42,6 +42,8 @@ EXPORTS = [
     "floam_odom_set_trace", "floam_odom_get_traces", "floam_odom_get_correspondences",
     "floam_odom_find_correspondences",
     "floam_comm_unique_id", "floam_odom_set_shard", "floam_odom_set_shard_callback",
+    "floam_odom_shard_exchange", "floam_odom_set_shard_peers",
+    "floam_lp_feature_extraction_host", "floam_odom_update_selector_host",
     "floam_last_error", "floam_version", "floam_abi_version", "floam_reset_process_state", "floam_device_synchronize",
     "floam_profile_enable", "floam_profile_read", "floam_profile_reset", "floam_profile_mark",
     "floam_imu_create", "floam_imu_destroy", "floam_imu_add_msg", "floam_imu_add_msgs", "floam_imu_size",
@@ -121,6 +123,8 @@ def load(path: str | None = None):
         "floam_odom_get_map": [vp, vp], "floam_odom_get_map_sizes": [vp, szp, szp],
         "floam_odom_download_maps": [vp, vp, sz, vp, sz], "floam_odom_get_stats": [vp, C.POINTER(OdomStats)],
         "floam_odom_set_async": [vp, i32], "floam_odom_wait": [vp, sz, dp, sz, szp],
+        "floam_lp_feature_extraction_host": [vp, vp, sz, sz, vp, sz, szp, vp, sz, szp],
+        "floam_odom_update_selector_host": [vp, vp, sz, vp, sz, sz, i32],
         "floam_odom_keyframe_update": [vp, vp, vp, dp, dp, ip],
         "floam_odom_get_keyframe": [vp, sz, dp, dp, vp, vp, szp], "floam_odom_set_precision": [vp, i32],
         "floam_odom_set_trace": [vp, sz], "floam_odom_get_traces": [vp, dp, sz, szp],
@@ -128,6 +132,7 @@ def load(path: str | None = None):
         "floam_odom_find_correspondences": [vp, vp, vp, dp, dp],
         "floam_comm_unique_id": [vp], "floam_odom_set_shard": [vp, i32, i32, vp],
         "floam_odom_set_shard_callback": [vp, i32, i32, ALLREDUCE_FN, vp],
+        "floam_odom_shard_exchange": [vp, vp, C.POINTER(vp)], "floam_odom_set_shard_peers": [vp, i32, i32, vp, vp],
         "floam_device_synchronize": [i32], "floam_profile_enable": [i32, i32],
         "floam_profile_read": [i32, C.POINTER(KernelTiming), i32, C.POINTER(C.c_int)], "floam_profile_reset": [i32], "floam_profile_mark": [i32, i32],
         "floam_imu_create": [i32, pp], "floam_imu_destroy": [vp], "floam_imu_add_msg": [vp, dbl, dp, ip],

@@ -1,0 +1,103 @@
+// Stable sort of the VoxelGrid pipelines' (u32 key, i32 value) pairs in two launches after the key producer —
+// see bucket.hip.  Keys carry the cloud in bit 31 (vox_keys / mm_keys); 0xFFFFFFFF marks a dropped element and
+// sorts last.
+#pragma once
+#include "floam_common.hpp"
+#include "radix.hpp"
+
+namespace floam {
+
+constexpr int kBuckets = 256;     // buckets 0..254 hold keys (254 splitters), 255 the dropped elements
+constexpr int kSplitters = kBuckets - 2;
+constexpr int kBucketCap = 4096;  // sorted in registers by one block; a larger bucket streams through global memory
+constexpr int kGeoWords = 16;     // per job j: geo[8 j + 0..2] min_b, +3 dx, +4 dy, +5 index overflow (Q9)
+
+struct BucketScratch {
+  DevBuf<unsigned long long> split;   // [kSplitters] (job << 63 | cell key) at the quantiles of the previous sort
+  DevBuf<uint8_t> bkt;                // per element: its bucket (the scatter's digit)
+  DevBuf<int> geo;                    // [kGeoWords] the key producer's grids (cell key <-> voxel index)
+  bool seeded = false;                // host: split holds quantiles (else this sort takes the digit passes and seeds)
+  void reserve(int n, hipStream_t st);
+};
+
+// The key producer's view (all null: the four digit passes of radix.hip follow instead)
+struct BucketDev {
+  const unsigned long long* split;
+  uint8_t* bkt;
+  int* geo;
+};
+
+// Producer side.  bucket_keys_lds: the splitters as 32-bit sort keys of the calling block's cloud `job` (its grid: min_b,
+// dx, dy, dz, overflow), in LDS s[256] (ascending; the other cloud's splitters collapse to 0 below / ~0 above):
+// a splitter cell outside the grid saturates to the grid's first / last cell of its row, plane or grid, which keeps the
+// order.  All threads call it (it ends with a barrier).  bucket_of: the bucket of a sort key.
+__device__ __forceinline__ void bucket_keys_lds(const unsigned long long* __restrict__ split, int job, const int (&mb)[3],
+                                                long long dx, long long dy, long long dz, bool ovf, uint32_t* s) {
+  const int t = threadIdx.x;
+  for (int m = t; m < kBuckets; m += blockDim.x) {
+    uint32_t v = 0xFFFFFFFFu;
+    if (m < kSplitters) {
+      const unsigned long long sp = split[m];
+      const int sj = (int)(sp >> 63);
+      if (sj < job) {
+        v = 0u;
+      } else if (sj == job) {
+        if (ovf) {
+          v = ((uint32_t)job << 31) | 0x7FFFFFFFu;   // identity keys (Q9): the whole cloud in one bucket
+        } else {
+          const unsigned long long ck = sp & 0x7FFFFFFFFFFFFFFFull;
+          const long long cx = (long long)(ck & 0x1FFFFFull) - (1 << 20) - mb[0];
+          const long long cy = (long long)((ck >> 21) & 0x1FFFFFull) - (1 << 20) - mb[1];
+          const long long cz = (long long)((ck >> 42) & 0x1FFFFFull) - (1 << 20) - mb[2];
+          const long long plane = dx * dy;
+          long long idx;
+          if (cz < 0) idx = 0;
+          else if (cz >= dz) idx = plane * dz - 1;
+          else if (cy < 0) idx = cz * plane;
+          else if (cy >= dy) idx = cz * plane + plane - 1;
+          else if (cx < 0) idx = cz * plane + cy * dx;
+          else if (cx >= dx) idx = cz * plane + cy * dx + dx - 1;
+          else idx = cz * plane + cy * dx + cx;
+          idx = idx < 0 ? 0 : (idx > 0x7FFFFFFEll ? 0x7FFFFFFEll : idx);
+          v = ((uint32_t)job << 31) | (uint32_t)idx;
+        }
+      }
+    }
+    s[m] = v;
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ unsigned bucket_of(const uint32_t* s, uint32_t key) {
+  if (key == 0xFFFFFFFFu) return kBuckets - 1;
+  unsigned b = 0;   // splitters <= key among s[0 .. 253] (s[254], s[255] = ~0 never count)
+#pragma unroll
+  for (int step = 128; step > 0; step >>= 1)
+    if (s[b + step - 1] <= key) b += step;
+  return b;
+}
+
+// the producer's grid of cloud `job` for the next splitters (block 0 of the job, one thread)
+__device__ __forceinline__ void bucket_geo_store(int* geo, int job, const int (&mb)[3], int dx, int dy, bool ovf) {
+  int* g = geo + 8 * job;
+  g[0] = mb[0]; g[1] = mb[1]; g[2] = mb[2];
+  g[3] = dx; g[4] = dy; g[5] = ovf ? 1 : 0;
+}
+
+// Sort-only form (the map merge, mapmerge.hip): scatter by bucket (one stable digit pass: the producer's bucket
+// histogram is that pass's, in rs.ctl), then one block per bucket sorts it into k0 / v0 and writes the next
+// splitters.  The producer must have run with the BucketDev of bs (bs.seeded) — else use radix_sort_launch followed
+// by bucket_seed_launch.
+void bucket_sort_launch(BucketScratch& bs, RadixScratch& rs, uint32_t* k0, int* v0, uint32_t* k1, int* v1, int n,
+                        hipStream_t st, const int* gate, const int* n_dev);
+
+// After a digit-pass sort of the same pipeline (sorted keys in k0, n_dev elements): the first splitters, from its
+// quantiles (one block)
+void bucket_seed_launch(BucketScratch& bs, const uint32_t* k0, const int* n_dev, int n, hipStream_t st,
+                        const int* gate);
+
+// pipeline 0: the VoxelGrids (voxel2_launch), 1: the map merge (map_merge_launch).  FLOAM_SORT=radix|bucket|merge
+// (read once per process; default bucket: both pipelines)
+bool bucket_sort_enabled(int pipeline);
+
+}  // namespace floam

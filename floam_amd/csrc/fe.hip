@@ -498,8 +498,216 @@ __global__ __launch_bounds__(kSortThreads) void fe_sector(const int* __restrict_
                                        surf_pos, status, stamps, long_list, long_count);
 }
 
-// the listed long sectors (1024 < m <= 4096; longer: FE_STATUS_SECTOR_TOO_LONG), a few blocks looping over the list
-// (a grid of one block per sector would cost a launch of 6 R blocks that nearly all find nothing to do)
+// ---- sectors beyond 4096 entries (a ring of more than ~24.6k points: e.g. a cloud whose ring field is all zero,
+// which PCL produces when the field is absent): the sector of src/laserProcessingClass.cpp:88-231 through global
+// memory by one block — curvature keys, a stable LSD sort of the 64-bit keys in entry order (ties keep ascending
+// entries: the (value, entry) order of the LDS networks), the reference's serial greedy pick (:129-170) by one thread,
+// the surf compaction (:220-227).  Slow; for inputs the fast path cannot hold.
+// Concurrent huge sectors (several blocks) keep apart: keys and entries at the sector's ring-major position off + a
+// (n each), the per-point flags at off + a + 10 sec (its m + 10 staged points; n + 60 R each).
+struct HugeScratch {
+  unsigned long long *k0, *k1;   // curvature keys (ping-pong)
+  int *i0, *i1;                  // entries
+  uint8_t *picked, *gap;         // per staged point: picked; far from the next point (the suppression test)
+};
+
+__device__ __forceinline__ unsigned long long match8(unsigned d, bool valid) {
+  unsigned long long m = __ballot(valid);
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    const bool bit = (d >> b) & 1u;
+    const unsigned long long v = __ballot(bit);
+    m &= bit ? v : ~v;
+  }
+  return m;
+}
+
+__device__ void fe_sector_huge(int sec, const int* __restrict__ ring_count, const float4* __restrict__ ring_xyz,
+                               int* __restrict__ sec_edge_cnt, int* __restrict__ sec_edge_pos,
+                               int* __restrict__ sec_surf_cnt, int* __restrict__ surf_pos, int* __restrict__ status,
+                               const HugeScratch& H) {
+  constexpr int TB = kSortThreads, R8 = 8, CH = TB * R8, NW = TB / 64;
+  __shared__ int s_off;
+  __shared__ unsigned s_cnt[NW][256], s_base[256], s_run[256], s_off8[257], s_ws[NW];
+  __shared__ unsigned long long s_mm[2][NW];
+  __shared__ int s_edges[kMaxEdgesPerSector], s_nedge, smem[33];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int r = sec / 6, s = sec % 6;
+  const int n_r = ring_count[r];
+  int a, b;
+  sector_range(n_r, s, a, b);
+  const int m = b - a, npts = m + 10;
+  const int off = ring_offset(ring_count, r, &s_off);
+  if (!H.k0) {   // (fe_launch reserves the scratch whenever a sector can exceed 4096 entries: never expected)
+    if (t == 0) { atomicOr(status, FE_STATUS_SECTOR_TOO_LONG); sec_edge_cnt[sec] = 0; sec_surf_cnt[sec] = 0; }
+    return;
+  }
+  const float4* P = ring_xyz + off + a;   // staged points [0, m + 10): entry k's stencil is points k .. k + 10
+  unsigned long long* const K0 = H.k0 + off + a;
+  unsigned long long* const K1 = H.k1 + off + a;
+  int* const I0 = H.i0 + off + a;
+  int* const I1 = H.i1 + off + a;
+  uint8_t* const PK = H.picked + off + a + 10 * sec;
+  uint8_t* const GP = H.gap + off + a + 10 * sec;
+  unsigned long long mn = ~0ull, mx = 0ull;
+  for (int k = t; k < m; k += TB) {   // curvature (:95-101) in the float summation order, double squares
+    const int c = k + 5;
+    float4 q[11];
+#pragma unroll
+    for (int j = 0; j < 11; ++j) q[j] = P[c - 5 + j];
+    const float fx = q[0].x + q[1].x + q[2].x + q[3].x + q[4].x - 10 * q[5].x + q[6].x + q[7].x + q[8].x + q[9].x + q[10].x;
+    const float fy = q[0].y + q[1].y + q[2].y + q[3].y + q[4].y - 10 * q[5].y + q[6].y + q[7].y + q[8].y + q[9].y + q[10].y;
+    const float fz = q[0].z + q[1].z + q[2].z + q[3].z + q[4].z - 10 * q[5].z + q[6].z + q[7].z + q[8].z + q[9].z + q[10].z;
+    const double dX = fx, dY = fy, dZ = fz;
+    const unsigned long long v = (unsigned long long)__double_as_longlong(dX * dX + dY * dY + dZ * dZ);
+    K0[k] = v;
+    I0[k] = k;
+    mn = v < mn ? v : mn;
+    mx = v > mx ? v : mx;
+  }
+  for (int j = t; j < npts; j += TB) {   // the neighbour test (:151-166) between consecutive points, once per pair
+    bool gap = false;
+    if (j + 1 < npts) {
+      const float4 p0 = P[j], p1 = P[j + 1];
+      const double dX = p1.x - p0.x, dY = p1.y - p0.y, dZ = p1.z - p0.z;
+      gap = dX * dX + dY * dY + dZ * dZ > 0.05;
+    }
+    GP[j] = gap ? 1 : 0;
+    PK[j] = 0;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long a2 = __shfl_xor(mn, o, 64), b2 = __shfl_xor(mx, o, 64);
+    mn = a2 < mn ? a2 : mn;
+    mx = b2 > mx ? b2 : mx;
+  }
+  if (lane == 0) { s_mm[0][w] = mn; s_mm[1][w] = mx; }
+  __syncthreads();
+  unsigned long long kmin = s_mm[0][0], kmax = s_mm[1][0];
+  for (int k = 1; k < NW; ++k) {
+    kmin = s_mm[0][k] < kmin ? s_mm[0][k] : kmin;
+    kmax = s_mm[1][k] > kmax ? s_mm[1][k] : kmax;
+  }
+  const unsigned long long range = kmax - kmin;
+  const int npass = range ? (64 - __clzll((long long)range) + 7) / 8 : 0;
+  unsigned long long *ks = K0, *kd = K1;
+  int *is = I0, *id = I1;
+  for (int p = 0; p < npass; ++p) {   // stable LSD passes over the keys' varying bytes
+    const int sh = 8 * p;
+    s_run[t] = 0u;
+    __syncthreads();
+    for (int e = t; e < m; e += TB) atomicAdd(&s_run[((ks[e] - kmin) >> sh) & 255u], 1u);
+    __syncthreads();
+    {
+      const unsigned c = s_run[t];
+      unsigned inc = c;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const unsigned u = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += u;
+      }
+      if (lane == 63) s_ws[w] = inc;
+      __syncthreads();
+      unsigned add = 0;
+      for (int k = 0; k < w; ++k) add += s_ws[k];
+      s_base[t] = add + inc - c;
+      s_run[t] = 0u;
+      __syncthreads();
+    }
+    for (int c0 = 0; c0 < m; c0 += CH) {   // chunks in order; within a chunk a stable rank by wave ballots
+      const int nc = min(CH, m - c0);
+      unsigned long long key[R8];
+      int val[R8];
+      unsigned dig[R8], rank[R8];
+      for (int k = t; k < NW * 256; k += TB) (&s_cnt[0][0])[k] = 0u;
+#pragma unroll
+      for (int rr = 0; rr < R8; ++rr) {
+        const int e = w * 64 * R8 + rr * 64 + lane;
+        key[rr] = e < nc ? ks[c0 + e] : 0ull;
+        val[rr] = e < nc ? is[c0 + e] : 0;
+        dig[rr] = (unsigned)(((key[rr] - kmin) >> sh) & 255u);
+      }
+      __syncthreads();
+      const unsigned long long lt = (1ull << lane) - 1ull;
+#pragma unroll
+      for (int rr = 0; rr < R8; ++rr) {
+        const int e = w * 64 * R8 + rr * 64 + lane;
+        const bool valid = e < nc;
+        const unsigned long long peers = match8(dig[rr], valid);
+        const unsigned before = s_cnt[w][dig[rr]];
+        rank[rr] = before + (unsigned)__popcll(peers & lt);
+        if (valid && lane == 63 - __clzll((long long)peers)) s_cnt[w][dig[rr]] = before + (unsigned)__popcll(peers);
+      }
+      __syncthreads();
+      unsigned tot = 0;
+      for (int k = 0; k < NW; ++k) {   // thread t = digit t: offsets of the waves within the chunk's digit
+        const unsigned v = s_cnt[k][t];
+        s_cnt[k][t] = tot;
+        tot += v;
+      }
+      s_off8[t] = tot;   // the chunk's count of digit t
+      __syncthreads();
+#pragma unroll
+      for (int rr = 0; rr < R8; ++rr) {
+        const int e = w * 64 * R8 + rr * 64 + lane;
+        if (e >= nc) continue;
+        const unsigned d = dig[rr];
+        const unsigned dst = s_base[d] + s_run[d] + s_cnt[w][d] + rank[rr];
+        kd[dst] = key[rr];
+        id[dst] = val[rr];
+      }
+      __syncthreads();
+      s_run[t] += s_off8[t];
+      __syncthreads();
+    }
+    unsigned long long* tk = ks; ks = kd; kd = tk;
+    int* ti = is; is = id; id = ti;
+  }
+  __threadfence_block();
+  __syncthreads();
+  // greedy edge pick (:129-170): the entries in descending (value, entry) order, the reference's loop, one thread
+  if (t == 0) {
+    int picked_num = 0, nedge = 0;
+    for (int i = m - 1; i >= 0; --i) {
+      const int ind = is[i] + 5;
+      if (PK[ind]) continue;
+      if (__longlong_as_double((long long)ks[i]) <= 0.1) break;
+      ++picked_num;
+      if (picked_num > 20) {   // picked, not kept (Q1), and the loop ends
+        PK[ind] = 1;
+        break;
+      }
+      s_edges[nedge++] = ind;
+      PK[ind] = 1;
+      for (int k = 1; k <= 5 && !GP[ind + k - 1]; ++k) PK[ind + k] = 1;   // pairs (ind+k-1, ind+k)
+      for (int k = 1; k <= 5 && !GP[ind - k]; ++k) PK[ind - k] = 1;       // pairs (ind-k, ind-k+1)
+    }
+    s_nedge = nedge;
+  }
+  __threadfence_block();
+  __syncthreads();
+  const int nedge = s_nedge;
+  if (t < nedge) sec_edge_pos[sec * kMaxEdgesPerSector + t] = off + a + s_edges[t];
+  // surf = unpicked entries in ascending order (:220-227): contiguous chunk per thread, block scan, then in order
+  const int per = (m + TB - 1) / TB;
+  const int j0 = t * per, j1 = min(m, j0 + per);
+  int c = 0;
+  for (int i = j0; i < j1; ++i) c += !PK[is[i] + 5];
+  int total;
+  int pos = block_exclusive_scan_1024(c, smem, &total);
+  for (int i = j0; i < j1; ++i) {
+    const int ind = is[i] + 5;
+    if (!PK[ind]) surf_pos[off + a + pos++] = off + a + ind;
+  }
+  if (t == 0) {
+    sec_edge_cnt[sec] = nedge;
+    sec_surf_cnt[sec] = total;
+  }
+}
+
+// the listed long sectors (m > 1024), a few blocks looping over the list (a grid of one block per sector would cost
+// a launch of 6 R blocks that nearly all find nothing to do): up to 4096 entries in LDS, longer ones through global
+// memory (fe_sector_huge)
 __global__ __launch_bounds__(kSortThreads) void fe_sector_long(const int* __restrict__ ring_count,
                                                                const float4* __restrict__ ring_xyz,
                                                                int* __restrict__ sec_edge_cnt,
@@ -507,11 +715,19 @@ __global__ __launch_bounds__(kSortThreads) void fe_sector_long(const int* __rest
                                                                int* __restrict__ sec_surf_cnt,
                                                                int* __restrict__ surf_pos, int* __restrict__ status,
                                                                const int* __restrict__ long_list,
-                                                               const int* __restrict__ long_count) {
+                                                               const int* __restrict__ long_count, HugeScratch H) {
   const int nl = *long_count;
   for (int j = blockIdx.x; j < nl; j += gridDim.x) {
-    fe_sector_body<1024, 4096, true>(long_list[j], ring_count, ring_xyz, sec_edge_cnt, sec_edge_pos, sec_surf_cnt,
-                                     surf_pos, status, 0, nullptr, nullptr);
+    const int sec = long_list[j];
+    const int n_r = ring_count[sec / 6];
+    int a, b;
+    sector_range(n_r, sec % 6, a, b);
+    if (b - a > 4096) {   // (block-uniform)
+      fe_sector_huge(sec, ring_count, ring_xyz, sec_edge_cnt, sec_edge_pos, sec_surf_cnt, surf_pos, status, H);
+    } else {
+      fe_sector_body<1024, 4096, true>(sec, ring_count, ring_xyz, sec_edge_cnt, sec_edge_pos, sec_surf_cnt, surf_pos,
+                                       status, 0, nullptr, nullptr);
+    }
     __syncthreads();   // (the body's LDS is reused by the next listed sector)
   }
 }
@@ -743,9 +959,18 @@ void fe_launch(FeScratch& sc, const FeParams& prm, const PointRec* d_in, int n, 
                        sc.ring_xyz.p, sc.sec_edge_cnt.p, sc.sec_edge_pos.p, sc.sec_surf_cnt.p, sc.surf_pos.p,
                        sc.status, fe_stamps_on(), sc.long_sec.p + 1, sc.long_sec.p + 0);
     FLOAM_LAUNCH_CHECK();
+    // sectors beyond 4096 entries (a sector holds at most n / 6) run through the global scratch of fe_sector_huge
+    HugeScratch H{};
+    if (n / 6 + 8 > 4096) {
+      const size_t nb = (size_t)n + 60 * (size_t)R + 16;
+      sc.huge_k.reserve(2 * (size_t)n);
+      sc.huge_i.reserve(2 * (size_t)n);
+      sc.huge_b.reserve(2 * nb);
+      H = HugeScratch{sc.huge_k.p, sc.huge_k.p + n, sc.huge_i.p, sc.huge_i.p + n, sc.huge_b.p, sc.huge_b.p + nb};
+    }
     hipLaunchKernelGGL(fe_sector_long, dim3(16), dim3(kSortThreads), 0, st, sc.ring_count.p, sc.ring_xyz.p,
                        sc.sec_edge_cnt.p, sc.sec_edge_pos.p, sc.sec_surf_cnt.p, sc.surf_pos.p, sc.status,
-                       sc.long_sec.p + 1, sc.long_sec.p + 0);
+                       sc.long_sec.p + 1, sc.long_sec.p + 0, H);
   } else {
     hipLaunchKernelGGL((fe_sector<0, 1024, true>), dim3(6 * R), dim3(kSortThreads), 0, st, sc.ring_count.p,
                        sc.ring_xyz.p, sc.sec_edge_cnt.p, sc.sec_edge_pos.p, sc.sec_surf_cnt.p, sc.surf_pos.p,

@@ -22,6 +22,10 @@ struct FeScratch {
   DevBuf<int> out3;        // edge count, surf count, status after the call (one D2H)
   DevBuf<unsigned> ticket; // fe_output's arrival counter (its last block commits)
   DevBuf<int> long_sec;    // [0] count, [1..] sectors longer than 1024 entries (fe_sector -> fe_sector_long)
+  // sectors beyond 4096 entries (fe_sector_huge): curvature keys, entries, picked / gap flags, two halves each
+  DevBuf<unsigned long long> huge_k;
+  DevBuf<int> huge_i;
+  DevBuf<uint8_t> huge_b;
   int* status = nullptr;   // device int, owned by the caller
   bool zeroed = false;
   int zeroed_lines = 0;

@@ -275,6 +275,8 @@ struct floam_lp {
   HostBuf<int> h_out;   // edge count, surf count, status
   bool async = false;   // floam_lp_set_async: no synchronisation, counts stay on the device (upper bounds on host)
   hipStream_t stream = nullptr;   // the extraction's own stream (overlaps the odometry on the device stream)
+  // floam_lp_feature_extraction_host: the device copies of the caller's cloud and of the two outputs
+  std::unique_ptr<floam_cloud> h_in, h_edge, h_surf;
 };
 
 struct floam_odom {
@@ -300,6 +302,9 @@ struct floam_odom {
   bool grid_count_off = true;
   int map_violate_mod = 0;        // FLOAM_MM_VIOLATE=n: every n-th merge reports its keys out of order (tests)
   int mm_per = 4;                 // FLOAM_MM_PER=2: 512-element merge tiles instead of 1024 (tests, A/B)
+  // FLOAM_LM_PRE0=1: the geometry launch evaluates iteration zero's edge half (measured slower, r4d: geometry +6 us
+  // per pass for -2 to -3 us of solve; off by default)
+  bool lm_pre0 = false;
   size_t mapE_n = 0, mapS_n = 0;   // map sizes: exact after a synchronisation, else upper bounds
   // scratch
   DevBuf<PointRec> dE, dS, tmp;
@@ -394,6 +399,12 @@ struct floam_odom {
   floam_allreduce_fn ar_fn = nullptr;   // host all-reduce (validation mode), used when comm is null
   void* ar_user = nullptr;
   HostBuf<double> h_sums;
+  // peer sharding (floam_odom_set_shard_peers): this rank's exchange buffer, the ranks' buffers as mapped here, and
+  // the IPC mappings to close
+  unsigned long long* xbuf = nullptr;
+  ShardPeers peers;
+  std::vector<void*> xopened;
+  bool peer = false;
   bool sharded() const { return world > 1 || comm != nullptr; }
   int coresident[16] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};   // lm_resident, per mode
   floam_odom_stats stats{};
@@ -402,6 +413,17 @@ struct floam_odom {
   // frozen (OdomDev::failed: no pose taken, no keyframe, no map update from then on): every later update of the
   // handle fails with the first failure's message instead of returning stale odometry
   std::string poisoned;
+  // floam_odom_update_selector_host: device copies of the caller's clouds, and the Q5 write-back of the deskewed
+  // records into the caller's arrays on a copy stream once deskew_bridge has run (overlapped with call 2)
+  std::unique_ptr<floam_cloud> h_edge, h_surf;
+  struct WriteBack {
+    bool active = false;
+    void* edge = nullptr;
+    void* surf = nullptr;
+    size_t ne = 0, ns = 0;
+  } wb;
+  hipStream_t copy = nullptr;
+  hipEvent_t wb_ev = nullptr;
 };
 
 // dmapping::ImuHandler (include/dataHandler.h:31-66): the stamped orientation stream, host-side (AddMsg / Get /
@@ -466,6 +488,17 @@ void check_params(const floam_lidar_params* p) {
 }
 
 // ------------------------------------------------------------------------------------- odometry internals
+// peer sharding off: close the IPC mappings of the other ranks' exchange buffers
+void shard_peers_release(floam_odom* o) {
+  if (!o->xopened.empty()) {
+    (void)hipStreamSynchronize(ctx_for(o->device).stream);
+    for (void* p : o->xopened) (void)hipIpcCloseMemHandle(p);
+    o->xopened.clear();
+  }
+  o->peers = ShardPeers{};
+  o->peer = false;
+}
+
 // the one collective of the sharded path: the 29 sums (cost, J^T J, J^T r, count) of an LM evaluation, summed over
 // the ranks in place — RCCL on the library stream (no host synchronisation), or the validation callback
 void allreduce_sums(floam_odom* o, DeviceCtx& ctx) {
@@ -587,6 +620,12 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
   const bool sharded = o->sharded();
   const int mode = lm_mode(o->huber, o->fp32);
   const bool gram = (mode & LM_GRAM) != 0;
+  // the geometry launch evaluates iteration zero's edge half for the resident squared-loss solve (FLOAM_LM_PRE0=1:
+  // the solve evaluates it itself, A/B)
+  const bool peer = o->peer && o->world > 1;   // peer sharding: the resident solve exchanges the ranks' sums itself
+  if (peer && !lm_resident(o, mode))
+    throw Error(FLOAM_ERR_UNSUPPORTED, "peer sharding needs the resident solve (its grid does not fit the device)");
+  const bool pre0 = gram && (!sharded || peer) && o->lm_pre0 && lm_resident(o, mode);
   for (int it = 0; it < o->optimization_count; ++it) {
     {
       ProfScope ps(ctx, "knn", FLOAM_PROF_KNN);   // the correspondence pass: search + geometry
@@ -597,16 +636,17 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
                    o->mapS.count.p, o->rank, o->world, st);
       }
       ProfScope ps2(ctx, "knn_geometry", FLOAM_PROF_KNN_DETAIL);
-      geom_launch(o->lm.p, qe, o->ce, qs, o->cs, gram, o->fp32_geom, o->lmb, st);
+      geom_launch(o->lm.p, qe, o->ce, qs, o->cs, gram, o->fp32_geom, o->lmb, st, pre0);
     }
     if (ctx.profile & FLOAM_PROF_KNN_BYTES) {   // replay only: algorithmic bytes of the two launches above
       knn_traffic_launch(o->lm.p, qe, o->gE, o->ce, o->rank, o->world, o->traffic_set, o->prof_bytes.p + 0, st);
       knn_traffic_launch(o->lm.p, qs, o->gS, o->cs, o->rank, o->world, o->traffic_set, o->prof_bytes.p + 1, st);
     }
     // ceres::Solve: iteration zero + at most max_num_iterations = 4 candidates (odomEstimationClass.cpp:102)
-    if (!sharded && lm_resident(o, mode)) {
+    if ((!sharded || peer) && lm_resident(o, mode)) {
       ProfScope ps(ctx, "lm_solve", FLOAM_PROF_LM);
-      lm_solve_launch(o->lm.p, o->ce, dcnt + 0, ne_ub, o->cs, dcnt + 1, ns_ub, mode, o->lmb, st, o->dbg_stamps.p);
+      lm_solve_launch(o->lm.p, o->ce, dcnt + 0, ne_ub, o->cs, dcnt + 1, ns_ub, mode, o->lmb, st, o->dbg_stamps.p,
+                      pre0, peer ? &o->peers : nullptr);
     } else {   // one launch (+ one all-reduce of the 29 sums when sharded) per evaluation, all on the stream
       ProfScope ps(ctx, "lm_solve_sharded", FLOAM_PROF_LM);
       for (int ev = 0; ev < 5; ++ev) {
@@ -732,7 +772,7 @@ floam_status odom_collect_one(floam_odom* o, DeviceCtx& ctx) {
     if (U.counts[0] < 0 || U.counts[1] < 0 || U.counts[2] < 0 || U.counts[3] < 0)
       poison("voxel-grid compaction failed (lookback timeout)");
     if (U.fe_status & FE_STATUS_SECTOR_TOO_LONG)
-      throw Error(FLOAM_ERR_UNSUPPORTED, "a ring sector exceeds 4096 points (ring longer than ~24k points)");
+      throw Error(FLOAM_ERR_UNSUPPORTED, "a ring sector had no feature scratch (internal error)");
     if (U.fe_status & FE_STATUS_BAD_RING)
       throw Error(FLOAM_ERR_INVALID_ARGUMENT, "point ring index >= num_lines (out of bounds in the reference)");
   }
@@ -1030,12 +1070,23 @@ floam_status odom_update_deskew(floam_odom* o, floam_cloud* edge, floam_cloud* s
       deskew_bridge_launch(o->lm.p, o->ds.p, o->lp.scan_period, edge->pts.p, edge->count.p, ne_ub, surf->pts.p,
                            surf->count.p, ns_ub, ctx.stream, g1, fuse ? &vf2 : nullptr);
     }
+    if (o->wb.active) {   // the clouds are final here (CompensateVelocity, Q5): the write-back may start
+      if (!o->wb_ev) FLOAM_HIP(hipEventCreateWithFlags(&o->wb_ev, hipEventDisableTiming));
+      FLOAM_HIP(hipEventRecord(o->wb_ev, ctx.stream));
+    }
     if (o->optimization_count > 2) o->optimization_count--;
     MapUpdatePlan mp = odom_map_plan(o, ctx, ne_ub, ns_ub);
     odom_issue(o, ctx, edge, surf, ne_ub, ns_ub, o->ds.p->x0[1], 2 * ring + 1,
                GATHER_FINISH | GATHER_AFTER_MID | gather_keyframe_mode(o), -1, false, nullptr, fuse, &mp);
     size_t addE = 0, addS = 0;
     odom_map_update(o, ctx, mp, addE, addS);
+    if (o->wb.active) {   // the whole update is issued: copy the deskewed records back while call 2 runs
+      FLOAM_HIP(hipStreamWaitEvent(o->copy, o->wb_ev, 0));
+      if (o->wb.ne)
+        FLOAM_HIP(hipMemcpyAsync(o->wb.edge, edge->pts.p, o->wb.ne * sizeof(PointRec), hipMemcpyDeviceToHost, o->copy));
+      if (o->wb.ns)
+        FLOAM_HIP(hipMemcpyAsync(o->wb.surf, surf->pts.p, o->wb.ns * sizeof(PointRec), hipMemcpyDeviceToHost, o->copy));
+    }
     const floam_status r = odom_end(o, ctx, ring, 2, 1, addE, addS, captured, 1);
     if (pre >= 0) {   // the side stream may refill this parity's buffers once this update has run (its end event)
       o->side_ev[pre] = o->end_ev;
@@ -1064,7 +1115,7 @@ void set_last_error(const std::string& m) { t_err = m; }
 extern "C" {
 
 const char* floam_last_error(void) { return t_err.c_str(); }
-const char* floam_version(void) { return "floam_amd 0.2.0 (gfx950, ABI 2)"; }
+const char* floam_version(void) { return "floam_amd 0.3.0 (gfx950, ABI 3)"; }
 int floam_abi_version(void) { return FLOAM_ABI_VERSION; }
 void floam_reset_process_state(void) { g_keyframe_first = true; }
 
@@ -1254,7 +1305,7 @@ floam_status floam_lp_wait(floam_lp* lp) {
     FLOAM_HIP(hipStreamSynchronize(lp->stream));
     const int status = lp->h_out.p[2];
     if (status & FE_STATUS_SECTOR_TOO_LONG)
-      throw Error(FLOAM_ERR_UNSUPPORTED, "a ring sector exceeds 4096 points (ring longer than ~24k points)");
+      throw Error(FLOAM_ERR_UNSUPPORTED, "a ring sector had no feature scratch (internal error)");
     if (status & FE_STATUS_BAD_RING)
       throw Error(FLOAM_ERR_INVALID_ARGUMENT, "point ring index >= num_lines (out of bounds in the reference)");
     return FLOAM_OK;
@@ -1334,9 +1385,64 @@ floam_status floam_lp_feature_extraction(floam_lp* lp, const floam_cloud* in, fl
     surf->host_count_valid = true;
     const int status = lp->h_out.p[2];
     if (status & FE_STATUS_SECTOR_TOO_LONG)
-      throw Error(FLOAM_ERR_UNSUPPORTED, "a ring sector exceeds 4096 points (ring longer than ~24k points)");
+      throw Error(FLOAM_ERR_UNSUPPORTED, "a ring sector had no feature scratch (internal error)");
     if (status & FE_STATUS_BAD_RING)
       throw Error(FLOAM_ERR_INVALID_ARGUMENT, "point ring index >= num_lines (out of bounds in the reference)");
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_lp_feature_extraction_host(floam_lp* lp, const void* in, size_t n, size_t stride, void* edge,
+                                              size_t edge_cap, size_t* n_edge, void* surf, size_t surf_cap,
+                                              size_t* n_surf) {
+  return guarded([&] {
+    if (!lp || (!in && n) || !n_edge || !n_surf) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
+    if (stride != sizeof(PointRec)) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "input must be 32-B PointXYZIRT records");
+    if (n > (size_t)INT32_MAX) throw Error(FLOAM_ERR_UNSUPPORTED, "cloud larger than 2^31 points");
+    hipStream_t st = lp->stream;
+    FLOAM_HIP(hipSetDevice(lp->device));
+    for (auto* c : {&lp->h_in, &lp->h_edge, &lp->h_surf})
+      if (!*c) {
+        *c = std::make_unique<floam_cloud>();
+        cloud_init(c->get(), lp->device, 0);
+      }
+    floam_cloud *ci = lp->h_in.get(), *ce = lp->h_edge.get(), *cs = lp->h_surf.get();
+    for (floam_cloud* c : {ci, ce, cs}) cloud_on(c, st);
+    FLOAM_HIP(hipStreamSynchronize(st));
+    *n_edge = *n_surf = 0;
+    if (n == 0) return FLOAM_OK;
+    const size_t ne_ub = std::min(n, (size_t)lp->prm.num_lines * 6 * 20);
+    cloud_reserve(ci, n, 0, st);
+    cloud_reserve(ce, ne_ub + 1, 0, st);
+    cloud_reserve(cs, n + 1, 0, st);
+    ce->fe_stat.reserve(1);
+    cs->fe_stat.reserve(1);
+    FLOAM_HIP(hipMemcpyAsync(ci->pts.p, in, n * sizeof(PointRec), hipMemcpyHostToDevice, st));
+    FLOAM_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ci->count.p), (int)n, 1, st));
+    // the outputs start empty: the clear is folded into the extraction's kernels
+    fe_launch(lp->sc, lp->prm, ci->pts.p, (int)n, ce->pts.p, ce->count.p, cs->pts.p, cs->count.p, st, ce->fe_stat.p,
+              cs->fe_stat.p, 3);
+    FLOAM_HIP(hipMemcpyAsync(lp->h_out.p, lp->sc.out3.p, sizeof(int) * 3, hipMemcpyDeviceToHost, st));
+    FLOAM_HIP(hipStreamSynchronize(st));
+    const int status = lp->h_out.p[2];
+    if (status & FE_STATUS_SECTOR_TOO_LONG)
+      throw Error(FLOAM_ERR_UNSUPPORTED, "a ring sector had no feature scratch (internal error)");
+    if (status & FE_STATUS_BAD_RING)
+      throw Error(FLOAM_ERR_INVALID_ARGUMENT, "point ring index >= num_lines (out of bounds in the reference)");
+    const size_t ne = (size_t)lp->h_out.p[0], ns = (size_t)lp->h_out.p[1];
+    for (floam_cloud* c : {ce, cs}) {
+      c->host_count = c == ce ? ne : ns;
+      c->host_count_valid = true;
+    }
+    ci->host_count = n;
+    ci->host_count_valid = true;
+    if (ne > edge_cap || ns > surf_cap || (ne && !edge) || (ns && !surf))
+      throw Error(FLOAM_ERR_INVALID_ARGUMENT, "output capacity too small for the extracted features");
+    if (ne) FLOAM_HIP(hipMemcpyAsync(edge, ce->pts.p, ne * sizeof(PointRec), hipMemcpyDeviceToHost, st));
+    if (ns) FLOAM_HIP(hipMemcpyAsync(surf, cs->pts.p, ns * sizeof(PointRec), hipMemcpyDeviceToHost, st));
+    FLOAM_HIP(hipStreamSynchronize(st));
+    *n_edge = ne;
+    *n_surf = ns;
     return FLOAM_OK;
   });
 }
@@ -1359,6 +1465,7 @@ floam_status floam_odom_create(const floam_lidar_params* p, double map_resolutio
     if (const char* e = std::getenv("FLOAM_MM_VIOLATE")) o->map_violate_mod = std::atoi(e);
     if (const char* e = std::getenv("FLOAM_MM_PER")) o->mm_per = std::atoi(e) == 2 ? 2 : 4;
     if (const char* e = std::getenv("FLOAM_LM_FAIL_TEST")) o->lmb.fail_test = std::atoi(e) != 0;
+    if (const char* e = std::getenv("FLOAM_LM_PRE0")) o->lm_pre0 = e[0] != '0';
     if (const char* e = std::getenv("FLOAM_GRID_COUNT_FUSED")) o->grid_count_off = std::atoi(e) == 0;
     std::string l = loss ? loss : "";
     std::transform(l.begin(), l.end(), l.begin(), [](unsigned char c) { return (char)std::tolower(c); });
@@ -1406,6 +1513,11 @@ floam_status floam_odom_destroy(floam_odom* o) {
                      "state written %.2f us\n", h[4], h[0] / n / 100.0, h[1] / n / 100.0, h[2] / n / 100.0,
                      h[3] / n / 100.0, h[5] / n / 100.0, h[6] / n / 100.0);
       }
+      if (o->copy) {
+        (void)hipStreamSynchronize(o->copy);
+        (void)hipStreamDestroy(o->copy);
+      }
+      if (o->wb_ev) (void)hipEventDestroy(o->wb_ev);
       if (o->side) {
         (void)hipStreamSynchronize(o->side);
         if (o->pre_ev) (void)hipEventDestroy(o->pre_ev);
@@ -1413,6 +1525,8 @@ floam_status floam_odom_destroy(floam_odom* o) {
       }
       *o->done_ctr = ~0ull;   // (the stream is idle: clouds that still point here never wait)
       if (o->comm) ncclCommDestroy(o->comm);
+      shard_peers_release(o);
+      if (o->xbuf) (void)hipFree(o->xbuf);
       for (const auto& k : o->keyframes)
         for (floam_cloud* c : {k.surf, k.edge}) floam_cloud_destroy(c);
       for (floam_cloud* c : o->kf_spare) floam_cloud_destroy(c);
@@ -1466,9 +1580,71 @@ floam_status floam_odom_update(floam_odom* o, const floam_cloud* edge, const flo
   });
 }
 
+namespace {
+floam_status update_selector_impl(floam_odom* o, floam_cloud* edge, floam_cloud* surf, int deskew);
+}
+
 floam_status floam_odom_update_selector(floam_odom* o, floam_cloud* edge, floam_cloud* surf, int deskew) {
   return guarded([&] {
     if (!o || !edge || !surf) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
+    return update_selector_impl(o, edge, surf, deskew);
+  });
+}
+
+floam_status floam_odom_update_selector_host(floam_odom* o, void* edge, size_t n_edge, void* surf, size_t n_surf,
+                                             size_t stride, int deskew) {
+  return guarded([&] {
+    if (!o || (!edge && n_edge) || (!surf && n_surf)) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null argument");
+    if (stride != sizeof(PointRec))
+      throw Error(FLOAM_ERR_INVALID_ARGUMENT, "host clouds must be 32-B PointXYZIRT / PointXYZI records");
+    if (n_edge > (size_t)INT32_MAX || n_surf > (size_t)INT32_MAX)
+      throw Error(FLOAM_ERR_UNSUPPORTED, "cloud larger than 2^31 points");
+    DeviceCtx& ctx = ctx_for(o->device);
+    FLOAM_HIP(hipSetDevice(o->device));
+    odom_collect(o, ctx, 0);   // (a synchronous call: nothing of this handle stays in flight)
+    for (auto* c : {&o->h_edge, &o->h_surf})
+      if (!*c) {
+        *c = std::make_unique<floam_cloud>();
+        cloud_init(c->get(), o->device, 0);
+      }
+    floam_cloud* ce = o->h_edge.get();
+    floam_cloud* cs = o->h_surf.get();
+    cloud_on_main(ce);
+    cloud_on_main(cs);
+    FLOAM_HIP(hipStreamSynchronize(ctx.stream));   // (their previous users are done before the buffers are refilled)
+    cloud_reserve(ce, std::max<size_t>(n_edge, 1), 0, ctx.stream);
+    cloud_reserve(cs, std::max<size_t>(n_surf, 1), 0, ctx.stream);
+    if (n_edge) FLOAM_HIP(hipMemcpyAsync(ce->pts.p, edge, n_edge * sizeof(PointRec), hipMemcpyHostToDevice, ctx.stream));
+    if (n_surf) FLOAM_HIP(hipMemcpyAsync(cs->pts.p, surf, n_surf * sizeof(PointRec), hipMemcpyHostToDevice, ctx.stream));
+    FLOAM_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ce->count.p), (int)n_edge, 1, ctx.stream));
+    FLOAM_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(cs->count.p), (int)n_surf, 1, ctx.stream));
+    ce->host_count = n_edge;
+    cs->host_count = n_surf;
+    ce->host_count_valid = cs->host_count_valid = true;
+    ce->fe_status = cs->fe_status = nullptr;
+    if (deskew && !o->copy) make_stream(&o->copy, false);
+    const int depth = o->depth;   // synchronous whatever the streaming mode
+    o->depth = 0;
+    o->wb = floam_odom::WriteBack{deskew != 0, edge, surf, n_edge, n_surf};
+    floam_status r = FLOAM_OK;
+    try {
+      r = update_selector_impl(o, ce, cs, deskew);
+    } catch (...) {
+      o->depth = depth;
+      if (o->wb.active && o->copy) (void)hipStreamSynchronize(o->copy);
+      o->wb.active = false;
+      throw;
+    }
+    o->depth = depth;
+    if (o->wb.active) FLOAM_HIP(hipStreamSynchronize(o->copy));
+    o->wb.active = false;
+    return r;
+  });
+}
+
+namespace {
+floam_status update_selector_impl(floam_odom* o, floam_cloud* edge, floam_cloud* surf, int deskew) {
+  {
     if (deskew && edge != surf) odom_prevoxel(o, edge, surf);
     if (deskew && o->pre_valid >= 0) {   // ordered after the grid rebuild (odom_issue)
       o->late_wait[0] = edge;
@@ -1490,8 +1666,9 @@ floam_status floam_odom_update_selector(floam_odom* o, floam_cloud* edge, floam_
       if (surf != edge) cloud_publish_update(surf, st, o->end_ev, o->done_ctr, o->issued);
     }
     return r;
-  });
+  }
 }
+}  // namespace
 
 floam_status floam_odom_get_pose(const floam_odom* o, double q[4], double t[3]) {
   return guarded([&] {
@@ -1609,6 +1786,7 @@ floam_status floam_odom_set_shard(floam_odom* o, int rank, int world, const void
     if (!o || world < 1 || rank < 0 || rank >= world) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "bad rank / world");
     if (world > 1 && !id) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null unique id");
     odom_collect(o, ctx_for(o->device), 0);
+    shard_peers_release(o);
     if (o->comm) {
       ncclCommDestroy(o->comm);
       o->comm = nullptr;
@@ -1627,11 +1805,81 @@ floam_status floam_odom_set_shard(floam_odom* o, int rank, int world, const void
   });
 }
 
+// peer sharding: this rank's exchange buffer (zeroed: tag 0 never matches, epochs start at 8), allocated once
+void shard_xbuf(floam_odom* o) {
+  if (o->xbuf) return;
+  FLOAM_HIP(hipSetDevice(o->device));
+  FLOAM_HIP(hipMalloc(&o->xbuf, sizeof(unsigned long long) * kShardXchgWords));
+  FLOAM_HIP(hipMemset(o->xbuf, 0, sizeof(unsigned long long) * kShardXchgWords));
+}
+
+floam_status floam_odom_shard_exchange(floam_odom* o, void* ipc_handle_64, void** dev_ptr) {
+  return guarded([&] {
+    if (!o || (!ipc_handle_64 && !dev_ptr)) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null handle or outputs");
+    shard_xbuf(o);
+    if (ipc_handle_64) {
+      hipIpcMemHandle_t h;
+      FLOAM_HIP(hipIpcGetMemHandle(&h, o->xbuf));
+      static_assert(sizeof(h) == 64, "hipIpcMemHandle_t is 64 bytes");
+      std::memcpy(ipc_handle_64, &h, sizeof(h));
+    }
+    if (dev_ptr) *dev_ptr = o->xbuf;
+    return FLOAM_OK;
+  });
+}
+
+floam_status floam_odom_set_shard_peers(floam_odom* o, int rank, int world, const void* ipc_handles,
+                                        void* const* dev_ptrs) {
+  return guarded([&] {
+    if (!o || world < 1 || world > kMaxShardRanks || rank < 0 || rank >= world)
+      throw Error(FLOAM_ERR_INVALID_ARGUMENT, "bad rank / world (1 <= world <= 8)");
+    if (world > 1 && (!ipc_handles == !dev_ptrs))
+      throw Error(FLOAM_ERR_INVALID_ARGUMENT, "give exactly one of ipc_handles and dev_ptrs");
+    odom_collect(o, ctx_for(o->device), 0);
+    if (o->comm) {
+      ncclCommDestroy(o->comm);
+      o->comm = nullptr;
+    }
+    o->ar_fn = nullptr;
+    shard_peers_release(o);
+    shard_xbuf(o);
+    ShardPeers P;
+    P.world = world;
+    P.mine = o->xbuf;
+    for (int r = 0; r < world && world > 1; ++r) {
+      if (r == rank) {
+        P.buf[r] = o->xbuf;
+      } else if (dev_ptrs) {
+        if (!dev_ptrs[r]) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null peer buffer");
+        P.buf[r] = static_cast<const unsigned long long*>(dev_ptrs[r]);
+      } else {
+        hipIpcMemHandle_t h;
+        std::memcpy(&h, static_cast<const char*>(ipc_handles) + 64 * r, sizeof(h));
+        void* p = nullptr;
+        const hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+        if (e != hipSuccess) {
+          shard_peers_release(o);
+          throw Error(FLOAM_ERR_COMM, std::string("hipIpcOpenMemHandle (rank ") + std::to_string(r) +
+                                          "): " + hipGetErrorString(e));
+        }
+        o->xopened.push_back(p);
+        P.buf[r] = static_cast<const unsigned long long*>(p);
+      }
+    }
+    o->peers = P;
+    o->rank = rank;
+    o->world = world;
+    o->peer = world > 1;
+    return FLOAM_OK;
+  });
+}
+
 floam_status floam_odom_set_shard_callback(floam_odom* o, int rank, int world, floam_allreduce_fn fn, void* user) {
   return guarded([&] {
     if (!o || world < 1 || rank < 0 || rank >= world) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "bad rank / world");
     if (world > 1 && !fn) throw Error(FLOAM_ERR_INVALID_ARGUMENT, "null all-reduce callback");
     odom_collect(o, ctx_for(o->device), 0);
+    shard_peers_release(o);
     if (o->comm) {
       ncclCommDestroy(o->comm);
       o->comm = nullptr;

@@ -31,11 +31,13 @@
 #include <cfloat>
 #include <climits>
 
+#include "lm_eval.hpp"
 #include "odom_kernels.hpp"
 
 namespace floam {
 
 namespace {
+using namespace lmev;
 constexpr int kTB = 256;     // solve blocks: 4 waves, one per SIMD (the control wave keeps the LM state in 512 registers)
 constexpr int kStrips = 8;   // block_sums strips
 constexpr long long kSpin = 1ll << 23;   // bounded polls (s_sleep 1 each): ~0.3 s
@@ -46,115 +48,6 @@ __device__ __forceinline__ void wave_lds_order() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-template <typename R>
-__device__ __forceinline__ R real_min() { return DBL_MIN; }
-template <>
-__device__ __forceinline__ float real_min<float>() { return FLT_MIN; }
-
-// 1 / d for the dependent chains of the solve: v_rcp_f64 + two Newton steps (within an ulp of the division, a third of
-// its instructions); the float variant is the plain division
-__device__ __forceinline__ double recip(double d) {
-  double r = __builtin_amdgcn_rcp(d);
-  double e = fma(-d, r, 1.0);
-  r = fma(r, e, r);
-  e = fma(-d, r, 1.0);
-  return fma(r, e, r);
-}
-__device__ __forceinline__ float recip(float d) { return 1.0f / d; }
-
-// ===================================================================================== residuals (R = double | float)
-// Eigen's q * v: uv = 2 q.vec x v; v + w uv + q.vec x uv
-template <typename R>
-__device__ __forceinline__ void rot(const R* x, R vx, R vy, R vz, R& ox, R& oy, R& oz) {
-  const R qx = x[0], qy = x[1], qz = x[2], qw = x[3];
-  R ux = qy * vz - qz * vy, uy = qz * vx - qx * vz, uz = qx * vy - qy * vx;
-  ux = ux + ux; uy = uy + uy; uz = uz + uz;
-  const R ax = vx + qw * ux, ay = vy + qw * uy, az = vz + qw * uz;
-  ox = ax + (qy * uz - qz * uy);
-  oy = ay + (qz * ux - qx * uz);
-  oz = az + (qx * uy - qy * ux);
-}
-
-// EdgeAnalyticCostFunction::Evaluate (src/lidarOptimization.cpp:12-43): J = -(nu/|nu|)^T [de]x [-[lp]x, I] / |de|
-// (the divisions by |nu| and |de| as products with their reciprocals: the same values to an ulp)
-template <typename R>
-__device__ __forceinline__ R edge_residual(const R* x, const R* r9, R J[6]) {
-  R lx, ly, lz;
-  rot(x, r9[0], r9[1], r9[2], lx, ly, lz);
-  lx = lx + x[4]; ly = ly + x[5]; lz = lz + x[6];
-  const R pax = lx - r9[3], pay = ly - r9[4], paz = lz - r9[5];
-  const R pbx = lx - r9[6], pby = ly - r9[7], pbz = lz - r9[8];
-  const R nux = pay * pbz - paz * pby, nuy = paz * pbx - pax * pbz, nuz = pax * pby - pay * pbx;
-  const R dex = r9[3] - r9[6], dey = r9[4] - r9[7], dez = r9[5] - r9[8];
-  const R de_norm = sqrt(dex * dex + dey * dey + dez * dez);
-  const R nn = sqrt(nux * nux + nuy * nuy + nuz * nuz);
-  const R ide = recip(de_norm), inn = recip(nn);   // one reciprocal each instead of ten divisions
-  const R r = nn * ide;
-  const R w0 = -nux * inn, w1 = -nuy * inn, w2 = -nuz * inn;
-  // r1 = w * skew(de): skew(de) = [[0,-dz,dy],[dz,0,-dx],[-dy,dx,0]]
-  const R r10 = w1 * dez + w2 * (-dey);
-  const R r11 = w0 * (-dez) + w2 * dex;
-  const R r12 = w0 * dey + w1 * (-dex);
-  // dp = [-skew(lp), I]; -skew(lp) = [[0,lz,-ly],[-lz,0,lx],[ly,-lx,0]]
-  J[0] = (r11 * (-lz) + r12 * ly) * ide;
-  J[1] = (r10 * lz + r12 * (-lx)) * ide;
-  J[2] = (r10 * (-ly) + r11 * lx) * ide;
-  J[3] = r10 * ide;
-  J[4] = r11 * ide;
-  J[5] = r12 * ide;
-  return r;
-}
-
-// SurfNormAnalyticCostFunction::Evaluate (src/lidarOptimization.cpp:51-74): J = n^T [-[pw]x, I]
-template <typename R>
-__device__ __forceinline__ R surf_residual(const R* x, const R* r7, R J[6]) {
-  R px, py, pz;
-  rot(x, r7[0], r7[1], r7[2], px, py, pz);
-  px = px + x[4]; py = py + x[5]; pz = pz + x[6];
-  const R nx = r7[3], ny = r7[4], nz = r7[5];
-  const R r = (nx * px + ny * py + nz * pz) + r7[6];
-  J[0] = ny * (-pz) + nz * py;
-  J[1] = nx * pz + nz * (-px);
-  J[2] = nx * (-py) + ny * px;
-  J[3] = nx;
-  J[4] = ny;
-  J[5] = nz;
-  return r;
-}
-
-// one residual (r, J) into the 29 sums (cost, J^T J upper, J^T r, count), with ceres::HuberLoss(0.1) + Corrector
-// (rho'' <= 0 everywhere: residual scaling by sqrt(rho')) when HUBER (src/odomEstimationClass.cpp:84-87)
-template <bool HUBER, typename R>
-__device__ __forceinline__ void accumulate_residual(R (&acc)[LM_NSUM], R r, R (&J)[6]) {
-  const R sq = r * r;
-  if (HUBER) {
-    R rho0, rho1;
-    if (sq > R(0.01)) {
-      const R rr = sqrt(sq);
-      rho0 = R(2.0) * R(0.1) * rr - R(0.01);
-      rho1 = fmax(real_min<R>(), R(0.1) / rr);
-    } else {
-      rho0 = sq;
-      rho1 = R(1.0);
-    }
-    acc[0] += R(0.5) * rho0;
-    const R sr = sqrt(rho1);
-    r *= sr;
-#pragma unroll
-    for (int k = 0; k < 6; ++k) J[k] *= sr;
-  } else {
-    acc[0] += R(0.5) * sq;
-  }
-  int h = 1;
-#pragma unroll
-  for (int a = 0; a < 6; ++a)
-#pragma unroll
-    for (int b = a; b < 6; ++b) acc[h++] += J[a] * J[b];
-#pragma unroll
-  for (int a = 0; a < 6; ++a) acc[22 + a] += J[a] * r;
-  acc[28] += R(1.0);
 }
 
 // record slot (edge: 9 fields, surf: 7) of the device-resident correspondence arrays, converted to R
@@ -394,6 +287,35 @@ __device__ __forceinline__ void gram_unpack(double gv, double (*G)[kGramW], doub
 // run side by side in lanes 0 and 1 of the same instruction stream; the 6x6 LDL^T divides by each pivot once.
 // Loops are fully unrolled with constant indices so nothing leaves registers.
 
+// sin and cos of |x| <= pi / 4 by fdlibm's kernel polynomials (__kernel_sin / __kernel_cos, < 1 ulp): the two
+// 6-term chains interleave, one dependent chain instead of the library sincos's range reduction and branches (the
+// control step is one wave's serial fp64 instruction stream).  Larger |x| (a huge step, or the gradient projection of
+// the iteration-zero test) takes the library's sincos.
+__device__ __forceinline__ void sincos_small(double x, double* s, double* c) {
+  if (!(fabs(x) <= 0.78125)) {
+    sincos(x, s, c);
+    return;
+  }
+  const double z = x * x, v = z * x;
+  const double rs = 8.33333333332248946124e-03 +
+                    z * (-1.98412698298579493134e-04 +
+                         z * (2.75573137070700676789e-06 + z * (-2.50507602534068634195e-08 + z * 1.58969099521155010221e-10)));
+  const double rc = z * (4.16666666666666019037e-02 +
+                         z * (-1.38888888888741095749e-03 +
+                              z * (2.48015872894767294178e-05 +
+                                   z * (-2.75573143513906633035e-07 +
+                                        z * (2.08757232129817482790e-09 + z * -1.13596475577881948265e-11)))));
+  *s = x + v * (-1.66666666666666324348e-01 + z * rs);
+  if (fabs(x) < 0.3) {
+    *c = 1.0 - (0.5 * z - z * rc);
+  } else {   // fdlibm's split of 1 - z / 2 for 0.3 <= |x| <= 0.78125: qx = |x| / 4 with its low word cleared
+    const long long hb = __double_as_longlong(fabs(x)) - (0x00200000ll << 32);
+    const double qx = __longlong_as_double(hb & (long long)0xFFFFFFFF00000000ull);
+    const double hz = 0.5 * z - qx, a = 1.0 - qx;
+    *c = a - (hz - z * rc);
+  }
+}
+
 // PoseSE3Parameterization::Plus + getTransformFromSe3 (src/lidarOptimization.cpp:77-140).  theta^3 is formed by
 // multiplication where the reference calls pow(theta, 3) (<= 1 ulp apart).
 __device__ __forceinline__ void se3_plus(const double (&x)[7], const double (&d)[6], double (&out)[7]) {
@@ -401,7 +323,7 @@ __device__ __forceinline__ void se3_plus(const double (&x)[7], const double (&d)
   const double theta = sqrt(wx * wx + wy * wy + wz * wz);
   const double half = 0.5 * theta;
   double sh, ch;
-  sincos(half, &sh, &ch);
+  sincos_small(half, &sh, &ch);
   const double real_factor = ch;
   double imag;
   const bool small = theta < 1e-10;
@@ -684,6 +606,20 @@ __device__ __forceinline__ void store_state_core(LMState& dst, const LMState& s)
   dst.successful = s.successful; dst.n_res = s.n_res;
 }
 
+__device__ __forceinline__ void load_state_core(LMState& s, const LMState& src) {
+#pragma unroll
+  for (int k = 0; k < 7; ++k) { s.x[k] = src.x[k]; s.cand[k] = src.cand[k]; }
+  s.x_cost = src.x_cost;
+#pragma unroll
+  for (int k = 0; k < 21; ++k) s.H[k] = src.H[k];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) { s.g[k] = src.g[k]; s.scale[k] = src.scale[k]; s.diag[k] = src.diag[k]; }
+  s.radius = src.radius; s.dfac = src.dfac; s.mcc = src.mcc; s.x_norm = src.x_norm; s.gmax = src.gmax;
+  s.initial_cost = src.initial_cost;
+  s.phase = src.phase; s.done = src.done; s.iteration = src.iteration; s.reuse = src.reuse; s.invalid = src.invalid;
+  s.successful = src.successful; s.n_res = src.n_res;
+}
+
 // iteration zero's trace (x_in, J^T J, J^T r) into the LDS state, by one lane
 __device__ __forceinline__ void record_iteration_zero(LMState& dst, const LMState& s, const double (&sums)[LM_NSUM]) {
 #pragma unroll
@@ -701,6 +637,24 @@ __device__ __forceinline__ void control_step(LMState& s, LMState& sst, const dou
   for (int k = 0; k < LM_NSUM; ++k) sm[k] = sums_lds[k];
   if (s.phase == 0 && lane == 0) record_iteration_zero(sst, s, sm);
   lm_logic(s, sm, lane);
+}
+
+// the control step on the LDS copy (wave 0): the state is loaded into registers for the step and written back by
+// lane 0, so nothing of it stays live across the evaluations (whose registers it would otherwise share: the
+// register-resident form spilled it to AGPRs and back around every step); then the next point and the done flag
+#ifndef FLOAM_LM_STATE_REGS
+#define FLOAM_LM_STATE_REGS 0
+#endif
+__device__ __forceinline__ double point_component(const LMState& s, int k);
+__device__ __forceinline__ void control_step_lds(LMState& sst, const double* sums_lds, int lane, double* s_pt,
+                                                 int* s_done) {
+  LMState s;
+  load_state_core(s, sst);
+  control_step(s, sst, sums_lds, lane);
+  __builtin_amdgcn_wave_barrier();   // (every lane's reads of sst precede lane 0's write-back: one wave, in order)
+  if (lane == 0) store_state_core(sst, s);
+  if (lane < 7) s_pt[lane] = point_component(s, lane);
+  if (lane == 0) *s_done = s.done;
 }
 
 __device__ __forceinline__ double point_component(const LMState& s, int k) {   // k wave-uniform or per lane
@@ -782,7 +736,60 @@ struct LMArgs {
   unsigned* ticket;                // sharded: arrival ticket
   unsigned long long* dbg;         // FLOAM_DEBUG_STAMPS: block 0's segment times (diagnostic, normally null)
   int fail_test;                   // LMBuffers::fail_test: report the first hand-off as timed out (tests)
+  const double* epart;             // pre0: [nbe][29] iteration zero's edge sums by geometry block, else null
+  int nbe;
+  // peer sharding (world > 1): this rank's exchange granules [2][2 * LM_NSUM] and every rank's, peer-mapped, rank order
+  int world;
+  unsigned long long* xme;
+  const unsigned long long* xpeer[kMaxShardRanks];
 };
+
+// Peer sharding: after a block has its rank's 29 sums (block partials + the surf half), block 0 publishes them as
+// tagged granules in this rank's exchange buffer and every block gathers all ranks' granules (system scope: the buffers
+// of the other ranks are on other GPUs, read through xGMI) and sums them in rank order — every block of every rank the
+// same bits, so every rank takes the same LM decisions.  Slot reuse follows the block hand-off's parity argument one
+// level up: a rank's total of evaluation k + 1 exists only after each of its blocks has read every rank's evaluation
+// k, and a rank overwrites its evaluation-k slot at k + 2, after it has seen every rank's k + 1.  The wait is bounded
+// in time (~20 s: ranks in other processes may be far apart at the first solve), not in polls.
+__device__ __forceinline__ bool peer_exchange(const LMArgs& a, int it, unsigned tag, double* s_sums, unsigned* s_x) {
+  const int tid = (int)threadIdx.x;
+  const int slot = (it & 1) * 2 * LM_NSUM;
+  if (blockIdx.x == 0 && tid < 2 * LM_NSUM) {
+    const int c = tid >> 1, h = tid & 1;
+    const unsigned long long b = (unsigned long long)__double_as_longlong(s_sums[c]);
+    __hip_atomic_store(&a.xme[slot + tid], granule(tag, h ? (unsigned)(b >> 32) : (unsigned)b), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  bool ok = true;
+  if (tid < a.world * 2 * LM_NSUM) {
+    const int r = tid / (2 * LM_NSUM), j = tid - r * 2 * LM_NSUM;
+    const unsigned long long* src = a.xpeer[r] + slot + j;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+      const unsigned long long v = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if ((unsigned)(v >> 32) == tag) {
+        s_x[tid] = (unsigned)v;
+        break;
+      }
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000000ull) {   // 100 MHz: 20 s
+        ok = false;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  if (__syncthreads_or(!ok)) return false;
+  if (tid < LM_NSUM) {
+    double v = 0.0;
+    for (int r = 0; r < a.world; ++r) {
+      const int g = r * 2 * LM_NSUM + 2 * tid;
+      v += __longlong_as_double((long long)(((unsigned long long)s_x[g + 1] << 32) | s_x[g]));
+    }
+    s_sums[tid] = v;
+  }
+  __syncthreads();
+  return true;
+}
 
 // the block's first record (the one kept in registers across the evaluations) of record thread i0
 template <typename R>
@@ -855,19 +862,50 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
   if (sst.done) return;   // (never after lm_reset)
   if (GRAM) gram_unpack(gv, G, o);
   const unsigned ep = sst.epoch;
+#if FLOAM_LM_STATE_REGS
   LMState s;   // wave 0: the whole LM state in registers for the whole solve
   if (tid < 64) s = sst;
+#endif
   if (tid < 7) s_pt[tid] = sst.x[tid];   // iteration zero evaluates at x (set by the kNN launch; kernel boundary)
   if (tid == 0) s_done = 0;
   unsigned* tab = s_tab;   // [nact][2 * LM_NSUM]
   const int ngr = nact * 2 * LM_NSUM;
   unsigned long long tm[4] = {0, 0, 0, 0};
+  // pre0: iteration zero's edge half, summed over the geometry blocks' partials in block order (every block the same
+  // bits); the surf half is formed from G below as in every evaluation
+  __shared__ double s_esum[LM_NSUM];
+  __shared__ unsigned s_xch[kMaxShardRanks * 2 * LM_NSUM];   // peer sharding: every rank's sums (u32 halves)
+  const bool pre0 = GRAM && !HUBER && a.epart != nullptr;
+  if (pre0) reduce_blocks([&](int c, int b) { return a.epart[b * LM_NSUM + c]; }, a.nbe, s_esum);
   const unsigned long long t_loop = __builtin_amdgcn_s_memrealtime();
   int failed_at = -1;   // evaluation whose granules never arrived (never expected)
   for (int it = 0; it < 5; ++it) {
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     __syncthreads();   // s_pt and s_done of this evaluation
     if (s_done) break;
+    if (pre0 && it == 0) {   // (block-uniform) no records to evaluate, nothing to hand off: the surf half, then control
+      if (tid >= NR) surf_sums_wave(s_pt, o, G, (double)sst.corr_surf, s_ssum, lane);
+      if (__syncthreads_or(a.fail_test != 0)) {
+        failed_at = it;
+        break;
+      }
+      if (tid < LM_NSUM) s_sums[tid] = s_esum[tid] + s_ssum[tid];   // edge + surf
+      __syncthreads();
+      if (a.world > 1 && !peer_exchange(a, it, ep + (unsigned)it, s_sums, s_xch)) {
+        failed_at = it;
+        break;
+      }
+      if (tid < 64) {
+#if FLOAM_LM_STATE_REGS
+        control_step(s, sst, s_sums, lane);
+        if (tid < 7) s_pt[tid] = point_component(s, tid);
+        if (lane == 0) s_done = s.done;
+#else
+        control_step_lds(sst, s_sums, lane, s_pt, &s_done);
+#endif
+      }
+      continue;
+    }
     double acc[LM_NSUM];
     if (tid < NR) {
       R x[7];
@@ -906,11 +944,19 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
     }, nact, s_sums);
     if (GRAM && tid < LM_NSUM) s_sums[tid] = s_sums[tid] + s_ssum[tid];   // edge + surf
     __syncthreads();
+    if (a.world > 1 && !peer_exchange(a, it, tag, s_sums, s_xch)) {
+      failed_at = it;
+      break;
+    }
     const unsigned long long t3 = __builtin_amdgcn_s_memrealtime();
-    if (tid < 64) {
+    if (tid < 64) {   // the next point (if the solve goes on)
+#if FLOAM_LM_STATE_REGS
       control_step(s, sst, s_sums, lane);
-      if (tid < 7) s_pt[tid] = point_component(s, tid);   // the next point (if the solve goes on)
+      if (tid < 7) s_pt[tid] = point_component(s, tid);
       if (lane == 0) s_done = s.done;
+#else
+      control_step_lds(sst, s_sums, lane, s_pt, &s_done);
+#endif
     }
     if (a.dbg && blk == 0) {
       const unsigned long long t4 = __builtin_amdgcn_s_memrealtime();
@@ -918,11 +964,19 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
     }
   }
   if (blk != 0) return;
+#if FLOAM_LM_STATE_REGS
   if (failed_at >= 0 && tid < 64) {   // end the solve, report through n_res
     s.done = 1;
     s.n_res = -1;
   }
   if (tid == 0) store_state_core(sst, s);
+#else
+  __syncthreads();   // (wave 0's last write-back)
+  if (failed_at >= 0 && tid == 0) {   // end the solve, report through n_res
+    sst.done = 1;
+    sst.n_res = -1;
+  }
+#endif
   __syncthreads();
   publish_state(sst, a.st);
   if (a.dbg && tid == 0) {   // diagnostic stamps (100 MHz): evaluate + publish, all-gather, reduce, control step,
@@ -1052,9 +1106,16 @@ __global__ void lm_trace(const LMState* __restrict__ st, const int* __restrict__
 }
 
 LMArgs make_args(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const CorrSet& cs, const int* d_ns,
-                 int ns_ub, LMBuffers& b, unsigned long long* dbg) {
-  return LMArgs{d_st, ce.rec.p, ce.valid.p, ce.cap, d_ne, std::max(ne_ub, 0), cs.rec.p, cs.valid.p, cs.cap, d_ns,
-                std::max(ns_ub, 0), b.gmat.p, b.part.p, b.partials.p, b.sums.p, b.ticket.p, dbg, b.fail_test};
+                 int ns_ub, LMBuffers& b, unsigned long long* dbg, bool pre0 = false, const ShardPeers* peers = nullptr) {
+  LMArgs a{d_st, ce.rec.p, ce.valid.p, ce.cap, d_ne, std::max(ne_ub, 0), cs.rec.p, cs.valid.p, cs.cap, d_ns,
+           std::max(ns_ub, 0), b.gmat.p, b.part.p, b.partials.p, b.sums.p, b.ticket.p, dbg, b.fail_test,
+           pre0 ? b.epart.p : nullptr, pre0 ? b.epart_blocks : 0, 1, nullptr, {}};
+  if (peers && peers->world > 1) {
+    a.world = peers->world;
+    a.xme = peers->mine;
+    for (int r = 0; r < peers->world; ++r) a.xpeer[r] = peers->buf[r];
+  }
+  return a;
 }
 }  // namespace
 
@@ -1075,9 +1136,10 @@ void LMBuffers::reserve(hipStream_t st) {
 }
 
 void lm_solve_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const CorrSet& cs,
-                     const int* d_ns, int ns_ub, int mode, LMBuffers& b, hipStream_t st, unsigned long long* dbg) {
+                     const int* d_ns, int ns_ub, int mode, LMBuffers& b, hipStream_t st, unsigned long long* dbg,
+                     bool pre0, const ShardPeers* peers) {
   b.reserve(st);
-  const LMArgs a = make_args(d_st, ce, d_ne, ne_ub, cs, d_ns, ns_ub, b, dbg);
+  const LMArgs a = make_args(d_st, ce, d_ne, ne_ub, cs, d_ns, ns_ub, b, dbg, pre0 && (mode & LM_GRAM) != 0, peers);
   // the active blocks (at most 64 or 128 blocks of 256 threads on 256 CUs) are co-resident: checked by the caller
   // through lm_solve_coresident before it chooses this path
   if (mode & LM_GRAM) {

@@ -43,7 +43,8 @@ __global__ __launch_bounds__(kTB) void mm_keys(VoxelJobDev A, VoxelJobDev B, con
                                                unsigned* __restrict__ radix_ctl, const int* __restrict__ gate,
                                                int* __restrict__ n_dev, int* __restrict__ ctl,
                                                const MapMeta* __restrict__ metaA, const MapMeta* __restrict__ metaB,
-                                               const unsigned* __restrict__ flags, unsigned seq, int force_full) {
+                                               const unsigned* __restrict__ flags, unsigned seq, int force_full,
+                                               BucketDev bd) {
   // the prologue's loads are all issued before any is waited on (one round trip instead of four in a row): the gate,
   // the bounding-box partials, the metas, the flags, the counts and — for the merge path, where element e is scan
   // point e — this thread's first scan record and the pose (the host bound n1_ub keeps the load inside the array)
@@ -72,7 +73,7 @@ __global__ __launch_bounds__(kTB) void mm_keys(VoxelJobDev A, VoxelJobDev B, con
   __shared__ float s_mm[2][6];
   __shared__ unsigned s_hist[kRadixHistWords];
   __shared__ int s_kept;
-  radix_hist_begin(s_hist);
+  radix_hist_begin(s_hist);   // (bd.split: the bucket histogram in its first 256 words)
   if (threadIdx.x == 0) s_kept = 0;
   // both maps' bounding boxes (job B's elements are packed after job A's, whose count depends on A's mode)
 #pragma unroll
@@ -133,6 +134,8 @@ __global__ __launch_bounds__(kTB) void mm_keys(VoxelJobDev A, VoxelJobDev B, con
   const VoxelGeom& G = job ? gB : gA;
   const int n0 = job ? nB0 : nA0, n1 = job ? nB1 : nA1;
   const int start = full ? 0 : n0, count = job ? sizeB : sizeA, base = job ? sizeA : 0;
+  __shared__ uint32_t s_spl[kBuckets];
+  const bool bucket = vox_bucket_begin(bd, job, G, job ? s_mm[1][5] : s_mm[0][5], J.inv, s_spl);
   int kept = 0;
   for (int e = e0; e < count; e += gridDim.x * blockDim.x) {
     const int i = start + e;   // index into the job's [map ; scan] concatenation
@@ -155,7 +158,13 @@ __global__ __launch_bounds__(kTB) void mm_keys(VoxelJobDev A, VoxelJobDev B, con
     }
     keys[base + e] = key;
     vals[base + e] = i;
-    radix_hist_add(s_hist, key);
+    if (bucket) {
+      const unsigned b = bucket_of(s_spl, key);
+      bd.bkt[base + e] = (uint8_t)b;
+      atomicAdd(&s_hist[b], 1u);
+    } else {
+      radix_hist_add(s_hist, key);
+    }
   }
   if (kept) atomicAdd(&s_kept, kept);
   radix_hist_end(s_hist, radix_ctl);   // (its barrier orders s_kept)
@@ -658,11 +667,23 @@ void map_merge_launch(VoxelScratch2& vs, MapMergeScratch& ms, const VoxelJob& a,
   // the sort set is the scan's points on the merge path: a grid for them (a full-sort update loops over more)
   const int nset_ub = std::max(a.n1_ub, b.n1_ub);
   const unsigned kblocks = std::max(1u, std::min(div_up(std::max(nset_ub, 1), 4 * kTB), 64u));
+  // the bucket sort once its splitters are seeded (bucket.hip); the first sort takes the digit passes and seeds them
+  const bool bucket = bucket_sort_enabled(1), use_bucket = bucket && ms.bs.seeded;
+  BucketDev bd{nullptr, nullptr, nullptr};
+  if (bucket) {
+    ms.bs.reserve(n, st);
+    bd = BucketDev{use_bucket ? ms.bs.split.p : nullptr, ms.bs.bkt.p, ms.bs.geo.p};
+  }
   hipLaunchKernelGGL(mm_keys, dim3(kblocks, 2), dim3(kTB), 0, st, A, B, vs.partials.p, vs.s.k0.p, vs.s.v0.p,
                      ms.status.p, 2 * ms.tiles_cap, vs.rs.ctl.p, gate, vs.overflow.p + 2, ms.ctl.p, ka.meta_in,
-                     kb.meta_in, ms.flags.p, seq, force_full ? 1 : 0);
+                     kb.meta_in, ms.flags.p, seq, force_full ? 1 : 0, bd);
   FLOAM_LAUNCH_CHECK();
-  radix_sort_launch(vs.rs, vs.s.k0.p, vs.s.v0.p, vs.s.k1.p, vs.s.v1.p, n, st, gate, vs.overflow.p + 2);
+  if (use_bucket) {
+    bucket_sort_launch(ms.bs, vs.rs, vs.s.k0.p, vs.s.v0.p, vs.s.k1.p, vs.s.v1.p, n, st, gate, vs.overflow.p + 2);
+  } else {
+    radix_sort_launch(vs.rs, vs.s.k0.p, vs.s.v0.p, vs.s.k1.p, vs.s.v1.p, n, st, gate, vs.overflow.p + 2);
+    if (bucket) bucket_seed_launch(ms.bs, vs.s.k0.p, vs.overflow.p + 2, n, st, gate);
+  }
   if (per == 2)
     hipLaunchKernelGGL(mm_merge<2>, dim3(tilesA + tilesB), dim3(kTB), 0, st, A, B, ka, kb, vs.s.k0.p, vs.s.v0.p,
                        ms.ctl.p, ms.status.p, ms.tiles_cap, tilesA, vs.rs.ctl.p, gate, seq, violate_mod,

@@ -1,6 +1,7 @@
 // Incremental map update of addPointsToMap (src/odomEstimationClass.cpp:253-294): merge the sorted new scan voxels
 // into the voxel-ordered map instead of re-sorting the whole map — see mapmerge.hip.
 #pragma once
+#include "bucket.hpp"
 #include "grid.hpp"
 #include "voxel.hpp"
 
@@ -10,6 +11,10 @@ struct MapMergeScratch {
   DevBuf<unsigned long long> status;   // [2][tiles_cap] lookback words of the merge (one array per map)
   DevBuf<int> ctl;                     // [kMergeCtlWords]
   DevBuf<unsigned> flags;              // [2]
+  // the scan-voxel sort's splitters: the map merge's own (its keys are map-frame cells of the new scan; the call's
+  // VoxelGrids, whose scratch the merge otherwise shares, sort sensor-frame cells — each pipeline's quantiles predict
+  // only its own next sort)
+  BucketScratch bs;
   int tiles_cap = 0;
   void reserve(int tiles_per_job, hipStream_t st);
 };

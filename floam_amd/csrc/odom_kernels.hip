@@ -9,6 +9,7 @@
 #include <climits>
 
 #include "grid.hpp"
+#include "lm_eval.hpp"
 #include "odom_kernels.hpp"
 
 namespace floam {
@@ -674,9 +675,11 @@ __device__ __forceinline__ int xcd_block(int p, int nactive) {
 // points within 1 m matter.  Stage 1 scans the 3x3x3 FINE cells (edge 0.5 m) around the query's cell: every point
 // outside that block is at least 0.5 m away along some axis, so its float sq-distance is >= 0.25 (exact: the cell
 // bounds are exact and fl(dx) >= 0.5 by monotone rounding); if 5 points with sq-distance < 0.25 were found they are
-// the exact 5-NN.  Otherwise stage 2 scans the COARSE cells (1 m) spanning [q-1, q+1] on every axis (<= 3x3x3),
-// which contain every point within 1 m.  Ties at equal float distance go to the lower map index (FLANN's own order
-// depends on its tree traversal; tie-free data is identical).
+// the exact 5-NN.  Otherwise stage 2 scans the COARSE cells (1 m) spanning [q - r, q + r] on every axis (<= 3x3x3):
+// r = 1 m (every point within 1 m) unless stage 1 already found 5 points within 1 m, then r = sqrt(d5) (1 + 1e-6) with
+// d5 their 5th float sq-distance (the ball that holds the 5-NN and every tie with the 5th; see knn_group).  Ties at
+// equal float distance go to the lower map index (FLANN's own order depends on its tree traversal; tie-free data is
+// identical).
 // Output: valid bit 0 = 5 neighbours within sqd < 1 (their coordinates in nnxyz), bit 1 = stage 2 was needed.
 // Low fine corner of a query's stage-1 block: nb = 3, the cells around the query's (qx, qy, qz); nb = 2, the
 // query's cell and the neighbour on the nearer side per axis (2 w - f is exact: f = floor(2 w) and 2 w are floats
@@ -814,8 +817,10 @@ __global__ __launch_bounds__(kTB, W) void knn_kernel(LMState* __restrict__ st, c
 // Surf record i as the 13-vector w = [n (x) p (9), n (3), d + n.o] (p the sensor-frame point, n the unit normal,
 // d the plane offset, o the solve's starting translation): every surf residual and Jacobian entry is linear in w
 // (see lm.hip surf_sums_from_gram), so the surf half of each squared-loss LM evaluation needs only sum(w w^T).
+// EDGE with w != null: the record's 9 values are also returned in w (the iteration-zero edge sums).  Returns whether
+// the query produced a record.
 template <bool EDGE, typename R>
-__device__ __forceinline__ void geom_query(LMState* __restrict__ st, const CorrArgs& A, int i,
+__device__ __forceinline__ bool geom_query(LMState* __restrict__ st, const CorrArgs& A, int i,
                                            double* __restrict__ w = nullptr, const double* o = nullptr) {
   const int n = min(*A.d_n, A.n_ub);
   bool ok = false;
@@ -856,6 +861,13 @@ __device__ __forceinline__ void geom_query(LMState* __restrict__ st, const CorrA
         rec[5 * cap + i] = R(0.1) * u[2] + cc[2];
         rec[6 * cap + i] = R(-0.1) * u[0] + cc[0]; rec[7 * cap + i] = R(-0.1) * u[1] + cc[1];
         rec[8 * cap + i] = R(-0.1) * u[2] + cc[2];
+        if (w) {   // (the same values as stored)
+          w[0] = cpx; w[1] = cpy; w[2] = cpz;
+          w[3] = (double)(R(0.1) * u[0] + cc[0]); w[4] = (double)(R(0.1) * u[1] + cc[1]);
+          w[5] = (double)(R(0.1) * u[2] + cc[2]);
+          w[6] = (double)(R(-0.1) * u[0] + cc[0]); w[7] = (double)(R(-0.1) * u[1] + cc[1]);
+          w[8] = (double)(R(-0.1) * u[2] + cc[2]);
+        }
       }
     } else {
       // addSurfCostFactor geometry (odomEstimationClass.cpp:208-243)
@@ -892,6 +904,7 @@ __device__ __forceinline__ void geom_query(LMState* __restrict__ st, const CorrA
   }
   const unsigned long long b = __ballot(ok);
   if ((threadIdx.x & 63) == 0 && b) atomicAdd(EDGE ? &st->corr_edge : &st->corr_surf, __popcll(b));
+  return ok;
 }
 
 __device__ __forceinline__ void gram_pair(int e, int& i, int& j) {   // upper-triangle entry e -> (i, j), i <= j
@@ -909,9 +922,44 @@ __device__ __forceinline__ void gram_pair(int e, int& i, int& j) {   // upper-tr
 template <typename R>
 __global__ __launch_bounds__(kTB) void geom_kernel(LMState* __restrict__ st, CorrArgs E, CorrArgs S, int nbE,
                                                    double* __restrict__ gpart, double* __restrict__ gmat,
-                                                   unsigned* __restrict__ gcnt) {
+                                                   unsigned* __restrict__ gcnt, double* __restrict__ epart) {
   if ((int)blockIdx.x < nbE) {
-    geom_query<true, R>(st, E, blockIdx.x * blockDim.x + threadIdx.x);
+    if (!epart) {
+      geom_query<true, R>(st, E, blockIdx.x * blockDim.x + threadIdx.x);
+      return;
+    }
+    // the record's residual and Jacobian at the solve's starting point (EdgeAnalyticCostFunction::Evaluate,
+    // src/lidarOptimization.cpp:12-43): iteration zero's edge half of the next solve, summed per block in a fixed
+    // order (wave butterflies, then the 4 waves in order) into epart[block]
+    double x[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) x[k] = st->x[k];
+    double r9[9];
+    const bool ok = geom_query<true, R>(st, E, blockIdx.x * blockDim.x + threadIdx.x, r9);
+    double acc[LM_NSUM];
+#pragma unroll
+    for (int k = 0; k < LM_NSUM; ++k) acc[k] = 0.0;
+    if (ok) {
+      double J[6];
+      const double r = lmev::edge_residual<double>(x, r9, J);
+      lmev::accumulate_residual<false, double>(acc, r, J);
+    }
+    __shared__ double s_e[kTB / 64][LM_NSUM];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < LM_NSUM; ++k) {
+      double v = acc[k];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      if (lane == 0) s_e[wv][k] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < LM_NSUM) {
+      double v = s_e[0][threadIdx.x];
+#pragma unroll
+      for (int k = 1; k < kTB / 64; ++k) v += s_e[k][threadIdx.x];
+      epart[blockIdx.x * LM_NSUM + threadIdx.x] = v;
+    }
     return;
   }
   const int sb = (int)blockIdx.x - nbE;
@@ -1369,7 +1417,7 @@ void knn_launch(LMState* d_st, const double* x0_dev, const QuerySet& qe, const G
 }
 
 void geom_launch(LMState* d_st, const QuerySet& qe, CorrSet& ce, const QuerySet& qs, CorrSet& cs, bool gram,
-                 bool fp32, LMBuffers& b, hipStream_t st) {
+                 bool fp32, LMBuffers& b, hipStream_t st, bool edge_sums) {
   if (qe.n_ub <= 0 && qs.n_ub <= 0) return;
   if (gram) b.reserve(st);
   Grid none;
@@ -1378,12 +1426,18 @@ void geom_launch(LMState* d_st, const QuerySet& qe, CorrSet& ce, const QuerySet&
   const unsigned gE = div_up(std::max(qe.n_ub, 1), kTB);
   double* gpart = gram ? b.gpart.p : nullptr;
   double* gmat = gram ? b.gmat.p : nullptr;
+  double* epart = nullptr;
+  if (gram && edge_sums && !fp32) {
+    b.epart.reserve((size_t)gE * LM_NSUM);
+    b.epart_blocks = (int)gE;
+    epart = b.epart.p;
+  }
   if (fp32)
     hipLaunchKernelGGL(geom_kernel<float>, dim3(gE + kSurfGeomBlocks), dim3(kTB), 0, st, d_st, E, S, (int)gE,
-                       gpart, gmat, b.gcnt.p);
+                       gpart, gmat, b.gcnt.p, nullptr);
   else
     hipLaunchKernelGGL(geom_kernel<double>, dim3(gE + kSurfGeomBlocks), dim3(kTB), 0, st, d_st, E, S, (int)gE,
-                       gpart, gmat, b.gcnt.p);
+                       gpart, gmat, b.gcnt.p, epart);
   FLOAM_LAUNCH_CHECK();
 }
 

@@ -165,6 +165,8 @@ __device__ __forceinline__ double gram_load(const double* __restrict__ gmat, int
 }
 constexpr int kEdgeEvalBlocks = 64;                // edge-only evaluation grid of the Gram solves (fixed order)
 constexpr int kRecEvalBlocks = 128;                // per-record evaluation grid (Huber / fp32; fixed order)
+constexpr int kMaxShardRanks = 8;                   // peer sharding: ranks (one node's GPUs)
+constexpr int kShardXchgWords = 512;                // peer sharding: exchange buffer granules (2 x 58 used; 4 KB)
 
 // LM modes: surf half from the Gram matrix (squared loss, fp64), Huber loss, fp32 geometry + residuals / Jacobians
 enum { LM_GRAM = 1, LM_HUBER = 2, LM_FP32 = 4 };
@@ -179,6 +181,10 @@ struct LMBuffers {
   DevBuf<double> gpart;              // surf Gram matrix: per-block and per-group partials (geom_kernel)
   DevBuf<double> gmat;               // the solve's surf Gram matrix + its origin
   DevBuf<unsigned> gcnt;             // ticket words of the Gram reduction
+  // the edge half of a squared-loss solve's iteration zero, evaluated by the geometry launch's edge blocks while they
+  // build the records (one 29-sum partial per block, fixed order; the solve adds them up in its prologue)
+  DevBuf<double> epart;
+  int epart_blocks = 0;
   int fail_test = 0;                 // FLOAM_LM_FAIL_TEST=1 (tests): every resident solve reports its hand-off as
                                      // timed out (n_res < 0), the path a lost block would take
   void reserve(hipStream_t st);
@@ -275,8 +281,10 @@ void knn_launch(LMState* d_st, const double* x0_dev, const QuerySet& qe, const G
                 const QuerySet& qs, const Grid& gs, CorrSet& cs, const int* d_me, const int* d_ms, int rank, int world,
                 hipStream_t st);
 // gram: the squared-loss solves' surf Gram matrix of the accepted surf records into b.gmat (b.gpart's partials)
+// edge_sums (gram only): the edge blocks also evaluate their accepted records at st->x into b.epart — iteration zero's
+// edge half for a resident solve launched with pre0 (lm_solve_launch)
 void geom_launch(LMState* d_st, const QuerySet& qe, CorrSet& ce, const QuerySet& qs, CorrSet& cs, bool gram,
-                 bool fp32, LMBuffers& b, hipStream_t st);
+                 bool fp32, LMBuffers& b, hipStream_t st, bool edge_sums = false);
 // algorithmic bytes of the correspondence pass just issued (profiling only), accumulated into *d_bytes
 void knn_traffic_launch(const LMState* d_st, const QuerySet& q, const Grid& g, CorrSet& c, int rank, int world,
                         DevBuf<unsigned long long>& set, unsigned long long* d_bytes, hipStream_t st);
@@ -285,9 +293,19 @@ void knn_traffic_launch(const LMState* d_st, const QuerySet& q, const Grid& g, C
 // A whole ceres::Solve (iteration zero + up to max_num_iterations = 4 candidates, src/odomEstimationClass.cpp:95-108)
 // in ONE launch on a single GPU: every block keeps its records in registers, evaluates them, all-gathers the blocks'
 // partial sums and runs the Ceres 1.13 control step itself (the same bits in every block).  mode = LM_*.
+// pre0 (LM_GRAM only): iteration zero's edge sums come from the geometry launch (geom_launch edge_sums): the solve
+// starts with its first control step, without the first evaluation's records and hand-off.
+// peers (world > 1): query sharding with the resident solve — each rank's blocks reduce the rank's sums as above, then
+// exchange them with the other ranks through peer-mapped buffers (every rank's buffer readable from every GPU), summed
+// in rank order; one launch per solve, no collective launch, no host round trip.
+struct ShardPeers {
+  int world = 1;
+  unsigned long long* mine = nullptr;                            // this rank's exchange buffer (kShardXchgWords)
+  const unsigned long long* buf[kMaxShardRanks] = {};            // every rank's, as mapped on this GPU (rank order)
+};
 void lm_solve_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const CorrSet& cs,
                      const int* d_ns, int ns_ub, int mode, LMBuffers& b, hipStream_t st,
-                     unsigned long long* dbg = nullptr);
+                     unsigned long long* dbg = nullptr, bool pre0 = false, const ShardPeers* peers = nullptr);
 // The same solve sharded over ranks (one process per GPU): evaluation k = 0..4 in one launch each (the control step
 // of evaluation k - 1 folded in, run redundantly by every block on the all-reduced sums), leaving this rank's 29
 // sums in b.sums for the caller's all-reduce; lm_shard_final_launch runs the last control step.

@@ -47,7 +47,7 @@ __global__ __launch_bounds__(kTB) void vox_keys(VoxelJobDev A, VoxelJobDev B, co
                                                 int* __restrict__ overflow, unsigned long long* __restrict__ status,
                                                 int ntiles, unsigned* __restrict__ ticket,
                                                 unsigned* __restrict__ radix_ctl, const int* __restrict__ gate,
-                                                int* __restrict__ n_dev) {
+                                                int* __restrict__ n_dev, BucketDev bd) {
   // the prologue's loads are issued together (one round trip instead of three in a row): the gate, the partials,
   // the counts and this thread's first record of the first part (inside the array by the host bound n0_ub)
   const int job = blockIdx.y;
@@ -65,6 +65,7 @@ __global__ __launch_bounds__(kTB) void vox_keys(VoxelJobDev A, VoxelJobDev B, co
   if (!gv) return;
   __shared__ float s_mm[6];
   __shared__ unsigned s_hist[kRadixHistWords];
+  // bd.split: the bucket sort (its bucket histogram in s_hist[0, 256)), else the four digit histograms
   radix_hist_begin(s_hist);
   if (threadIdx.x < 6 * 32) {   // the partials' min / max per component: 32 lanes, then a 32-lane reduction
     const bool is_min = c < 3;
@@ -92,6 +93,8 @@ __global__ __launch_bounds__(kTB) void vox_keys(VoxelJobDev A, VoxelJobDev B, co
   const int n0 = job ? nB0 : nA0, n1 = job ? nB1 : nA1;
   const int base = job ? nA0 + nA1 : 0;
   if (job == 0 && blockIdx.x == 0 && threadIdx.x == 0) *n_dev = nA0 + nA1 + nB0 + nB1;
+  __shared__ uint32_t s_spl[kBuckets];
+  const bool bucket = vox_bucket_begin(bd, job, g, mx[2], J.inv, s_spl);
   for (int i = i0; i < n0 + n1; i += gridDim.x * blockDim.x) {
     uint32_t key = 0xFFFFFFFFu;
     PointRec p;
@@ -113,9 +116,15 @@ __global__ __launch_bounds__(kTB) void vox_keys(VoxelJobDev A, VoxelJobDev B, co
     }
     keys[base + i] = key;
     vals[base + i] = i;
-    radix_hist_add(s_hist, key);
+    if (bucket) {
+      const unsigned b = bucket_of(s_spl, key);
+      bd.bkt[base + i] = (uint8_t)b;
+      atomicAdd(&s_hist[b], 1u);
+    } else {
+      radix_hist_add(s_hist, key);
+    }
   }
-  radix_hist_end(s_hist, radix_ctl);
+  radix_hist_end(s_hist, radix_ctl);   // (the bucket counts are the words of digit pass 0)
 }
 
 // Run heads of the sorted keys -> output slot per cloud (decoupled lookback over tiles) -> centroid of the run.
@@ -468,8 +477,10 @@ void voxel2_launch(VoxelScratch2& sc, const VoxelJob& a, const VoxelJob& b, hipS
   sc.s.reserve(n);
   sc.partials.reserve(2 * kMinMaxBlocks * 6);
   sc.overflow.reserve(3);   // [0, 1] index overflow per cloud, [2] packed element count
+  const bool bucket = bucket_sort_enabled(0);
   const int ntiles = (int)div_up(n, kTile);
-  sc.status.reserve(ntiles);
+  const int nstatus = bucket ? std::max(ntiles, kBuckets) : ntiles;   // the compaction's lookback words
+  sc.status.reserve(nstatus);
   sc.ticket.reserve(1);
   const int umax = std::max(A.n0_ub + A.n1_ub, b.n0_ub + (b.part1 ? b.n1_ub : 0));
   sc.rs.reserve(n, st);
@@ -479,11 +490,24 @@ void voxel2_launch(VoxelScratch2& sc, const VoxelJob& a, const VoxelJob& b, hipS
   }
   // few blocks: each folds its LDS digit histograms into the global ones with one atomic per non-zero bin
   const unsigned kb = std::max(1u, std::min(div_up(std::max(umax, 1), kTB), 64u));
+  // the bucket sort once its splitters are seeded; the first sort of the pipeline takes the digit passes and seeds them
+  const bool use_bucket = bucket && sc.bs.seeded;
+  BucketDev bd{nullptr, nullptr, nullptr};
+  if (bucket) {
+    sc.bs.reserve(n, st);
+    bd = BucketDev{use_bucket ? sc.bs.split.p : nullptr, sc.bs.bkt.p, sc.bs.geo.p};
+  }
   hipLaunchKernelGGL(vox_keys, dim3(kb, 2), dim3(kTB), 0, st, A, B, sc.partials.p, sc.s.k0.p, sc.s.v0.p,
-                     sc.overflow.p, sc.status.p, ntiles, sc.ticket.p, sc.rs.ctl.p, gate, sc.overflow.p + 2);
+                     sc.overflow.p, sc.status.p, nstatus, sc.ticket.p, sc.rs.ctl.p, gate, sc.overflow.p + 2, bd);
   FLOAM_LAUNCH_CHECK();
+  if (use_bucket) {   // scatter by bucket, and one block per bucket that sorts it and emits its voxels
+    bucket_voxel_launch(sc.bs, sc.rs, A, B, sc.s.k0.p, sc.s.v0.p, sc.s.k1.p, sc.s.v1.p, n, sc.overflow.p,
+                        sc.status.p, st, gate, sc.overflow.p + 2);
+    return;
+  }
   // sorted pairs in k0 / v0; the passes and the compaction work on the packed device count
   radix_sort_launch(sc.rs, sc.s.k0.p, sc.s.v0.p, sc.s.k1.p, sc.s.v1.p, n, st, gate, sc.overflow.p + 2);
+  if (bucket) bucket_seed_launch(sc.bs, sc.s.k0.p, sc.overflow.p + 2, n, st, gate);
   hipLaunchKernelGGL(vox_compact, dim3(ntiles), dim3(kTB), 0, st, A, B, sc.s.k0.p, sc.s.v0.p, sc.overflow.p,
                      sc.overflow.p + 2, sc.status.p, sc.ticket.p, sc.rs.ctl.p, gate, n, vox_stamps_on());
   FLOAM_LAUNCH_CHECK();

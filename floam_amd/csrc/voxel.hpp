@@ -3,6 +3,7 @@
 #include <cfloat>
 #include <climits>
 
+#include "bucket.hpp"
 #include "cloud_ops.hpp"
 #include "floam_common.hpp"
 #include "radix.hpp"
@@ -204,7 +205,29 @@ struct VoxelScratch2 {
   DevBuf<unsigned long long> status;
   DevBuf<unsigned> ticket;
   RadixScratch rs;
+  BucketScratch bs;   // the bucket sort (bucket.hip), the default; FLOAM_SORT=radix: the four digit passes of rs
 };
+
+// dy and dz of a VoxelGrid's box (dx = divb_mul[1]) from its geometry and the box's max z
+__device__ __forceinline__ void voxel_dims(const VoxelGeom& g, float mx_z, float inv, long long& dx, long long& dy,
+                                           long long& dz) {
+  dx = g.divb_mul[1];
+  dy = g.divb_mul[1] ? g.divb_mul[2] / g.divb_mul[1] : 0;
+  dz = (long long)floorf(mx_z * inv) - g.min_b[2] + 1;
+}
+
+// The key producer's bucket stage (bucket.hip), called by every thread of a block whose cloud is `job`: the grid's
+// splitters into s_spl (LDS, 256), the grid for the next splitters (block 0 of the job).  Returns whether the
+// bucket sort runs (else the producer builds digit histograms for the radix passes).
+__device__ __forceinline__ bool vox_bucket_begin(const BucketDev& bd, int job, const VoxelGeom& g, float mx_z,
+                                                 float inv, uint32_t* s_spl) {
+  long long dx, dy, dz;
+  voxel_dims(g, mx_z, inv, dx, dy, dz);
+  if (bd.geo && blockIdx.x == 0 && threadIdx.x == 0) bucket_geo_store(bd.geo, job, g.min_b, (int)dx, (int)dy, g.overflow);
+  if (!bd.split) return false;
+  bucket_keys_lds(bd.split, job, g.min_b, dx, dy, dz, g.overflow, s_spl);
+  return true;
+}
 
 // Two independent voxel grids in one pipeline (3 kernels + the 4 radix passes).  *d_out of each job receives the
 // voxel count (-1 if the single-pass compaction failed, never expected).  gate (device int, nullable): when it reads
@@ -212,6 +235,13 @@ struct VoxelScratch2 {
 // minmax_done: a producer kernel already ran the bounding-box stage with voxel2_prepare's VoxelFused (same jobs).
 // FLOAM_VOX_STAMPS=1: print vox_compact's in-kernel phase times (diagnostic; synchronises the device)
 void vox_stamps_print();
+
+// The sort + compaction half of the pipeline with the bucket sort (bucket.hip): plan, bucket scatter, and one block
+// per bucket that sorts it and emits its voxels (output slots by lookback over the 256 buckets: status must hold >= 256
+// zeroed words).  k0 / v0 hold the keys from vox_keys (with the bucket histogram); the outputs land in A.out / B.out.
+void bucket_voxel_launch(BucketScratch& bs, RadixScratch& rs, const VoxelJobDev& A, const VoxelJobDev& B, uint32_t* k0,
+                         int* v0, uint32_t* k1, int* v1, int n, const int* overflow, unsigned long long* status,
+                         hipStream_t st, const int* gate, const int* n_dev);
 
 void voxel2_launch(VoxelScratch2& sc, const VoxelJob& a, const VoxelJob& b, hipStream_t st,
                    const int* gate = nullptr, bool minmax_done = false);

@@ -6,6 +6,8 @@ Same method names, argument meaning and append semantics as the reference; cloud
 from __future__ import annotations
 
 import ctypes as C
+
+import numpy as np
 from dataclasses import dataclass
 
 from . import _ffi
@@ -59,6 +61,7 @@ class LaserProcessingClass:
         p = lidar_param.to_c()
         _ffi.check(self._L.floam_lp_create(C.byref(p), self.device, C.byref(h)))
         self._h = h
+        self._lines = int(lidar_param.num_lines)
         if self.asynchronous:
             _ffi.check(self._L.floam_lp_set_async(self._h, 1))
 
@@ -73,6 +76,22 @@ class LaserProcessingClass:
         if self._h is None:
             raise _ffi.FloamError(_ffi.ERR_INVALID_ARGUMENT, "LaserProcessingClass.init() not called")
         _ffi.check(self._L.floam_lp_feature_extraction(self._h, pc_in.handle, pc_out_edge.handle, pc_out_surf.handle))
+
+    def featureExtractionHost(self, points):
+        """featureExtraction on a host cloud (POINT_DTYPE array, what the processing node holds): returns the
+        (edge, surf) feature arrays — floam_lp_feature_extraction_host, the drop-in adapter's one-call path."""
+        from .synth import POINT_DTYPE
+        if self._h is None:
+            raise _ffi.FloamError(_ffi.ERR_INVALID_ARGUMENT, "LaserProcessingClass.init() not called")
+        a = np.ascontiguousarray(points, dtype=POINT_DTYPE)
+        n = a.shape[0]
+        edge = np.zeros(max(1, min(n, self._lines * 120)), POINT_DTYPE)
+        surf = np.zeros(max(1, n), POINT_DTYPE)
+        ne, ns = C.c_size_t(), C.c_size_t()
+        _ffi.check(self._L.floam_lp_feature_extraction_host(
+            self._h, a.ctypes.data_as(C.c_void_p), n, 32, edge.ctypes.data_as(C.c_void_p), edge.shape[0],
+            C.byref(ne), surf.ctypes.data_as(C.c_void_p), surf.shape[0], C.byref(ns)))
+        return edge[: ne.value].copy(), surf[: ns.value].copy()
 
     def close(self) -> None:
         if getattr(self, "_h", None):

@@ -66,6 +66,18 @@ class OdomEstimationClass:
                                                                           surf_in.handle, int(bool(deskew))))
         return self.last_status
 
+    def UpdatePointsToMapSelectorHost(self, edge_in, surf_in, deskew: bool) -> int:
+        """UpdatePointsToMapSelector on host clouds (POINT_DTYPE arrays, deskewed IN PLACE like the reference, Q5):
+        floam_odom_update_selector_host, the drop-in adapter's one-call path (synchronous)."""
+        from .synth import POINT_DTYPE
+        for a in (edge_in, surf_in):
+            if not (isinstance(a, np.ndarray) and a.dtype == POINT_DTYPE and a.flags["C_CONTIGUOUS"]):
+                raise _ffi.FloamError(_ffi.ERR_INVALID_ARGUMENT, "host clouds must be contiguous POINT_DTYPE arrays")
+        self.last_status = _ffi.check(self._L.floam_odom_update_selector_host(
+            self._need(), edge_in.ctypes.data_as(C.c_void_p), edge_in.shape[0], surf_in.ctypes.data_as(C.c_void_p),
+            surf_in.shape[0], 32, int(bool(deskew))))
+        return self.last_status
+
     def updatePointsToMap(self, edge_in: DeviceCloud, surf_in: DeviceCloud,
                           update_type: UpdateType = UpdateType.VANILLA) -> int:
         """src/odomEstimationClass.cpp:52-124"""
@@ -253,6 +265,26 @@ class OdomEstimationClass:
                 return 1
         self._ar_cb = _ffi.ALLREDUCE_FN(_cb)   # keep alive
         _ffi.check(self._L.floam_odom_set_shard_callback(self._need(), rank, world, self._ar_cb, None))
+
+    def shard_exchange(self):
+        """This rank's peer-sharding exchange buffer: (64-byte IPC handle for other processes, device pointer)."""
+        h = C.create_string_buffer(64)
+        ptr = C.c_void_p()
+        _ffi.check(self._L.floam_odom_shard_exchange(self._need(), h, C.byref(ptr)))
+        return h.raw, ptr.value
+
+    def set_shard_peers(self, rank: int, world: int, handles=None, ptrs=None) -> None:
+        """Peer sharding (one resident LM launch per solve; the ranks' sums exchanged through peer-mapped buffers):
+        ``handles`` = every rank's 64-byte IPC handle (rank order; other processes) or ``ptrs`` = every rank's
+        device pointer (handles in this process)."""
+        hb = pp = None
+        if handles is not None:
+            assert len(handles) == world and all(len(h) == 64 for h in handles)
+            hb = C.create_string_buffer(b"".join(bytes(h) for h in handles), 64 * world)
+        if ptrs is not None:
+            assert len(ptrs) == world
+            pp = (C.c_void_p * world)(*ptrs)
+        _ffi.check(self._L.floam_odom_set_shard_peers(self._need(), rank, world, hb, pp))
 
     def close(self) -> None:
         if getattr(self, "_h", None):

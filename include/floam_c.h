@@ -23,7 +23,7 @@
  *   2  floam_odom_keyframe_update gained the (surf, edge) cloud parameters of KeyFrameUpdate
  *      (include/odomEstimationClass.h:80); floam_abi_version added
  * A caller checks `floam_abi_version() == FLOAM_ABI_VERSION` once after loading the library. */
-#define FLOAM_ABI_VERSION 2
+#define FLOAM_ABI_VERSION 3
 
 #include <stddef.h>
 #include <stdint.h>
@@ -37,7 +37,7 @@ typedef enum floam_status {
   FLOAM_ERR_INVALID_ARGUMENT = 1,
   FLOAM_ERR_DEVICE = 2,        /* HIP runtime / kernel launch failure, or no usable gfx950 device */
   FLOAM_ERR_OUT_OF_MEMORY = 3,
-  FLOAM_ERR_UNSUPPORTED = 4,   /* input outside the kernels' envelope (e.g. a ring sector > 4096 points) */
+  FLOAM_ERR_UNSUPPORTED = 4,   /* input outside the kernels' envelope (e.g. more than 2^31 points) */
   FLOAM_ERR_COMM = 5,          /* RCCL failure in the sharded path */
   /* non-fatal, same conditions as the reference's printf warnings */
   FLOAM_WARN_MAP_TOO_SMALL = 100,       /* src/odomEstimationClass.cpp:112 "not enough points in map" */
@@ -95,6 +95,15 @@ floam_status floam_lp_destroy(floam_lp* lp);
 /* featureExtraction(pc_in, pc_out_edge, pc_out_surf) (include/laserProcessingClass.h:40,
  * src/laserProcessingClass.cpp:72-118).  Appends to edge/surf like the reference (never clears them). */
 floam_status floam_lp_feature_extraction(floam_lp* lp, const floam_cloud* in, floam_cloud* edge, floam_cloud* surf);
+/* The same for host-resident clouds (the drop-in adapter's path: the node hands PCL clouds in and publishes PCL
+ * clouds): `in` = n PointXYZIRT records (stride 32, e.g. pcl::PointCloud::points.data()); the edge / surf features
+ * are WRITTEN (not appended) to the caller's arrays of capacity edge_cap / surf_cap records and their counts returned
+ * (the adapter appends by passing the ends of its vectors, resized by the bounds num_lines * 120 and n).  One upload,
+ * the extraction and both downloads with a single synchronisation.  FLOAM_ERR_INVALID_ARGUMENT if a capacity is
+ * short (nothing written). */
+floam_status floam_lp_feature_extraction_host(floam_lp* lp, const void* in, size_t n, size_t stride, void* edge,
+                                              size_t edge_cap, size_t* n_edge, void* surf, size_t surf_cap,
+                                              size_t* n_surf);
 /* pcl::VoxelGrid<PointXYZI> with a cubic leaf (PCL 1.8.1 semantics; the filter of downSamplingToMap,
  * src/odomEstimationClass.cpp:137-142, and of the mapping node, src/laserMappingClass.cpp:174-183): one centroid
  * of x, y, z, intensity per occupied voxel in ascending voxel index, the input returned unchanged when the index
@@ -225,6 +234,12 @@ floam_status floam_odom_init_map(floam_odom* o, const floam_cloud* edge, const f
 /* UpdatePointsToMapSelector(edge_in, surf_in, deskew) (src/odomEstimationClass.cpp:34-50).  With deskew the
  * clouds are velocity-compensated IN PLACE, as the reference does (Q5). */
 floam_status floam_odom_update_selector(floam_odom* o, floam_cloud* edge, floam_cloud* surf, int deskew);
+/* The same for host-resident clouds (the drop-in adapter: UpdatePointsToMapSelector on the node's PCL clouds, stride
+ * 32 records): both clouds uploaded, the update run synchronously, and with deskew the compensated records copied
+ * back into the caller's arrays (Q5) on a copy stream as soon as the deskew kernel has run — overlapped with the
+ * update's second call — instead of 2 uploads + the update + 2 size queries + 2 downloads. */
+floam_status floam_odom_update_selector_host(floam_odom* o, void* edge, size_t n_edge, void* surf, size_t n_surf,
+                                             size_t stride, int deskew);
 /* updatePointsToMap(edge_in, surf_in, update_type) (src/odomEstimationClass.cpp:52-124) */
 floam_status floam_odom_update(floam_odom* o, const floam_cloud* edge, const floam_cloud* surf, int update_type);
 /* Streaming mode (no reference counterpart: the reference's odometry node processes one scan per callback,
@@ -320,6 +335,19 @@ floam_status floam_odom_set_shard(floam_odom* o, int rank, int world, const void
  * run (several ranks on one GPU); synchronises once per LM evaluation. */
 typedef int (*floam_allreduce_fn)(double* values, int count, void* user);
 floam_status floam_odom_set_shard_callback(floam_odom* o, int rank, int world, floam_allreduce_fn fn, void* user);
+/* Peer sharding (ABI 3): the same query partition, but the LM solve stays ONE resident launch per ceres::Solve
+ * (src/odomEstimationClass.cpp:100-108): each rank publishes its 29 sums per LM evaluation into a 4-KB exchange buffer
+ * on its own GPU and reads every rank's buffer through peer mappings (xGMI), summing them in rank order — no
+ * collective launch, no host round trip; every rank takes the same LM decisions.  A rank that never publishes ends
+ * the solve after ~20 s with FLOAM_ERR_DEVICE (the handle is then poisoned).
+ *   floam_odom_shard_exchange: this rank's buffer as an IPC handle (64 bytes, for the other processes) and/or as a
+ *   device pointer (for handles in the same process).
+ *   floam_odom_set_shard_peers: every rank's buffer, either as world x 64 bytes of IPC handles (entry `rank` is not
+ *   opened) or as world device pointers; exactly one of the two.  world <= 8.  All ranks must issue their updates
+ *   concurrently (one process or host thread per rank). */
+floam_status floam_odom_shard_exchange(floam_odom* o, void* ipc_handle_64, void** dev_ptr);
+floam_status floam_odom_set_shard_peers(floam_odom* o, int rank, int world, const void* ipc_handles,
+                                        void* const* dev_ptrs);
 
 /* ------------------------------------------------------------------------------------------ misc */
 const char* floam_last_error(void);

@@ -45,6 +45,19 @@ int main(int argc, char** argv) {
   const bool expect_no_device = argc > 2 && std::strcmp(argv[2], "nodevice") == 0;
 
   CHECK(std::strstr(floam_version(), "gfx950") != nullptr);
+  CHECK(floam_abi_version() == FLOAM_ABI_VERSION);
+  {   // the one-call host entry points of the drop-in adapters (ABI 2): argument validation needs no device
+    size_t ne = 7, ns = 7;
+    CHECK(floam_lp_feature_extraction_host(nullptr, nullptr, 0, 32, nullptr, 0, &ne, nullptr, 0, &ns) ==
+          FLOAM_ERR_INVALID_ARGUMENT);
+    CHECK(floam_odom_update_selector_host(nullptr, nullptr, 0, nullptr, 0, 32, 1) == FLOAM_ERR_INVALID_ARGUMENT);
+  }
+  {   // peer sharding (ABI 3): validation before any device work
+    char h[64];
+    void* p = nullptr;
+    CHECK(floam_odom_shard_exchange(nullptr, h, &p) == FLOAM_ERR_INVALID_ARGUMENT && p == nullptr);
+    CHECK(floam_odom_set_shard_peers(nullptr, 0, 2, h, nullptr) == FLOAM_ERR_INVALID_ARGUMENT);
+  }
 
   // null handles / arguments are rejected with a message, never dereferenced
   CHECK(floam_cloud_create(0, 0, nullptr) == FLOAM_ERR_INVALID_ARGUMENT);

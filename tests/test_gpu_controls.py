@@ -47,6 +47,18 @@ def test_per_evaluation_fallback_matches_resident_solve(floam_gpu, monkeypatch, 
         np.testing.assert_allclose(qb, qa, rtol=0, atol=1e-12, err_msg=f"scan {k}")
 
 
+def test_iteration_zero_from_geometry_matches(floam_gpu, monkeypatch):
+    """FLOAM_LM_PRE0=1 (off by default, measured slower): the geometry launch evaluates iteration zero's edge half
+    and the solve starts with its first control step.  Only the summation order of that evaluation differs: same LM
+    decisions, poses to ulps."""
+    ref, _ = _run(floam_gpu, 6)
+    monkeypatch.setenv("FLOAM_LM_PRE0", "1")
+    alt, _ = _run(floam_gpu, 6)
+    for k, ((qa, ta), (qb, tb)) in enumerate(zip(ref, alt)):
+        np.testing.assert_allclose(tb, ta, rtol=0, atol=1e-12, err_msg=f"scan {k}")
+        np.testing.assert_allclose(qb, qa, rtol=0, atol=1e-12, err_msg=f"scan {k}")
+
+
 def test_trace_overflow_is_reported(floam_gpu):
     """a trace capacity below the number of solves is reported (n_out > capacity), not hidden."""
     from floam_amd import FloamError

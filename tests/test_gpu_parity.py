@@ -84,8 +84,8 @@ def test_feature_extraction_edge_cases(floam_gpu, oracle_lib):
 
 def test_feature_extraction_long_sectors(floam_gpu, oracle_lib):
     """Sectors of more than 1024 entries take fe_sector's second path (listed by the first launch, run by
-    fe_sector_long): ring 0 seven times as dense (~1190-entry sectors) stays byte-identical to the oracle; a ring
-    whose sectors exceed 4096 entries is refused (FLOAM_ERR_UNSUPPORTED) rather than truncated."""
+    fe_sector_long): ring 0 seven times as dense (~1190-entry sectors) stays byte-identical to the oracle, and so
+    does a ring whose sectors exceed 4096 entries (fe_sector_huge: the sector through global memory)."""
     raw = synth.generate_scan("c1", 1)
     r0 = raw[raw["ring"] == 0]
     rng = np.random.default_rng(5)
@@ -107,8 +107,25 @@ def test_feature_extraction_long_sectors(floam_gpu, oracle_lib):
     _assert_same_cloud(s, s_ref, "surf")
     huge = np.concatenate([raw] + copies(24))   # sectors of ~4260 entries
     assert (len(r0) * 25 - 10) // 6 > 4096
-    with pytest.raises(floam_gpu.FloamError):
-        _gpu_fe(floam_gpu, huge, 16)
+    e_ref, s_ref, _ = oracle_lib.feature_extraction(huge, 16, 0.5, 90.0, canonical=True)
+    e, s, _ = _gpu_fe(floam_gpu, huge, 16)
+    _assert_same_cloud(e, e_ref, "edge (huge)")
+    _assert_same_cloud(s, s_ref, "surf (huge)")
+
+
+@pytest.mark.parametrize("config", ["c2", "c3"])
+def test_feature_extraction_ring_field_zero(floam_gpu, oracle_lib, config):
+    """A cloud whose ring field is all zero (what a PCL conversion leaves when the field is absent): the whole scan is
+    ring 0, six sectors of n / 6 entries (c2, 16 rings: ~4.8k; c3: ~21.7k) — byte-identical to the oracle."""
+    raw = synth.generate_scan(config, 2)
+    raw["ring"] = 0
+    R = synth.lidar_model(config).rings
+    assert (len(raw) - 10) // 6 > 4096
+    e_ref, s_ref, _ = oracle_lib.feature_extraction(raw, R, 0.5, 90.0, canonical=True)
+    assert len(e_ref) > 0 and len(s_ref) > 0
+    e, s, _ = _gpu_fe(floam_gpu, raw, R)
+    _assert_same_cloud(e, e_ref, "edge")
+    _assert_same_cloud(s, s_ref, "surf")
 
 
 def _angle_between(q1, q2):

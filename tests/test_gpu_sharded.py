@@ -192,3 +192,112 @@ def test_rccl_world1_matches_unsharded(floam_gpu, loss, fp32):
     ref = _run(0, 1, _free_port(), None, loss=loss, fp32=fp32)
     got = _run(0, 1, _free_port(), None, rccl_world1=True, loss=loss, fp32=fp32)
     np.testing.assert_allclose(got, ref, rtol=1e-12, atol=1e-14)
+
+
+def _run_peer(rank, world, port, q, config, nscan, maps=None):
+    """Peer sharding (floam_odom_set_shard_peers): one process per rank, the ranks' exchange buffers shared as IPC
+    handles (gathered over gloo), the resident solve exchanging the 29 sums through them.  On the one-GPU box both
+    ranks are processes on device 0 (the same IPC path as one process per GPU)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import floam_amd
+        from floam_amd import synth
+        from floam_amd.odom_estimation import reset_process_state
+        R = synth.lidar_model(config).rings
+        p = floam_amd.LidarParams(num_lines=R, scan_period=0.1, max_distance=90.0, min_distance=0.5)
+        lp = floam_amd.LaserProcessingClass(device=0)
+        lp.init(p)
+        odo = floam_amd.OdomEstimationClass(device=0)
+        odo.init(p, 0.1, "Cauchy")
+        reset_process_state()
+        handle, _ = odo.shard_exchange()
+        handles = [None] * world
+        dist.all_gather_object(handles, handle)
+        odo.set_shard_peers(rank, world, handles=handles)
+        dist.barrier()
+        poses = []
+        first = 0
+        if maps is not None:
+            odo.initMapWithPoints(floam_amd.DeviceCloud(maps[0], device=0), floam_amd.DeviceCloud(maps[1], device=0))
+            first = 1
+        for k in range(first, first + nscan):
+            de, ds = floam_amd.DeviceCloud(device=0), floam_amd.DeviceCloud(device=0)
+            lp.featureExtraction(floam_amd.DeviceCloud(synth.generate_scan(config, k), device=0), de, ds)
+            if k == 0:
+                odo.initMapWithPoints(de, ds)
+            else:
+                odo.UpdatePointsToMapSelector(de, ds, True)
+            q_, t_ = odo.pose()
+            poses.append(np.r_[q_, t_])
+        out = (np.array(poses), odo.map_sizes())
+        dist.barrier()   # (no rank closes its exchange buffer while another may still read it)
+        odo.close()
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def _peer_ranks(config, nscan, maps=None, world=2):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_run_peer, args=(r, world, port, q, config, nscan, maps)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for pr in procs:
+        pr.join(timeout=120)
+        assert pr.exitcode == 0
+    return res
+
+
+def test_peer_two_ranks_match_unsharded(floam_gpu):
+    """Peer sharding, two ranks (processes, IPC-mapped exchange buffers): poses identical on both ranks and within
+    1e-9 of the unsharded run (C1, 5 scans: the first is the map)."""
+    ref = _run(0, 1, _free_port(), None)
+    res = _peer_ranks("c1", NSCAN)
+    assert np.array_equal(res[0][0], res[1][0])
+    for k in range(NSCAN):
+        dt = np.linalg.norm(res[0][0][k][4:] - ref[k][4:])
+        dr = 2 * math.acos(min(1.0, abs(float(np.dot(res[0][0][k][:4], ref[k][:4])))))
+        assert dt < 1e-9 and dr < 1e-9, (k, dt, dr)
+
+
+def test_peer_two_ranks_c4_match_oracle(floam_gpu, oracle_lib, prefilled_map):
+    """the resident solve sharded over two ranks through peer-mapped exchange buffers at C4
+    (128 rings, 500k prefill): poses identical on both ranks and within 1e-6 m / rad of the oracle, map sizes equal."""
+    mapE, mapS = prefilled_map("c4")
+    ref, ref_sizes = _c4_oracle(oracle_lib, mapE, mapS)
+    res = _peer_ranks("c4", C4_SCANS, maps=(mapE, mapS))
+    assert np.array_equal(res[0][0], res[1][0])
+    assert res[0][1] == res[1][1] == ref_sizes, (res[0][1], res[1][1], ref_sizes)
+    _assert_close_to_oracle(res[0][0], ref, "2-rank peer shard")
+
+
+def test_peer_world1_is_the_resident_solve(floam_gpu):
+    """world = 1 peers: the plain resident solve (no exchange), bit-identical to the unsharded run."""
+    import floam_amd
+    from floam_amd import synth
+    from floam_amd.odom_estimation import reset_process_state
+    ref = _run(0, 1, _free_port(), None)
+    p = floam_amd.LidarParams(num_lines=16, scan_period=0.1, max_distance=90.0, min_distance=0.5)
+    lp = floam_amd.LaserProcessingClass(device=0)
+    lp.init(p)
+    odo = floam_amd.OdomEstimationClass(device=0)
+    odo.init(p, 0.1, "Cauchy")
+    reset_process_state()
+    h, ptr = odo.shard_exchange()
+    assert len(h) == 64 and ptr
+    odo.set_shard_peers(0, 1, ptrs=[ptr])
+    for k in range(NSCAN):
+        de, ds = floam_amd.DeviceCloud(device=0), floam_amd.DeviceCloud(device=0)
+        lp.featureExtraction(floam_amd.DeviceCloud(synth.generate_scan("c1", k), device=0), de, ds)
+        if k == 0:
+            odo.initMapWithPoints(de, ds)
+        else:
+            odo.UpdatePointsToMapSelector(de, ds, True)
+        q_, t_ = odo.pose()
+        assert np.array_equal(np.r_[q_, t_], ref[k]), k

@@ -64,3 +64,24 @@ def test_voxel_overflow_passthrough(floam_gpu, oracle_lib):
 def test_voxel_empty(floam_gpu):
     out = floam_gpu.DeviceCloud(_cloud(np.zeros((0, 3), np.float32))).voxel_grid(0.1)
     assert len(out) == 0
+
+
+def test_voxel_dense_bucket_streams(floam_gpu, oracle_lib):
+    """bucket.hip: 20000 points in 12 voxels of one thin slab share one fine-histogram bin, so one bucket exceeds
+    the 8192 elements a block sorts in LDS and is sorted through global memory (stream_sort, two digit passes over
+    the slab's key range); runs of ~1700 points also cross many compaction tiles.  Sparse points around it fill
+    the other buckets."""
+    rng = np.random.default_rng(11)
+    dense = np.stack([rng.uniform(1.0, 1.6, 20000), rng.uniform(1.0, 1.2, 20000), rng.uniform(1.0, 1.1, 20000)], 1)
+    sparse = rng.uniform(-50, 50, (6000, 3))
+    pts = _cloud(np.concatenate([sparse[:3000], dense, sparse[3000:]]).astype(np.float32))
+    got = _check(floam_gpu, oracle_lib, pts, 0.1)
+    assert got.shape[0] < pts.shape[0]
+
+
+@pytest.mark.parametrize("n", [1, 63, 257, 8193])
+def test_voxel_small_and_ragged(floam_gpu, oracle_lib, n):
+    """Counts around the sort's block and wave sizes, a few voxels each (one bucket, one digit pass or none)."""
+    rng = np.random.default_rng(n)
+    pts = _cloud(rng.uniform(0.0, 0.35, (n, 3)).astype(np.float32))
+    _check(floam_gpu, oracle_lib, pts, 0.1)
