@@ -445,19 +445,26 @@ __global__ __launch_bounds__(kTB) void bucket_compact(VoxelJobDev A, VoxelJobDev
                                                       const unsigned* __restrict__ radix_ctl,
                                                       const int* __restrict__ gate,
                                                       unsigned long long* __restrict__ split,
-                                                      const int* __restrict__ geo) {
-  const int b = blockIdx.x;
+                                                      const int* __restrict__ geo, unsigned* __restrict__ ticket) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  // prologue loads together: gate, the clouds' counts, the overflow flags (the histogram in bucket_range)
+  // the bucket is the block's ticket (zeroed by vox_keys): a bucket's lookback only waits on buckets that are already
+  // running (HIP promises no dispatch order).  Prologue loads together with it: gate, the clouds' counts, the
+  // overflow flags (the histogram in bucket_range)
+  __shared__ int s_b;
+  if (t == 0) s_b = ticket ? (int)atomicAdd(ticket, 1u) : (int)blockIdx.x;   // (null: by index, A/B only)
   const int gv = gate ? *gate : 1;
   const int nA0 = *A.d_n0, nA1 = A.d_n1 ? *A.d_n1 : 0, nB0 = *B.d_n0, nB1 = B.d_n1 ? *B.d_n1 : 0;
   const int ovf[2] = {overflow[0], overflow[1]};
-  if (!gv) {   // gated off (no keyframe): the output is the unchanged first part (the map)
+  __syncthreads();
+  const int b = s_b;
+  if (!gv) {   // gated off (no keyframe): the output is the unchanged first part (the map).  By block index: no
+    // lookback here, and the ticket counter is zeroed only by an ungated vox_keys
+    const int bi = (int)blockIdx.x;
     for (int job = 0; job < 2; ++job) {
       const VoxelJobDev& J = job == 0 ? A : B;
       const int n0 = job ? nB0 : nA0;
-      for (int i = b * kTB + t; i < n0; i += gridDim.x * kTB) J.out[i] = J.part0[i];
-      if (b == 0 && t == 0) *J.d_out = n0;
+      for (int i = bi * kTB + t; i < n0; i += gridDim.x * kTB) J.out[i] = J.part0[i];
+      if (bi == 0 && t == 0) *J.d_out = n0;
     }
     return;
   }
@@ -471,7 +478,7 @@ __global__ __launch_bounds__(kTB) void bucket_compact(VoxelJobDev A, VoxelJobDev
   if (b == kBuckets - 1 || size == 0) {   // nothing to emit: publish zero; the last bucket ends the outputs
     const Prefix2 pre = lookback_prefix(status, b, Prefix2{0, 0});
     if (b == kBuckets - 1 && t == 0) {
-      const bool failed = pre.a < 0 || radix_ctl[kRadixHistWords + 4] != 0u;   // a lookback timed out (never)
+      const bool failed = pre.a < 0 || radix_ctl[kRadixErrorWord] != 0u;   // a lookback timed out (never)
       *A.d_out = failed ? -1 : pre.a;
       *B.d_out = failed ? -1 : pre.b;
     }
@@ -666,13 +673,13 @@ bool bucket_sort_enabled(int pipeline) {
 
 void bucket_voxel_launch(BucketScratch& bs, RadixScratch& rs, const VoxelJobDev& A, const VoxelJobDev& B, uint32_t* k0,
                          int* v0, uint32_t* k1, int* v1, int n, const int* overflow, unsigned long long* status,
-                         hipStream_t st, const int* gate, const int* n_dev) {
+                         unsigned* ticket, hipStream_t st, const int* gate, const int* n_dev) {
   if (n <= 0) return;
   bs.reserve(n, st);
   rs.reserve(n, st);
   radix_digit_pass_launch(rs, k0, v0, k1, v1, n, bs.bkt.p, st, gate, n_dev);
   hipLaunchKernelGGL(bucket_compact, dim3(kBuckets), dim3(kTB), 0, st, A, B, k1, v1, k0, v0, rs.ctl.p, overflow,
-                     status, rs.ctl.p, gate, bs.split.p, bs.geo.p);
+                     status, rs.ctl.p, gate, bs.split.p, bs.geo.p, tile_by_index() ? nullptr : ticket);
   FLOAM_LAUNCH_CHECK();
 }
 

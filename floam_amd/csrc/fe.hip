@@ -18,6 +18,7 @@
 
 #include "floam_common.hpp"
 #include "fe.hpp"
+#include "profwb.hpp"
 #include "radix.hpp"
 
 namespace floam {
@@ -944,7 +945,10 @@ void fe_launch(FeScratch& sc, const FeParams& prm, const PointRec* d_in, int n, 
   // stable bucketing by ring: rings < 255 differ in the low digit only (dropped points: 0xFFFF, last); the pass
   // stages the scan ring-major
   if (R <= 255) {
+    const bool wb = prof_wb_enabled();   // (diagnostic: the pass's own write bytes, profwb.hpp)
+    if (wb) prof_l2_writeback(st);
     radix_pass_payload_launch(sc.rs, sc.keys.p, nullptr, nullptr, n, d_in, sc.ring_xyz.p, sc.ring_pts.p, st);
+    if (wb) prof_l2_writeback(st);
   } else {
     radix_pass_launch(sc.rs, sc.keys.p, sc.vals.p, sc.keys2.p, sc.surf_pos.p, n, 0, st);
     radix_pass_launch(sc.rs, sc.keys2.p, sc.surf_pos.p, sc.keys.p, sc.ring_idx.p, n, 1, st);

@@ -29,6 +29,7 @@
 // with FMA contraction, and the compiler may contract the two kernels' evaluations differently); its LM decisions are
 // identical.
 #include <cfloat>
+#include <cstdio>
 #include <climits>
 
 #include "lm_eval.hpp"
@@ -478,6 +479,23 @@ __device__ __forceinline__ bool solve_step(LMState& s, double (&delta)[6]) {
   return true;
 }
 
+// -DFLOAM_CTRL_STAMPS (diagnostic build): block 0's control-step segments, s_memrealtime (100 MHz), accumulated by
+// lane 0: [0] steps, [1] bookkeeping before the step, [2] solve_step, [3] se3_plus, [4] gradient test + candidate
+// broadcast, [5] whole step; printed by lm_ctrl_stamps_print
+#ifdef FLOAM_CTRL_STAMPS
+__device__ unsigned long long g_ctrl_stamps[8];
+#define CTRL_T(v) const unsigned long long v = __builtin_amdgcn_s_memrealtime()
+#define CTRL_ADD(k, d)                                                          \
+  do {                                                                          \
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_ctrl_stamps[k], d);   \
+  } while (0)
+#else
+#define CTRL_T(v)
+#define CTRL_ADD(k, d) \
+  do {                 \
+  } while (0)
+#endif
+
 // value of lane src (a compile-time / wave-uniform lane) to every lane: two v_readlane (no LDS round trip)
 __device__ __forceinline__ double bcast(double v, int src) {
   const unsigned long long b = (unsigned long long)__double_as_longlong(v);
@@ -491,13 +509,18 @@ __device__ __forceinline__ double bcast(double v, int src) {
 // gradient test ends the solve the step is discarded, as in the sequential order (test first, then step).
 __device__ __forceinline__ void next_step_wave(LMState& s, bool check_gmax, int lane) {
   for (;;) {
+    CTRL_T(ta);
     double delta[6];
     const bool valid = solve_step(s, delta);
+    CTRL_T(tb);
     double d[6];
 #pragma unroll
     for (int k = 0; k < 6; ++k) d[k] = lane == 1 ? -s.g[k] : (valid ? delta[k] : 0.0);
     double out[7];
     se3_plus(s.x, d, out);
+    CTRL_T(tc);
+    CTRL_ADD(2, tb - ta);
+    CTRL_ADD(3, tc - tb);
     if (check_gmax) {
       double m = 0.0;
 #pragma unroll
@@ -511,6 +534,8 @@ __device__ __forceinline__ void next_step_wave(LMState& s, bool check_gmax, int 
 #pragma unroll
       for (int i = 0; i < 7; ++i) s.cand[i] = bcast(out[i], 0);
       s.invalid = 0;
+      CTRL_T(td);
+      CTRL_ADD(4, td - tc);
       return;   // candidate pending evaluation
     }
     // HandleInvalidStep -> StepIsInvalid -> StepRejected(0)
@@ -532,6 +557,7 @@ __device__ __forceinline__ double norm7(const double (&a)[7]) {
 // One Ceres control step after an evaluation (sums = cost, J^T J, J^T r, count at x in phase 0, else at cand).
 // Called by all 64 lanes of one wave with identical s and sums; every lane ends with the same s.
 __device__ __forceinline__ void lm_logic(LMState& s, const double (&sums)[LM_NSUM], int lane) {
+  CTRL_T(t0);
   if (s.phase == 0) {   // IterationZero
     s.n_res = (int)sums[28];
     s.x_cost = sums[0];
@@ -587,7 +613,12 @@ __device__ __forceinline__ void lm_logic(LMState& s, const double (&sums)[LM_NSU
     s.reuse = 1;
   }
   if (s.iteration >= 4 || s.radius < 1e-32) { s.done = 1; return; }
+  CTRL_T(t1);
+  CTRL_ADD(1, t1 - t0);
   next_step_wave(s, success, lane);
+  CTRL_T(t2);
+  CTRL_ADD(5, t2 - t0);
+  CTRL_ADD(0, 1ull);
 }
 
 // the LM state without the trace fields (the register-resident copy of the control wave writes these back; the
@@ -1118,6 +1149,18 @@ LMArgs make_args(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, c
   return a;
 }
 }  // namespace
+
+void lm_ctrl_stamps_print() {
+#ifdef FLOAM_CTRL_STAMPS
+  unsigned long long h[8];
+  FLOAM_HIP(hipDeviceSynchronize());
+  FLOAM_HIP(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_ctrl_stamps), sizeof(h)));
+  const double n = h[0] ? (double)h[0] : 1.0;
+  std::fprintf(stderr, "[floam ctrl] %llu phase-1 control steps (block 0): bookkeeping %.3f us, solve_step %.3f us, "
+               "se3_plus %.3f us, gradient test + broadcast %.3f us; whole step %.3f us\n", h[0], h[1] / n / 100.0,
+               h[2] / n / 100.0, h[3] / n / 100.0, h[4] / n / 100.0, h[5] / n / 100.0);
+#endif
+}
 
 void LMBuffers::reserve(hipStream_t st) {
   if (part.p) return;

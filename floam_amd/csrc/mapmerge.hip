@@ -29,6 +29,7 @@
 #include "grid.hpp"
 #include "lookback.hpp"
 #include "mapmerge.hpp"
+#include "profwb.hpp"
 #include "radix.hpp"
 
 namespace floam {
@@ -268,13 +269,16 @@ __device__ __forceinline__ PointRec centroid_rec(float4 c) {   // VoxelGrid's ou
 template <int PER>
 __global__ __launch_bounds__(kTB) void mm_merge(VoxelJobDev A, VoxelJobDev B, MapKeys KA, MapKeys KB,
                                                 const uint32_t* __restrict__ skeys, const int* __restrict__ svals,
-                                                const int* __restrict__ ctl, unsigned long long* __restrict__ mstatus,
+                                                int* __restrict__ ctl, unsigned long long* __restrict__ mstatus,
                                                 int tiles_cap, int tilesA,
                                                 const unsigned* __restrict__ radix_ctl, const int* __restrict__ gate,
                                                 unsigned seq, int violate_mod, GridCountDev GA, GridCountDev GB,
-                                                int count_grid) {
+                                                int count_grid, int by_index) {
   const int job = (int)blockIdx.x < tilesA ? 0 : 1;
-  const int tile = job ? (int)blockIdx.x - tilesA : (int)blockIdx.x;
+  // the tile within the job is the block's ticket (ctl[18 + job], zeroed by the status gather): a tile's lookback
+  // only waits on tiles that are already running (HIP promises no dispatch order)
+  __shared__ int s_tile;
+  if (threadIdx.x == 0) s_tile = by_index ? (job ? (int)blockIdx.x - tilesA : (int)blockIdx.x) : atomicAdd(&ctl[18 + job], 1);
   const int njb = job ? (int)gridDim.x - tilesA : tilesA;   // this job's blocks
   MergeView V;
   V.J = job ? B : A;
@@ -282,8 +286,11 @@ __global__ __launch_bounds__(kTB) void mm_merge(VoxelJobDev A, VoxelJobDev B, Ma
   V.n0 = min(*V.J.d_n0, V.J.n0_ub);
   V.n1 = min(*V.J.d_n1, V.J.n1_ub);
   const int t = threadIdx.x;
+  __syncthreads();
+  const int tile = s_tile;
   const GridCountDev& G = job ? GB : GA;
-  if (gate && !*gate) {   // no keyframe: the map, its keys and their verdict stay as they are
+  if (gate && !*gate) {   // no keyframe: the map, its keys and their verdict stay as they are (no lookback: by index)
+    const int tile = job ? (int)blockIdx.x - tilesA : (int)blockIdx.x;
     for (int i0 = tile * kTB; i0 < V.n0; i0 += njb * kTB) {   // (wave-uniform trip count: the grid count)
       const int i = i0 + t;
       const bool valid = i < V.n0;
@@ -618,7 +625,7 @@ __global__ __launch_bounds__(kTB) void mm_merge(VoxelJobDev A, VoxelJobDev B, Ma
   // the next kNN grid's per-point step (grid_count_job) for the map's points pre.a + k, all rounds at once
   if (count_grid) grid_count_points<PER>(G, gi, gv, gx, gy, gz);
   if (tile == ntiles - 1 && t == 0) {
-    const bool sort_failed = radix_ctl[kRadixHistWords + 4] != 0u;   // a sort lookback timed out (never expected)
+    const bool sort_failed = radix_ctl[kRadixErrorWord] != 0u;   // a sort lookback timed out (never expected)
     *V.J.d_out = sort_failed ? -1 : pre.a + nloc;
     V.K.meta_out->valid = 1;
     V.K.meta_out->seq = seq;
@@ -684,15 +691,20 @@ void map_merge_launch(VoxelScratch2& vs, MapMergeScratch& ms, const VoxelJob& a,
     radix_sort_launch(vs.rs, vs.s.k0.p, vs.s.v0.p, vs.s.k1.p, vs.s.v1.p, n, st, gate, vs.overflow.p + 2);
     if (bucket) bucket_seed_launch(ms.bs, vs.s.k0.p, vs.overflow.p + 2, n, st, gate);
   }
+  const bool wb = prof_wb_enabled();   // (diagnostic: the merge's own write bytes, profwb.hpp)
+  if (wb) prof_l2_writeback(st);
   if (per == 2)
     hipLaunchKernelGGL(mm_merge<2>, dim3(tilesA + tilesB), dim3(kTB), 0, st, A, B, ka, kb, vs.s.k0.p, vs.s.v0.p,
                        ms.ctl.p, ms.status.p, ms.tiles_cap, tilesA, vs.rs.ctl.p, gate, seq, violate_mod,
-                       grids ? grids[0] : GridCountDev{}, grids ? grids[1] : GridCountDev{}, grids ? 1 : 0);
+                       grids ? grids[0] : GridCountDev{}, grids ? grids[1] : GridCountDev{}, grids ? 1 : 0,
+                       tile_by_index() ? 1 : 0);
   else
     hipLaunchKernelGGL(mm_merge<4>, dim3(tilesA + tilesB), dim3(kTB), 0, st, A, B, ka, kb, vs.s.k0.p, vs.s.v0.p,
                        ms.ctl.p, ms.status.p, ms.tiles_cap, tilesA, vs.rs.ctl.p, gate, seq, violate_mod,
-                       grids ? grids[0] : GridCountDev{}, grids ? grids[1] : GridCountDev{}, grids ? 1 : 0);
+                       grids ? grids[0] : GridCountDev{}, grids ? grids[1] : GridCountDev{}, grids ? 1 : 0,
+                       tile_by_index() ? 1 : 0);
   FLOAM_LAUNCH_CHECK();
+  if (wb) prof_l2_writeback(st);
 }
 
 }  // namespace floam

@@ -696,10 +696,17 @@ __device__ __forceinline__ void knn_block_corner(int nb, float wx, float wy, flo
   }
 }
 
-template <int G, int U, int NB>
+template <bool EDGE, typename R>
+__device__ __forceinline__ bool geom_fit(const R (&P)[5][3], float4 pq, double* __restrict__ rec, int cap, int i,
+                                         double* __restrict__ w, const double* o);
+
+// FUSED (FLOAM_KNN_FUSED_PROTO=1, a measurement prototype): lane 0 of the group also runs the
+// query's line / plane fit and writes its record (the geometry launch still runs after it — the prototype prices
+// the fits inside the search, a lower bound of a fused kernel, which would also need the surf Gram reduction)
+template <int G, int U, int NB, bool FUSED = false>
 __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArgs& A, int gid, int ngroups,
                                           int lane, bool gate, int rank, int world, int* __restrict__ s_pre,
-                                          int* __restrict__ s_start, int* __restrict__ s_cc) {
+                                          int* __restrict__ s_start, int* __restrict__ s_cc, bool edge = true) {
   const int n = min(*A.d_n, A.n_ub);
   const int lo = (int)(((long long)n * rank) / world), hi = (int)(((long long)n * (rank + 1)) / world);
   // grid-stride over the queries the device holds (the host only knows an upper bound)
@@ -764,6 +771,29 @@ __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArg
             A.nnsqd[lane * A.cap + i] = __uint_as_float((unsigned)(kk >> 32));
           }
         }
+        if (FUSED) {   // (prototype) the 5 neighbours' coordinates to every lane of the group, the fit on lane 0
+          float mx = 0.f, my = 0.f, mz = 0.f;
+          if (lane < 5) {
+            unsigned long long kk = t.k[0];
+#pragma unroll
+            for (int k = 1; k < 5; ++k)
+              if (lane == k) kk = t.k[k];
+            const float4 m = A.map[(int)(kk & 0xFFFFFFFFull)];
+            mx = m.x; my = m.y; mz = m.z;
+          }
+          double P[5][3];
+#pragma unroll
+          for (int j = 0; j < 5; ++j) {
+            P[j][0] = __shfl(mx, j, G);
+            P[j][1] = __shfl(my, j, G);
+            P[j][2] = __shfl(mz, j, G);
+          }
+          if (lane == 0) {
+            const float4 pq = *reinterpret_cast<const float4*>(&A.q[i].x);
+            if (edge) geom_fit<true, double>(P, pq, A.rec, A.cap, i, nullptr, nullptr);
+            else geom_fit<false, double>(P, pq, A.rec, A.cap, i, nullptr, nullptr);
+          }
+        }
       }
     }
     if (lane == 0) A.valid[i] = (uint8_t)flags;
@@ -773,7 +803,7 @@ __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArg
 // Edge and surf kNN in one launch: blocks [0, nbE) run edge groups, the others surf groups.  The launch also starts
 // the solve (lm_init folded in): block 0 resets the LM state and, for the first solve of an update, stores the
 // prediction x0 that every block uses for its transforms (the others never read st->x in that case).
-template <int G, int U, int W, int NB>
+template <int G, int U, int W, int NB, bool FUSED = false>
 __global__ __launch_bounds__(kTB, W) void knn_kernel(LMState* __restrict__ st, const double* __restrict__ x0_dev,
                                                   CorrArgs E, CorrArgs S, int nbE,
                                                   const int* __restrict__ d_me, const int* __restrict__ d_ms,
@@ -808,8 +838,8 @@ __global__ __launch_bounds__(kTB, W) void knn_kernel(LMState* __restrict__ st, c
   const int nq = min(*A.d_n, A.n_ub);
   const int nact = min(nb, (int)(((long long)nq * G + kTB - 1) / kTB));
   if (p < nact) p = xcd_block(p, nact);
-  knn_group<G, U, NB>(pose, A, (p * kTB + (int)threadIdx.x) / G, nb * (kTB / G), lane, gate, rank, world, s_pre[g],
-                  s_start[g], s_cc[g]);
+  knn_group<G, U, NB, FUSED>(pose, A, (p * kTB + (int)threadIdx.x) / G, nb * (kTB / G), lane, gate, rank, world,
+                             s_pre[g], s_start[g], s_cc[g], edge);
 }
 
 // Pass 2: line / plane geometry, one query per lane (all 64 lanes busy), in R = double (the reference's precision)
@@ -819,22 +849,14 @@ __global__ __launch_bounds__(kTB, W) void knn_kernel(LMState* __restrict__ st, c
 // (see lm.hip surf_sums_from_gram), so the surf half of each squared-loss LM evaluation needs only sum(w w^T).
 // EDGE with w != null: the record's 9 values are also returned in w (the iteration-zero edge sums).  Returns whether
 // the query produced a record.
+// the line / plane fit of query i from its 5 neighbours P and its sensor-frame point pq: the record at rec[. * cap + i]
+// (and w, below); returns whether the fit produced a record
 template <bool EDGE, typename R>
-__device__ __forceinline__ bool geom_query(LMState* __restrict__ st, const CorrArgs& A, int i,
-                                           double* __restrict__ w = nullptr, const double* o = nullptr) {
-  const int n = min(*A.d_n, A.n_ub);
+__device__ __forceinline__ bool geom_fit(const R (&P)[5][3], float4 pq, double* __restrict__ rec, int cap, int i,
+                                         double* __restrict__ w, const double* o) {
   bool ok = false;
-  const int flags = i < n ? A.valid[i] : 0;
-  if (flags & 1) {
-    R P[5][3];
-#pragma unroll
-    for (int j = 0; j < 5; ++j)
-#pragma unroll
-      for (int a = 0; a < 3; ++a) P[j][a] = A.nnxyz[(3 * j + a) * A.cap + i];
-    const float4 pq = *reinterpret_cast<const float4*>(&A.q[i].x);
+  {
     const double cpx = pq.x, cpy = pq.y, cpz = pq.z;
-    double* rec = A.rec;
-    const int cap = A.cap;
     if (EDGE) {
       // addEdgeCostFactor geometry (odomEstimationClass.cpp:156-189)
       R cc[3] = {R(0), R(0), R(0)};
@@ -900,6 +922,24 @@ __device__ __forceinline__ bool geom_query(LMState* __restrict__ st, const CorrA
         }
       }
     }
+  }
+  return ok;
+}
+
+template <bool EDGE, typename R>
+__device__ __forceinline__ bool geom_query(LMState* __restrict__ st, const CorrArgs& A, int i,
+                                           double* __restrict__ w = nullptr, const double* o = nullptr) {
+  const int n = min(*A.d_n, A.n_ub);
+  bool ok = false;
+  const int flags = i < n ? A.valid[i] : 0;
+  if (flags & 1) {
+    R P[5][3];
+#pragma unroll
+    for (int j = 0; j < 5; ++j)
+#pragma unroll
+      for (int a = 0; a < 3; ++a) P[j][a] = A.nnxyz[(3 * j + a) * A.cap + i];
+    const float4 pq = *reinterpret_cast<const float4*>(&A.q[i].x);
+    ok = geom_fit<EDGE, R>(P, pq, A.rec, A.cap, i, w, o);
     A.valid[i] = (uint8_t)((flags & 2) | (ok ? 1 : 0) | 4);   // bit 2: the search found 5 neighbours
   }
   const unsigned long long b = __ballot(ok);
@@ -1407,7 +1447,19 @@ void knn_launch(LMState* d_st, const double* x0_dev, const QuerySet& qe, const G
   const int nS = qs.grid_hint > 0 ? std::min(qs.grid_hint, qs.n_ub) : qs.n_ub;
   const unsigned nbE = std::min(div_up((size_t)std::max(nE, 1) * G, kTB), 4096u);
   const unsigned nbS = std::min(div_up((size_t)std::max(nS, 1) * G, kTB), 8192u);
-  if (knn_block() == 2)
+  // FLOAM_KNN_FUSED_PROTO=1|2 (measurement prototype: the fits inside the search at 6 | 4 waves per SIMD; the
+  // geometry launch still follows)
+  static const int fused_proto = [] {
+    const char* e = std::getenv("FLOAM_KNN_FUSED_PROTO");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (fused_proto == 1)
+    hipLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6, 3, true>), dim3(nbE + nbS), dim3(kTB), 0, st, d_st, x0_dev,
+                       E, S, (int)nbE, d_me, d_ms, rank, world);
+  else if (fused_proto == 2)
+    hipLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 4, 3, true>), dim3(nbE + nbS), dim3(kTB), 0, st, d_st, x0_dev,
+                       E, S, (int)nbE, d_me, d_ms, rank, world);
+  else if (knn_block() == 2)
     hipLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6, 2>), dim3(nbE + nbS), dim3(kTB), 0, st, d_st, x0_dev, E, S,
                        (int)nbE, d_me, d_ms, rank, world);
   else

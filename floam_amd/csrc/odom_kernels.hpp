@@ -316,6 +316,8 @@ void lm_shard_final_launch(LMState* d_st, LMBuffers& b, hipStream_t st);
 // occupancy of the instance `mode` selects times the device's CU count covers its grid.  Otherwise the caller runs
 // the per-evaluation path (lm_shard_eval + lm_shard_final on one rank, no spin between blocks).
 bool lm_solve_coresident(int mode, int device);
+// -DFLOAM_CTRL_STAMPS builds: block 0's control-step segments to stderr (no-op otherwise)
+void lm_ctrl_stamps_print();
 // Stage inspection: append this solve's trace record (49 doubles, oracle/odom.cpp SolveTrace order) to trace[] at
 // *count when the map-size gate (:77) let the solve run and *count < cap.
 constexpr int kTraceWords = 49;

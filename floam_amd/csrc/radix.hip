@@ -1,7 +1,9 @@
 // Stable LSD radix sort, one single-pass launch per 8-bit digit (see radix.hpp).
 //
-// A launch sorts by one digit.  Each block is a tile (256 threads x kItems consecutive elements, tile = block index;
-// blocks are dispatched in index order, so a tile only ever waits on tiles that were already running) and
+// A launch sorts by one digit.  Each block is a tile (256 threads x kItems consecutive elements; tile = the block's
+// ticket, the order blocks start in, so a tile only ever waits on tiles that are already running: HIP promises no
+// dispatch order, and a tile taken by block index can wait on a block that never gets a CU — MI355X_MICROARCH.md
+// "Workgroup dispatch"; observed with two processes' kernels on one GPU) and
 //   1. loads its elements: wave w owns the 64 * kItems elements [w * 64 * kItems, ...), lane l element r * 64 + l in
 //      round r, so (round, lane) order is input order;
 //   2. ranks them stably: per round, the lanes holding the same digit find each other with 8 ballots, each takes
@@ -54,17 +56,21 @@ __global__ __launch_bounds__(kTB) void radix_pass(const uint32_t* __restrict__ k
                                                   const int* __restrict__ gate, const int* __restrict__ n_dev,
                                                   int stamps, const PointRec* __restrict__ pin,
                                                   float4* __restrict__ pxyz, PointRec* __restrict__ prec,
-                                                  const uint8_t* __restrict__ digs) {
+                                                  const uint8_t* __restrict__ digs, int by_index) {
   const unsigned long long ts0 = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
   // every load of the prologue is issued at once (one memory round trip, not three in a row): the gate, the epoch,
   // the device count, this digit's histogram count and the tile's elements up to the host bound n (allocated; the
   // ones past the device count are dropped below)
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int tile = (int)blockIdx.x;
+  // the ticket (zeroed per sort with the histograms) with the tile-independent loads in flight beside it
+  __shared__ int s_tile;
+  if (t == 0) s_tile = by_index ? (int)blockIdx.x : (int)atomicAdd(&ctl[kRadixTicketWord + pass], 1u);
   const int gv = gate ? *gate : 1;
   const unsigned epoch = ctl[kRadixEpochWord];
   const int nd = n_dev ? *n_dev : n;
   const unsigned h = ctl[pass * kRadixDigits + t];   // digit t's histogram count
+  __syncthreads();
+  const int tile = s_tile;
   const int base = tile * kTile + w * 64 * kItems;
   uint32_t key[kItems];
   int val[kItems];
@@ -86,8 +92,6 @@ __global__ __launch_bounds__(kTB) void radix_pass(const uint32_t* __restrict__ k
   }
   if (!gv) return;
   n = min(n, nd);
-  // the tile is the block index: workgroups are dispatched in index order and a launch has at most a few hundred
-  // tiles, so a tile only waits on tiles that are running or done (no ticket round trip)
   if (tile * kTile >= n) return;   // beyond the elements (block-uniform); nobody waits on a later tile
   __shared__ unsigned s_wcnt[kTB / 64][kRadixDigits];
   __shared__ unsigned s_off[kRadixDigits];
@@ -175,7 +179,7 @@ __global__ __launch_bounds__(kTB) void radix_pass(const uint32_t* __restrict__ k
         __builtin_amdgcn_s_sleep(1);
       }
     }
-    if (failed) atomicOr(&ctl[kRadixHistWords + 4], 1u);
+    if (failed) atomicOr(&ctl[kRadixErrorWord], 1u);
     __hip_atomic_store(&st[(size_t)tile * kRadixDigits + t], lb_word(epoch, kFlagInc, prefix + cnt), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -264,6 +268,14 @@ static int stamps_on() {
   return on ? (int)(launches++ % (unsigned)kStampSlots) + 1 : 0;   // per launch: its slot + 1
 }
 
+bool tile_by_index() {
+  static const bool on = [] {
+    const char* e = std::getenv("FLOAM_TILE_BY_INDEX");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 void radix_stamps_print() {
   if (!std::getenv("FLOAM_RADIX_STAMPS")) return;
   static unsigned long long h[8 + 2 * kStampSlots];
@@ -305,7 +317,7 @@ void radix_pass_launch(RadixScratch& sc, const uint32_t* kin, const int* vin, ui
   const int tiles = (int)div_up((unsigned)n, (unsigned)kTile);
   hipLaunchKernelGGL(radix_pass<false>, dim3(tiles), dim3(kTB), 0, st, kin, vin, kout, vout, n, pass, sc.ctl.p,
                      sc.status.p + (size_t)pass * sc.tiles_cap * kRadixDigits, nullptr, nullptr, stamps_on(), nullptr,
-                     nullptr, nullptr, nullptr);
+                     nullptr, nullptr, nullptr, tile_by_index());
   FLOAM_LAUNCH_CHECK();
 }
 
@@ -315,7 +327,7 @@ void radix_pass_payload_launch(RadixScratch& sc, const uint32_t* kin, uint32_t* 
   sc.reserve(n, st);
   const int tiles = (int)div_up((unsigned)n, (unsigned)kTile);
   hipLaunchKernelGGL(radix_pass<true>, dim3(tiles), dim3(kTB), 0, st, kin, nullptr, kout, vout, n, 0, sc.ctl.p,
-                     sc.status.p, nullptr, nullptr, stamps_on(), pin, pxyz, prec, nullptr);
+                     sc.status.p, nullptr, nullptr, stamps_on(), pin, pxyz, prec, nullptr, tile_by_index());
   FLOAM_LAUNCH_CHECK();
 }
 
@@ -329,7 +341,7 @@ void radix_sort_launch(RadixScratch& sc, uint32_t* k0, int* v0, uint32_t* k1, in
     hipLaunchKernelGGL(radix_pass<false>, dim3(tiles), dim3(kTB), 0, st, even ? k0 : k1, even ? v0 : v1,
                        even ? k1 : k0, even ? v1 : v0, n, p, sc.ctl.p,
                        sc.status.p + (size_t)p * sc.tiles_cap * kRadixDigits, gate, n_dev, stamps_on(), nullptr,
-                       nullptr, nullptr, nullptr);
+                       nullptr, nullptr, nullptr, tile_by_index());
     FLOAM_LAUNCH_CHECK();
   }
 }
@@ -340,7 +352,7 @@ void radix_digit_pass_launch(RadixScratch& sc, const uint32_t* kin, const int* v
   sc.reserve(n, st);
   const int tiles = (int)div_up((unsigned)n, (unsigned)kTile);
   hipLaunchKernelGGL(radix_pass<false>, dim3(tiles), dim3(kTB), 0, st, kin, vin, kout, vout, n, 0, sc.ctl.p,
-                     sc.status.p, gate, n_dev, stamps_on(), nullptr, nullptr, nullptr, digs);
+                     sc.status.p, gate, n_dev, stamps_on(), nullptr, nullptr, nullptr, digs, tile_by_index());
   FLOAM_LAUNCH_CHECK();
 }
 

@@ -9,6 +9,8 @@ namespace floam {
 constexpr int kRadixDigits = 256;
 constexpr int kRadixPasses = 4;
 constexpr int kRadixHistWords = kRadixPasses * kRadixDigits;   // followed by 4 tile tickets + 1 error word
+constexpr int kRadixTicketWord = kRadixHistWords;               // [pass]: the pass's tile tickets
+constexpr int kRadixErrorWord = kRadixHistWords + 4;            // != 0: a lookback timed out
 constexpr int kRadixZeroWords = kRadixHistWords + 5;            // zeroed per sort
 constexpr int kRadixEpochWord = kRadixHistWords + 5;            // sort counter (tags the lookback words)
 constexpr int kRadixCtlWords = kRadixHistWords + 8;
@@ -69,6 +71,10 @@ void radix_pass_payload_launch(RadixScratch& sc, const uint32_t* kin, uint32_t* 
 
 // FLOAM_RADIX_STAMPS=1: print the passes' in-kernel phase times (diagnostic; synchronises the device)
 void radix_stamps_print();
+
+// FLOAM_TILE_BY_INDEX=1 (A/B only): the decoupled lookbacks (radix passes, vox_compact, bucket_compact, mm_merge)
+// take their tile from the block index instead of a ticket — the dispatch-order assumption HIP does not promise
+bool tile_by_index();
 
 void radix_pass_launch(RadixScratch& sc, const uint32_t* kin, const int* vin, uint32_t* kout, int* vout, int n,
                        int pass, hipStream_t st);

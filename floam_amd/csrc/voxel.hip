@@ -132,17 +132,22 @@ __global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B,
                                                    const int* __restrict__ vals, const int* __restrict__ overflow,
                                                    const int* __restrict__ n_dev, unsigned long long* __restrict__ status,
                                                    unsigned* __restrict__ ticket, const unsigned* __restrict__ radix_ctl,
-                                                   const int* __restrict__ gate, int n_cap, int stamps) {
+                                                   const int* __restrict__ gate, int n_cap, int stamps, int by_index) {
   const unsigned long long T0 = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
   // the prologue's loads are issued together (one round trip instead of four in a row): the gate, the device
   // counts, and the tile's keys and values up to the host bound n_cap (allocated; entries past the device count are
   // masked below)
+  // the tile is the block's ticket (zeroed by vox_keys): a tile only waits on tiles that are already running (HIP
+  // promises no dispatch order); the tile-independent loads in flight beside the ticket
+  __shared__ int s_tile;
+  if (threadIdx.x == 0) s_tile = by_index ? (int)blockIdx.x : (int)atomicAdd(ticket, 1u);
   const int gv = gate ? *gate : 1;
-  const int tile = (int)blockIdx.x;   // (workgroups dispatch in index order: a tile only waits on earlier tiles)
-  const int t0 = tile * kTile;
   const int total_d = *n_dev;   // packed elements (vox_keys)
   const int nA0 = *A.d_n0, nA1 = A.d_n1 ? *A.d_n1 : 0, nB0 = *B.d_n0, nB1 = B.d_n1 ? *B.d_n1 : 0;
   const int ovf[2] = {overflow[0], overflow[1]};
+  __syncthreads();
+  const int tile = s_tile;
+  const int t0 = tile * kTile;
   // s_key[k] = key of element t0 - 1 + k, k in [0, kTile + 1 + kHalo]: the rounds of the prologue's key loads
   // also cover kHalo elements past the tile (the continuation of a run that crosses the tile end, usually short)
   constexpr int kRounds = (kTile + 2 + kTB - 1) / kTB;
@@ -401,7 +406,7 @@ __global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B,
     }
   }
   if (tile == ntiles - 1 && threadIdx.x == 0) {
-    const bool sort_failed = radix_ctl[kRadixHistWords + 4] != 0u;   // a sort lookback timed out (never expected)
+    const bool sort_failed = radix_ctl[kRadixErrorWord] != 0u;   // a sort lookback timed out (never expected)
     *A.d_out = sort_failed ? -1 : pre.a + agg[0];
     *B.d_out = sort_failed ? -1 : pre.b + agg[1];
   }
@@ -502,14 +507,14 @@ void voxel2_launch(VoxelScratch2& sc, const VoxelJob& a, const VoxelJob& b, hipS
   FLOAM_LAUNCH_CHECK();
   if (use_bucket) {   // scatter by bucket, and one block per bucket that sorts it and emits its voxels
     bucket_voxel_launch(sc.bs, sc.rs, A, B, sc.s.k0.p, sc.s.v0.p, sc.s.k1.p, sc.s.v1.p, n, sc.overflow.p,
-                        sc.status.p, st, gate, sc.overflow.p + 2);
+                        sc.status.p, sc.ticket.p, st, gate, sc.overflow.p + 2);
     return;
   }
   // sorted pairs in k0 / v0; the passes and the compaction work on the packed device count
   radix_sort_launch(sc.rs, sc.s.k0.p, sc.s.v0.p, sc.s.k1.p, sc.s.v1.p, n, st, gate, sc.overflow.p + 2);
   if (bucket) bucket_seed_launch(sc.bs, sc.s.k0.p, sc.overflow.p + 2, n, st, gate);
   hipLaunchKernelGGL(vox_compact, dim3(ntiles), dim3(kTB), 0, st, A, B, sc.s.k0.p, sc.s.v0.p, sc.overflow.p,
-                     sc.overflow.p + 2, sc.status.p, sc.ticket.p, sc.rs.ctl.p, gate, n, vox_stamps_on());
+                     sc.overflow.p + 2, sc.status.p, sc.ticket.p, sc.rs.ctl.p, gate, n, vox_stamps_on(), tile_by_index());
   FLOAM_LAUNCH_CHECK();
 }
 

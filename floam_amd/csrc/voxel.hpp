@@ -168,7 +168,7 @@ struct MergeCheck {
 };
 // [0, 1] kept set elements of job A / B, [2, 3] mode (1 full), [4, 5] overflow, [6 + 6j .. 11 + 6j] job j's min_b[3],
 // div_b[3]
-constexpr int kMergeCtlWords = 18;
+constexpr int kMergeCtlWords = 20;   // ... [18 + job] mm_merge's tile tickets
 
 // bounding box of one cloud (as vox_minmax_block) + the MergeCheck test of its scan points
 __device__ __forceinline__ void mm_minmax_block(const VoxelJobDev& J, int job, int b, int nblocks,
@@ -238,10 +238,11 @@ void vox_stamps_print();
 
 // The sort + compaction half of the pipeline with the bucket sort (bucket.hip): plan, bucket scatter, and one block
 // per bucket that sorts it and emits its voxels (output slots by lookback over the 256 buckets: status must hold >= 256
-// zeroed words).  k0 / v0 hold the keys from vox_keys (with the bucket histogram); the outputs land in A.out / B.out.
+// zeroed words, ticket a zeroed counter: vox_keys zeroes both).  k0 / v0 hold the keys from vox_keys (with the
+// bucket histogram); the outputs land in A.out / B.out.
 void bucket_voxel_launch(BucketScratch& bs, RadixScratch& rs, const VoxelJobDev& A, const VoxelJobDev& B, uint32_t* k0,
                          int* v0, uint32_t* k1, int* v1, int n, const int* overflow, unsigned long long* status,
-                         hipStream_t st, const int* gate, const int* n_dev);
+                         unsigned* ticket, hipStream_t st, const int* gate, const int* n_dev);
 
 void voxel2_launch(VoxelScratch2& sc, const VoxelJob& a, const VoxelJob& b, hipStream_t st,
                    const int* gate = nullptr, bool minmax_done = false);

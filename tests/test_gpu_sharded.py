@@ -187,11 +187,17 @@ def test_rccl_world1_matches_unsharded(floam_gpu, loss, fp32):
     """The sharded solve (one launch + one ncclAllReduce of the 29 sums per LM evaluation, the control step folded
     into the next launch) on a one-rank RCCL communicator: the same partition and fixed-order reductions as the
     resident single-GPU solve.  lm.hip is compiled with FMA contraction, which the compiler may apply differently
-    in the two kernels, so the poses agree to the last few ulps (observed <= 1e-15 m) rather than bit for bit;
-    the LM decisions (iteration counts) are identical."""
+    in the two kernels, so the fp64 poses agree to the last few ulps (observed <= 1e-15 m) rather than bit for bit,
+    with identical LM decisions; fp32 residuals: see below."""
     ref = _run(0, 1, _free_port(), None, loss=loss, fp32=fp32)
     got = _run(0, 1, _free_port(), None, rccl_world1=True, loss=loss, fp32=fp32)
-    np.testing.assert_allclose(got, ref, rtol=1e-12, atol=1e-14)
+    if fp32:
+        # float residuals: a contraction difference between the two kernels moves the float sums by ~1e-7 relative,
+        # which can flip a borderline tolerance test (|x_cost - cand_cost| <= 1e-6 x_cost) and end a solve one
+        # iteration apart (observed 1.9e-5 in r04e); the fp32 variant's bar against the oracle is 5e-3 m (test_gpu_parity)
+        np.testing.assert_allclose(got, ref, rtol=0, atol=1e-4)
+    else:
+        np.testing.assert_allclose(got, ref, rtol=1e-12, atol=1e-14)
 
 
 def _run_peer(rank, world, port, q, config, nscan, maps=None):
