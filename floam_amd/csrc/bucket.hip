@@ -412,7 +412,11 @@ __device__ __forceinline__ void chunk_heads(const uint32_t* k, int nc, uint32_t 
   thread_range(nc, e0, e1);
   for (int e = e0; e < e1; ++e) {
     const uint32_t kp = e ? k[e - 1] : prev;
-    if ((e == 0 && first) || k[e] != kp) ++c[k[e] >> 31];
+    if ((e == 0 && first) || k[e] != kp) {   // (no dynamic index into c: it would be private memory)
+      const int j = (int)(k[e] >> 31);
+      c[0] += 1 - j;
+      c[1] += j;
+    }
   }
 }
 
@@ -501,7 +505,11 @@ __global__ __launch_bounds__(kTB) void bucket_compact(VoxelJobDev A, VoxelJobDev
     hc[0] = hc[1] = 0;
     for (int e = t; e < size; e += kTB) {
       const uint32_t k = kout[start + e];
-      if (e == 0 || k != kout[start + e - 1]) ++hc[k >> 31];
+      if (e == 0 || k != kout[start + e - 1]) {
+        const int j = (int)(k >> 31);
+        hc[0] += 1 - j;
+        hc[1] += j;
+      }
     }
   }
   block_sum2(hc, L.hw);

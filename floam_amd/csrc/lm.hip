@@ -293,6 +293,10 @@ __device__ __forceinline__ void gram_unpack(double gv, double (*G)[kGramW], doub
 // control step is one wave's serial fp64 instruction stream).  Larger |x| (a huge step, or the gradient projection of
 // the iteration-zero test) takes the library's sincos.
 __device__ __forceinline__ void sincos_small(double x, double* s, double* c) {
+#ifdef FLOAM_LM_LIBSINCOS   // (A/B builds only: the library's sincos for every angle)
+  sincos(x, s, c);
+  return;
+#endif
   if (!(fabs(x) <= 0.78125)) {
     sincos(x, s, c);
     return;
@@ -507,15 +511,32 @@ __device__ __forceinline__ double bcast(double v, int src) {
 // NextStep with the gradient-norm test folded in: ComputeTrustRegionStep (+ HandleInvalidStep retries) and, when
 // check_gmax, the projected-gradient max norm at x (lane 1) computed alongside the candidate (lane 0).  If the
 // gradient test ends the solve the step is discarded, as in the sequential order (test first, then step).
+// The gradient test only asks whether max_i |x_i - (x [+] -g)_i| <= 1e-10.  A rotation of angle th moves the unit
+// quaternion by |dq - 1| = 2 |sin(th / 4)| in the 2-norm (the product with q preserves it), so some component by at
+// least |sin(th / 4)|: when th / 4 is more than 1e-6 from every multiple of pi (a two-constant reduction, exact far
+// beyond any gradient) the test fails without the projection.  Large gradients are the rule before convergence, and
+// their angle would send lane 1 through the library sincos's range reduction while lane 0 waits (one wave).
+__device__ __forceinline__ bool gradient_step_far(const double (&g)[6]) {
+  const double th = sqrt(g[0] * g[0] + g[1] * g[1] + g[2] * g[2]);
+  if (!(th > 1.5625 && th < 1e15)) return false;   // (small angles take sincos_small anyway)
+  const double u = 0.25 * th;
+  const double k = rint(u * 0.31830988618379067154);
+  double r = fma(-k, 3.141592653589793116, u);
+  r = fma(-k, 1.2246467991473532072e-16, r);
+  return fabs(r) > 1e-6 && fabs(r) < 3.1415916;
+}
+
 __device__ __forceinline__ void next_step_wave(LMState& s, bool check_gmax, int lane) {
   for (;;) {
     CTRL_T(ta);
     double delta[6];
     const bool valid = solve_step(s, delta);
     CTRL_T(tb);
+    // lane 1: the gradient projection x [+] -g, when the test is due and cannot be decided from the angle alone
+    const bool far = check_gmax && gradient_step_far(s.g);   // (wave-uniform: every lane holds the same g)
     double d[6];
 #pragma unroll
-    for (int k = 0; k < 6; ++k) d[k] = lane == 1 ? -s.g[k] : (valid ? delta[k] : 0.0);
+    for (int k = 0; k < 6; ++k) d[k] = lane == 1 ? (check_gmax && !far ? -s.g[k] : 0.0) : (valid ? delta[k] : 0.0);
     double out[7];
     se3_plus(s.x, d, out);
     CTRL_T(tc);
@@ -525,7 +546,7 @@ __device__ __forceinline__ void next_step_wave(LMState& s, bool check_gmax, int 
       double m = 0.0;
 #pragma unroll
       for (int i = 0; i < 7; ++i) m = fmax(m, fabs(s.x[i] - bcast(out[i], 1)));
-      s.gmax = m;
+      s.gmax = far ? HUGE_VAL : m;   // (only its comparison with the tolerance is used)
       check_gmax = false;
       if (s.gmax <= 1e-10) { s.done = 1; return; }   // (phase 0: before any step; phase 1: success && gmax)
     }
@@ -670,11 +691,12 @@ __device__ __forceinline__ void control_step(LMState& s, LMState& sst, const dou
   lm_logic(s, sm, lane);
 }
 
-// the control step on the LDS copy (wave 0): the state is loaded into registers for the step and written back by
-// lane 0, so nothing of it stays live across the evaluations (whose registers it would otherwise share: the
-// register-resident form spilled it to AGPRs and back around every step); then the next point and the done flag
+// FLOAM_LM_STATE_REGS=0 (A/B builds): the control step on the LDS copy (wave 0) — the state loaded into registers
+// for the step and written back by lane 0, so nothing of it stays live across the evaluations; measured 1.3 % faster
+// before the peer exchange joined the kernel (r04c), after it the compiler spills 12-36 B/lane to scratch in that
+// form and none in the register-resident one (the default)
 #ifndef FLOAM_LM_STATE_REGS
-#define FLOAM_LM_STATE_REGS 0
+#define FLOAM_LM_STATE_REGS 1
 #endif
 __device__ __forceinline__ double point_component(const LMState& s, int k);
 __device__ __forceinline__ void control_step_lds(LMState& sst, const double* sums_lds, int lane, double* s_pt,
@@ -906,7 +928,16 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
   // bits); the surf half is formed from G below as in every evaluation
   __shared__ double s_esum[LM_NSUM];
   __shared__ unsigned s_xch[kMaxShardRanks * 2 * LM_NSUM];   // peer sharding: every rank's sums (u32 halves)
+#ifdef FLOAM_LM_NO_PRE0   // (A/B builds only: the pre0 paths compiled out)
+  constexpr bool pre0 = false;
+#else
   const bool pre0 = GRAM && !HUBER && a.epart != nullptr;
+#endif
+#ifdef FLOAM_LM_NO_PEER   // (A/B builds only: the peer exchange compiled out)
+  constexpr bool peers = false;
+#else
+  const bool peers = a.world > 1;
+#endif
   if (pre0) reduce_blocks([&](int c, int b) { return a.epart[b * LM_NSUM + c]; }, a.nbe, s_esum);
   const unsigned long long t_loop = __builtin_amdgcn_s_memrealtime();
   int failed_at = -1;   // evaluation whose granules never arrived (never expected)
@@ -922,7 +953,7 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
       }
       if (tid < LM_NSUM) s_sums[tid] = s_esum[tid] + s_ssum[tid];   // edge + surf
       __syncthreads();
-      if (a.world > 1 && !peer_exchange(a, it, ep + (unsigned)it, s_sums, s_xch)) {
+      if (peers && !peer_exchange(a, it, ep + (unsigned)it, s_sums, s_xch)) {
         failed_at = it;
         break;
       }
@@ -975,7 +1006,7 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
     }, nact, s_sums);
     if (GRAM && tid < LM_NSUM) s_sums[tid] = s_sums[tid] + s_ssum[tid];   // edge + surf
     __syncthreads();
-    if (a.world > 1 && !peer_exchange(a, it, tag, s_sums, s_xch)) {
+    if (peers && !peer_exchange(a, it, tag, s_sums, s_xch)) {
       failed_at = it;
       break;
     }

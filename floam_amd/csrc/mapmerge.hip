@@ -185,7 +185,16 @@ struct MergeView {   // one map of the update as mm_merge sees it
 };
 
 // the record of concatenation element i (kept: in the crop box)
-__device__ __forceinline__ bool mv_fetch(const MergeView& V, int i, PointRec& p) { return vox_fetch(V.J, V.n0, V.n1, i, p); }
+__device__ __forceinline__ bool mv_fetch4(const MergeView& V, int i, float4& q) { return vox_fetch4(V.J, V.n0, V.n1, i, q); }
+
+// ov[nout++] = v with nout in registers: every slot a compare-select (a dynamically indexed array is private memory)
+template <int PER>
+__device__ __forceinline__ void put_out(float4 (&ov)[PER], int& nout, float4 v) {
+#pragma unroll
+  for (int q = 0; q < PER; ++q)
+    if (q == nout) ov[q] = v;
+  ++nout;
+}
 
 // voxel index of sort-set element j (its sort key without the cloud bit)
 __device__ __forceinline__ unsigned long long set_idx(const MergeView& V, int j) {
@@ -258,49 +267,46 @@ __device__ __forceinline__ unsigned long long mv_idx(const MergeView& V, float x
   return (unsigned long long)i0 + (unsigned long long)i1 * V.dx + (unsigned long long)i2 * V.dx * V.dy;
 }
 
-__device__ __forceinline__ PointRec centroid_rec(float4 c) {   // VoxelGrid's output record of a centroid
-  PointRec o;
-  o.x = c.x; o.y = c.y; o.z = c.z; o.pad0 = 1.0f;
-  o.intensity = c.w;
-  o.ring = 0; o.pad1 = 0; o.time = 0.0f; o.pad2 = 0.0f;
-  return o;
-}
 
+// One job's tile (the kernel below calls it with the job's own kernel arguments: selecting the argument structs by a
+// run-time job index made the compiler copy both into scratch and load every field from there — 144-176 B / lane of
+// private memory traffic per launch)
 template <int PER>
-__global__ __launch_bounds__(kTB) void mm_merge(VoxelJobDev A, VoxelJobDev B, MapKeys KA, MapKeys KB,
-                                                const uint32_t* __restrict__ skeys, const int* __restrict__ svals,
-                                                int* __restrict__ ctl, unsigned long long* __restrict__ mstatus,
-                                                int tiles_cap, int tilesA,
-                                                const unsigned* __restrict__ radix_ctl, const int* __restrict__ gate,
-                                                unsigned seq, int violate_mod, GridCountDev GA, GridCountDev GB,
-                                                int count_grid, int by_index) {
-  const int job = (int)blockIdx.x < tilesA ? 0 : 1;
-  // the tile within the job is the block's ticket (ctl[18 + job], zeroed by the status gather): a tile's lookback
-  // only waits on tiles that are already running (HIP promises no dispatch order)
+__device__ __forceinline__ void mm_merge_job(const VoxelJobDev& JJ, const MapKeys& KK, const GridCountDev& G, int job,
+                                             const uint32_t* __restrict__ skeys, const int* __restrict__ svals,
+                                             int* __restrict__ ctl, unsigned long long* __restrict__ mstatus,
+                                             int tiles_cap, int tilesA,
+                                             const unsigned* __restrict__ radix_ctl, const int* __restrict__ gate,
+                                             unsigned seq, int violate_mod, int count_grid, int by_index) {
+  // the tile within the job is the block's ticket (ctl[kMergeTicketWord + 32 job], zeroed by the status gather): a
+  // tile's lookback only waits on tiles that are already running (HIP promises no dispatch order)
   __shared__ int s_tile;
-  if (threadIdx.x == 0) s_tile = by_index ? (job ? (int)blockIdx.x - tilesA : (int)blockIdx.x) : atomicAdd(&ctl[18 + job], 1);
+  if (threadIdx.x == 0)
+    s_tile = by_index ? (job ? (int)blockIdx.x - tilesA : (int)blockIdx.x) : atomicAdd(&ctl[kMergeTicketWord + 32 * job], 1);
   const int njb = job ? (int)gridDim.x - tilesA : tilesA;   // this job's blocks
   MergeView V;
-  V.J = job ? B : A;
-  V.K = job ? KB : KA;
+  V.J = JJ;
+  V.K = KK;
   V.n0 = min(*V.J.d_n0, V.J.n0_ub);
   V.n1 = min(*V.J.d_n1, V.J.n1_ub);
   const int t = threadIdx.x;
   __syncthreads();
   const int tile = s_tile;
-  const GridCountDev& G = job ? GB : GA;
   if (gate && !*gate) {   // no keyframe: the map, its keys and their verdict stay as they are (no lookback: by index)
     const int tile = job ? (int)blockIdx.x - tilesA : (int)blockIdx.x;
     for (int i0 = tile * kTB; i0 < V.n0; i0 += njb * kTB) {   // (wave-uniform trip count: the grid count)
       const int i = i0 + t;
       const bool valid = i < V.n0;
-      PointRec p;
+      float4 lo = make_float4(0.f, 0.f, 0.f, 0.f);
       if (valid) {
-        p = V.J.part0[i];
-        V.J.out[i] = p;
+        const float4* q = reinterpret_cast<const float4*>(V.J.part0 + i);
+        float4* o = reinterpret_cast<float4*>(V.J.out + i);
+        lo = q[0];
+        o[0] = lo;
+        o[1] = q[1];
         V.K.out[i] = V.K.in[i];
       }
-      if (count_grid) grid_count_point(G, i, valid, p.x, p.y, p.z);
+      if (count_grid) grid_count_point(G, i, valid, lo.x, lo.y, lo.z);
     }
     if (tile == 0 && t == 0) {
       *V.J.d_out = V.n0;
@@ -344,10 +350,10 @@ __global__ __launch_bounds__(kTB) void mm_merge(VoxelJobDev A, VoxelJobDev B, Ma
     for (int k = t; k < cnt; k += kTB) {
       const int pos = V.base + d0 + k;
       const int src = svals[pos];
-      PointRec p;
-      mv_fetch(V, src, p);
+      float4 q;
+      mv_fetch4(V, src, q);
       s_key[k + 1] = skeys[pos];
-      s_pt[k] = make_float4(p.x, p.y, p.z, p.intensity);
+      s_pt[k] = q;
       s_src[k] = src;
       s_live[k] = 1;
     }
@@ -379,20 +385,20 @@ __global__ __launch_bounds__(kTB) void mm_merge(VoxelJobDev A, VoxelJobDev B, Ma
       rl[r] = false;
       rp[r] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (k >= na + nb) continue;
-      PointRec p;
+      float4 q;
       if (k < na) {
         const int i = i0 + k;
-        rl[r] = mv_fetch(V, i, p);
+        rl[r] = mv_fetch4(V, i, q);
         rs[r] = i;
         s_ak[k] = map_idx(V, i);
       } else {
         const int j = j0 + k - na;
         rs[r] = svals[V.base + j];
         rl[r] = true;
-        mv_fetch(V, rs[r], p);
+        mv_fetch4(V, rs[r], q);
         s_bk[k - na] = set_idx(V, j);
       }
-      rp[r] = make_float4(p.x, p.y, p.z, p.intensity);
+      rp[r] = q;
     }
     if (t == 0) {   // the merged element before the tile: the later of map[i0 - 1] and set[j0 - 1]
       unsigned long long prev = kNone;
@@ -469,7 +475,7 @@ __global__ __launch_bounds__(kTB) void mm_merge(VoxelJobDev A, VoxelJobDev B, Ma
     while (e < cnt && s_key[e + 1] == key) ++e;
     const bool crosses = e == cnt && next_key == key;
     if (V.ovf) {   // index overflow: every point is returned unchanged (Q9; identity keys: runs of one)
-      ov[nout++] = make_float4(__int_as_float(s_src[k]), 0.f, 0.f, 0.f);
+      put_out(ov, nout, make_float4(__int_as_float(s_src[k]), 0.f, 0.f, 0.f));
       continue;
     }
     float c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f;
@@ -491,7 +497,7 @@ __global__ __launch_bounds__(kTB) void mm_merge(VoxelJobDev A, VoxelJobDev B, Ma
     }
     if (n == 0) continue;   // only cropped map points
     const float cn = (float)n;
-    ov[nout++] = make_float4(c0 / cn, c1 / cn, c2 / cn, c3 / cn);
+    put_out(ov, nout, make_float4(c0 / cn, c1 / cn, c2 / cn, c3 / cn));
     if (mv_idx(V, c0 / cn, c1 / cn, c2 / cn) != (key & 0x7FFFFFFFull)) bad = true;
   }
   __syncthreads();
@@ -510,18 +516,18 @@ __global__ __launch_bounds__(kTB) void mm_merge(VoxelJobDev A, VoxelJobDev B, Ma
         bool in = false, live = false;
         float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
         if (j < jend) {
-          PointRec p;
+          float4 pq = make_float4(0.f, 0.f, 0.f, 0.f);
           if (part == 0) {
             in = map_idx(V, j) == key;
-            if (in) live = mv_fetch(V, j, p);
+            if (in) live = mv_fetch4(V, j, pq);
           } else {
             in = (V.full ? (unsigned long long)skeys[V.base + j] : set_idx(V, j)) == key;
             if (in) {
-              mv_fetch(V, svals[V.base + j], p);
+              mv_fetch4(V, svals[V.base + j], pq);
               live = true;
             }
           }
-          if (live) q = make_float4(p.x, p.y, p.z, p.intensity);
+          if (live) q = pq;
         }
         s_cp[t] = q;
         s_cl[t] = live ? 1 : 0;
@@ -588,9 +594,9 @@ __global__ __launch_bounds__(kTB) void mm_merge(VoxelJobDev A, VoxelJobDev B, Ma
     const float4 c = s_pt[k];
     float x = c.x, y = c.y, z = c.z;
     if (V.ovf) {
-      PointRec p;
-      mv_fetch(V, __float_as_int(c.x), p);
-      x = p.x; y = p.y; z = p.z;
+      float4 q;
+      mv_fetch4(V, __float_as_int(c.x), q);
+      x = q.x; y = q.y; z = q.z;
     }
     bool ok;
     s_key[k] = mm_cell_key(x, y, z, V.J.inv, ok);
@@ -614,12 +620,18 @@ __global__ __launch_bounds__(kTB) void mm_merge(VoxelJobDev A, VoxelJobDev B, Ma
     gx[r] = gy[r] = gz[r] = 0.f;
     if (gv[r]) {
       const float4 c = s_pt[k];
-      PointRec o;
-      if (V.ovf) mv_fetch(V, __float_as_int(c.x), o);
-      else o = centroid_rec(c);
-      V.J.out[pre.a + k] = o;
+      float4 lo, hi;   // (the record as two halves: no PointRec temporary)
+      if (V.ovf) {
+        vox_fetch_halves(V.J, V.n0, V.n1, __float_as_int(c.x), lo, hi);
+      } else {   // VoxelGrid's output record of a centroid: x, y, z, 1 | intensity, ring 0, time 0, 0
+        lo = make_float4(c.x, c.y, c.z, 1.0f);
+        hi = make_float4(c.w, 0.0f, 0.0f, 0.0f);
+      }
+      float4* o = reinterpret_cast<float4*>(V.J.out + pre.a + k);
+      o[0] = lo;
+      o[1] = hi;
       V.K.out[pre.a + k] = s_key[k];
-      gx[r] = o.x; gy[r] = o.y; gz[r] = o.z;
+      gx[r] = lo.x; gy[r] = lo.y; gz[r] = lo.z;
     }
   }
   // the next kNN grid's per-point step (grid_count_job) for the map's points pre.a + k, all rounds at once
@@ -630,6 +642,22 @@ __global__ __launch_bounds__(kTB) void mm_merge(VoxelJobDev A, VoxelJobDev B, Ma
     V.K.meta_out->valid = 1;
     V.K.meta_out->seq = seq;
   }
+}
+
+template <int PER>
+__global__ __launch_bounds__(kTB) void mm_merge(VoxelJobDev A, VoxelJobDev B, MapKeys KA, MapKeys KB,
+                                                const uint32_t* __restrict__ skeys, const int* __restrict__ svals,
+                                                int* __restrict__ ctl, unsigned long long* __restrict__ mstatus,
+                                                int tiles_cap, int tilesA,
+                                                const unsigned* __restrict__ radix_ctl, const int* __restrict__ gate,
+                                                unsigned seq, int violate_mod, GridCountDev GA, GridCountDev GB,
+                                                int count_grid, int by_index) {
+  if ((int)blockIdx.x < tilesA)   // (block-uniform)
+    mm_merge_job<PER>(A, KA, GA, 0, skeys, svals, ctl, mstatus, tiles_cap, tilesA, radix_ctl, gate, seq, violate_mod,
+                      count_grid, by_index);
+  else
+    mm_merge_job<PER>(B, KB, GB, 1, skeys, svals, ctl, mstatus, tiles_cap, tilesA, radix_ctl, gate, seq, violate_mod,
+                      count_grid, by_index);
 }
 
 }  // namespace

@@ -28,6 +28,7 @@ namespace {
 constexpr int kTB = 256;
 constexpr int kItems = 8;
 constexpr int kTile = kTB * kItems;
+typedef int v4i __attribute__((ext_vector_type(4)));
 constexpr unsigned long long kFlagAgg = 1ull << 32, kFlagInc = 2ull << 32;
 
 __device__ __forceinline__ unsigned long long lb_word(unsigned epoch, unsigned long long flag, unsigned v) {
@@ -82,12 +83,18 @@ __global__ __launch_bounds__(kTB) void radix_pass(const uint32_t* __restrict__ k
     val[r] = PAYLOAD ? i : (i < n ? vin[i] : 0);
     dig[r] = digs ? (i < n ? (unsigned)digs[i] : 0u) : (key[r] >> (8 * pass)) & 255u;
   }
-  PointRec rec[PAYLOAD ? kItems : 1];
+  // (as two native 4-int vectors: an array of PointRec or of HIP's int4 — structs — stayed a private array, 272 B /
+  // lane of scratch whose traffic the pass's HBM counters showed; native vectors are promoted to VGPRs)
+  v4i rlo[PAYLOAD ? kItems : 1], rhi[PAYLOAD ? kItems : 1];
   if (PAYLOAD) {
 #pragma unroll
     for (int r = 0; r < kItems; ++r) {
       const int i = base + r * 64 + lane;
-      if (i < n) rec[r] = pin[i];
+      if (i < n) {
+        const v4i* q = reinterpret_cast<const v4i*>(pin + i);
+        rlo[r] = q[0];
+        rhi[r] = q[1];
+      }
     }
   }
   if (!gv) return;
@@ -201,14 +208,15 @@ __global__ __launch_bounds__(kTB) void radix_pass(const uint32_t* __restrict__ k
   const unsigned long long ts2 = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
   // 4. scatter
   if (PAYLOAD) {   // keys / values as below; the records through LDS in tile-sorted order, then written as runs
-    __shared__ PointRec s_rec[PAYLOAD ? kTile : 1];
+    __shared__ v4i s_rec[PAYLOAD ? kTile : 1][2];
     __shared__ unsigned char s_dig[PAYLOAD ? kTile : 1];
 #pragma unroll
     for (int r = 0; r < kItems; ++r) {
       if (base + r * 64 + lane < n) {
         const unsigned d = dig[r];
         const unsigned loc = s_tstart[d] + s_wcnt[w][d] + rank[r];
-        s_rec[loc] = rec[r];
+        s_rec[loc][0] = rlo[r];
+        s_rec[loc][1] = rhi[r];
         s_dig[loc] = (unsigned char)d;
         if (kout) {
           const unsigned dst = s_off[d] + s_wcnt[w][d] + rank[r];
@@ -222,9 +230,11 @@ __global__ __launch_bounds__(kTB) void radix_pass(const uint32_t* __restrict__ k
     for (int j = t; j < nloc; j += kTB) {   // consecutive j of one digit land on consecutive slots
       const unsigned d = s_dig[j];
       const unsigned dst = s_off[d] + ((unsigned)j - s_tstart[d]);
-      const PointRec q = s_rec[j];
-      prec[dst] = q;
-      pxyz[dst] = make_float4(q.x, q.y, q.z, 0.0f);
+      const v4i lo = s_rec[j][0], hi = s_rec[j][1];
+      v4i* o = reinterpret_cast<v4i*>(prec + dst);
+      o[0] = lo;
+      o[1] = hi;
+      pxyz[dst] = make_float4(__int_as_float(lo.x), __int_as_float(lo.y), __int_as_float(lo.z), 0.0f);
     }
   } else {
 #pragma unroll

@@ -8,12 +8,14 @@ namespace floam {
 
 constexpr int kRadixDigits = 256;
 constexpr int kRadixPasses = 4;
-constexpr int kRadixHistWords = kRadixPasses * kRadixDigits;   // followed by 4 tile tickets + 1 error word
-constexpr int kRadixTicketWord = kRadixHistWords;               // [pass]: the pass's tile tickets
+constexpr int kRadixHistWords = kRadixPasses * kRadixDigits;   // followed by 4 spare words + 1 error word
 constexpr int kRadixErrorWord = kRadixHistWords + 4;            // != 0: a lookback timed out
 constexpr int kRadixZeroWords = kRadixHistWords + 5;            // zeroed per sort
 constexpr int kRadixEpochWord = kRadixHistWords + 5;            // sort counter (tags the lookback words)
-constexpr int kRadixCtlWords = kRadixHistWords + 8;
+// [pass]: the pass's tile tickets, on a 128-B line of their own (the every-block reads of the epoch and the
+// histograms would otherwise queue behind the tickets' atomics), zeroed per sort with the words above
+constexpr int kRadixTicketWord = kRadixHistWords + 32;
+constexpr int kRadixCtlWords = kRadixHistWords + 64;
 
 struct RadixScratch {
   DevBuf<unsigned> ctl;                  // [4][256] digit histograms, [4] tickets, [1] error (zeroed per sort),
@@ -46,6 +48,7 @@ __device__ __forceinline__ void radix_hist_end(const unsigned* s_hist, unsigned*
 // zero the per-sort words and advance the sort counter (epoch 0x3FFFFFFF is the fresh-array pattern: skipped)
 __device__ __forceinline__ void radix_ctl_zero(unsigned* ctl, int t, int stride) {
   for (int k = t; k < kRadixZeroWords; k += stride) ctl[k] = 0u;
+  for (int k = t; k < kRadixPasses; k += stride) ctl[kRadixTicketWord + k] = 0u;
   if (t == 0) {
     unsigned e = (ctl[kRadixEpochWord] + 1u) & 0x3FFFFFFFu;
     if (e == 0x3FFFFFFFu) e = 0u;

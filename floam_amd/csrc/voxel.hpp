@@ -71,6 +71,44 @@ __device__ __forceinline__ bool vox_fetch(const VoxelJobDev& J, int n0, int n1, 
   return true;
 }
 
+// The same element as two 16-B halves — lo = {x, y, z, pad0}, hi = {intensity, ring | pad1, time, pad2} — without a
+// PointRec temporary (a struct with 16-bit fields copied along conditional paths stays a private array in some
+// kernels: mm_merge's scratch).  xyzi only: vox_fetch4.
+__device__ __forceinline__ bool vox_fetch_halves(const VoxelJobDev& J, int n0, int n1, int i, float4& lo, float4& hi) {
+  const PointRec* src;
+  bool to_map = false;
+  if (i < n0) {
+    src = J.part0 + i;
+  } else if (i < n0 + n1) {
+    src = J.part1 + (i - n0);
+    to_map = J.pose != nullptr;
+  } else {
+    return false;
+  }
+  const float4* q = reinterpret_cast<const float4*>(src);
+  lo = q[0];
+  hi = q[1];
+  if (to_map) {   // pointAssociateToMap (:126-135) into an XYZI record
+    float x, y, z;
+    associate_to_map(J.pose, lo.x, lo.y, lo.z, x, y, z);
+    lo = make_float4(x, y, z, 1.0f);
+    hi = make_float4(hi.x, 0.0f, 0.0f, 0.0f);   // intensity; ring = pad1 = 0 (bits), time = pad2 = 0
+  }
+  if (J.pose) {   // CropBox min/max = Vector4f(t -+ 100) (double -> float), inclusive (:270-287)
+    const double* t = J.pose + 4;
+    const float mnx = (float)(t[0] - 100), mny = (float)(t[1] - 100), mnz = (float)(t[2] - 100);
+    const float mxx = (float)(t[0] + 100), mxy = (float)(t[1] + 100), mxz = (float)(t[2] + 100);
+    if (lo.x < mnx || lo.y < mny || lo.z < mnz || lo.x > mxx || lo.y > mxy || lo.z > mxz) return false;
+  }
+  return true;
+}
+__device__ __forceinline__ bool vox_fetch4(const VoxelJobDev& J, int n0, int n1, int i, float4& xyzi) {
+  float4 lo, hi;
+  const bool kept = vox_fetch_halves(J, n0, n1, i, lo, hi);
+  xyzi = make_float4(lo.x, lo.y, lo.z, hi.x);
+  return kept;
+}
+
 constexpr int kVoxMinMaxBlocks = 64;   // bounding-box partials per cloud
 
 struct VoxelGeom {
@@ -168,7 +206,10 @@ struct MergeCheck {
 };
 // [0, 1] kept set elements of job A / B, [2, 3] mode (1 full), [4, 5] overflow, [6 + 6j .. 11 + 6j] job j's min_b[3],
 // div_b[3]
-constexpr int kMergeCtlWords = 20;   // ... [18 + job] mm_merge's tile tickets
+// ... [32], [64]: mm_merge's tile tickets per job, each on a 128-B line of its own (every block reads [0, 18) at its
+// start: beside the tickets' atomics those reads would queue behind them — +7 us per merge, r04i)
+constexpr int kMergeCtlWords = 96;
+constexpr int kMergeTicketWord = 32;   // + 32 * job
 
 // bounding box of one cloud (as vox_minmax_block) + the MergeCheck test of its scan points
 __device__ __forceinline__ void mm_minmax_block(const VoxelJobDev& J, int job, int b, int nblocks,
