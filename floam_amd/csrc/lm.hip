@@ -536,7 +536,8 @@ __device__ __forceinline__ void next_step_wave(LMState& s, bool check_gmax, int 
     const bool far = check_gmax && gradient_step_far(s.g);   // (wave-uniform: every lane holds the same g)
     double d[6];
 #pragma unroll
-    for (int k = 0; k < 6; ++k) d[k] = lane == 1 ? (check_gmax && !far ? -s.g[k] : 0.0) : (valid ? delta[k] : 0.0);
+    for (int k = 0; k < 6; ++k)   // (lane 1 without a projection to compute follows lane 0: no divergent branch)
+      d[k] = (lane == 1 && check_gmax && !far) ? -s.g[k] : (valid ? delta[k] : 0.0);
     double out[7];
     se3_plus(s.x, d, out);
     CTRL_T(tc);
@@ -561,7 +562,7 @@ __device__ __forceinline__ void next_step_wave(LMState& s, bool check_gmax, int 
     }
     // HandleInvalidStep -> StepIsInvalid -> StepRejected(0)
     if (++s.invalid >= 5) { s.done = 1; return; }
-    s.radius /= s.dfac;
+    s.radius *= recip(s.dfac);   // (dfac a power of two: exact)
     s.dfac *= 2.0;
     s.reuse = 1;
     if (s.iteration >= 4 || s.radius < 1e-32) { s.done = 1; return; }
@@ -611,7 +612,7 @@ __device__ __forceinline__ void lm_logic(LMState& s, const double (&sums)[LM_NSU
   if (sn <= 1e-8 * (s.x_norm + 1e-8)) { s.done = 1; return; }
   // FunctionToleranceReached
   if (fabs(s.x_cost - cand_cost) <= 1e-6 * s.x_cost) { s.done = 1; return; }
-  const double rho = (s.x_cost - cand_cost) / s.mcc;
+  const double rho = (s.x_cost - cand_cost) * recip(s.mcc);   // (mcc > 0; within an ulp of the division)
   bool success = false;
   if (rho > 1e-3) {
 #pragma unroll
@@ -623,13 +624,13 @@ __device__ __forceinline__ void lm_logic(LMState& s, const double (&sums)[LM_NSU
 #pragma unroll
     for (int k = 0; k < 6; ++k) s.g[k] = sums[22 + k];
     const double t = 2.0 * rho - 1.0;
-    s.radius = fmin(1e16, s.radius / fmax(1.0 / 3.0, 1.0 - t * t * t));
+    s.radius = fmin(1e16, s.radius * recip(fmax(1.0 / 3.0, 1.0 - t * t * t)));
     s.dfac = 2.0;
     s.reuse = 0;
     s.successful++;
     success = true;
   } else {
-    s.radius /= s.dfac;
+    s.radius *= recip(s.dfac);   // (dfac a power of two: exact)
     s.dfac *= 2.0;
     s.reuse = 1;
   }
