@@ -580,6 +580,7 @@ __device__ __forceinline__ double norm7(const double (&a)[7]) {
 // Called by all 64 lanes of one wave with identical s and sums; every lane ends with the same s.
 __device__ __forceinline__ void lm_logic(LMState& s, const double (&sums)[LM_NSUM], int lane) {
   CTRL_T(t0);
+  bool check_gmax;   // the gradient-norm test is due: at iteration zero and after a successful step
   if (s.phase == 0) {   // IterationZero
     s.n_res = (int)sums[28];
     s.x_cost = sums[0];
@@ -599,45 +600,44 @@ __device__ __forceinline__ void lm_logic(LMState& s, const double (&sums)[LM_NSU
     s.invalid = 0;
     s.iteration = 0;
     s.phase = 1;
-    next_step_wave(s, true, lane);
-    return;
-  }
-  double cand_cost = sums[0];
-  if (!isfinite(cand_cost)) cand_cost = DBL_MAX;
-  // ParameterToleranceReached (candidate not applied)
-  double sn = 0.0;
-#pragma unroll
-  for (int i = 0; i < 7; ++i) sn += (s.x[i] - s.cand[i]) * (s.x[i] - s.cand[i]);
-  sn = sqrt(sn);
-  if (sn <= 1e-8 * (s.x_norm + 1e-8)) { s.done = 1; return; }
-  // FunctionToleranceReached
-  if (fabs(s.x_cost - cand_cost) <= 1e-6 * s.x_cost) { s.done = 1; return; }
-  const double rho = (s.x_cost - cand_cost) * recip(s.mcc);   // (mcc > 0; within an ulp of the division)
-  bool success = false;
-  if (rho > 1e-3) {
-#pragma unroll
-    for (int i = 0; i < 7; ++i) s.x[i] = s.cand[i];
-    s.x_norm = norm7(s.x);
-    s.x_cost = cand_cost;
-#pragma unroll
-    for (int k = 0; k < 21; ++k) s.H[k] = sums[1 + k];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) s.g[k] = sums[22 + k];
-    const double t = 2.0 * rho - 1.0;
-    s.radius = fmin(1e16, s.radius * recip(fmax(1.0 / 3.0, 1.0 - t * t * t)));
-    s.dfac = 2.0;
-    s.reuse = 0;
-    s.successful++;
-    success = true;
+    check_gmax = true;
   } else {
-    s.radius *= recip(s.dfac);   // (dfac a power of two: exact)
-    s.dfac *= 2.0;
-    s.reuse = 1;
+    double cand_cost = sums[0];
+    if (!isfinite(cand_cost)) cand_cost = DBL_MAX;
+    // ParameterToleranceReached (candidate not applied)
+    double sn = 0.0;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) sn += (s.x[i] - s.cand[i]) * (s.x[i] - s.cand[i]);
+    sn = sqrt(sn);
+    if (sn <= 1e-8 * (s.x_norm + 1e-8)) { s.done = 1; return; }
+    // FunctionToleranceReached
+    if (fabs(s.x_cost - cand_cost) <= 1e-6 * s.x_cost) { s.done = 1; return; }
+    const double rho = (s.x_cost - cand_cost) * recip(s.mcc);   // (mcc > 0; within an ulp of the division)
+    check_gmax = rho > 1e-3;   // (success)
+    if (check_gmax) {
+#pragma unroll
+      for (int i = 0; i < 7; ++i) s.x[i] = s.cand[i];
+      s.x_norm = norm7(s.x);
+      s.x_cost = cand_cost;
+#pragma unroll
+      for (int k = 0; k < 21; ++k) s.H[k] = sums[1 + k];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) s.g[k] = sums[22 + k];
+      const double t = 2.0 * rho - 1.0;
+      s.radius = fmin(1e16, s.radius * recip(fmax(1.0 / 3.0, 1.0 - t * t * t)));
+      s.dfac = 2.0;
+      s.reuse = 0;
+      s.successful++;
+    } else {
+      s.radius *= recip(s.dfac);   // (dfac a power of two: exact)
+      s.dfac *= 2.0;
+      s.reuse = 1;
+    }
+    if (s.iteration >= 4 || s.radius < 1e-32) { s.done = 1; return; }
   }
-  if (s.iteration >= 4 || s.radius < 1e-32) { s.done = 1; return; }
   CTRL_T(t1);
   CTRL_ADD(1, t1 - t0);
-  next_step_wave(s, success, lane);
+  next_step_wave(s, check_gmax, lane);   // (one call site: the step's code is inlined once)
   CTRL_T(t2);
   CTRL_ADD(5, t2 - t0);
   CTRL_ADD(0, 1ull);
@@ -946,6 +946,8 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     __syncthreads();   // s_pt and s_done of this evaluation
     if (s_done) break;
+    unsigned long long t1 = t0, t2 = t0;
+    unsigned tag = ep + (unsigned)it;
     if (pre0 && it == 0) {   // (block-uniform) no records to evaluate, nothing to hand off: the surf half, then control
       if (tid >= NR) surf_sums_wave(s_pt, o, G, (double)sst.corr_surf, s_ssum, lane);
       if (__syncthreads_or(a.fail_test != 0)) {
@@ -953,60 +955,47 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
         break;
       }
       if (tid < LM_NSUM) s_sums[tid] = s_esum[tid] + s_ssum[tid];   // edge + surf
-      __syncthreads();
-      if (peers && !peer_exchange(a, it, ep + (unsigned)it, s_sums, s_xch)) {
+    } else {
+      double acc[LM_NSUM];
+      if (tid < NR) {
+        R x[7];
+#pragma unroll
+        for (int k = 0; k < 7; ++k) x[k] = (R)s_pt[k];
+        eval_records<HUBER, R>(x, has0, edge0, f0, i0 + stride, stride, ne, total, a.erec, a.evalid, a.ecap, a.srec,
+                               a.svalid, a.scap, acc);
+      } else {
+#pragma unroll
+        for (int k = 0; k < LM_NSUM; ++k) acc[k] = 0.0;
+        if (GRAM) surf_sums_wave(s_pt, o, G, (double)sst.corr_surf, s_ssum, lane);   // beside the edge records
+      }
+      const double v = block_sums<NR>(acc, s_buf);
+      unsigned long long* slot = a.part + (size_t)(it & 1) * kRecEvalBlocks * 2 * LM_NSUM;
+      if (tid < LM_NSUM * kStrips && (tid & 7) < 2) {   // 58 granules: component c in 32-bit halves (lanes 8c, 8c + 1)
+        const int c = tid >> 3, h = tid & 1;
+        const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+        put_granule(&slot[blk * 2 * LM_NSUM + 2 * c + h], granule(tag, h ? (unsigned)(b >> 32) : (unsigned)b));
+      }
+      t1 = __builtin_amdgcn_s_memrealtime();
+      // every active block's granules of this evaluation (this block's own included): kSweep loads in flight per
+      // thread and poll round
+      int bad = 0;
+      for (int j0 = tid; j0 < ngr; j0 += kSweep * kTB)
+        if (!sweep_granules(slot, j0, ngr, tag, tab)) bad = 1;
+      if (a.fail_test) bad = 1;
+      if (__syncthreads_or(bad)) {
         failed_at = it;
         break;
       }
-      if (tid < 64) {
-#if FLOAM_LM_STATE_REGS
-        control_step(s, sst, s_sums, lane);
-        if (tid < 7) s_pt[tid] = point_component(s, tid);
-        if (lane == 0) s_done = s.done;
-#else
-        control_step_lds(sst, s_sums, lane, s_pt, &s_done);
-#endif
-      }
-      continue;
+      t2 = __builtin_amdgcn_s_memrealtime();
+      reduce_blocks([&](int c, int b) {
+        const int g = b * 2 * LM_NSUM + 2 * c;
+        return __longlong_as_double((long long)(((unsigned long long)tab[g + 1] << 32) | tab[g]));
+      }, nact, s_sums);
+      if (GRAM && tid < LM_NSUM) s_sums[tid] = s_sums[tid] + s_ssum[tid];   // edge + surf
     }
-    double acc[LM_NSUM];
-    if (tid < NR) {
-      R x[7];
-#pragma unroll
-      for (int k = 0; k < 7; ++k) x[k] = (R)s_pt[k];
-      eval_records<HUBER, R>(x, has0, edge0, f0, i0 + stride, stride, ne, total, a.erec, a.evalid, a.ecap, a.srec,
-                             a.svalid, a.scap, acc);
-    } else {
-#pragma unroll
-      for (int k = 0; k < LM_NSUM; ++k) acc[k] = 0.0;
-      if (GRAM) surf_sums_wave(s_pt, o, G, (double)sst.corr_surf, s_ssum, lane);   // beside the edge records
-    }
-    const double v = block_sums<NR>(acc, s_buf);
-    unsigned long long* slot = a.part + (size_t)(it & 1) * kRecEvalBlocks * 2 * LM_NSUM;
-    const unsigned tag = ep + (unsigned)it;
-    if (tid < LM_NSUM * kStrips && (tid & 7) < 2) {   // 58 granules: component c in 32-bit halves (lanes 8c, 8c + 1)
-      const int c = tid >> 3, h = tid & 1;
-      const unsigned long long b = (unsigned long long)__double_as_longlong(v);
-      put_granule(&slot[blk * 2 * LM_NSUM + 2 * c + h], granule(tag, h ? (unsigned)(b >> 32) : (unsigned)b));
-    }
-    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
-    // every active block's granules of this evaluation (this block's own included): kSweep loads in flight per
-    // thread and poll round
-    int bad = 0;
-    for (int j0 = tid; j0 < ngr; j0 += kSweep * kTB)
-      if (!sweep_granules(slot, j0, ngr, tag, tab)) bad = 1;
-    if (a.fail_test) bad = 1;
-    if (__syncthreads_or(bad)) {
-      failed_at = it;
-      break;
-    }
-    const unsigned long long t2 = __builtin_amdgcn_s_memrealtime();
-    reduce_blocks([&](int c, int b) {
-      const int g = b * 2 * LM_NSUM + 2 * c;
-      return __longlong_as_double((long long)(((unsigned long long)tab[g + 1] << 32) | tab[g]));
-    }, nact, s_sums);
-    if (GRAM && tid < LM_NSUM) s_sums[tid] = s_sums[tid] + s_ssum[tid];   // edge + surf
     __syncthreads();
+    // (one call site each for the exchange and the control step: a second inlined copy of the control step doubled
+    // the kernel's code, 16k instructions against 8k, past what the instruction cache holds)
     if (peers && !peer_exchange(a, it, tag, s_sums, s_xch)) {
       failed_at = it;
       break;
