@@ -389,6 +389,7 @@ struct floam_odom {
   hipGraphExec_t graph_exec[2][kExecRing] = {};
   DevBuf<unsigned long long> prof_bytes;
   DevBuf<unsigned long long> traffic_set;
+  DevBuf<float4> knn_evict;   // FLOAM_KNN_STAGES (diagnostic): the L2 eviction buffer of knn_stage_launch
   bool prof_bytes_init = false;
   // host mirror of the controller poses, as of the last collected update
   Pose odom = pose_identity(), last_odom = pose_identity();
@@ -630,6 +631,10 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
     {
       ProfScope ps(ctx, "knn", FLOAM_PROF_KNN);   // the correspondence pass: search + geometry
       {
+        static const bool stages = std::getenv("FLOAM_KNN_STAGES") != nullptr;
+        if (stages && (ctx.profile & FLOAM_PROF_KNN_BYTES))   // (replay only, before the timed scope)
+          knn_stage_launch(o->lm.p, it == 0 ? x0_dev : nullptr, qe, o->gE, o->ce, qs, o->gS, o->cs, o->mapE.count.p,
+                           o->mapS.count.p, o->rank, o->world, o->knn_evict, st);
         ProfScope ps1(ctx, "knn_search", FLOAM_PROF_KNN_DETAIL);
         // (also starts the solve: LM state reset, the first solve at the prediction)
         knn_launch(o->lm.p, it == 0 ? x0_dev : nullptr, qe, o->gE, o->ce, qs, o->gS, o->cs, o->mapE.count.p,

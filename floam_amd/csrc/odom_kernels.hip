@@ -703,7 +703,10 @@ __device__ __forceinline__ bool geom_fit(const R (&P)[5][3], float4 pq, double* 
 // FUSED (FLOAM_KNN_FUSED_PROTO=1, a measurement prototype): lane 0 of the group also runs the
 // query's line / plane fit and writes its record (the geometry launch still runs after it — the prototype prices
 // the fits inside the search, a lower bound of a fused kernel, which would also need the surf Gram reduction)
-template <int G, int U, int NB, bool FUSED = false>
+// STOP (diagnostic, FLOAM_KNN_STAGES: the per-round-trip read attribution of DESIGN.md §3) ends each query after
+// its first STOP dependent memory round trips — 1: the query load and transform; 2: + the coarse probes of the fine
+// block; 3: + stage 1's candidate loads; 4: + stage 2 — and writes only a flag derived from what it loaded
+template <int G, int U, int NB, bool FUSED = false, int STOP = 0>
 __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArgs& A, int gid, int ngroups,
                                           int lane, bool gate, int rank, int world, int* __restrict__ s_pre,
                                           int* __restrict__ s_start, int* __restrict__ s_cc, bool edge = true) {
@@ -720,12 +723,22 @@ __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArg
       associate_to_map(pose, pq.x, pq.y, pq.z, wx, wy, wz);   // pointAssociateToMap (:126-135)
       int qx, qy, qz;
       fine_cell(wx, wy, wz, qx, qy, qz);
+      if constexpr (STOP == 1) {
+        if (lane == 0) A.valid[i] = (uint8_t)(qx ^ qy ^ qz);
+        continue;
+      }
       Top5 t;
 #pragma unroll
       for (int k = 0; k < 5; ++k) t.k[k] = ~0ull;
       int cnt = 0;
       int lx, ly, lz;
       knn_block_corner(NB, wx, wy, wz, qx, qy, qz, lx, ly, lz);
+      if constexpr (STOP == 2) {
+        fine_block_ranges<G, NB>(A, lx, ly, lz, lane, s_pre, s_start, s_cc);
+        if (lane == 0) A.valid[i] = (uint8_t)s_pre[NB * NB * NB];
+        wave_lds_order();
+        continue;
+      }
       stencil_scan<G, U, false, NB>(A, lx, lx + NB - 1, ly, ly + NB - 1, lz, lz + NB - 1, wx, wy, wz, lane, s_pre,
                                     s_start, t, cnt, s_cc);
       group_merge<G>(t, cnt);
@@ -737,6 +750,10 @@ __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArg
                                   fminf(wy - 0.5f * (float)ly, 0.5f * (float)(ly + NB) - wy)),
                             fminf(wz - 0.5f * (float)lz, 0.5f * (float)(lz + NB) - wz));
       const bool complete = cnt >= 5 && __uint_as_float((unsigned)(t.k[4] >> 32)) < b * b;
+      if constexpr (STOP == 3) {
+        if (lane == 0) A.valid[i] = (uint8_t)(cnt + (complete ? 1 : 0) + (int)(t.k[4] & 0xFF));
+        continue;
+      }
       if (!complete) {
         // coarse cells floor(q - r) .. floor(q + r) per axis (exact in double).  r = 1 (every point within 1 m)
         // unless stage 1 already holds 5 points within 1 m: then the 5-NN and every point tied with the 5th lie in
@@ -754,6 +771,10 @@ __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArg
                                  s_start, t, cnt);
         group_merge<G>(t, cnt);
         flags |= 2;
+      }
+      if constexpr (STOP == 4) {
+        if (lane == 0) A.valid[i] = (uint8_t)(flags + cnt + (int)(t.k[4] & 0xFF));
+        continue;
       }
       if (cnt >= 5) {   // sqd[4] < 1 (:154, :210)
         flags |= 1;
@@ -803,7 +824,7 @@ __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArg
 // Edge and surf kNN in one launch: blocks [0, nbE) run edge groups, the others surf groups.  The launch also starts
 // the solve (lm_init folded in): block 0 resets the LM state and, for the first solve of an update, stores the
 // prediction x0 that every block uses for its transforms (the others never read st->x in that case).
-template <int G, int U, int W, int NB, bool FUSED = false>
+template <int G, int U, int W, int NB, bool FUSED = false, int STOP = 0>
 __global__ __launch_bounds__(kTB, W) void knn_kernel(LMState* __restrict__ st, const double* __restrict__ x0_dev,
                                                   CorrArgs E, CorrArgs S, int nbE,
                                                   const int* __restrict__ d_me, const int* __restrict__ d_ms,
@@ -838,7 +859,7 @@ __global__ __launch_bounds__(kTB, W) void knn_kernel(LMState* __restrict__ st, c
   const int nq = min(*A.d_n, A.n_ub);
   const int nact = min(nb, (int)(((long long)nq * G + kTB - 1) / kTB));
   if (p < nact) p = xcd_block(p, nact);
-  knn_group<G, U, NB, FUSED>(pose, A, (p * kTB + (int)threadIdx.x) / G, nb * (kTB / G), lane, gate, rank, world,
+  knn_group<G, U, NB, FUSED, STOP>(pose, A, (p * kTB + (int)threadIdx.x) / G, nb * (kTB / G), lane, gate, rank, world,
                              s_pre[g], s_start[g], s_cc[g], edge);
 }
 
@@ -1490,6 +1511,52 @@ void geom_launch(LMState* d_st, const QuerySet& qe, CorrSet& ce, const QuerySet&
   else
     hipLaunchKernelGGL(geom_kernel<double>, dim3(gE + kSurfGeomBlocks), dim3(kTB), 0, st, d_st, E, S, (int)gE,
                        gpart, gmat, b.gcnt.p, epart);
+  FLOAM_LAUNCH_CHECK();
+}
+
+// (diagnostic) every XCD's L2 refilled with other lines: a grid-stride read of a buffer 16x the size of one XCD's
+// L2 by every block, so that the next launch finds none of its lines cached (FETCH_SIZE then counts its cold fetches)
+__global__ __launch_bounds__(kTB) void l2_evict(const float4* __restrict__ buf, size_t n, float* __restrict__ sink) {
+  float acc = 0.f;
+  for (size_t i = (size_t)blockIdx.x * kTB + threadIdx.x; i < n; i += (size_t)gridDim.x * kTB) acc += buf[i].x;
+  if (acc == 1234.5f) sink[0] = acc;   // (never: keeps the loads)
+}
+
+void knn_stage_launch(LMState* d_st, const double* x0_dev, const QuerySet& qe, const Grid& ge, CorrSet& ce,
+                      const QuerySet& qs, const Grid& gs, CorrSet& cs, const int* d_me, const int* d_ms, int rank,
+                      int world, DevBuf<float4>& evict, hipStream_t st) {
+  if (qe.n_ub <= 0 && qs.n_ub <= 0) return;
+  constexpr size_t kEvict = (size_t)64 << 20;   // bytes
+  if (!evict.p) {
+    evict.reserve(kEvict / sizeof(float4) + 1);
+    FLOAM_HIP(hipMemsetAsync(evict.p, 0, kEvict, st));
+  }
+  CorrArgs E, S;
+  corr_args(qe, ge, ce, qs, gs, cs, E, S);
+  constexpr int G = kGroupDefault;
+  const int nE = qe.grid_hint > 0 ? std::min(qe.grid_hint, qe.n_ub) : qe.n_ub;
+  const int nS = qs.grid_hint > 0 ? std::min(qs.grid_hint, qs.n_ub) : qs.n_ub;
+  const unsigned nbE = std::min(div_up((size_t)std::max(nE, 1) * G, kTB), 4096u);
+  const unsigned nbS = std::min(div_up((size_t)std::max(nS, 1) * G, kTB), 8192u);
+  const dim3 g(nbE + nbS);
+  auto flush = [&] {
+    hipLaunchKernelGGL(l2_evict, dim3(2048), dim3(kTB), 0, st, evict.p, kEvict / sizeof(float4),
+                       reinterpret_cast<float*>(evict.p) + kEvict / sizeof(float));
+    FLOAM_LAUNCH_CHECK();
+  };
+  flush();
+  hipLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6, 3, false, 1>), g, dim3(kTB), 0, st, d_st, x0_dev, E, S, (int)nbE,
+                     d_me, d_ms, rank, world);
+  flush();
+  hipLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6, 3, false, 2>), g, dim3(kTB), 0, st, d_st, x0_dev, E, S, (int)nbE,
+                     d_me, d_ms, rank, world);
+  flush();
+  hipLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6, 3, false, 3>), g, dim3(kTB), 0, st, d_st, x0_dev, E, S, (int)nbE,
+                     d_me, d_ms, rank, world);
+  flush();
+  hipLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6, 3, false, 4>), g, dim3(kTB), 0, st, d_st, x0_dev, E, S, (int)nbE,
+                     d_me, d_ms, rank, world);
+  flush();   // (the real search follows, cold as well)
   FLOAM_LAUNCH_CHECK();
 }
 

@@ -286,6 +286,11 @@ void knn_launch(LMState* d_st, const double* x0_dev, const QuerySet& qe, const G
 void geom_launch(LMState* d_st, const QuerySet& qe, CorrSet& ce, const QuerySet& qs, CorrSet& cs, bool gram,
                  bool fp32, LMBuffers& b, hipStream_t st, bool edge_sums = false);
 // algorithmic bytes of the correspondence pass just issued (profiling only), accumulated into *d_bytes
+// (diagnostic, FLOAM_KNN_STAGES=1 in a profiled replay) the search cut after each of its dependent round trips, every
+// variant after an L2 eviction, then one more eviction before the real search
+void knn_stage_launch(LMState* d_st, const double* x0_dev, const QuerySet& qe, const Grid& ge, CorrSet& ce,
+                      const QuerySet& qs, const Grid& gs, CorrSet& cs, const int* d_me, const int* d_ms, int rank,
+                      int world, DevBuf<float4>& evict, hipStream_t st);
 void knn_traffic_launch(const LMState* d_st, const QuerySet& q, const Grid& g, CorrSet& c, int rank, int world,
                         DevBuf<unsigned long long>& set, unsigned long long* d_bytes, hipStream_t st);
 

@@ -12,5 +12,6 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 tail -2 gpurun_out/$TAG/smoke.log
 bash tools/gpu_wb.sh ${TAG}_wb || exit $?
 bash tools/gpu_prof.sh ${TAG}_prof --cpu-baseline-seconds 3 || exit $?
+bash tools/gpu_knn_stages.sh ${TAG}_ks || exit $?
 bash tools/gpu_stamps.sh ${TAG}_st || exit $?
 echo all-done
