@@ -206,13 +206,48 @@ constexpr SurfTable make_surf_table() {
 }
 __constant__ SurfTable c_surf = make_surf_table();
 
+// How each of the 29 outputs follows from Y = G [K_0, K_1, K_2, c] (G symmetric, the products commute, so every
+// shortcut below is the very sum the full quadratic form computes, in the same order): a 13-term dot of one of
+// K_0, K_1, K_2, c with a row of Y; a single entry of Y (K_a . row r of G = (G K_a)_r, e_{9+a} . row of Y); a single
+// entry of G (e_{9+a} . row of G); or the count
+struct SurfOut {
+  signed char kind[LM_NSUM];   // 0 dot, 1 Y entry, 2 G entry, 3 count
+  signed char a[LM_NSUM];      // dot: A row (0..2 K_a, 3 c); entry: row
+  signed char b[LM_NSUM];      // dot: Y row; entry: column
+};
+constexpr SurfOut make_surf_out() {
+  const SurfTable T = make_surf_table();
+  SurfOut S{};
+  for (int t = 0; t < LM_NSUM; ++t) {
+    const int ra = T.ra[t], rb = T.rb[t];
+    if (t == 28) { S.kind[t] = 3; continue; }
+    if (rb >= 7 && rb < 11) {   // with a row of Y
+      if (ra < 3 || ra == 6) { S.kind[t] = 0; S.a[t] = (signed char)(ra == 6 ? 3 : ra); S.b[t] = (signed char)(rb - 7); }
+      else { S.kind[t] = 1; S.a[t] = (signed char)(rb - 7); S.b[t] = (signed char)(9 + ra - 3); }
+    } else {                    // with row rb - 11 of G
+      if (ra < 3) { S.kind[t] = 1; S.a[t] = (signed char)ra; S.b[t] = (signed char)(rb - 11); }
+      else { S.kind[t] = 2; S.a[t] = (signed char)(rb - 11); S.b[t] = (signed char)(9 + ra - 3); }
+    }
+  }
+  return S;
+}
+__constant__ SurfOut c_surf_out = make_surf_out();
+
+// Two LDS phases: every lane forms M and the translations itself (the wave-uniform values lane 0 used to publish;
+// the V rows are compile-time selections of them), lanes 0..12 form row i of Y from row i of G; then lane t < 29
+// forms output t.  Bit-identical to the four-phase form (same products, same summation orders).
 __device__ void surf_sums_wave(const double* x /* LDS [7] */, const double* o /* LDS [3] */,
                                const double (*G)[kGramW] /* LDS */, double n_surf, double* out /* LDS [29] */,
                                int t /* lane */) {
-  __shared__ double V[7][kGramW];   // K_0..K_5, c
-  __shared__ double Y[4][kGramW];   // G K_0, G K_1, G K_2, G c
-  __shared__ double Mt[16];         // M (row-major), t' = t - o, t, 1
-  if (t == 0) {
+  __shared__ double Yl[4][kGramW];   // G K_0, G K_1, G K_2, G c
+  constexpr SurfTable T = make_surf_table();
+  double g[kGramW];
+  if (t < kGramW) {
+#pragma unroll
+    for (int j = 0; j < kGramW; ++j) g[j] = G[t][j];
+  }
+  double Mt[16];
+  {
     const double qx = x[0], qy = x[1], qz = x[2], qw = x[3];
     const double U[3][3] = {{0, -qz, qy}, {qz, 0, -qx}, {-qy, qx, 0}};
 #pragma unroll
@@ -229,31 +264,43 @@ __device__ void surf_sums_wave(const double* x /* LDS [7] */, const double* o /*
     }
     Mt[15] = 1.0;
   }
-  wave_lds_order();
-  for (int e = t; e < 7 * kGramW; e += 64) {
-    const int v = e / kGramW, m = e % kGramW;
-    const int sg = c_surf.sgn[v][m];
-    const double mv = Mt[c_surf.idx[v][m]];
-    V[v][m] = sg > 0 ? mv : (sg < 0 ? -mv : 0.0);
+  auto V = [&](int v, int m) -> double {   // (v, m compile-time after unrolling)
+    const int sg = T.sgn[v][m];
+    const double mv = Mt[T.idx[v][m]];
+    return sg > 0 ? mv : (sg < 0 ? -mv : 0.0);
+  };
+  if (t < kGramW) {   // Y[v][t] = row t of G . V row (K_0, K_1, K_2, c)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      double a = 0.0;
+#pragma unroll
+      for (int j = 0; j < kGramW; ++j) a += g[j] * V(v == 3 ? 6 : v, j);
+      Yl[v][t] = a;
+    }
   }
   wave_lds_order();
-  if (t < 4 * kGramW) {   // Y = G [K_0, K_1, K_2, c]
-    const int v = t / kGramW, i = t % kGramW;
-    const double* vv = V[v == 3 ? 6 : v];
-    double a = 0.0;
+  if (t < LM_NSUM) {
+    const int kind = c_surf_out.kind[t], ra = c_surf_out.a[t], rb = c_surf_out.b[t];
+    double r;
+    if (kind == 0) {   // the four candidate dots in independent chains, then the lane's own
+      double d0 = 0.0, d1 = 0.0, d2 = 0.0, d3 = 0.0;
 #pragma unroll
-    for (int j = 0; j < kGramW; ++j) a += G[i][j] * vv[j];
-    Y[v][i] = a;
-  }
-  wave_lds_order();
-  if (t < LM_NSUM) {   // cost, J^T J upper (row-major), J^T r, count
-    const int ra = c_surf.ra[t], rb = c_surf.rb[t];
-    const double* A = V[ra];
-    const double* B = rb < 7 ? V[rb] : (rb < 11 ? Y[rb - 7] : G[rb - 11]);
-    double a = 0.0;
-#pragma unroll
-    for (int i = 0; i < kGramW; ++i) a += A[i] * B[i];
-    out[t] = t == 28 ? n_surf : (t == 0 ? 0.5 * a : a);
+      for (int m = 0; m < kGramW; ++m) {
+        const double y = Yl[rb][m];
+        d0 += V(0, m) * y;
+        d1 += V(1, m) * y;
+        d2 += V(2, m) * y;
+        d3 += V(6, m) * y;
+      }
+      r = ra == 0 ? d0 : (ra == 1 ? d1 : (ra == 2 ? d2 : d3));
+    } else if (kind == 1) {
+      r = Yl[ra][rb];
+    } else if (kind == 2) {
+      r = G[ra][rb];
+    } else {
+      r = n_surf;
+    }
+    out[t] = t == 0 ? 0.5 * r : r;
   }
   wave_lds_order();
 }

@@ -13,5 +13,7 @@ tail -2 gpurun_out/$TAG/smoke.log
 bash tools/gpu_wb.sh ${TAG}_wb || exit $?
 bash tools/gpu_prof.sh ${TAG}_prof --cpu-baseline-seconds 3 || exit $?
 bash tools/gpu_knn_stages.sh ${TAG}_ks || exit $?
+timeout -k 10 200 hipcc -O3 -std=c++17 -ffp-contract=fast --offload-arch=gfx950 tools/micro/lm_ctrl.hip -o /tmp/lm_ctrl \
+    > gpurun_out/$TAG/lm_ctrl_build.log 2>&1 && timeout -k 10 60 /tmp/lm_ctrl > gpurun_out/$TAG/lm_ctrl.txt 2>&1; cat gpurun_out/$TAG/lm_ctrl.txt
 bash tools/gpu_stamps.sh ${TAG}_st || exit $?
 echo all-done
