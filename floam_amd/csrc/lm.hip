@@ -499,34 +499,30 @@ __device__ __forceinline__ bool solve_step(LMState& s, double (&delta)[6]) {
     y[i] = v;
   }
 #pragma unroll
-  for (int i = 5; i >= 0; --i) {   // L^T y = D^-1 z
+  for (int i = 5; i >= 0; --i) {   // L^T y = D^-1 z (the newest unknown, y[i + 1], enters last: one FMA a row)
     double v = y[i] * rD[i];
 #pragma unroll
-    for (int k = i + 1; k < 6; ++k) v -= A[k * (k + 1) / 2 + i] * y[k];
+    for (int k = 5; k > i; --k) v -= A[k * (k + 1) / 2 + i] * y[k];
     y[i] = v;
   }
   bool finite = true;
 #pragma unroll
-  for (int k = 0; k < 6; ++k) {
-    y[k] = -y[k];   // the step
-    finite = finite && isfinite(y[k]);
-  }
+  for (int k = 0; k < 6; ++k) finite = finite && isfinite(y[k]);
   if (!finite) return false;
-  // model cost change -(step^T gs + step^T Hs step / 2)
-  double sg = 0.0, sHs = 0.0;
+  // model cost change -(step^T gs + step^T Hs step / 2) with step = -y and (Hs + D / radius) y = gs:
+  // = (y^T gs + y^T (D / radius) y) / 2 — two 6-term sums instead of the 6x6 quadratic form (equal in exact
+  // arithmetic; both terms non-negative, so no cancellation)
+  double yg = 0.0, yDy = 0.0;
 #pragma unroll
   for (int a = 0; a < 6; ++a) {
-    sg += y[a] * gs[a];
-    double hv = 0.0;
-#pragma unroll
-    for (int b = 0; b < 6; ++b) hv += Hs[a >= b ? a * (a + 1) / 2 + b : b * (b + 1) / 2 + a] * y[b];
-    sHs += y[a] * hv;
+    yg += y[a] * gs[a];
+    yDy += (y[a] * y[a]) * dg[a];
   }
-  const double mcc = -(sg + 0.5 * sHs);
+  const double mcc = 0.5 * (yg + yDy * inv_radius);
   if (!(mcc > 0.0)) return false;
   s.mcc = mcc;
 #pragma unroll
-  for (int k = 0; k < 6; ++k) delta[k] = y[k] * sc[k];
+  for (int k = 0; k < 6; ++k) delta[k] = -y[k] * sc[k];
   return true;
 }
 
