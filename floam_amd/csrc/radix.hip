@@ -83,18 +83,17 @@ __global__ __launch_bounds__(kTB) void radix_pass(const uint32_t* __restrict__ k
     val[r] = PAYLOAD ? i : (i < n ? vin[i] : 0);
     dig[r] = digs ? (i < n ? (unsigned)digs[i] : 0u) : (key[r] >> (8 * pass)) & 255u;
   }
-  // (as two native 4-int vectors: an array of PointRec or of HIP's int4 — structs — stayed a private array, 272 B /
-  // lane of scratch whose traffic the pass's HBM counters showed; native vectors are promoted to VGPRs)
-  v4i rlo[PAYLOAD ? kItems : 1], rhi[PAYLOAD ? kItems : 1];
+  // PAYLOAD: the tile's records into LDS in input order as 16-B chunks, thread t chunk t + 256 k (every load
+  // instruction covers whole contiguous lines once; a lane loading both halves of its own record made each 128-B line
+  // two requests of two instructions); the scatter reads them back by input position
+  __shared__ v4i s_nat[PAYLOAD ? 2 * kTile : 1];
   if (PAYLOAD) {
+    const v4i* q = reinterpret_cast<const v4i*>(pin + (size_t)tile * kTile);
+    const int nchunk = 2 * (min(n, (tile + 1) * kTile) - tile * kTile);   // (host bound: allocated)
 #pragma unroll
-    for (int r = 0; r < kItems; ++r) {
-      const int i = base + r * 64 + lane;
-      if (i < n) {
-        const v4i* q = reinterpret_cast<const v4i*>(pin + i);
-        rlo[r] = q[0];
-        rhi[r] = q[1];
-      }
+    for (int k = 0; k < 2 * kItems; ++k) {
+      const int c = t + k * kTB;
+      if (c < nchunk) s_nat[c] = q[c];
     }
   }
   if (!gv) return;
@@ -208,15 +207,14 @@ __global__ __launch_bounds__(kTB) void radix_pass(const uint32_t* __restrict__ k
   const unsigned long long ts2 = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
   // 4. scatter
   if (PAYLOAD) {   // keys / values as below; the records through LDS in tile-sorted order, then written as runs
-    __shared__ v4i s_rec[PAYLOAD ? kTile : 1][2];
+    __shared__ unsigned short s_src[PAYLOAD ? kTile : 1];   // input position in the tile, by tile-sorted slot
     __shared__ unsigned char s_dig[PAYLOAD ? kTile : 1];
 #pragma unroll
     for (int r = 0; r < kItems; ++r) {
       if (base + r * 64 + lane < n) {
         const unsigned d = dig[r];
         const unsigned loc = s_tstart[d] + s_wcnt[w][d] + rank[r];
-        s_rec[loc][0] = rlo[r];
-        s_rec[loc][1] = rhi[r];
+        s_src[loc] = (unsigned short)(w * 64 * kItems + r * 64 + lane);
         s_dig[loc] = (unsigned char)d;
         if (kout) {
           const unsigned dst = s_off[d] + s_wcnt[w][d] + rank[r];
@@ -230,7 +228,8 @@ __global__ __launch_bounds__(kTB) void radix_pass(const uint32_t* __restrict__ k
     for (int j = t; j < nloc; j += kTB) {   // consecutive j of one digit land on consecutive slots
       const unsigned d = s_dig[j];
       const unsigned dst = s_off[d] + ((unsigned)j - s_tstart[d]);
-      const v4i lo = s_rec[j][0], hi = s_rec[j][1];
+      const int src = s_src[j];
+      const v4i lo = s_nat[2 * src], hi = s_nat[2 * src + 1];
       v4i* o = reinterpret_cast<v4i*>(prec + dst);
       o[0] = lo;
       o[1] = hi;
