@@ -586,18 +586,24 @@ __device__ __forceinline__ void next_step_wave(LMState& s, bool check_gmax, int 
     CTRL_T(tc);
     CTRL_ADD(2, tb - ta);
     CTRL_ADD(3, tc - tb);
+    // (wave-uniform) lane 1 computed the projection: the lanes' outputs differ and lane 0's is broadcast; otherwise
+    // every lane holds the candidate already (no read-lanes on the common path)
+    const bool proj = check_gmax && !far;
     if (check_gmax) {
-      double m = 0.0;
+      double m = HUGE_VAL;   // (far: the test fails; only the comparison with the tolerance is used)
+      if (proj) {
+        m = 0.0;
 #pragma unroll
-      for (int i = 0; i < 7; ++i) m = fmax(m, fabs(s.x[i] - bcast(out[i], 1)));
-      s.gmax = far ? HUGE_VAL : m;   // (only its comparison with the tolerance is used)
+        for (int i = 0; i < 7; ++i) m = fmax(m, fabs(s.x[i] - bcast(out[i], 1)));
+      }
+      s.gmax = m;
       check_gmax = false;
       if (s.gmax <= 1e-10) { s.done = 1; return; }   // (phase 0: before any step; phase 1: success && gmax)
     }
     s.iteration++;
     if (valid) {
 #pragma unroll
-      for (int i = 0; i < 7; ++i) s.cand[i] = bcast(out[i], 0);
+      for (int i = 0; i < 7; ++i) s.cand[i] = proj ? bcast(out[i], 0) : out[i];
       s.invalid = 0;
       CTRL_T(td);
       CTRL_ADD(4, td - tc);
@@ -647,17 +653,20 @@ __device__ __forceinline__ void lm_logic(LMState& s, const double (&sums)[LM_NSU
   } else {
     double cand_cost = sums[0];
     if (!isfinite(cand_cost)) cand_cost = DBL_MAX;
-    // ParameterToleranceReached (candidate not applied)
-    double sn = 0.0;
+    // ParameterToleranceReached (candidate not applied): |x - cand| <= 1e-8 (|x| + 1e-8), compared squared (both
+    // sides are non-negative: no square root on the step's dependent chain)
+    double sn2 = 0.0;
 #pragma unroll
-    for (int i = 0; i < 7; ++i) sn += (s.x[i] - s.cand[i]) * (s.x[i] - s.cand[i]);
-    sn = sqrt(sn);
-    if (sn <= 1e-8 * (s.x_norm + 1e-8)) { s.done = 1; return; }
+    for (int i = 0; i < 7; ++i) sn2 += (s.x[i] - s.cand[i]) * (s.x[i] - s.cand[i]);
+    const double ptol = 1e-8 * (s.x_norm + 1e-8);
+    if (sn2 <= ptol * ptol) { s.done = 1; return; }
     // FunctionToleranceReached
     if (fabs(s.x_cost - cand_cost) <= 1e-6 * s.x_cost) { s.done = 1; return; }
-    const double rho = (s.x_cost - cand_cost) * recip(s.mcc);   // (mcc > 0; within an ulp of the division)
-    check_gmax = rho > 1e-3;   // (success)
+    // rho = decrease / mcc > 1e-3 decided without the reciprocal (mcc > 0); rho itself only for the radius update
+    const double dec = s.x_cost - cand_cost;
+    check_gmax = dec > 1e-3 * s.mcc;   // (success)
     if (check_gmax) {
+      const double rho = dec * recip(s.mcc);   // (within an ulp of the division)
 #pragma unroll
       for (int i = 0; i < 7; ++i) s.x[i] = s.cand[i];
       s.x_norm = norm7(s.x);
