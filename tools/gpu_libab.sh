@@ -18,6 +18,7 @@ for round in 1 2; do
     python -c "import json; d=json.load(open('$OUT/b_${v}_$round.json')); r=d['roofline']; print('$v', '$round', d['value'], 'knn', r['avg_us'], 'knn+geom', r['knn_geometry_avg_us'], 'lm', r['lm_solve_avg_us'])"
   done
 done
+[ -n "$NO_TRACE" ] && { echo done; exit 0; }
 for v in tree "$@"; do
   use $v
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/tr_$v -o run -- \
