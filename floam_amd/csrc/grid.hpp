@@ -29,6 +29,18 @@ __device__ __forceinline__ unsigned hash_slot64(unsigned long long key, int bits
   return (unsigned)((key * 0x9E3779B97F4A7C15ull) >> (64 - bits));
 }
 
+// Initial slot of a coarse cell in the open-addressing table: the 2x2x2 block of coarse cells that holds it (its
+// "super-cell", coordinates halved) picks a bucket of 8 consecutive entries (512 B: 4 cache lines) and the cell's
+// position in the block picks the entry, so the 8 coarse cells a query's fine block spans sit in 1 to 8 buckets and
+// neighbouring cells share lines, where a hash per cell put every probe on a line of its own (profiles/r04l: a third
+// of the search's reads).  Collisions still probe linearly (+1), so every insert and lookup terminates as before.
+__device__ __forceinline__ unsigned coarse_slot(unsigned long long key, int bits) {
+  const int x = (int)(key & 0x1FFFFFull) - (1 << 20), y = (int)((key >> 21) & 0x1FFFFFull) - (1 << 20),
+            z = (int)(key >> 42) - (1 << 20);
+  const unsigned sub = (unsigned)((x & 1) | ((y & 1) << 1) | ((z & 1) << 2));
+  return (hash_slot64(cell_key(x >> 1, y >> 1, z >> 1), bits - 3) << 3) | sub;
+}
+
 constexpr double kFineCell = 0.5;
 
 struct alignas(64) CoarseCell {   // 64 B, one per half cache line: a probe never straddles two lines
@@ -104,7 +116,7 @@ __device__ __forceinline__ void grid_count_points(const GridCountDev& J, const i
     leader[r] = valid[r] ? __ffsll((long long)my_grp[r]) - 1 : lane;
     ins[r] = valid[r] && leader[r] == lane;
     fresh[r] = false;
-    h[r] = ins[r] ? hash_slot64(key[r], J.bits) : 0u;
+    h[r] = ins[r] ? coarse_slot(key[r], J.bits) : 0u;
   }
   // the leaders' inserts: every round's probe issued together, until each found its cell or an empty slot
   for (;;) {

@@ -373,7 +373,7 @@ constexpr int kUnrollDefault = 2;   // candidate loads in flight per lane (U; 2 
 template <typename Cell>
 __device__ __forceinline__ int2 grid_lookup(const Cell* __restrict__ tab, unsigned long long key, int bits,
                                             unsigned mask) {
-  unsigned h = hash_slot64(key, bits);
+  unsigned h = coarse_slot(key, bits);
   for (;;) {
     const int4 e = *reinterpret_cast<const int4*>(&tab[h]);
     const unsigned long long k = ((unsigned long long)(unsigned)e.y << 32) | (unsigned)e.x;
@@ -470,7 +470,7 @@ struct CorrArgs {
 
 __device__ __forceinline__ int fine_count(const CorrArgs& A, int fx, int fy, int fz) {
   const unsigned long long key = cell_key(fx >> 1, fy >> 1, fz >> 1);
-  unsigned h = hash_slot64(key, A.bits);
+  unsigned h = coarse_slot(key, A.bits);
   for (;;) {
     const CoarseCell& c = A.coarse[h];
     if (c.key == key) return c.sub[(fx & 1) | ((fy & 1) << 1) | ((fz & 1) << 2)];
@@ -509,7 +509,7 @@ __device__ __forceinline__ void fine_block_ranges(const CorrArgs& A, int lx, int
   }
   if (lane < 8 && need) {
     const unsigned long long key = cell_key(cx0 + (lane & 1), cy0 + ((lane >> 1) & 1), cz0 + (lane >> 2));
-    unsigned slot = hash_slot64(key, A.bits);
+    unsigned slot = coarse_slot(key, A.bits);
     const int4* e = reinterpret_cast<const int4*>(&A.coarse[slot]);
     int4 h = e[0], s0 = e[1], s1 = e[2];
     unsigned long long k = ((unsigned long long)(unsigned)h.y << 32) | (unsigned)h.x;
@@ -583,7 +583,7 @@ __device__ __forceinline__ void stencil_scan(const CorrArgs& A, int x0, int x1, 
     e[j] = make_int4(-1, -1, 0, 0);
     if (c < ce) {
       key[j] = cell_key(x0 + c % nxr, y0 + (c / nxr) % nyr, z0 + c / (nxr * nyr));
-      slot[j] = hash_slot64(key[j], A.bits);
+      slot[j] = coarse_slot(key[j], A.bits);
       e[j] = *reinterpret_cast<const int4*>(&A.coarse[slot[j]]);
     }
   }
@@ -1114,7 +1114,7 @@ __device__ double stage2_radius(const CorrArgs& A, int nb, float wx, float wy, f
     for (int fy = ly; fy < ly + nb; ++fy)
       for (int fx = lx; fx < lx + nb; ++fx) {
         const unsigned long long key = cell_key(fx >> 1, fy >> 1, fz >> 1);
-        unsigned h = hash_slot64(key, A.bits);
+        unsigned h = coarse_slot(key, A.bits);
         while (A.coarse[h].key != key && A.coarse[h].key != kEmptyKey) h = (h + 1) & A.mask;
         const CoarseCell& c = A.coarse[h];
         if (c.key != key) continue;
