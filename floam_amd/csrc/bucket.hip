@@ -441,6 +441,10 @@ __device__ __forceinline__ void block_sum2(int (&c)[2], unsigned (*hw)[kW]) {
   __syncthreads();
 }
 
+// FLOAM_BC_STAMPS=1 (diagnostic): per-bucket phase times of the last two bucket_compact launches (slot = launch
+// parity: call 1's VoxelGrids on the side stream, then call 2's on the main stream), printed by bucket_stamps_print
+__device__ unsigned g_bc_st[2][kBuckets][5];
+
 __global__ __launch_bounds__(kTB) void bucket_compact(VoxelJobDev A, VoxelJobDev B, uint32_t* __restrict__ kin,
                                                       int* __restrict__ vin, uint32_t* __restrict__ kout,
                                                       int* __restrict__ vout, const unsigned* __restrict__ hist,
@@ -449,7 +453,9 @@ __global__ __launch_bounds__(kTB) void bucket_compact(VoxelJobDev A, VoxelJobDev
                                                       const unsigned* __restrict__ radix_ctl,
                                                       const int* __restrict__ gate,
                                                       unsigned long long* __restrict__ split,
-                                                      const int* __restrict__ geo, unsigned* __restrict__ ticket) {
+                                                      const int* __restrict__ geo, unsigned* __restrict__ ticket,
+                                                      int stamps) {
+  const unsigned long long T0 = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   // the bucket is the block's ticket (zeroed by vox_keys): a bucket's lookback only waits on buckets that are already
   // running (HIP promises no dispatch order).  Prologue loads together with it: gate, the clouds' counts, the
@@ -497,6 +503,7 @@ __global__ __launch_bounds__(kTB) void bucket_compact(VoxelJobDev A, VoxelJobDev
       bucket_bitonic<E>(kin + start, vin + start, size, L.u.x, L.k, L.v);
     });
   }
+  const unsigned long long T1 = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
   // the bucket's heads per cloud -> its output range (lookback over the buckets)
   int hc[2];
   if (!streamed) {
@@ -513,8 +520,10 @@ __global__ __launch_bounds__(kTB) void bucket_compact(VoxelJobDev A, VoxelJobDev
     }
   }
   block_sum2(hc, L.hw);
+  const unsigned long long T2 = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
   const Prefix2 pre = lookback_prefix(status, b, Prefix2{hc[0], hc[1]});
   if (pre.a < 0) return;   // (timed out, never expected: bucket 255 reports it)
+  const unsigned long long T3 = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
   if (streamed) write_splitters(split, geo, R.kept, start, size, [&](int q) { return kout[start + q]; });
   else write_splitters(split, geo, R.kept, start, size, [&](int q) { return L.k[q]; });
   int run_base[2] = {pre.a, pre.b};   // output slot of the next head, per cloud
@@ -633,6 +642,15 @@ __global__ __launch_bounds__(kTB) void bucket_compact(VoxelJobDev A, VoxelJobDev
   __syncthreads();
   if (t == 0 && L.carry_pos >= 0)   // (a streamed bucket whose last run reached its end)
     (L.carry_job ? B : A).out[L.carry_pos] = centroid_out(L.carry[0], L.carry[1], L.carry[2], L.carry[3], L.carry_n);
+  if (stamps) {   // plain per-bucket records (start, sort, heads + sum, lookback, gather + emit + drain)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) {
+      unsigned* q = g_bc_st[stamps - 1][b];
+      q[0] = (unsigned)T0; q[1] = (unsigned)(T1 - T0); q[2] = (unsigned)(T2 - T1); q[3] = (unsigned)(T3 - T2);
+      q[4] = (unsigned)(__builtin_amdgcn_s_memrealtime() - T3);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------------------- seeding
@@ -686,9 +704,43 @@ void bucket_voxel_launch(BucketScratch& bs, RadixScratch& rs, const VoxelJobDev&
   bs.reserve(n, st);
   rs.reserve(n, st);
   radix_digit_pass_launch(rs, k0, v0, k1, v1, n, bs.bkt.p, st, gate, n_dev);
+  static const bool stamps = std::getenv("FLOAM_BC_STAMPS") != nullptr;
+  static unsigned launches = 0;
   hipLaunchKernelGGL(bucket_compact, dim3(kBuckets), dim3(kTB), 0, st, A, B, k1, v1, k0, v0, rs.ctl.p, overflow,
-                     status, rs.ctl.p, gate, bs.split.p, bs.geo.p, tile_by_index() ? nullptr : ticket);
+                     status, rs.ctl.p, gate, bs.split.p, bs.geo.p, tile_by_index() ? nullptr : ticket,
+                     stamps ? (int)(launches++ & 1u) + 1 : 0);
   FLOAM_LAUNCH_CHECK();
+}
+
+void bucket_stamps_print() {
+  if (!std::getenv("FLOAM_BC_STAMPS")) return;
+  static unsigned q[2][kBuckets][5];
+  FLOAM_HIP(hipDeviceSynchronize());
+  FLOAM_HIP(hipMemcpyFromSymbol(q, HIP_SYMBOL(g_bc_st), sizeof(q)));
+  for (int sl = 0; sl < 2; ++sl) {
+    int nb = 0, smin = 0, emax = 0, worst = 0, worst_end = 0;
+    double ph[4] = {0, 0, 0, 0}, mx[4] = {0, 0, 0, 0};
+    for (int b = 0; b < kBuckets; ++b) {
+      if (q[sl][b][1] == 0 && q[sl][b][4] == 0) continue;
+      ++nb;
+      for (int k = 0; k < 4; ++k) {
+        ph[k] += q[sl][b][1 + k];
+        mx[k] = std::max(mx[k], (double)q[sl][b][1 + k]);
+      }
+      const int st = (int)(q[sl][b][0] - q[sl][0][0]);
+      const int end = st + (int)(q[sl][b][1] + q[sl][b][2] + q[sl][b][3] + q[sl][b][4]);
+      smin = std::min(smin, st);
+      if (end > emax) { emax = end; worst = b; worst_end = end; }
+    }
+    if (!nb) continue;
+    std::fprintf(stderr, "[bc stamps] launch slot %d (%s), %d buckets: sort %.2f (max %.2f), heads + sum %.2f (max "
+                 "%.2f), lookback %.2f (max %.2f), gather + emit + drain %.2f (max %.2f) us; first start -> last end "
+                 "%.2f us (bucket %d: start +%.2f)\n", sl, sl ? "call 2, main stream" : "call 1, side stream", nb,
+                 ph[0] / nb / 100.0, mx[0] / 100.0, ph[1] / nb / 100.0, mx[1] / 100.0, ph[2] / nb / 100.0, mx[2] / 100.0,
+                 ph[3] / nb / 100.0, mx[3] / 100.0, (emax - smin) / 100.0, worst,
+                 (int)(q[sl][worst][0] - q[sl][0][0]) / 100.0);
+    (void)worst_end;
+  }
 }
 
 void bucket_sort_launch(BucketScratch& bs, RadixScratch& rs, uint32_t* k0, int* v0, uint32_t* k1, int* v1, int n,

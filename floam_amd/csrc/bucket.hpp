@@ -100,4 +100,6 @@ void bucket_seed_launch(BucketScratch& bs, const uint32_t* k0, const int* n_dev,
 // (read once per process; default bucket: both pipelines)
 bool bucket_sort_enabled(int pipeline);
 
+void bucket_stamps_print();   // FLOAM_BC_STAMPS (diagnostic)
+
 }  // namespace floam
