@@ -271,13 +271,21 @@ __device__ __forceinline__ unsigned long long mv_idx(const MergeView& V, float x
 // One job's tile (the kernel below calls it with the job's own kernel arguments: selecting the argument structs by a
 // run-time job index made the compiler copy both into scratch and load every field from there — 144-176 B / lane of
 // private memory traffic per launch)
+// FLOAM_MM_STAMPS=1 (diagnostic): per-tile phase times of the last merge (start, split, LDS merge, runs, lookback,
+// stores), printed by mm_stamps_print
+constexpr int kMmStampTiles = 512;
+__device__ unsigned g_mm_st[2][kMmStampTiles][6];
+__device__ __forceinline__ unsigned long long mm_now(int on) { return on ? __builtin_amdgcn_s_memrealtime() : 0ull; }
+
 template <int PER>
 __device__ __forceinline__ void mm_merge_job(const VoxelJobDev& JJ, const MapKeys& KK, const GridCountDev& G, int job,
                                              const uint32_t* __restrict__ skeys, const int* __restrict__ svals,
                                              int* __restrict__ ctl, unsigned long long* __restrict__ mstatus,
                                              int tiles_cap, int tilesA,
                                              const unsigned* __restrict__ radix_ctl, const int* __restrict__ gate,
-                                             unsigned seq, int violate_mod, int count_grid, int by_index) {
+                                             unsigned seq, int violate_mod, int count_grid, int by_index,
+                                             int stamps) {
+  const unsigned long long T0 = mm_now(stamps);
   // the tile within the job is the block's ticket (ctl[kMergeTicketWord + 32 job], zeroed by the status gather): a
   // tile's lookback only waits on tiles that are already running (HIP promises no dispatch order)
   __shared__ int s_tile;
@@ -343,6 +351,7 @@ __device__ __forceinline__ void mm_merge_job(const VoxelJobDev& JJ, const MapKey
   __shared__ unsigned char s_live[(PER * kTB)];
   __shared__ int s_split[2], s_first[2], s_open[2];
   __shared__ int s_has_cross;   // a run of this tile continues past it (finished cooperatively below)
+  unsigned long long T1 = 0ull;
   int j1 = d1;       // first set element after the tile (sorted order)
   int i1m = V.n0;    // first map element after the tile (the merge path; none on the full path: the map is in the set)
   if (t == 0) s_has_cross = 0;
@@ -372,6 +381,7 @@ __device__ __forceinline__ void mm_merge_job(const VoxelJobDev& JJ, const MapKey
       j1 = d1 - i1;
       i1m = i1;
     }
+    T1 = mm_now(stamps);
     const int na = i1 - i0, nb = j1 - j0;
     // the two runs' indices in LDS (points, sources, kept flags stay in registers: element k = t + r kTB)
     __shared__ unsigned long long s_ak[(PER * kTB)], s_bk[(PER * kTB)];
@@ -450,6 +460,7 @@ __device__ __forceinline__ void mm_merge_job(const VoxelJobDev& JJ, const MapKey
     }
   }
   __syncthreads();
+  const unsigned long long T2 = mm_now(stamps);
   // runs: element k heads a run when its key differs from the previous element's; a run is output when one of its
   // elements is kept (a cropped map point takes part in the order only); its centroid sums the kept points in merged
   // order.  A run that continues past the tile is finished by the whole block: its continuation is the merged
@@ -556,6 +567,7 @@ __device__ __forceinline__ void mm_merge_job(const VoxelJobDev& JJ, const MapKey
       else cross_u = -1;            // only cropped map points: no output (as a run inside a tile)
     }
   }
+  const unsigned long long T3 = mm_now(stamps);
   if (t == 0) s_cross_local = -1;
   // the tile's output order: block exclusive scan of the per-thread counts
   __shared__ int s_w[kTB / 64];
@@ -607,6 +619,7 @@ __device__ __forceinline__ void mm_merge_job(const VoxelJobDev& JJ, const MapKey
     if (t == 0) *V.J.d_out = -1;
     return;
   }
+  const unsigned long long T4 = mm_now(stamps);
   if (violate_mod > 0 && seq % (unsigned)violate_mod == 0) bad = true;   // (test knob: exercise the fallback)
   if (__syncthreads_or(bad) && t == 0) V.K.meta_out->violation = seq;
   int gi[PER];
@@ -636,6 +649,15 @@ __device__ __forceinline__ void mm_merge_job(const VoxelJobDev& JJ, const MapKey
   }
   // the next kNN grid's per-point step (grid_count_job) for the map's points pre.a + k, all rounds at once
   if (count_grid) grid_count_points<PER>(G, gi, gv, gx, gy, gz);
+  if (stamps && tile < kMmStampTiles) {   // plain per-tile records
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) {
+      unsigned* q = g_mm_st[job][tile];
+      q[0] = (unsigned)T0; q[1] = (unsigned)(T1 ? T1 - T0 : 0ull); q[2] = (unsigned)(T2 - (T1 ? T1 : T0));
+      q[3] = (unsigned)(T3 - T2); q[4] = (unsigned)(T4 - T3); q[5] = (unsigned)(mm_now(1) - T4);
+    }
+  }
   if (tile == ntiles - 1 && t == 0) {
     const bool sort_failed = radix_ctl[kRadixErrorWord] != 0u;   // a sort lookback timed out (never expected)
     *V.J.d_out = sort_failed ? -1 : pre.a + nloc;
@@ -651,13 +673,13 @@ __global__ __launch_bounds__(kTB) void mm_merge(VoxelJobDev A, VoxelJobDev B, Ma
                                                 int tiles_cap, int tilesA,
                                                 const unsigned* __restrict__ radix_ctl, const int* __restrict__ gate,
                                                 unsigned seq, int violate_mod, GridCountDev GA, GridCountDev GB,
-                                                int count_grid, int by_index) {
+                                                int count_grid, int by_index, int stamps) {
   if ((int)blockIdx.x < tilesA)   // (block-uniform)
     mm_merge_job<PER>(A, KA, GA, 0, skeys, svals, ctl, mstatus, tiles_cap, tilesA, radix_ctl, gate, seq, violate_mod,
-                      count_grid, by_index);
+                      count_grid, by_index, stamps);
   else
     mm_merge_job<PER>(B, KB, GB, 1, skeys, svals, ctl, mstatus, tiles_cap, tilesA, radix_ctl, gate, seq, violate_mod,
-                      count_grid, by_index);
+                      count_grid, by_index, stamps);
 }
 
 }  // namespace
@@ -682,6 +704,38 @@ MergeCheck merge_check(MapMergeScratch& ms, unsigned seq) {
   mc.ctl = ms.ctl.p;
   mc.seq = seq;
   return mc;
+}
+
+void mm_stamps_print() {
+  if (!std::getenv("FLOAM_MM_STAMPS")) return;
+  static unsigned q[2][kMmStampTiles][6];
+  FLOAM_HIP(hipDeviceSynchronize());
+  FLOAM_HIP(hipMemcpyFromSymbol(q, HIP_SYMBOL(g_mm_st), sizeof(q)));
+  const unsigned t00 = q[0][0][0];
+  int nt = 0, smin = 0, smax = 0, emax = 0;
+  double ph[5] = {0, 0, 0, 0, 0}, mx[5] = {0, 0, 0, 0, 0};
+  for (int j = 0; j < 2; ++j)
+    for (int t = 0; t < kMmStampTiles; ++t) {
+      const unsigned* r = q[j][t];
+      if (r[0] == 0) continue;
+      ++nt;
+      int len = 0;
+      for (int k = 0; k < 5; ++k) {
+        ph[k] += r[1 + k];
+        mx[k] = std::max(mx[k], (double)r[1 + k]);
+        len += (int)r[1 + k];
+      }
+      const int st = (int)(r[0] - t00);
+      smin = std::min(smin, st);
+      smax = std::max(smax, st);
+      emax = std::max(emax, st + len);
+    }
+  if (!nt) return;
+  std::fprintf(stderr, "[mm stamps] last merge, %d tiles: split %.2f (max %.2f), LDS merge %.2f (max %.2f), runs %.2f "
+               "(max %.2f), lookback %.2f (max %.2f), stores %.2f (max %.2f) us; tile starts spread %.2f us; first start "
+               "-> last end %.2f us\n", nt, ph[0] / nt / 100.0, mx[0] / 100.0, ph[1] / nt / 100.0, mx[1] / 100.0,
+               ph[2] / nt / 100.0, mx[2] / 100.0, ph[3] / nt / 100.0, mx[3] / 100.0, ph[4] / nt / 100.0, mx[4] / 100.0,
+               (smax - smin) / 100.0, (emax - smin) / 100.0);
 }
 
 void map_merge_launch(VoxelScratch2& vs, MapMergeScratch& ms, const VoxelJob& a, const VoxelJob& b, const MapKeys& ka,
@@ -720,17 +774,18 @@ void map_merge_launch(VoxelScratch2& vs, MapMergeScratch& ms, const VoxelJob& a,
     if (bucket) bucket_seed_launch(ms.bs, vs.s.k0.p, vs.overflow.p + 2, n, st, gate);
   }
   const bool wb = prof_wb_enabled();   // (diagnostic: the merge's own write bytes, profwb.hpp)
+  static const int stamps = std::getenv("FLOAM_MM_STAMPS") ? 1 : 0;
   if (wb) prof_l2_writeback(st);
   if (per == 2)
     hipLaunchKernelGGL(mm_merge<2>, dim3(tilesA + tilesB), dim3(kTB), 0, st, A, B, ka, kb, vs.s.k0.p, vs.s.v0.p,
                        ms.ctl.p, ms.status.p, ms.tiles_cap, tilesA, vs.rs.ctl.p, gate, seq, violate_mod,
                        grids ? grids[0] : GridCountDev{}, grids ? grids[1] : GridCountDev{}, grids ? 1 : 0,
-                       tile_by_index() ? 1 : 0);
+                       tile_by_index() ? 1 : 0, stamps);
   else
     hipLaunchKernelGGL(mm_merge<4>, dim3(tilesA + tilesB), dim3(kTB), 0, st, A, B, ka, kb, vs.s.k0.p, vs.s.v0.p,
                        ms.ctl.p, ms.status.p, ms.tiles_cap, tilesA, vs.rs.ctl.p, gate, seq, violate_mod,
                        grids ? grids[0] : GridCountDev{}, grids ? grids[1] : GridCountDev{}, grids ? 1 : 0,
-                       tile_by_index() ? 1 : 0);
+                       tile_by_index() ? 1 : 0, stamps);
   FLOAM_LAUNCH_CHECK();
   if (wb) prof_l2_writeback(st);
 }

@@ -55,4 +55,6 @@ void map_merge_launch(VoxelScratch2& vs, MapMergeScratch& ms, const VoxelJob& a,
                       const MapKeys& kb, const int* gate, unsigned seq, bool force_full, int violate_mod,
                       const GridCountDev* grids, hipStream_t st, int per = 4);
 
+void mm_stamps_print();   // FLOAM_MM_STAMPS (diagnostic)
+
 }  // namespace floam
