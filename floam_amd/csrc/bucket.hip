@@ -464,7 +464,7 @@ __global__ __launch_bounds__(kTB) void bucket_compact(VoxelJobDev A, VoxelJobDev
   if (t == 0) s_b = ticket ? (int)atomicAdd(ticket, 1u) : (int)blockIdx.x;   // (null: by index, A/B only)
   const int gv = gate ? *gate : 1;
   const int nA0 = *A.d_n0, nA1 = A.d_n1 ? *A.d_n1 : 0, nB0 = *B.d_n0, nB1 = B.d_n1 ? *B.d_n1 : 0;
-  const int ovf[2] = {overflow[0], overflow[1]};
+  const int ovf0 = overflow[0], ovf1 = overflow[1];   // (no two-element arrays indexed by a run-time job: scratch)
   __syncthreads();
   const int b = s_b;
   if (!gv) {   // gated off (no keyframe): the output is the unchanged first part (the map).  By block index: no
@@ -592,6 +592,7 @@ __global__ __launch_bounds__(kTB) void bucket_compact(VoxelJobDev A, VoxelJobDev
       }
     pos[0] += inc[0] - c[0];
     pos[1] += inc[1] - c[1];
+    int pos0 = pos[0], pos1 = pos[1];   // the next output slot per cloud (selected by job below, never indexed)
     int e0, e1;
     thread_range(nc, e0, e1);
     for (int e = e0; e < e1; ++e) {
@@ -600,10 +601,12 @@ __global__ __launch_bounds__(kTB) void bucket_compact(VoxelJobDev A, VoxelJobDev
       if (!((e == 0 && c0 == 0) || key != kp)) continue;
       const int job = (int)(key >> 31);
       const VoxelJobDev& J = job ? B : A;
-      if (ovf[job]) {   // index overflow: the input returned unchanged (Q9; identity keys: runs of one)
+      const int slot = job ? pos1 : pos0;
+      if (job) ++pos1; else ++pos0;
+      if (job ? ovf1 : ovf0) {   // index overflow: the input returned unchanged (Q9; identity keys: runs of one)
         PointRec o;
         vox_fetch(J, job ? nB0 : nA0, job ? nB1 : nA1, L.v[e], o);
-        J.out[pos[job]++] = o;
+        J.out[slot] = o;
         continue;
       }
       const float4 f = L.u.pt[e];
@@ -627,12 +630,12 @@ __global__ __launch_bounds__(kTB) void bucket_compact(VoxelJobDev A, VoxelJobDev
       if (j == nc && streamed && c0 + nc < size) {   // reaches the chunk end of a streamed bucket: carried over
         L.carry[0] = s0; L.carry[1] = s1; L.carry[2] = s2; L.carry[3] = s3;
         L.carry_n = j - e;
-        L.carry_pos = pos[job]++;
+        L.carry_pos = slot;
         L.carry_job = job;
         L.carry_key = key;
         continue;
       }
-      J.out[pos[job]++] = centroid_out(s0, s1, s2, s3, j - e);
+      J.out[slot] = centroid_out(s0, s1, s2, s3, j - e);
     }
     run_base[0] += tot[0];
     run_base[1] += tot[1];

@@ -67,6 +67,20 @@ __host__ __device__ inline Mat3 quat_to_mat(const double q[4]) {
   r.m[2][0] = txz - twy; r.m[2][1] = tyz + twx; r.m[2][2] = 1 - (txx + tyy);
   return r;
 }
+// Shepperd's branch for the largest diagonal entry I (compile-time indices: a run-time index into the matrix made the
+// device compiler keep it in scratch, 104 B per lane in every kernel that forms a pose)
+template <int I>
+__host__ __device__ inline void mat_to_quat_branch(const Mat3& a, double q[4]) {
+  constexpr int J = (I + 1) % 3, K = (J + 1) % 3;
+  double t = sqrt(a.m[I][I] - a.m[J][J] - a.m[K][K] + 1.0);
+  double c[3];
+  c[I] = 0.5 * t;
+  t = 0.5 / t;
+  q[3] = (a.m[K][J] - a.m[J][K]) * t;
+  c[J] = (a.m[J][I] + a.m[I][J]) * t;
+  c[K] = (a.m[K][I] + a.m[I][K]) * t;
+  q[0] = c[0]; q[1] = c[1]; q[2] = c[2];
+}
 // Rotation matrix -> quaternion (x, y, z, w) (Eigen quaternionbase_assign_impl, Shepperd's method)
 __host__ __device__ inline void mat_to_quat(const Mat3& a, double q[4]) {
   double t = a.m[0][0] + a.m[1][1] + a.m[2][2];
@@ -80,16 +94,10 @@ __host__ __device__ inline void mat_to_quat(const Mat3& a, double q[4]) {
   } else {
     int i = 0;
     if (a.m[1][1] > a.m[0][0]) i = 1;
-    if (a.m[2][2] > a.m[i][i]) i = 2;
-    const int j = (i + 1) % 3, k = (j + 1) % 3;
-    t = sqrt(a.m[i][i] - a.m[j][j] - a.m[k][k] + 1.0);
-    double c[3];
-    c[i] = 0.5 * t;
-    t = 0.5 / t;
-    q[3] = (a.m[k][j] - a.m[j][k]) * t;
-    c[j] = (a.m[j][i] + a.m[i][j]) * t;
-    c[k] = (a.m[k][i] + a.m[i][k]) * t;
-    q[0] = c[0]; q[1] = c[1]; q[2] = c[2];
+    if (a.m[2][2] > (i == 0 ? a.m[0][0] : a.m[1][1])) i = 2;
+    if (i == 0) mat_to_quat_branch<0>(a, q);
+    else if (i == 1) mat_to_quat_branch<1>(a, q);
+    else mat_to_quat_branch<2>(a, q);
   }
 }
 // Eigen::AngleAxisd(R).angle()
