@@ -815,8 +815,12 @@ __device__ __forceinline__ bool sweep_granules(const unsigned long long* __restr
 
 // evaluation blocks that hold records: one record slot per record thread while they fit, at most nblk (a function of
 // the device count only, so the partition and the reduction order never depend on the host's upper bounds)
+// (rpt: records per record thread before another block is taken — 1 by default; FLOAM_LM_RPT=2 halves the active
+// blocks, A/B)
 template <int NR>
-__device__ __forceinline__ int active_blocks(int total, int nblk) { return max(1, min(nblk, (total + NR - 1) / NR)); }
+__device__ __forceinline__ int active_blocks(int total, int nblk, int rpt) {
+  return max(1, min(nblk, (total + NR * rpt - 1) / (NR * rpt)));
+}
 
 // record threads of a solve block: GRAM — waves 0..2 hold edge records and wave 3 forms the surf half from G;
 // otherwise every thread holds records
@@ -848,6 +852,7 @@ struct LMArgs {
   int world;
   unsigned long long* xme;
   const unsigned long long* xpeer[kMaxShardRanks];
+  int rpt;                         // records per record thread before another block is taken (active_blocks)
 };
 
 // Peer sharding: after a block has its rank's 29 sums (block partials + the surf half), block 0 publishes them as
@@ -958,7 +963,7 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
   }
   const int ne = min(ne_dev, a.ne_ub);
   const int total = ne + (GRAM ? 0 : min(ns_dev, a.ns_ub));
-  const int nact = active_blocks<NR>(total, nblk);
+  const int nact = active_blocks<NR>(total, nblk, a.rpt);
   if (blk >= nact) return;   // no records: nobody waits for this block
   if (tid < kStateWords) reinterpret_cast<unsigned*>(&sst)[tid] = sw;
   const int stride = nact * NR;
@@ -1122,7 +1127,7 @@ __global__ __launch_bounds__(kTB) void lm_shard_eval(LMArgs a, int k) {
   const bool done = s_done != 0;
   const int ne = min(*a.d_ne, a.ne_ub);
   const int total = ne + (GRAM ? 0 : min(*a.d_ns, a.ns_ub));
-  const int nact = active_blocks<NR>(total, nblk);
+  const int nact = active_blocks<NR>(total, nblk, a.rpt);
   if (!done && blk < nact) {   // block-uniform
     double acc[LM_NSUM];
     if (tid < NR) {
@@ -1213,7 +1218,12 @@ LMArgs make_args(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, c
                  int ns_ub, LMBuffers& b, unsigned long long* dbg, bool pre0 = false, const ShardPeers* peers = nullptr) {
   LMArgs a{d_st, ce.rec.p, ce.valid.p, ce.cap, d_ne, std::max(ne_ub, 0), cs.rec.p, cs.valid.p, cs.cap, d_ns,
            std::max(ns_ub, 0), b.gmat.p, b.part.p, b.partials.p, b.sums.p, b.ticket.p, dbg, b.fail_test,
-           pre0 ? b.epart.p : nullptr, pre0 ? b.epart_blocks : 0, 1, nullptr, {}};
+           pre0 ? b.epart.p : nullptr, pre0 ? b.epart_blocks : 0, 1, nullptr, {}, 1};
+  static const int rpt = [] {
+    const char* e = std::getenv("FLOAM_LM_RPT");
+    return e ? std::max(1, std::min(8, std::atoi(e))) : 1;
+  }();
+  a.rpt = rpt;
   if (peers && peers->world > 1) {
     a.world = peers->world;
     a.xme = peers->mine;
