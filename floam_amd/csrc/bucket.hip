@@ -147,18 +147,26 @@ __device__ __forceinline__ void bucket_bitonic(const uint32_t* __restrict__ kin,
                                                unsigned long long* s_x, uint32_t* s_k, int* s_v) {
   const int t = threadIdx.x;
   unsigned long long k[E];
+  // the values are loaded with the keys and parked in s_v by input position (one memory round trip for both; the
+  // network does not touch s_v), then picked up by sorted position from LDS instead of a second gather from memory
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const int q = E * t + e;
     k[e] = q < size ? ((unsigned long long)kin[q] << 32) | (unsigned)q : ~0ull;
+    if (q < size) s_v[q] = vin[q];
   }
   bitonic_sizes64<E, 2>(k, s_x);
+  __syncthreads();   // (every value parked; a one-wave network has no barrier of its own)
+  int val[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) val[e] = E * t + e < size ? s_v[(int)(unsigned)k[e]] : 0;
+  __syncthreads();
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const int p = E * t + e;
     if (p < size) {
       s_k[p] = (uint32_t)(k[e] >> 32);
-      s_v[p] = vin[(int)(unsigned)k[e]];
+      s_v[p] = val[e];
     }
   }
   __syncthreads();
@@ -538,13 +546,25 @@ __global__ __launch_bounds__(kTB) void bucket_compact(VoxelJobDev A, VoxelJobDev
       }
       __syncthreads();
     }
-    // every element's point, one parallel round trip
-    for (int e = t; e < nc; e += kTB) {
-      const uint32_t k = L.k[e];
-      PointRec p;
-      if (k >> 31) vox_fetch(B, nB0, nB1, L.v[e], p);
-      else vox_fetch(A, nA0, nA1, L.v[e], p);
-      L.u.pt[e] = make_float4(p.x, p.y, p.z, p.intensity);
+    // every element's point: kGather elements per thread with all their loads in flight before any is used (one
+    // memory round trip for a bucket of up to kGather x 256, not one per 256)
+    constexpr int kGather = 4;
+    for (int g0 = 0; g0 < nc; g0 += kGather * kTB) {
+      float4 lo[kGather], hi[kGather];
+#pragma unroll
+      for (int u = 0; u < kGather; ++u) {
+        const int e = g0 + u * kTB + t;
+        lo[u] = hi[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (e < nc) {
+          if (L.k[e] >> 31) vox_fetch_halves(B, nB0, nB1, L.v[e], lo[u], hi[u]);
+          else vox_fetch_halves(A, nA0, nA1, L.v[e], lo[u], hi[u]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kGather; ++u) {
+        const int e = g0 + u * kTB + t;
+        if (e < nc) L.u.pt[e] = make_float4(lo[u].x, lo[u].y, lo[u].z, hi[u].x);   // x, y, z, intensity
+      }
     }
     const uint32_t prev = c0 ? L.prev_key : 0u;
     __syncthreads();

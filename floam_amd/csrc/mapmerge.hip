@@ -711,13 +711,18 @@ void mm_stamps_print() {
   static unsigned q[2][kMmStampTiles][6];
   FLOAM_HIP(hipDeviceSynchronize());
   FLOAM_HIP(hipMemcpyFromSymbol(q, HIP_SYMBOL(g_mm_st), sizeof(q)));
-  const unsigned t00 = q[0][0][0];
-  int nt = 0, smin = 0, smax = 0, emax = 0;
+  // (tiles beyond the last merge's count keep older records: only those started within 200 us of the latest start)
+  unsigned tmax = 0;
+  for (int j = 0; j < 2; ++j)
+    for (int t = 0; t < kMmStampTiles; ++t)
+      if (q[j][t][0] && (int)(q[j][t][0] - tmax) > 0) tmax = q[j][t][0];
+  const unsigned t00 = tmax - 20000u;
+  int nt = 0, smin = 1 << 30, smax = 0, emax = 0;
   double ph[5] = {0, 0, 0, 0, 0}, mx[5] = {0, 0, 0, 0, 0};
   for (int j = 0; j < 2; ++j)
     for (int t = 0; t < kMmStampTiles; ++t) {
       const unsigned* r = q[j][t];
-      if (r[0] == 0) continue;
+      if (r[0] == 0 || (int)(r[0] - t00) < 0) continue;
       ++nt;
       int len = 0;
       for (int k = 0; k < 5; ++k) {
