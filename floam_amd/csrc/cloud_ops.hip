@@ -46,7 +46,17 @@ __global__ void add_count(int* __restrict__ d_dst_count, const int* __restrict__
 __global__ void floam_profile_marker(int id) {
   if (id < 0) __builtin_trap();
 }
+// (diagnostic, FLOAM_UPDATE_NOP=1) a do-nothing dispatch at the start of every odometry update: whether the main
+// stream's idle time before the update's first kernel belongs to that kernel or to the update boundary
+__global__ void update_nop(int id) {
+  if (id < 0) __builtin_trap();
+}
 }  // namespace
+
+void update_nop_launch(hipStream_t st) {
+  hipLaunchKernelGGL(update_nop, dim3(1), dim3(64), 0, st, 0);
+  FLOAM_LAUNCH_CHECK();
+}
 
 void profile_marker_launch(int id, hipStream_t st) {
   hipLaunchKernelGGL(floam_profile_marker, dim3(1), dim3(64), 0, st, id);

@@ -26,6 +26,7 @@ struct SortScratch {   // (key, value) ping-pong buffers of the voxel sort
 
 // one marker dispatch (kernel floam_profile_marker) on the stream: tools/prof_summary.py slices traces by it
 void profile_marker_launch(int id, hipStream_t st);
+void update_nop_launch(hipStream_t st);   // FLOAM_UPDATE_NOP (diagnostic)
 
 // dmapping::CompensateVelocity (src/dataHandler.cpp:82-92), in place
 void compensate_velocity_launch(PointRec* pts, const int* d_n, int n_ub, double vx, double vy, double vz,

@@ -1057,6 +1057,8 @@ floam_status odom_update_deskew(floam_odom* o, floam_cloud* edge, floam_cloud* s
   const int ring = odom_begin(o, ctx);
   const int ne_ub = (int)cloud_ub(edge), ns_ub = (int)cloud_ub(surf);
   const bool captured = odom_capture_begin(o, ctx);
+  static const bool nop = std::getenv("FLOAM_UPDATE_NOP") != nullptr;
+  if (nop) update_nop_launch(ctx.stream);
   try {
     if (o->optimization_count > 2) o->optimization_count--;
     GatherArgs g1;
