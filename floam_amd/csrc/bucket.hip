@@ -451,7 +451,7 @@ __device__ __forceinline__ void block_sum2(int (&c)[2], unsigned (*hw)[kW]) {
 
 // FLOAM_BC_STAMPS=1 (diagnostic): per-bucket phase times of the last two bucket_compact launches (slot = launch
 // parity: call 1's VoxelGrids on the side stream, then call 2's on the main stream), printed by bucket_stamps_print
-__device__ unsigned g_bc_st[2][kBuckets][5];
+__device__ unsigned g_bc_st[2][kBuckets][8];
 
 __global__ __launch_bounds__(kTB) void bucket_compact(VoxelJobDev A, VoxelJobDev B, uint32_t* __restrict__ kin,
                                                       int* __restrict__ vin, uint32_t* __restrict__ kout,
@@ -532,6 +532,7 @@ __global__ __launch_bounds__(kTB) void bucket_compact(VoxelJobDev A, VoxelJobDev
   const Prefix2 pre = lookback_prefix(status, b, Prefix2{hc[0], hc[1]});
   if (pre.a < 0) return;   // (timed out, never expected: bucket 255 reports it)
   const unsigned long long T3 = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  unsigned long long Tg = T3, Th = T3, Te = T3;   // (stamps: gather done, heads scanned, emit loop done)
   if (streamed) write_splitters(split, geo, R.kept, start, size, [&](int q) { return kout[start + q]; });
   else write_splitters(split, geo, R.kept, start, size, [&](int q) { return L.k[q]; });
   int run_base[2] = {pre.a, pre.b};   // output slot of the next head, per cloud
@@ -585,6 +586,7 @@ __global__ __launch_bounds__(kTB) void bucket_compact(VoxelJobDev A, VoxelJobDev
         L.carry_n = n;
       }
     }
+    if (stamps) Tg = __builtin_amdgcn_s_memrealtime();   // (gather + carry done)
     // this thread's heads in its contiguous range; slots by a block scan of the per-thread counts (element order)
     int c[2];
     chunk_heads(L.k, nc, prev, c0 == 0, c);
@@ -615,6 +617,7 @@ __global__ __launch_bounds__(kTB) void bucket_compact(VoxelJobDev A, VoxelJobDev
     int pos0 = pos[0], pos1 = pos[1];   // the next output slot per cloud (selected by job below, never indexed)
     int e0, e1;
     thread_range(nc, e0, e1);
+    if (stamps) Th = __builtin_amdgcn_s_memrealtime();
     for (int e = e0; e < e1; ++e) {
       const uint32_t key = L.k[e];
       const uint32_t kp = e ? L.k[e - 1] : prev;
@@ -660,6 +663,7 @@ __global__ __launch_bounds__(kTB) void bucket_compact(VoxelJobDev A, VoxelJobDev
     run_base[0] += tot[0];
     run_base[1] += tot[1];
     __syncthreads();
+    if (stamps) Te = __builtin_amdgcn_s_memrealtime();
     if (t == 0) L.prev_key = L.k[nc - 1];
   }
   __syncthreads();
@@ -672,6 +676,7 @@ __global__ __launch_bounds__(kTB) void bucket_compact(VoxelJobDev A, VoxelJobDev
       unsigned* q = g_bc_st[stamps - 1][b];
       q[0] = (unsigned)T0; q[1] = (unsigned)(T1 - T0); q[2] = (unsigned)(T2 - T1); q[3] = (unsigned)(T3 - T2);
       q[4] = (unsigned)(__builtin_amdgcn_s_memrealtime() - T3);
+      q[5] = (unsigned)(Tg - T3); q[6] = (unsigned)(Th - Tg); q[7] = (unsigned)(Te - Th);
     }
   }
 }
@@ -737,15 +742,16 @@ void bucket_voxel_launch(BucketScratch& bs, RadixScratch& rs, const VoxelJobDev&
 
 void bucket_stamps_print() {
   if (!std::getenv("FLOAM_BC_STAMPS")) return;
-  static unsigned q[2][kBuckets][5];
+  static unsigned q[2][kBuckets][8];
   FLOAM_HIP(hipDeviceSynchronize());
   FLOAM_HIP(hipMemcpyFromSymbol(q, HIP_SYMBOL(g_bc_st), sizeof(q)));
   for (int sl = 0; sl < 2; ++sl) {
     int nb = 0, smin = 0, emax = 0, worst = 0, worst_end = 0;
-    double ph[4] = {0, 0, 0, 0}, mx[4] = {0, 0, 0, 0};
+    double ph[4] = {0, 0, 0, 0}, mx[4] = {0, 0, 0, 0}, sub[3] = {0, 0, 0};
     for (int b = 0; b < kBuckets; ++b) {
       if (q[sl][b][1] == 0 && q[sl][b][4] == 0) continue;
       ++nb;
+      for (int k = 0; k < 3; ++k) sub[k] += q[sl][b][5 + k];
       for (int k = 0; k < 4; ++k) {
         ph[k] += q[sl][b][1 + k];
         mx[k] = std::max(mx[k], (double)q[sl][b][1 + k]);
@@ -763,6 +769,9 @@ void bucket_stamps_print() {
                  ph[3] / nb / 100.0, mx[3] / 100.0, (emax - smin) / 100.0, worst,
                  (int)(q[sl][worst][0] - q[sl][0][0]) / 100.0);
     (void)worst_end;
+    std::fprintf(stderr, "[bc stamps]   slot %d gather + emit: gather %.2f, heads + scans %.2f, emit loop + barrier %.2f, "
+                 "drain %.2f us (means)\n", sl, sub[0] / nb / 100.0, sub[1] / nb / 100.0, sub[2] / nb / 100.0,
+                 (ph[3] - sub[0] - sub[1] - sub[2]) / nb / 100.0);
   }
 }
 
