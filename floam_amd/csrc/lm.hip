@@ -212,7 +212,6 @@ constexpr SurfTable make_surf_table() {
   T.ra[28] = 6; T.rb[28] = 6;   // (count: not a dot product)
   return T;
 }
-__constant__ SurfTable c_surf = make_surf_table();
 
 // How each of the 29 outputs follows from Y = G [K_0, K_1, K_2, c] (G symmetric, the products commute, so every
 // shortcut below is the very sum the full quadratic form computes, in the same order): a 13-term dot of one of
