@@ -635,20 +635,26 @@ __global__ __launch_bounds__(kTB) void bucket_compact(VoxelJobDev A, VoxelJobDev
       const float4 f = L.u.pt[e];
       float s0 = f.x, s1 = f.y, s2 = f.z, s3 = f.w;
       int j = e + 1;
-      for (; j + 8 <= nc; j += 8) {   // 8 points per LDS round trip, the additions in order
-        bool stop = false;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) stop = stop || L.k[j + q] != key;
-        if (stop) break;
+      // 8 keys and 8 points per LDS round trip (the points loaded beside the keys, not after the run test), the
+      // additions in order up to the first key of another voxel
+      for (bool more = true; more && j < nc;) {
+        uint32_t kq[8];
         float4 p[8];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) p[q] = L.u.pt[j + q];
+        for (int q = 0; q < 8; ++q) {
+          const int jj = min(j + q, nc - 1);
+          kq[q] = L.k[jj];
+          p[q] = L.u.pt[jj];
+        }
 #pragma unroll
-        for (int q = 0; q < 8; ++q) { s0 += p[q].x; s1 += p[q].y; s2 += p[q].z; s3 += p[q].w; }
-      }
-      for (; j < nc && L.k[j] == key; ++j) {
-        const float4 q = L.u.pt[j];
-        s0 += q.x; s1 += q.y; s2 += q.z; s3 += q.w;
+        for (int q = 0; q < 8; ++q) {
+          if (more && j < nc && kq[q] == key) {
+            s0 += p[q].x; s1 += p[q].y; s2 += p[q].z; s3 += p[q].w;
+            ++j;
+          } else {
+            more = false;
+          }
+        }
       }
       if (j == nc && streamed && c0 + nc < size) {   // reaches the chunk end of a streamed bucket: carried over
         L.carry[0] = s0; L.carry[1] = s1; L.carry[2] = s2; L.carry[3] = s3;
@@ -658,7 +664,12 @@ __global__ __launch_bounds__(kTB) void bucket_compact(VoxelJobDev A, VoxelJobDev
         L.carry_key = key;
         continue;
       }
-      J.out[slot] = centroid_out(s0, s1, s2, s3, j - e);
+      {   // VoxelGrid's output record as two 16-B stores: x, y, z, 1 | intensity, ring 0 + pad, time 0, 0
+        const float cn = (float)(j - e);
+        float4* o = reinterpret_cast<float4*>(J.out + slot);
+        o[0] = make_float4(s0 / cn, s1 / cn, s2 / cn, 1.0f);
+        o[1] = make_float4(s3 / cn, 0.0f, 0.0f, 0.0f);
+      }
     }
     run_base[0] += tot[0];
     run_base[1] += tot[1];
