@@ -1815,11 +1815,18 @@ floam_status floam_odom_set_shard(floam_odom* o, int rank, int world, const void
   });
 }
 
-// peer sharding: this rank's exchange buffer (zeroed: tag 0 never matches, epochs start at 8), allocated once
+// peer sharding: this rank's exchange buffer (zeroed: tag 0 never matches, epochs start at 8), allocated once.
+// Uncached device memory: the other ranks poll it over xGMI with system-scope loads, which are served from L2
+// (MI355X_MICROARCH.md: sc1 / sc0 sc1 loads bypass L1 only), and coarse-grained memory of another GPU gives no
+// cross-device coherence inside a kernel; uncached, every store and poll goes to this GPU's memory
 void shard_xbuf(floam_odom* o) {
   if (o->xbuf) return;
   FLOAM_HIP(hipSetDevice(o->device));
-  FLOAM_HIP(hipMalloc(&o->xbuf, sizeof(unsigned long long) * kShardXchgWords));
+  if (hipExtMallocWithFlags(&o->xbuf, sizeof(unsigned long long) * kShardXchgWords, hipDeviceMallocUncached) !=
+      hipSuccess) {
+    (void)hipGetLastError();
+    FLOAM_HIP(hipMalloc(&o->xbuf, sizeof(unsigned long long) * kShardXchgWords));
+  }
   FLOAM_HIP(hipMemset(o->xbuf, 0, sizeof(unsigned long long) * kShardXchgWords));
 }
 
