@@ -1822,7 +1822,8 @@ floam_status floam_odom_set_shard(floam_odom* o, int rank, int world, const void
 void shard_xbuf(floam_odom* o) {
   if (o->xbuf) return;
   FLOAM_HIP(hipSetDevice(o->device));
-  if (hipExtMallocWithFlags(&o->xbuf, sizeof(unsigned long long) * kShardXchgWords, hipDeviceMallocUncached) !=
+  if (hipExtMallocWithFlags(reinterpret_cast<void**>(&o->xbuf), sizeof(unsigned long long) * kShardXchgWords,
+                            hipDeviceMallocUncached) !=
       hipSuccess) {
     (void)hipGetLastError();
     FLOAM_HIP(hipMalloc(&o->xbuf, sizeof(unsigned long long) * kShardXchgWords));
