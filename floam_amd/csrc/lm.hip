@@ -62,16 +62,8 @@ __device__ __forceinline__ void load_rec(const double* __restrict__ rec, int cap
 // 29 x 8 = 232 threads) adds threads p, p + 8, p + 16, ... (the strip threads read consecutive LDS words: no bank
 // conflicts), then the 8 strips are added in order.  Returns, to thread t < 58, the sum of component t >> 1 (the
 // caller publishes it in two halves); no barrier after the last LDS read of `strip`.
-// Row stride of the thread-sums table (in doubles): a strip read has lanes (c, p) of 8 components x 8 strips read
-// red[c RS + 8 j + p]; with RS = 8 mod 32 the 8 rows start 16 banks apart (2 RS = 16 mod 64 four-byte banks), so the
-// 64 lanes' 128 dwords fill each bank exactly twice — the minimum for 512 B.  (An odd stride put the rows 2 banks
-// apart: lanes (c, p) and (c + 1, p - 1) collided, up to 8-way.)  The writes (thread t, column t) are conflict-free
-// for any stride.
 template <int NR>
-constexpr int red_stride() {
-  static_assert(NR % 32 == 0, "record threads: whole half-waves");
-  return NR + 8;
-}
+constexpr int red_stride() { return NR + 1; }   // odd row stride (in doubles): the 8 rows a wave reads hit 8 bank sets
 
 // the 8 strip sums of component c live in lanes 8c .. 8c + 7 of one wave: a fixed butterfly gives every one of them
 // the same total (each step adds two values, commutatively, so all eight lanes compute the same bits)
@@ -238,39 +230,7 @@ constexpr SurfOut make_surf_out() {
   }
   return S;
 }
-// make_surf_out's entry t by integer arithmetic on the lane (a per-lane load from constant memory is a vector memory
-// round trip on the surf half's path): cost = c . Y3; J^T J (a <= b): b < 3 a dot of K_a with Y row b, a < 3 <= b
-// Y[a][6 + b], 3 <= a the G entry [6 + b][6 + a]; J^T r: a < 3 a dot of K_a with Y3, else Y[3][6 + a]; the count.
-__host__ __device__ constexpr void surf_out_decode(int t, int& kind, int& ra, int& rb) {
-  kind = 3; ra = 0; rb = 0;
-  if (t == 0) {
-    kind = 0; ra = 3; rb = 3;
-  } else if (t < 22) {
-    int e = t - 1, a = 0;
-#pragma unroll
-    for (int r = 0; r < 5; ++r)
-      if (e >= 6 - a) { e -= 6 - a; ++a; }
-    const int b = a + e;
-    if (b < 3) { kind = 0; ra = a; rb = b; }
-    else if (a < 3) { kind = 1; ra = a; rb = 6 + b; }
-    else { kind = 2; ra = 6 + b; rb = 6 + a; }
-  } else if (t < 28) {
-    const int a = t - 22;
-    if (a < 3) { kind = 0; ra = a; rb = 3; }
-    else { kind = 1; ra = 3; rb = 6 + a; }
-  }
-}
-constexpr bool surf_out_decode_matches_table() {
-  const SurfOut S = make_surf_out();
-  for (int t = 0; t < LM_NSUM; ++t) {
-    int kind = 0, ra = 0, rb = 0;
-    surf_out_decode(t, kind, ra, rb);
-    if (kind != S.kind[t]) return false;
-    if (kind != 3 && (ra != S.a[t] || rb != S.b[t])) return false;
-  }
-  return true;
-}
-static_assert(surf_out_decode_matches_table(), "surf_out_decode must reproduce make_surf_out");
+__constant__ SurfOut c_surf_out = make_surf_out();
 
 // Two LDS phases: every lane forms M and the translations itself (the wave-uniform values lane 0 used to publish;
 // the V rows are compile-time selections of them), lanes 0..12 form row i of Y from row i of G; then lane t < 29
@@ -319,8 +279,7 @@ __device__ void surf_sums_wave(const double* x /* LDS [7] */, const double* o /*
   }
   wave_lds_order();
   if (t < LM_NSUM) {
-    int kind, ra, rb;
-    surf_out_decode(t, kind, ra, rb);
+    const int kind = c_surf_out.kind[t], ra = c_surf_out.a[t], rb = c_surf_out.b[t];
     double r;
     if (kind == 0) {   // the four candidate dots in independent chains, then the lane's own
       double d0 = 0.0, d1 = 0.0, d2 = 0.0, d3 = 0.0;

@@ -16,7 +16,7 @@ __global__ __launch_bounds__(256) void ctrl_bench(unsigned long long* out, doubl
   __shared__ double G[kGramW][kGramW];
   __shared__ double o[3];
   __shared__ double ssum[LM_NSUM];
-  __shared__ double red[LM_NSUM * red_stride<192>()];
+  __shared__ double red[LM_NSUM * 193];
   __shared__ double pt[7];
   const int t = threadIdx.x, lane = t & 63;
   unsigned long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
