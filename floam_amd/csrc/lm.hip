@@ -67,10 +67,19 @@ constexpr int red_stride() { return NR + 1; }   // odd row stride (in doubles): 
 
 // the 8 strip sums of component c live in lanes 8c .. 8c + 7 of one wave: a fixed butterfly gives every one of them
 // the same total (each step adds two values, commutatively, so all eight lanes compute the same bits)
+// (DPP lane moves, no LDS crossbar round trip: quad_perm xor 1, quad_perm xor 2, then the half-row mirrored — lane i
+// with 7 - i pairs the two uniform quads exactly as xor 4 did, so the bits are those of the xor butterfly)
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
 __device__ __forceinline__ double strip8_total(double v) {
-  v += __shfl_xor(v, 1, 8);
-  v += __shfl_xor(v, 2, 8);
-  v += __shfl_xor(v, 4, 8);
+  v += dpp_f64<0xB1>(v);
+  v += dpp_f64<0x4E>(v);
+  v += dpp_f64<0x141>(v);
   return v;
 }
 

@@ -649,16 +649,42 @@ __device__ __forceinline__ void stencil_scan(const CorrArgs& A, int x0, int x1, 
   wave_lds_order();   // the group's LDS slot is rewritten by its next scan
 }
 
-// group-wide top-5 (every lane ends with the merged list) and count
+// one merge step with the partner lane given by a DPP control (a VALU lane move within a row of 16: no LDS crossbar
+// round trip, which ds_bpermute — __shfl_xor — costs for each of the 11 words)
+template <int CTRL>
+__device__ __forceinline__ int dpp_i32(int v) { return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false); }
+template <int CTRL>
+__device__ __forceinline__ void merge_step_dpp(Top5& t, int& cnt) {
+  Top5 o;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const int lo = dpp_i32<CTRL>((int)(t.k[k] & 0xFFFFFFFFull)), hi = dpp_i32<CTRL>((int)(t.k[k] >> 32));
+    o.k[k] = ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
+  }
+  top5_merge(t, o);
+  cnt += dpp_i32<CTRL>(cnt);
+}
+
+// group-wide top-5 (every lane ends with the merged list) and count.  The merge of two top-5 lists is the top 5 of
+// their union (keys are distinct), so any pairing that leaves every lane of the group with the whole union gives
+// the same list: for G = 16 (one DPP row) quad_perm xor 1, quad_perm xor 2, then the half-row and the row mirrored
+// (lane i with 7 - i, then with 15 - i), each step pairing two groups that are already uniform
 template <int G>
 __device__ __forceinline__ void group_merge(Top5& t, int& cnt) {
+  if constexpr (G == 16) {
+    merge_step_dpp<0xB1>(t, cnt);    // quad_perm [1, 0, 3, 2]
+    merge_step_dpp<0x4E>(t, cnt);    // quad_perm [2, 3, 0, 1]
+    merge_step_dpp<0x141>(t, cnt);   // row_half_mirror
+    merge_step_dpp<0x140>(t, cnt);   // row_mirror
+  } else {
 #pragma unroll
-  for (int mm = G / 2; mm > 0; mm >>= 1) {
-    Top5 o;
+    for (int mm = G / 2; mm > 0; mm >>= 1) {
+      Top5 o;
 #pragma unroll
-    for (int k = 0; k < 5; ++k) o.k[k] = shfl_xor_u64<G>(t.k[k], mm);
-    top5_merge(t, o);
-    cnt += __shfl_xor(cnt, mm, G);
+      for (int k = 0; k < 5; ++k) o.k[k] = shfl_xor_u64<G>(t.k[k], mm);
+      top5_merge(t, o);
+      cnt += __shfl_xor(cnt, mm, G);
+    }
   }
 }
 
