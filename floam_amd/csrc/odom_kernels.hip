@@ -425,6 +425,13 @@ __device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v,
 
 template <int G>
 __device__ __forceinline__ int group_incl_scan(int v, int lane) {
+  if constexpr (G == 16) {   // one DPP row: row_shr 1, 2, 4, 8 (lanes below the shift get 0: bound_ctrl)
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, true);
+    return v;
+  }
 #pragma unroll
   for (int o = 1; o < G; o <<= 1) {
     const int u = __shfl_up(v, o, G);
