@@ -69,11 +69,7 @@ __device__ __forceinline__ BucketRange bucket_range(const unsigned* __restrict__
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const unsigned c = hist[t];
   unsigned inc = c;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const unsigned u = __shfl_up(inc, o, 64);
-    if (lane >= o) inc += u;
-  }
+  inc = wave_incl_scan(inc);   // (DPP, floam_common.hpp)
   if (lane == 63) s_tmp[w] = inc;
   __syncthreads();
   unsigned add = 0;
@@ -234,11 +230,7 @@ __device__ __forceinline__ void chunk_rank(const unsigned (&dig)[kStreamR], int 
     tot += v;
   }
   inc = tot;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const unsigned u = __shfl_up(inc, o, 64);
-    if (lane >= o) inc += u;
-  }
+  inc = wave_incl_scan(inc);   // (DPP, floam_common.hpp)
   if (lane == 63) L.ws[w] = inc;
   __syncthreads();
   unsigned add = 0;
@@ -286,11 +278,7 @@ __device__ void stream_sort(uint32_t* __restrict__ ka, int* __restrict__ va, uin
     __syncthreads();
     const unsigned c = L.run[t];
     unsigned inc = c;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const unsigned u = __shfl_up(inc, o, 64);
-      if (lane >= o) inc += u;
-    }
+    inc = wave_incl_scan(inc);   // (DPP, floam_common.hpp)
     if (lane == 63) L.ws[w] = inc;
     __syncthreads();
     unsigned add = 0;
@@ -594,11 +582,7 @@ __global__ __launch_bounds__(kTB) void bucket_compact(VoxelJobDev A, VoxelJobDev
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       int v = c[j];
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const int x = __shfl_up(v, o, 64);
-        if (lane >= o) v += x;
-      }
+      v = wave_incl_scan(v);   // (DPP, floam_common.hpp)
       inc[j] = v;
     }
     __syncthreads();   // (the carry above is done before a head below may start a new one)

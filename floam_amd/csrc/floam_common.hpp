@@ -112,6 +112,21 @@ struct HostBuf {
   }
 };
 
+// Inclusive prefix sum over the 64 lanes of a wave by DPP lane moves: row_shr 1, 2, 4, 8 inside each row of 16 (lanes
+// below the shift read 0), then row_bcast 15 (the row total into the next row, rows 1 and 3) and row_bcast 31 (rows
+// 0 + 1 into rows 2 and 3) — six VALU steps where a __shfl_up loop takes six ds_bpermute round trips.  Every lane of
+// the wave must be active (the callers run it in wave-uniform code).
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, true);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, true);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, true);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, true);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);
+  return v;
+}
+__device__ __forceinline__ unsigned wave_incl_scan(unsigned v) { return (unsigned)wave_incl_scan((int)v); }
+
 }  // namespace floam
 
 // Device-resident cloud behind the opaque floam_cloud handle.

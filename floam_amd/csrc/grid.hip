@@ -91,11 +91,7 @@ __global__ __launch_bounds__(kTB) void grid_alloc(GridJob E, GridJob S, OdomDev*
     // block exclusive scan of the totals: wave inclusive scan, then the wave totals
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     int incl = total;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int u = __shfl_up(incl, o, 64);
-      if (lane >= o) incl += u;
-    }
+    incl = wave_incl_scan(incl);   // (DPP, floam_common.hpp)
     if (lane == 63) s_wave[w] = incl;
     __syncthreads();
     int wbase = 0, btotal = 0;

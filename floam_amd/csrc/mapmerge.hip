@@ -573,11 +573,7 @@ __device__ __forceinline__ void mm_merge_job(const VoxelJobDev& JJ, const MapKey
   __shared__ int s_w[kTB / 64];
   const int lane = t & 63, w = t >> 6;
   int inc = nout;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int x = __shfl_up(inc, o, 64);
-    if (lane >= o) inc += x;
-  }
+  inc = wave_incl_scan(inc);   // (DPP, floam_common.hpp)
   if (lane == 63) s_w[w] = inc;
   __syncthreads();
   int wb = 0, nloc = 0;

@@ -132,21 +132,13 @@ __global__ __launch_bounds__(kTB) void radix_pass(const uint32_t* __restrict__ k
                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // bucket start of digit t: exclusive scan of the pass histogram (wave scan + wave totals)
   unsigned incl = h;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const unsigned u = __shfl_up(incl, o, 64);
-    if (lane >= o) incl += u;
-  }
+  incl = wave_incl_scan(incl);   // (DPP, floam_common.hpp)
   if (lane == 63) s_wsum[w] = incl;
   // PAYLOAD: the tile-local start of digit t (exclusive scan of the tile's digit counts) for the LDS staging
   __shared__ unsigned s_twsum[kTB / 64];
   unsigned tincl = cnt;
   if (PAYLOAD) {
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const unsigned u = __shfl_up(tincl, o, 64);
-      if (lane >= o) tincl += u;
-    }
+    tincl = wave_incl_scan(tincl);   // (DPP, floam_common.hpp)
     if (lane == 63) s_twsum[w] = tincl;
   }
   unsigned prefix = 0;

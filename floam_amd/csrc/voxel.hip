@@ -255,11 +255,7 @@ __global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B,
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
     int v = cnt[c];
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int x = __shfl_up(v, o, 64);
-      if (lane >= o) v += x;
-    }
+    v = wave_incl_scan(v);   // (DPP, floam_common.hpp)
     inc[c] = v;
     if (lane == 63) s_w[c][w] = v;
   }
