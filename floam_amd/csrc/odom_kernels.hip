@@ -983,16 +983,24 @@ __device__ __forceinline__ bool geom_fit(const R (&P)[5][3], float4 pq, double* 
 template <bool EDGE, typename R>
 __device__ __forceinline__ bool geom_query(LMState* __restrict__ st, const CorrArgs& A, int i,
                                            double* __restrict__ w = nullptr, const double* o = nullptr) {
-  const int n = min(*A.d_n, A.n_ub);
-  bool ok = false;
-  const int flags = i < n ? A.valid[i] : 0;
-  if (flags & 1) {
-    R P[5][3];
+  // the flag, the neighbours and the query loaded speculatively for every slot inside the arrays (i < n_ub <= cap),
+  // beside the device count: one memory round trip before the fit instead of three dependent ones (count -> flag ->
+  // coordinates); slots without a search result are read but never used
+  R P[5][3];
+  float4 pq = make_float4(0.f, 0.f, 0.f, 0.f);
+  int flags0 = 0;
+  if (i < A.n_ub) {
+    flags0 = A.valid[i];
 #pragma unroll
     for (int j = 0; j < 5; ++j)
 #pragma unroll
       for (int a = 0; a < 3; ++a) P[j][a] = A.nnxyz[(3 * j + a) * A.cap + i];
-    const float4 pq = *reinterpret_cast<const float4*>(&A.q[i].x);
+    pq = *reinterpret_cast<const float4*>(&A.q[i].x);
+  }
+  const int n = min(*A.d_n, A.n_ub);
+  bool ok = false;
+  const int flags = i < n ? flags0 : 0;
+  if (flags & 1) {
     ok = geom_fit<EDGE, R>(P, pq, A.rec, A.cap, i, w, o);
     A.valid[i] = (uint8_t)((flags & 2) | (ok ? 1 : 0) | 4);   // bit 2: the search found 5 neighbours
   }
