@@ -166,6 +166,18 @@ def main():
         except floam_amd.FloamError as e:
             log(f"[rank {rank}] peer exchange buffer unavailable ({e})")
             ok, h = False, b""
+        # every rank's GPU must be able to read the others' memory (xGMI peer access) before the solve polls it
+        devs = [None] * world
+        dist.all_gather_object(devs, dev)
+        try:
+            import torch
+            for d in set(devs):
+                if d != dev and not torch.cuda.can_device_access_peer(dev, d):
+                    log(f"[rank {rank}] GPU {dev} cannot access GPU {d}: no peer exchange")
+                    ok = False
+        except Exception as e:   # (no peer query: fall back to RCCL rather than risk a fault)
+            log(f"[rank {rank}] peer access query failed ({e})")
+            ok = False
         handles = [None] * world
         dist.all_gather_object(handles, h)
         if ok and all(len(x) == 64 for x in handles):
