@@ -1422,10 +1422,19 @@ __global__ void gather_status(const LMState* __restrict__ lm, const int* __restr
       radix_ctl_zero(vctl, threadIdx.x, blockDim.x);
       if (mc.ctl && threadIdx.x < kMergeCtlWords) mc.ctl[threadIdx.x] = 0;
     }
-    if (mc.flags)   // + the incremental merge's checks (mapmerge.hip)
-      mm_minmax_block(blockIdx.y == 0 ? A : B, (int)blockIdx.y, (int)blockIdx.x, (int)gridDim.x, vpart, mc);
-    else
-      vox_minmax_block(blockIdx.y == 0 ? A : B, (int)blockIdx.y, (int)blockIdx.x, (int)gridDim.x, vpart);
+    // job A's points over blocks 1 .. n-1 only: block (0, 0) publishes the status (host memory, system-scope fence)
+    // and would finish last with a share of points on top; it stores an empty box into the partial slot n-1
+    const int job = (int)blockIdx.y;
+    const int nb = job == 0 ? (int)gridDim.x - 1 : (int)gridDim.x;
+    const int b = job == 0 ? (int)blockIdx.x - 1 : (int)blockIdx.x;
+    if (b < 0) {
+      float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+      vox_partial_store(mn, mx, 0, nb, vpart);
+    } else if (mc.flags) {   // + the incremental merge's checks (mapmerge.hip)
+      mm_minmax_block(job == 0 ? A : B, job, b, nb, vpart, mc);
+    } else {
+      vox_minmax_block(job == 0 ? A : B, job, b, nb, vpart);
+    }
   } else if (gcE.coarse) {   // blocks of their own: the next grid builds' clears (this update's kNN launches are done)
     grid_clear_part(blockIdx.y == 2 ? gcE : gcS, blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x,
                     blockIdx.x == 0 && threadIdx.x == 0);
