@@ -1268,11 +1268,15 @@ __global__ __launch_bounds__(kTB) void deskew_bridge(const LMState* __restrict__
   if (vpart) {
     // fused with the next VoxelGrids' bounding-box stage: blockIdx.y = the cloud (0 edge, 1 surf), partial
     // blockIdx.x of its min / max over the compensated coordinates (edge != surf)
+    // (the edge cloud over blocks 1 .. n-1: block (0, 0) publishes call 1's status and forms the prediction, and
+    // stores an empty box into the edge cloud's partial slot n-1)
     const int job = (int)blockIdx.y;
     PointRec* __restrict__ c = job ? surf : edge;
     const int n = job ? min(*d_ns, ns_ub) : ne;
+    const int nb = job ? (int)gridDim.x : (int)gridDim.x - 1;
+    const int bx = job ? (int)blockIdx.x : (int)blockIdx.x - 1;
     float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    for (int i = bx * blockDim.x + threadIdx.x; bx >= 0 && i < n; i += nb * blockDim.x) {
       PointRec& p = c[i];   // CompensateVelocity: p += v * time, double -> float
       const double t = p.time;
       const float x = (float)((double)p.x + vx * t), y = (float)((double)p.y + vy * t), z = (float)((double)p.z + vz * t);
@@ -1282,7 +1286,7 @@ __global__ __launch_bounds__(kTB) void deskew_bridge(const LMState* __restrict__
       mn[0] = fminf(mn[0], x); mn[1] = fminf(mn[1], y); mn[2] = fminf(mn[2], z);
       mx[0] = fmaxf(mx[0], x); mx[1] = fmaxf(mx[1], y); mx[2] = fmaxf(mx[2], z);
     }
-    vox_partial_store(mn, mx, job, (int)blockIdx.x, vpart);
+    vox_partial_store(mn, mx, job, bx >= 0 ? bx : nb, vpart);
     if (lead) radix_ctl_zero(vctl, threadIdx.x, blockDim.x);
   } else {
     // aliased (edge and surf are one cloud): the reference's two CompensateVelocity calls (src/odomEstimationClass.cpp:
