@@ -61,13 +61,13 @@ __device__ __forceinline__ void write_splitters(unsigned long long* __restrict__
   }
 }
 
-// bucket b's start and size from the producer's bucket histogram (256 words): every block scans it
+// bucket b's start and size from the producer's bucket histogram (256 words): every block scans it.  c = hist[t],
+// loaded by the caller in its prologue (it does not depend on b, so it travels with the ticket / gate loads)
 struct BucketRange {
   int start, size, kept;
 };
-__device__ __forceinline__ BucketRange bucket_range(const unsigned* __restrict__ hist, int b, unsigned* s_tmp) {
+__device__ __forceinline__ BucketRange bucket_range(unsigned c, int b, unsigned* s_tmp) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const unsigned c = hist[t];
   unsigned inc = c;
   inc = wave_incl_scan(inc);   // (DPP, floam_common.hpp)
   if (lane == 63) s_tmp[w] = inc;
@@ -337,13 +337,14 @@ __global__ __launch_bounds__(kTB) void bucket_sort(uint32_t* __restrict__ kin, i
                                                    const unsigned* __restrict__ hist, const int* __restrict__ gate,
                                                    unsigned long long* __restrict__ split, const int* __restrict__ geo) {
   const int b = blockIdx.x, t = threadIdx.x;
+  const unsigned hc = hist[t];   // (kTB == kBuckets; issued with the gate load)
   const int gv = gate ? *gate : 1;
   if (!gv) return;
   __shared__ union {
     SortLds s;
     StreamLds st;
   } L;
-  const BucketRange R = bucket_range(hist, b, L.s.tmp);
+  const BucketRange R = bucket_range(hc, b, L.s.tmp);
   const int start = R.start, size = R.size;
   if (size == 0) return;
   if (b == kBuckets - 1) {   // the dropped elements: already in input order
@@ -455,12 +456,13 @@ __global__ __launch_bounds__(kTB) void bucket_compact(VoxelJobDev A, VoxelJobDev
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   // the bucket is the block's ticket (zeroed by vox_keys): a bucket's lookback only waits on buckets that are already
   // running (HIP promises no dispatch order).  Prologue loads together with it: gate, the clouds' counts, the
-  // overflow flags (the histogram in bucket_range)
+  // overflow flags and this thread's histogram word (bucket_range)
   __shared__ int s_b;
   if (t == 0) s_b = ticket ? (int)atomicAdd(ticket, 1u) : (int)blockIdx.x;   // (null: by index, A/B only)
   const int gv = gate ? *gate : 1;
   const int nA0 = *A.d_n0, nA1 = A.d_n1 ? *A.d_n1 : 0, nB0 = *B.d_n0, nB1 = B.d_n1 ? *B.d_n1 : 0;
   const int ovf0 = overflow[0], ovf1 = overflow[1];   // (no two-element arrays indexed by a run-time job: scratch)
+  const unsigned hw0 = hist[t];                        // (kTB == kBuckets)
   __syncthreads();
   const int b = s_b;
   if (!gv) {   // gated off (no keyframe): the output is the unchanged first part (the map).  By block index: no
@@ -479,7 +481,7 @@ __global__ __launch_bounds__(kTB) void bucket_compact(VoxelJobDev A, VoxelJobDev
     StreamLds st;
   } U;
   CompactLds& L = U.c;
-  const BucketRange R = bucket_range(hist, b, L.tmp);
+  const BucketRange R = bucket_range(hw0, b, L.tmp);
   const int start = R.start, size = R.size;
   if (b == kBuckets - 1 || size == 0) {   // nothing to emit: publish zero; the last bucket ends the outputs
     const Prefix2 pre = lookback_prefix(status, b, Prefix2{0, 0});

@@ -286,21 +286,32 @@ __device__ __forceinline__ void mm_merge_job(const VoxelJobDev& JJ, const MapKey
                                              unsigned seq, int violate_mod, int count_grid, int by_index,
                                              int stamps) {
   const unsigned long long T0 = mm_now(stamps);
+  // prologue loads first, so they travel with the ticket: the counts, the gate and the status gather's verdict words
+  // (none depends on the tile; on the gated-off path the verdict words are read but unused)
+  MergeView V;
+  V.J = JJ;
+  V.K = KK;
+  V.n0 = min(*V.J.d_n0, V.J.n0_ub);
+  V.n1 = min(*V.J.d_n1, V.J.n1_ub);
+  const bool gated_off = gate && !*gate;
+  V.full = ctl[2 + job] != 0;
+  V.ovf = ctl[4 + job] != 0;
+  V.nset = ctl[job];
+  V.base = job ? ctl[0] : 0;
+  for (int d = 0; d < 3; ++d) V.mb[d] = ctl[6 + 6 * job + d];
+  V.dx = ctl[9 + 6 * job];
+  V.dy = ctl[10 + 6 * job];
+  V.dz = ctl[11 + 6 * job];
   // the tile within the job is the block's ticket (ctl[kMergeTicketWord + 32 job], zeroed by the status gather): a
   // tile's lookback only waits on tiles that are already running (HIP promises no dispatch order)
   __shared__ int s_tile;
   if (threadIdx.x == 0)
     s_tile = by_index ? (job ? (int)blockIdx.x - tilesA : (int)blockIdx.x) : atomicAdd(&ctl[kMergeTicketWord + 32 * job], 1);
   const int njb = job ? (int)gridDim.x - tilesA : tilesA;   // this job's blocks
-  MergeView V;
-  V.J = JJ;
-  V.K = KK;
-  V.n0 = min(*V.J.d_n0, V.J.n0_ub);
-  V.n1 = min(*V.J.d_n1, V.J.n1_ub);
   const int t = threadIdx.x;
   __syncthreads();
   const int tile = s_tile;
-  if (gate && !*gate) {   // no keyframe: the map, its keys and their verdict stay as they are (no lookback: by index)
+  if (gated_off) {   // no keyframe: the map, its keys and their verdict stay as they are (no lookback: by index)
     const int tile = job ? (int)blockIdx.x - tilesA : (int)blockIdx.x;
     for (int i0 = tile * kTB; i0 < V.n0; i0 += njb * kTB) {   // (wave-uniform trip count: the grid count)
       const int i = i0 + t;
@@ -322,14 +333,6 @@ __device__ __forceinline__ void mm_merge_job(const VoxelJobDev& JJ, const MapKey
     }
     return;
   }
-  V.full = ctl[2 + job] != 0;
-  V.ovf = ctl[4 + job] != 0;
-  V.nset = ctl[job];
-  V.base = job ? ctl[0] : 0;
-  for (int d = 0; d < 3; ++d) V.mb[d] = ctl[6 + 6 * job + d];
-  V.dx = ctl[9 + 6 * job];
-  V.dy = ctl[10 + 6 * job];
-  V.dz = ctl[11 + 6 * job];
   V.skeys = skeys;
   V.svals = svals;
   const int L = V.full ? V.nset : V.n0 + V.nset;   // merged elements
