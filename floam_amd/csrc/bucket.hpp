@@ -31,13 +31,19 @@ struct BucketDev {
 // dx, dy, dz, overflow), in LDS s[256] (ascending; the other cloud's splitters collapse to 0 below / ~0 above):
 // a splitter cell outside the grid saturates to the grid's first / last cell of its row, plane or grid, which keeps the
 // order.  All threads call it (it ends with a barrier).  bucket_of: the bucket of a sort key.
-__device__ __forceinline__ void bucket_keys_lds(const unsigned long long* __restrict__ split, int job, const int (&mb)[3],
-                                                long long dx, long long dy, long long dz, bool ovf, uint32_t* s) {
+// sp_t: split[threadIdx.x], loaded by the caller in its prologue (bucket_split_prefetch) so the splitters do not add a
+// memory round trip after the bounding box
+__device__ __forceinline__ unsigned long long bucket_split_prefetch(const unsigned long long* __restrict__ split) {
+  return split && (int)threadIdx.x < kSplitters ? split[threadIdx.x] : 0ull;
+}
+__device__ __forceinline__ void bucket_keys_lds(const unsigned long long* __restrict__ split, unsigned long long sp_t,
+                                                int job, const int (&mb)[3], long long dx, long long dy, long long dz,
+                                                bool ovf, uint32_t* s) {
   const int t = threadIdx.x;
   for (int m = t; m < kBuckets; m += blockDim.x) {
     uint32_t v = 0xFFFFFFFFu;
     if (m < kSplitters) {
-      const unsigned long long sp = split[m];
+      const unsigned long long sp = m == t ? sp_t : split[m];
       const int sj = (int)(sp >> 63);
       if (sj < job) {
         v = 0u;

@@ -24,6 +24,7 @@ struct GridJob {
   const PointRec* map;
   const int* d_m;
   int m_ub;
+  int spec_ub;      // speculative loads of the first stride: below the map's and the slot words' buffer sizes
   float4* pts;
   CoarseCell* coarse;
   uint2* where;
@@ -60,13 +61,18 @@ __host__ __device__ inline GridCountDev count_dev(const GridJob& J) {
 __global__ __launch_bounds__(kTB) void grid_count(GridJob E, GridJob S, OdomDev* __restrict__ predict) {
   const GridJob& J = blockIdx.y == 0 ? E : S;
   if (predict && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) odom_predict_step(predict);
+  // the first stride's point loaded speculatively beside the device count (inside the map's buffer), so the
+  // inserts start one memory round trip earlier; the load is used only when i < m
+  const int i_first = blockIdx.x * blockDim.x + threadIdx.x;
+  float4 p_first = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i_first < J.spec_ub) p_first = *reinterpret_cast<const float4*>(&J.map[i_first].x);
   const int m = min(*J.d_m, J.m_ub);
   const GridCountDev C = count_dev(J);
   for (int i0 = blockIdx.x * blockDim.x; i0 < m; i0 += gridDim.x * blockDim.x) {   // wave-uniform trip count
     const int i = i0 + threadIdx.x;
     const bool valid = i < m;
     float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (valid) p = *reinterpret_cast<const float4*>(&J.map[i].x);
+    if (valid) p = i == i_first ? p_first : *reinterpret_cast<const float4*>(&J.map[i].x);
     grid_count_point(C, i, valid, p.x, p.y, p.z);
   }
 }
@@ -75,6 +81,10 @@ __global__ __launch_bounds__(kTB) void grid_count(GridJob E, GridJob S, OdomDev*
 __global__ __launch_bounds__(kTB) void grid_alloc(GridJob E, GridJob S, OdomDev* __restrict__ predict) {
   const GridJob& J = blockIdx.y == 0 ? E : S;
   if (predict && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) odom_predict_step(predict);
+  // the first stride's list entry loaded speculatively beside the list size (t <= mask: inside the list's buffer;
+  // entries past the size are stale and never used)
+  const int t_first = blockIdx.x * blockDim.x + threadIdx.x;
+  const int slot_first = t_first <= (int)J.mask ? J.clist_new[t_first] : 0;
   const int nc = J.counters[1 + J.parity];
   __shared__ int s_wave[kTB / 64];
   __shared__ int s_base;
@@ -83,7 +93,7 @@ __global__ __launch_bounds__(kTB) void grid_alloc(GridJob E, GridJob S, OdomDev*
     CoarseCell c;
     int total = 0, slot = 0;
     if (t < nc) {
-      slot = J.clist_new[t];
+      slot = t == t_first ? slot_first : J.clist_new[t];
       c = J.coarse[slot];
 #pragma unroll
       for (int k = 0; k < 8; ++k) total += c.sub[k];
@@ -112,16 +122,24 @@ __global__ __launch_bounds__(kTB) void grid_alloc(GridJob E, GridJob S, OdomDev*
 
 __global__ __launch_bounds__(kTB) void grid_scatter(GridJob E, GridJob S) {
   const GridJob& J = blockIdx.y == 0 ? E : S;
+  // the first stride's slot word and point loaded speculatively beside the device count (inside both buffers)
+  const int i_first = blockIdx.x * blockDim.x + threadIdx.x;
+  uint2 wr_first = make_uint2(0u, 0u);
+  float4 p_first = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i_first < J.spec_ub) {
+    wr_first = J.where[i_first];
+    p_first = *reinterpret_cast<const float4*>(&J.map[i_first].x);
+  }
   const int m = min(*J.d_m, J.m_ub);
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
-    const uint2 wr = J.where[i];
+  for (int i = i_first; i < m; i += gridDim.x * blockDim.x) {
+    const uint2 wr = i == i_first ? wr_first : J.where[i];
     const int sub = (int)(wr.y >> 28), rank = (int)(wr.y & 0x0FFFFFFFu);
     const CoarseCell& c = J.coarse[wr.x];
     int pos = c.start + rank;
 #pragma unroll
     for (int k = 0; k < 8; ++k)
       if (k < sub) pos += c.sub[k];
-    const float4 p = *reinterpret_cast<const float4*>(&J.map[i].x);
+    const float4 p = i == i_first ? p_first : *reinterpret_cast<const float4*>(&J.map[i].x);
     J.pts[pos] = make_float4(p.x, p.y, p.z, __int_as_float(i));
     J.xyz[i] = make_float4(p.x, p.y, p.z, 0.0f);
   }
@@ -149,9 +167,10 @@ GridClearDev clear_job(const Grid& g) {
   return GridClearDev{g.coarse.p, g.clist[g.parity ^ 1].p, g.counters.p, g.parity, g.fresh ? 1 : 0, g.mask};
 }
 
-GridJob make_job(Grid& g, const PointRec* map, const int* d_m, int m_ub) {
+GridJob make_job(Grid& g, const PointRec* map, const int* d_m, int m_ub, size_t map_cap = 0) {
   const int p = g.parity;
-  return GridJob{map, d_m, m_ub, g.pts.p, g.coarse.p, g.where.p, g.xyz.p, g.clist[p].p, g.clist[p ^ 1].p,
+  const int spec = (int)std::min<size_t>({(size_t)m_ub, map_cap, g.where.cap});
+  return GridJob{map, d_m, m_ub, spec, g.pts.p, g.coarse.p, g.where.p, g.xyz.p, g.clist[p].p, g.clist[p ^ 1].p,
                  g.counters.p, p, g.fresh ? 1 : 0, g.bits, g.mask};
 }
 }  // namespace
@@ -171,7 +190,8 @@ GridClearDev grid_clear_prepare(Grid& g, int ub, hipStream_t st) {
 }
 
 void grid_build_launch(Grid& gE, const PointRec* mapE, const int* d_mE, int mE_ub, Grid& gS, const PointRec* mapS,
-                       const int* d_mS, int mS_ub, hipStream_t st, OdomDev* predict, bool precleared) {
+                       const int* d_mS, int mS_ub, hipStream_t st, OdomDev* predict, bool precleared,
+                       size_t mE_cap, size_t mS_cap) {
   mE_ub = std::max(mE_ub, 1);
   mS_ub = std::max(mS_ub, 1);
   // a build cleared in advance was sized for at least this map (the upper bounds only shrink once the update that
@@ -191,7 +211,7 @@ void grid_build_launch(Grid& gE, const PointRec* mapE, const int* d_mE, int mE_u
     if (gE.fresh) FLOAM_HIP(hipMemsetAsync(gE.counters.p, 0, sizeof(int) * 8, st));
     if (gS.fresh) FLOAM_HIP(hipMemsetAsync(gS.counters.p, 0, sizeof(int) * 8, st));
   }
-  const GridJob E = make_job(gE, mapE, d_mE, mE_ub), S = make_job(gS, mapS, d_mS, mS_ub);
+  const GridJob E = make_job(gE, mapE, d_mE, mE_ub, mE_cap), S = make_job(gS, mapS, d_mS, mS_ub, mS_cap);
   if (!precleared) {
     const bool full = gE.fresh || gS.fresh;
     const int tmax = (int)std::max(gE.mask, gS.mask) + 1;

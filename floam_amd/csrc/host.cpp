@@ -583,7 +583,7 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
   if (o->grid_dirty) {
     ProfScope ps(ctx, "grid_build", FLOAM_PROF_CLOUD);
     grid_build_launch(o->gE, o->mapE.pts.p, o->mapE.count.p, mE_ub, o->gS, o->mapS.pts.p, o->mapS.count.p, mS_ub, st,
-                      predict ? o->ds.p : nullptr, true);
+                      predict ? o->ds.p : nullptr, true, o->mapE.pts.cap, o->mapS.pts.cap);
     o->grid_dirty = false;
   }
   if (o->late_wait[0]) {   // one wait orders the main stream after the side stream's VoxelGrids and, through them,
@@ -1981,7 +1981,7 @@ floam_status floam_odom_find_correspondences(floam_odom* o, const floam_cloud* e
     voxel2_launch(o->vs, je, js, st);
     if (o->grid_dirty) {
       grid_build_launch(o->gE, o->mapE.pts.p, o->mapE.count.p, (int)o->mapE_n, o->gS, o->mapS.pts.p,
-                        o->mapS.count.p, (int)o->mapS_n, st, nullptr);
+                        o->mapS.count.p, (int)o->mapS_n, st, nullptr, false, o->mapE.pts.cap, o->mapS.pts.cap);
       o->grid_dirty = false;
     }
     o->lm.reserve(1);

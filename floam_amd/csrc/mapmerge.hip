@@ -48,7 +48,8 @@ __global__ __launch_bounds__(kTB) void mm_keys(VoxelJobDev A, VoxelJobDev B, con
                                                BucketDev bd) {
   // the prologue's loads are all issued before any is waited on (one round trip instead of four in a row): the gate,
   // the bounding-box partials, the metas, the flags, the counts and — for the merge path, where element e is scan
-  // point e — this thread's first scan record and the pose (the host bound n1_ub keeps the load inside the array)
+  // point e — this thread's first scan record and the pose (the host bound n1_ub keeps the load inside the array), and
+  // this thread's splitter
   const int job = blockIdx.y;
   const int gv = gate ? *gate : 1;
   const MapMeta mA = *metaA, mB = *metaB;
@@ -70,6 +71,7 @@ __global__ __launch_bounds__(kTB) void mm_keys(VoxelJobDev A, VoxelJobDev B, con
   double pose0[7];
 #pragma unroll
   for (int k = 0; k < 7; ++k) pose0[k] = J0.pose[k];
+  const unsigned long long sp_t = bucket_split_prefetch(bd.split);   // (the splitters, bucket_keys_lds)
   if (!gv) return;
   __shared__ float s_mm[2][6];
   __shared__ unsigned s_hist[kRadixHistWords];
@@ -136,7 +138,7 @@ __global__ __launch_bounds__(kTB) void mm_keys(VoxelJobDev A, VoxelJobDev B, con
   const int n0 = job ? nB0 : nA0, n1 = job ? nB1 : nA1;
   const int start = full ? 0 : n0, count = job ? sizeB : sizeA, base = job ? sizeA : 0;
   __shared__ uint32_t s_spl[kBuckets];
-  const bool bucket = vox_bucket_begin(bd, job, G, job ? s_mm[1][5] : s_mm[0][5], J.inv, s_spl);
+  const bool bucket = vox_bucket_begin(bd, sp_t, job, G, job ? s_mm[1][5] : s_mm[0][5], J.inv, s_spl);
   int kept = 0;
   for (int e = e0; e < count; e += gridDim.x * blockDim.x) {
     const int i = start + e;   // index into the job's [map ; scan] concatenation

@@ -49,7 +49,7 @@ __global__ __launch_bounds__(kTB) void vox_keys(VoxelJobDev A, VoxelJobDev B, co
                                                 unsigned* __restrict__ radix_ctl, const int* __restrict__ gate,
                                                 int* __restrict__ n_dev, BucketDev bd) {
   // the prologue's loads are issued together (one round trip instead of three in a row): the gate, the partials,
-  // the counts and this thread's first record of the first part (inside the array by the host bound n0_ub)
+  // the counts, this thread's first record of the first part (inside the array by the host bound n0_ub) and its splitter
   const int job = blockIdx.y;
   const VoxelJobDev& J = job == 0 ? A : B;
   const int gv = gate ? *gate : 1;
@@ -62,6 +62,7 @@ __global__ __launch_bounds__(kTB) void vox_keys(VoxelJobDev A, VoxelJobDev B, co
   const int i0 = blockIdx.x * blockDim.x + threadIdx.x;
   PointRec p0;
   if (i0 < J.n0_ub) p0 = J.part0[i0];
+  const unsigned long long sp_t = bucket_split_prefetch(bd.split);   // (the splitters, bucket_keys_lds)
   if (!gv) return;
   __shared__ float s_mm[6];
   __shared__ unsigned s_hist[kRadixHistWords];
@@ -94,7 +95,7 @@ __global__ __launch_bounds__(kTB) void vox_keys(VoxelJobDev A, VoxelJobDev B, co
   const int base = job ? nA0 + nA1 : 0;
   if (job == 0 && blockIdx.x == 0 && threadIdx.x == 0) *n_dev = nA0 + nA1 + nB0 + nB1;
   __shared__ uint32_t s_spl[kBuckets];
-  const bool bucket = vox_bucket_begin(bd, job, g, mx[2], J.inv, s_spl);
+  const bool bucket = vox_bucket_begin(bd, sp_t, job, g, mx[2], J.inv, s_spl);
   for (int i = i0; i < n0 + n1; i += gridDim.x * blockDim.x) {
     uint32_t key = 0xFFFFFFFFu;
     PointRec p;

@@ -258,15 +258,15 @@ __device__ __forceinline__ void voxel_dims(const VoxelGeom& g, float mx_z, float
 }
 
 // The key producer's bucket stage (bucket.hip), called by every thread of a block whose cloud is `job`: the grid's
-// splitters into s_spl (LDS, 256), the grid for the next splitters (block 0 of the job).  Returns whether the
+// splitters into s_spl (LDS, 256; sp_t = bucket_split_prefetch(bd.split) from the prologue), the grid for the next splitters (block 0 of the job).  Returns whether the
 // bucket sort runs (else the producer builds digit histograms for the radix passes).
-__device__ __forceinline__ bool vox_bucket_begin(const BucketDev& bd, int job, const VoxelGeom& g, float mx_z,
-                                                 float inv, uint32_t* s_spl) {
+__device__ __forceinline__ bool vox_bucket_begin(const BucketDev& bd, unsigned long long sp_t, int job,
+                                                 const VoxelGeom& g, float mx_z, float inv, uint32_t* s_spl) {
   long long dx, dy, dz;
   voxel_dims(g, mx_z, inv, dx, dy, dz);
   if (bd.geo && blockIdx.x == 0 && threadIdx.x == 0) bucket_geo_store(bd.geo, job, g.min_b, (int)dx, (int)dy, g.overflow);
   if (!bd.split) return false;
-  bucket_keys_lds(bd.split, job, g.min_b, dx, dy, dz, g.overflow, s_spl);
+  bucket_keys_lds(bd.split, sp_t, job, g.min_b, dx, dy, dz, g.overflow, s_spl);
   return true;
 }
 
