@@ -1513,6 +1513,7 @@ floam_status floam_odom_destroy(floam_odom* o) {
       vox_stamps_print();
       bucket_stamps_print();
       mm_stamps_print();
+      geom_stamps_print();
       lm_ctrl_stamps_print();
       if (o->dbg_stamps.p) {   // FLOAM_DEBUG_STAMPS: the resident solve's segments in block 0 (100 MHz ticks)
         unsigned long long h[8];

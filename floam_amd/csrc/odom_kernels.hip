@@ -106,6 +106,62 @@ __device__ __forceinline__ void tridiag_qr_step(R (&d)[3], R (&e)[2], R (&Q)[3][
   }
 }
 
+// The three variants above as ONE instruction stream: lanes of a wave whose matrices need different variants
+// (<0, 2>, <1, 2>, <0, 1> by their deflation state) would otherwise run all three bodies one after the other every
+// iteration.  Operands are selected, not recomputed: every value is the same expression of the same inputs as in
+// the variant the lane needs (bit-identical); the second rotation of <0, 2> runs only when a lane needs it.
+template <typename R>
+__device__ __forceinline__ void tridiag_qr_step_any(R (&d)[3], R (&e)[2], R (&Q)[3][3], int end, int start) {
+  const bool two = end == 2 && start == 0;   // <0, 2>
+  const bool hi = end == 2 && start == 1;    // <1, 2>: the rotation acts on rows 1..2 (else rows 0..1)
+  const bool lo_tail = end == 1;             // <0, 1>: the shift from rows 0..1 (else rows 1..2)
+  const R t0 = lo_tail ? d[0] : d[1], t1 = lo_tail ? d[1] : d[2], ee = lo_tail ? e[0] : e[1];
+  const R td = (t0 - t1) * R(0.5);
+  R mu = t1;
+  if (td == R(0)) {
+    mu -= fabs(ee);
+  } else {
+    const R e2 = ee * ee;
+    const R h = e_hypot(td, ee);
+    if (e2 == R(0)) mu -= (ee / (td + (td > R(0) ? R(1) : R(-1)))) * (ee / h);
+    else mu -= e2 / (td + (td > R(0) ? h : -h));
+  }
+  // rotation k = S on rows (a, b) = (d[S], d[S + 1]), off-diagonal ek = e[S]
+  const R a = hi ? d[1] : d[0], b = hi ? d[2] : d[1], ek = hi ? e[1] : e[0];
+  R c, s;
+  make_givens(a - mu, ek, c, s);
+  const R sdk = s * a + c * ek;
+  const R dkp1 = s * ek + c * b;
+  const R na = c * (c * a - s * ek) - s * (c * ek - s * b);
+  const R nb = s * sdk + c * dkp1;
+  const R nek = c * sdk - s * dkp1;
+  if (hi) { d[1] = na; d[2] = nb; e[1] = nek; } else { d[0] = na; d[1] = nb; e[0] = nek; }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const R xi = hi ? Q[1][i] : Q[0][i], yi = hi ? Q[2][i] : Q[1][i];
+    const R qa = c * xi - s * yi, qb = s * xi + c * yi;
+    if (hi) { Q[1][i] = qa; Q[2][i] = qb; } else { Q[0][i] = qa; Q[1][i] = qb; }
+  }
+  if (two) {   // <0, 2>: the bulge chased to rows 1..2
+    const R z = -s * e[1];
+    e[1] = c * e[1];
+    R c2, s2;
+    make_givens(e[0], z, c2, s2);
+    const R sdk2 = s2 * d[1] + c2 * e[1];
+    const R dkp12 = s2 * e[1] + c2 * d[2];
+    d[1] = c2 * (c2 * d[1] - s2 * e[1]) - s2 * (c2 * e[1] - s2 * d[2]);
+    d[2] = s2 * sdk2 + c2 * dkp12;
+    e[1] = c2 * sdk2 - s2 * dkp12;
+    e[0] = c2 * e[0] - s2 * z;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const R xi = Q[1][i], yi = Q[2][i];
+      Q[1][i] = c2 * xi - s2 * yi;
+      Q[2][i] = s2 * xi + c2 * yi;
+    }
+  }
+}
+
 template <typename R>
 __device__ __forceinline__ void swap_r(R& a, R& b) {
   const R t = a;
@@ -160,12 +216,16 @@ __device__ void eig_sym3(const R (&A)[3][3], R (&ev)[3], R (&u_top)[3]) {
     if (end <= 0) break;
     if (++iter > 90) break;
     start = (end == 2 && e[0] != R(0)) ? 0 : end - 1;
+#ifdef FLOAM_EIG_VARIANTS   // (A/B and bit-identity checks: the three variants as separate bodies)
     if (end == 2) {
       if (start == 0) tridiag_qr_step<0, 2>(d, e, Q);
       else tridiag_qr_step<1, 2>(d, e, Q);
     } else {
       tridiag_qr_step<0, 1>(d, e, Q);
     }
+#else
+    tridiag_qr_step_any(d, e, Q, end, start);
+#endif
   }
   // ascending selection sort (first minimum), swapping eigenvector columns
   int k = 0;
@@ -980,9 +1040,32 @@ __device__ __forceinline__ bool geom_fit(const R (&P)[5][3], float4 pq, double* 
   return ok;
 }
 
+// -DFLOAM_GEOM_STAMPS (diagnostic build): geom_kernel's phase times per block of the latest launches (s_memrealtime,
+// 100 MHz), stored by thread 0 with plain stores into the block's own row (no shared counters: atomics on shared
+// words would queue behind each other and inflate what they measure): [0] start, [1] query loads done (flags
+// known), [2] fit done, [3] edge sums / Gram done, [4] hand-off done (surf), [5] end, [6] role (0 edge, 1 surf,
+// 2 surf with the group reduce); printed by geom_stamps_print for the blocks of the newest launch
+#ifdef FLOAM_GEOM_STAMPS
+constexpr int kGeomStampBlocks = 4096;
+__device__ unsigned long long g_geom_blk[kGeomStampBlocks][8];
+__device__ __forceinline__ unsigned long long geom_now() { return __builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ void geom_row(unsigned long long t0, unsigned long long ta, unsigned long long tb,
+                                         unsigned long long tg, unsigned long long th, int role) {
+  if (threadIdx.x != 0 || blockIdx.x >= (unsigned)kGeomStampBlocks) return;
+  unsigned long long* r = g_geom_blk[blockIdx.x];
+  r[0] = t0; r[1] = ta; r[2] = tb; r[3] = tg; r[4] = th; r[5] = geom_now(); r[6] = (unsigned long long)role;
+}
+#define GEOM_STAMP(v, dep)                  \
+  asm volatile("" ::"v"((int)(dep)));       \
+  const unsigned long long v = geom_now()
+#else
+#define GEOM_STAMP(v, dep)
+#endif
+
 template <bool EDGE, typename R>
 __device__ __forceinline__ bool geom_query(LMState* __restrict__ st, const CorrArgs& A, int i,
-                                           double* __restrict__ w = nullptr, const double* o = nullptr) {
+                                           double* __restrict__ w = nullptr, const double* o = nullptr,
+                                           unsigned long long* tst = nullptr) {
   // the flag, the neighbours and the query loaded speculatively for every slot inside the arrays (i < n_ub <= cap),
   // beside the device count: one memory round trip before the fit instead of three dependent ones (count -> flag ->
   // coordinates); slots without a search result are read but never used
@@ -1000,10 +1083,15 @@ __device__ __forceinline__ bool geom_query(LMState* __restrict__ st, const CorrA
   const int n = min(*A.d_n, A.n_ub);
   bool ok = false;
   const int flags = i < n ? flags0 : 0;
+  GEOM_STAMP(ta, flags + (int)P[4][2] + (int)pq.x);
   if (flags & 1) {
     ok = geom_fit<EDGE, R>(P, pq, A.rec, A.cap, i, w, o);
     A.valid[i] = (uint8_t)((flags & 2) | (ok ? 1 : 0) | 4);   // bit 2: the search found 5 neighbours
   }
+#ifdef FLOAM_GEOM_STAMPS
+  GEOM_STAMP(tb, ok);
+  if (tst) { tst[0] = ta; tst[1] = tb; }
+#endif
   const unsigned long long b = __ballot(ok);
   if ((threadIdx.x & 63) == 0 && b) atomicAdd(EDGE ? &st->corr_edge : &st->corr_surf, __popcll(b));
   return ok;
@@ -1025,9 +1113,19 @@ template <typename R>
 __global__ __launch_bounds__(kTB) void geom_kernel(LMState* __restrict__ st, CorrArgs E, CorrArgs S, int nbE,
                                                    double* __restrict__ gpart, double* __restrict__ gmat,
                                                    unsigned* __restrict__ gcnt, double* __restrict__ epart) {
+#ifdef FLOAM_GEOM_STAMPS
+  GEOM_STAMP(t0, 0);
+  unsigned long long tq[2] = {t0, t0};
+#define GEOM_TQ , tq
+#else
+#define GEOM_TQ
+#endif
   if ((int)blockIdx.x < nbE) {
     if (!epart) {
-      geom_query<true, R>(st, E, blockIdx.x * blockDim.x + threadIdx.x);
+      geom_query<true, R>(st, E, blockIdx.x * blockDim.x + threadIdx.x, nullptr, nullptr GEOM_TQ);
+#ifdef FLOAM_GEOM_STAMPS
+      geom_row(t0, tq[0], tq[1], tq[1], tq[1], 0);
+#endif
       return;
     }
     // the record's residual and Jacobian at the solve's starting point (EdgeAnalyticCostFunction::Evaluate,
@@ -1037,7 +1135,7 @@ __global__ __launch_bounds__(kTB) void geom_kernel(LMState* __restrict__ st, Cor
 #pragma unroll
     for (int k = 0; k < 7; ++k) x[k] = st->x[k];
     double r9[9];
-    const bool ok = geom_query<true, R>(st, E, blockIdx.x * blockDim.x + threadIdx.x, r9);
+    const bool ok = geom_query<true, R>(st, E, blockIdx.x * blockDim.x + threadIdx.x, r9, nullptr GEOM_TQ);
     double acc[LM_NSUM];
 #pragma unroll
     for (int k = 0; k < LM_NSUM; ++k) acc[k] = 0.0;
@@ -1055,6 +1153,9 @@ __global__ __launch_bounds__(kTB) void geom_kernel(LMState* __restrict__ st, Cor
       for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
       if (lane == 0) s_e[wv][k] = v;
     }
+#ifdef FLOAM_GEOM_STAMPS
+    GEOM_STAMP(t3, __double_as_longlong(acc[0]) & 1);
+#endif
     __syncthreads();
     if (threadIdx.x < LM_NSUM) {
       double v = s_e[0][threadIdx.x];
@@ -1062,6 +1163,9 @@ __global__ __launch_bounds__(kTB) void geom_kernel(LMState* __restrict__ st, Cor
       for (int k = 1; k < kTB / 64; ++k) v += s_e[k][threadIdx.x];
       epart[blockIdx.x * LM_NSUM + threadIdx.x] = v;
     }
+#ifdef FLOAM_GEOM_STAMPS
+    geom_row(t0, tq[0], tq[1], t3, t3, 0);
+#endif
     return;
   }
   const int sb = (int)blockIdx.x - nbE;
@@ -1080,11 +1184,17 @@ __global__ __launch_bounds__(kTB) void geom_kernel(LMState* __restrict__ st, Cor
   gram_pair(lane, ei0, ej0);
   if (lane + 64 < kGram) gram_pair(lane + 64, ei1, ej1);
   double g0 = 0.0, g1 = 0.0;
+#ifdef FLOAM_GEOM_STAMPS
+  unsigned long long sl = 0ull, sf = 0ull, sg = 0ull;
+#endif
   for (int i0 = sb * kTB; i0 < ns; i0 += kSurfGeomBlocks * kTB) {   // wave-uniform trip count
+#ifdef FLOAM_GEOM_STAMPS
+    GEOM_STAMP(ti, 0);
+#endif
     double w[kGramW];
 #pragma unroll
     for (int k = 0; k < kGramW; ++k) w[k] = 0.0;
-    geom_query<false, R>(st, S, i0 + threadIdx.x, w, o);
+    geom_query<false, R>(st, S, i0 + threadIdx.x, w, o GEOM_TQ);
 #pragma unroll
     for (int k = 0; k < kGramW; ++k) s_w[wv][k][lane] = w[k];
     wave_lds_order();
@@ -1097,6 +1207,12 @@ __global__ __launch_bounds__(kTB) void geom_kernel(LMState* __restrict__ st, Cor
     g0 += a0;
     g1 += a1;
     wave_lds_order();
+#ifdef FLOAM_GEOM_STAMPS
+    GEOM_STAMP(tg, __double_as_longlong(g0) & 1);
+    sl += tq[0] - ti;
+    sf += tq[1] - tq[0];
+    sg += tg - tq[1];
+#endif
   }
   s_part[wv][lane] = g0;
   if (lane + 64 < kGram) s_part[wv][lane + 64] = g1;
@@ -1121,6 +1237,10 @@ __global__ __launch_bounds__(kTB) void geom_kernel(LMState* __restrict__ st, Cor
   __syncthreads();
   if (threadIdx.x == 0) s_last = atomicAdd(&gcnt[grp], 1u) == (unsigned)(per - 1);
   __syncthreads();
+#ifdef FLOAM_GEOM_STAMPS
+  GEOM_STAMP(t4, s_last);
+  if (!s_last) geom_row(t0, t0 + sl, t0 + sl + sf, t0 + sl + sf + sg, t4, 1);
+#endif
   if (!s_last) return;
   if (threadIdx.x < kGram) {   // the group's partial of G into gmat[grp] (the solve adds the groups, gram_load)
     double v = 0.0;
@@ -1134,7 +1254,11 @@ __global__ __launch_bounds__(kTB) void geom_kernel(LMState* __restrict__ st, Cor
     gmat[kGramGroups * kGram + threadIdx.x - kGram] = o[threadIdx.x - kGram];   // the origin the records use
   }
   if (threadIdx.x == 0) gcnt[grp] = 0u;   // every block of the group has arrived (next launch: kernel boundary)
+#ifdef FLOAM_GEOM_STAMPS
+  geom_row(t0, t0 + sl, t0 + sl + sf, t0 + sl + sf + sg, t4, 2);
+#endif
 }
+#undef GEOM_TQ
 
 // Algorithmic traffic of one launch of the search kernel (knn_kernel; SURVEY.md §8 d): every map
 // cell any query scans is streamed once (16 B per map point: the union over queries of the fine 3x3x3 block around
@@ -1574,6 +1698,49 @@ __global__ __launch_bounds__(kTB) void l2_evict(const float4* __restrict__ buf, 
   float acc = 0.f;
   for (size_t i = (size_t)blockIdx.x * kTB + threadIdx.x; i < n; i += (size_t)gridDim.x * kTB) acc += buf[i].x;
   if (acc == 1234.5f) sink[0] = acc;   // (never: keeps the loads)
+}
+
+void geom_stamps_print() {
+#ifdef FLOAM_GEOM_STAMPS
+  static unsigned long long h[kGeomStampBlocks][8];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_geom_blk), sizeof(h)) != hipSuccess) {
+    (void)hipGetLastError();
+    return;
+  }
+  unsigned long long last = 0;   // the newest launch: rows that started within 50 us of the latest start
+  for (int b = 0; b < kGeomStampBlocks; ++b) last = std::max(last, h[b][0]);
+  unsigned long long t_min = ~0ull, t_end = 0;
+  double sum[3][6] = {}, mx[3][6] = {};
+  int n[3] = {0, 0, 0};
+  for (int b = 0; b < kGeomStampBlocks; ++b) {
+    if (!h[b][0] || h[b][0] + 5000 < last) continue;
+    t_min = std::min(t_min, h[b][0]);
+  }
+  for (int b = 0; b < kGeomStampBlocks; ++b) {
+    if (!h[b][0] || h[b][0] + 5000 < last) continue;
+    const int r = (int)h[b][6];
+    if (r < 0 || r > 2) continue;
+    ++n[r];
+    t_end = std::max(t_end, h[b][5]);
+    const double v[6] = {(double)(h[b][0] - t_min), (double)(h[b][1] - h[b][0]), (double)(h[b][2] - h[b][1]),
+                         (double)(h[b][3] - h[b][2]), (double)(h[b][4] - h[b][3]), (double)(h[b][5] - h[b][4])};
+    for (int k = 0; k < 6; ++k) {
+      sum[r][k] += v[k];
+      mx[r][k] = std::max(mx[r][k], v[k]);
+    }
+  }
+  const char* names[3] = {"edge", "surf", "surf (group reduce)"};
+  for (int r = 0; r < 3; ++r) {
+    if (!n[r]) continue;
+    std::fprintf(stderr, "[geom stamps] %s, %d blocks, avg (max) us: start after the first %.2f (%.2f), loads %.2f (%.2f), "
+                 "fit %.2f (%.2f), sums / Gram %.2f (%.2f), hand-off %.2f (%.2f), tail %.2f (%.2f)\n", names[r], n[r],
+                 sum[r][0] / n[r] / 100, mx[r][0] / 100, sum[r][1] / n[r] / 100, mx[r][1] / 100, sum[r][2] / n[r] / 100,
+                 mx[r][2] / 100, sum[r][3] / n[r] / 100, mx[r][3] / 100, sum[r][4] / n[r] / 100, mx[r][4] / 100,
+                 sum[r][5] / n[r] / 100, mx[r][5] / 100);
+  }
+  std::fprintf(stderr, "[geom stamps] newest launch: first block start -> last block end %.2f us\n",
+               t_end > t_min ? (double)(t_end - t_min) / 100 : 0.0);
+#endif
 }
 
 void knn_stage_launch(LMState* d_st, const double* x0_dev, const QuerySet& qe, const Grid& ge, CorrSet& ce,
