@@ -36,8 +36,8 @@ struct Lim<float> {
 template <typename R>
 __device__ __forceinline__ R e_hypot(R x, R y) {
   const R ax = fabs(x), ay = fabs(y);
-  R p, qp;
-  if (ax > ay) { p = ax; qp = ay / p; } else { p = ay; qp = ax / p; }
+  const bool xb = ax > ay;   // (one division for both orders: lanes of a wave may take either)
+  const R p = xb ? ax : ay, qp = (xb ? ay : ax) / p;
   if (p == R(0)) return R(0);
   return p * sqrt(R(1) + qp * qp);
 }
@@ -51,18 +51,15 @@ __device__ __forceinline__ void make_givens(R p, R q, R& c, R& s) {
   } else if (p == R(0)) {
     c = R(0);
     s = q < R(0) ? R(1) : R(-1);
-  } else if (fabs(p) > fabs(q)) {
-    const R t = q / p;
+  } else {   // |p| > |q|: t = q / p, c = 1 / u, s = -t c; else t = p / q, s = -1 / u, c = -t s (one division, one
+    // square root and one reciprocal for both cases: lanes of a wave may take either)
+    const bool pb = fabs(p) > fabs(q);
+    const R t = (pb ? q : p) / (pb ? p : q);
     R u = sqrt(R(1) + t * t);
-    if (p < R(0)) u = -u;
-    c = R(1) / u;
-    s = -t * c;
-  } else {
-    const R t = p / q;
-    R u = sqrt(R(1) + t * t);
-    if (q < R(0)) u = -u;
-    s = R(-1) / u;
-    c = -t * s;
+    if ((pb ? p : q) < R(0)) u = -u;
+    const R r = (pb ? R(1) : R(-1)) / u;
+    c = pb ? r : -t * r;
+    s = pb ? -t * r : r;
   }
 }
 
