@@ -11,4 +11,4 @@ from .laser_processing import LaserProcessingClass, LidarParams  # noqa: F401
 from .odom_estimation import OdomEstimationClass, UpdateType  # noqa: F401
 from .synth import POINT_DTYPE  # noqa: F401
 
-__version__ = "0.1.0"
+__version__ = "0.4.0"   # floam_version() of the library it binds (ABI 3)

@@ -9,7 +9,17 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libfloam_amd.so")
+# FLOAM_AMD_LIB=diag selects the diagnostic build of the same sources (libfloam_amd_diag.so: the A/B, stamp and
+# test-hook environment variables, floam_amd/csrc/floam_common.hpp FLOAM_DIAG_ENV) — for the tests that need a hook
+# and for measurement scripts; the product library reads only FLOAM_GRAPH and FLOAM_MAP_MERGE
+PRODUCT_LIB_PATH = os.path.join(_HERE, "libfloam_amd.so")
+DIAG_LIB_PATH = os.path.join(_HERE, "libfloam_amd_diag.so")
+LIB_PATH = PRODUCT_LIB_PATH
+
+
+def lib_path() -> str:
+    """The library load() opens: the diagnostic build when FLOAM_AMD_LIB=diag, else the product library."""
+    return DIAG_LIB_PATH if os.environ.get("FLOAM_AMD_LIB") == "diag" else PRODUCT_LIB_PATH
 
 # floam_status (include/floam_c.h)
 ABI_VERSION = 3   # FLOAM_ABI_VERSION of include/floam_c.h this package binds
@@ -98,7 +108,7 @@ def load(path: str | None = None):
     global _LIB
     if _LIB is not None and path is None:
         return _LIB
-    p = path or LIB_PATH
+    p = path or lib_path()
     if not os.path.exists(p):
         raise FileNotFoundError(f"{p} not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
                                 "or `make -C floam_amd/csrc`")

@@ -458,7 +458,7 @@ __global__ __launch_bounds__(kTB) void bucket_compact(VoxelJobDev A, VoxelJobDev
   // running (HIP promises no dispatch order).  Prologue loads together with it: gate, the clouds' counts, the
   // overflow flags and this thread's histogram word (bucket_range)
   __shared__ int s_b;
-  if (t == 0) s_b = ticket ? (int)atomicAdd(ticket, 1u) : (int)blockIdx.x;   // (null: by index, A/B only)
+  if (t == 0) s_b = (int)atomicAdd(ticket, 1u);
   const int gv = gate ? *gate : 1;
   const int nA0 = *A.d_n0, nA1 = A.d_n1 ? *A.d_n1 : 0, nB0 = *B.d_n0, nB1 = B.d_n1 ? *B.d_n1 : 0;
   const int ovf0 = overflow[0], ovf1 = overflow[1];   // (no two-element arrays indexed by a run-time job: scratch)
@@ -714,7 +714,7 @@ bool bucket_sort_enabled(int pipeline) {
   // FLOAM_SORT: radix (the four digit passes everywhere), merge (the bucket sort in the map merge only), bucket (both
   // pipelines; the default: r4d, 1914-1918 scans/s against 1800 merge-only and 1691-1706 radix, one box)
   static const int mask = [] {
-    const char* e = std::getenv("FLOAM_SORT");
+    const char* e = FLOAM_DIAG_ENV("FLOAM_SORT");
     if (e && e[0] == 'r') return 0;
     if (e && e[0] == 'm') return 2;
     return 3;
@@ -729,16 +729,16 @@ void bucket_voxel_launch(BucketScratch& bs, RadixScratch& rs, const VoxelJobDev&
   bs.reserve(n, st);
   rs.reserve(n, st);
   radix_digit_pass_launch(rs, k0, v0, k1, v1, n, bs.bkt.p, st, gate, n_dev);
-  static const bool stamps = std::getenv("FLOAM_BC_STAMPS") != nullptr;
+  static const bool stamps = FLOAM_DIAG_ENV("FLOAM_BC_STAMPS") != nullptr;
   static unsigned launches = 0;
   hipLaunchKernelGGL(bucket_compact, dim3(kBuckets), dim3(kTB), 0, st, A, B, k1, v1, k0, v0, rs.ctl.p, overflow,
-                     status, rs.ctl.p, gate, bs.split.p, bs.geo.p, tile_by_index() ? nullptr : ticket,
+                     status, rs.ctl.p, gate, bs.split.p, bs.geo.p, ticket,
                      stamps ? (int)(launches++ & 1u) + 1 : 0);
   FLOAM_LAUNCH_CHECK();
 }
 
 void bucket_stamps_print() {
-  if (!std::getenv("FLOAM_BC_STAMPS")) return;
+  if (!FLOAM_DIAG_ENV("FLOAM_BC_STAMPS")) return;
   static unsigned q[2][kBuckets][8];
   FLOAM_HIP(hipDeviceSynchronize());
   FLOAM_HIP(hipMemcpyFromSymbol(q, HIP_SYMBOL(g_bc_st), sizeof(q)));

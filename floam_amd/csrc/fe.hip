@@ -845,7 +845,7 @@ __global__ void fe_stage(const PointRec* __restrict__ in, const int* __restrict_
 }  // namespace
 
 static int fe_stamps_on() {
-  static const int on = std::getenv("FLOAM_FE_STAMPS") ? 1 : 0;
+  static const int on = FLOAM_DIAG_ENV("FLOAM_FE_STAMPS") ? 1 : 0;
   static unsigned launches = 0;
   static bool init = false;
   if (on && !init) {
@@ -858,7 +858,7 @@ static int fe_stamps_on() {
 }
 
 void fe_stamps_print() {
-  if (!std::getenv("FLOAM_FE_STAMPS")) return;
+  if (!FLOAM_DIAG_ENV("FLOAM_FE_STAMPS")) return;
   static unsigned long long h[8 + 3 * 1024];
   FLOAM_HIP(hipDeviceSynchronize());
   FLOAM_HIP(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_fe_stamps), sizeof(h)));

@@ -12,6 +12,16 @@
 #include <string>
 #include <vector>
 
+// Diagnostic, A/B and test hooks read from the environment exist only in the diagnostic build (-DFLOAM_DIAG:
+// libfloam_amd_diag.so, which the tests that need a hook load); in the product library FLOAM_DIAG_ENV(name) is a null
+// pointer and the name is not in the binary.  The product library reads two documented variables: FLOAM_GRAPH and
+// FLOAM_MAP_MERGE.
+#ifdef FLOAM_DIAG
+#define FLOAM_DIAG_ENV(name) std::getenv(name)
+#else
+#define FLOAM_DIAG_ENV(name) (static_cast<const char*>(nullptr))
+#endif
+
 #include "../../include/floam_c.h"
 
 namespace floam {
@@ -89,8 +99,8 @@ struct DevBuf {
     FLOAM_HIP(hipMalloc(&p, c * sizeof(T)));
     cap = c;
   }
-  static bool alloc_log() {   // FLOAM_LOG_ALLOC=1: report device (re)allocations (diagnostic)
-    static const bool on = std::getenv("FLOAM_LOG_ALLOC") != nullptr;
+  static bool alloc_log() {   // FLOAM_LOG_ALLOC=1: report device (re)allocations (diagnostic build)
+    static const bool on = FLOAM_DIAG_ENV("FLOAM_LOG_ALLOC") != nullptr;
     return on;
   }
 };

@@ -100,17 +100,8 @@ struct DeviceCtx {
 static std::mutex g_ctx_mu;
 static std::map<int, std::unique_ptr<DeviceCtx>> g_ctx;
 
-// Stream creation.  FLOAM_STREAM_PRIO=1 (experiment): the odometry stream at the highest priority, the side and
-// feature-extraction streams at the lowest, so that the command processor prefers the odometry's workgroups.
-static void make_stream(hipStream_t* s, bool high) {
-  static const bool prio = std::getenv("FLOAM_STREAM_PRIO") != nullptr;
-  if (!prio) {
-    FLOAM_HIP(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
-    return;
-  }
-  int least = 0, greatest = 0;
-  FLOAM_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
-  FLOAM_HIP(hipStreamCreateWithPriority(s, hipStreamNonBlocking, high ? greatest : least));
+static void make_stream(hipStream_t* s, bool /*high*/) {
+  FLOAM_HIP(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
 }
 
 
@@ -301,10 +292,6 @@ struct floam_odom {
   // against grid_count's 16.5 us), so off by default
   bool grid_count_off = true;
   int map_violate_mod = 0;        // FLOAM_MM_VIOLATE=n: every n-th merge reports its keys out of order (tests)
-  int mm_per = 4;                 // FLOAM_MM_PER=2: 512-element merge tiles instead of 1024 (tests, A/B)
-  // FLOAM_LM_PRE0=1: the geometry launch evaluates iteration zero's edge half (measured slower, r4d: geometry +6 us
-  // per pass for -2 to -3 us of solve; off by default)
-  bool lm_pre0 = false;
   size_t mapE_n = 0, mapS_n = 0;   // map sizes: exact after a synchronisation, else upper bounds
   // scratch
   DevBuf<PointRec> dE, dS, tmp;
@@ -520,11 +507,11 @@ void allreduce_sums(floam_odom* o, DeviceCtx& ctx) {
 
 // The resident solve needs its whole grid on the device at once (its blocks poll each other): checked once per mode
 // from the kernel's occupancy (a partitioned or smaller device falls back to one launch per evaluation, the sharded
-// path on one rank).  FLOAM_LM_PER_EVAL=1 forces the fallback (tests).
+// path on one rank).  FLOAM_LM_PER_EVAL=1 forces the fallback (tests, diagnostic build).
 bool lm_resident(floam_odom* o, int mode) {
   int& c = o->coresident[mode & 15];
   if (c < 0) {
-    const char* f = std::getenv("FLOAM_LM_PER_EVAL");
+    const char* f = FLOAM_DIAG_ENV("FLOAM_LM_PER_EVAL");
     c = (f && f[0] == '1') ? 0 : (lm_solve_coresident(mode, o->device) ? 1 : 0);
   }
   return c == 1;
@@ -598,7 +585,7 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
   }
   o->lm.reserve(1);
   o->lmb.reserve(st);
-  if (!o->dbg_stamps.p && std::getenv("FLOAM_DEBUG_STAMPS")) {
+  if (!o->dbg_stamps.p && FLOAM_DIAG_ENV("FLOAM_DEBUG_STAMPS")) {
     o->dbg_stamps.reserve(8);
     FLOAM_HIP(hipMemsetAsync(o->dbg_stamps.p, 0, sizeof(unsigned long long) * 8, st));
   }
@@ -621,17 +608,14 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
   const bool sharded = o->sharded();
   const int mode = lm_mode(o->huber, o->fp32);
   const bool gram = (mode & LM_GRAM) != 0;
-  // the geometry launch evaluates iteration zero's edge half for the resident squared-loss solve (FLOAM_LM_PRE0=1:
-  // the solve evaluates it itself, A/B)
   const bool peer = o->peer && o->world > 1;   // peer sharding: the resident solve exchanges the ranks' sums itself
   if (peer && !lm_resident(o, mode))
     throw Error(FLOAM_ERR_UNSUPPORTED, "peer sharding needs the resident solve (its grid does not fit the device)");
-  const bool pre0 = gram && (!sharded || peer) && o->lm_pre0 && lm_resident(o, mode);
   for (int it = 0; it < o->optimization_count; ++it) {
     {
       ProfScope ps(ctx, "knn", FLOAM_PROF_KNN);   // the correspondence pass: search + geometry
       {
-        static const bool stages = std::getenv("FLOAM_KNN_STAGES") != nullptr;
+        static const bool stages = FLOAM_DIAG_ENV("FLOAM_KNN_STAGES") != nullptr;
         if (stages && (ctx.profile & FLOAM_PROF_KNN_BYTES))   // (replay only, before the timed scope)
           knn_stage_launch(o->lm.p, it == 0 ? x0_dev : nullptr, qe, o->gE, o->ce, qs, o->gS, o->cs, o->mapE.count.p,
                            o->mapS.count.p, o->rank, o->world, o->knn_evict, st);
@@ -641,7 +625,7 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
                    o->mapS.count.p, o->rank, o->world, st);
       }
       ProfScope ps2(ctx, "knn_geometry", FLOAM_PROF_KNN_DETAIL);
-      geom_launch(o->lm.p, qe, o->ce, qs, o->cs, gram, o->fp32_geom, o->lmb, st, pre0);
+      geom_launch(o->lm.p, qe, o->ce, qs, o->cs, gram, o->fp32_geom, o->lmb, st);
     }
     if (ctx.profile & FLOAM_PROF_KNN_BYTES) {   // replay only: algorithmic bytes of the two launches above
       knn_traffic_launch(o->lm.p, qe, o->gE, o->ce, o->rank, o->world, o->traffic_set, o->prof_bytes.p + 0, st);
@@ -651,7 +635,7 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
     if ((!sharded || peer) && lm_resident(o, mode)) {
       ProfScope ps(ctx, "lm_solve", FLOAM_PROF_LM);
       lm_solve_launch(o->lm.p, o->ce, dcnt + 0, ne_ub, o->cs, dcnt + 1, ns_ub, mode, o->lmb, st, o->dbg_stamps.p,
-                      pre0, peer ? &o->peers : nullptr);
+                      peer ? &o->peers : nullptr);
     } else {   // one launch (+ one all-reduce of the 29 sums when sharded) per evaluation, all on the stream
       ProfScope ps(ctx, "lm_solve_sharded", FLOAM_PROF_LM);
       for (int ev = 0; ev < 5; ++ev) {
@@ -726,7 +710,7 @@ void wait_status(floam_odom* o, DeviceCtx& ctx, const floam_odom::Pending& P) {
       if (__atomic_load_n(&slots[k].seq, __ATOMIC_ACQUIRE) != want) return false;
     return true;
   };
-  static const bool query = !std::getenv("FLOAM_NOQUERY");   // (diagnostic knob)
+  static const bool query = !FLOAM_DIAG_ENV("FLOAM_NOQUERY");   // (diagnostic knob)
   for (long long spin = 0; !done(); ++spin) {
     if (query && (spin & 1023) == 1023) {   // now and then: has the stream stopped without the status?
       const hipError_t q = hipStreamQuery(ctx.stream);
@@ -749,7 +733,7 @@ floam_status odom_collect_one(floam_odom* o, DeviceCtx& ctx) {
   o->pendS -= P.addS;
   if (P.ev) FLOAM_HIP(hipEventSynchronize(P.ev));   // (a recycled event: not destroyed)
   wait_status(o, ctx, P);
-  static const bool mm_debug = std::getenv("FLOAM_MM_DEBUG") != nullptr;   // (diagnostic: the merge's modes)
+  static const bool mm_debug = FLOAM_DIAG_ENV("FLOAM_MM_DEBUG") != nullptr;   // (diagnostic: the merge's modes)
   if (mm_debug && o->map_merge && o->mms.ctl.p) {
     FLOAM_HIP(hipStreamSynchronize(ctx.stream));
     int c[kMergeCtlWords];
@@ -773,7 +757,7 @@ floam_status odom_collect_one(floam_odom* o, DeviceCtx& ctx) {
       std::strncpy(t.name, "knn_search", sizeof(t.name) - 1);
       t.algorithmic_bytes += (double)U.prof[0] + (double)U.prof[1];
     }
-    if (U.lm.n_res < 0) poison("LM evaluation blocks did not arrive at the control block (timeout)");
+    if (U.lm.n_res < 0 || U.lm.xfail) poison("an LM solve's hand-off timed out (blocks or peer ranks did not arrive)");
     if (U.counts[0] < 0 || U.counts[1] < 0 || U.counts[2] < 0 || U.counts[3] < 0)
       poison("voxel-grid compaction failed (lookback timeout)");
     if (U.fe_status & FE_STATUS_SECTOR_TOO_LONG)
@@ -835,8 +819,9 @@ int odom_begin(floam_odom* o, DeviceCtx& ctx) {
 
 // Graph capture of one update (when enabled): odom_capture_begin before its first device operation,
 // odom_capture_end after its last one instantiates or updates the executable graph of its kind and launches it.
+// (not while the one-call host entry point's write-back is active: its copy stream would join the capture)
 bool odom_capture_begin(floam_odom* o, DeviceCtx& ctx) {
-  if (!o->use_graph || ctx.profile != 0 || o->sharded()) return false;
+  if (!o->use_graph || ctx.profile != 0 || o->sharded() || o->wb.active) return false;
   FLOAM_HIP(hipStreamBeginCapture(ctx.stream, hipStreamCaptureModeRelaxed));
   capture_state().active = true;
   return true;
@@ -969,7 +954,7 @@ void odom_map_update(floam_odom* o, DeviceCtx& ctx, const MapUpdatePlan& P, size
       gcount[1] = grid_count_job(o->gS);
     }
     map_merge_launch(o->vs, o->mms, P.je, P.js, P.ke, P.ks, &o->ds.p->kf_flag, (unsigned)o->issued,
-                     o->map_force_full, o->map_violate_mod, fuse ? gcount : nullptr, st, o->mm_per);
+                     o->map_force_full, o->map_violate_mod, fuse ? gcount : nullptr, st);
     o->mkcur ^= 1;
   } else {
     voxel2_launch(o->vs, P.je, P.js, st, &o->ds.p->kf_flag, true);
@@ -1057,7 +1042,7 @@ floam_status odom_update_deskew(floam_odom* o, floam_cloud* edge, floam_cloud* s
   const int ring = odom_begin(o, ctx);
   const int ne_ub = (int)cloud_ub(edge), ns_ub = (int)cloud_ub(surf);
   const bool captured = odom_capture_begin(o, ctx);
-  static const bool nop = std::getenv("FLOAM_UPDATE_NOP") != nullptr;
+  static const bool nop = FLOAM_DIAG_ENV("FLOAM_UPDATE_NOP") != nullptr;
   if (nop) update_nop_launch(ctx.stream);
   try {
     if (o->optimization_count > 2) o->optimization_count--;
@@ -1122,7 +1107,7 @@ void set_last_error(const std::string& m) { t_err = m; }
 extern "C" {
 
 const char* floam_last_error(void) { return t_err.c_str(); }
-const char* floam_version(void) { return "floam_amd 0.3.0 (gfx950, ABI 3)"; }
+const char* floam_version(void) { return "floam_amd 0.4.0 (gfx950, ABI 3)"; }
 int floam_abi_version(void) { return FLOAM_ABI_VERSION; }
 void floam_reset_process_state(void) { g_keyframe_first = true; }
 
@@ -1468,12 +1453,10 @@ floam_status floam_odom_create(const floam_lidar_params* p, double map_resolutio
     o->lp = *p;
     o->map_resolution = map_resolution;
     if (const char* e = std::getenv("FLOAM_MAP_MERGE")) o->map_merge = e[0] != '0';
-    if (const char* e = std::getenv("FLOAM_MAP_FULL")) o->map_force_full = e[0] == '1';
-    if (const char* e = std::getenv("FLOAM_MM_VIOLATE")) o->map_violate_mod = std::atoi(e);
-    if (const char* e = std::getenv("FLOAM_MM_PER")) o->mm_per = std::atoi(e) == 2 ? 2 : 4;
-    if (const char* e = std::getenv("FLOAM_LM_FAIL_TEST")) o->lmb.fail_test = std::atoi(e) != 0;
-    if (const char* e = std::getenv("FLOAM_LM_PRE0")) o->lm_pre0 = e[0] != '0';
-    if (const char* e = std::getenv("FLOAM_GRID_COUNT_FUSED")) o->grid_count_off = std::atoi(e) == 0;
+    if (const char* e = FLOAM_DIAG_ENV("FLOAM_MAP_FULL")) o->map_force_full = e[0] == '1';
+    if (const char* e = FLOAM_DIAG_ENV("FLOAM_MM_VIOLATE")) o->map_violate_mod = std::atoi(e);
+    if (const char* e = FLOAM_DIAG_ENV("FLOAM_LM_FAIL_TEST")) o->lmb.fail_test = std::atoi(e) != 0;
+    if (const char* e = FLOAM_DIAG_ENV("FLOAM_PEER_DELAY_US")) o->lmb.peer_delay_us = std::atoi(e);
     std::string l = loss ? loss : "";
     std::transform(l.begin(), l.end(), l.begin(), [](unsigned char c) { return (char)std::tolower(c); });
     o->huber = (l == "huber");   // any other string: no robust loss (Q3)
@@ -1816,18 +1799,22 @@ floam_status floam_odom_set_shard(floam_odom* o, int rank, int world, const void
   });
 }
 
-// peer sharding: this rank's exchange buffer (zeroed: tag 0 never matches, epochs start at 8), allocated once.
-// Uncached device memory: the other ranks poll it over xGMI with system-scope loads, which are served from L2
+// peer sharding: this rank's exchange buffer (zeroed: the exchange tags are odd, lm.hip peer_exchange), allocated
+// once.  Uncached device memory: the other ranks poll it over xGMI with system-scope loads, which are served from L2
 // (MI355X_MICROARCH.md: sc1 / sc0 sc1 loads bypass L1 only), and coarse-grained memory of another GPU gives no
-// cross-device coherence inside a kernel; uncached, every store and poll goes to this GPU's memory
+// cross-device coherence inside a kernel; uncached, every store and poll goes to this GPU's memory.  Without uncached
+// memory peer sharding is refused (FLOAM_ERR_UNSUPPORTED: the caller takes the RCCL form) — a cached buffer would
+// show up as sporadic 20-s hand-off timeouts, not as an error.
 void shard_xbuf(floam_odom* o) {
   if (o->xbuf) return;
   FLOAM_HIP(hipSetDevice(o->device));
-  if (hipExtMallocWithFlags(reinterpret_cast<void**>(&o->xbuf), sizeof(unsigned long long) * kShardXchgWords,
-                            hipDeviceMallocUncached) !=
-      hipSuccess) {
+  const hipError_t e = hipExtMallocWithFlags(reinterpret_cast<void**>(&o->xbuf),
+                                             sizeof(unsigned long long) * kShardXchgWords, hipDeviceMallocUncached);
+  if (e != hipSuccess) {
     (void)hipGetLastError();
-    FLOAM_HIP(hipMalloc(&o->xbuf, sizeof(unsigned long long) * kShardXchgWords));
+    o->xbuf = nullptr;
+    throw Error(FLOAM_ERR_UNSUPPORTED, std::string("peer sharding needs uncached device memory: ") +
+                                           hipGetErrorString(e));
   }
   FLOAM_HIP(hipMemset(o->xbuf, 0, sizeof(unsigned long long) * kShardXchgWords));
 }
@@ -1885,6 +1872,14 @@ floam_status floam_odom_set_shard_peers(floam_odom* o, int rank, int world, cons
         P.buf[r] = static_cast<const unsigned long long*>(p);
       }
     }
+    // every rank starts a fresh exchange sequence: the counter (LMState::xseq) at zero and its own buffer zeroed, so
+    // the tags of all ranks agree whatever each rank ran before (the ranks then meet at a barrier before updating)
+    DeviceCtx& ctx = ctx_for(o->device);
+    o->lm.reserve(1);
+    FLOAM_HIP(hipMemsetAsync(reinterpret_cast<char*>(o->lm.p) + offsetof(LMState, xseq), 0, sizeof(unsigned),
+                             ctx.stream));
+    FLOAM_HIP(hipMemsetAsync(o->xbuf, 0, sizeof(unsigned long long) * kShardXchgWords, ctx.stream));
+    FLOAM_HIP(hipStreamSynchronize(ctx.stream));
     o->peers = P;
     o->rank = rank;
     o->world = world;

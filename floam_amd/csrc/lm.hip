@@ -784,10 +784,11 @@ __device__ __forceinline__ void stage_state(const LMState* __restrict__ st, LMSt
   unsigned* dst = reinterpret_cast<unsigned*>(&sst);
   for (int w = threadIdx.x; w < kStateWords; w += blockDim.x) dst[w] = src[w];
 }
+// (every word but xfail, which only a block reporting a timed-out hand-off writes)
 __device__ __forceinline__ void publish_state(const LMState& sst, LMState* __restrict__ st) {
   const unsigned* src = reinterpret_cast<const unsigned*>(&sst);
   unsigned* dst = reinterpret_cast<unsigned*>(st);
-  for (int w = threadIdx.x; w < kStateWords; w += blockDim.x) dst[w] = src[w];
+  for (int w = threadIdx.x; w < kPublishWords; w += blockDim.x) dst[w] = src[w];
 }
 
 __device__ __forceinline__ unsigned long long granule(unsigned tag, unsigned data) {
@@ -823,11 +824,9 @@ __device__ __forceinline__ bool sweep_granules(const unsigned long long* __restr
 
 // evaluation blocks that hold records: one record slot per record thread while they fit, at most nblk (a function of
 // the device count only, so the partition and the reduction order never depend on the host's upper bounds)
-// (rpt: records per record thread before another block is taken — 1 by default; FLOAM_LM_RPT=2 halves the active
-// blocks, A/B)
 template <int NR>
-__device__ __forceinline__ int active_blocks(int total, int nblk, int rpt) {
-  return max(1, min(nblk, (total + NR * rpt - 1) / (NR * rpt)));
+__device__ __forceinline__ int active_blocks(int total, int nblk) {
+  return max(1, min(nblk, (total + NR - 1) / NR));
 }
 
 // record threads of a solve block: GRAM — waves 0..2 hold edge records and wave 3 forms the surf half from G;
@@ -854,54 +853,88 @@ struct LMArgs {
   unsigned* ticket;                // sharded: arrival ticket
   unsigned long long* dbg;         // FLOAM_DEBUG_STAMPS: block 0's segment times (diagnostic, normally null)
   int fail_test;                   // LMBuffers::fail_test: report the first hand-off as timed out (tests)
-  const double* epart;             // pre0: [nbe][29] iteration zero's edge sums by geometry block, else null
-  int nbe;
   // peer sharding (world > 1): this rank's exchange granules [2][2 * LM_NSUM] and every rank's, peer-mapped, rank order
   int world;
   unsigned long long* xme;
   const unsigned long long* xpeer[kMaxShardRanks];
-  int rpt;                         // records per record thread before another block is taken (active_blocks)
+  unsigned peer_delay;             // (diagnostic build, tests) 100-MHz ticks the non-zero blocks wait before a peer poll
 };
 
 // Peer sharding: after a block has its rank's 29 sums (block partials + the surf half), block 0 publishes them as
 // tagged granules in this rank's exchange buffer and every block gathers all ranks' granules (system scope: the buffers
 // of the other ranks are on other GPUs, read through xGMI) and sums them in rank order — every block of every rank the
-// same bits, so every rank takes the same LM decisions.  Slot reuse follows the block hand-off's parity argument one
-// level up: a rank's total of evaluation k + 1 exists only after each of its blocks has read every rank's evaluation
-// k, and a rank overwrites its evaluation-k slot at k + 2, after it has seen every rank's k + 1.  The wait is bounded
-// in time (~20 s: ranks in other processes may be far apart at the first solve), not in polls.
-__device__ __forceinline__ bool peer_exchange(const LMArgs& a, int it, unsigned tag, double* s_sums, unsigned* s_x) {
+// same bits, so every rank takes the same LM decisions.
+// Slot and tag come from the exchange counter xs (LMState::xseq): the evaluations exchanged since
+// floam_odom_set_shard_peers reset it on every rank, continued across solves — the same sequence on every rank, since
+// every rank takes the same decisions.  Slot xs & 1, tag 2 xs + 1 (odd: the zeroed buffer never matches).  Reuse: a
+// rank overwrites the slot of exchange xs only at xs + 2, after it has read every rank's granules of xs + 1, and a rank
+// publishes xs + 1 only after each of its blocks has finished reading xs — inside a solve because the block all-gather
+// of the evaluation behind xs + 1 waits for every block of the rank, across solves because the next solve is a later
+// launch on the rank's stream.  (A per-solve counter broke the second case: after a solve that ended on an even
+// evaluation the next solve's first exchange reused slot 0 while a late block of another rank could still be polling
+// it for the old tag.)  The wait is bounded in time (~20 s: ranks in other processes may be far apart at the first
+// solve), not in polls.
+__device__ __forceinline__ bool peer_exchange(const LMArgs& a, unsigned xs, double* s_sums, unsigned* s_x) {
+  constexpr int kG = 2 * LM_NSUM;   // granules per rank and slot
+  static_assert(kMaxShardRanks * kG <= 2 * kTB, "every rank's granules: at most two per thread");
+  static_assert(2 * kG <= kShardXchgWords, "two slots in the exchange buffer");
   const int tid = (int)threadIdx.x;
-  const int slot = (it & 1) * 2 * LM_NSUM;
-  if (blockIdx.x == 0 && tid < 2 * LM_NSUM) {
+  const int slot = (int)(xs & 1u) * kG;
+  const unsigned tag = 2u * xs + 1u;
+  if (blockIdx.x == 0 && tid < kG) {
     const int c = tid >> 1, h = tid & 1;
     const unsigned long long b = (unsigned long long)__double_as_longlong(s_sums[c]);
     __hip_atomic_store(&a.xme[slot + tid], granule(tag, h ? (unsigned)(b >> 32) : (unsigned)b), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  bool ok = true;
-  if (tid < a.world * 2 * LM_NSUM) {
-    const int r = tid / (2 * LM_NSUM), j = tid - r * 2 * LM_NSUM;
-    const unsigned long long* src = a.xpeer[r] + slot + j;
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    for (;;) {
-      const unsigned long long v = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      if ((unsigned)(v >> 32) == tag) {
-        s_x[tid] = (unsigned)v;
-        break;
-      }
-      if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000000ull) {   // 100 MHz: 20 s
-        ok = false;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
+#ifdef FLOAM_DIAG
+  if (a.peer_delay && blockIdx.x != 0) {   // (tests: a late block, the case the slot reuse argument must cover)
+    const unsigned long long d0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - d0 < a.peer_delay) __builtin_amdgcn_s_sleep(8);
+  }
+#endif
+  // granules j = tid and tid + kTB of the world x kG (rank r's granule j - r kG)
+  const int n = a.world * kG;
+  const unsigned long long* src[2] = {nullptr, nullptr};
+  unsigned pend = 0;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int j = tid + u * kTB;
+    if (j < n) {
+      const int r = j / kG;
+      const unsigned long long* base = a.xpeer[0];
+#pragma unroll
+      for (int q = 1; q < kMaxShardRanks; ++q)   // (selected, not indexed: the argument array stays in registers)
+        if (q == r) base = a.xpeer[q];
+      src[u] = base + slot + (j - r * kG);
+      pend |= 1u << u;
     }
+  }
+  bool ok = true;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (pend) {
+    unsigned long long v[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)   // both loads in flight before either is examined
+      v[u] = (pend >> u) & 1u ? __hip_atomic_load(src[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      if (((pend >> u) & 1u) && (unsigned)(v[u] >> 32) == tag) {
+        s_x[tid + u * kTB] = (unsigned)v[u];
+        pend &= ~(1u << u);
+      }
+    if (!pend) break;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000000ull) {   // 100 MHz: 20 s
+      ok = false;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(2);
   }
   if (__syncthreads_or(!ok)) return false;
   if (tid < LM_NSUM) {
     double v = 0.0;
     for (int r = 0; r < a.world; ++r) {
-      const int g = r * 2 * LM_NSUM + 2 * tid;
+      const int g = r * kG + 2 * tid;
       v += __longlong_as_double((long long)(((unsigned long long)s_x[g + 1] << 32) | s_x[g]));
     }
     s_sums[tid] = v;
@@ -971,7 +1004,7 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
   }
   const int ne = min(ne_dev, a.ne_ub);
   const int total = ne + (GRAM ? 0 : min(ns_dev, a.ns_ub));
-  const int nact = active_blocks<NR>(total, nblk, a.rpt);
+  const int nact = active_blocks<NR>(total, nblk);
   if (blk >= nact) return;   // no records: nobody waits for this block
   if (tid < kStateWords) reinterpret_cast<unsigned*>(&sst)[tid] = sw;
   const int stride = nact * NR;
@@ -981,6 +1014,7 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
   if (sst.done) return;   // (never after lm_reset)
   if (GRAM) gram_unpack(gv, G, o);
   const unsigned ep = sst.epoch;
+  const unsigned xs0 = sst.xseq;   // peer sharding: this solve's first exchange
 #if FLOAM_LM_STATE_REGS
   LMState s;   // wave 0: the whole LM state in registers for the whole solve
   if (tid < 64) s = sst;
@@ -990,21 +1024,9 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
   unsigned* tab = s_tab;   // [nact][2 * LM_NSUM]
   const int ngr = nact * 2 * LM_NSUM;
   unsigned long long tm[4] = {0, 0, 0, 0};
-  // pre0: iteration zero's edge half, summed over the geometry blocks' partials in block order (every block the same
-  // bits); the surf half is formed from G below as in every evaluation
-  __shared__ double s_esum[LM_NSUM];
   __shared__ unsigned s_xch[kMaxShardRanks * 2 * LM_NSUM];   // peer sharding: every rank's sums (u32 halves)
-#ifdef FLOAM_LM_NO_PRE0   // (A/B builds only: the pre0 paths compiled out)
-  constexpr bool pre0 = false;
-#else
-  const bool pre0 = GRAM && !HUBER && a.epart != nullptr;
-#endif
-#ifdef FLOAM_LM_NO_PEER   // (A/B builds only: the peer exchange compiled out)
-  constexpr bool peers = false;
-#else
   const bool peers = a.world > 1;
-#endif
-  if (pre0) reduce_blocks([&](int c, int b) { return a.epart[b * LM_NSUM + c]; }, a.nbe, s_esum);
+  unsigned nx = 0;   // evaluations exchanged with the other ranks in this solve
   const unsigned long long t_loop = __builtin_amdgcn_s_memrealtime();
   int failed_at = -1;   // evaluation whose granules never arrived (never expected)
   for (int it = 0; it < 5; ++it) {
@@ -1013,14 +1035,7 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
     if (s_done) break;
     unsigned long long t1 = t0, t2 = t0;
     unsigned tag = ep + (unsigned)it;
-    if (pre0 && it == 0) {   // (block-uniform) no records to evaluate, nothing to hand off: the surf half, then control
-      if (tid >= NR) surf_sums_wave(s_pt, o, G, (double)sst.corr_surf, s_ssum, lane);
-      if (__syncthreads_or(a.fail_test != 0)) {
-        failed_at = it;
-        break;
-      }
-      if (tid < LM_NSUM) s_sums[tid] = s_esum[tid] + s_ssum[tid];   // edge + surf
-    } else {
+    {
       double acc[LM_NSUM];
       if (tid < NR) {
         R x[7];
@@ -1061,9 +1076,12 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
     __syncthreads();
     // (one call site each for the exchange and the control step: a second inlined copy of the control step doubled
     // the kernel's code, 16k instructions against 8k, past what the instruction cache holds)
-    if (peers && !peer_exchange(a, it, tag, s_sums, s_xch)) {
-      failed_at = it;
-      break;
+    if (peers) {
+      if (!peer_exchange(a, xs0 + nx, s_sums, s_xch)) {
+        failed_at = it;
+        break;
+      }
+      ++nx;
     }
     const unsigned long long t3 = __builtin_amdgcn_s_memrealtime();
     if (tid < 64) {   // the next point (if the solve goes on)
@@ -1080,18 +1098,27 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
       tm[0] += t1 - t0; tm[1] += t2 - t1; tm[2] += t3 - t2; tm[3] += t4 - t3;
     }
   }
+  // a timed-out hand-off in ANY block fails the update: xfail, which the state write-back never overwrites, is read
+  // by the status gather (the solve's pose is not taken, the handle is poisoned on the host)
+  if (failed_at >= 0 && tid == 0) __hip_atomic_store(&a.st->xfail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (blk != 0) return;
 #if FLOAM_LM_STATE_REGS
   if (failed_at >= 0 && tid < 64) {   // end the solve, report through n_res
     s.done = 1;
     s.n_res = -1;
   }
-  if (tid == 0) store_state_core(sst, s);
+  if (tid == 0) {
+    store_state_core(sst, s);
+    sst.xseq = xs0 + nx;
+  }
 #else
   __syncthreads();   // (wave 0's last write-back)
-  if (failed_at >= 0 && tid == 0) {   // end the solve, report through n_res
-    sst.done = 1;
-    sst.n_res = -1;
+  if (tid == 0) {
+    if (failed_at >= 0) {   // end the solve, report through n_res
+      sst.done = 1;
+      sst.n_res = -1;
+    }
+    sst.xseq = xs0 + nx;
   }
 #endif
   __syncthreads();
@@ -1135,7 +1162,7 @@ __global__ __launch_bounds__(kTB) void lm_shard_eval(LMArgs a, int k) {
   const bool done = s_done != 0;
   const int ne = min(*a.d_ne, a.ne_ub);
   const int total = ne + (GRAM ? 0 : min(*a.d_ns, a.ns_ub));
-  const int nact = active_blocks<NR>(total, nblk, a.rpt);
+  const int nact = active_blocks<NR>(total, nblk);
   if (!done && blk < nact) {   // block-uniform
     double acc[LM_NSUM];
     if (tid < NR) {
@@ -1223,15 +1250,10 @@ __global__ void lm_trace(const LMState* __restrict__ st, const int* __restrict__
 }
 
 LMArgs make_args(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const CorrSet& cs, const int* d_ns,
-                 int ns_ub, LMBuffers& b, unsigned long long* dbg, bool pre0 = false, const ShardPeers* peers = nullptr) {
+                 int ns_ub, LMBuffers& b, unsigned long long* dbg, const ShardPeers* peers = nullptr) {
   LMArgs a{d_st, ce.rec.p, ce.valid.p, ce.cap, d_ne, std::max(ne_ub, 0), cs.rec.p, cs.valid.p, cs.cap, d_ns,
-           std::max(ns_ub, 0), b.gmat.p, b.part.p, b.partials.p, b.sums.p, b.ticket.p, dbg, b.fail_test,
-           pre0 ? b.epart.p : nullptr, pre0 ? b.epart_blocks : 0, 1, nullptr, {}, 1};
-  static const int rpt = [] {
-    const char* e = std::getenv("FLOAM_LM_RPT");
-    return e ? std::max(1, std::min(8, std::atoi(e))) : 1;
-  }();
-  a.rpt = rpt;
+           std::max(ns_ub, 0), b.gmat.p, b.part.p, b.partials.p, b.sums.p, b.ticket.p, dbg, b.fail_test, 1, nullptr,
+           {}, (unsigned)std::max(b.peer_delay_us, 0) * 100u};
   if (peers && peers->world > 1) {
     a.world = peers->world;
     a.xme = peers->mine;
@@ -1271,9 +1293,9 @@ void LMBuffers::reserve(hipStream_t st) {
 
 void lm_solve_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const CorrSet& cs,
                      const int* d_ns, int ns_ub, int mode, LMBuffers& b, hipStream_t st, unsigned long long* dbg,
-                     bool pre0, const ShardPeers* peers) {
+                     const ShardPeers* peers) {
   b.reserve(st);
-  const LMArgs a = make_args(d_st, ce, d_ne, ne_ub, cs, d_ns, ns_ub, b, dbg, pre0 && (mode & LM_GRAM) != 0, peers);
+  const LMArgs a = make_args(d_st, ce, d_ne, ne_ub, cs, d_ns, ns_ub, b, dbg, peers);
   // the active blocks (at most 64 or 128 blocks of 256 threads on 256 CUs) are co-resident: checked by the caller
   // through lm_solve_coresident before it chooses this path
   if (mode & LM_GRAM) {

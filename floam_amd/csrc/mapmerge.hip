@@ -36,6 +36,7 @@ namespace floam {
 
 namespace {
 constexpr int kTB = 256;
+constexpr int kMergePer = 4;   // merged elements per thread: 1024-element tiles (512 measured the same)
 constexpr unsigned long long kNone = ~0ull;   // no element (never an index or a sort key: both < 2^32)
 
 __global__ __launch_bounds__(kTB) void mm_keys(VoxelJobDev A, VoxelJobDev B, const float* __restrict__ partials,
@@ -285,7 +286,7 @@ __device__ __forceinline__ void mm_merge_job(const VoxelJobDev& JJ, const MapKey
                                              int* __restrict__ ctl, unsigned long long* __restrict__ mstatus,
                                              int tiles_cap, int tilesA,
                                              const unsigned* __restrict__ radix_ctl, const int* __restrict__ gate,
-                                             unsigned seq, int violate_mod, int count_grid, int by_index,
+                                             unsigned seq, int violate_mod, int count_grid,
                                              int stamps) {
   const unsigned long long T0 = mm_now(stamps);
   // prologue loads first, so they travel with the ticket: the counts, the gate and the status gather's verdict words
@@ -308,7 +309,7 @@ __device__ __forceinline__ void mm_merge_job(const VoxelJobDev& JJ, const MapKey
   // tile's lookback only waits on tiles that are already running (HIP promises no dispatch order)
   __shared__ int s_tile;
   if (threadIdx.x == 0)
-    s_tile = by_index ? (job ? (int)blockIdx.x - tilesA : (int)blockIdx.x) : atomicAdd(&ctl[kMergeTicketWord + 32 * job], 1);
+    s_tile = atomicAdd(&ctl[kMergeTicketWord + 32 * job], 1);
   const int njb = job ? (int)gridDim.x - tilesA : tilesA;   // this job's blocks
   const int t = threadIdx.x;
   __syncthreads();
@@ -674,13 +675,13 @@ __global__ __launch_bounds__(kTB) void mm_merge(VoxelJobDev A, VoxelJobDev B, Ma
                                                 int tiles_cap, int tilesA,
                                                 const unsigned* __restrict__ radix_ctl, const int* __restrict__ gate,
                                                 unsigned seq, int violate_mod, GridCountDev GA, GridCountDev GB,
-                                                int count_grid, int by_index, int stamps) {
+                                                int count_grid, int stamps) {
   if ((int)blockIdx.x < tilesA)   // (block-uniform)
     mm_merge_job<PER>(A, KA, GA, 0, skeys, svals, ctl, mstatus, tiles_cap, tilesA, radix_ctl, gate, seq, violate_mod,
-                      count_grid, by_index, stamps);
+                      count_grid, stamps);
   else
     mm_merge_job<PER>(B, KB, GB, 1, skeys, svals, ctl, mstatus, tiles_cap, tilesA, radix_ctl, gate, seq, violate_mod,
-                      count_grid, by_index, stamps);
+                      count_grid, stamps);
 }
 
 }  // namespace
@@ -708,7 +709,7 @@ MergeCheck merge_check(MapMergeScratch& ms, unsigned seq) {
 }
 
 void mm_stamps_print() {
-  if (!std::getenv("FLOAM_MM_STAMPS")) return;
+  if (!FLOAM_DIAG_ENV("FLOAM_MM_STAMPS")) return;
   static unsigned q[2][kMmStampTiles][6];
   FLOAM_HIP(hipDeviceSynchronize());
   FLOAM_HIP(hipMemcpyFromSymbol(q, HIP_SYMBOL(g_mm_st), sizeof(q)));
@@ -746,12 +747,11 @@ void mm_stamps_print() {
 
 void map_merge_launch(VoxelScratch2& vs, MapMergeScratch& ms, const VoxelJob& a, const VoxelJob& b, const MapKeys& ka,
                       const MapKeys& kb, const int* gate, unsigned seq, bool force_full, int violate_mod,
-                      const GridCountDev* grids, hipStream_t st, int per) {
+                      const GridCountDev* grids, hipStream_t st) {
   const VoxelJobDev A = to_dev(a, 0);
   const VoxelJobDev B = to_dev(b, a.n0_ub + a.n1_ub);
   const int nA = a.n0_ub + a.n1_ub, nB = b.n0_ub + b.n1_ub, n = std::max(nA + nB, 1);
-  per = per == 2 ? 2 : 4;   // merged elements per tile: 256 threads x per
-  const int tile = kTB * per;
+  const int tile = kTB * kMergePer;
   const int tilesA = std::max(1, (int)div_up(std::max(nA, 1), tile));
   const int tilesB = std::max(1, (int)div_up(std::max(nB, 1), tile));
   ms.reserve(std::max(tilesA, tilesB), st);
@@ -780,18 +780,12 @@ void map_merge_launch(VoxelScratch2& vs, MapMergeScratch& ms, const VoxelJob& a,
     if (bucket) bucket_seed_launch(ms.bs, vs.s.k0.p, vs.overflow.p + 2, n, st, gate);
   }
   const bool wb = prof_wb_enabled();   // (diagnostic: the merge's own write bytes, profwb.hpp)
-  static const int stamps = std::getenv("FLOAM_MM_STAMPS") ? 1 : 0;
+  static const int stamps = FLOAM_DIAG_ENV("FLOAM_MM_STAMPS") ? 1 : 0;
   if (wb) prof_l2_writeback(st);
-  if (per == 2)
-    hipLaunchKernelGGL(mm_merge<2>, dim3(tilesA + tilesB), dim3(kTB), 0, st, A, B, ka, kb, vs.s.k0.p, vs.s.v0.p,
+  hipLaunchKernelGGL(mm_merge<kMergePer>, dim3(tilesA + tilesB), dim3(kTB), 0, st, A, B, ka, kb, vs.s.k0.p, vs.s.v0.p,
                        ms.ctl.p, ms.status.p, ms.tiles_cap, tilesA, vs.rs.ctl.p, gate, seq, violate_mod,
                        grids ? grids[0] : GridCountDev{}, grids ? grids[1] : GridCountDev{}, grids ? 1 : 0,
-                       tile_by_index() ? 1 : 0, stamps);
-  else
-    hipLaunchKernelGGL(mm_merge<4>, dim3(tilesA + tilesB), dim3(kTB), 0, st, A, B, ka, kb, vs.s.k0.p, vs.s.v0.p,
-                       ms.ctl.p, ms.status.p, ms.tiles_cap, tilesA, vs.rs.ctl.p, gate, seq, violate_mod,
-                       grids ? grids[0] : GridCountDev{}, grids ? grids[1] : GridCountDev{}, grids ? 1 : 0,
-                       tile_by_index() ? 1 : 0, stamps);
+                       stamps);
   FLOAM_LAUNCH_CHECK();
   if (wb) prof_l2_writeback(st);
 }

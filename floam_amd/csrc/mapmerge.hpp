@@ -53,7 +53,7 @@ MergeCheck merge_check(MapMergeScratch& ms, unsigned seq);
 // handle was created with FLOAM_MM_PER=2 — small tiles put more runs across tile edges, which the tests exercise).
 void map_merge_launch(VoxelScratch2& vs, MapMergeScratch& ms, const VoxelJob& a, const VoxelJob& b, const MapKeys& ka,
                       const MapKeys& kb, const int* gate, unsigned seq, bool force_full, int violate_mod,
-                      const GridCountDev* grids, hipStream_t st, int per = 4);
+                      const GridCountDev* grids, hipStream_t st);
 
 void mm_stamps_print();   // FLOAM_MM_STAMPS (diagnostic)
 

@@ -790,16 +790,13 @@ template <bool EDGE, typename R>
 __device__ __forceinline__ bool geom_fit(const R (&P)[5][3], float4 pq, double* __restrict__ rec, int cap, int i,
                                          double* __restrict__ w, const double* o);
 
-// FUSED (FLOAM_KNN_FUSED_PROTO=1, a measurement prototype): lane 0 of the group also runs the
-// query's line / plane fit and writes its record (the geometry launch still runs after it — the prototype prices
-// the fits inside the search, a lower bound of a fused kernel, which would also need the surf Gram reduction)
 // STOP (diagnostic, FLOAM_KNN_STAGES: the per-round-trip read attribution of DESIGN.md §3) ends each query after
 // its first STOP dependent memory round trips — 1: the query load and transform; 2: + the coarse probes of the fine
 // block; 3: + stage 1's candidate loads; 4: + stage 2 — and writes only a flag derived from what it loaded
-template <int G, int U, int NB, bool FUSED = false, int STOP = 0>
+template <int G, int U, int NB, int STOP = 0>
 __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArgs& A, int gid, int ngroups,
                                           int lane, bool gate, int rank, int world, int* __restrict__ s_pre,
-                                          int* __restrict__ s_start, int* __restrict__ s_cc, bool edge = true) {
+                                          int* __restrict__ s_start, int* __restrict__ s_cc) {
   const int n = min(*A.d_n, A.n_ub);
   const int lo = (int)(((long long)n * rank) / world), hi = (int)(((long long)n * (rank + 1)) / world);
   // grid-stride over the queries the device holds (the host only knows an upper bound)
@@ -882,29 +879,6 @@ __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArg
             A.nnsqd[lane * A.cap + i] = __uint_as_float((unsigned)(kk >> 32));
           }
         }
-        if (FUSED) {   // (prototype) the 5 neighbours' coordinates to every lane of the group, the fit on lane 0
-          float mx = 0.f, my = 0.f, mz = 0.f;
-          if (lane < 5) {
-            unsigned long long kk = t.k[0];
-#pragma unroll
-            for (int k = 1; k < 5; ++k)
-              if (lane == k) kk = t.k[k];
-            const float4 m = A.map[(int)(kk & 0xFFFFFFFFull)];
-            mx = m.x; my = m.y; mz = m.z;
-          }
-          double P[5][3];
-#pragma unroll
-          for (int j = 0; j < 5; ++j) {
-            P[j][0] = __shfl(mx, j, G);
-            P[j][1] = __shfl(my, j, G);
-            P[j][2] = __shfl(mz, j, G);
-          }
-          if (lane == 0) {
-            const float4 pq = *reinterpret_cast<const float4*>(&A.q[i].x);
-            if (edge) geom_fit<true, double>(P, pq, A.rec, A.cap, i, nullptr, nullptr);
-            else geom_fit<false, double>(P, pq, A.rec, A.cap, i, nullptr, nullptr);
-          }
-        }
       }
     }
     if (lane == 0) A.valid[i] = (uint8_t)flags;
@@ -914,7 +888,7 @@ __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArg
 // Edge and surf kNN in one launch: blocks [0, nbE) run edge groups, the others surf groups.  The launch also starts
 // the solve (lm_init folded in): block 0 resets the LM state and, for the first solve of an update, stores the
 // prediction x0 that every block uses for its transforms (the others never read st->x in that case).
-template <int G, int U, int W, int NB, bool FUSED = false, int STOP = 0>
+template <int G, int U, int W, int NB, int STOP = 0>
 __global__ __launch_bounds__(kTB, W) void knn_kernel(LMState* __restrict__ st, const double* __restrict__ x0_dev,
                                                   CorrArgs E, CorrArgs S, int nbE,
                                                   const int* __restrict__ d_me, const int* __restrict__ d_ms,
@@ -949,8 +923,8 @@ __global__ __launch_bounds__(kTB, W) void knn_kernel(LMState* __restrict__ st, c
   const int nq = min(*A.d_n, A.n_ub);
   const int nact = min(nb, (int)(((long long)nq * G + kTB - 1) / kTB));
   if (p < nact) p = xcd_block(p, nact);
-  knn_group<G, U, NB, FUSED, STOP>(pose, A, (p * kTB + (int)threadIdx.x) / G, nb * (kTB / G), lane, gate, rank, world,
-                             s_pre[g], s_start[g], s_cc[g], edge);
+  knn_group<G, U, NB, STOP>(pose, A, (p * kTB + (int)threadIdx.x) / G, nb * (kTB / G), lane, gate, rank, world,
+                            s_pre[g], s_start[g], s_cc[g]);
 }
 
 // Pass 2: line / plane geometry, one query per lane (all 64 lanes busy), in R = double (the reference's precision)
@@ -1109,7 +1083,7 @@ __device__ __forceinline__ void gram_pair(int e, int& i, int& j) {   // upper-tr
 template <typename R>
 __global__ __launch_bounds__(kTB) void geom_kernel(LMState* __restrict__ st, CorrArgs E, CorrArgs S, int nbE,
                                                    double* __restrict__ gpart, double* __restrict__ gmat,
-                                                   unsigned* __restrict__ gcnt, double* __restrict__ epart) {
+                                                   unsigned* __restrict__ gcnt) {
 #ifdef FLOAM_GEOM_STAMPS
   GEOM_STAMP(t0, 0);
   unsigned long long tq[2] = {t0, t0};
@@ -1118,50 +1092,9 @@ __global__ __launch_bounds__(kTB) void geom_kernel(LMState* __restrict__ st, Cor
 #define GEOM_TQ
 #endif
   if ((int)blockIdx.x < nbE) {
-    if (!epart) {
-      geom_query<true, R>(st, E, blockIdx.x * blockDim.x + threadIdx.x, nullptr, nullptr GEOM_TQ);
+    geom_query<true, R>(st, E, blockIdx.x * blockDim.x + threadIdx.x, nullptr, nullptr GEOM_TQ);
 #ifdef FLOAM_GEOM_STAMPS
-      geom_row(t0, tq[0], tq[1], tq[1], tq[1], 0);
-#endif
-      return;
-    }
-    // the record's residual and Jacobian at the solve's starting point (EdgeAnalyticCostFunction::Evaluate,
-    // src/lidarOptimization.cpp:12-43): iteration zero's edge half of the next solve, summed per block in a fixed
-    // order (wave butterflies, then the 4 waves in order) into epart[block]
-    double x[7];
-#pragma unroll
-    for (int k = 0; k < 7; ++k) x[k] = st->x[k];
-    double r9[9];
-    const bool ok = geom_query<true, R>(st, E, blockIdx.x * blockDim.x + threadIdx.x, r9, nullptr GEOM_TQ);
-    double acc[LM_NSUM];
-#pragma unroll
-    for (int k = 0; k < LM_NSUM; ++k) acc[k] = 0.0;
-    if (ok) {
-      double J[6];
-      const double r = lmev::edge_residual<double>(x, r9, J);
-      lmev::accumulate_residual<false, double>(acc, r, J);
-    }
-    __shared__ double s_e[kTB / 64][LM_NSUM];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-#pragma unroll
-    for (int k = 0; k < LM_NSUM; ++k) {
-      double v = acc[k];
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-      if (lane == 0) s_e[wv][k] = v;
-    }
-#ifdef FLOAM_GEOM_STAMPS
-    GEOM_STAMP(t3, __double_as_longlong(acc[0]) & 1);
-#endif
-    __syncthreads();
-    if (threadIdx.x < LM_NSUM) {
-      double v = s_e[0][threadIdx.x];
-#pragma unroll
-      for (int k = 1; k < kTB / 64; ++k) v += s_e[k][threadIdx.x];
-      epart[blockIdx.x * LM_NSUM + threadIdx.x] = v;
-    }
-#ifdef FLOAM_GEOM_STAMPS
-    geom_row(t0, tq[0], tq[1], t3, t3, 0);
+    geom_row(t0, tq[0], tq[1], tq[1], tq[1], 0);
 #endif
     return;
   }
@@ -1512,7 +1445,7 @@ __device__ __forceinline__ void gather_block(const LMState* __restrict__ lm, con
     out->prof[1] = prof ? prof[1] : 0ull;
     out->kf_flag = 0;
     s->kf_flag = 0;   // (the map update's gate)
-    if (lm->n_res < 0) s->failed = 1;   // an abandoned solve: its pose is not taken, no keyframe, no
+    if (lm->n_res < 0 || lm->xfail) s->failed = 1;   // an abandoned solve: its pose is not taken, no keyframe, no
     if (!s->failed) {                   // map update — for this update and every later one; the host raises it
       if (mode & GATHER_FINISH) {
         if (mode & GATHER_AFTER_MID) s->last_odom = s->mid;
@@ -1619,15 +1552,6 @@ static void corr_args(const QuerySet& qe, const Grid& ge, CorrSet& ce, const Que
                cs.valid.p, cs.nnxyz.p, cs.trace ? cs.nnidx.p : nullptr, cs.trace ? cs.nnsqd.p : nullptr, cs.cap};
 }
 
-// stage-1 block edge in fine cells (FLOAM_KNN_BLOCK=2|3)
-static int knn_block() {
-  static const int nb = [] {
-    const char* e = std::getenv("FLOAM_KNN_BLOCK");
-    return e && std::atoi(e) == 2 ? 2 : 3;
-  }();
-  return nb;
-}
-
 void knn_launch(LMState* d_st, const double* x0_dev, const QuerySet& qe, const Grid& ge, CorrSet& ce,
                 const QuerySet& qs, const Grid& gs, CorrSet& cs, const int* d_me, const int* d_ms, int rank, int world,
                 hipStream_t st) {
@@ -1643,29 +1567,13 @@ void knn_launch(LMState* d_st, const double* x0_dev, const QuerySet& qe, const G
   const int nS = qs.grid_hint > 0 ? std::min(qs.grid_hint, qs.n_ub) : qs.n_ub;
   const unsigned nbE = std::min(div_up((size_t)std::max(nE, 1) * G, kTB), 4096u);
   const unsigned nbS = std::min(div_up((size_t)std::max(nS, 1) * G, kTB), 8192u);
-  // FLOAM_KNN_FUSED_PROTO=1|2 (measurement prototype: the fits inside the search at 6 | 4 waves per SIMD; the
-  // geometry launch still follows)
-  static const int fused_proto = [] {
-    const char* e = std::getenv("FLOAM_KNN_FUSED_PROTO");
-    return e ? std::atoi(e) : 0;
-  }();
-  if (fused_proto == 1)
-    hipLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6, 3, true>), dim3(nbE + nbS), dim3(kTB), 0, st, d_st, x0_dev,
-                       E, S, (int)nbE, d_me, d_ms, rank, world);
-  else if (fused_proto == 2)
-    hipLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 4, 3, true>), dim3(nbE + nbS), dim3(kTB), 0, st, d_st, x0_dev,
-                       E, S, (int)nbE, d_me, d_ms, rank, world);
-  else if (knn_block() == 2)
-    hipLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6, 2>), dim3(nbE + nbS), dim3(kTB), 0, st, d_st, x0_dev, E, S,
-                       (int)nbE, d_me, d_ms, rank, world);
-  else
-    hipLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6, 3>), dim3(nbE + nbS), dim3(kTB), 0, st, d_st, x0_dev, E, S,
+  hipLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6, 3>), dim3(nbE + nbS), dim3(kTB), 0, st, d_st, x0_dev, E, S,
                        (int)nbE, d_me, d_ms, rank, world);
   FLOAM_LAUNCH_CHECK();
 }
 
 void geom_launch(LMState* d_st, const QuerySet& qe, CorrSet& ce, const QuerySet& qs, CorrSet& cs, bool gram,
-                 bool fp32, LMBuffers& b, hipStream_t st, bool edge_sums) {
+                 bool fp32, LMBuffers& b, hipStream_t st) {
   if (qe.n_ub <= 0 && qs.n_ub <= 0) return;
   if (gram) b.reserve(st);
   Grid none;
@@ -1674,18 +1582,12 @@ void geom_launch(LMState* d_st, const QuerySet& qe, CorrSet& ce, const QuerySet&
   const unsigned gE = div_up(std::max(qe.n_ub, 1), kTB);
   double* gpart = gram ? b.gpart.p : nullptr;
   double* gmat = gram ? b.gmat.p : nullptr;
-  double* epart = nullptr;
-  if (gram && edge_sums && !fp32) {
-    b.epart.reserve((size_t)gE * LM_NSUM);
-    b.epart_blocks = (int)gE;
-    epart = b.epart.p;
-  }
   if (fp32)
     hipLaunchKernelGGL(geom_kernel<float>, dim3(gE + kSurfGeomBlocks), dim3(kTB), 0, st, d_st, E, S, (int)gE,
-                       gpart, gmat, b.gcnt.p, nullptr);
+                       gpart, gmat, b.gcnt.p);
   else
     hipLaunchKernelGGL(geom_kernel<double>, dim3(gE + kSurfGeomBlocks), dim3(kTB), 0, st, d_st, E, S, (int)gE,
-                       gpart, gmat, b.gcnt.p, epart);
+                       gpart, gmat, b.gcnt.p);
   FLOAM_LAUNCH_CHECK();
 }
 
@@ -1763,16 +1665,16 @@ void knn_stage_launch(LMState* d_st, const double* x0_dev, const QuerySet& qe, c
     FLOAM_LAUNCH_CHECK();
   };
   flush();
-  hipLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6, 3, false, 1>), g, dim3(kTB), 0, st, d_st, x0_dev, E, S, (int)nbE,
+  hipLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6, 3, 1>), g, dim3(kTB), 0, st, d_st, x0_dev, E, S, (int)nbE,
                      d_me, d_ms, rank, world);
   flush();
-  hipLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6, 3, false, 2>), g, dim3(kTB), 0, st, d_st, x0_dev, E, S, (int)nbE,
+  hipLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6, 3, 2>), g, dim3(kTB), 0, st, d_st, x0_dev, E, S, (int)nbE,
                      d_me, d_ms, rank, world);
   flush();
-  hipLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6, 3, false, 3>), g, dim3(kTB), 0, st, d_st, x0_dev, E, S, (int)nbE,
+  hipLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6, 3, 3>), g, dim3(kTB), 0, st, d_st, x0_dev, E, S, (int)nbE,
                      d_me, d_ms, rank, world);
   flush();
-  hipLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6, 3, false, 4>), g, dim3(kTB), 0, st, d_st, x0_dev, E, S, (int)nbE,
+  hipLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6, 3, 4>), g, dim3(kTB), 0, st, d_st, x0_dev, E, S, (int)nbE,
                      d_me, d_ms, rank, world);
   flush();   // (the real search follows, cold as well)
   FLOAM_LAUNCH_CHECK();
@@ -1789,7 +1691,7 @@ void knn_traffic_launch(const LMState* d_st, const QuerySet& q, const Grid& g, C
   for (int level = 0; level < 2; ++level) {
     FLOAM_HIP(hipMemsetAsync(set.p, 0xFF, sizeof(unsigned long long) << bits, st));
     hipLaunchKernelGGL(knn_traffic, dim3(div_up(q.n_ub, kTB)), dim3(kTB), 0, st, d_st, A, rank, world,
-                       level, knn_block(), set.p, (1u << bits) - 1u, bits, d_bytes);
+                       level, 3, set.p, (1u << bits) - 1u, bits, d_bytes);
     FLOAM_LAUNCH_CHECK();
   }
 }

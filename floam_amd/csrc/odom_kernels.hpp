@@ -137,8 +137,16 @@ struct LMState {
   int n_res;
   int corr_edge, corr_surf;   // accepted correspondences (this solve)
   unsigned epoch;     // hand-off tag base of the resident solve (lm.hip): advanced by 8 per solve (lm_reset)
+  // peer sharding: evaluations exchanged with the other ranks since floam_odom_set_shard_peers (continues across
+  // solves; lm_reset keeps it): the exchange slot and tag of each evaluation (lm.hip peer_exchange)
+  unsigned xseq;
+  // set (never cleared) by any block of a resident solve whose hand-off timed out; the one word the state write-back
+  // (publish_state) leaves alone, so block 0 cannot overwrite another block's report.  Must stay the last word.
+  int xfail;
 };
 constexpr int kStateWords = (int)(sizeof(LMState) / sizeof(unsigned));
+constexpr int kPublishWords = kStateWords - 1;   // every word but xfail
+static_assert(offsetof(LMState, xfail) == sizeof(unsigned) * kPublishWords, "xfail is the last LMState word");
 static_assert(sizeof(LMState) % 8 == 0, "LMState is copied as whole dwords");
 
 enum { LM_NSUM = 29 };   // cost, H[21], g[6], count
@@ -183,12 +191,10 @@ struct LMBuffers {
   DevBuf<double> gpart;              // surf Gram matrix: per-block and per-group partials (geom_kernel)
   DevBuf<double> gmat;               // the solve's surf Gram matrix + its origin
   DevBuf<unsigned> gcnt;             // ticket words of the Gram reduction
-  // the edge half of a squared-loss solve's iteration zero, evaluated by the geometry launch's edge blocks while they
-  // build the records (one 29-sum partial per block, fixed order; the solve adds them up in its prologue)
-  DevBuf<double> epart;
-  int epart_blocks = 0;
-  int fail_test = 0;                 // FLOAM_LM_FAIL_TEST=1 (tests): every resident solve reports its hand-off as
-                                     // timed out (n_res < 0), the path a lost block would take
+  int fail_test = 0;                 // FLOAM_LM_FAIL_TEST=1 (tests, diagnostic build): every resident solve reports
+                                     // its hand-off as timed out (n_res < 0), the path a lost block would take
+  int peer_delay_us = 0;             // FLOAM_PEER_DELAY_US=n (tests, diagnostic build): the non-zero blocks of a
+                                     // peer-sharded solve wait n us before every poll of the other ranks' sums
   void reserve(hipStream_t st);
 };
 
@@ -283,10 +289,8 @@ void knn_launch(LMState* d_st, const double* x0_dev, const QuerySet& qe, const G
                 const QuerySet& qs, const Grid& gs, CorrSet& cs, const int* d_me, const int* d_ms, int rank, int world,
                 hipStream_t st);
 // gram: the squared-loss solves' surf Gram matrix of the accepted surf records into b.gmat (b.gpart's partials)
-// edge_sums (gram only): the edge blocks also evaluate their accepted records at st->x into b.epart — iteration zero's
-// edge half for a resident solve launched with pre0 (lm_solve_launch)
 void geom_launch(LMState* d_st, const QuerySet& qe, CorrSet& ce, const QuerySet& qs, CorrSet& cs, bool gram,
-                 bool fp32, LMBuffers& b, hipStream_t st, bool edge_sums = false);
+                 bool fp32, LMBuffers& b, hipStream_t st);
 // algorithmic bytes of the correspondence pass just issued (profiling only), accumulated into *d_bytes
 // (diagnostic, FLOAM_KNN_STAGES=1 in a profiled replay) the search cut after each of its dependent round trips, every
 // variant after an L2 eviction, then one more eviction before the real search
@@ -300,8 +304,6 @@ void knn_traffic_launch(const LMState* d_st, const QuerySet& q, const Grid& g, C
 // A whole ceres::Solve (iteration zero + up to max_num_iterations = 4 candidates, src/odomEstimationClass.cpp:95-108)
 // in ONE launch on a single GPU: every block keeps its records in registers, evaluates them, all-gathers the blocks'
 // partial sums and runs the Ceres 1.13 control step itself (the same bits in every block).  mode = LM_*.
-// pre0 (LM_GRAM only): iteration zero's edge sums come from the geometry launch (geom_launch edge_sums): the solve
-// starts with its first control step, without the first evaluation's records and hand-off.
 // peers (world > 1): query sharding with the resident solve — each rank's blocks reduce the rank's sums as above, then
 // exchange them with the other ranks through peer-mapped buffers (every rank's buffer readable from every GPU), summed
 // in rank order; one launch per solve, no collective launch, no host round trip.
@@ -312,7 +314,7 @@ struct ShardPeers {
 };
 void lm_solve_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const CorrSet& cs,
                      const int* d_ns, int ns_ub, int mode, LMBuffers& b, hipStream_t st,
-                     unsigned long long* dbg = nullptr, bool pre0 = false, const ShardPeers* peers = nullptr);
+                     unsigned long long* dbg = nullptr, const ShardPeers* peers = nullptr);
 // The same solve sharded over ranks (one process per GPU): evaluation k = 0..4 in one launch each (the control step
 // of evaluation k - 1 folded in, run redundantly by every block on the all-reduced sums), leaving this rank's 29
 // sums in b.sums for the caller's all-reduce; lm_shard_final_launch runs the last control step.

@@ -16,7 +16,7 @@ __global__ void l2_writeback() {
 
 bool prof_wb_enabled() {
   static const bool on = [] {
-    const char* e = std::getenv("FLOAM_PROF_WB");
+    const char* e = FLOAM_DIAG_ENV("FLOAM_PROF_WB");
     return e && e[0] == '1';
   }();
   return on;

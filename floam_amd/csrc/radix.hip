@@ -57,7 +57,7 @@ __global__ __launch_bounds__(kTB) void radix_pass(const uint32_t* __restrict__ k
                                                   const int* __restrict__ gate, const int* __restrict__ n_dev,
                                                   int stamps, const PointRec* __restrict__ pin,
                                                   float4* __restrict__ pxyz, PointRec* __restrict__ prec,
-                                                  const uint8_t* __restrict__ digs, int by_index) {
+                                                  const uint8_t* __restrict__ digs) {
   const unsigned long long ts0 = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
   // every load of the prologue is issued at once (one memory round trip, not three in a row): the gate, the epoch,
   // the device count, this digit's histogram count and the tile's elements up to the host bound n (allocated; the
@@ -65,7 +65,7 @@ __global__ __launch_bounds__(kTB) void radix_pass(const uint32_t* __restrict__ k
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   // the ticket (zeroed per sort with the histograms) with the tile-independent loads in flight beside it
   __shared__ int s_tile;
-  if (t == 0) s_tile = by_index ? (int)blockIdx.x : (int)atomicAdd(&ctl[kRadixTicketWord + pass], 1u);
+  if (t == 0) s_tile = (int)atomicAdd(&ctl[kRadixTicketWord + pass], 1u);
   const int gv = gate ? *gate : 1;
   const unsigned epoch = ctl[kRadixEpochWord];
   const int nd = n_dev ? *n_dev : n;
@@ -258,7 +258,7 @@ __global__ __launch_bounds__(kTB) void radix_pass(const uint32_t* __restrict__ k
 
 static int stamps_on() {
   static unsigned launches = 0;
-  static const int on = std::getenv("FLOAM_RADIX_STAMPS") ? 1 : 0;
+  static const int on = FLOAM_DIAG_ENV("FLOAM_RADIX_STAMPS") ? 1 : 0;
   static bool init = false;
   if (on && !init) {
     init = true;
@@ -269,16 +269,8 @@ static int stamps_on() {
   return on ? (int)(launches++ % (unsigned)kStampSlots) + 1 : 0;   // per launch: its slot + 1
 }
 
-bool tile_by_index() {
-  static const bool on = [] {
-    const char* e = std::getenv("FLOAM_TILE_BY_INDEX");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
 void radix_stamps_print() {
-  if (!std::getenv("FLOAM_RADIX_STAMPS")) return;
+  if (!FLOAM_DIAG_ENV("FLOAM_RADIX_STAMPS")) return;
   static unsigned long long h[8 + 2 * kStampSlots];
   FLOAM_HIP(hipDeviceSynchronize());
   FLOAM_HIP(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_radix_stamps), sizeof(h)));
@@ -318,7 +310,7 @@ void radix_pass_launch(RadixScratch& sc, const uint32_t* kin, const int* vin, ui
   const int tiles = (int)div_up((unsigned)n, (unsigned)kTile);
   hipLaunchKernelGGL(radix_pass<false>, dim3(tiles), dim3(kTB), 0, st, kin, vin, kout, vout, n, pass, sc.ctl.p,
                      sc.status.p + (size_t)pass * sc.tiles_cap * kRadixDigits, nullptr, nullptr, stamps_on(), nullptr,
-                     nullptr, nullptr, nullptr, tile_by_index());
+                     nullptr, nullptr, nullptr);
   FLOAM_LAUNCH_CHECK();
 }
 
@@ -328,7 +320,7 @@ void radix_pass_payload_launch(RadixScratch& sc, const uint32_t* kin, uint32_t* 
   sc.reserve(n, st);
   const int tiles = (int)div_up((unsigned)n, (unsigned)kTile);
   hipLaunchKernelGGL(radix_pass<true>, dim3(tiles), dim3(kTB), 0, st, kin, nullptr, kout, vout, n, 0, sc.ctl.p,
-                     sc.status.p, nullptr, nullptr, stamps_on(), pin, pxyz, prec, nullptr, tile_by_index());
+                     sc.status.p, nullptr, nullptr, stamps_on(), pin, pxyz, prec, nullptr);
   FLOAM_LAUNCH_CHECK();
 }
 
@@ -342,7 +334,7 @@ void radix_sort_launch(RadixScratch& sc, uint32_t* k0, int* v0, uint32_t* k1, in
     hipLaunchKernelGGL(radix_pass<false>, dim3(tiles), dim3(kTB), 0, st, even ? k0 : k1, even ? v0 : v1,
                        even ? k1 : k0, even ? v1 : v0, n, p, sc.ctl.p,
                        sc.status.p + (size_t)p * sc.tiles_cap * kRadixDigits, gate, n_dev, stamps_on(), nullptr,
-                       nullptr, nullptr, nullptr, tile_by_index());
+                       nullptr, nullptr, nullptr);
     FLOAM_LAUNCH_CHECK();
   }
 }
@@ -353,7 +345,7 @@ void radix_digit_pass_launch(RadixScratch& sc, const uint32_t* kin, const int* v
   sc.reserve(n, st);
   const int tiles = (int)div_up((unsigned)n, (unsigned)kTile);
   hipLaunchKernelGGL(radix_pass<false>, dim3(tiles), dim3(kTB), 0, st, kin, vin, kout, vout, n, 0, sc.ctl.p,
-                     sc.status.p, gate, n_dev, stamps_on(), nullptr, nullptr, nullptr, digs, tile_by_index());
+                     sc.status.p, gate, n_dev, stamps_on(), nullptr, nullptr, nullptr, digs);
   FLOAM_LAUNCH_CHECK();
 }
 

@@ -75,10 +75,6 @@ void radix_pass_payload_launch(RadixScratch& sc, const uint32_t* kin, uint32_t* 
 // FLOAM_RADIX_STAMPS=1: print the passes' in-kernel phase times (diagnostic; synchronises the device)
 void radix_stamps_print();
 
-// FLOAM_TILE_BY_INDEX=1 (A/B only): the decoupled lookbacks (radix passes, vox_compact, bucket_compact, mm_merge)
-// take their tile from the block index instead of a ticket — the dispatch-order assumption HIP does not promise
-bool tile_by_index();
-
 void radix_pass_launch(RadixScratch& sc, const uint32_t* kin, const int* vin, uint32_t* kout, int* vout, int n,
                        int pass, hipStream_t st);
 

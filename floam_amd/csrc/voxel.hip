@@ -133,7 +133,7 @@ __global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B,
                                                    const int* __restrict__ vals, const int* __restrict__ overflow,
                                                    const int* __restrict__ n_dev, unsigned long long* __restrict__ status,
                                                    unsigned* __restrict__ ticket, const unsigned* __restrict__ radix_ctl,
-                                                   const int* __restrict__ gate, int n_cap, int stamps, int by_index) {
+                                                   const int* __restrict__ gate, int n_cap, int stamps) {
   const unsigned long long T0 = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
   // the prologue's loads are issued together (one round trip instead of four in a row): the gate, the device
   // counts, and the tile's keys and values up to the host bound n_cap (allocated; entries past the device count are
@@ -141,7 +141,7 @@ __global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B,
   // the tile is the block's ticket (zeroed by vox_keys): a tile only waits on tiles that are already running (HIP
   // promises no dispatch order); the tile-independent loads in flight beside the ticket
   __shared__ int s_tile;
-  if (threadIdx.x == 0) s_tile = by_index ? (int)blockIdx.x : (int)atomicAdd(ticket, 1u);
+  if (threadIdx.x == 0) s_tile = (int)atomicAdd(ticket, 1u);
   const int gv = gate ? *gate : 1;
   const int total_d = *n_dev;   // packed elements (vox_keys)
   const int nA0 = *A.d_n0, nA1 = A.d_n1 ? *A.d_n1 : 0, nB0 = *B.d_n0, nB1 = B.d_n1 ? *B.d_n1 : 0;
@@ -422,7 +422,7 @@ __global__ __launch_bounds__(kTB) void vox_compact(VoxelJobDev A, VoxelJobDev B,
 }  // namespace
 
 static int vox_stamps_on() {
-  static const int on = std::getenv("FLOAM_VOX_STAMPS") ? 1 : 0;
+  static const int on = FLOAM_DIAG_ENV("FLOAM_VOX_STAMPS") ? 1 : 0;
   return on;
 }
 
@@ -511,7 +511,7 @@ void voxel2_launch(VoxelScratch2& sc, const VoxelJob& a, const VoxelJob& b, hipS
   radix_sort_launch(sc.rs, sc.s.k0.p, sc.s.v0.p, sc.s.k1.p, sc.s.v1.p, n, st, gate, sc.overflow.p + 2);
   if (bucket) bucket_seed_launch(sc.bs, sc.s.k0.p, sc.overflow.p + 2, n, st, gate);
   hipLaunchKernelGGL(vox_compact, dim3(ntiles), dim3(kTB), 0, st, A, B, sc.s.k0.p, sc.s.v0.p, sc.overflow.p,
-                     sc.overflow.p + 2, sc.status.p, sc.ticket.p, sc.rs.ctl.p, gate, n, vox_stamps_on(), tile_by_index());
+                     sc.overflow.p + 2, sc.status.p, sc.ticket.p, sc.rs.ctl.p, gate, n, vox_stamps_on());
   FLOAM_LAUNCH_CHECK();
 }
 

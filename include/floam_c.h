@@ -8,8 +8,10 @@
  *
  * Ownership: the caller owns host buffers.  floam_cloud / floam_lp / floam_odom handles own their device memory.
  * Threading: a handle is used from one host thread at a time (the reference drives each class from one worker
- * thread, src/odomEstimationNode.cpp:365, src/laserProcessingNode.cpp:212).  All handles on one device share
- * one HIP stream, so work issued through different handles is ordered.
+ * thread, src/odomEstimationNode.cpp:365, src/laserProcessingNode.cpp:212).  The odometry and feature-extraction
+ * handles of one device issue their main work on one shared HIP stream (in issue order); a handle may add streams of
+ * its own (the odometry's side stream for the first call's VoxelGrids, the asynchronous feature extraction's stream,
+ * the one-call host entry points' copy stream), ordered with the shared stream by events, never by the caller.
  * Errors: every call returns floam_status; floam_last_error() gives a thread-local message.  Warnings
  * (status >= 100) are non-fatal and mirror the reference's printf diagnostics; the pose is then left where the
  * reference leaves it.
@@ -22,6 +24,8 @@
  *   1  round 1-2 entry points
  *   2  floam_odom_keyframe_update gained the (surf, edge) cloud parameters of KeyFrameUpdate
  *      (include/odomEstimationClass.h:80); floam_abi_version added
+ *   3  the one-call host entry points (floam_lp_feature_extraction_host, floam_odom_update_selector_host) and peer
+ *      sharding (floam_odom_shard_exchange, floam_odom_set_shard_peers)
  * A caller checks `floam_abi_version() == FLOAM_ABI_VERSION` once after loading the library. */
 #define FLOAM_ABI_VERSION 3
 
@@ -343,8 +347,12 @@ floam_status floam_odom_set_shard_callback(floam_odom* o, int rank, int world, f
  *   floam_odom_shard_exchange: this rank's buffer as an IPC handle (64 bytes, for the other processes) and/or as a
  *   device pointer (for handles in the same process).
  *   floam_odom_set_shard_peers: every rank's buffer, either as world x 64 bytes of IPC handles (entry `rank` is not
- *   opened) or as world device pointers; exactly one of the two.  world <= 8.  All ranks must issue their updates
- *   concurrently (one process or host thread per rank). */
+ *   opened) or as world device pointers; exactly one of the two.  world <= 8.  It starts a fresh exchange sequence
+ *   (the rank's exchange counter reset, its buffer zeroed), so every rank calls it — also when re-peering — and the
+ *   ranks then meet at a barrier before their next update; from there on all ranks issue the same sequence of
+ *   updates concurrently (one process per rank: the handles of one process share a stream, so ranks in one process
+ *   would wait on each other).  FLOAM_ERR_UNSUPPORTED when uncached device memory (which the cross-GPU polls need)
+ *   cannot be allocated: use floam_odom_set_shard (RCCL) instead. */
 floam_status floam_odom_shard_exchange(floam_odom* o, void* ipc_handle_64, void** dev_ptr);
 floam_status floam_odom_set_shard_peers(floam_odom* o, int rank, int world, const void* ipc_handles,
                                         void* const* dev_ptrs);

@@ -83,3 +83,27 @@ def test_pose_qt_any_rotation():
                            [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
             assert abs(np.linalg.norm(q) - 1.0) < 1e-12
             np.testing.assert_allclose(R2, R, atol=1e-12)
+
+
+def _env_names(path):
+    data = open(path, "rb").read()
+    return sorted(set(m.decode() for m in re.findall(rb"FLOAM_[A-Z0-9_]+", data)))
+
+
+def test_product_library_reads_only_documented_variables():
+    """A/B switches, stamps and test hooks live in the diagnostic build only
+    (FLOAM_DIAG_ENV, floam_amd/csrc/floam_common.hpp); the product library names exactly the two documented variables
+    (FLOAM_GRAPH opts into hipGraph capture, FLOAM_MAP_MERGE=0 re-voxelises the whole map)."""
+    names = [n for n in _env_names(_ffi.PRODUCT_LIB_PATH) if not n.startswith(("FLOAM_OK", "FLOAM_ERR", "FLOAM_WARN"))]
+    assert names == ["FLOAM_GRAPH", "FLOAM_MAP_MERGE"], names
+
+
+def test_diagnostic_library_exports_every_declared_symbol():
+    """The diagnostic build (tests/diag.py loads it for the hook tests) is the same ABI."""
+    import ctypes as C
+    assert os.path.exists(_ffi.DIAG_LIB_PATH), "libfloam_amd_diag.so not built"
+    L = C.CDLL(_ffi.DIAG_LIB_PATH)
+    missing = [n for n in _declared() if not hasattr(L, n)]
+    assert not missing, missing
+    assert L.floam_abi_version() == _ffi.ABI_VERSION
+    assert "FLOAM_LM_FAIL_TEST" in _env_names(_ffi.DIAG_LIB_PATH)

@@ -6,7 +6,7 @@ OUT=gpurun_out/${1:-ks}
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 for c in FETCH_SIZE WRITE_SIZE; do
-  FLOAM_KNN_STAGES=1 timeout -k 10 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $OUT/st_$c -o run -- \
+  FLOAM_AMD_LIB=diag FLOAM_KNN_STAGES=1 timeout -k 10 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $OUT/st_$c -o run -- \
       python3 bench.py --cpu-baseline-seconds 0 --no-secondary --steps 20 > $OUT/st_$c.log 2>&1 || { tail -20 $OUT/st_$c.log; exit 1; }
   echo "== $c"
   python tools/knn_stages.py $OUT/st_$c/run_counter_collection.csv $c --json $OUT/knn_stages_$c.json
