@@ -287,10 +287,6 @@ struct floam_odom {
   MapMergeScratch mms;
   bool map_merge = true;          // FLOAM_MAP_MERGE=0: the whole-map VoxelGrid of round 2 (A/B)
   bool map_force_full = false;    // FLOAM_MAP_FULL=1: the merge pipeline always takes its full-sort path (tests)
-  // FLOAM_GRID_COUNT_FUSED=1: the merge also counts its output into the next kNN grids (grid_count_job) instead of
-  // the grid build's own count launch — measured slower (r03g/r03h: mm_merge 27.6 -> 46 us, grid_scatter 6.5 -> 14 us
-  // against grid_count's 16.5 us), so off by default
-  bool grid_count_off = true;
   int map_violate_mod = 0;        // FLOAM_MM_VIOLATE=n: every n-th merge reports its keys out of order (tests)
   size_t mapE_n = 0, mapS_n = 0;   // map sizes: exact after a synchronisation, else upper bounds
   // scratch
@@ -570,7 +566,7 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
   if (o->grid_dirty) {
     ProfScope ps(ctx, "grid_build", FLOAM_PROF_CLOUD);
     grid_build_launch(o->gE, o->mapE.pts.p, o->mapE.count.p, mE_ub, o->gS, o->mapS.pts.p, o->mapS.count.p, mS_ub, st,
-                      predict ? o->ds.p : nullptr, true, o->mapE.pts.cap, o->mapS.pts.cap);
+                      predict ? o->ds.p : nullptr, true, o->mapE.pts.cap, o->mapS.pts.cap, &o->ds.p->grid_err);
     o->grid_dirty = false;
   }
   if (o->late_wait[0]) {   // one wait orders the main stream after the side stream's VoxelGrids and, through them,
@@ -758,6 +754,7 @@ floam_status odom_collect_one(floam_odom* o, DeviceCtx& ctx) {
       t.algorithmic_bytes += (double)U.prof[0] + (double)U.prof[1];
     }
     if (U.lm.n_res < 0 || U.lm.xfail) poison("an LM solve's hand-off timed out (blocks or peer ranks did not arrive)");
+    if (U.grid_err) poison("a kNN grid build could not place the map's points (pool exhausted)");
     if (U.counts[0] < 0 || U.counts[1] < 0 || U.counts[2] < 0 || U.counts[3] < 0)
       poison("voxel-grid compaction failed (lookback timeout)");
     if (U.fe_status & FE_STATUS_SECTOR_TOO_LONG)
@@ -946,15 +943,8 @@ void odom_map_update(floam_odom* o, DeviceCtx& ctx, const MapUpdatePlan& P, size
   ProfScope ps(ctx, "map_update", FLOAM_PROF_CLOUD);
   const int ubS = (int)o->mapS_n + P.ns_ub, ubE = (int)o->mapE_n + P.ne_ub;
   if (o->map_merge) {   // the new scan voxels merged into the voxel-ordered maps (mapmerge.hip)
-    // (the next grid builds' clears ran in the status gather: the merge also counts the points it writes into them)
-    GridCountDev gcount[2];
-    const bool fuse = o->gE.precleared && o->gS.precleared && !o->grid_count_off;
-    if (fuse) {
-      gcount[0] = grid_count_job(o->gE);
-      gcount[1] = grid_count_job(o->gS);
-    }
     map_merge_launch(o->vs, o->mms, P.je, P.js, P.ke, P.ks, &o->ds.p->kf_flag, (unsigned)o->issued,
-                     o->map_force_full, o->map_violate_mod, fuse ? gcount : nullptr, st);
+                     o->map_force_full, o->map_violate_mod, st);
     o->mkcur ^= 1;
   } else {
     voxel2_launch(o->vs, P.je, P.js, st, &o->ds.p->kf_flag, true);
@@ -1549,11 +1539,6 @@ floam_status floam_odom_init_map(floam_odom* o, const floam_cloud* edge, const f
     o->mapE.host_count = o->mapE_n; o->mapE.host_count_valid = true;
     o->mapS.host_count = o->mapS_n; o->mapS.host_count_valid = true;
     o->grid_dirty = true;
-    for (Grid* g : {&o->gE, &o->gS})
-      if (g->counted) {   // a map update counted its points into the next grids: those tables are cleared whole
-        g->counted = g->precleared = false;
-        g->fresh = true;
-      }
     for (int m = 0; m < 2; ++m) {   // a raw map (Q8): no cell keys until a map update has voxelised it
       o->mmeta[m][o->mkcur].reserve(1);
       FLOAM_HIP(hipMemsetAsync(o->mmeta[m][o->mkcur].p, 0, sizeof(MapMeta), st));
@@ -1977,7 +1962,8 @@ floam_status floam_odom_find_correspondences(floam_odom* o, const floam_cloud* e
     voxel2_launch(o->vs, je, js, st);
     if (o->grid_dirty) {
       grid_build_launch(o->gE, o->mapE.pts.p, o->mapE.count.p, (int)o->mapE_n, o->gS, o->mapS.pts.p,
-                        o->mapS.count.p, (int)o->mapS_n, st, nullptr, false, o->mapE.pts.cap, o->mapS.pts.cap);
+                        o->mapS.count.p, (int)o->mapS_n, st, nullptr, false, o->mapE.pts.cap, o->mapS.pts.cap,
+                        &o->ds.p->grid_err);
       o->grid_dirty = false;
     }
     o->lm.reserve(1);

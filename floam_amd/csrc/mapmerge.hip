@@ -17,8 +17,7 @@
 // Launches per update (both maps at once): mm_keys (the sort set's 32-bit voxel keys + digit histograms, the
 // VoxelGrid's own key arithmetic), the four radix passes (radix.hip) — over the scan voxels only on the merge path —
 // and mm_merge (merge-path tiles: partition by a 128-ary search of the two index sequences, the tile's elements
-// merged in LDS, runs -> centroids, decoupled-lookback output positions, the new map's cell keys and verdict, and
-// the kNN grid's per-point count of the new map: grid_count_point, so that the grid build skips that launch).
+// merged in LDS, runs -> centroids, decoupled-lookback output positions, the new map's cell keys and verdict).
 // Merge comparisons run on voxel indices: the set's sort keys, and the map's stored cell keys mapped into the same
 // grid — a cropped map point may lie outside it and is saturated to the first / last cell of its row, plane or grid,
 // which keeps the order (it takes part in the order only: a cropped point adds nothing to a centroid).
@@ -26,7 +25,6 @@
 #include <climits>
 
 #include "cloud_ops.hpp"
-#include "grid.hpp"
 #include "lookback.hpp"
 #include "mapmerge.hpp"
 #include "profwb.hpp"
@@ -281,12 +279,12 @@ __device__ unsigned g_mm_st[2][kMmStampTiles][6];
 __device__ __forceinline__ unsigned long long mm_now(int on) { return on ? __builtin_amdgcn_s_memrealtime() : 0ull; }
 
 template <int PER>
-__device__ __forceinline__ void mm_merge_job(const VoxelJobDev& JJ, const MapKeys& KK, const GridCountDev& G, int job,
+__device__ __forceinline__ void mm_merge_job(const VoxelJobDev& JJ, const MapKeys& KK, int job,
                                              const uint32_t* __restrict__ skeys, const int* __restrict__ svals,
                                              int* __restrict__ ctl, unsigned long long* __restrict__ mstatus,
                                              int tiles_cap, int tilesA,
                                              const unsigned* __restrict__ radix_ctl, const int* __restrict__ gate,
-                                             unsigned seq, int violate_mod, int count_grid,
+                                             unsigned seq, int violate_mod,
                                              int stamps) {
   const unsigned long long T0 = mm_now(stamps);
   // prologue loads first, so they travel with the ticket: the counts, the gate and the status gather's verdict words
@@ -318,17 +316,13 @@ __device__ __forceinline__ void mm_merge_job(const VoxelJobDev& JJ, const MapKey
     const int tile = job ? (int)blockIdx.x - tilesA : (int)blockIdx.x;
     for (int i0 = tile * kTB; i0 < V.n0; i0 += njb * kTB) {   // (wave-uniform trip count: the grid count)
       const int i = i0 + t;
-      const bool valid = i < V.n0;
-      float4 lo = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (valid) {
+      if (i < V.n0) {
         const float4* q = reinterpret_cast<const float4*>(V.J.part0 + i);
         float4* o = reinterpret_cast<float4*>(V.J.out + i);
-        lo = q[0];
-        o[0] = lo;
+        o[0] = q[0];
         o[1] = q[1];
         V.K.out[i] = V.K.in[i];
       }
-      if (count_grid) grid_count_point(G, i, valid, lo.x, lo.y, lo.z);
     }
     if (tile == 0 && t == 0) {
       *V.J.d_out = V.n0;
@@ -624,16 +618,10 @@ __device__ __forceinline__ void mm_merge_job(const VoxelJobDev& JJ, const MapKey
   const unsigned long long T4 = mm_now(stamps);
   if (violate_mod > 0 && seq % (unsigned)violate_mod == 0) bad = true;   // (test knob: exercise the fallback)
   if (__syncthreads_or(bad) && t == 0) V.K.meta_out->violation = seq;
-  int gi[PER];
-  bool gv[PER];
-  float gx[PER], gy[PER], gz[PER];
 #pragma unroll
   for (int r = 0; r < PER; ++r) {   // (nloc <= (PER * kTB): every output in one of the PER rounds)
     const int k = r * kTB + t;
-    gv[r] = k < nloc;
-    gi[r] = pre.a + k;
-    gx[r] = gy[r] = gz[r] = 0.f;
-    if (gv[r]) {
+    if (k < nloc) {
       const float4 c = s_pt[k];
       float4 lo, hi;   // (the record as two halves: no PointRec temporary)
       if (V.ovf) {
@@ -646,11 +634,8 @@ __device__ __forceinline__ void mm_merge_job(const VoxelJobDev& JJ, const MapKey
       o[0] = lo;
       o[1] = hi;
       V.K.out[pre.a + k] = s_key[k];
-      gx[r] = lo.x; gy[r] = lo.y; gz[r] = lo.z;
     }
   }
-  // the next kNN grid's per-point step (grid_count_job) for the map's points pre.a + k, all rounds at once
-  if (count_grid) grid_count_points<PER>(G, gi, gv, gx, gy, gz);
   if (stamps && tile < kMmStampTiles) {   // plain per-tile records
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -674,14 +659,13 @@ __global__ __launch_bounds__(kTB) void mm_merge(VoxelJobDev A, VoxelJobDev B, Ma
                                                 int* __restrict__ ctl, unsigned long long* __restrict__ mstatus,
                                                 int tiles_cap, int tilesA,
                                                 const unsigned* __restrict__ radix_ctl, const int* __restrict__ gate,
-                                                unsigned seq, int violate_mod, GridCountDev GA, GridCountDev GB,
-                                                int count_grid, int stamps) {
+                                                unsigned seq, int violate_mod, int stamps) {
   if ((int)blockIdx.x < tilesA)   // (block-uniform)
-    mm_merge_job<PER>(A, KA, GA, 0, skeys, svals, ctl, mstatus, tiles_cap, tilesA, radix_ctl, gate, seq, violate_mod,
-                      count_grid, stamps);
+    mm_merge_job<PER>(A, KA, 0, skeys, svals, ctl, mstatus, tiles_cap, tilesA, radix_ctl, gate, seq, violate_mod,
+                      stamps);
   else
-    mm_merge_job<PER>(B, KB, GB, 1, skeys, svals, ctl, mstatus, tiles_cap, tilesA, radix_ctl, gate, seq, violate_mod,
-                      count_grid, stamps);
+    mm_merge_job<PER>(B, KB, 1, skeys, svals, ctl, mstatus, tiles_cap, tilesA, radix_ctl, gate, seq, violate_mod,
+                      stamps);
 }
 
 }  // namespace
@@ -747,7 +731,7 @@ void mm_stamps_print() {
 
 void map_merge_launch(VoxelScratch2& vs, MapMergeScratch& ms, const VoxelJob& a, const VoxelJob& b, const MapKeys& ka,
                       const MapKeys& kb, const int* gate, unsigned seq, bool force_full, int violate_mod,
-                      const GridCountDev* grids, hipStream_t st) {
+                      hipStream_t st) {
   const VoxelJobDev A = to_dev(a, 0);
   const VoxelJobDev B = to_dev(b, a.n0_ub + a.n1_ub);
   const int nA = a.n0_ub + a.n1_ub, nB = b.n0_ub + b.n1_ub, n = std::max(nA + nB, 1);
@@ -784,7 +768,6 @@ void map_merge_launch(VoxelScratch2& vs, MapMergeScratch& ms, const VoxelJob& a,
   if (wb) prof_l2_writeback(st);
   hipLaunchKernelGGL(mm_merge<kMergePer>, dim3(tilesA + tilesB), dim3(kTB), 0, st, A, B, ka, kb, vs.s.k0.p, vs.s.v0.p,
                        ms.ctl.p, ms.status.p, ms.tiles_cap, tilesA, vs.rs.ctl.p, gate, seq, violate_mod,
-                       grids ? grids[0] : GridCountDev{}, grids ? grids[1] : GridCountDev{}, grids ? 1 : 0,
                        stamps);
   FLOAM_LAUNCH_CHECK();
   if (wb) prof_l2_writeback(st);

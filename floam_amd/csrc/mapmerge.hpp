@@ -46,14 +46,12 @@ MergeCheck merge_check(MapMergeScratch& ms, unsigned seq);
 // clean (MapMeta), the scan is finite and the index range does not overflow, only the scan's cropped voxels are
 // sorted (one 32-bit radix sort of the scan points of both maps) and merged into the map; otherwise the map's points
 // join the sort (the full VoxelGrid of map + scan, PCL semantics incl. the overflow pass-through).  gate: as
-// voxel2_launch (0 = no keyframe: the maps, keys and metas are copied unchanged).  Test knobs: force_full: always the
-// full sort; violate_mod > 0: the merges of updates seq % violate_mod == 0 report their keys out of order (the next
-// update then takes the full sort).  grids (nullable): [corner, surf] grid_count_job of the maps' next kNN grids — the
-// merge counts the points it writes.  per: merged elements per thread of a 256-thread tile (2 or 4; 4 unless the
-// handle was created with FLOAM_MM_PER=2 — small tiles put more runs across tile edges, which the tests exercise).
+// voxel2_launch (0 = no keyframe: the maps, keys and metas are copied unchanged).  Test knobs (diagnostic build): force_full:
+// always the full sort; violate_mod > 0: the merges of updates seq % violate_mod == 0 report their keys out of order
+// (the next update then takes the full sort).
 void map_merge_launch(VoxelScratch2& vs, MapMergeScratch& ms, const VoxelJob& a, const VoxelJob& b, const MapKeys& ka,
                       const MapKeys& kb, const int* gate, unsigned seq, bool force_full, int violate_mod,
-                      const GridCountDev* grids, hipStream_t st);
+                      hipStream_t st);
 
 void mm_stamps_print();   // FLOAM_MM_STAMPS (diagnostic)
 
