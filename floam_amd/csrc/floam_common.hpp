@@ -137,6 +137,14 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
 }
 __device__ __forceinline__ unsigned wave_incl_scan(unsigned v) { return (unsigned)wave_incl_scan((int)v); }
 
+// Physical block p of the first `nactive` blocks -> logical block, so that the blocks with equal p % 8 (one XCD
+// under the round-robin dispatch of MI355X_MICROARCH.md "Workgroup dispatch") get consecutive logical indices.
+// A bijection on [0, nactive); placement only affects speed, never results.
+__device__ __forceinline__ int xcd_block(int p, int nactive) {
+  const int x = p & 7, r = p >> 3, base = nactive >> 3, rem = nactive & 7;
+  return x * base + min(x, rem) + r;
+}
+
 }  // namespace floam
 
 // Device-resident cloud behind the opaque floam_cloud handle.

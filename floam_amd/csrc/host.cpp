@@ -566,7 +566,7 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
   if (o->grid_dirty) {
     ProfScope ps(ctx, "grid_build", FLOAM_PROF_CLOUD);
     grid_build_launch(o->gE, o->mapE.pts.p, o->mapE.count.p, mE_ub, o->gS, o->mapS.pts.p, o->mapS.count.p, mS_ub, st,
-                      predict ? o->ds.p : nullptr, true, o->mapE.pts.cap, o->mapS.pts.cap, &o->ds.p->grid_err);
+                      predict ? o->ds.p : nullptr, true, o->mapE.pts.cap, o->mapS.pts.cap);
     o->grid_dirty = false;
   }
   if (o->late_wait[0]) {   // one wait orders the main stream after the side stream's VoxelGrids and, through them,
@@ -754,7 +754,6 @@ floam_status odom_collect_one(floam_odom* o, DeviceCtx& ctx) {
       t.algorithmic_bytes += (double)U.prof[0] + (double)U.prof[1];
     }
     if (U.lm.n_res < 0 || U.lm.xfail) poison("an LM solve's hand-off timed out (blocks or peer ranks did not arrive)");
-    if (U.grid_err) poison("a kNN grid build could not place the map's points (pool exhausted)");
     if (U.counts[0] < 0 || U.counts[1] < 0 || U.counts[2] < 0 || U.counts[3] < 0)
       poison("voxel-grid compaction failed (lookback timeout)");
     if (U.fe_status & FE_STATUS_SECTOR_TOO_LONG)
@@ -1962,8 +1961,7 @@ floam_status floam_odom_find_correspondences(floam_odom* o, const floam_cloud* e
     voxel2_launch(o->vs, je, js, st);
     if (o->grid_dirty) {
       grid_build_launch(o->gE, o->mapE.pts.p, o->mapE.count.p, (int)o->mapE_n, o->gS, o->mapS.pts.p,
-                        o->mapS.count.p, (int)o->mapS_n, st, nullptr, false, o->mapE.pts.cap, o->mapS.pts.cap,
-                        &o->ds.p->grid_err);
+                        o->mapS.count.p, (int)o->mapS_n, st, nullptr, false, o->mapE.pts.cap, o->mapS.pts.cap);
       o->grid_dirty = false;
     }
     o->lm.reserve(1);

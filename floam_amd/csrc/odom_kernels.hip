@@ -426,6 +426,23 @@ __device__ __forceinline__ void lm_reset(LMState* st, const X7& x0) {
 constexpr int kGroupDefault = 16;   // lanes per query (template parameter G below)
 constexpr int kUnrollDefault = 2;   // candidate loads in flight per lane (U; 2 beat 4 and 8 at C3)
 
+// (start, count) of a coarse cell, or (0, 0): the entry's {key, start, total} head (one 16-B load)
+template <typename Cell>
+__device__ __forceinline__ int2 grid_lookup(const Cell* __restrict__ tab, unsigned long long key, int bits,
+                                            unsigned mask) {
+  unsigned h = coarse_slot(key, bits);
+  for (;;) {
+    const int4 e = *reinterpret_cast<const int4*>(&tab[h]);
+    const unsigned long long k = ((unsigned long long)(unsigned)e.y << 32) | (unsigned)e.x;
+    if (k == key) return make_int2(e.z, e.w);
+    if (k == kEmptyKey) return make_int2(0, 0);
+    h = (h + 1) & mask;
+  }
+}
+
+// points in the fine (0.5-m) cell (fx, fy, fz): its sub-cell count in the entry of the coarse cell that holds it
+__device__ __forceinline__ int fine_count(const struct CorrArgs& A, int fx, int fy, int fz);
+
 __device__ __forceinline__ void cswap(unsigned long long& a, unsigned long long& b) {
   const unsigned long long lo = a < b ? a : b, hi = a < b ? b : a;
   a = lo;
@@ -502,9 +519,9 @@ struct CorrArgs {
   const PointRec* q;       // downsampled scan points (sensor frame)
   const int* d_n;          // device count
   int n_ub;
-  const float4* gpts;      // the map grouped by cell: {x, y, z, map index bits} (the grid's pool)
-  const CellHead* head;    // the grid's table of fine cells
-  int bits;                // table size 1 << bits
+  const float4* gpts;      // the map grouped by cell: {x, y, z, map index bits}
+  const CoarseCell* coarse;
+  int bits;                // table size 1 << bits (both tables)
   unsigned mask;
   const float4* map;       // the map's coordinates in its own order (neighbour coordinates by map index)
   double* rec;
@@ -515,85 +532,151 @@ struct CorrArgs {
   int cap;
 };
 
-// (start, fill) of fine cell (x, y, z), or (0, 0): its head, found along the probe chain (one 16-B load per probe)
-__device__ __forceinline__ int2 cell_lookup(const CorrArgs& A, int x, int y, int z) {
-  const unsigned long long key = cell_key(x, y, z);
-  unsigned h = cell_slot(x, y, z, A.bits);
+__device__ __forceinline__ int fine_count(const CorrArgs& A, int fx, int fy, int fz) {
+  const unsigned long long key = cell_key(fx >> 1, fy >> 1, fz >> 1);
+  unsigned h = coarse_slot(key, A.bits);
   for (;;) {
-    const int4 e = *reinterpret_cast<const int4*>(&A.head[h]);
-    const unsigned long long k = ((unsigned long long)(unsigned)e.y << 32) | (unsigned)e.x;
-    if (k == key) return make_int2(e.z, e.w);
-    if (k == kEmptyKey) return make_int2(0, 0);
+    const CoarseCell& c = A.coarse[h];
+    if (c.key == key) return c.sub[(fx & 1) | ((fy & 1) << 1) | ((fz & 1) << 2)];
+    if (c.key == kEmptyKey) return 0;
     h = (h + 1) & A.mask;
   }
 }
 
-// Scan a box of fine cells [x0, x1] x [y0, y1] x [z0, z1] (at most kMaxBox) into the lane-local top-5 (keys: float
-// sq-distance bits << 32 | map index, so ties go to the lower map index).  Lane l looks up a contiguous run of the box's
-// cells (kProbe heads in flight at a time), the group scans the fills into an exclusive prefix in LDS (cell order),
-// and the lanes walk the flattened candidate list t = lane, lane + G, ... with a forward cursor and U independent
-// 16-B loads in flight (coalesced within a cell: a cell's points are one contiguous range of the pool).
-constexpr int kStage1Box = 27;    // the 3 x 3 x 3 fine block around the query's cell
-constexpr int kMaxBox = 125;      // stage 2: the fine cells covering [q - r, q + r], r <= 1 m: at most 5 per axis
-constexpr int kProbe = 4;
+// Scan a block of up to 3 x 3 x 3 cells of one table into the lane-local top-5 (keys: float sq-distance bits << 32
+// | position in the cell-sorted array, so ties go to the lower position).  Lane l looks up a contiguous run of the
+// block's cells (all first probes issued before any is waited on), the group scans the counts into an exclusive
+// prefix in LDS (cell order), and the lanes walk the flattened candidate list t = lane, lane + G, ... with a forward
+// cursor and U independent 16-B loads in flight (coalesced within a cell).
+constexpr int kMaxStencil = 27;
 
-template <int G, int MAXC>
-__device__ __forceinline__ int box_ranges(const CorrArgs& A, int x0, int x1, int y0, int y1, int z0, int z1, int lane,
-                                          int* __restrict__ s_pre, int* __restrict__ s_start) {
-  constexpr int P = (MAXC + G - 1) / G;   // cells per lane (at most)
-  const int nxr = x1 - x0 + 1, nyr = y1 - y0 + 1, nzr = z1 - z0 + 1;
-  const int ncell = nxr * nyr * nzr;
-  const int per = (ncell + G - 1) / G;
-  const int cb = min(ncell, lane * per), ce = min(ncell, cb + per);
+// Fine 3x3x3 block (stage 1) without a fine-cell table: the block's 27 fine cells lie in exactly 2x2x2 coarse cells
+// (three consecutive fine indices halve to two consecutive coarse indices), whose entries carry the coarse range
+// start and the point count of each of their 8 fine sub-cells (sub-cells are consecutive inside the range, in sub
+// order: grid.hip).  Lanes 0..7 probe the 8 coarse cells (head and sub counts of a slot in one round trip) into LDS
+// (s_cc[8][9]: start, 8 counts), then every fine cell's range is start + the counts of the sub-cells before it.
+// NB = 2: the 2x2x2 fine block with low corner (lx, ly, lz) (the query's cell and its nearer neighbour per axis),
+// whose cells lie in 1 or 2 coarse cells per axis (only those are probed).
+template <int G, int NB = 3>
+__device__ __forceinline__ void fine_block_ranges(const CorrArgs& A, int lx, int ly, int lz, int lane,
+                                                  int* __restrict__ s_pre, int* __restrict__ s_start,
+                                                  int* __restrict__ s_cc) {
+  static_assert(G >= 8, "one coarse probe per lane");
+  const int cx0 = lx >> 1, cy0 = ly >> 1, cz0 = lz >> 1;   // floor division by 2
+  // (NB = 3: three consecutive fine indices always span two coarse indices; NB = 2: two when lx is odd)
+  const bool need = NB == 3 || (((lane & 1) == 0 || (lx & 1)) && (((lane >> 1) & 1) == 0 || (ly & 1)) &&
+                                ((lane >> 2) == 0 || (lz & 1)));
+  if (lane < 8 && !need) {
+    int* cc = s_cc + 9 * lane;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) cc[k] = 0;
+  }
+  if (lane < 8 && need) {
+    const unsigned long long key = cell_key(cx0 + (lane & 1), cy0 + ((lane >> 1) & 1), cz0 + (lane >> 2));
+    unsigned slot = coarse_slot(key, A.bits);
+    const int4* e = reinterpret_cast<const int4*>(&A.coarse[slot]);
+    int4 h = e[0], s0 = e[1], s1 = e[2];
+    unsigned long long k = ((unsigned long long)(unsigned)h.y << 32) | (unsigned)h.x;
+    while (k != key && k != kEmptyKey) {   // collision chain (rare)
+      slot = (slot + 1) & A.mask;
+      e = reinterpret_cast<const int4*>(&A.coarse[slot]);
+      h = e[0];
+      s0 = e[1];
+      s1 = e[2];
+      k = ((unsigned long long)(unsigned)h.y << 32) | (unsigned)h.x;
+    }
+    const bool hit = k == key;
+    int* cc = s_cc + 9 * lane;
+    cc[0] = hit ? h.z : 0;
+    cc[1] = hit ? s0.x : 0; cc[2] = hit ? s0.y : 0; cc[3] = hit ? s0.z : 0; cc[4] = hit ? s0.w : 0;
+    cc[5] = hit ? s1.x : 0; cc[6] = hit ? s1.y : 0; cc[7] = hit ? s1.z : 0; cc[8] = hit ? s1.w : 0;
+  }
+  wave_lds_order();
+  constexpr int NC = NB * NB * NB;
+  constexpr int P = (NC + G - 1) / G;   // fine cells per lane
+  const int cb = min(NC, lane * P), ce = min(NC, cb + P);
   int local = 0;
 #pragma unroll
-  for (int j0 = 0; j0 < P; j0 += kProbe) {
-    unsigned long long key[kProbe];
-    unsigned slot[kProbe];
-    int4 e[kProbe];
+  for (int j = 0; j < P; ++j) {
+    const int c = cb + j;
+    if (c < ce) {
+      const int fx = lx + c % NB, fy = ly + (c / NB) % NB, fz = lz + c / (NB * NB);
+      const int ci = ((fx >> 1) - cx0) | (((fy >> 1) - cy0) << 1) | (((fz >> 1) - cz0) << 2);
+      const int sub = (fx & 1) | ((fy & 1) << 1) | ((fz & 1) << 2);
+      const int* cc = s_cc + 9 * ci;
+      int start = cc[0];
 #pragma unroll
-    for (int j = 0; j < kProbe; ++j) {   // the batch's first probes issued before any is waited on
-      const int c = cb + j0 + j;
-      key[j] = kEmptyKey;
-      e[j] = make_int4(-1, -1, 0, 0);
-      if (j0 + j < P && c < ce) {
-        const int x = x0 + c % nxr, y = y0 + (c / nxr) % nyr, z = z0 + c / (nxr * nyr);
-        key[j] = cell_key(x, y, z);
-        slot[j] = cell_slot(x, y, z, A.bits);
-        e[j] = *reinterpret_cast<const int4*>(&A.head[slot[j]]);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < kProbe; ++j) {
-      const int c = cb + j0 + j;
-      if (j0 + j < P && c < ce) {
-        unsigned long long k = ((unsigned long long)(unsigned)e[j].y << 32) | (unsigned)e[j].x;
-        while (k != key[j] && k != kEmptyKey) {   // collision chain (rare)
-          slot[j] = (slot[j] + 1) & A.mask;
-          e[j] = *reinterpret_cast<const int4*>(&A.head[slot[j]]);
-          k = ((unsigned long long)(unsigned)e[j].y << 32) | (unsigned)e[j].x;
-        }
-        const bool hit = k == key[j];
-        s_start[c] = hit ? e[j].z : 0;
-        s_pre[c] = local;
-        local += hit ? e[j].w : 0;
-      }
+      for (int k = 0; k < 8; ++k)
+        if (k < sub) start += cc[1 + k];
+      s_start[c] = start;
+      s_pre[c] = local;
+      local += cc[1 + sub];
     }
   }
   const int incl = group_incl_scan<G>(local, lane);
   const int excl = incl - local;
-  for (int c = cb; c < ce; ++c) s_pre[c] += excl;
-  const int tot = __shfl(incl, G - 1, G);
-  if (lane == 0) s_pre[ncell] = tot;
+#pragma unroll
+  for (int j = 0; j < P; ++j)
+    if (cb + j < ce) s_pre[cb + j] += excl;
+  if (lane == G - 1) s_pre[NC] = incl;
   wave_lds_order();
-  return tot;
 }
 
-template <int G, int U, int MAXC>
+template <int G, int U, bool COARSE, int NB = 3>
 __device__ __forceinline__ void stencil_scan(const CorrArgs& A, int x0, int x1, int y0, int y1, int z0, int z1,
                                              float wx, float wy, float wz, int lane, int* __restrict__ s_pre,
-                                             int* __restrict__ s_start, Top5& t, int& cnt) {
-  const int tot = box_ranges<G, MAXC>(A, x0, x1, y0, y1, z0, z1, lane, s_pre, s_start);
+                                             int* __restrict__ s_start, Top5& t, int& cnt,
+                                             int* __restrict__ s_cc = nullptr) {
+  constexpr int P = (kMaxStencil + G - 1) / G;   // cells per lane
+  const int nxr = x1 - x0 + 1, nyr = y1 - y0 + 1, nzr = z1 - z0 + 1;
+  const int ncell = nxr * nyr * nzr;
+  int tot;
+  if constexpr (!COARSE) {   // the fine block with low corner (x0, y0, z0), ranges from the coarse entries
+    fine_block_ranges<G, NB>(A, x0, y0, z0, lane, s_pre, s_start, s_cc);
+    tot = s_pre[NB * NB * NB];
+  } else {
+  const int per = (ncell + G - 1) / G;
+  const int cb = min(ncell, lane * per), ce = min(ncell, cb + per);
+  unsigned long long key[P];
+  unsigned slot[P];
+  int4 e[P];
+#pragma unroll
+  for (int j = 0; j < P; ++j) {
+    const int c = cb + j;
+    key[j] = kEmptyKey;
+    e[j] = make_int4(-1, -1, 0, 0);
+    if (c < ce) {
+      key[j] = cell_key(x0 + c % nxr, y0 + (c / nxr) % nyr, z0 + c / (nxr * nyr));
+      slot[j] = coarse_slot(key[j], A.bits);
+      e[j] = *reinterpret_cast<const int4*>(&A.coarse[slot[j]]);
+    }
+  }
+  int local = 0;
+#pragma unroll
+  for (int j = 0; j < P; ++j) {
+    const int c = cb + j;
+    if (c < ce) {
+      unsigned long long k = ((unsigned long long)(unsigned)e[j].y << 32) | (unsigned)e[j].x;
+      while (k != key[j] && k != kEmptyKey) {   // collision chain (rare)
+        slot[j] = (slot[j] + 1) & A.mask;
+        e[j] = *reinterpret_cast<const int4*>(&A.coarse[slot[j]]);
+        k = ((unsigned long long)(unsigned)e[j].y << 32) | (unsigned)e[j].x;
+      }
+      const bool hit = k == key[j];
+      s_start[c] = hit ? e[j].z : 0;
+      s_pre[c] = local;
+      local += hit ? e[j].w : 0;
+    }
+  }
+  const int incl = group_incl_scan<G>(local, lane);
+  const int excl = incl - local;
+#pragma unroll
+  for (int j = 0; j < P; ++j)
+    if (cb + j < ce) s_pre[cb + j] += excl;
+  tot = __shfl(incl, G - 1, G);
+  if (lane == 0) s_pre[ncell] = tot;
+  wave_lds_order();
+  }
   int c = 0, c_lo = 0, c_hi = s_pre[1], c_start = s_start[0];   // cursor: cell c = [c_lo, c_hi)
   for (int tb = 0; tb < tot; tb += G * U) {
     float4 m[U];
@@ -669,42 +752,44 @@ __device__ __forceinline__ void group_merge(Top5& t, int& cnt) {
   }
 }
 
-// Physical block p of the first `nactive` blocks -> logical block, so that the blocks with equal p % 8 (one XCD
-// under the round-robin dispatch of MI355X_MICROARCH.md "Workgroup dispatch") get consecutive logical indices.
-// A bijection on [0, nactive); placement only affects speed, never results.
-__device__ __forceinline__ int xcd_block(int p, int nactive) {
-  const int x = p & 7, r = p >> 3, base = nactive >> 3, rem = nactive & 7;
-  return x * base + min(x, rem) + r;
-}
 
 // Pass 1: exact 5-NN of every query (no fp64 geometry here, so the kernel stays small and at high occupancy).
 // The reference keeps a correspondence iff the 5th-nearest float sq-distance is < 1 (:154, :210), so only map
 // points within 1 m matter.  Stage 1 scans the 3x3x3 FINE cells (edge 0.5 m) around the query's cell: every point
 // outside that block is at least 0.5 m away along some axis, so its float sq-distance is >= 0.25 (exact: the cell
 // bounds are exact and fl(dx) >= 0.5 by monotone rounding); if 5 points with sq-distance < 0.25 were found they are
-// the exact 5-NN.  Otherwise stage 2 scans the fine cells spanning [q - r, q + r] on every axis (<= 5x5x5):
+// the exact 5-NN.  Otherwise stage 2 scans the COARSE cells (1 m) spanning [q - r, q + r] on every axis (<= 3x3x3):
 // r = 1 m (every point within 1 m) unless stage 1 already found 5 points within 1 m, then r = sqrt(d5) (1 + 1e-6) with
 // d5 their 5th float sq-distance (the ball that holds the 5-NN and every tie with the 5th; see knn_group).  Ties at
 // equal float distance go to the lower map index (FLANN's own order depends on its tree traversal; tie-free data is
 // identical).
 // Output: valid bit 0 = 5 neighbours within sqd < 1 (their coordinates in nnxyz), bit 1 = stage 2 was needed.
+// Low fine corner of a query's stage-1 block: nb = 3, the cells around the query's (qx, qy, qz); nb = 2, the
+// query's cell and the neighbour on the nearer side per axis (2 w - f is exact: f = floor(2 w) and 2 w are floats
+// within a factor 2)
+__device__ __forceinline__ void knn_block_corner(int nb, float wx, float wy, float wz, int qx, int qy, int qz, int& lx,
+                                                 int& ly, int& lz) {
+  lx = qx - 1;
+  ly = qy - 1;
+  lz = qz - 1;
+  if (nb == 2) {
+    if (2.0f * wx - (float)qx >= 0.5f) ++lx;
+    if (2.0f * wy - (float)qy >= 0.5f) ++ly;
+    if (2.0f * wz - (float)qz >= 0.5f) ++lz;
+  }
+}
 
 template <bool EDGE, typename R>
 __device__ __forceinline__ bool geom_fit(const R (&P)[5][3], float4 pq, double* __restrict__ rec, int cap, int i,
                                          double* __restrict__ w, const double* o);
 
-// the fine cells [lo, hi] per axis that cover [v - r, v + r] (exact in double: v is a float, r has a 1e-6 margin)
-__device__ __forceinline__ int2 fine_span(float v, double r) {
-  return make_int2((int)floor(((double)v - r) * 2.0), (int)floor(((double)v + r) * 2.0));
-}
-
 // STOP (diagnostic, FLOAM_KNN_STAGES: the per-round-trip read attribution of DESIGN.md §3) ends each query after
-// its first STOP dependent memory round trips — 1: the query load and transform; 2: + the table probes of the fine
+// its first STOP dependent memory round trips — 1: the query load and transform; 2: + the coarse probes of the fine
 // block; 3: + stage 1's candidate loads; 4: + stage 2 — and writes only a flag derived from what it loaded
-template <int G, int U, int STOP = 0>
+template <int G, int U, int NB, int STOP = 0>
 __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArgs& A, int gid, int ngroups,
                                           int lane, bool gate, int rank, int world, int* __restrict__ s_pre,
-                                          int* __restrict__ s_start) {
+                                          int* __restrict__ s_start, int* __restrict__ s_cc) {
   const int n = min(*A.d_n, A.n_ub);
   const int lo = (int)(((long long)n * rank) / world), hi = (int)(((long long)n * (rank + 1)) / world);
   // grid-stride over the queries the device holds (the host only knows an upper bound)
@@ -726,28 +811,31 @@ __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArg
 #pragma unroll
       for (int k = 0; k < 5; ++k) t.k[k] = ~0ull;
       int cnt = 0;
-      const int lx = qx - 1, ly = qy - 1, lz = qz - 1;   // the 3x3x3 fine block's low corner
+      int lx, ly, lz;
+      knn_block_corner(NB, wx, wy, wz, qx, qy, qz, lx, ly, lz);
       if constexpr (STOP == 2) {
-        const int tot = box_ranges<G, kStage1Box>(A, lx, lx + 2, ly, ly + 2, lz, lz + 2, lane, s_pre, s_start);
-        if (lane == 0) A.valid[i] = (uint8_t)tot;
+        fine_block_ranges<G, NB>(A, lx, ly, lz, lane, s_pre, s_start, s_cc);
+        if (lane == 0) A.valid[i] = (uint8_t)s_pre[NB * NB * NB];
         wave_lds_order();
         continue;
       }
-      stencil_scan<G, U, kStage1Box>(A, lx, lx + 2, ly, ly + 2, lz, lz + 2, wx, wy, wz, lane, s_pre, s_start, t, cnt);
+      stencil_scan<G, U, false, NB>(A, lx, lx + NB - 1, ly, ly + NB - 1, lz, lz + NB - 1, wx, wy, wz, lane, s_pre,
+                                    s_start, t, cnt, s_cc);
       group_merge<G>(t, cnt);
-      // exact early exit: a map point outside the fine block [lo, hi) (lo = l / 2, hi = (l + 3) / 2 per axis, exact
+      // exact early exit: a map point outside the fine block [lo, hi) (lo = l / 2, hi = (l + NB) / 2 per axis, exact
       // in float) lies beyond a face, so on that axis |fl(q - p)| >= fl(q - lo) or fl(hi - q) (monotone rounding)
-      // and its float sq-distance is >= fl(b^2), b the query's smallest face distance (>= 0.5)
-      const float b = fminf(fminf(fminf(wx - 0.5f * (float)lx, 0.5f * (float)(lx + 3) - wx),
-                                  fminf(wy - 0.5f * (float)ly, 0.5f * (float)(ly + 3) - wy)),
-                            fminf(wz - 0.5f * (float)lz, 0.5f * (float)(lz + 3) - wz));
+      // and its float sq-distance is >= fl(b^2), b the query's smallest face distance (>= 0.5 for NB = 3, >= 0.25
+      // for NB = 2)
+      const float b = fminf(fminf(fminf(wx - 0.5f * (float)lx, 0.5f * (float)(lx + NB) - wx),
+                                  fminf(wy - 0.5f * (float)ly, 0.5f * (float)(ly + NB) - wy)),
+                            fminf(wz - 0.5f * (float)lz, 0.5f * (float)(lz + NB) - wz));
       const bool complete = cnt >= 5 && __uint_as_float((unsigned)(t.k[4] >> 32)) < b * b;
       if constexpr (STOP == 3) {
         if (lane == 0) A.valid[i] = (uint8_t)(cnt + (complete ? 1 : 0) + (int)(t.k[4] & 0xFF));
         continue;
       }
       if (!complete) {
-        // fine cells floor(2 (q - r)) .. floor(2 (q + r)) per axis (exact in double).  r = 1 (every point within 1 m)
+        // coarse cells floor(q - r) .. floor(q + r) per axis (exact in double).  r = 1 (every point within 1 m)
         // unless stage 1 already holds 5 points within 1 m: then the 5-NN and every point tied with the 5th lie in
         // the ball of its float sq-distance d5, and r = sqrt(d5) (1 + 1e-6) covers that ball with margin — a point
         // outside the box is more than r away along one axis, so its float sq-distance is >= r^2 (1 - 2^-24)^5 > d5
@@ -757,8 +845,10 @@ __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArg
 #pragma unroll
         for (int k = 0; k < 5; ++k) t.k[k] = ~0ull;
         cnt = 0;
-        const int2 sx = fine_span(wx, r), sy = fine_span(wy, r), sz = fine_span(wz, r);
-        stencil_scan<G, U, kMaxBox>(A, sx.x, sx.y, sy.x, sy.y, sz.x, sz.y, wx, wy, wz, lane, s_pre, s_start, t, cnt);
+        stencil_scan<G, U, true>(A, (int)floor((double)wx - r), (int)floor((double)wx + r),
+                                 (int)floor((double)wy - r), (int)floor((double)wy + r),
+                                 (int)floor((double)wz - r), (int)floor((double)wz + r), wx, wy, wz, lane, s_pre,
+                                 s_start, t, cnt);
         group_merge<G>(t, cnt);
         flags |= 2;
       }
@@ -791,13 +881,14 @@ __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArg
 // Edge and surf kNN in one launch: blocks [0, nbE) run edge groups, the others surf groups.  The launch also starts
 // the solve (lm_init folded in): block 0 resets the LM state and, for the first solve of an update, stores the
 // prediction x0 that every block uses for its transforms (the others never read st->x in that case).
-template <int G, int U, int W, int STOP = 0>
+template <int G, int U, int W, int NB, int STOP = 0>
 __global__ __launch_bounds__(kTB, W) void knn_kernel(LMState* __restrict__ st, const double* __restrict__ x0_dev,
                                                   CorrArgs E, CorrArgs S, int nbE,
                                                   const int* __restrict__ d_me, const int* __restrict__ d_ms,
                                                   int rank, int world) {
-  __shared__ int s_pre[kTB / G][kMaxBox + 1];
-  __shared__ int s_start[kTB / G][kMaxBox];
+  __shared__ int s_pre[kTB / G][kMaxStencil + 1];
+  __shared__ int s_start[kTB / G][kMaxStencil];
+  __shared__ int s_cc[kTB / G][8 * 9];
   const int lane = threadIdx.x & (G - 1);
   const int g = threadIdx.x / G;
   double pose[7];   // wave-uniform: kept in SGPRs (readfirstlane), not in 14 VGPRs of every lane
@@ -825,8 +916,8 @@ __global__ __launch_bounds__(kTB, W) void knn_kernel(LMState* __restrict__ st, c
   const int nq = min(*A.d_n, A.n_ub);
   const int nact = min(nb, (int)(((long long)nq * G + kTB - 1) / kTB));
   if (p < nact) p = xcd_block(p, nact);
-  knn_group<G, U, STOP>(pose, A, (p * kTB + (int)threadIdx.x) / G, nb * (kTB / G), lane, gate, rank, world, s_pre[g],
-                        s_start[g]);
+  knn_group<G, U, NB, STOP>(pose, A, (p * kTB + (int)threadIdx.x) / G, nb * (kTB / G), lane, gate, rank, world,
+                            s_pre[g], s_start[g], s_cc[g]);
 }
 
 // Pass 2: line / plane geometry, one query per lane (all 64 lanes busy), in R = double (the reference's precision)
@@ -1094,24 +1185,32 @@ __global__ __launch_bounds__(kTB) void geom_kernel(LMState* __restrict__ st, Cor
 
 // Algorithmic traffic of one launch of the search kernel (knn_kernel; SURVEY.md §8 d): every map
 // cell any query scans is streamed once (16 B per map point: the union over queries of the fine 3x3x3 block around
-// the query's cell — level 0 — and of the fine cells covering [q - r, q + r] for the queries whose bit 1 says they
-// needed stage 2 — level 1), every query is read once (16 B) and writes its flag (1 B) and, with 5 neighbours, their coordinates
+// the query's cell — level 0 — and of the coarse +-1 m stencil for the queries whose bit 1 says they needed stage 2
+// — level 1), every query is read once (16 B) and writes its flag (1 B) and, with 5 neighbours, their coordinates
 // (60 B) (counted at level 0).  Runs untimed, on a replay, only when profiling.
 //
 // The radius of a query's stage 2 (knn_group): 1, or with 5 points within 1 m in the fine block around the query's
-// cell (27 fine cells), sqrt of the 5th-smallest float sq-distance among them times (1 + 1e-6) — recomputed here
+// block (nb^3 fine cells), sqrt of the 5th-smallest float sq-distance among them times (1 + 1e-6) — recomputed here
 // serially over the same fine cells with the same float arithmetic
-__device__ double stage2_radius(const CorrArgs& A, float wx, float wy, float wz) {
-  int qx, qy, qz;
+__device__ double stage2_radius(const CorrArgs& A, int nb, float wx, float wy, float wz) {
+  int qx, qy, qz, lx, ly, lz;
   fine_cell(wx, wy, wz, qx, qy, qz);
+  knn_block_corner(nb, wx, wy, wz, qx, qy, qz, lx, ly, lz);
   float best[5] = {2.f, 2.f, 2.f, 2.f, 2.f};   // ascending
   int cnt = 0;
-  for (int fz = qz - 1; fz <= qz + 1; ++fz)
-    for (int fy = qy - 1; fy <= qy + 1; ++fy)
-      for (int fx = qx - 1; fx <= qx + 1; ++fx) {
-        const int2 c = cell_lookup(A, fx, fy, fz);
-        for (int j = 0; j < c.y; ++j) {
-          const float4 m = A.gpts[c.x + j];
+  for (int fz = lz; fz < lz + nb; ++fz)
+    for (int fy = ly; fy < ly + nb; ++fy)
+      for (int fx = lx; fx < lx + nb; ++fx) {
+        const unsigned long long key = cell_key(fx >> 1, fy >> 1, fz >> 1);
+        unsigned h = coarse_slot(key, A.bits);
+        while (A.coarse[h].key != key && A.coarse[h].key != kEmptyKey) h = (h + 1) & A.mask;
+        const CoarseCell& c = A.coarse[h];
+        if (c.key != key) continue;
+        const int sub = (fx & 1) | ((fy & 1) << 1) | ((fz & 1) << 2);
+        int start = c.start;
+        for (int k = 0; k < sub; ++k) start += c.sub[k];
+        for (int j = 0; j < c.sub[sub]; ++j) {
+          const float4 m = A.gpts[start + j];
           float dd = 0.0f, df = wx - m.x;
           dd += df * df;
           df = wy - m.y;
@@ -1132,7 +1231,7 @@ __device__ double stage2_radius(const CorrArgs& A, float wx, float wy, float wz)
 }
 
 __global__ __launch_bounds__(kTB) void knn_traffic(const LMState* __restrict__ st, CorrArgs A, int rank,
-                                                   int world, int level,
+                                                   int world, int level, int nb,
                                                    unsigned long long* __restrict__ set,
                                                    unsigned set_mask, int set_bits,
                                                    unsigned long long* __restrict__ out) {
@@ -1151,20 +1250,21 @@ __global__ __launch_bounds__(kTB) void knn_traffic(const LMState* __restrict__ s
   unsigned long long bytes = level ? 0ull : 16ull + 1ull + ((f & 4) ? 60ull : 0ull);
   int x0, y0, z0, x1, y1, z1;
   if (level) {
-    const double r = stage2_radius(A, wx, wy, wz);
-    const int2 sx = fine_span(wx, r), sy = fine_span(wy, r), sz = fine_span(wz, r);
-    x0 = sx.x; x1 = sx.y; y0 = sy.x; y1 = sy.y; z0 = sz.x; z1 = sz.y;
+    const double r = stage2_radius(A, nb, wx, wy, wz);
+    x0 = (int)floor((double)wx - r); x1 = (int)floor((double)wx + r);
+    y0 = (int)floor((double)wy - r); y1 = (int)floor((double)wy + r);
+    z0 = (int)floor((double)wz - r); z1 = (int)floor((double)wz + r);
   } else {
     int qx, qy, qz;
     fine_cell(wx, wy, wz, qx, qy, qz);
-    x0 = qx - 1; y0 = qy - 1; z0 = qz - 1;
-    x1 = qx + 1; y1 = qy + 1; z1 = qz + 1;
+    knn_block_corner(nb, wx, wy, wz, qx, qy, qz, x0, y0, z0);
+    x1 = x0 + nb - 1; y1 = y0 + nb - 1; z1 = z0 + nb - 1;
   }
   for (int z = z0; z <= z1; ++z)
     for (int y = y0; y <= y1; ++y)
       for (int x = x0; x <= x1; ++x) {
         const unsigned long long k = cell_key(x, y, z);
-        const int cnt = cell_lookup(A, x, y, z).y;
+        const int cnt = level ? grid_lookup(A.coarse, k, A.bits, A.mask).y : fine_count(A, x, y, z);
         if (cnt == 0) continue;
         unsigned h = hash_slot64(k, set_bits);
         for (;;) {
@@ -1271,7 +1371,6 @@ __global__ void odom_dev_init(OdomDev* s) {
   s->kf_count = 0;
   s->kf_flag = 0;
   s->failed = 0;
-  s->grid_err = 0;
   pose_to_params(pose_identity(), s->x0[0]);
   pose_to_params(pose_identity(), s->x0[1]);
 }
@@ -1339,8 +1438,7 @@ __device__ __forceinline__ void gather_block(const LMState* __restrict__ lm, con
     out->prof[1] = prof ? prof[1] : 0ull;
     out->kf_flag = 0;
     s->kf_flag = 0;   // (the map update's gate)
-    out->grid_err = s->grid_err;
-    if (lm->n_res < 0 || lm->xfail || s->grid_err) s->failed = 1;   // an abandoned solve: its pose is not taken, no keyframe, no
+    if (lm->n_res < 0 || lm->xfail) s->failed = 1;   // an abandoned solve: its pose is not taken, no keyframe, no
     if (!s->failed) {                   // map update — for this update and every later one; the host raises it
       if (mode & GATHER_FINISH) {
         if (mode & GATHER_AFTER_MID) s->last_odom = s->mid;
@@ -1388,7 +1486,7 @@ __global__ void gather_status(const LMState* __restrict__ lm, const int* __restr
     } else {
       vox_minmax_block(job == 0 ? A : B, job, b, nb, vpart);
     }
-  } else if (gcE.head) {   // blocks of their own: the next grid builds' clears (this update's kNN launches are done)
+  } else if (gcE.coarse) {   // blocks of their own: the next grid builds' clears (this update's kNN launches are done)
     grid_clear_part(blockIdx.y == 2 ? gcE : gcS, blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x,
                     blockIdx.x == 0 && threadIdx.x == 0);
   }
@@ -1441,9 +1539,9 @@ static void corr_args(const QuerySet& qe, const Grid& ge, CorrSet& ce, const Que
                       CorrSet& cs, CorrArgs& E, CorrArgs& S) {
   ce.reserve(std::max(qe.n_ub, 1), EDGE_FIELDS);
   cs.reserve(std::max(qs.n_ub, 1), SURF_FIELDS);
-  E = CorrArgs{qe.pts, qe.d_n, qe.n_ub, ge.pool.p, ge.head.p, ge.bits, ge.mask, ge.xyz.p, ce.rec.p,
+  E = CorrArgs{qe.pts, qe.d_n, qe.n_ub, ge.pts.p, ge.coarse.p, ge.bits, ge.mask, ge.xyz.p, ce.rec.p,
                ce.valid.p, ce.nnxyz.p, ce.trace ? ce.nnidx.p : nullptr, ce.trace ? ce.nnsqd.p : nullptr, ce.cap};
-  S = CorrArgs{qs.pts, qs.d_n, qs.n_ub, gs.pool.p, gs.head.p, gs.bits, gs.mask, gs.xyz.p, cs.rec.p,
+  S = CorrArgs{qs.pts, qs.d_n, qs.n_ub, gs.pts.p, gs.coarse.p, gs.bits, gs.mask, gs.xyz.p, cs.rec.p,
                cs.valid.p, cs.nnxyz.p, cs.trace ? cs.nnidx.p : nullptr, cs.trace ? cs.nnsqd.p : nullptr, cs.cap};
 }
 
@@ -1462,7 +1560,7 @@ void knn_launch(LMState* d_st, const double* x0_dev, const QuerySet& qe, const G
   const int nS = qs.grid_hint > 0 ? std::min(qs.grid_hint, qs.n_ub) : qs.n_ub;
   const unsigned nbE = std::min(div_up((size_t)std::max(nE, 1) * G, kTB), 4096u);
   const unsigned nbS = std::min(div_up((size_t)std::max(nS, 1) * G, kTB), 8192u);
-  hipLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6>), dim3(nbE + nbS), dim3(kTB), 0, st, d_st, x0_dev, E, S,
+  hipLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6, 3>), dim3(nbE + nbS), dim3(kTB), 0, st, d_st, x0_dev, E, S,
                        (int)nbE, d_me, d_ms, rank, world);
   FLOAM_LAUNCH_CHECK();
 }
@@ -1560,16 +1658,16 @@ void knn_stage_launch(LMState* d_st, const double* x0_dev, const QuerySet& qe, c
     FLOAM_LAUNCH_CHECK();
   };
   flush();
-  hipLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6, 1>), g, dim3(kTB), 0, st, d_st, x0_dev, E, S, (int)nbE,
+  hipLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6, 3, 1>), g, dim3(kTB), 0, st, d_st, x0_dev, E, S, (int)nbE,
                      d_me, d_ms, rank, world);
   flush();
-  hipLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6, 2>), g, dim3(kTB), 0, st, d_st, x0_dev, E, S, (int)nbE,
+  hipLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6, 3, 2>), g, dim3(kTB), 0, st, d_st, x0_dev, E, S, (int)nbE,
                      d_me, d_ms, rank, world);
   flush();
-  hipLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6, 3>), g, dim3(kTB), 0, st, d_st, x0_dev, E, S, (int)nbE,
+  hipLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6, 3, 3>), g, dim3(kTB), 0, st, d_st, x0_dev, E, S, (int)nbE,
                      d_me, d_ms, rank, world);
   flush();
-  hipLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6, 4>), g, dim3(kTB), 0, st, d_st, x0_dev, E, S, (int)nbE,
+  hipLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6, 3, 4>), g, dim3(kTB), 0, st, d_st, x0_dev, E, S, (int)nbE,
                      d_me, d_ms, rank, world);
   flush();   // (the real search follows, cold as well)
   FLOAM_LAUNCH_CHECK();
@@ -1579,14 +1677,14 @@ void knn_traffic_launch(const LMState* d_st, const QuerySet& q, const Grid& g, C
                         DevBuf<unsigned long long>& set, unsigned long long* d_bytes, hipStream_t st) {
   if (q.n_ub <= 0) return;
   int bits = 10;
-  while ((1 << bits) < 256 * q.n_ub) ++bits;   // distinct occupied cells scanned (<= 125 per query)
+  while ((1 << bits) < 64 * q.n_ub) ++bits;   // distinct occupied cells scanned (<= 27 per query)
   set.reserve((size_t)1 << bits);
   CorrArgs A, B;
   corr_args(q, g, c, q, g, c, A, B);
   for (int level = 0; level < 2; ++level) {
     FLOAM_HIP(hipMemsetAsync(set.p, 0xFF, sizeof(unsigned long long) << bits, st));
     hipLaunchKernelGGL(knn_traffic, dim3(div_up(q.n_ub, kTB)), dim3(kTB), 0, st, d_st, A, rank, world,
-                       level, set.p, (1u << bits) - 1u, bits, d_bytes);
+                       level, 3, set.p, (1u << bits) - 1u, bits, d_bytes);
     FLOAM_LAUNCH_CHECK();
   }
 }

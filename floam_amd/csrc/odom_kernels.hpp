@@ -8,83 +8,69 @@
 namespace floam {
 
 // ----------------------------------------------------------------------------------------- hash grid
-// Map points bucketed into fine cells (edge 0.5 m, ABSOLUTE coordinates: no bounding box) of a persistent hash table
-// (grid.hpp); every cell owns a contiguous range of a point pool.  The kNN probes the 27 fine cells around a query
-// (stage 1) and the fine cells covering [q - r, q + r] (stage 2).  Layout order inside a cell is not deterministic; the
-// kNN breaks distance ties by map index, so results are.  Exact replacement of the 5-NN KD-tree under the reference's
-// sqd[4] < 1 gate (knn_group).
-//
-// A build (grid.hip) is two launches, both maps at once:
-//   grid_fill    per point: its cell found (plain load; a cell not in the table is inserted with capacity 0), its
-//                fill incremented (one atomic per cell and wave), the point written at start + rank when the rank is
-//                inside the cell's capacity, else kept as an overflow entry; the point's coordinates by map index
-//   grid_fixup   per overflow entry: its cell moved to a fresh range of the pool (the first of the cell's entries
-//                allocates it, copies the points already in the old range and publishes it; the others wait for it),
-//                the point written at new start + rank
-// and a clear that runs inside an earlier launch (the status gather, after the last kNN of an update): every listed
-// cell's fill and relocation words reset — or, when the table holds too many cells or the pool is nearly used up,
-// everything reset (the next build then relocates every cell: a full rebuild).
+// Map points bucketed into a two-level cubic grid with ABSOLUTE cell coordinates (no bounding box): fine cells of
+// edge kFineCell = 0.5 m nested 2x2x2 in coarse cells of 1 m.  Built without sorting (grid.hip): points are counted
+// per coarse cell and fine sub-cell (atomics into an open-addressing table of coarse cells), every coarse cell gets
+// a contiguous range of `pts` (block-aggregated bump allocation, fine sub-cells consecutive inside it), and the
+// points are scattered into place.  The coarse table maps a 64-bit cell key to its range and its 8 sub-cell counts,
+// from which the kNN derives every fine cell's range (no fine-cell table).
+// Layout order inside a cell is not deterministic; the kNN breaks distance ties by map index, so results are.
+// Exact replacement of the 5-NN KD-tree under the reference's sqd[4] < 1 gate (knn_group).
+
 struct Grid {
-  DevBuf<CellHead> head;
-  DevBuf<CellAux> aux;
-  DevBuf<float4> pool;
+  DevBuf<float4> pts;        // {x, y, z, map index bits}, grouped by coarse cell then fine sub-cell
   DevBuf<float4> xyz;        // {x, y, z, 0} by map index: 16-B neighbour gathers from a compact, L2-resident array
-  DevBuf<int> cells;         // the persistent list of occupied slots
-  DevBuf<int4> ovf;          // overflow entries of a build
-  DevBuf<float4> ovf_pt;
-  DevBuf<int> ctr;           // [2][kGridCtrWords] by build parity
-  int bits = 0;              // table size = 1 << bits (at least twice the map size: load <= 1/2 plus one build)
+  DevBuf<CoarseCell> coarse;
+  DevBuf<uint2> where;       // per map point: coarse slot, sub-cell << 28 | rank in the sub-cell
+  // occupied slots of the coarse table (persistent: a build appends the cells new to the map)
+  DevBuf<int> clist;
+  DevBuf<int> counters;      // [0] bump cursor, [1..2] coarse list length (by build parity)
+  int bits = 0;              // table size = 1 << bits (at least twice the map size: load <= 1/2)
   unsigned mask = 0;
-  int parity = 0;            // the counters of the next build: ctr + parity * kGridCtrWords
-  int ub = 0;                // the map size the pool and the table were sized for
-  bool fresh = true;         // table or pool (re)allocated: the next clear is a full one
+  int parity = 0;
+  bool fresh = true;         // tables (re)allocated: the next clear is a full one
   bool precleared = false;   // the next build's clear was issued in advance (grid_clear_prepare)
 };
 
-// The clear of the next build (see above) as a device job, so that it can run inside an earlier launch once the
-// previous grid's last reader (the kNN) is done.  Reads the previous build's counters, writes the next build's.
+// The first step of a grid build — reset the counts of the listed cells (the whole table after a reallocation or
+// when too many stale cells accumulated) and the cursors — as a device job, so that it can run inside an earlier
+// launch once the previous grid's last reader (the kNN) is done.
 struct GridClearDev {
-  CellHead* head;
-  CellAux* aux;
-  const int* cells;
-  const int* ctr_old;
-  int* ctr_new;
-  int full;          // the host's verdict: a fresh table or pool
+  CoarseCell* coarse;
+  const int* clist_old;
+  int* counters;
+  int parity;
+  int full_clear;
   unsigned mask;
-  int gc_cells;      // more listed cells than this: full reset (table load)
-  int gc_cursor;     // pool cursor beyond this: full reset (room for one build's relocations)
 };
+// Cells persist from build to build (their keys stay in the table and in the slot list, so a build inserts only the
+// cells new to the map): the clear resets the counts and ranges of the listed cells.  When the list holds more than
+// a quarter of the table (stale cells of a map that moved on) or the table is fresh, everything is emptied instead.
+// The decision reads the previous build's list length only (the lead writes the next build's words), so every
+// thread takes the same branch.
 __device__ __forceinline__ void grid_clear_part(const GridClearDev& J, int t0, int stride, bool lead) {
-  const int nc = J.ctr_old[1], cur = J.ctr_old[0];
-  const bool full = J.full || nc > J.gc_cells || cur > J.gc_cursor;   // (uniform: nobody writes ctr_old here)
-  CellAux a;
-  a.cap = 0;
-  a.lock = 0;
-  a.nstart = -1;
-  a.pad = 0;
+  const int nc = J.counters[1 + (J.parity ^ 1)];
+  const bool full = J.full_clear || nc > (int)((J.mask + 1u) >> 2);
   if (full) {
-    CellHead h;
-    h.key = kEmptyKey;
-    h.start = 0;
-    h.fill = 0;
+    CoarseCell e;
+    e.key = kEmptyKey;
+    e.start = 0;
+    e.total = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) e.sub[k] = 0;
     const int size = (int)J.mask + 1;
-    for (int t = t0; t < size; t += stride) {
-      J.head[t] = h;
-      J.aux[t] = a;
-    }
+    for (int t = t0; t < size; t += stride) J.coarse[t] = e;
   } else {
-    for (int t = t0; t < nc; t += stride) {
-      const int slot = J.cells[t];
-      J.head[slot].fill = 0;
-      J.aux[slot].lock = 0;
-      J.aux[slot].nstart = -1;
+    for (int t = t0; t < nc; t += stride) {   // (the key stays: 48 B of counts and range reset)
+      char* c = reinterpret_cast<char*>(&J.coarse[J.clist_old[t]]);
+      *reinterpret_cast<int2*>(c + 8) = make_int2(0, 0);
+      *reinterpret_cast<int4*>(c + 16) = make_int4(0, 0, 0, 0);
+      *reinterpret_cast<int4*>(c + 32) = make_int4(0, 0, 0, 0);
     }
   }
   if (lead) {
-    J.ctr_new[0] = full ? 0 : cur;
-    J.ctr_new[1] = full ? 0 : nc;
-    J.ctr_new[2] = 0;
-    J.ctr_new[3] = 0;
+    J.counters[0] = 0;
+    J.counters[1 + J.parity] = full ? 0 : nc;   // the next build appends its new cells after the persistent ones
   }
 }
 // sizes the grid for a map of up to ub points and returns its next build's clear (the build is then issued with
@@ -92,16 +78,13 @@ __device__ __forceinline__ void grid_clear_part(const GridClearDev& J, int t0, i
 GridClearDev grid_clear_prepare(Grid& g, int ub, hipStream_t st);
 
 struct OdomDev;
-// Rebuild the grids of both local maps (corner and surf) in two launches (three when not precleared).  predict
+// Rebuild the grids of both local maps (corner and surf) in four launches (three when precleared).  predict
 // (nullable): the update's constant-velocity prediction (odom_predict_step) runs in the first of them instead of a
 // launch of its own.
 void geom_stamps_print();   // -DFLOAM_GEOM_STAMPS (diagnostic build)
 void grid_build_launch(Grid& gE, const PointRec* mapE, const int* d_mE, int mE_ub, Grid& gS, const PointRec* mapS,
                        const int* d_mS, int mS_ub, hipStream_t st, OdomDev* predict = nullptr, bool precleared = false,
-                       size_t mE_cap = 0, size_t mS_cap = 0,   // caps: the maps' buffer sizes (speculative loads)
-                       int* err = nullptr);                     // err: OdomDev::grid_err (a failed build poisons)
-// the build's counters (the kNN and the traffic counter read the table only)
-inline int* grid_ctr(const Grid& g, int parity) { return g.ctr.p + parity * kGridCtrWords; }
+                       size_t mE_cap = 0, size_t mS_cap = 0);   // caps: the maps' buffer sizes (speculative loads)
 
 // ----------------------------------------------------------------------------------------- correspondences
 // Edge record (EdgeAnalyticCostFunction inputs): cp (sensor point), a, b.  Surf: cp, unit normal n, d.
@@ -244,8 +227,6 @@ struct OdomDev {
   int kf_flag;             // the last KeyFrameUpdate result: gates the map update
   int failed;              // a solve ended without its blocks' hand-offs (n_res < 0): from then on the status
                            // gathers leave the pose, the keyframe and the maps untouched (the host raises the error)
-  int grid_err;            // a kNN grid build could not place its points (grid.hip grid_fixup; never expected): the
-                           // same freeze
   double x0[2][7];         // parameters {q, t} of the predictions of the first / second call
 };
 void odom_dev_init_launch(OdomDev* s, hipStream_t st);   // identity poses, no keyframes
@@ -265,8 +246,6 @@ struct UpdateStatus {
   int counts[4];                  // downsampled edge, surf; corner map, surf map
   int fe_status;                  // status flags of the feature extraction that produced the inputs (async FE)
   int kf_flag;                    // KeyFrameUpdate result of this call (when it ran)
-  int grid_err;                   // a kNN grid build of this handle failed (OdomDev::grid_err)
-  int grid_err_pad;
   unsigned long long prof[2];     // algorithmic bytes of the kNN launches (profiling)
   Pose odom, last_odom;           // controller poses after this call
   unsigned seq;                   // the update's serial number, stored last (system scope): the host polls it
