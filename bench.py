@@ -620,6 +620,22 @@ def main():
                    "config": f"c3: {m3.rings}-ring synthetic scans ({raws3[0].shape[0]} pts), map prefilled "
                              f"{synth.MAP_PREFILL.get('c3', 0)} pts, sharded like the main line ({allreduce_impl})",
                    "same_config_1gpu": c3_1gpu}
+        # the deployment that scales: every rank runs its own C3 sequence unsharded (one odometry per
+        # sensor); the aggregate is all ranks' scans over the max-over-ranks time of the same timed region
+        lp3, odo3 = make_pipeline(sharded=False, params_=p3, maps=maps3)
+        ps3 = []
+        run(lp3, odo3, 0, args.warmup, ps3, d_raw3)
+        barrier_sync()
+        t1 = time.perf_counter()
+        run(lp3, odo3, args.warmup, n_scans, ps3, d_raw3)
+        barrier_sync()
+        t = torch.tensor([time.perf_counter() - t1], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        odo3.close()
+        lp3.close()
+        c3_line["replica"] = {"value": round(world * args.steps / float(t.item()), 3), "unit": "scans/s",
+                              "scaling": "weak", "note": f"replica x{world}: every rank its own unsharded c3 "
+                                                         f"sequence (all ranks' scans / max-over-ranks time)"}
         for c in list(d_raw3) + list(maps3):
             c.close()
         lp, odo = None, None

@@ -2,19 +2,21 @@
 //
 // Reference: src/odomEstimationClass.cpp:78-79 rebuilds pcl::KdTreeFLANN over both maps on every
 // updatePointsToMap call; here the grids are rebuilt only when the maps changed (a keyframe, :117-122), both maps in
-// the same launches:
-//   grid_clear   reset the counts and ranges of the listed cells (run inside the status gather before the build;
-//                keys stay: cells persist from build to build, the whole table is emptied only after a resize or
-//                when stale cells fill a quarter of it)
-//   grid_count   per point: find its coarse cell (1 m, absolute coordinates -> 64-bit key; a plain-load probe, CAS
-//                only for a cell new to the map, which is appended to the list), count it in its fine sub-cell
-//                (0.5 m) and keep its rank there
-//   grid_alloc   per listed coarse cell: a contiguous range of the cell-grouped array (one atomic per block on a
-//                bump cursor), fine sub-cells consecutive inside it
+// the same four launches:
+//   grid_clear   empty the table entries the previous build occupied (its slot lists; everything after a resize) —
+//                run inside the status gather before the build (grid_clear_prepare)
+//   grid_count   per point: insert its coarse cell (1 m, absolute coordinates -> 64-bit key; new cells appended to
+//                the occupied list), count it in its fine sub-cell (0.5 m) and keep its rank there
+//   grid_alloc   per occupied coarse cell (from the list): a contiguous range of the cell-grouped array (one atomic
+//                per block on a bump cursor), fine sub-cells consecutive inside it
 //   grid_scatter per point: its slot = coarse start + preceding sub-cells + rank
-// No bounding box, no sort: O(M) work, every step one launch; count and scatter take XCD-local point ranges.
-// (Measured against it, profiles/r05b_proto_fine_cells: a fine-cell table whose cells kept their pool ranges across
-// builds — one counting launch plus a relocation fix-up — took 36 us for the build and made the kNN 1.6x slower.)
+// No bounding box, no sort: O(M) work, every step one launch.
+// Incremental variants measured against this rebuild (round 5) and not kept:
+//  * a fine-cell table whose cells keep their pool ranges across builds (one counting launch + a relocation fix-up,
+//    no alloc / scatter pass): build 23.7 + 12.1 us and the kNN 22 -> 36 us (27 probes per query, cells scattered
+//    through the pool) — profiles/r05b_proto_fine_cells (prototype.patch);
+//  * this table with persistent cells (keys kept, counts reset; plain-load probes, CAS only for new cells) and
+//    XCD-local point ranges: count 14.1, alloc 5.3, scatter 6.3 us against 13.5, 5.1, 5.1 — profiles/r05c_proto_persistent_cells.
 #include "floam_common.hpp"
 #include "grid.hpp"
 #include "odom_kernels.hpp"
@@ -66,15 +68,13 @@ __global__ __launch_bounds__(kTB) void grid_count(GridJob E, GridJob S, OdomDev*
   const GridJob& J = blockIdx.y == 0 ? E : S;
   if (predict && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) odom_predict_step(predict);
   // the first stride's point loaded speculatively beside the device count (inside the map's buffer), so the
-  // inserts start one memory round trip earlier; the load is used only when i < m.  XCD-aware: the blocks of one XCD
-  // take consecutive point ranges (xcd_block), so each XCD's L2 holds the table lines of a slab of the map
-  const int lb = xcd_block((int)blockIdx.x, (int)gridDim.x);
-  const int i_first = lb * blockDim.x + threadIdx.x;
+  // inserts start one memory round trip earlier; the load is used only when i < m
+  const int i_first = blockIdx.x * blockDim.x + threadIdx.x;
   float4 p_first = make_float4(0.f, 0.f, 0.f, 0.f);
   if (i_first < J.spec_ub) p_first = *reinterpret_cast<const float4*>(&J.map[i_first].x);
   const int m = min(*J.d_m, J.m_ub);
   const GridCountDev C = count_dev(J);
-  for (int i0 = lb * blockDim.x; i0 < m; i0 += gridDim.x * blockDim.x) {   // wave-uniform trip count
+  for (int i0 = blockIdx.x * blockDim.x; i0 < m; i0 += gridDim.x * blockDim.x) {   // wave-uniform trip count
     const int i = i0 + threadIdx.x;
     const bool valid = i < m;
     float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -126,9 +126,8 @@ __global__ __launch_bounds__(kTB) void grid_alloc(GridJob E, GridJob S) {
 
 __global__ __launch_bounds__(kTB) void grid_scatter(GridJob E, GridJob S) {
   const GridJob& J = blockIdx.y == 0 ? E : S;
-  // the first stride's slot word and point loaded speculatively beside the device count (inside both buffers);
-  // XCD-aware point ranges as in grid_count
-  const int i_first = xcd_block((int)blockIdx.x, (int)gridDim.x) * blockDim.x + threadIdx.x;
+  // the first stride's slot word and point loaded speculatively beside the device count (inside both buffers)
+  const int i_first = blockIdx.x * blockDim.x + threadIdx.x;
   uint2 wr_first = make_uint2(0u, 0u);
   float4 p_first = make_float4(0.f, 0.f, 0.f, 0.f);
   if (i_first < J.spec_ub) {
@@ -161,7 +160,7 @@ void reserve_grid(Grid& g, int ub) {
   while ((1 << bits) < 2 * ub) ++bits;
   if (bits > g.bits) {   // (reserve keeps the arrays when their capacity already covers the larger table)
     g.coarse.reserve((size_t)1 << bits);
-    g.clist.reserve((size_t)1 << bits);
+    for (int k = 0; k < 2; ++k) g.clist[k].reserve((size_t)1 << bits);
     g.bits = bits;
     g.mask = (1u << bits) - 1u;
     g.fresh = true;
@@ -169,13 +168,13 @@ void reserve_grid(Grid& g, int ub) {
 }
 
 GridClearDev clear_job(const Grid& g) {
-  return GridClearDev{g.coarse.p, g.clist.p, g.counters.p, g.parity, g.fresh ? 1 : 0, g.mask};
+  return GridClearDev{g.coarse.p, g.clist[g.parity ^ 1].p, g.counters.p, g.parity, g.fresh ? 1 : 0, g.mask};
 }
 
 GridJob make_job(Grid& g, const PointRec* map, const int* d_m, int m_ub, size_t map_cap = 0) {
   const int p = g.parity;
   const int spec = (int)std::min<size_t>({(size_t)m_ub, map_cap, g.where.cap});
-  return GridJob{map, d_m, m_ub, spec, g.pts.p, g.coarse.p, g.where.p, g.xyz.p, g.clist.p, g.clist.p,
+  return GridJob{map, d_m, m_ub, spec, g.pts.p, g.coarse.p, g.where.p, g.xyz.p, g.clist[p].p, g.clist[p ^ 1].p,
                  g.counters.p, p, g.fresh ? 1 : 0, g.bits, g.mask};
 }
 }  // namespace

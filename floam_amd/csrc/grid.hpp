@@ -51,8 +51,7 @@ struct alignas(64) CoarseCell {   // 64 B, one per half cache line: a probe neve
 };
 constexpr unsigned long long kEmptyKey = ~0ull;
 
-// The per-point step of a grid build (grid.hip), also run by the map update that writes the map (mapmerge.hip): the
-// point's coarse cell inserted (new cells appended to the build's slot list), its fine sub-cell counted and its rank
+// The per-point step of a grid build (grid.hip): the point's coarse cell inserted (new cells appended to the build's slot list), its fine sub-cell counted and its rank
 // there kept in where[i].
 struct GridCountDev {
   CoarseCell* coarse;
@@ -118,31 +117,24 @@ __device__ __forceinline__ void grid_count_points(const GridCountDev& J, const i
     fresh[r] = false;
     h[r] = ins[r] ? coarse_slot(key[r], J.bits) : 0u;
   }
-  // the leaders' lookups: every round's probe issued together, until each found its cell or an empty slot.  Cells
-  // persist from build to build, so most probes find their key with a plain load; an empty slot is claimed by CAS
-  // (another wave may have claimed it for the same cell just before: then it is found)
+  // the leaders' inserts: every round's probe issued together, until each found its cell or an empty slot
   for (;;) {
     unsigned long long prev[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) prev[r] = ins[r] ? J.coarse[h[r]].key : key[r];
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-      if (ins[r] && prev[r] == kEmptyKey) {
-        prev[r] = atomicCAS(&J.coarse[h[r]].key, kEmptyKey, key[r]);
-        if (prev[r] == kEmptyKey) fresh[r] = true;
-      }
+    for (int r = 0; r < R; ++r) prev[r] = ins[r] ? atomicCAS(&J.coarse[h[r]].key, kEmptyKey, key[r]) : key[r];
     bool more = false;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       if (!ins[r]) continue;
-      if (fresh[r] || prev[r] == key[r]) {
+      if (prev[r] == kEmptyKey) fresh[r] = true;
+      if (prev[r] == kEmptyKey || prev[r] == key[r]) {
         ins[r] = false;
       } else {
         h[r] = (h[r] + 1) & J.mask;
         more = true;
       }
     }
-    if (!__any(more)) break;
+    if (!more) break;
   }
   int leader2[R], base[R];
   unsigned long long sub_grp[R];

@@ -22,9 +22,9 @@ struct Grid {
   DevBuf<float4> xyz;        // {x, y, z, 0} by map index: 16-B neighbour gathers from a compact, L2-resident array
   DevBuf<CoarseCell> coarse;
   DevBuf<uint2> where;       // per map point: coarse slot, sub-cell << 28 | rank in the sub-cell
-  // occupied slots of the coarse table (persistent: a build appends the cells new to the map)
-  DevBuf<int> clist;
-  DevBuf<int> counters;      // [0] bump cursor, [1..2] coarse list length (by build parity)
+  // occupied slots of the coarse table, per build parity: the next build clears exactly these entries
+  DevBuf<int> clist[2];
+  DevBuf<int> counters;      // [0] bump cursor, [1..2] coarse list sizes (by parity)
   int bits = 0;              // table size = 1 << bits (at least twice the map size: load <= 1/2)
   unsigned mask = 0;
   int parity = 0;
@@ -32,9 +32,9 @@ struct Grid {
   bool precleared = false;   // the next build's clear was issued in advance (grid_clear_prepare)
 };
 
-// The first step of a grid build — reset the counts of the listed cells (the whole table after a reallocation or
-// when too many stale cells accumulated) and the cursors — as a device job, so that it can run inside an earlier
-// launch once the previous grid's last reader (the kNN) is done.
+// The first step of a grid build — empty the table entries the previous build occupied (its slot list; the whole
+// table after a reallocation) and reset the cursors — as a device job, so that it can run inside an earlier launch
+// once the previous grid's last reader (the kNN) is done.
 struct GridClearDev {
   CoarseCell* coarse;
   const int* clist_old;
@@ -43,34 +43,23 @@ struct GridClearDev {
   int full_clear;
   unsigned mask;
 };
-// Cells persist from build to build (their keys stay in the table and in the slot list, so a build inserts only the
-// cells new to the map): the clear resets the counts and ranges of the listed cells.  When the list holds more than
-// a quarter of the table (stale cells of a map that moved on) or the table is fresh, everything is emptied instead.
-// The decision reads the previous build's list length only (the lead writes the next build's words), so every
-// thread takes the same branch.
 __device__ __forceinline__ void grid_clear_part(const GridClearDev& J, int t0, int stride, bool lead) {
-  const int nc = J.counters[1 + (J.parity ^ 1)];
-  const bool full = J.full_clear || nc > (int)((J.mask + 1u) >> 2);
-  if (full) {
-    CoarseCell e;
-    e.key = kEmptyKey;
-    e.start = 0;
-    e.total = 0;
+  CoarseCell e;
+  e.key = kEmptyKey;
+  e.start = 0;
+  e.total = 0;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) e.sub[k] = 0;
+  for (int k = 0; k < 8; ++k) e.sub[k] = 0;
+  if (J.full_clear) {
     const int size = (int)J.mask + 1;
     for (int t = t0; t < size; t += stride) J.coarse[t] = e;
   } else {
-    for (int t = t0; t < nc; t += stride) {   // (the key stays: 48 B of counts and range reset)
-      char* c = reinterpret_cast<char*>(&J.coarse[J.clist_old[t]]);
-      *reinterpret_cast<int2*>(c + 8) = make_int2(0, 0);
-      *reinterpret_cast<int4*>(c + 16) = make_int4(0, 0, 0, 0);
-      *reinterpret_cast<int4*>(c + 32) = make_int4(0, 0, 0, 0);
-    }
+    const int nc = J.counters[1 + (J.parity ^ 1)];
+    for (int t = t0; t < nc; t += stride) J.coarse[J.clist_old[t]] = e;
   }
   if (lead) {
     J.counters[0] = 0;
-    J.counters[1 + J.parity] = full ? 0 : nc;   // the next build appends its new cells after the persistent ones
+    J.counters[1 + J.parity] = 0;
   }
 }
 // sizes the grid for a map of up to ub points and returns its next build's clear (the build is then issued with
