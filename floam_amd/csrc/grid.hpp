@@ -51,8 +51,8 @@ struct alignas(64) CoarseCell {   // 64 B, one per half cache line: a probe neve
 };
 constexpr unsigned long long kEmptyKey = ~0ull;
 
-// The per-point step of a grid build (grid.hip): the point's coarse cell inserted (new cells appended to the build's slot list), its fine sub-cell counted and its rank
-// there kept in where[i].
+// The per-point step of a grid build (grid.hip): the point's coarse cell inserted (new cells appended to the build's
+// slot list), its fine sub-cell counted and its rank there kept in where[i].
 struct GridCountDev {
   CoarseCell* coarse;
   uint2* where;
