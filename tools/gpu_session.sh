@@ -6,6 +6,7 @@
 #   prof[=ARGS]    tools/gpu_prof.sh: bench + rocprofv3 kernel-trace stats + FETCH_SIZE / WRITE_SIZE passes
 #   n2             tools/gpu_n2.sh: the N = 2 bench line rehearsed with two ranks on this one GPU
 #   stamps         tools/gpu_stamps.sh: the LM solve's segment stamps (diagnostic build)
+#   sweep=CONFIG   tools/precision_sweep.py: fp64 / fp32 / fp32-geometry poses against the oracle (8 scans)
 #   envab=SPEC;..  tools/gpu_envab.sh over environment settings (SPEC NAME:VAR=V,VAR=V; ';'-separated)
 #   libab=NAME,..  tools/gpu_libab.sh: the tree's library against prebuilt ones (floam_amd/ab/)
 # Usage: bash tools/gpu_session.sh TAG STEP...
@@ -34,6 +35,10 @@ for step in "$@"; do
     prof) bash tools/gpu_prof.sh ${TAG}/prof ${arg//,/ } || exit $? ;;
     n2) bash tools/gpu_n2.sh ${TAG}/n2 || exit $? ;;
     stamps) bash tools/gpu_stamps.sh ${TAG}/stamps || exit $? ;;
+    sweep)
+      timeout -k 10 600 python tools/precision_sweep.py --config ${arg:-c5} --scans 8 --out $OUT/precision_${arg:-c5}.json \
+          > $OUT/precision_${arg:-c5}.log 2>&1 || { tail -20 $OUT/precision_${arg:-c5}.log; exit 1; }
+      tail -12 $OUT/precision_${arg:-c5}.log ;;
     envab) IFS=';' read -ra specs <<< "$arg"; bash tools/gpu_envab.sh ${TAG}/envab "${specs[@]}" || exit $? ;;
     libab) bash tools/gpu_libab.sh ${TAG}/libab ${arg//,/ } || exit $? ;;
     *) echo "unknown step $name"; exit 2 ;;
