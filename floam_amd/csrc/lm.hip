@@ -594,15 +594,17 @@ __device__ __forceinline__ void next_step_wave(LMState& s, bool check_gmax, int 
     CTRL_T(tc);
     CTRL_ADD(2, tb - ta);
     CTRL_ADD(3, tc - tb);
-    // (wave-uniform) lane 1 computed the projection: the lanes' outputs differ and lane 0's is broadcast; otherwise
-    // every lane holds the candidate already (no read-lanes on the common path)
+    // (wave-uniform) lane 1 computed the projection: it measures its own distance to x, which is read from it (one
+    // read-lane pair), and takes the candidate from lane 0 by a DPP quad permutation [0, 0, 2, 3] (every other lane
+    // computed the candidate itself); otherwise every lane holds the candidate already
     const bool proj = check_gmax && !far;
     if (check_gmax) {
       double m = HUGE_VAL;   // (far: the test fails; only the comparison with the tolerance is used)
       if (proj) {
-        m = 0.0;
+        double ml = 0.0;
 #pragma unroll
-        for (int i = 0; i < 7; ++i) m = fmax(m, fabs(s.x[i] - bcast(out[i], 1)));
+        for (int i = 0; i < 7; ++i) ml = fmax(ml, fabs(s.x[i] - out[i]));
+        m = bcast(ml, 1);
       }
       s.gmax = m;
       check_gmax = false;
@@ -611,7 +613,7 @@ __device__ __forceinline__ void next_step_wave(LMState& s, bool check_gmax, int 
     s.iteration++;
     if (valid) {
 #pragma unroll
-      for (int i = 0; i < 7; ++i) s.cand[i] = proj ? bcast(out[i], 0) : out[i];
+      for (int i = 0; i < 7; ++i) s.cand[i] = proj ? dpp_f64<0xE0>(out[i]) : out[i];
       s.invalid = 0;
       CTRL_T(td);
       CTRL_ADD(4, td - tc);

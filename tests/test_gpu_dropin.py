@@ -16,16 +16,21 @@ def _params(R):
     return LidarParams(num_lines=R, scan_period=0.1, vertical_angle=2.0, max_distance=90.0, min_distance=0.5)
 
 
-@pytest.mark.parametrize("config,nscan", [("c1", 6), ("c3", 3)])
-def test_host_entry_points_match_device_path(floam_gpu, config, nscan):
+@pytest.mark.parametrize("config,nscan,graph", [("c1", 6, False), ("c3", 3, False), ("c1", 6, True)])
+def test_host_entry_points_match_device_path(floam_gpu, monkeypatch, config, nscan, graph):
+    """graph: the host-path odometry created with FLOAM_GRAPH=1 (hipGraph capture of each update, a documented
+    product variable): the one-call entry point's write-back copy stream must stay out of the capture."""
     from floam_amd.odom_estimation import reset_process_state
     R = synth.lidar_model(config).rings
     pipes = []
-    for _ in range(2):
+    for j in range(2):
         lp = floam_gpu.LaserProcessingClass()
         lp.init(_params(R))
+        if graph and j == 1:
+            monkeypatch.setenv("FLOAM_GRAPH", "1")   # (read when the handle is created)
         odo = floam_gpu.OdomEstimationClass()
         odo.init(_params(R), 0.1, "Cauchy")
+        monkeypatch.delenv("FLOAM_GRAPH", raising=False)
         pipes.append((lp, odo))
     poses = {0: [], 1: []}
     for k in range(nscan):
