@@ -150,7 +150,8 @@ def main():
     allreduce_impl = None
     uid = None
     if mode == "shard":
-        uid = [(comm_unique_id(), comm_unique_id()) if rank == 0 else None]   # timed run, byte-count replay
+        # one RCCL communicator per sharded pipeline: timed run, byte-count replay, the C3 line, a fallback rebuild
+        uid = [tuple(comm_unique_id() for _ in range(4)) if rank == 0 else None]
         if dist is not None:
             dist.broadcast_object_list(uid, src=0)
     n_pipelines = 0
@@ -293,7 +294,28 @@ def main():
         same_cfg_1gpu = round(args.steps / dt1, 3)
     lp, odo = make_pipeline()
     poses = []
-    run(lp, odo, 0, args.warmup, poses)
+    peer_failed = False
+    try:
+        run(lp, odo, 0, args.warmup, poses)
+    except floam_amd.FloamError as e:   # (the peer exchange is the one path that can fail here on a new node)
+        if allreduce_impl != "peer":
+            raise
+        log(f"[rank {rank}] peer exchange failed in the warm-up ({e})")
+        peer_failed = True
+    if allreduce_impl == "peer" and dist is not None:
+        import torch
+        t = torch.tensor([1 if peer_failed else 0], dtype=torch.int32)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        if int(t.item()):   # every rank leaves the peer exchange together and shards through RCCL instead
+            for h in (odo, lp):
+                try:
+                    h.close()
+                except floam_amd.FloamError:
+                    pass
+            peer_ok[0] = False
+            lp, odo = make_pipeline()
+            poses = []
+            run(lp, odo, 0, args.warmup, poses)
     barrier_sync()
     _ffi.check(L.floam_profile_mark(dev, 1))   # trace marker: the timed region starts (tools/prof_summary.py)
     barrier_sync()
