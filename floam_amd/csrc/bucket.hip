@@ -621,16 +621,25 @@ __global__ __launch_bounds__(kTB) void bucket_compact(VoxelJobDev A, VoxelJobDev
       const float4 f = L.u.pt[e];
       float s0 = f.x, s1 = f.y, s2 = f.z, s3 = f.w;
       int j = e + 1;
-      // 8 keys and 8 points per LDS round trip (the points loaded beside the keys, not after the run test), the
-      // additions in order up to the first key of another voxel
+      // 8 keys and 8 points per LDS round trip (the points loaded beside the keys, not after the run test), the next
+      // 8 loaded before the additions of these 8 (long runs — dense voxels near the sensor — stream at the rate of the
+      // in-order adds, not of one LDS round trip per 8), the additions in order up to the first key of another voxel
+      uint32_t kq[8];
+      float4 p[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int jj = min(j + q, nc - 1);
+        kq[q] = L.k[jj];
+        p[q] = L.u.pt[jj];
+      }
       for (bool more = true; more && j < nc;) {
-        uint32_t kq[8];
-        float4 p[8];
+        uint32_t kn[8];
+        float4 pn[8];
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
-          const int jj = min(j + q, nc - 1);
-          kq[q] = L.k[jj];
-          p[q] = L.u.pt[jj];
+          const int jj = min(j + 8 + q, nc - 1);
+          kn[q] = L.k[jj];
+          pn[q] = L.u.pt[jj];
         }
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
@@ -640,6 +649,11 @@ __global__ __launch_bounds__(kTB) void bucket_compact(VoxelJobDev A, VoxelJobDev
           } else {
             more = false;
           }
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          kq[q] = kn[q];
+          p[q] = pn[q];
         }
       }
       if (j == nc && streamed && c0 + nc < size) {   // reaches the chunk end of a streamed bucket: carried over
