@@ -629,13 +629,10 @@ __device__ __forceinline__ void fine_block_ranges(const CorrArgs& A, int lx, int
 // entries [27][9], then s_pre [126] and s_start [125]).  Against the coarse box of round 4 the fine box scans a
 // third to a half of the volume at the stage-2 radii that occur (1.5-2 m of span per axis instead of 2-3 m).
 constexpr int kStage2Cells = 125;
-constexpr int kBoxLds = 27 * 9 > 2 * kStage2Cells + 1 ? 27 * 9 : 2 * kStage2Cells + 1;
-constexpr int kGroupLds = kBoxLds + 11;   // ints per query group: + stage 1's list and count parked during stage 2's ranges
-// Cells of the stage-1 block [lx, lx + 2] x [ly, ly + 2] x [lz, lz + 2] are left out (count 0): stage 2 continues
-// stage 1's top-5, which already holds the block's points.
+constexpr int kGroupLds = 27 * 9 > 2 * kStage2Cells + 1 ? 27 * 9 : 2 * kStage2Cells + 1;   // ints per query group
 template <int G>
 __device__ __forceinline__ int fine_box_ranges(const CorrArgs& A, int fx0, int fx1, int fy0, int fy1, int fz0,
-                                               int fz1, int lx, int ly, int lz, int lane, int* __restrict__ s_buf) {
+                                               int fz1, int lane, int* __restrict__ s_buf) {
   const int cx0 = fx0 >> 1, cy0 = fy0 >> 1, cz0 = fz0 >> 1;   // floor division by 2
   const int ncx = (fx1 >> 1) - cx0 + 1, ncy = (fy1 >> 1) - cy0 + 1, ncz = (fz1 >> 1) - cz0 + 1;
   const int nco = ncx * ncy * ncz;   // <= 27
@@ -700,9 +697,8 @@ __device__ __forceinline__ int fine_box_ranges(const CorrArgs& A, int fx0, int f
 #pragma unroll
       for (int k = 0; k < 8; ++k)
         if (k < sub) start += cc[1 + k];
-      const bool in_block = (unsigned)(fx - lx) < 3u && (unsigned)(fy - ly) < 3u && (unsigned)(fz - lz) < 3u;
       st[j] = start;
-      ct[j] = in_block ? 0 : cc[1 + sub];
+      ct[j] = cc[1 + sub];
       local += ct[j];
     }
   }
@@ -904,34 +900,13 @@ __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArg
         // the ball of its float sq-distance d5, and r = sqrt(d5) (1 + 1e-6) covers that ball with margin — a point
         // outside the box is more than r away along one axis, so its float sq-distance is >= r^2 (1 - 2^-24)^5 > d5
         // (monotone rounding of the 3 squares and 2 adds) and it can neither enter nor tie the top-5
-        // The scan continues stage 1's top-5 and count over the box's cells outside the stage-1 block: the top-5 of
-        // the union is the top-5 of the box (a block point outside the box is more than r away, beyond the true 5th
-        // distance), and a block point outside the box is at float sq-distance >= 1 when r = 1 (not counted twice
-        // nor wrongly) while cnt >= 5 already holds when r < 1
         double r = 1.0;
         if (cnt >= 5) r = fmin(1.0, sqrt((double)__uint_as_float((unsigned)(t.k[4] >> 32))) * (1.0 + 1e-6));
-        // every lane holds the merged list and count: lane 0 carries them on (parked in LDS while the box's ranges are
-        // built, so they hold no registers there), the other lanes restart empty
-        int* const park = s_buf + kBoxLds;
-        if (lane == 0) {
-#pragma unroll
-          for (int k = 0; k < 5; ++k) {
-            park[2 * k] = (int)(unsigned)t.k[k];
-            park[2 * k + 1] = (int)(unsigned)(t.k[k] >> 32);
-          }
-          park[10] = cnt;
-        }
 #pragma unroll
         for (int k = 0; k < 5; ++k) t.k[k] = ~0ull;
         cnt = 0;
         const int2 sx = fine_span(wx, r), sy = fine_span(wy, r), sz = fine_span(wz, r);
-        const int tot2 = fine_box_ranges<G>(A, sx.x, sx.y, sy.x, sy.y, sz.x, sz.y, lx, ly, lz, lane, s_buf);
-        if (lane == 0) {
-#pragma unroll
-          for (int k = 0; k < 5; ++k)
-            t.k[k] = ((unsigned long long)(unsigned)park[2 * k + 1] << 32) | (unsigned)park[2 * k];
-          cnt = park[10];
-        }
+        const int tot2 = fine_box_ranges<G>(A, sx.x, sx.y, sy.x, sy.y, sz.x, sz.y, lane, s_buf);
         walk_cells<G, U>(A, tot2, s_buf, s_buf + kStage2Cells + 1, wx, wy, wz, lane, t, cnt);
         group_merge<G>(t, cnt);
         flags |= 2;
