@@ -622,112 +622,61 @@ __device__ __forceinline__ void fine_block_ranges(const CorrArgs& A, int lx, int
   wave_lds_order();
 }
 
-// Stage 2's box, in FINE cells: [fx0, fx1] x [fy0, fy1] x [fz0, fz1] (at most 5 per axis: the box [q - r, q + r] with
-// r <= 1 m), from the entries of the coarse cells that hold them (at most 3 per axis).  Lanes probe the coarse cells
-// (two each, first probes issued together) into LDS, every lane derives the (start, count) of its run of fine cells
-// into registers, and — once the group has read the entries — the prefix and starts overwrite them (s_buf: the coarse
-// entries [27][9], then s_pre [126] and s_start [125]).  Against the coarse box of round 4 the fine box scans a
-// third to a half of the volume at the stage-2 radii that occur (1.5-2 m of span per axis instead of 2-3 m).
-constexpr int kStage2Cells = 125;
-constexpr int kGroupLds = 27 * 9 > 2 * kStage2Cells + 1 ? 27 * 9 : 2 * kStage2Cells + 1;   // ints per query group
-template <int G>
-__device__ __forceinline__ int fine_box_ranges(const CorrArgs& A, int fx0, int fx1, int fy0, int fy1, int fz0,
-                                               int fz1, int lane, int* __restrict__ s_buf) {
-  const int cx0 = fx0 >> 1, cy0 = fy0 >> 1, cz0 = fz0 >> 1;   // floor division by 2
-  const int ncx = (fx1 >> 1) - cx0 + 1, ncy = (fy1 >> 1) - cy0 + 1, ncz = (fz1 >> 1) - cz0 + 1;
-  const int nco = ncx * ncy * ncz;   // <= 27
-  {
-    constexpr int PC = (27 + G - 1) / G;
-    unsigned long long key[PC];
-    unsigned slot[PC];
-    int4 h[PC], s0[PC], s1[PC];
+template <int G, int U, bool COARSE, int NB = 3>
+__device__ __forceinline__ void stencil_scan(const CorrArgs& A, int x0, int x1, int y0, int y1, int z0, int z1,
+                                             float wx, float wy, float wz, int lane, int* __restrict__ s_pre,
+                                             int* __restrict__ s_start, Top5& t, int& cnt,
+                                             int* __restrict__ s_cc = nullptr) {
+  constexpr int P = (kMaxStencil + G - 1) / G;   // cells per lane
+  const int nxr = x1 - x0 + 1, nyr = y1 - y0 + 1, nzr = z1 - z0 + 1;
+  const int ncell = nxr * nyr * nzr;
+  int tot;
+  if constexpr (!COARSE) {   // the fine block with low corner (x0, y0, z0), ranges from the coarse entries
+    fine_block_ranges<G, NB>(A, x0, y0, z0, lane, s_pre, s_start, s_cc);
+    tot = s_pre[NB * NB * NB];
+  } else {
+  const int per = (ncell + G - 1) / G;
+  const int cb = min(ncell, lane * per), ce = min(ncell, cb + per);
+  unsigned long long key[P];
+  unsigned slot[P];
+  int4 e[P];
 #pragma unroll
-    for (int j = 0; j < PC; ++j) {   // first probes of both cells issued before either is waited on
-      const int c = lane + j * G;
-      key[j] = kEmptyKey;
-      h[j] = make_int4(-1, -1, 0, 0);
-      s0[j] = s1[j] = make_int4(0, 0, 0, 0);
-      if (c < nco) {
-        key[j] = cell_key(cx0 + c % ncx, cy0 + (c / ncx) % ncy, cz0 + c / (ncx * ncy));
-        slot[j] = coarse_slot(key[j], A.bits);
-        const int4* e = reinterpret_cast<const int4*>(&A.coarse[slot[j]]);
-        h[j] = e[0];
-        s0[j] = e[1];
-        s1[j] = e[2];
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < PC; ++j) {
-      const int c = lane + j * G;
-      if (c >= nco) continue;
-      unsigned long long k = ((unsigned long long)(unsigned)h[j].y << 32) | (unsigned)h[j].x;
-      while (k != key[j] && k != kEmptyKey) {   // collision chain (rare)
-        slot[j] = (slot[j] + 1) & A.mask;
-        const int4* e = reinterpret_cast<const int4*>(&A.coarse[slot[j]]);
-        h[j] = e[0];
-        s0[j] = e[1];
-        s1[j] = e[2];
-        k = ((unsigned long long)(unsigned)h[j].y << 32) | (unsigned)h[j].x;
-      }
-      const bool hit = k == key[j];
-      int* cc = s_buf + 9 * c;
-      cc[0] = hit ? h[j].z : 0;
-      cc[1] = hit ? s0[j].x : 0; cc[2] = hit ? s0[j].y : 0; cc[3] = hit ? s0[j].z : 0; cc[4] = hit ? s0[j].w : 0;
-      cc[5] = hit ? s1[j].x : 0; cc[6] = hit ? s1[j].y : 0; cc[7] = hit ? s1[j].z : 0; cc[8] = hit ? s1[j].w : 0;
+  for (int j = 0; j < P; ++j) {
+    const int c = cb + j;
+    key[j] = kEmptyKey;
+    e[j] = make_int4(-1, -1, 0, 0);
+    if (c < ce) {
+      key[j] = cell_key(x0 + c % nxr, y0 + (c / nxr) % nyr, z0 + c / (nxr * nyr));
+      slot[j] = coarse_slot(key[j], A.bits);
+      e[j] = *reinterpret_cast<const int4*>(&A.coarse[slot[j]]);
     }
   }
-  wave_lds_order();
-  const int nfx = fx1 - fx0 + 1, nfy = fy1 - fy0 + 1;
-  const int nf = nfx * nfy * (fz1 - fz0 + 1);   // <= 125
-  constexpr int P = (kStage2Cells + G - 1) / G;
-  const int per = (nf + G - 1) / G;
-  const int cb = min(nf, lane * per), ce = min(nf, cb + per);
-  int st[P], ct[P];
   int local = 0;
 #pragma unroll
   for (int j = 0; j < P; ++j) {
     const int c = cb + j;
-    st[j] = ct[j] = 0;
     if (c < ce) {
-      const int fx = fx0 + c % nfx, fy = fy0 + (c / nfx) % nfy, fz = fz0 + c / (nfx * nfy);
-      const int ci = ((fx >> 1) - cx0) + ncx * (((fy >> 1) - cy0) + ncy * ((fz >> 1) - cz0));
-      const int sub = (fx & 1) | ((fy & 1) << 1) | ((fz & 1) << 2);
-      const int* cc = s_buf + 9 * ci;
-      int start = cc[0];
-#pragma unroll
-      for (int k = 0; k < 8; ++k)
-        if (k < sub) start += cc[1 + k];
-      st[j] = start;
-      ct[j] = cc[1 + sub];
-      local += ct[j];
+      unsigned long long k = ((unsigned long long)(unsigned)e[j].y << 32) | (unsigned)e[j].x;
+      while (k != key[j] && k != kEmptyKey) {   // collision chain (rare)
+        slot[j] = (slot[j] + 1) & A.mask;
+        e[j] = *reinterpret_cast<const int4*>(&A.coarse[slot[j]]);
+        k = ((unsigned long long)(unsigned)e[j].y << 32) | (unsigned)e[j].x;
+      }
+      const bool hit = k == key[j];
+      s_start[c] = hit ? e[j].z : 0;
+      s_pre[c] = local;
+      local += hit ? e[j].w : 0;
     }
   }
   const int incl = group_incl_scan<G>(local, lane);
-  int run = incl - local;
-  wave_lds_order();   // (every lane of the group has read the coarse entries: the prefix may overwrite them)
-  int* s_pre = s_buf;
-  int* s_start = s_buf + kStage2Cells + 1;
+  const int excl = incl - local;
 #pragma unroll
-  for (int j = 0; j < P; ++j) {
-    const int c = cb + j;
-    if (c < ce) {
-      s_pre[c] = run;
-      s_start[c] = st[j];
-      run += ct[j];
-    }
-  }
-  const int tot = __shfl(incl, G - 1, G);
-  if (lane == 0) s_pre[nf] = tot;
+  for (int j = 0; j < P; ++j)
+    if (cb + j < ce) s_pre[cb + j] += excl;
+  tot = __shfl(incl, G - 1, G);
+  if (lane == 0) s_pre[ncell] = tot;
   wave_lds_order();
-  return tot;
-}
-
-// walk the flattened candidate list of the cells prepared in s_pre / s_start (tot candidates) into the lane-local
-// top-5
-template <int G, int U>
-__device__ __forceinline__ void walk_cells(const CorrArgs& A, int tot, const int* __restrict__ s_pre,
-                                           const int* __restrict__ s_start, float wx, float wy, float wz, int lane,
-                                           Top5& t, int& cnt) {
+  }
   int c = 0, c_lo = 0, c_hi = s_pre[1], c_start = s_start[0];   // cursor: cell c = [c_lo, c_hi)
   for (int tb = 0; tb < tot; tb += G * U) {
     float4 m[U];
@@ -834,22 +783,13 @@ template <bool EDGE, typename R>
 __device__ __forceinline__ bool geom_fit(const R (&P)[5][3], float4 pq, double* __restrict__ rec, int cap, int i,
                                          double* __restrict__ w, const double* o);
 
-// the fine cells [lo, hi] per axis that cover [v - r, v + r] (exact in double: v is a float, r has a 1e-6 margin)
-__device__ __forceinline__ int2 fine_span(float v, double r) {
-  return make_int2((int)floor(((double)v - r) * 2.0), (int)floor(((double)v + r) * 2.0));
-}
-
 // STOP (diagnostic, FLOAM_KNN_STAGES: the per-round-trip read attribution of DESIGN.md §3) ends each query after
 // its first STOP dependent memory round trips — 1: the query load and transform; 2: + the coarse probes of the fine
 // block; 3: + stage 1's candidate loads; 4: + stage 2 — and writes only a flag derived from what it loaded
 template <int G, int U, int NB, int STOP = 0>
 __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArgs& A, int gid, int ngroups,
-                                          int lane, bool gate, int rank, int world, int* __restrict__ s_buf) {
-  // the group's LDS: stage 1 — the 8 coarse entries [8][9], the prefix [28] and the starts [27]; stage 2 —
-  // fine_box_ranges' layout (kGroupLds ints)
-  int* const s_cc = s_buf;
-  int* const s_pre = s_buf + 72;
-  int* const s_start = s_buf + 72 + kMaxStencil + 1;
+                                          int lane, bool gate, int rank, int world, int* __restrict__ s_pre,
+                                          int* __restrict__ s_start, int* __restrict__ s_cc) {
   const int n = min(*A.d_n, A.n_ub);
   const int lo = (int)(((long long)n * rank) / world), hi = (int)(((long long)n * (rank + 1)) / world);
   // grid-stride over the queries the device holds (the host only knows an upper bound)
@@ -879,8 +819,8 @@ __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArg
         wave_lds_order();
         continue;
       }
-      fine_block_ranges<G, NB>(A, lx, ly, lz, lane, s_pre, s_start, s_cc);
-      walk_cells<G, U>(A, s_pre[NB * NB * NB], s_pre, s_start, wx, wy, wz, lane, t, cnt);
+      stencil_scan<G, U, false, NB>(A, lx, lx + NB - 1, ly, ly + NB - 1, lz, lz + NB - 1, wx, wy, wz, lane, s_pre,
+                                    s_start, t, cnt, s_cc);
       group_merge<G>(t, cnt);
       // exact early exit: a map point outside the fine block [lo, hi) (lo = l / 2, hi = (l + NB) / 2 per axis, exact
       // in float) lies beyond a face, so on that axis |fl(q - p)| >= fl(q - lo) or fl(hi - q) (monotone rounding)
@@ -895,7 +835,7 @@ __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArg
         continue;
       }
       if (!complete) {
-        // fine cells floor(2 (q - r)) .. floor(2 (q + r)) per axis (exact in double).  r = 1 (every point within 1 m)
+        // coarse cells floor(q - r) .. floor(q + r) per axis (exact in double).  r = 1 (every point within 1 m)
         // unless stage 1 already holds 5 points within 1 m: then the 5-NN and every point tied with the 5th lie in
         // the ball of its float sq-distance d5, and r = sqrt(d5) (1 + 1e-6) covers that ball with margin — a point
         // outside the box is more than r away along one axis, so its float sq-distance is >= r^2 (1 - 2^-24)^5 > d5
@@ -905,9 +845,10 @@ __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArg
 #pragma unroll
         for (int k = 0; k < 5; ++k) t.k[k] = ~0ull;
         cnt = 0;
-        const int2 sx = fine_span(wx, r), sy = fine_span(wy, r), sz = fine_span(wz, r);
-        const int tot2 = fine_box_ranges<G>(A, sx.x, sx.y, sy.x, sy.y, sz.x, sz.y, lane, s_buf);
-        walk_cells<G, U>(A, tot2, s_buf, s_buf + kStage2Cells + 1, wx, wy, wz, lane, t, cnt);
+        stencil_scan<G, U, true>(A, (int)floor((double)wx - r), (int)floor((double)wx + r),
+                                 (int)floor((double)wy - r), (int)floor((double)wy + r),
+                                 (int)floor((double)wz - r), (int)floor((double)wz + r), wx, wy, wz, lane, s_pre,
+                                 s_start, t, cnt);
         group_merge<G>(t, cnt);
         flags |= 2;
       }
@@ -945,7 +886,9 @@ __global__ __launch_bounds__(kTB, W) void knn_kernel(LMState* __restrict__ st, c
                                                   CorrArgs E, CorrArgs S, int nbE,
                                                   const int* __restrict__ d_me, const int* __restrict__ d_ms,
                                                   int rank, int world) {
-  __shared__ int s_buf[kTB / G][kGroupLds];
+  __shared__ int s_pre[kTB / G][kMaxStencil + 1];
+  __shared__ int s_start[kTB / G][kMaxStencil];
+  __shared__ int s_cc[kTB / G][8 * 9];
   const int lane = threadIdx.x & (G - 1);
   const int g = threadIdx.x / G;
   double pose[7];   // wave-uniform: kept in SGPRs (readfirstlane), not in 14 VGPRs of every lane
@@ -974,7 +917,7 @@ __global__ __launch_bounds__(kTB, W) void knn_kernel(LMState* __restrict__ st, c
   const int nact = min(nb, (int)(((long long)nq * G + kTB - 1) / kTB));
   if (p < nact) p = xcd_block(p, nact);
   knn_group<G, U, NB, STOP>(pose, A, (p * kTB + (int)threadIdx.x) / G, nb * (kTB / G), lane, gate, rank, world,
-                            s_buf[g]);
+                            s_pre[g], s_start[g], s_cc[g]);
 }
 
 // Pass 2: line / plane geometry, one query per lane (all 64 lanes busy), in R = double (the reference's precision)
@@ -1242,8 +1185,8 @@ __global__ __launch_bounds__(kTB) void geom_kernel(LMState* __restrict__ st, Cor
 
 // Algorithmic traffic of one launch of the search kernel (knn_kernel; SURVEY.md §8 d): every map
 // cell any query scans is streamed once (16 B per map point: the union over queries of the fine 3x3x3 block around
-// the query's cell — level 0 — and of the fine cells covering [q - r, q + r] for the queries whose bit 1 says they
-// needed stage 2 — level 1), every query is read once (16 B) and writes its flag (1 B) and, with 5 neighbours, their coordinates
+// the query's cell — level 0 — and of the coarse +-1 m stencil for the queries whose bit 1 says they needed stage 2
+// — level 1), every query is read once (16 B) and writes its flag (1 B) and, with 5 neighbours, their coordinates
 // (60 B) (counted at level 0).  Runs untimed, on a replay, only when profiling.
 //
 // The radius of a query's stage 2 (knn_group): 1, or with 5 points within 1 m in the fine block around the query's
@@ -1308,8 +1251,9 @@ __global__ __launch_bounds__(kTB) void knn_traffic(const LMState* __restrict__ s
   int x0, y0, z0, x1, y1, z1;
   if (level) {
     const double r = stage2_radius(A, nb, wx, wy, wz);
-    const int2 sx = fine_span(wx, r), sy = fine_span(wy, r), sz = fine_span(wz, r);
-    x0 = sx.x; x1 = sx.y; y0 = sy.x; y1 = sy.y; z0 = sz.x; z1 = sz.y;
+    x0 = (int)floor((double)wx - r); x1 = (int)floor((double)wx + r);
+    y0 = (int)floor((double)wy - r); y1 = (int)floor((double)wy + r);
+    z0 = (int)floor((double)wz - r); z1 = (int)floor((double)wz + r);
   } else {
     int qx, qy, qz;
     fine_cell(wx, wy, wz, qx, qy, qz);
@@ -1320,7 +1264,7 @@ __global__ __launch_bounds__(kTB) void knn_traffic(const LMState* __restrict__ s
     for (int y = y0; y <= y1; ++y)
       for (int x = x0; x <= x1; ++x) {
         const unsigned long long k = cell_key(x, y, z);
-        const int cnt = fine_count(A, x, y, z);
+        const int cnt = level ? grid_lookup(A.coarse, k, A.bits, A.mask).y : fine_count(A, x, y, z);
         if (cnt == 0) continue;
         unsigned h = hash_slot64(k, set_bits);
         for (;;) {
