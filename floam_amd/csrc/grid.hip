@@ -158,6 +158,7 @@ void reserve_grid(Grid& g, int ub) {
   // capacity >= 2 x points >= 2 x cells: the load never exceeds 1/2, so every insert and every probe of an absent
   // cell (the kNN's lookups) reaches an empty slot and terminates, even when every point has a cell of its own
   while ((1 << bits) < 2 * ub) ++bits;
+  bits = std::max(bits, kDirectBits);   // (the direct-indexed table's minimum, grid.hpp coarse_slot)
   if (bits > g.bits) {   // (reserve keeps the arrays when their capacity already covers the larger table)
     g.coarse.reserve((size_t)1 << bits);
     for (int k = 0; k < 2; ++k) g.clist[k].reserve((size_t)1 << bits);

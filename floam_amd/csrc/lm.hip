@@ -442,96 +442,63 @@ __host__ __device__ constexpr int hidx(int a, int b) {   // upper-triangle row-m
   return a * 6 - a * (a - 1) / 2 + (b - a);
 }
 
-// LevenbergMarquardtStrategy::ComputeStep in normal-equation form on the Jacobi-scaled system:
-// (Hs + diag(Hs)/radius) y = gs, step = -y; then TrustRegionMinimizer::ComputeTrustRegionStep's model cost change.
-// (The oracle solves the equivalent [J; sqrt(D/radius)] least-squares problem by Householder QR like Ceres'
-// DENSE_QR; the two agree to ~cond * eps.)  Returns false for an invalid step; delta = scaled step.
-__device__ __forceinline__ bool solve_step(LMState& s, double (&delta)[6]) {
-  double sc[6], gs[6], Hu[21], dg[6];
-#pragma unroll
-  for (int a = 0; a < 6; ++a) {
-    sc[a] = s.scale[a];
-    dg[a] = s.diag[a];
-  }
-#pragma unroll
-  for (int k = 0; k < 21; ++k) Hu[k] = s.H[k];
-#pragma unroll
-  for (int a = 0; a < 6; ++a) gs[a] = sc[a] * s.g[a];
-  const int reuse = s.reuse;
-  const double inv_radius = recip(s.radius);
-  // packed lower triangle (row-major, l(i,j) = i(i+1)/2 + j): Hs = S H S, then A = Hs + diag/radius factored in place
-  double Hs[21], A[21];
-#pragma unroll
-  for (int i = 0; i < 6; ++i)
-#pragma unroll
-    for (int j = 0; j <= i; ++j) {
-      Hs[i * (i + 1) / 2 + j] = sc[i] * Hu[hidx(j, i)] * sc[j];
-      A[i * (i + 1) / 2 + j] = Hs[i * (i + 1) / 2 + j];
-    }
-  if (!reuse) {
-#pragma unroll
-    for (int k = 0; k < 6; ++k) dg[k] = fmin(fmax(Hs[k * (k + 1) / 2 + k], 1e-6), 1e32);
-#pragma unroll
-    for (int k = 0; k < 6; ++k) s.diag[k] = dg[k];
-  }
-  s.reuse = 1;
-  // LDL^T of A = Hs + diag / radius (no square roots on the dependent chain; one reciprocal per pivot): W[i][j] =
-  // L[i][j] D[j] is kept beside L, packed lower like A
-#pragma unroll
-  for (int k = 0; k < 6; ++k) A[k * (k + 1) / 2 + k] += dg[k] * inv_radius;
-  double W[21], rD[6];
+// LevenbergMarquardtStrategy::ComputeStep in normal-equation form + TrustRegionMinimizer::ComputeTrustRegionStep's
+// model cost change, on the UNSCALED system.  Ceres solves the Jacobi-scaled system (S H S + D / radius) y = S g with
+// S = diag(scale) and D = clamp(diag(S H S), 1e-6, 1e32), and steps by delta = -S y.  With z = S y that is
+// (H + E / radius) z = g, delta = -z, where E = D S^-2 = clamp(diag(H), 1e-6 S^-2, 1e32 S^-2) (bounds fixed with S
+// at iteration zero: LMState::dlo, dhi), and the model cost change (y.Sg + y.D y / radius) / 2 = (z.g + z.E z /
+// radius) / 2 — the same step in exact arithmetic without the 54 products of the scaling; the rounding differs at
+// ~cond * eps, as the oracle's Householder QR of [J; sqrt(D / radius)] (Ceres' DENSE_QR) differs from both.
+// LDL^T by rows (W = L D of the current row only, one reciprocal per pivot).  Returns false for an invalid step.
+__device__ __forceinline__ bool lm_step(const double (&H)[21], const double (&g)[6], const double (&E)[6],
+                                        double inv_r, double (&z)[6], double& mcc) {
+  double L[15], rD[6];   // L strictly lower, packed by rows: l(i, j) = i (i - 1) / 2 + j
   bool pd = true;
 #pragma unroll
-  for (int j = 0; j < 6; ++j) {
-    double d = A[j * (j + 1) / 2 + j];
+  for (int i = 0; i < 6; ++i) {
+    double W[6];
 #pragma unroll
-    for (int k = 0; k < j; ++k) d -= A[j * (j + 1) / 2 + k] * W[j * (j + 1) / 2 + k];
-    pd = pd && (d > 0.0);
-    rD[j] = recip(d);
+    for (int j = 0; j < i; ++j) {
+      double w = H[hidx(j, i)];
 #pragma unroll
-    for (int i = j + 1; i < 6; ++i) {
-      double v = A[i * (i + 1) / 2 + j];
-#pragma unroll
-      for (int k = 0; k < j; ++k) v -= A[i * (i + 1) / 2 + k] * W[j * (j + 1) / 2 + k];
-      W[i * (i + 1) / 2 + j] = v;            // L[i][j] D[j]
-      A[i * (i + 1) / 2 + j] = v * rD[j];    // L[i][j]
+      for (int k = 0; k < j; ++k) w -= W[k] * L[j * (j - 1) / 2 + k];
+      W[j] = w;                            // L[i][j] D[j]
+      L[i * (i - 1) / 2 + j] = w * rD[j];
     }
+    double d = fma(E[i], inv_r, H[hidx(i, i)]);
+#pragma unroll
+    for (int k = 0; k < i; ++k) d -= W[k] * L[i * (i - 1) / 2 + k];
+    pd = pd && (d > 0.0);
+    rD[i] = recip(d);
   }
   if (!pd) return false;
   double y[6];
 #pragma unroll
-  for (int i = 0; i < 6; ++i) {   // L z = gs
-    double v = gs[i];
+  for (int i = 0; i < 6; ++i) {   // L u = g
+    double v = g[i];
 #pragma unroll
-    for (int k = 0; k < i; ++k) v -= A[i * (i + 1) / 2 + k] * y[k];
+    for (int k = 0; k < i; ++k) v -= L[i * (i - 1) / 2 + k] * y[k];
     y[i] = v;
   }
 #pragma unroll
-  for (int i = 5; i >= 0; --i) {   // L^T y = D^-1 z (the newest unknown, y[i + 1], enters last: one FMA a row)
+  for (int i = 5; i >= 0; --i) {   // L^T z = D^-1 u
     double v = y[i] * rD[i];
 #pragma unroll
-    for (int k = 5; k > i; --k) v -= A[k * (k + 1) / 2 + i] * y[k];
-    y[i] = v;
+    for (int k = 5; k > i; --k) v -= L[k * (k - 1) / 2 + i] * z[k];
+    z[i] = v;
   }
   bool finite = true;
 #pragma unroll
-  for (int k = 0; k < 6; ++k) finite = finite && isfinite(y[k]);
+  for (int k = 0; k < 6; ++k) finite = finite && isfinite(z[k]);
   if (!finite) return false;
-  // model cost change -(step^T gs + step^T Hs step / 2) with step = -y and (Hs + D / radius) y = gs:
-  // = (y^T gs + y^T (D / radius) y) / 2 — two 6-term sums instead of the 6x6 quadratic form (equal in exact
-  // arithmetic; both terms non-negative, so no cancellation)
-  double yg = 0.0, yDy = 0.0;
+  double zg = 0.0, zEz = 0.0;
 #pragma unroll
   for (int a = 0; a < 6; ++a) {
-    yg += y[a] * gs[a];
-    yDy += (y[a] * y[a]) * dg[a];
+    zg += z[a] * g[a];
+    zEz += (z[a] * z[a]) * E[a];
   }
-  const double mcc = 0.5 * (yg + yDy * inv_radius);
-  if (!(mcc > 0.0)) return false;
-  s.mcc = mcc;
-#pragma unroll
-  for (int k = 0; k < 6; ++k) delta[k] = -y[k] * sc[k];
-  return true;
+  mcc = 0.5 * (zg + zEz * inv_r);
+  return mcc > 0.0;
 }
 
 // -DFLOAM_CTRL_STAMPS (diagnostic build): block 0's control-step segments, s_memrealtime (100 MHz), accumulated by
@@ -559,14 +526,14 @@ __device__ __forceinline__ double bcast(double v, int src) {
   return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
-// NextStep with the gradient-norm test folded in: ComputeTrustRegionStep (+ HandleInvalidStep retries) and, when
-// check_gmax, the projected-gradient max norm at x (lane 1) computed alongside the candidate (lane 0).  If the
-// gradient test ends the solve the step is discarded, as in the sequential order (test first, then step).
-// The gradient test only asks whether max_i |x_i - (x [+] -g)_i| <= 1e-10.  A rotation of angle th moves the unit
-// quaternion by |dq - 1| = 2 |sin(th / 4)| in the 2-norm (the product with q preserves it), so some component by at
-// least |sin(th / 4)|: when th / 4 is more than 1e-6 from every multiple of pi (a two-constant reduction, exact far
-// beyond any gradient) the test fails without the projection.  Large gradients are the rule before convergence, and
-// their angle would send lane 1 through the library sincos's range reduction while lane 0 waits (one wave).
+// The gradient-norm test (at iteration zero and after a successful step) only asks whether
+// max_i |x_i - (x [+] -g)_i| <= 1e-10; lane 1 forms the projection x [+] -g beside lane 0's candidate, in the same
+// instruction stream.  If the test ends the solve the step is discarded, as in the sequential order (test first, then
+// step).  A rotation of angle th moves the unit quaternion by |dq - 1| = 2 |sin(th / 4)| in the 2-norm (the product
+// with q preserves it), so some component by at least |sin(th / 4)|: when th / 4 is more than 1e-6 from every multiple
+// of pi (a two-constant reduction, exact far beyond any gradient) the test fails without the projection.  Large
+// gradients are the rule before convergence, and their angle would send lane 1 through the library sincos's range
+// reduction while lane 0 waits (one wave).
 __device__ __forceinline__ bool gradient_step_far(const double (&g)[6]) {
   const double th = sqrt(g[0] * g[0] + g[1] * g[1] + g[2] * g[2]);
   if (!(th > 1.5625 && th < 1e15)) return false;   // (small angles take sincos_small anyway)
@@ -577,55 +544,11 @@ __device__ __forceinline__ bool gradient_step_far(const double (&g)[6]) {
   return fabs(r) > 1e-6 && fabs(r) < 3.1415916;
 }
 
-__device__ __forceinline__ void next_step_wave(LMState& s, bool check_gmax, int lane) {
-  for (;;) {
-    CTRL_T(ta);
-    double delta[6];
-    const bool valid = solve_step(s, delta);
-    CTRL_T(tb);
-    // lane 1: the gradient projection x [+] -g, when the test is due and cannot be decided from the angle alone
-    const bool far = check_gmax && gradient_step_far(s.g);   // (wave-uniform: every lane holds the same g)
-    double d[6];
-#pragma unroll
-    for (int k = 0; k < 6; ++k)   // (lane 1 without a projection to compute follows lane 0: no divergent branch)
-      d[k] = (lane == 1 && check_gmax && !far) ? -s.g[k] : (valid ? delta[k] : 0.0);
-    double out[7];
-    se3_plus(s.x, d, out);
-    CTRL_T(tc);
-    CTRL_ADD(2, tb - ta);
-    CTRL_ADD(3, tc - tb);
-    // (wave-uniform) lane 1 computed the projection: it measures its own distance to x, which is read from it (one
-    // read-lane pair), and takes the candidate from lane 0 by a DPP quad permutation [0, 0, 2, 3] (every other lane
-    // computed the candidate itself); otherwise every lane holds the candidate already
-    const bool proj = check_gmax && !far;
-    if (check_gmax) {
-      double m = HUGE_VAL;   // (far: the test fails; only the comparison with the tolerance is used)
-      if (proj) {
-        double ml = 0.0;
-#pragma unroll
-        for (int i = 0; i < 7; ++i) ml = fmax(ml, fabs(s.x[i] - out[i]));
-        m = bcast(ml, 1);
-      }
-      s.gmax = m;
-      check_gmax = false;
-      if (s.gmax <= 1e-10) { s.done = 1; return; }   // (phase 0: before any step; phase 1: success && gmax)
-    }
-    s.iteration++;
-    if (valid) {
-#pragma unroll
-      for (int i = 0; i < 7; ++i) s.cand[i] = proj ? dpp_f64<0xE0>(out[i]) : out[i];
-      s.invalid = 0;
-      CTRL_T(td);
-      CTRL_ADD(4, td - tc);
-      return;   // candidate pending evaluation
-    }
-    // HandleInvalidStep -> StepIsInvalid -> StepRejected(0)
-    if (++s.invalid >= 5) { s.done = 1; return; }
-    s.radius *= recip(s.dfac);   // (dfac a power of two: exact)
-    s.dfac *= 2.0;
-    s.reuse = 1;
-    if (s.iteration >= 4 || s.radius < 1e-32) { s.done = 1; return; }
-  }
+// H[21] followed by g[6] (H0 by g0), the layout of sums[1..27]: the 27 words, one a lane
+static_assert(offsetof(LMState, g) == offsetof(LMState, H) + 21 * sizeof(double) &&
+              offsetof(LMState, g0) == offsetof(LMState, H0) + 21 * sizeof(double), "H, g contiguous");
+__device__ __forceinline__ double* state_words(LMState& S, size_t off) {
+  return reinterpret_cast<double*>(reinterpret_cast<char*>(&S) + off);
 }
 
 __device__ __forceinline__ double norm7(const double (&a)[7]) {
@@ -635,150 +558,193 @@ __device__ __forceinline__ double norm7(const double (&a)[7]) {
   return sqrt(v);
 }
 
-// One Ceres control step after an evaluation (sums = cost, J^T J, J^T r, count at x in phase 0, else at cand).
-// Called by all 64 lanes of one wave with identical s and sums; every lane ends with the same s.
-__device__ __forceinline__ void lm_logic(LMState& s, const double (&sums)[LM_NSUM], int lane) {
+// One Ceres control step after an evaluation (sums: cost, J^T J, J^T r, count at x in phase 0, else at cand), run by
+// the 64 lanes of one wave on the LM state in LDS.  Every lane reads the same words (LDS broadcast) and computes the
+// same values — but lane 1, which forms the gradient projection of the gradient-norm test beside lane 0's candidate —
+// so every branch is wave-uniform; vector copies (x_in, H0 / g0, H / g on a successful step, the clamp bounds) go one
+// element a lane, and lane 0 writes the scalars back once at the end.  Nothing of the state stays in registers
+// between steps: the evaluation's registers and the step's do not compete (the register-resident form spent a third
+// of its instructions moving the state through the accumulation registers).  The next point is S.cand (every block's
+// evaluation reads it there); S.done ends the solve.  The step itself is NextStep: ComputeTrustRegionStep (lm_step)
+// with HandleInvalidStep's retries, the gradient-norm test folded in.
+__device__ __forceinline__ void control_step(LMState& S, const double* __restrict__ sums, int lane) {
   CTRL_T(t0);
-  bool check_gmax;   // the gradient-norm test is due: at iteration zero and after a successful step
-  if (s.phase == 0) {   // IterationZero
-    s.n_res = (int)sums[28];
-    s.x_cost = sums[0];
-    s.initial_cost = sums[0];
-    if (s.n_res == 0) { s.done = 1; return; }   // no residual blocks: parameters untouched
-    if (!isfinite(s.x_cost)) { s.done = 1; return; }
+  double x[7], c[7];
 #pragma unroll
-    for (int k = 0; k < 21; ++k) s.H[k] = sums[1 + k];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) s.g[k] = sums[22 + k];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) s.scale[k] = 1.0 / (1.0 + sqrt(s.H[hidx(k, k)]));
-    s.x_norm = norm7(s.x);
-    s.radius = 1e4;
-    s.dfac = 2.0;
-    s.reuse = 0;
-    s.invalid = 0;
-    s.iteration = 0;
-    s.phase = 1;
-    check_gmax = true;
+  for (int k = 0; k < 7; ++k) {
+    x[k] = S.x[k];
+    c[k] = S.cand[k];
+  }
+  double x_cost = S.x_cost, radius = S.radius, dfac = S.dfac, mcc = S.mcc, x_norm = S.x_norm, gmax = S.gmax;
+  int iteration = S.iteration, reuse = S.reuse, invalid = S.invalid, successful = S.successful;
+  int phase = S.phase;
+  const double cost = sums[0];
+  int done = 0;
+  bool fresh = false;        // H, g (and E) from this evaluation's sums
+  bool check_gmax = false;   // the gradient-norm test is due: at iteration zero and after a successful step
+  bool moved = false;        // x <- cand
+  if (phase == 0) {   // IterationZero
+    if (lane < 7) S.x_in[lane] = S.x[lane];                // the trace of iteration zero
+    if (lane < 27) state_words(S, offsetof(LMState, H0))[lane] = sums[1 + lane];   // H0, g0
+    const int n_res = (int)sums[28];
+    if (lane == 0) {
+      S.n_res = n_res;
+      S.initial_cost = cost;
+    }
+    x_cost = cost;
+    if (n_res == 0 || !isfinite(cost)) {   // no residual blocks (parameters untouched), or a non-finite cost
+      done = 1;
+    } else {
+      if (lane < 6) {   // Jacobi scaling 1 / (1 + sqrt(H_kk)), as the bounds of the unscaled diagonal (lm_step)
+        const double r = 1.0 + sqrt(sums[1 + hidx(lane, lane)]);
+        S.dlo[lane] = 1e-6 * (r * r);
+        S.dhi[lane] = 1e32 * (r * r);
+      }
+      x_norm = norm7(x);
+      radius = 1e4;
+      dfac = 2.0;
+      reuse = 0;
+      invalid = 0;
+      iteration = 0;
+      phase = 1;
+      fresh = true;
+      check_gmax = true;
+    }
   } else {
-    double cand_cost = sums[0];
-    if (!isfinite(cand_cost)) cand_cost = DBL_MAX;
+    const double cand_cost = isfinite(cost) ? cost : DBL_MAX;
     // ParameterToleranceReached (candidate not applied): |x - cand| <= 1e-8 (|x| + 1e-8), compared squared (both
     // sides are non-negative: no square root on the step's dependent chain)
     double sn2 = 0.0;
 #pragma unroll
-    for (int i = 0; i < 7; ++i) sn2 += (s.x[i] - s.cand[i]) * (s.x[i] - s.cand[i]);
-    const double ptol = 1e-8 * (s.x_norm + 1e-8);
-    if (sn2 <= ptol * ptol) { s.done = 1; return; }
-    // FunctionToleranceReached
-    if (fabs(s.x_cost - cand_cost) <= 1e-6 * s.x_cost) { s.done = 1; return; }
-    // rho = decrease / mcc > 1e-3 decided without the reciprocal (mcc > 0); rho itself only for the radius update
-    const double dec = s.x_cost - cand_cost;
-    check_gmax = dec > 1e-3 * s.mcc;   // (success)
-    if (check_gmax) {
-      const double rho = dec * recip(s.mcc);   // (within an ulp of the division)
-#pragma unroll
-      for (int i = 0; i < 7; ++i) s.x[i] = s.cand[i];
-      s.x_norm = norm7(s.x);
-      s.x_cost = cand_cost;
-#pragma unroll
-      for (int k = 0; k < 21; ++k) s.H[k] = sums[1 + k];
-#pragma unroll
-      for (int k = 0; k < 6; ++k) s.g[k] = sums[22 + k];
-      const double t = 2.0 * rho - 1.0;
-      s.radius = fmin(1e16, s.radius * recip(fmax(1.0 / 3.0, 1.0 - t * t * t)));
-      s.dfac = 2.0;
-      s.reuse = 0;
-      s.successful++;
+    for (int i = 0; i < 7; ++i) sn2 += (x[i] - c[i]) * (x[i] - c[i]);
+    const double ptol = 1e-8 * (x_norm + 1e-8);
+    if (sn2 <= ptol * ptol) {
+      done = 1;
+    } else if (fabs(x_cost - cand_cost) <= 1e-6 * x_cost) {   // FunctionToleranceReached
+      done = 1;
     } else {
-      s.radius *= recip(s.dfac);   // (dfac a power of two: exact)
-      s.dfac *= 2.0;
-      s.reuse = 1;
+      // rho = decrease / mcc > 1e-3 decided without the reciprocal (mcc > 0); rho itself only for the radius update
+      const double dec = x_cost - cand_cost;
+      if (dec > 1e-3 * mcc) {   // success
+        const double rho = dec * recip(mcc);   // (within an ulp of the division)
+#pragma unroll
+        for (int i = 0; i < 7; ++i) x[i] = c[i];
+        x_norm = norm7(x);
+        x_cost = cand_cost;
+        const double t = 2.0 * rho - 1.0;
+        radius = fmin(1e16, radius * recip(fmax(1.0 / 3.0, 1.0 - t * t * t)));
+        dfac = 2.0;
+        reuse = 0;
+        successful++;
+        fresh = true;
+        check_gmax = true;
+        moved = true;
+      } else {
+        radius *= recip(dfac);   // (dfac a power of two: exact)
+        dfac *= 2.0;
+        reuse = 1;
+      }
+      if (iteration >= 4 || radius < 1e-32) done = 1;
     }
-    if (s.iteration >= 4 || s.radius < 1e-32) { s.done = 1; return; }
   }
+  if (fresh && !done && lane < 27) state_words(S, offsetof(LMState, H))[lane] = sums[1 + lane];   // H, g
   CTRL_T(t1);
   CTRL_ADD(1, t1 - t0);
-  next_step_wave(s, check_gmax, lane);   // (one call site: the step's code is inlined once)
+  bool have_cand = false;
+  double out[7];
+  if (!done) {
+    const double* Hp = fresh ? sums + 1 : state_words(S, offsetof(LMState, H));   // H, then g
+    double H[21], g[6], E[6];
+#pragma unroll
+    for (int k = 0; k < 21; ++k) H[k] = Hp[k];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) g[k] = Hp[21 + k];
+    if (!reuse) {
+      wave_lds_order();   // (iteration zero: the bounds written above by lanes 0..5)
+#pragma unroll
+      for (int k = 0; k < 6; ++k) E[k] = fmin(fmax(H[hidx(k, k)], S.dlo[k]), S.dhi[k]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) E[k] = S.diag[k];
+    }
+    const bool new_diag = !reuse;
+    reuse = 1;
+    for (;;) {
+      CTRL_T(ta);
+      double z[6], m = 0.0;
+      const bool valid = lm_step(H, g, E, recip(radius), z, m);
+      CTRL_T(tb);
+      // lane 1: the gradient projection x [+] -g, when the test is due and cannot be decided from the angle alone
+      const bool far = check_gmax && gradient_step_far(g);
+      double d[6];
+#pragma unroll
+      for (int k = 0; k < 6; ++k)   // (lane 1 without a projection to compute follows lane 0: no divergent branch)
+        d[k] = (lane == 1 && check_gmax && !far) ? -g[k] : (valid ? -z[k] : 0.0);
+      se3_plus(x, d, out);
+      CTRL_T(tc);
+      CTRL_ADD(2, tb - ta);
+      CTRL_ADD(3, tc - tb);
+      // (wave-uniform) lane 1 computed the projection: it measures its own distance to x, which is read from it (one
+      // read-lane pair); lane 0 writes the candidate
+      if (check_gmax) {
+        double gm = HUGE_VAL;   // (far: the test fails; only the comparison with the tolerance is used)
+        if (!far) {
+          double ml = 0.0;
+#pragma unroll
+          for (int i = 0; i < 7; ++i) ml = fmax(ml, fabs(x[i] - out[i]));
+          gm = bcast(ml, 1);
+        }
+        gmax = gm;
+        check_gmax = false;
+        if (gmax <= 1e-10) {   // (phase 0: before any step; phase 1: success && gmax)
+          done = 1;
+          break;
+        }
+      }
+      iteration++;
+      if (valid) {
+        mcc = m;
+        invalid = 0;
+        have_cand = true;
+        CTRL_T(td);
+        CTRL_ADD(4, td - tc);
+        break;   // candidate pending evaluation
+      }
+      // HandleInvalidStep -> StepIsInvalid -> StepRejected(0)
+      if (++invalid >= 5) {
+        done = 1;
+        break;
+      }
+      radius *= recip(dfac);   // (dfac a power of two: exact)
+      dfac *= 2.0;
+      if (iteration >= 4 || radius < 1e-32) {
+        done = 1;
+        break;
+      }
+    }
+    if (new_diag && lane == 0) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) S.diag[k] = E[k];
+    }
+  }
+  if (lane == 0) {
+    if (moved) {
+#pragma unroll
+      for (int k = 0; k < 7; ++k) S.x[k] = x[k];
+    }
+    if (have_cand) {
+#pragma unroll
+      for (int k = 0; k < 7; ++k) S.cand[k] = out[k];
+    }
+    S.x_cost = x_cost; S.radius = radius; S.dfac = dfac; S.mcc = mcc; S.x_norm = x_norm; S.gmax = gmax;
+    S.iteration = iteration; S.reuse = reuse; S.invalid = invalid; S.successful = successful;
+    S.phase = phase;
+    S.done = done;
+  }
+  wave_lds_order();
   CTRL_T(t2);
   CTRL_ADD(5, t2 - t0);
   CTRL_ADD(0, 1ull);
-}
-
-// the LM state without the trace fields (the register-resident copy of the control wave writes these back; the
-// trace fields of the LDS copy are written directly at iteration zero)
-__device__ __forceinline__ void store_state_core(LMState& dst, const LMState& s) {
-#pragma unroll
-  for (int k = 0; k < 7; ++k) { dst.x[k] = s.x[k]; dst.cand[k] = s.cand[k]; }
-  dst.x_cost = s.x_cost;
-#pragma unroll
-  for (int k = 0; k < 21; ++k) dst.H[k] = s.H[k];
-#pragma unroll
-  for (int k = 0; k < 6; ++k) { dst.g[k] = s.g[k]; dst.scale[k] = s.scale[k]; dst.diag[k] = s.diag[k]; }
-  dst.radius = s.radius; dst.dfac = s.dfac; dst.mcc = s.mcc; dst.x_norm = s.x_norm; dst.gmax = s.gmax;
-  dst.initial_cost = s.initial_cost;
-  dst.phase = s.phase; dst.done = s.done; dst.iteration = s.iteration; dst.reuse = s.reuse; dst.invalid = s.invalid;
-  dst.successful = s.successful; dst.n_res = s.n_res;
-}
-
-__device__ __forceinline__ void load_state_core(LMState& s, const LMState& src) {
-#pragma unroll
-  for (int k = 0; k < 7; ++k) { s.x[k] = src.x[k]; s.cand[k] = src.cand[k]; }
-  s.x_cost = src.x_cost;
-#pragma unroll
-  for (int k = 0; k < 21; ++k) s.H[k] = src.H[k];
-#pragma unroll
-  for (int k = 0; k < 6; ++k) { s.g[k] = src.g[k]; s.scale[k] = src.scale[k]; s.diag[k] = src.diag[k]; }
-  s.radius = src.radius; s.dfac = src.dfac; s.mcc = src.mcc; s.x_norm = src.x_norm; s.gmax = src.gmax;
-  s.initial_cost = src.initial_cost;
-  s.phase = src.phase; s.done = src.done; s.iteration = src.iteration; s.reuse = src.reuse; s.invalid = src.invalid;
-  s.successful = src.successful; s.n_res = src.n_res;
-}
-
-// iteration zero's trace (x_in, J^T J, J^T r) into the LDS state, by one lane
-__device__ __forceinline__ void record_iteration_zero(LMState& dst, const LMState& s, const double (&sums)[LM_NSUM]) {
-#pragma unroll
-  for (int k = 0; k < 7; ++k) dst.x_in[k] = s.x[k];
-#pragma unroll
-  for (int k = 0; k < 21; ++k) dst.H0[k] = sums[1 + k];
-#pragma unroll
-  for (int k = 0; k < 6; ++k) dst.g0[k] = sums[22 + k];
-}
-
-// one control step by wave 0 on its register state s, with the sums from LDS; lane 0 records iteration zero
-__device__ __forceinline__ void control_step(LMState& s, LMState& sst, const double* sums_lds, int lane) {
-  double sm[LM_NSUM];
-#pragma unroll
-  for (int k = 0; k < LM_NSUM; ++k) sm[k] = sums_lds[k];
-  if (s.phase == 0 && lane == 0) record_iteration_zero(sst, s, sm);
-  lm_logic(s, sm, lane);
-}
-
-// FLOAM_LM_STATE_REGS=0 (A/B builds): the control step on the LDS copy (wave 0) — the state loaded into registers
-// for the step and written back by lane 0, so nothing of it stays live across the evaluations; measured 1.3 % faster
-// before the peer exchange joined the kernel (r04c), after it the compiler spills 12-36 B/lane to scratch in that
-// form and none in the register-resident one (the default)
-#ifndef FLOAM_LM_STATE_REGS
-#define FLOAM_LM_STATE_REGS 1
-#endif
-__device__ __forceinline__ double point_component(const LMState& s, int k);
-__device__ __forceinline__ void control_step_lds(LMState& sst, const double* sums_lds, int lane, double* s_pt,
-                                                 int* s_done) {
-  LMState s;
-  load_state_core(s, sst);
-  control_step(s, sst, sums_lds, lane);
-  __builtin_amdgcn_wave_barrier();   // (every lane's reads of sst precede lane 0's write-back: one wave, in order)
-  if (lane == 0) store_state_core(sst, s);
-  if (lane < 7) s_pt[lane] = point_component(s, lane);
-  if (lane == 0) *s_done = s.done;
-}
-
-__device__ __forceinline__ double point_component(const LMState& s, int k) {   // k wave-uniform or per lane
-  double v = 0.0;
-#pragma unroll
-  for (int j = 0; j < 7; ++j)
-    if (j == k) v = s.phase == 0 ? s.x[j] : s.cand[j];
-  return v;
 }
 
 __device__ __forceinline__ void stage_state(const LMState* __restrict__ st, LMState& sst) {
@@ -978,11 +944,9 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
   __shared__ unsigned s_tab[kRecEvalBlocks * 2 * LM_NSUM];   // the all-gathered block partials (u32 halves)
   __shared__ double s_sums[LM_NSUM];
   __shared__ double s_ssum[LM_NSUM];
-  __shared__ double s_pt[7];
   __shared__ LMState sst;
   __shared__ double G[kGramW][kGramW];
   __shared__ double o[3];
-  __shared__ int s_done;
   const int nblk = (int)gridDim.x, blk = (int)blockIdx.x, tid = (int)threadIdx.x, lane = tid & 63;
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
   // the counts, the LM state, G and (GRAM) this thread's edge record — speculatively, for i0 < ne_ub, which is
@@ -1017,12 +981,8 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
   if (GRAM) gram_unpack(gv, G, o);
   const unsigned ep = sst.epoch;
   const unsigned xs0 = sst.xseq;   // peer sharding: this solve's first exchange
-#if FLOAM_LM_STATE_REGS
-  LMState s;   // wave 0: the whole LM state in registers for the whole solve
-  if (tid < 64) s = sst;
-#endif
-  if (tid < 7) s_pt[tid] = sst.x[tid];   // iteration zero evaluates at x (set by the kNN launch; kernel boundary)
-  if (tid == 0) s_done = 0;
+  // every evaluation is at sst.cand: iteration zero's at x (set by the kNN launch; kernel boundary)
+  if (tid < 7 && sst.phase == 0) sst.cand[tid] = sst.x[tid];
   unsigned* tab = s_tab;   // [nact][2 * LM_NSUM]
   const int ngr = nact * 2 * LM_NSUM;
   unsigned long long tm[4] = {0, 0, 0, 0};
@@ -1033,8 +993,8 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
   int failed_at = -1;   // evaluation whose granules never arrived (never expected)
   for (int it = 0; it < 5; ++it) {
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    __syncthreads();   // s_pt and s_done of this evaluation
-    if (s_done) break;
+    __syncthreads();   // the point and done flag of this evaluation
+    if (sst.done) break;
     unsigned long long t1 = t0, t2 = t0;
     unsigned tag = ep + (unsigned)it;
     {
@@ -1042,13 +1002,13 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
       if (tid < NR) {
         R x[7];
 #pragma unroll
-        for (int k = 0; k < 7; ++k) x[k] = (R)s_pt[k];
+        for (int k = 0; k < 7; ++k) x[k] = (R)sst.cand[k];
         eval_records<HUBER, R>(x, has0, edge0, f0, i0 + stride, stride, ne, total, a.erec, a.evalid, a.ecap, a.srec,
                                a.svalid, a.scap, acc);
       } else {
 #pragma unroll
         for (int k = 0; k < LM_NSUM; ++k) acc[k] = 0.0;
-        if (GRAM) surf_sums_wave(s_pt, o, G, (double)sst.corr_surf, s_ssum, lane);   // beside the edge records
+        if (GRAM) surf_sums_wave(sst.cand, o, G, (double)sst.corr_surf, s_ssum, lane);   // beside the edge records
       }
       const double v = block_sums<NR>(acc, s_buf);
       unsigned long long* slot = a.part + (size_t)(it & 1) * kRecEvalBlocks * 2 * LM_NSUM;
@@ -1086,15 +1046,7 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
       ++nx;
     }
     const unsigned long long t3 = __builtin_amdgcn_s_memrealtime();
-    if (tid < 64) {   // the next point (if the solve goes on)
-#if FLOAM_LM_STATE_REGS
-      control_step(s, sst, s_sums, lane);
-      if (tid < 7) s_pt[tid] = point_component(s, tid);
-      if (lane == 0) s_done = s.done;
-#else
-      control_step_lds(sst, s_sums, lane, s_pt, &s_done);
-#endif
-    }
+    if (tid < 64) control_step(sst, s_sums, lane);   // the next point (if the solve goes on)
     if (a.dbg && blk == 0) {
       const unsigned long long t4 = __builtin_amdgcn_s_memrealtime();
       tm[0] += t1 - t0; tm[1] += t2 - t1; tm[2] += t3 - t2; tm[3] += t4 - t3;
@@ -1104,17 +1056,7 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
   // by the status gather (the solve's pose is not taken, the handle is poisoned on the host)
   if (failed_at >= 0 && tid == 0) __hip_atomic_store(&a.st->xfail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (blk != 0) return;
-#if FLOAM_LM_STATE_REGS
-  if (failed_at >= 0 && tid < 64) {   // end the solve, report through n_res
-    s.done = 1;
-    s.n_res = -1;
-  }
-  if (tid == 0) {
-    store_state_core(sst, s);
-    sst.xseq = xs0 + nx;
-  }
-#else
-  __syncthreads();   // (wave 0's last write-back)
+  __syncthreads();   // (wave 0's last control step)
   if (tid == 0) {
     if (failed_at >= 0) {   // end the solve, report through n_res
       sst.done = 1;
@@ -1122,7 +1064,6 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
     }
     sst.xseq = xs0 + nx;
   }
-#endif
   __syncthreads();
   publish_state(sst, a.st);
   if (a.dbg && tid == 0) {   // diagnostic stamps (100 MHz): evaluate + publish, all-gather, reduce, control step,
@@ -1147,21 +1088,18 @@ __global__ __launch_bounds__(kTB) void lm_shard_eval(LMArgs a, int k) {
   __shared__ double s_buf[LM_NSUM * red_stride<NR>()];
   __shared__ double s_sums[LM_NSUM];
   __shared__ double s_ssum[LM_NSUM];
-  __shared__ double s_pt[7];
   __shared__ LMState sst;
-  __shared__ int s_done, s_last;
+  __shared__ int s_last;
   const int nblk = (int)gridDim.x, blk = (int)blockIdx.x, tid = (int)threadIdx.x, lane = tid & 63;
   stage_state(a.st, sst);
+  if (k > 0 && tid < LM_NSUM) s_sums[tid] = a.sums[tid];   // all-reduced (kernel boundary)
   __syncthreads();
-  LMState s;
   if (tid < 64) {
-    s = sst;
-    if (k > 0 && !s.done) control_step(s, sst, a.sums, lane);   // a.sums: all-reduced (kernel boundary)
-    if (tid < 7) s_pt[tid] = point_component(s, tid);
-    if (lane == 0) s_done = s.done;
+    if (k > 0 && !sst.done) control_step(sst, s_sums, lane);
+    else if (tid < 7 && sst.phase == 0) sst.cand[tid] = sst.x[tid];   // iteration zero evaluates at x
   }
   __syncthreads();
-  const bool done = s_done != 0;
+  const bool done = sst.done != 0;
   const int ne = min(*a.d_ne, a.ne_ub);
   const int total = ne + (GRAM ? 0 : min(*a.d_ns, a.ns_ub));
   const int nact = active_blocks<NR>(total, nblk);
@@ -1170,7 +1108,7 @@ __global__ __launch_bounds__(kTB) void lm_shard_eval(LMArgs a, int k) {
     if (tid < NR) {
       R x[7];
 #pragma unroll
-      for (int q = 0; q < 7; ++q) x[q] = (R)s_pt[q];
+      for (int q = 0; q < 7; ++q) x[q] = (R)sst.cand[q];
       const int stride = nact * NR, i0 = blk * NR + tid;
       R f0[9];
       bool has0, edge0;
@@ -1203,7 +1141,7 @@ __global__ __launch_bounds__(kTB) void lm_shard_eval(LMArgs a, int k) {
       __shared__ double G[kGramW][kGramW];
       __shared__ double o[3];
       gram_unpack(gram_load(a.gmat, tid), G, o);
-      if (tid < 64) surf_sums_wave(s_pt, o, G, (double)sst.corr_surf, s_ssum, lane);
+      if (tid < 64) surf_sums_wave(sst.cand, o, G, (double)sst.corr_surf, s_ssum, lane);
       __syncthreads();
       if (tid < LM_NSUM) s_sums[tid] = s_sums[tid] + s_ssum[tid];
       __syncthreads();
@@ -1212,10 +1150,7 @@ __global__ __launch_bounds__(kTB) void lm_shard_eval(LMArgs a, int k) {
   } else if (tid < LM_NSUM) {
     a.sums[tid] = 0.0;   // nothing evaluated: the all-reduce still runs on every rank (the same decision everywhere)
   }
-  if (tid == 0) {
-    store_state_core(sst, s);
-    *a.ticket = 0u;   // every block has arrived (next launch: kernel boundary)
-  }
+  if (tid == 0) *a.ticket = 0u;   // every block has arrived (next launch: kernel boundary)
   __syncthreads();
   publish_state(sst, a.st);
 }
@@ -1223,12 +1158,11 @@ __global__ __launch_bounds__(kTB) void lm_shard_eval(LMArgs a, int k) {
 // the control step after the last evaluation of a sharded solve
 __global__ __launch_bounds__(64) void lm_shard_final(LMState* __restrict__ st, const double* __restrict__ sums) {
   __shared__ LMState sst;
+  __shared__ double s_sums[LM_NSUM];
   stage_state(st, sst);
+  if (threadIdx.x < LM_NSUM) s_sums[threadIdx.x] = sums[threadIdx.x];
   __syncthreads();
-  LMState s = sst;
-  if (!s.done) control_step(s, sst, sums, threadIdx.x);
-  __syncthreads();
-  if (threadIdx.x == 0) store_state_core(sst, s);
+  if (!sst.done) control_step(sst, s_sums, threadIdx.x);
   __syncthreads();
   publish_state(sst, st);
 }

@@ -114,8 +114,9 @@ struct LMState {
   double x_cost;
   double H[21];       // J^T J at x (unscaled, upper triangle row-major)
   double g[6];        // J^T r at x
-  double scale[6];    // Jacobi scaling, fixed at iteration 0
-  double diag[6];     // LM diagonal (reused after a rejected / invalid step)
+  double dlo[6], dhi[6];   // bounds of the unscaled LM diagonal: 1e-6, 1e32 over the squared Jacobi scaling, fixed
+                           // at iteration 0 (lm.hip lm_step)
+  double diag[6];     // unscaled LM diagonal (reused after a rejected / invalid step)
   double radius, dfac, mcc, x_norm, gmax, initial_cost;
   // the solve's iteration-zero quantities (stage inspection; oracle/odom.cpp SolveTrace): the starting point and the
   // unscaled J^T J and J^T r there
