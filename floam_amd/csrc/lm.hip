@@ -106,9 +106,10 @@ __device__ __forceinline__ double block_sums(const double (&acc)[LM_NSUM], doubl
 }
 
 // block partials P(c, b) (c < 29, b < nblk) -> 29 sums in out (LDS), fixed order: component c sums 8 strips of
-// consecutive blocks in block order, then the strip totals by strip8_total
+// consecutive blocks in block order, then the strip totals by strip8_total; + add[c] when add is given (the surf half)
 template <typename Load>
-__device__ __forceinline__ void reduce_blocks(Load P, int nblk, double* out /* LDS [LM_NSUM] */) {
+__device__ __forceinline__ void reduce_blocks(Load P, int nblk, double* out /* LDS [LM_NSUM] */,
+                                              const double* add = nullptr /* LDS [LM_NSUM] */) {
   const int t = threadIdx.x;
   double v = 0.0;
   if (t < LM_NSUM * 8) {
@@ -118,7 +119,7 @@ __device__ __forceinline__ void reduce_blocks(Load P, int nblk, double* out /* L
     for (int b = b0; b < b1; ++b) v += P(c, b);
   }
   v = strip8_total(v);
-  if (t < LM_NSUM * 8 && (t & 7) == 0) out[t >> 3] = v;
+  if (t < LM_NSUM * 8 && (t & 7) == 0) out[t >> 3] = add ? v + add[t >> 3] : v;
   __syncthreads();
 }
 
@@ -1032,10 +1033,8 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
       reduce_blocks([&](int c, int b) {
         const int g = b * 2 * LM_NSUM + 2 * c;
         return __longlong_as_double((long long)(((unsigned long long)tab[g + 1] << 32) | tab[g]));
-      }, nact, s_sums);
-      if (GRAM && tid < LM_NSUM) s_sums[tid] = s_sums[tid] + s_ssum[tid];   // edge + surf
+      }, nact, s_sums, GRAM ? s_ssum : nullptr);   // edge + surf
     }
-    __syncthreads();
     // (one call site each for the exchange and the control step: a second inlined copy of the control step doubled
     // the kernel's code, 16k instructions against 8k, past what the instruction cache holds)
     if (peers) {
