@@ -582,8 +582,8 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
   o->lm.reserve(1);
   o->lmb.reserve(st);
   if (!o->dbg_stamps.p && FLOAM_DIAG_ENV("FLOAM_DEBUG_STAMPS")) {
-    o->dbg_stamps.reserve(8);
-    FLOAM_HIP(hipMemsetAsync(o->dbg_stamps.p, 0, sizeof(unsigned long long) * 8, st));
+    o->dbg_stamps.reserve(10);
+    FLOAM_HIP(hipMemsetAsync(o->dbg_stamps.p, 0, sizeof(unsigned long long) * 10, st));
   }
   o->prof_bytes.reserve(2);
   if (!o->prof_bytes_init) {
@@ -1488,13 +1488,14 @@ floam_status floam_odom_destroy(floam_odom* o) {
       geom_stamps_print();
       lm_ctrl_stamps_print();
       if (o->dbg_stamps.p) {   // FLOAM_DEBUG_STAMPS: the resident solve's segments in block 0 (100 MHz ticks)
-        unsigned long long h[8];
+        unsigned long long h[10];
         FLOAM_HIP(hipMemcpy(h, o->dbg_stamps.p, sizeof(h), hipMemcpyDeviceToHost));
         const double n = h[4] ? (double)h[4] : 1.0;
         std::fprintf(stderr, "[floam stamps] %llu solves (block 0, per solve): evaluate + publish %.2f us, all-gather "
                      "%.2f us, reduce %.2f us, control step %.2f us; prologue %.2f us, block 0 first instruction to "
-                     "state written %.2f us\n", h[4], h[0] / n / 100.0, h[1] / n / 100.0, h[2] / n / 100.0,
-                     h[3] / n / 100.0, h[5] / n / 100.0, h[6] / n / 100.0);
+                     "state written %.2f us; inside the evaluations: wave 0's records %.2f us, wave 3's %.2f us\n",
+                     h[4], h[0] / n / 100.0, h[1] / n / 100.0, h[2] / n / 100.0, h[3] / n / 100.0, h[5] / n / 100.0,
+                     h[6] / n / 100.0, h[7] / n / 100.0, h[8] / n / 100.0);
       }
       if (o->copy) {
         (void)hipStreamSynchronize(o->copy);

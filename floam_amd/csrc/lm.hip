@@ -242,10 +242,21 @@ constexpr SurfOut make_surf_out() {
 }
 __constant__ SurfOut c_surf_out = make_surf_out();
 
+// lane t's output of surf_sums_wave (kind, a, b of c_surf_out), read from constant memory once per launch: inside
+// the evaluation loop the three byte loads were a memory round trip on the surf half's path every evaluation
+struct SurfRole {
+  int kind, ra, rb;
+};
+__device__ __forceinline__ SurfRole surf_role(int t) {
+  SurfRole r{3, 0, 0};
+  if (t < LM_NSUM) r = SurfRole{c_surf_out.kind[t], c_surf_out.a[t], c_surf_out.b[t]};
+  return r;
+}
+
 // Two LDS phases: every lane forms M and the translations itself (the wave-uniform values lane 0 used to publish;
 // the V rows are compile-time selections of them), lanes 0..12 form row i of Y from row i of G; then lane t < 29
 // forms output t.  Bit-identical to the four-phase form (same products, same summation orders).
-__device__ void surf_sums_wave(const double* x /* LDS [7] */, const double* o /* LDS [3] */,
+__device__ void surf_sums_wave(const SurfRole& role, const double* x /* LDS [7] */, const double* o /* LDS [3] */,
                                const double (*G)[kGramW] /* LDS */, double n_surf, double* out /* LDS [29] */,
                                int t /* lane */) {
   __shared__ double Yl[4][kGramW];   // G K_0, G K_1, G K_2, G c
@@ -289,7 +300,7 @@ __device__ void surf_sums_wave(const double* x /* LDS [7] */, const double* o /*
   }
   wave_lds_order();
   if (t < LM_NSUM) {
-    const int kind = c_surf_out.kind[t], ra = c_surf_out.a[t], rb = c_surf_out.b[t];
+    const int kind = role.kind, ra = role.ra, rb = role.rb;
     double r;
     if (kind == 0) {   // the four candidate dots in independent chains, then the lane's own
       double d0 = 0.0, d1 = 0.0, d2 = 0.0, d3 = 0.0;
@@ -519,6 +530,15 @@ __device__ unsigned long long g_ctrl_stamps[8];
   } while (0)
 #endif
 
+// the resident solve's segment stamps (FLOAM_DEBUG_STAMPS): read only by the diagnostic build — in the product
+// library the clock reads are gone from the evaluation loop altogether (each one is a scalar-memory message whose
+// return the next LDS wait also waits for)
+#ifdef FLOAM_DIAG
+#define LM_NOW() __builtin_amdgcn_s_memrealtime()
+#else
+#define LM_NOW() 0ull
+#endif
+
 // value of lane src (a compile-time / wave-uniform lane) to every lane: two v_readlane (no LDS round trip)
 __device__ __forceinline__ double bcast(double v, int src) {
   const unsigned long long b = (unsigned long long)__double_as_longlong(v);
@@ -559,6 +579,13 @@ __device__ __forceinline__ double norm7(const double (&a)[7]) {
   return sqrt(v);
 }
 
+// the values are taken as written here (an empty asm that "changes" them): their loads cannot sink below this point
+template <int N>
+__device__ __forceinline__ void pin(double (&v)[N]) {
+#pragma unroll
+  for (int k = 0; k < N; ++k) asm volatile("" : "+v"(v[k]));
+}
+
 // One Ceres control step after an evaluation (sums: cost, J^T J, J^T r, count at x in phase 0, else at cand), run by
 // the 64 lanes of one wave on the LM state in LDS.  Every lane reads the same words (LDS broadcast) and computes the
 // same values — but lane 1, which forms the gradient projection of the gradient-norm test beside lane 0's candidate —
@@ -570,16 +597,31 @@ __device__ __forceinline__ double norm7(const double (&a)[7]) {
 // with HandleInvalidStep's retries, the gradient-norm test folded in.
 __device__ __forceinline__ void control_step(LMState& S, const double* __restrict__ sums, int lane) {
   CTRL_T(t0);
-  double x[7], c[7];
+  // every word the decisions read, loaded together and pinned where they are loaded: one LDS round trip (the compiler
+  // otherwise sinks each load into the branch that uses it, a round trip per branch)
+  double x[7], c[7], sm[28], lo[6], hi[6];   // sm: cost, H[21], g[6]; lo, hi: the diagonal's clamp bounds
 #pragma unroll
   for (int k = 0; k < 7; ++k) {
     x[k] = S.x[k];
     c[k] = S.cand[k];
   }
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    lo[k] = S.dlo[k];
+    hi[k] = S.dhi[k];
+  }
+#pragma unroll
+  for (int k = 0; k < 28; ++k) sm[k] = sums[k];
   double x_cost = S.x_cost, radius = S.radius, dfac = S.dfac, mcc = S.mcc, x_norm = S.x_norm, gmax = S.gmax;
+  const double cand_norm = S.cand_norm;
   int iteration = S.iteration, reuse = S.reuse, invalid = S.invalid, successful = S.successful;
   int phase = S.phase;
-  const double cost = sums[0];
+  pin(x);
+  pin(c);
+  pin(sm);
+  pin(lo);
+  pin(hi);
+  const double cost = sm[0];
   int done = 0;
   bool fresh = false;        // H, g (and E) from this evaluation's sums
   bool check_gmax = false;   // the gradient-norm test is due: at iteration zero and after a successful step
@@ -601,6 +643,12 @@ __device__ __forceinline__ void control_step(LMState& S, const double* __restric
         S.dlo[lane] = 1e-6 * (r * r);
         S.dhi[lane] = 1e32 * (r * r);
       }
+      wave_lds_order();
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        lo[k] = S.dlo[k];
+        hi[k] = S.dhi[k];
+      }
       x_norm = norm7(x);
       radius = 1e4;
       dfac = 2.0;
@@ -612,39 +660,28 @@ __device__ __forceinline__ void control_step(LMState& S, const double* __restric
       check_gmax = true;
     }
   } else {
+    // (ParameterToleranceReached was decided when the candidate was formed: it does not depend on the evaluation)
     const double cand_cost = isfinite(cost) ? cost : DBL_MAX;
-    // ParameterToleranceReached (candidate not applied): |x - cand| <= 1e-8 (|x| + 1e-8), compared squared (both
-    // sides are non-negative: no square root on the step's dependent chain)
-    double sn2 = 0.0;
-#pragma unroll
-    for (int i = 0; i < 7; ++i) sn2 += (x[i] - c[i]) * (x[i] - c[i]);
-    const double ptol = 1e-8 * (x_norm + 1e-8);
-    if (sn2 <= ptol * ptol) {
-      done = 1;
-    } else if (fabs(x_cost - cand_cost) <= 1e-6 * x_cost) {   // FunctionToleranceReached
+    if (fabs(x_cost - cand_cost) <= 1e-6 * x_cost) {   // FunctionToleranceReached
       done = 1;
     } else {
       // rho = decrease / mcc > 1e-3 decided without the reciprocal (mcc > 0); rho itself only for the radius update
       const double dec = x_cost - cand_cost;
-      if (dec > 1e-3 * mcc) {   // success
-        const double rho = dec * recip(mcc);   // (within an ulp of the division)
+      moved = dec > 1e-3 * mcc;   // success
+      const double rho = dec * recip(mcc);   // (within an ulp of the division)
+      const double t = 2.0 * rho - 1.0;
+      const double up = fmin(1e16, radius * recip(fmax(1.0 / 3.0, 1.0 - t * t * t)));
+      const double down = radius * recip(dfac);   // (dfac a power of two: exact)
 #pragma unroll
-        for (int i = 0; i < 7; ++i) x[i] = c[i];
-        x_norm = norm7(x);
-        x_cost = cand_cost;
-        const double t = 2.0 * rho - 1.0;
-        radius = fmin(1e16, radius * recip(fmax(1.0 / 3.0, 1.0 - t * t * t)));
-        dfac = 2.0;
-        reuse = 0;
-        successful++;
-        fresh = true;
-        check_gmax = true;
-        moved = true;
-      } else {
-        radius *= recip(dfac);   // (dfac a power of two: exact)
-        dfac *= 2.0;
-        reuse = 1;
-      }
+      for (int i = 0; i < 7; ++i) x[i] = moved ? c[i] : x[i];
+      x_norm = moved ? cand_norm : x_norm;   // (norm7 of the candidate, formed with it)
+      x_cost = moved ? cand_cost : x_cost;
+      radius = moved ? up : down;
+      dfac = moved ? 2.0 : 2.0 * dfac;
+      reuse = moved ? 0 : 1;
+      successful += moved ? 1 : 0;
+      fresh = moved;
+      check_gmax = moved;
       if (iteration >= 4 || radius < 1e-32) done = 1;
     }
   }
@@ -652,18 +689,24 @@ __device__ __forceinline__ void control_step(LMState& S, const double* __restric
   CTRL_T(t1);
   CTRL_ADD(1, t1 - t0);
   bool have_cand = false;
-  double out[7];
+  double out[7], cand_norm_new = 0.0;
   if (!done) {
-    const double* Hp = fresh ? sums + 1 : state_words(S, offsetof(LMState, H));   // H, then g
     double H[21], g[6], E[6];
+    if (fresh) {
 #pragma unroll
-    for (int k = 0; k < 21; ++k) H[k] = Hp[k];
+      for (int k = 0; k < 21; ++k) H[k] = sm[1 + k];
 #pragma unroll
-    for (int k = 0; k < 6; ++k) g[k] = Hp[21 + k];
+      for (int k = 0; k < 6; ++k) g[k] = sm[22 + k];
+    } else {   // (a rejected step: J^T J and J^T r of x, kept in the state)
+      const double* Hp = state_words(S, offsetof(LMState, H));   // H, then g
+#pragma unroll
+      for (int k = 0; k < 21; ++k) H[k] = Hp[k];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) g[k] = Hp[21 + k];
+    }
     if (!reuse) {
-      wave_lds_order();   // (iteration zero: the bounds written above by lanes 0..5)
 #pragma unroll
-      for (int k = 0; k < 6; ++k) E[k] = fmin(fmax(H[hidx(k, k)], S.dlo[k]), S.dhi[k]);
+      for (int k = 0; k < 6; ++k) E[k] = fmin(fmax(H[hidx(k, k)], lo[k]), hi[k]);
     } else {
 #pragma unroll
       for (int k = 0; k < 6; ++k) E[k] = S.diag[k];
@@ -707,6 +750,17 @@ __device__ __forceinline__ void control_step(LMState& S, const double* __restric
         mcc = m;
         invalid = 0;
         have_cand = true;
+        // ParameterToleranceReached (the candidate not applied): |x - cand| <= 1e-8 (|x| + 1e-8), compared squared
+        // (both sides non-negative).  Ceres tests it after evaluating the candidate, but nothing of the evaluation
+        // enters the test and the solve ends with x unchanged either way, so the evaluation is skipped.  Lane 0 holds
+        // the candidate (lane 1 may hold the projection): its distance and norm are read from it.
+        double sn2 = 0.0;
+#pragma unroll
+        for (int i = 0; i < 7; ++i) sn2 += (x[i] - out[i]) * (x[i] - out[i]);
+        sn2 = bcast(sn2, 0);
+        cand_norm_new = bcast(norm7(out), 0);
+        const double ptol = 1e-8 * (x_norm + 1e-8);
+        if (sn2 <= ptol * ptol) done = 1;
         CTRL_T(td);
         CTRL_ADD(4, td - tc);
         break;   // candidate pending evaluation
@@ -736,6 +790,7 @@ __device__ __forceinline__ void control_step(LMState& S, const double* __restric
     if (have_cand) {
 #pragma unroll
       for (int k = 0; k < 7; ++k) S.cand[k] = out[k];
+      S.cand_norm = cand_norm_new;
     }
     S.x_cost = x_cost; S.radius = radius; S.dfac = dfac; S.mcc = mcc; S.x_norm = x_norm; S.gmax = gmax;
     S.iteration = iteration; S.reuse = reuse; S.invalid = invalid; S.successful = successful;
@@ -949,7 +1004,7 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
   __shared__ double G[kGramW][kGramW];
   __shared__ double o[3];
   const int nblk = (int)gridDim.x, blk = (int)blockIdx.x, tid = (int)threadIdx.x, lane = tid & 63;
-  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long t_start = LM_NOW();
   // the counts, the LM state, G and (GRAM) this thread's edge record — speculatively, for i0 < ne_ub, which is
   // inside the record arrays — all issued before any is waited on: one memory round trip before the first evaluation
   static_assert(kStateWords <= kTB, "one state word per thread");
@@ -958,6 +1013,7 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
   const int ns_dev = GRAM ? 0 : *a.d_ns;
   const unsigned sw = tid < kStateWords ? reinterpret_cast<const unsigned*>(a.st)[tid] : 0u;
   const double gv = GRAM ? gram_load(a.gmat, tid) : 0.0;
+  const SurfRole srole = GRAM && tid >= NR ? surf_role(lane) : SurfRole{3, 0, 0};   // (wave 3: the surf half)
   R f0[9];
   bool has0 = false, edge0 = true;
   uint8_t v0 = 0;
@@ -990,12 +1046,13 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
   __shared__ unsigned s_xch[kMaxShardRanks * 2 * LM_NSUM];   // peer sharding: every rank's sums (u32 halves)
   const bool peers = a.world > 1;
   unsigned nx = 0;   // evaluations exchanged with the other ranks in this solve
-  const unsigned long long t_loop = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long t_loop = LM_NOW();
   int failed_at = -1;   // evaluation whose granules never arrived (never expected)
   for (int it = 0; it < 5; ++it) {
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long t0 = LM_NOW();
     __syncthreads();   // the point and done flag of this evaluation
     if (sst.done) break;
+    const unsigned long long tw = LM_NOW();   // (this wave's start of the evaluation)
     unsigned long long t1 = t0, t2 = t0;
     unsigned tag = ep + (unsigned)it;
     {
@@ -1009,8 +1066,12 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
       } else {
 #pragma unroll
         for (int k = 0; k < LM_NSUM; ++k) acc[k] = 0.0;
-        if (GRAM) surf_sums_wave(sst.cand, o, G, (double)sst.corr_surf, s_ssum, lane);   // beside the edge records
+        if (GRAM) surf_sums_wave(srole, sst.cand, o, G, (double)sst.corr_surf, s_ssum, lane);   // beside the edges
       }
+#ifdef FLOAM_DIAG
+      // block 0's wave 0 (edge records) and wave 3 (GRAM: the surf half) from the evaluation's start to their sums
+      if (a.dbg && blk == 0 && (tid == 0 || tid == 3 * 64)) atomicAdd(&a.dbg[tid ? 8 : 7], LM_NOW() - tw);
+#endif
       const double v = block_sums<NR>(acc, s_buf);
       unsigned long long* slot = a.part + (size_t)(it & 1) * kRecEvalBlocks * 2 * LM_NSUM;
       if (tid < LM_NSUM * kStrips && (tid & 7) < 2) {   // 58 granules: component c in 32-bit halves (lanes 8c, 8c + 1)
@@ -1018,7 +1079,7 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
         const unsigned long long b = (unsigned long long)__double_as_longlong(v);
         put_granule(&slot[blk * 2 * LM_NSUM + 2 * c + h], granule(tag, h ? (unsigned)(b >> 32) : (unsigned)b));
       }
-      t1 = __builtin_amdgcn_s_memrealtime();
+      t1 = LM_NOW();
       // every active block's granules of this evaluation (this block's own included): kSweep loads in flight per
       // thread and poll round
       int bad = 0;
@@ -1029,7 +1090,7 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
         failed_at = it;
         break;
       }
-      t2 = __builtin_amdgcn_s_memrealtime();
+      t2 = LM_NOW();
       reduce_blocks([&](int c, int b) {
         const int g = b * 2 * LM_NSUM + 2 * c;
         return __longlong_as_double((long long)(((unsigned long long)tab[g + 1] << 32) | tab[g]));
@@ -1044,10 +1105,10 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
       }
       ++nx;
     }
-    const unsigned long long t3 = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long t3 = LM_NOW();
     if (tid < 64) control_step(sst, s_sums, lane);   // the next point (if the solve goes on)
     if (a.dbg && blk == 0) {
-      const unsigned long long t4 = __builtin_amdgcn_s_memrealtime();
+      const unsigned long long t4 = LM_NOW();
       tm[0] += t1 - t0; tm[1] += t2 - t1; tm[2] += t3 - t2; tm[3] += t4 - t3;
     }
   }
@@ -1072,7 +1133,7 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
     atomicAdd(&a.dbg[3], tm[3]);
     atomicAdd(&a.dbg[4], 1ull);
     atomicAdd(&a.dbg[5], t_loop - t_start);
-    atomicAdd(&a.dbg[6], __builtin_amdgcn_s_memrealtime() - t_start);
+    atomicAdd(&a.dbg[6], LM_NOW() - t_start);
   }
 }
 
@@ -1140,7 +1201,7 @@ __global__ __launch_bounds__(kTB) void lm_shard_eval(LMArgs a, int k) {
       __shared__ double G[kGramW][kGramW];
       __shared__ double o[3];
       gram_unpack(gram_load(a.gmat, tid), G, o);
-      if (tid < 64) surf_sums_wave(sst.cand, o, G, (double)sst.corr_surf, s_ssum, lane);
+      if (tid < 64) surf_sums_wave(surf_role(lane), sst.cand, o, G, (double)sst.corr_surf, s_ssum, lane);
       __syncthreads();
       if (tid < LM_NSUM) s_sums[tid] = s_sums[tid] + s_ssum[tid];
       __syncthreads();

@@ -118,6 +118,7 @@ struct LMState {
                            // at iteration 0 (lm.hip lm_step)
   double diag[6];     // unscaled LM diagonal (reused after a rejected / invalid step)
   double radius, dfac, mcc, x_norm, gmax, initial_cost;
+  double cand_norm;   // |cand|, formed with the candidate (x_norm once it is accepted)
   // the solve's iteration-zero quantities (stage inspection; oracle/odom.cpp SolveTrace): the starting point and the
   // unscaled J^T J and J^T r there
   double x_in[7];
