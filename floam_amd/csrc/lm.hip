@@ -821,29 +821,56 @@ __device__ __forceinline__ unsigned long long granule(unsigned tag, unsigned dat
 __device__ __forceinline__ void put_granule(unsigned long long* p, unsigned long long g) {
   __hip_atomic_store(p, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// granules j0, j0 + kTB, ..., j0 + (kSweep - 1) kTB (those < n) until all carry `tag` (bounded), data into out[j]
-constexpr int kSweep = 8;
-__device__ __forceinline__ bool sweep_granules(const unsigned long long* __restrict__ g, int j0, int n, unsigned tag,
-                                               unsigned* __restrict__ out) {
-  unsigned pending = 0;
+// The all-gather and the block reduction in one pass, straight from the granules: thread t < 232 (component
+// c = t >> 3, strip p = t & 7) polls the two halves of component c from the blocks of its strip (consecutive blocks,
+// in block order: reduce_blocks' partition) and adds them in block order; the 8 strips by strip8_total — the bits of
+// reduce_blocks over the gathered table, without the table (no LDS write and read, no barrier between them).
+// Every poll loop is bounded (kSpin); bad = a granule never arrived.  Called by every thread; returns, to the threads with
+// (t & 7) == 0 and t < 232, the sum of component t >> 3.
+constexpr int kGatherChunk = 4;   // blocks polled together by a thread (8 granule loads in flight)
+__device__ __forceinline__ double gather_blocks(const unsigned long long* __restrict__ slot, int nact, unsigned tag,
+                                                bool& bad) {
+  const int t = threadIdx.x;
+  const int c = t >> 3, p = t & 7;
+  const int per = (nact + 7) / 8;
+  const int b0 = min(nact, p * per), nb = t < LM_NSUM * 8 ? min(nact, b0 + per) - b0 : 0;
+  double v = 0.0;
+  bad = false;
+  for (int k0 = 0; k0 < nb; k0 += kGatherChunk) {   // chunks in block order
+    const unsigned long long* g = slot + (size_t)(b0 + k0) * 2 * LM_NSUM + 2 * c;
+    const int nk = min(kGatherChunk, nb - k0);
+    unsigned lo[kGatherChunk], hi[kGatherChunk];
+    unsigned pend = 0;   // bit 2k: block k's low half, 2k + 1 its high half
 #pragma unroll
-  for (int u = 0; u < kSweep; ++u)
-    if (j0 + u * kTB < n) pending |= 1u << u;
-  for (long long k = 0; k < kSpin && pending; ++k) {
-    unsigned long long v[kSweep];
+    for (int k = 0; k < kGatherChunk; ++k) {
+      lo[k] = 0u;
+      hi[k] = 0u;
+      if (k < nk) pend |= 3u << (2 * k);
+    }
+    for (long long it = 0; it < kSpin && pend; ++it) {
+      unsigned long long w[2 * kGatherChunk];
 #pragma unroll
-    for (int u = 0; u < kSweep; ++u)   // all loads of the round issued before any is examined
-      v[u] = (pending >> u) & 1u ? __hip_atomic_load(&g[j0 + u * kTB], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                 : 0ull;
+      for (int q = 0; q < 2 * kGatherChunk; ++q)   // all loads of the round issued before any is examined
+        w[q] = (pend >> q) & 1u ? __hip_atomic_load(&g[(q >> 1) * 2 * LM_NSUM + (q & 1)], __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT)
+                                : 0ull;
 #pragma unroll
-    for (int u = 0; u < kSweep; ++u)
-      if (((pending >> u) & 1u) && (unsigned)(v[u] >> 32) == tag) {
-        out[j0 + u * kTB] = (unsigned)v[u];
-        pending &= ~(1u << u);
-      }
-    if (pending) __builtin_amdgcn_s_sleep(1);
+      for (int q = 0; q < 2 * kGatherChunk; ++q)
+        if (((pend >> q) & 1u) && (unsigned)(w[q] >> 32) == tag) {
+          if (q & 1) hi[q >> 1] = (unsigned)w[q]; else lo[q >> 1] = (unsigned)w[q];
+          pend &= ~(1u << q);
+        }
+      if (pend) __builtin_amdgcn_s_sleep(1);
+    }
+    if (pend) {
+      bad = true;
+      break;
+    }
+#pragma unroll
+    for (int k = 0; k < kGatherChunk; ++k)
+      if (k < nk) v += __longlong_as_double((long long)(((unsigned long long)hi[k] << 32) | lo[k]));
   }
-  return pending == 0;
+  return strip8_total(v);
 }
 
 // evaluation blocks that hold records: one record slot per record thread while they fit, at most nblk (a function of
@@ -997,7 +1024,6 @@ template <bool GRAM, bool HUBER, typename R>
 __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
   constexpr int NR = rec_threads<GRAM>();
   __shared__ double s_buf[LM_NSUM * red_stride<NR>()];   // thread sums
-  __shared__ unsigned s_tab[kRecEvalBlocks * 2 * LM_NSUM];   // the all-gathered block partials (u32 halves)
   __shared__ double s_sums[LM_NSUM];
   __shared__ double s_ssum[LM_NSUM];
   __shared__ LMState sst;
@@ -1040,8 +1066,6 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
   const unsigned xs0 = sst.xseq;   // peer sharding: this solve's first exchange
   // every evaluation is at sst.cand: iteration zero's at x (set by the kNN launch; kernel boundary)
   if (tid < 7 && sst.phase == 0) sst.cand[tid] = sst.x[tid];
-  unsigned* tab = s_tab;   // [nact][2 * LM_NSUM]
-  const int ngr = nact * 2 * LM_NSUM;
   unsigned long long tm[4] = {0, 0, 0, 0};
   __shared__ unsigned s_xch[kMaxShardRanks * 2 * LM_NSUM];   // peer sharding: every rank's sums (u32 halves)
   const bool peers = a.world > 1;
@@ -1080,21 +1104,17 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
         put_granule(&slot[blk * 2 * LM_NSUM + 2 * c + h], granule(tag, h ? (unsigned)(b >> 32) : (unsigned)b));
       }
       t1 = LM_NOW();
-      // every active block's granules of this evaluation (this block's own included): kSweep loads in flight per
-      // thread and poll round
-      int bad = 0;
-      for (int j0 = tid; j0 < ngr; j0 += kSweep * kTB)
-        if (!sweep_granules(slot, j0, ngr, tag, tab)) bad = 1;
-      if (a.fail_test) bad = 1;
-      if (__syncthreads_or(bad)) {
+      // every active block's granules of this evaluation (this block's own included), summed in block order as they
+      // are gathered
+      bool bad = false;
+      const double vs = gather_blocks(slot, nact, tag, bad);
+      if (__syncthreads_or(bad || a.fail_test)) {
         failed_at = it;
         break;
       }
       t2 = LM_NOW();
-      reduce_blocks([&](int c, int b) {
-        const int g = b * 2 * LM_NSUM + 2 * c;
-        return __longlong_as_double((long long)(((unsigned long long)tab[g + 1] << 32) | tab[g]));
-      }, nact, s_sums, GRAM ? s_ssum : nullptr);   // edge + surf
+      if (tid < LM_NSUM * 8 && (tid & 7) == 0) s_sums[tid >> 3] = GRAM ? vs + s_ssum[tid >> 3] : vs;   // edge + surf
+      __syncthreads();
     }
     // (one call site each for the exchange and the control step: a second inlined copy of the control step doubled
     // the kernel's code, 16k instructions against 8k, past what the instruction cache holds)
