@@ -1,18 +1,18 @@
 // The Levenberg-Marquardt solve of updatePointsToMap on gfx950: ceres::Solve with LEVENBERG_MARQUARDT, DENSE_QR and
 // max_num_iterations = 4 (src/odomEstimationClass.cpp:95-108) over the residual blocks of src/lidarOptimization.cpp
 // (EdgeAnalyticCostFunction :12-43, SurfNormAnalyticCostFunction :51-74, PoseSE3Parameterization :77-140).  The
-// Ceres 1.13 TrustRegionMinimizer + LevenbergMarquardtStrategy control is restated in lm_logic (SURVEY.md §8 a-12;
-// oracle/odom.cpp ceres_solve is the CPU restatement).
+// Ceres 1.13 TrustRegionMinimizer + LevenbergMarquardtStrategy control is restated in control_step / lm_step
+// (oracle/odom.cpp ceres_solve is the CPU restatement).
 //
 // Single GPU — lm_solve, ONE launch per solve, no control block.  Every active block (256 threads) keeps its records
 // in registers across the up to five evaluations, evaluates them at the current point, publishes its 29 partial sums
 // as data-tagged 8-byte granules (MI355X_MICROARCH.md "handoff-1to1": one sc1 store per granule, {tag, 32 data
 // bits}; the consumer polls until every granule carries the tag it expects; no flags, counters or drains), then
-// gathers every active block's granules, reduces them in a fixed order and runs the Ceres control step on its wave 0
-// with the LM state in registers.  All blocks compute the same bits, so the next point is known everywhere without a
-// control -> evaluation hop: one hand-off per evaluation.  Tags are epoch + evaluation index, with the epoch advanced
-// by 8 at every solve (lm_reset), so a granule of an earlier evaluation or solve never matches and nothing is ever
-// cleared.  Every poll is bounded (~0.3 s); a timeout ends the solve with n_res = -1 (FLOAM_ERR_DEVICE on the host).
+// gathers every active block's granules, summing them in a fixed order as they arrive (gather_blocks), and runs the
+// Ceres control step on its wave 0 over the LM state in LDS.  All blocks compute the same bits, so the next point is
+// known everywhere without a control -> evaluation hop: one hand-off per evaluation.  Tags are epoch + evaluation
+// index, with the epoch advanced by 8 at every solve (lm_reset), so a granule of an earlier evaluation or solve never
+// matches and nothing is ever cleared.  Every poll is bounded (~0.3 s); a timeout ends the solve with n_res = -1 (FLOAM_ERR_DEVICE on the host).
 //
 // Modes (LM_*): GRAM — squared loss (the launch default, Q3): the surf half of every evaluation comes from the Gram
 // matrix of the surf records (exact in real arithmetic, see surf_sums_wave), formed by wave 3 of every block beside
