@@ -12,7 +12,8 @@
 // Ceres control step on its wave 0 over the LM state in LDS.  All blocks compute the same bits, so the next point is
 // known everywhere without a control -> evaluation hop: one hand-off per evaluation.  Tags are epoch + evaluation
 // index, with the epoch advanced by 8 at every solve (lm_reset), so a granule of an earlier evaluation or solve never
-// matches and nothing is ever cleared.  Every poll is bounded (~0.3 s); a timeout ends the solve with n_res = -1 (FLOAM_ERR_DEVICE on the host).
+// matches and nothing is ever cleared.  Every poll is bounded (~0.3 s); a timeout ends the solve with n_res = -1
+// (FLOAM_ERR_DEVICE on the host).
 //
 // Modes (LM_*): GRAM — squared loss (the launch default, Q3): the surf half of every evaluation comes from the Gram
 // matrix of the surf records (exact in real arithmetic, see surf_sums_wave), formed by wave 3 of every block beside
