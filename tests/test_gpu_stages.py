@@ -214,6 +214,49 @@ def test_knn_ties(floam_gpu, oracle_lib):
     print(f"lattice: {gated.size} queries with an 8-way tie, FLANN kept a different 5 of 8 on {differs}")
 
 
+def test_knn_direct_table_wraparound(floam_gpu, oracle_lib):
+    """The coarse table is direct-indexed (grid.hpp coarse_slot: super-cell coordinates wrapped to 128 x 128 x 32 at
+    the minimum table size), so coarse cells 256 m apart in x or y, or 64 m apart in z, share a home slot and are told
+    apart only by their keys (linear probing).  Five clusters placed exactly a window apart: every query's 5-NN, its
+    float squared distances and indices, equal the oracle's (tie-free random points)."""
+    from floam_amd.odom_estimation import reset_process_state
+    reset_process_state()
+    rng = np.random.default_rng(11)
+    centres = [(10.0, 0.0, 0.0), (266.0, 0.0, 0.0), (10.0, 256.0, 0.0), (10.0, 0.0, 64.0), (266.0, 256.0, 64.0)]
+    clusters, queries = [], []
+    for cx, cy, cz in centres:
+        p = np.zeros(600, synth.POINT_DTYPE)
+        p["x"] = cx + rng.uniform(-1.5, 1.5, p.size)
+        p["y"] = cy + rng.uniform(-1.5, 1.5, p.size)
+        p["z"] = cz + rng.uniform(-1.5, 1.5, p.size)
+        p["pad0"] = 1.0
+        clusters.append(p)
+        q = np.zeros(120, synth.POINT_DTYPE)
+        q["x"] = cx + rng.uniform(-1.2, 1.2, q.size)
+        q["y"] = cy + rng.uniform(-1.2, 1.2, q.size)
+        q["z"] = cz + rng.uniform(-1.2, 1.2, q.size)
+        q["pad0"] = 1.0
+        queries.append(q)
+    mp = np.concatenate(clusters)
+    mp = mp[rng.permutation(mp.size)]
+    qs = np.concatenate(queries)
+    odo = floam_gpu.OdomEstimationClass()
+    odo.init(_params(16), 0.1, "Cauchy")
+    odo.set_trace(8)
+    odo.initMapWithPoints(floam_gpu.DeviceCloud(mp), floam_gpu.DeviceCloud(mp))
+    ident = np.array([0.0, 0.0, 0.0, 1.0]), np.zeros(3)
+    odo.find_correspondences(floam_gpu.DeviceCloud(qs), floam_gpu.DeviceCloud(qs), *ident)
+    for which, leaf in ((0, 0.1), (1, 0.2)):
+        gpu = odo.correspondences(which)
+        vox = oracle_lib.voxel_grid(qs, leaf, stable=True)
+        ref = oracle_lib.stage_correspondences(mp, vox, np.r_[ident[0], ident[1]], edge=which == 0)
+        gated = np.nonzero(ref["flags"] & 4)[0]
+        assert gated.size > 0.9 * vox.shape[0]
+        np.testing.assert_array_equal(gpu["flags"] & 5, ref["flags"] & 5, err_msg=f"set {which}: flags")
+        np.testing.assert_array_equal(gpu["sqd"][gated], ref["sqd"][gated], err_msg=f"set {which}: distances")
+        np.testing.assert_array_equal(gpu["idx"][gated], ref["idx"][gated], err_msg=f"set {which}: indices")
+
+
 def _brute_top5(map_points, qx, qy, qz):
     """(float sq-distances, map indices) of the exact 5-NN under the GPU's rule — FLANN's float L2_Simple order, ties
     by map index — and the count within sqd < 1."""
