@@ -371,12 +371,13 @@ __global__ __launch_bounds__(kTB) void bucket_sort(uint32_t* __restrict__ kin, i
 }
 
 // ---------------------------------------------------------------------------------------------- VoxelGrid
+constexpr int kRunPad = 16;   // the emit loop's look-ahead reads up to 15 elements past the chunk (values unused)
 struct CompactLds {
   union {
     unsigned long long x[kBucketCap];
-    float4 pt[kBucketCap];
+    float4 pt[kBucketCap + kRunPad];
   } u;   // the network's exchanges, then the points (staged after the sort)
-  uint32_t k[kBucketCap];
+  uint32_t k[kBucketCap + kRunPad];
   int v[kBucketCap];
   unsigned tmp[kW];
   unsigned hw[2][kW];
@@ -621,40 +622,49 @@ __global__ __launch_bounds__(kTB) void bucket_compact(VoxelJobDev A, VoxelJobDev
       const float4 f = L.u.pt[e];
       float s0 = f.x, s1 = f.y, s2 = f.z, s3 = f.w;
       int j = e + 1;
-      // 8 keys and 8 points per LDS round trip (the points loaded beside the keys, not after the run test), the next
-      // 8 loaded before the additions of these 8 (long runs — dense voxels near the sensor — stream at the rate of the
-      // in-order adds, not of one LDS round trip per 8), the additions in order up to the first key of another voxel
-      uint32_t kq[8];
-      float4 p[8];
+      // The run's points in groups of 8 keys + 8 points per LDS round trip, double-buffered: the next group's loads are
+      // issued before this group's additions, so long runs (dense voxels near the sensor) stream at the rate of the
+      // in-order adds, not of one LDS round trip per group.  Keys ascend within the chunk, so a group whose last key is
+      // still this voxel's is the voxel's throughout: its 8 additions run without a test or a select (the dependent
+      // adds alone); only the run's last group tests each key.  Look-ahead reads past the chunk's end land in the
+      // arrays' padding (kRunPad) and are never used.  (Two buffers unrolled by hand: no register moves per group.)
+      constexpr int G = 8;
+      uint32_t ka[G], kb[G];
+      float4 pa[G], pb[G];
+      auto load = [&](uint32_t(&kk)[G], float4(&pp)[G], int at) {
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int jj = min(j + q, nc - 1);
-        kq[q] = L.k[jj];
-        p[q] = L.u.pt[jj];
-      }
-      for (bool more = true; more && j < nc;) {
-        uint32_t kn[8];
-        float4 pn[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const int jj = min(j + 8 + q, nc - 1);
-          kn[q] = L.k[jj];
-          pn[q] = L.u.pt[jj];
+        for (int q = 0; q < G; ++q) {
+          kk[q] = L.k[at + q];
+          pp[q] = L.u.pt[at + q];
         }
+      };
+      auto add_full = [&](const float4(&pp)[G]) {
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          if (more && j < nc && kq[q] == key) {
-            s0 += p[q].x; s1 += p[q].y; s2 += p[q].z; s3 += p[q].w;
+        for (int q = 0; q < G; ++q) {
+          s0 += pp[q].x; s1 += pp[q].y; s2 += pp[q].z; s3 += pp[q].w;
+        }
+        j += G;
+      };
+      auto add_tail = [&](const uint32_t(&kk)[G], const float4(&pp)[G]) {
+        bool more = true;
+#pragma unroll
+        for (int q = 0; q < G; ++q) {
+          if (more && j < nc && kk[q] == key) {
+            s0 += pp[q].x; s1 += pp[q].y; s2 += pp[q].z; s3 += pp[q].w;
             ++j;
           } else {
             more = false;
           }
         }
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          kq[q] = kn[q];
-          p[q] = pn[q];
-        }
+      };
+      load(ka, pa, j);
+      for (;;) {
+        load(kb, pb, j + G);
+        if (!(j + G <= nc && ka[G - 1] == key)) { add_tail(ka, pa); break; }
+        add_full(pa);
+        load(ka, pa, j + G);
+        if (!(j + G <= nc && kb[G - 1] == key)) { add_tail(kb, pb); break; }
+        add_full(pb);
       }
       if (j == nc && streamed && c0 + nc < size) {   // reaches the chunk end of a streamed bucket: carried over
         L.carry[0] = s0; L.carry[1] = s1; L.carry[2] = s2; L.carry[3] = s3;
