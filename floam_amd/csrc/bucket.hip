@@ -629,6 +629,7 @@ __global__ __launch_bounds__(kTB) void bucket_compact(VoxelJobDev A, VoxelJobDev
       // adds alone); only the run's last group tests each key.  Look-ahead reads past the chunk's end land in the
       // arrays' padding (kRunPad) and are never used.  (Two buffers unrolled by hand: no register moves per group.)
       constexpr int G = 8;
+      static_assert(2 * G - 1 <= kRunPad, "the look-ahead (up to 2 G - 1 past a run end <= nc) stays in the padding");
       uint32_t ka[G], kb[G];
       float4 pa[G], pb[G];
       auto load = [&](uint32_t(&kk)[G], float4(&pp)[G], int at) {
