@@ -85,3 +85,23 @@ def test_voxel_small_and_ragged(floam_gpu, oracle_lib, n):
     rng = np.random.default_rng(n)
     pts = _cloud(rng.uniform(0.0, 0.35, (n, 3)).astype(np.float32))
     _check(floam_gpu, oracle_lib, pts, 0.1)
+
+
+def test_voxel_run_lengths(floam_gpu, oracle_lib):
+    """Voxels of every run length 1..40 plus 100 and 257 points, shuffled: every residue of the compaction's 8-point
+    groups (bucket.hip emit loop: full groups added without tests, the last group tested per element), runs that end
+    on a group boundary or at the end of a bucket, and runs long enough for several double-buffered groups.  The
+    second call sorts with the splitters the first one wrote (balanced buckets: the in-LDS path)."""
+    rng = np.random.default_rng(17)
+    lens = list(range(1, 41)) + [100, 257]
+    blocks = []
+    for _ in range(12):
+        for n in lens:
+            base = rng.integers(-60, 60, 3) * 3 * 0.1   # voxel corners three cells apart (no index overflow)
+            blocks.append(base + rng.uniform(0.01, 0.09, (n, 3)))
+    xyz = np.concatenate(blocks)
+    xyz = xyz[rng.permutation(len(xyz))].astype(np.float32)
+    pts = _cloud(xyz, intensity=rng.uniform(0.0, 255.0, len(xyz)).astype(np.float32))
+    first = _check(floam_gpu, oracle_lib, pts, 0.1)
+    second = _check(floam_gpu, oracle_lib, pts, 0.1)
+    assert first.shape[0] <= 12 * len(lens) and second.shape == first.shape
