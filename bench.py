@@ -54,20 +54,56 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def hbm_traffic(kernel_substr, config):
-    """HBM bytes per launch of the roofline kernel from the newest committed rocprofv3 PMC summary of the SAME
-    config (profiles/<tag>/hbm_traffic.json, tools/prof_summary.py, separate --pmc FETCH_SIZE / WRITE_SIZE runs of
-    this bench; summaries without a config field are C3 runs).  (None, None) when none is committed."""
+def code_hash():
+    """sha256 (16 hex) of the device-code sources — floam_amd/csrc's kernels, headers, host code and Makefile plus
+    include/floam_c.h — that the product library is built from.  tools/gpu_prof.sh records it next to a profile, so a
+    bench line cites the PMC counters of the code it ran."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "hbm_traffic.json")))
-    for f in reversed(files):
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(ROOT, "floam_amd", "csrc", "*.hip")) +
+                   glob.glob(os.path.join(ROOT, "floam_amd", "csrc", "*.hpp")) +
+                   glob.glob(os.path.join(ROOT, "floam_amd", "csrc", "*.cpp")) +
+                   [os.path.join(ROOT, "floam_amd", "csrc", "Makefile"), os.path.join(ROOT, "include", "floam_c.h")])
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        h.update(open(f, "rb").read())
+    return h.hexdigest()[:16]
+
+
+def hbm_traffic(kernel_substr, config, steps):
+    """The committed rocprofv3 profile for the roofline kernel (profiles/<tag>/hbm_traffic.json, written by
+    tools/prof_summary.py from separate --pmc FETCH_SIZE / WRITE_SIZE runs of this bench): of the SAME config, chosen
+    first by the device-code hash the profile records (the code this bench runs), then by its step count, then by
+    recency (its `created` stamp; older summaries carry none and rank last).  Returns a dict with the HBM bytes per
+    launch, the profile's rocprof average duration of the kernel over its timed region (kernel_stats.csv) and whether
+    code and steps match — or None when no profile of the config is committed."""
+    import csv
+    import glob
+    want = code_hash()
+    best = None
+    for f in glob.glob(os.path.join(ROOT, "profiles", "*", "hbm_traffic.json")):
         d = json.load(open(f))
         if d.get("config", "c3") != config:
             continue
-        for name, v in d.get("kernels", {}).items():
-            if kernel_substr in name:
-                return round(v["total_bytes"]), os.path.relpath(f, ROOT)
-    return None, None
+        hit = next(((n, v) for n, v in d.get("kernels", {}).items() if kernel_substr in n), None)
+        if hit is None:
+            continue
+        rank = (d.get("code_hash") == want, d.get("steps") == steps, d.get("created", ""), f)
+        if best is None or rank > best[0]:
+            best = (rank, f, d, hit)
+    if best is None:
+        return None
+    rank, f, d, (name, v) = best
+    avg_us = None
+    ks = os.path.join(os.path.dirname(f), "kernel_stats.csv")
+    if os.path.exists(ks):
+        for r in csv.DictReader(open(ks)):
+            if r["Name"] == name:
+                avg_us = float(r["AvgUs"])
+    return {"bytes": round(v["total_bytes"]), "source": os.path.relpath(f, ROOT), "rocprof_avg_us": avg_us,
+            "code_match": rank[0], "steps_match": rank[1], "profile_code_hash": d.get("code_hash"),
+            "profile_steps": d.get("steps")}
 
 
 def main():
@@ -338,11 +374,11 @@ def main():
     stats = odo.stats()
 
     def read_timings():
-        arr = (_ffi.KernelTiming * 16)()
+        arr = (_ffi.KernelTiming * 64)()
         n = C.c_int()
-        _ffi.check(L.floam_profile_read(dev, arr, 16, C.byref(n)))
+        _ffi.check(L.floam_profile_read(dev, arr, 64, C.byref(n)))
         return {arr[i].name.decode(): (arr[i].launches, arr[i].total_ms, arr[i].algorithmic_bytes)
-                for i in range(min(n.value, 16))}
+                for i in range(min(n.value, 64))}
 
     roof = None
     if not args.no_roofline:
@@ -364,15 +400,28 @@ def main():
         same = all(np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) for a, b in zip(poses, replay))
         kt = timed.get("knn_search")
         if kt is not None and kt[0] > 0:
+            # HIP events set by the search launch itself (hipExtLaunchKernel: the dispatch's start / end, the duration
+            # rocprofv3 reports); "bracket_avg_us": events recorded on the stream around the launch (+ dispatch gaps)
             avg_ms = kt[1] / kt[0]
             bytes_per = kt[2] / kt[0]
             ach = bytes_per / (avg_ms * 1e-3) / 1e9
-            traffic, traffic_src = hbm_traffic("knn_kernel<", cfg)
+            tr = hbm_traffic("knn_kernel<", cfg, args.steps)
             roof = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": traffic_src,
+                    "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": tr["bytes"] if tr else None,
+                    "traffic_source": tr["source"] if tr else None,
                     "kernel": "knn_kernel (exact 5-NN search over the hash grid, edge + surf queries)",
                     "avg_us": round(avg_ms * 1e3, 2), "launches": int(kt[0]),
-                    "algorithmic_bytes_per_launch": round(bytes_per), "replay_bitwise_identical": bool(same)}
+                    "algorithmic_bytes_per_launch": round(bytes_per), "replay_bitwise_identical": bool(same),
+                    "code_hash": code_hash()}
+            kb = timed.get("knn_search_bracket")
+            if kb is not None and kb[0]:
+                roof["bracket_avg_us"] = round(kb[1] / kb[0] * 1e3, 2)
+            if tr:
+                # the committed profile of this code: its rocprof average for the kernel, and the fraction it gives
+                roof.update({"traffic_code_match": tr["code_match"], "traffic_steps_match": tr["steps_match"],
+                             "rocprof_avg_us": tr["rocprof_avg_us"]})
+                if tr["rocprof_avg_us"]:
+                    roof["frac_rocprof"] = round(bytes_per / (tr["rocprof_avg_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 5)
             for sub, key in (("knn", "correspondence_pass_avg_us"), ("knn_geometry", "knn_geometry_avg_us"),
                              ("lm_solve", "lm_solve_avg_us"), ("lm_solve_sharded", "lm_solve_avg_us")):
                 ks = timed.get(sub)

@@ -1,14 +1,16 @@
 // Stable (key, value) sort for the VoxelGrid pipelines (pcl::VoxelGrid's std::sort of (idx, point) pairs,
-// src/odomEstimationClass.cpp:137-142 and :278-292 via PCL 1.8.1) in two launches after the key producer, instead of
+// src/odomEstimationClass.cpp:137-142 and :278-292 via PCL 1.8.1) in ONE launch after the key producer, instead of
 // four 8-bit digit passes (radix.hip: ~9 us each at the scan's sizes whatever the size — each is a device-wide
 // ranking + decoupled lookback + scatter, bound by its latency).
 //
 // Sample sort with the previous sort's quantiles as splitters:
 //   * the key producer (vox_keys / mm_keys) puts every key into one of 255 buckets — contiguous key ranges cut at 254
-//     splitters — by a binary search in LDS, and counts the buckets (one LDS histogram, as a digit histogram);
-//   * one stable single-pass scatter by bucket (radix_pass with the bucket as the digit);
-//   * one block per bucket sorts its elements (in input order after the stable scatter) by (key, position) with a
-//     register bitonic network — every stride a compile-time constant, lane exchanges by ds_swizzle / ds_bpermute, LDS
+//     splitters — by a binary search in LDS, and appends it with its value to the bucket's region (bucket_append,
+//     bucket.hpp: one atomic per block and bucket reserves the block's slots; past the region's capacity the element
+//     goes to an overflow list).  Round 5 scattered the keys by bucket with a stable digit pass instead: a launch of
+//     ~9 us on each of the two main-stream sorts of a scan;
+//   * one block per bucket sorts its elements by (key, value) — the values are the input positions, so that is the
+//     stable order whatever order the appends landed in — with a register bitonic network — every stride a compile-time constant, lane exchanges by ds_swizzle / ds_bpermute, LDS
 //     only for strides that cross waves — and either writes them out (the map merge) or, for a VoxelGrid, emits its
 //     voxels' centroids itself (a voxel's points share one key, so they never straddle two buckets; output slots by
 //     decoupled lookback over the buckets in key order).  A bucket beyond 4096 elements (stale splitters) is sorted
@@ -83,6 +85,38 @@ __device__ __forceinline__ BucketRange bucket_range(unsigned c, int b, unsigned*
   return BucketRange{s_r[0], s_r[1], s_r[2]};
 }
 
+// ---------------------------------------------------------------------------------------------- bucket source
+struct BucketSrc {   // the consumer's view of the producer's appends (BucketDev)
+  const unsigned long long* reg;
+  const unsigned long long* ovf;
+  const uint8_t* ovf_b;
+  unsigned long long* gath;
+  int cap;
+};
+
+BucketSrc bucket_src(const BucketScratch& bs) { return BucketSrc{bs.reg.p, bs.ovf.p, bs.ovf_b.p, bs.gath.p, bs.cap}; }
+
+// Bucket b's `size` elements as (key << 32 | value) words: its region, or — when the appends overflowed it — the
+// region's words and the bucket's entries of the overflow list (novf long) gathered to gath[start, start + size).
+// Called by all threads (block-uniform arguments); contains barriers.
+__device__ __forceinline__ const unsigned long long* bucket_source(const BucketSrc& S, int b, int start, int size,
+                                                                   int novf) {
+  const unsigned long long* reg = S.reg + (size_t)b * S.cap;
+  if (size <= S.cap) return reg;
+  unsigned long long* g = S.gath + start;
+  __shared__ int s_n;
+  const int t = threadIdx.x;
+  for (int e = t; e < S.cap; e += kTB) g[e] = reg[e];
+  if (t == 0) s_n = S.cap;
+  __syncthreads();
+  for (int o0 = 0; o0 < novf; o0 += kTB) {   // (block-uniform trip count)
+    const int o = o0 + t;
+    if (o < novf && S.ovf_b[o] == (uint8_t)b) g[atomicAdd(&s_n, 1)] = S.ovf[o];
+  }
+  __syncthreads();
+  return g;
+}
+
 // ---------------------------------------------------------------------------------------------- bitonic network
 // E 64-bit words per thread (position p = E t + e), N = kTB E; a stage's stride is a compile-time constant
 template <int M>
@@ -136,33 +170,26 @@ __device__ __forceinline__ void bitonic_sizes64(unsigned long long (&k)[E], unsi
   if constexpr (SIZE < kTB * E) bitonic_sizes64<E, SIZE * 2>(k, s_x);
 }
 
-// The bucket's `size` (<= kTB E) elements kin[0, size) / vin (input order) sorted by (key, position): sorted keys and
-// values into s_k / s_v[0, size).  Contains barriers.
+// The bucket's `size` (<= kTB E) (key << 32 | value) words src[0, size) sorted: keys and values into s_k / s_v[0,
+// size).  Contains barriers.
 template <int E>
-__device__ __forceinline__ void bucket_bitonic(const uint32_t* __restrict__ kin, const int* __restrict__ vin, int size,
+__device__ __forceinline__ void bucket_bitonic(const unsigned long long* __restrict__ src, int size,
                                                unsigned long long* s_x, uint32_t* s_k, int* s_v) {
   const int t = threadIdx.x;
   unsigned long long k[E];
-  // the values are loaded with the keys and parked in s_v by input position (one memory round trip for both; the
-  // network does not touch s_v), then picked up by sorted position from LDS instead of a second gather from memory
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const int q = E * t + e;
-    k[e] = q < size ? ((unsigned long long)kin[q] << 32) | (unsigned)q : ~0ull;
-    if (q < size) s_v[q] = vin[q];
+    k[e] = q < size ? src[q] : ~0ull;
   }
   bitonic_sizes64<E, 2>(k, s_x);
-  __syncthreads();   // (every value parked; a one-wave network has no barrier of its own)
-  int val[E];
-#pragma unroll
-  for (int e = 0; e < E; ++e) val[e] = E * t + e < size ? s_v[(int)(unsigned)k[e]] : 0;
-  __syncthreads();
+  __syncthreads();   // (s_x's last reads, when s_k / s_v share its storage)
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const int p = E * t + e;
     if (p < size) {
       s_k[p] = (uint32_t)(k[e] >> 32);
-      s_v[p] = val[e];
+      s_v[p] = (int)(unsigned)k[e];
     }
   }
   __syncthreads();
@@ -178,8 +205,9 @@ __device__ __forceinline__ void by_size(int size, F f) {   // the smallest netwo
 }
 
 // ---------------------------------------------------------------------------------------------- streamed bucket
-// A bucket beyond kBucketCap (stale splitters): stable LSD passes over its key range through global memory, chunk by
-// chunk of kStreamChunk (ping-pong between the scatter's region and the output; the result lands in kb / vb).
+// A bucket beyond kBucketCap (stale splitters): stable LSD passes through global memory, chunk by chunk of
+// kStreamChunk (ping-pong between ka / va and kb / vb; the result lands in kb / vb) — first over the values' range,
+// then over the keys' range, so the result is in (key, value) order whatever the input order.
 constexpr int kStreamR = 8;
 constexpr int kStreamChunk = kTB * kStreamR;
 
@@ -247,34 +275,47 @@ __device__ __forceinline__ void chunk_rank(const unsigned (&dig)[kStreamR], int 
 __device__ void stream_sort(uint32_t* __restrict__ ka, int* __restrict__ va, uint32_t* __restrict__ kb,
                             int* __restrict__ vb, int size, StreamLds& L) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  uint32_t mn = 0xFFFFFFFFu, mx = 0u;
+  uint32_t mn[2] = {0xFFFFFFFFu, 0xFFFFFFFFu}, mx[2] = {0u, 0u};   // [0] keys, [1] values
   for (int e = t; e < size; e += kTB) {
-    const uint32_t k = ka[e];
-    mn = min(mn, k);
-    mx = max(mx, k);
+    const uint32_t k = ka[e], v = (uint32_t)va[e];
+    mn[0] = min(mn[0], k);
+    mx[0] = max(mx[0], k);
+    mn[1] = min(mn[1], v);
+    mx[1] = max(mx[1], v);
   }
+  uint32_t lo[2], hi[2];
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
-    mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
-  }
-  if (lane == 0) { L.red[0][w] = mn; L.red[1][w] = mx; }
-  __syncthreads();
-  uint32_t kmin = L.red[0][0], kmax = L.red[1][0];
+  for (int j = 0; j < 2; ++j) {
 #pragma unroll
-  for (int k = 1; k < kW; ++k) {
-    kmin = min(kmin, L.red[0][k]);
-    kmax = max(kmax, L.red[1][k]);
+    for (int o = 32; o > 0; o >>= 1) {
+      mn[j] = min(mn[j], (uint32_t)__shfl_xor((int)mn[j], o, 64));
+      mx[j] = max(mx[j], (uint32_t)__shfl_xor((int)mx[j], o, 64));
+    }
+    __syncthreads();
+    if (lane == 0) { L.red[0][w] = mn[j]; L.red[1][w] = mx[j]; }
+    __syncthreads();
+    lo[j] = L.red[0][0];
+    hi[j] = L.red[1][0];
+#pragma unroll
+    for (int k = 1; k < kW; ++k) {
+      lo[j] = min(lo[j], L.red[0][k]);
+      hi[j] = max(hi[j], L.red[1][k]);
+    }
   }
-  const uint32_t range = kmax - kmin;
-  const int npass = range ? (32 - __clz((int)range) + 7) / 8 : 0;
+  const uint32_t krange = hi[0] - lo[0], vrange = hi[1] - lo[1];
+  const int nkey = krange ? (32 - __clz((int)krange) + 7) / 8 : 0;
+  const int nval = vrange ? (32 - __clz((int)vrange) + 7) / 8 : 0;
+  const int npass = nval + nkey;
   uint32_t *ks = ka, *kd = kb;
   int *vs = va, *vd = vb;
   for (int p = 0; p < npass; ++p) {
-    const int sh = 8 * p;
+    const bool by_val = p < nval;   // (block-uniform)
+    const int sh = 8 * (by_val ? p : p - nval);
+    const uint32_t base = by_val ? lo[1] : lo[0];
+    auto digit = [&](uint32_t k, int v) { return (((by_val ? (uint32_t)v : k) - base) >> sh) & 255u; };
     L.run[t] = 0u;
     __syncthreads();
-    for (int e = t; e < size; e += kTB) atomicAdd(&L.run[((ks[e] - kmin) >> sh) & 255u], 1u);
+    for (int e = t; e < size; e += kTB) atomicAdd(&L.run[digit(ks[e], vs[e])], 1u);
     __syncthreads();
     const unsigned c = L.run[t];
     unsigned inc = c;
@@ -296,7 +337,7 @@ __device__ void stream_sort(uint32_t* __restrict__ ka, int* __restrict__ va, uin
         const int e = w * 64 * kStreamR + r * 64 + lane;
         key[r] = e < nc ? ks[c0 + e] : 0u;
         val[r] = e < nc ? vs[c0 + e] : 0;
-        dig[r] = ((key[r] - kmin) >> sh) & 255u;
+        dig[r] = digit(key[r], val[r]);
       }
       chunk_rank(dig, nc, pos, L);
 #pragma unroll
@@ -332,12 +373,25 @@ struct SortLds {
   unsigned tmp[kW];
 };
 
-__global__ __launch_bounds__(kTB) void bucket_sort(uint32_t* __restrict__ kin, int* __restrict__ vin,
+// a streamed bucket's elements unpacked into separate keys / values (stream_sort's layout)
+__device__ __forceinline__ void unpack_bucket(const unsigned long long* __restrict__ src, int size,
+                                              uint32_t* __restrict__ k, int* __restrict__ v) {
+  for (int e = threadIdx.x; e < size; e += kTB) {
+    const unsigned long long x = src[e];
+    k[e] = (uint32_t)(x >> 32);
+    v[e] = (int)(unsigned)x;
+  }
+  __syncthreads();
+}
+
+// kscr / vscr: scratch of a streamed bucket (at the bucket's output range)
+__global__ __launch_bounds__(kTB) void bucket_sort(BucketSrc S, uint32_t* __restrict__ kscr, int* __restrict__ vscr,
                                                    uint32_t* __restrict__ kout, int* __restrict__ vout,
                                                    const unsigned* __restrict__ hist, const int* __restrict__ gate,
                                                    unsigned long long* __restrict__ split, const int* __restrict__ geo) {
   const int b = blockIdx.x, t = threadIdx.x;
   const unsigned hc = hist[t];   // (kTB == kBuckets; issued with the gate load)
+  const int novf = (int)hist[kBucketOvfWord];
   const int gv = gate ? *gate : 1;
   if (!gv) return;
   __shared__ union {
@@ -346,22 +400,17 @@ __global__ __launch_bounds__(kTB) void bucket_sort(uint32_t* __restrict__ kin, i
   } L;
   const BucketRange R = bucket_range(hc, b, L.s.tmp);
   const int start = R.start, size = R.size;
-  if (size == 0) return;
-  if (b == kBuckets - 1) {   // the dropped elements: already in input order
-    for (int e = t; e < size; e += kTB) {
-      kout[start + e] = kin[start + e];
-      vout[start + e] = vin[start + e];
-    }
-    return;
-  }
+  if (size == 0) return;   // (bucket 255, the dropped elements, is never appended to)
+  const unsigned long long* src = bucket_source(S, b, start, size, novf);
   if (size > kBucketCap) {
-    stream_sort(kin + start, vin + start, kout + start, vout + start, size, L.st);
+    unpack_bucket(src, size, kscr + start, vscr + start);
+    stream_sort(kscr + start, vscr + start, kout + start, vout + start, size, L.st);
     write_splitters(split, geo, R.kept, start, size, [&](int q) { return kout[start + q]; });
     return;
   }
   by_size(size, [&](auto EC) {
     constexpr int E = decltype(EC)::value;
-    bucket_bitonic<E>(kin + start, vin + start, size, L.s.x, L.s.k, L.s.v);
+    bucket_bitonic<E>(src, size, L.s.x, L.s.k, L.s.v);
   });
   for (int e = t; e < size; e += kTB) {
     kout[start + e] = L.s.k[e];
@@ -443,7 +492,10 @@ __device__ __forceinline__ void block_sum2(int (&c)[2], unsigned (*hw)[kW]) {
 // parity: call 1's VoxelGrids on the side stream, then call 2's on the main stream), printed by bucket_stamps_print
 __device__ unsigned g_bc_st[2][kBuckets][8];
 
-__global__ __launch_bounds__(kTB) void bucket_compact(VoxelJobDev A, VoxelJobDev B, uint32_t* __restrict__ kin,
+// kin / vin: scratch of a streamed bucket (its keys and values unpacked at the bucket's range), kout / vout: the
+// streamed sort's output
+__global__ __launch_bounds__(kTB) void bucket_compact(VoxelJobDev A, VoxelJobDev B, BucketSrc S,
+                                                      uint32_t* __restrict__ kin,
                                                       int* __restrict__ vin, uint32_t* __restrict__ kout,
                                                       int* __restrict__ vout, const unsigned* __restrict__ hist,
                                                       const int* __restrict__ overflow,
@@ -464,6 +516,7 @@ __global__ __launch_bounds__(kTB) void bucket_compact(VoxelJobDev A, VoxelJobDev
   const int nA0 = *A.d_n0, nA1 = A.d_n1 ? *A.d_n1 : 0, nB0 = *B.d_n0, nB1 = B.d_n1 ? *B.d_n1 : 0;
   const int ovf0 = overflow[0], ovf1 = overflow[1];   // (no two-element arrays indexed by a run-time job: scratch)
   const unsigned hw0 = hist[t];                        // (kTB == kBuckets)
+  const int novf = (int)hist[kBucketOvfWord];
   __syncthreads();
   const int b = s_b;
   if (!gv) {   // gated off (no keyframe): the output is the unchanged first part (the map).  By block index: no
@@ -494,12 +547,14 @@ __global__ __launch_bounds__(kTB) void bucket_compact(VoxelJobDev A, VoxelJobDev
     return;
   }
   const bool streamed = size > kBucketCap;   // (block-uniform)
+  const unsigned long long* src = bucket_source(S, b, start, size, novf);
   if (streamed) {
+    unpack_bucket(src, size, kin + start, vin + start);
     stream_sort(kin + start, vin + start, kout + start, vout + start, size, U.st);
   } else {
     by_size(size, [&](auto EC) {
       constexpr int E = decltype(EC)::value;
-      bucket_bitonic<E>(kin + start, vin + start, size, L.u.x, L.k, L.v);
+      bucket_bitonic<E>(src, size, L.u.x, L.k, L.v);
     });
   }
   const unsigned long long T1 = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
@@ -732,7 +787,18 @@ void BucketScratch::reserve(int n, hipStream_t st) {
     geo.reserve(kGeoWords);
     FLOAM_HIP(hipMemsetAsync(geo.p, 0, sizeof(int) * kGeoWords, st));
   }
-  bkt.reserve((size_t)std::max(n, 1));
+  n = std::max(n, 1);
+  cap = std::max(cap, bucket_cap(n));   // (only grows: a region sized for more elements serves fewer)
+  reg.reserve((size_t)kBuckets * cap);
+  ovf.reserve((size_t)n);
+  ovf_b.reserve((size_t)n);
+  gath.reserve((size_t)n);
+}
+
+BucketDev bucket_dev(BucketScratch& bs, int n, hipStream_t st) {
+  bs.reserve(n, st);
+  return BucketDev{bs.seeded ? bs.split.p : nullptr, bs.geo.p, bs.reg.p, bs.ovf.p, bs.ovf_b.p, bs.cap,
+                   (int)std::min<size_t>(bs.ovf.cap, (size_t)INT_MAX)};
 }
 
 bool bucket_sort_enabled(int pipeline) {
@@ -753,10 +819,10 @@ void bucket_voxel_launch(BucketScratch& bs, RadixScratch& rs, const VoxelJobDev&
   if (n <= 0) return;
   bs.reserve(n, st);
   rs.reserve(n, st);
-  radix_digit_pass_launch(rs, k0, v0, k1, v1, n, bs.bkt.p, st, gate, n_dev);
   static const bool stamps = FLOAM_DIAG_ENV("FLOAM_BC_STAMPS") != nullptr;
   static unsigned launches = 0;
-  hipLaunchKernelGGL(bucket_compact, dim3(kBuckets), dim3(kTB), 0, st, A, B, k1, v1, k0, v0, rs.ctl.p, overflow,
+  hipLaunchKernelGGL(bucket_compact, dim3(kBuckets), dim3(kTB), 0, st, A, B, bucket_src(bs), k1, v1, k0, v0, rs.ctl.p,
+                     overflow,
                      status, rs.ctl.p, gate, bs.split.p, bs.geo.p, ticket,
                      stamps ? (int)(launches++ & 1u) + 1 : 0);
   FLOAM_LAUNCH_CHECK();
@@ -798,13 +864,12 @@ void bucket_stamps_print() {
 }
 
 void bucket_sort_launch(BucketScratch& bs, RadixScratch& rs, uint32_t* k0, int* v0, uint32_t* k1, int* v1, int n,
-                        hipStream_t st, const int* gate, const int* n_dev) {
+                        hipStream_t st, const int* gate) {
   if (n <= 0) return;
   bs.reserve(n, st);
   rs.reserve(n, st);
-  radix_digit_pass_launch(rs, k0, v0, k1, v1, n, bs.bkt.p, st, gate, n_dev);
-  hipLaunchKernelGGL(bucket_sort, dim3(kBuckets), dim3(kTB), 0, st, k1, v1, k0, v0, rs.ctl.p, gate, bs.split.p,
-                     bs.geo.p);
+  hipLaunchKernelGGL(bucket_sort, dim3(kBuckets), dim3(kTB), 0, st, bucket_src(bs), k1, v1, k0, v0, rs.ctl.p, gate,
+                     bs.split.p, bs.geo.p);
   FLOAM_LAUNCH_CHECK();
 }
 

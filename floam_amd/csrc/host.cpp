@@ -386,6 +386,7 @@ struct floam_odom {
   // peer sharding (floam_odom_set_shard_peers): this rank's exchange buffer, the ranks' buffers as mapped here, and
   // the IPC mappings to close
   unsigned long long* xbuf = nullptr;
+  DevBuf<int> probe;   // the peer mapping probe's verdict (set_shard_peers)
   ShardPeers peers;
   std::vector<void*> xopened;
   bool peer = false;
@@ -615,10 +616,17 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
         if (stages && (ctx.profile & FLOAM_PROF_KNN_BYTES))   // (replay only, before the timed scope)
           knn_stage_launch(o->lm.p, it == 0 ? x0_dev : nullptr, qe, o->gE, o->ce, qs, o->gS, o->cs, o->mapE.count.p,
                            o->mapS.count.p, o->rank, o->world, o->knn_evict, st);
-        ProfScope ps1(ctx, "knn_search", FLOAM_PROF_KNN_DETAIL);
+        ProfScope ps1(ctx, "knn_search_bracket", FLOAM_PROF_KNN_DETAIL);   // (events around the launch)
+        // "knn_search": HIP events set by the launch itself to the kernel's start and end (rocprofv3's duration)
+        hipEvent_t k0 = nullptr, k1 = nullptr;
+        if (ctx.profile & FLOAM_PROF_KNN_DETAIL) {
+          k0 = ctx.get_event();
+          k1 = ctx.get_event();
+        }
         // (also starts the solve: LM state reset, the first solve at the prediction)
         knn_launch(o->lm.p, it == 0 ? x0_dev : nullptr, qe, o->gE, o->ce, qs, o->gS, o->cs, o->mapE.count.p,
-                   o->mapS.count.p, o->rank, o->world, st);
+                   o->mapS.count.p, o->rank, o->world, st, k0, k1);
+        if (k0) ctx.pending.push_back(PendingTiming{"knn_search", k0, k1, 0.0});
       }
       ProfScope ps2(ctx, "knn_geometry", FLOAM_PROF_KNN_DETAIL);
       geom_launch(o->lm.p, qe, o->ce, qs, o->cs, gram, o->fp32_geom, o->lmb, st);
@@ -1826,14 +1834,18 @@ floam_status floam_odom_set_shard_peers(floam_odom* o, int rank, int world, cons
       throw Error(FLOAM_ERR_INVALID_ARGUMENT, "bad rank / world (1 <= world <= 8)");
     if (world > 1 && (!ipc_handles == !dev_ptrs))
       throw Error(FLOAM_ERR_INVALID_ARGUMENT, "give exactly one of ipc_handles and dev_ptrs");
-    odom_collect(o, ctx_for(o->device), 0);
+    DeviceCtx& ctx = ctx_for(o->device);
+    odom_collect(o, ctx, 0);
+    shard_xbuf(o);   // (may refuse: before the old configuration is torn down, so a refusal leaves it intact)
     if (o->comm) {
       ncclCommDestroy(o->comm);
       o->comm = nullptr;
     }
     o->ar_fn = nullptr;
     shard_peers_release(o);
-    shard_xbuf(o);
+    // from here on a failure leaves the handle unsharded (world 1), never half-configured
+    o->rank = 0;
+    o->world = 1;
     ShardPeers P;
     P.world = world;
     P.mine = o->xbuf;
@@ -1859,11 +1871,25 @@ floam_status floam_odom_set_shard_peers(floam_odom* o, int rank, int world, cons
     }
     // every rank starts a fresh exchange sequence: the counter (LMState::xseq) at zero and its own buffer zeroed, so
     // the tags of all ranks agree whatever each rank ran before (the ranks then meet at a barrier before updating)
-    DeviceCtx& ctx = ctx_for(o->device);
     o->lm.reserve(1);
     FLOAM_HIP(hipMemsetAsync(reinterpret_cast<char*>(o->lm.p) + offsetof(LMState, xseq), 0, sizeof(unsigned),
                              ctx.stream));
     FLOAM_HIP(hipMemsetAsync(o->xbuf, 0, sizeof(unsigned long long) * kShardXchgWords, ctx.stream));
+    if (world > 1) {   // every peer mapping answers before a solve relies on it (lm.hip peer_probe: <= 2 s)
+      o->probe.reserve(1);
+      peer_probe_launch(P, rank, o->probe.p, ctx.stream);
+      int fail = 0;
+      FLOAM_HIP(hipMemcpyAsync(&fail, o->probe.p, sizeof(int), hipMemcpyDeviceToHost, ctx.stream));
+      FLOAM_HIP(hipStreamSynchronize(ctx.stream));
+      if (fail) {
+        shard_peers_release(o);
+        std::string ranks;
+        for (int r = 0; r < world; ++r)
+          if ((fail >> r) & 1) ranks += (ranks.empty() ? "" : ", ") + std::to_string(r);
+        throw Error(FLOAM_ERR_COMM, "peer exchange probe: no answer from rank(s) " + ranks +
+                                        " within 2 s (the peer mapping does not work; use floam_odom_set_shard)");
+      }
+    }
     FLOAM_HIP(hipStreamSynchronize(ctx.stream));
     o->peers = P;
     o->rank = rank;

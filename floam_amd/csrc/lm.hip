@@ -1308,6 +1308,37 @@ void LMBuffers::reserve(hipStream_t st) {
   FLOAM_HIP(hipMemsetAsync(gmat.p, 0, sizeof(double) * gmat.cap, st));
 }
 
+// Peer mapping probe (floam_odom_set_shard_peers): every rank stores a fixed word at kShardProbeWord of its own
+// exchange buffer (system scope) and reads every rank's through the peer mappings until each carries its rank's word or
+// kShardProbeTicks have passed.  *fail = the mask of the ranks not seen.  The ranks call set_shard_peers together (they
+// have just gathered each other's handles), so a working xGMI mapping answers in microseconds; a mapping that does not
+// work fails the peering in seconds — and the caller takes the RCCL form — instead of the first solve's ~20-s wait.
+__device__ __forceinline__ unsigned long long probe_word(int r) { return (0x9E3779B9ull << 32) | (unsigned)(r + 1); }
+
+__global__ void peer_probe(ShardPeers P, int rank, int* __restrict__ fail) {
+  const int lane = (int)threadIdx.x;
+  if (lane == 0)
+    __hip_atomic_store(&P.mine[kShardProbeWord], probe_word(rank), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  bool seen = lane >= P.world;
+  const unsigned long long* src = P.buf[0];
+#pragma unroll
+  for (int q = 1; q < kMaxShardRanks; ++q)   // (selected, not indexed: the argument array stays in registers)
+    if (q == lane) src = P.buf[q];
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (!seen) {
+    seen = __hip_atomic_load(&src[kShardProbeWord], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == probe_word(lane);
+    if (seen || __builtin_amdgcn_s_memrealtime() - t0 > kShardProbeTicks) break;
+    __builtin_amdgcn_s_sleep(8);
+  }
+  const unsigned long long missing = __ballot(!seen);
+  if (lane == 0) *fail = (int)(unsigned)missing;
+}
+
+void peer_probe_launch(const ShardPeers& P, int rank, int* d_fail, hipStream_t st) {
+  hipLaunchKernelGGL(peer_probe, dim3(1), dim3(64), 0, st, P, rank, d_fail);
+  FLOAM_LAUNCH_CHECK();
+}
+
 void lm_solve_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const CorrSet& cs,
                      const int* d_ns, int ns_ub, int mode, LMBuffers& b, hipStream_t st, unsigned long long* dbg,
                      const ShardPeers* peers) {

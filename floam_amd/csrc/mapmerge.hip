@@ -64,7 +64,8 @@ __global__ __launch_bounds__(kTB) void mm_keys(VoxelJobDev A, VoxelJobDev B, con
       pv[h][u] = q < 2 * 6 * 32 ? partials[(jb * kVoxMinMaxBlocks + l + 32 * u) * 6 + c] : 0.f;
   }
   const VoxelJobDev& J0 = job ? B : A;
-  const int e0 = blockIdx.x * blockDim.x + threadIdx.x;
+  // this thread's first element: a chunk of kTB x kAppendR per block with the bucket append, else a grid stride
+  const int e0 = blockIdx.x * blockDim.x * (bd.split ? kAppendR : 1) + threadIdx.x;
   PointRec sp0;
   if (e0 < J0.n1_ub) sp0 = J0.part1[e0];
   double pose0[7];
@@ -133,43 +134,60 @@ __global__ __launch_bounds__(kTB) void mm_keys(VoxelJobDev A, VoxelJobDev B, con
   }
   const VoxelJobDev& J = job ? B : A;
   const bool full = job ? fullB : fullA;
-  const VoxelGeom& G = job ? gB : gA;
+  VoxelGeom G;   // (a copy selected field by field: a reference to one of the two kept both in scratch)
+  for (int d = 0; d < 3; ++d) {
+    G.min_b[d] = job ? gB.min_b[d] : gA.min_b[d];
+    G.divb_mul[d] = job ? gB.divb_mul[d] : gA.divb_mul[d];
+  }
+  G.overflow = job ? gB.overflow : gA.overflow;
   const int n0 = job ? nB0 : nA0, n1 = job ? nB1 : nA1;
   const int start = full ? 0 : n0, count = job ? sizeB : sizeA, base = job ? sizeA : 0;
   __shared__ uint32_t s_spl[kBuckets];
   const bool bucket = vox_bucket_begin(bd, sp_t, job, G, job ? s_mm[1][5] : s_mm[0][5], J.inv, s_spl);
   int kept = 0;
-  for (int e = e0; e < count; e += gridDim.x * blockDim.x) {
+  auto key_of = [&](int e) {   // sort key of element e of the job's set (0xFFFFFFFF: cropped)
     const int i = start + e;   // index into the job's [map ; scan] concatenation
-    uint32_t key = 0xFFFFFFFFu;
-    PointRec p;
+    float4 q;   // (x, y, z, intensity: no PointRec temporary, which stays a private array in this kernel)
     bool in;
     if (!full && e == e0) {   // the prefetched scan record: vox_fetch's transform and CropBox, on registers
       float x, y, z;
       associate_to_map(pose0, sp0.x, sp0.y, sp0.z, x, y, z);
-      p.x = x; p.y = y; p.z = z;
+      q = make_float4(x, y, z, 0.f);
       const float mnx = (float)(pose0[4] - 100), mny = (float)(pose0[5] - 100), mnz = (float)(pose0[6] - 100);
       const float mxx = (float)(pose0[4] + 100), mxy = (float)(pose0[5] + 100), mxz = (float)(pose0[6] + 100);
       in = !(x < mnx || y < mny || z < mnz || x > mxx || y > mxy || z > mxz);
     } else {
-      in = vox_fetch(J, n0, n1, i, p);
+      in = vox_fetch4(J, n0, n1, i, q);
     }
-    if (in) {
-      key = ((uint32_t)job << 31) | (G.overflow ? (uint32_t)i : voxel_idx(G, J.inv, p));
-      ++kept;
+    if (!in) return 0xFFFFFFFFu;
+    ++kept;
+    return ((uint32_t)job << 31) | (G.overflow ? (uint32_t)i : voxel_idx(G, J.inv, q.x, q.y, q.z));
+  };
+  if (bucket) {   // appended to the buckets' regions: no keys array, no scatter pass
+    for (int c0 = blockIdx.x * blockDim.x * kAppendR; c0 < count; c0 += gridDim.x * blockDim.x * kAppendR) {
+      uint32_t key[kAppendR];
+      int val[kAppendR];
+#pragma unroll
+      for (int r = 0; r < kAppendR; ++r) {
+        const int e = c0 + r * kTB + (int)threadIdx.x;
+        key[r] = e < count ? key_of(e) : 0xFFFFFFFFu;
+        val[r] = start + e;
+      }
+      bucket_append<kAppendR>(bd, radix_ctl, s_spl, key, val, s_hist, reinterpret_cast<int*>(s_hist + kBuckets),
+                              reinterpret_cast<int*>(s_hist + 2 * kBuckets));
     }
-    keys[base + e] = key;
-    vals[base + e] = i;
-    if (bucket) {
-      const unsigned b = bucket_of(s_spl, key);
-      bd.bkt[base + e] = (uint8_t)b;
-      atomicAdd(&s_hist[b], 1u);
-    } else {
+    if (kept) atomicAdd(&s_kept, kept);
+    __syncthreads();
+  } else {
+    for (int e = e0; e < count; e += gridDim.x * blockDim.x) {
+      const uint32_t key = key_of(e);
+      keys[base + e] = key;
+      vals[base + e] = start + e;
       radix_hist_add(s_hist, key);
     }
+    if (kept) atomicAdd(&s_kept, kept);
+    radix_hist_end(s_hist, radix_ctl);   // (its barrier orders s_kept)
   }
-  if (kept) atomicAdd(&s_kept, kept);
-  radix_hist_end(s_hist, radix_ctl);   // (its barrier orders s_kept)
   if (threadIdx.x == 0 && s_kept) atomicAdd(&ctl[job], s_kept);
 }
 
@@ -745,20 +763,20 @@ void map_merge_launch(VoxelScratch2& vs, MapMergeScratch& ms, const VoxelJob& a,
   vs.rs.reserve(n, st);
   // the sort set is the scan's points on the merge path: a grid for them (a full-sort update loops over more)
   const int nset_ub = std::max(a.n1_ub, b.n1_ub);
-  const unsigned kblocks = std::max(1u, std::min(div_up(std::max(nset_ub, 1), 4 * kTB), 64u));
   // the bucket sort once its splitters are seeded (bucket.hip); the first sort takes the digit passes and seeds them
   const bool bucket = bucket_sort_enabled(1), use_bucket = bucket && ms.bs.seeded;
-  BucketDev bd{nullptr, nullptr, nullptr};
-  if (bucket) {
-    ms.bs.reserve(n, st);
-    bd = BucketDev{use_bucket ? ms.bs.split.p : nullptr, ms.bs.bkt.p, ms.bs.geo.p};
-  }
+  BucketDev bd{};
+  if (bucket) bd = bucket_dev(ms.bs, n, st);
+  // the bucket append: one chunk of kTB x kAppendR elements per block (a full-sort update loops over more); the digit
+  // histograms: few blocks (one global atomic per non-zero bin and block)
+  const unsigned kblocks = use_bucket ? std::max(1u, std::min(div_up(std::max(nset_ub, 1), kTB * kAppendR), 512u))
+                                      : std::max(1u, std::min(div_up(std::max(nset_ub, 1), 4 * kTB), 64u));
   hipLaunchKernelGGL(mm_keys, dim3(kblocks, 2), dim3(kTB), 0, st, A, B, vs.partials.p, vs.s.k0.p, vs.s.v0.p,
                      ms.status.p, 2 * ms.tiles_cap, vs.rs.ctl.p, gate, vs.overflow.p + 2, ms.ctl.p, ka.meta_in,
                      kb.meta_in, ms.flags.p, seq, force_full ? 1 : 0, bd);
   FLOAM_LAUNCH_CHECK();
   if (use_bucket) {
-    bucket_sort_launch(ms.bs, vs.rs, vs.s.k0.p, vs.s.v0.p, vs.s.k1.p, vs.s.v1.p, n, st, gate, vs.overflow.p + 2);
+    bucket_sort_launch(ms.bs, vs.rs, vs.s.k0.p, vs.s.v0.p, vs.s.k1.p, vs.s.v1.p, n, st, gate);
   } else {
     radix_sort_launch(vs.rs, vs.s.k0.p, vs.s.v0.p, vs.s.k1.p, vs.s.v1.p, n, st, gate, vs.overflow.p + 2);
     if (bucket) bucket_seed_launch(ms.bs, vs.s.k0.p, vs.overflow.p + 2, n, st, gate);

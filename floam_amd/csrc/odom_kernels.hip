@@ -8,6 +8,8 @@
 #include <cstdlib>
 #include <climits>
 
+#include <hip/hip_ext.h>
+
 #include "grid.hpp"
 #include "lm_eval.hpp"
 #include "odom_kernels.hpp"
@@ -1547,7 +1549,7 @@ static void corr_args(const QuerySet& qe, const Grid& ge, CorrSet& ce, const Que
 
 void knn_launch(LMState* d_st, const double* x0_dev, const QuerySet& qe, const Grid& ge, CorrSet& ce,
                 const QuerySet& qs, const Grid& gs, CorrSet& cs, const int* d_me, const int* d_ms, int rank, int world,
-                hipStream_t st) {
+                hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
   CorrArgs E, S;
   corr_args(qe, ge, ce, qs, gs, cs, E, S);
   if (qe.n_ub <= 0 && qs.n_ub <= 0) {   // nothing to search: still start the solve
@@ -1560,7 +1562,11 @@ void knn_launch(LMState* d_st, const double* x0_dev, const QuerySet& qe, const G
   const int nS = qs.grid_hint > 0 ? std::min(qs.grid_hint, qs.n_ub) : qs.n_ub;
   const unsigned nbE = std::min(div_up((size_t)std::max(nE, 1) * G, kTB), 4096u);
   const unsigned nbS = std::min(div_up((size_t)std::max(nS, 1) * G, kTB), 8192u);
-  hipLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6, 3>), dim3(nbE + nbS), dim3(kTB), 0, st, d_st, x0_dev, E, S,
+  if (ev0 || ev1)
+    hipExtLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6, 3>), dim3(nbE + nbS), dim3(kTB), 0, st, ev0, ev1, 0,
+                          d_st, x0_dev, E, S, (int)nbE, d_me, d_ms, rank, world);
+  else
+    hipLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6, 3>), dim3(nbE + nbS), dim3(kTB), 0, st, d_st, x0_dev, E, S,
                        (int)nbE, d_me, d_ms, rank, world);
   FLOAM_LAUNCH_CHECK();
 }

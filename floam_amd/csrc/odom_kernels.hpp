@@ -173,6 +173,8 @@ constexpr int kEdgeEvalBlocks = 64;                // edge-only evaluation grid 
 constexpr int kRecEvalBlocks = 128;                // per-record evaluation grid (Huber / fp32; fixed order)
 constexpr int kMaxShardRanks = 8;                   // peer sharding: ranks (one node's GPUs)
 constexpr int kShardXchgWords = 512;                // peer sharding: exchange buffer granules (2 x 58 used; 4 KB)
+constexpr int kShardProbeWord = kShardXchgWords - 8;  // ... and the mapping probe's word (peer_probe_launch)
+constexpr unsigned long long kShardProbeTicks = 200000000ull;   // the probe's wait: 2 s (100-MHz s_memrealtime)
 
 // LM modes: surf half from the Gram matrix (squared loss, fp64), Huber loss, fp32 geometry + residuals / Jacobians
 enum { LM_GRAM = 1, LM_HUBER = 2, LM_FP32 = 4 };
@@ -281,9 +283,11 @@ void deskew_bridge_launch(const LMState* st, OdomDev* s, double scan_period, Poi
 // knn_launch — exact 5-NN (blocks [0, nbE) edge queries against the corner map, the rest surf against the surf map);
 // geom_launch — line / plane fits and the residual records (fp64, or fp32 with fp32).
 // knn_launch also starts the solve (lm_reset): LM state reset, x = x0_dev when non-null, hand-off epoch advanced
+// ev0 / ev1 (profiling): HIP events set to the search kernel's own start and end (hipExtLaunchKernel: the dispatch's
+// begin / end timestamps, what rocprofv3 reports), not to the stream position around it
 void knn_launch(LMState* d_st, const double* x0_dev, const QuerySet& qe, const Grid& ge, CorrSet& ce,
                 const QuerySet& qs, const Grid& gs, CorrSet& cs, const int* d_me, const int* d_ms, int rank, int world,
-                hipStream_t st);
+                hipStream_t st, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 // gram: the squared-loss solves' surf Gram matrix of the accepted surf records into b.gmat (b.gpart's partials)
 void geom_launch(LMState* d_st, const QuerySet& qe, CorrSet& ce, const QuerySet& qs, CorrSet& cs, bool gram,
                  bool fp32, LMBuffers& b, hipStream_t st);
@@ -311,6 +315,8 @@ struct ShardPeers {
 void lm_solve_launch(LMState* d_st, const CorrSet& ce, const int* d_ne, int ne_ub, const CorrSet& cs,
                      const int* d_ns, int ns_ub, int mode, LMBuffers& b, hipStream_t st,
                      unsigned long long* dbg = nullptr, const ShardPeers* peers = nullptr);
+// the peer mappings' probe (lm.hip): *d_fail = mask of the ranks whose buffer did not answer within 2 s (0: all did)
+void peer_probe_launch(const ShardPeers& P, int rank, int* d_fail, hipStream_t st);
 // The same solve sharded over ranks (one process per GPU): evaluation k = 0..4 in one launch each (the control step
 // of evaluation k - 1 folded in, run redundantly by every block on the all-reduced sums), leaving this rank's 29
 // sums in b.sums for the caller's all-reduce; lm_shard_final_launch runs the last control step.

@@ -56,8 +56,7 @@ __global__ __launch_bounds__(kTB) void radix_pass(const uint32_t* __restrict__ k
                                                   unsigned long long* __restrict__ status,
                                                   const int* __restrict__ gate, const int* __restrict__ n_dev,
                                                   int stamps, const PointRec* __restrict__ pin,
-                                                  float4* __restrict__ pxyz, PointRec* __restrict__ prec,
-                                                  const uint8_t* __restrict__ digs) {
+                                                  float4* __restrict__ pxyz, PointRec* __restrict__ prec) {
   const unsigned long long ts0 = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
   // every load of the prologue is issued at once (one memory round trip, not three in a row): the gate, the epoch,
   // the device count, this digit's histogram count and the tile's elements up to the host bound n (allocated; the
@@ -75,13 +74,13 @@ __global__ __launch_bounds__(kTB) void radix_pass(const uint32_t* __restrict__ k
   const int base = tile * kTile + w * 64 * kItems;
   uint32_t key[kItems];
   int val[kItems];
-  unsigned dig[kItems];   // digs (bucket.hip): each element's digit given (its bucket), else the key's digit `pass`
+  unsigned dig[kItems];
 #pragma unroll
   for (int r = 0; r < kItems; ++r) {
     const int i = base + r * 64 + lane;
     key[r] = i < n ? kin[i] : 0u;
     val[r] = PAYLOAD ? i : (i < n ? vin[i] : 0);
-    dig[r] = digs ? (i < n ? (unsigned)digs[i] : 0u) : (key[r] >> (8 * pass)) & 255u;
+    dig[r] = (key[r] >> (8 * pass)) & 255u;
   }
   // PAYLOAD: the tile's records into LDS in input order as 16-B chunks, thread t chunk t + 256 k (every load
   // instruction covers whole contiguous lines once; a lane loading both halves of its own record made each 128-B line
@@ -310,7 +309,7 @@ void radix_pass_launch(RadixScratch& sc, const uint32_t* kin, const int* vin, ui
   const int tiles = (int)div_up((unsigned)n, (unsigned)kTile);
   hipLaunchKernelGGL(radix_pass<false>, dim3(tiles), dim3(kTB), 0, st, kin, vin, kout, vout, n, pass, sc.ctl.p,
                      sc.status.p + (size_t)pass * sc.tiles_cap * kRadixDigits, nullptr, nullptr, stamps_on(), nullptr,
-                     nullptr, nullptr, nullptr);
+                     nullptr, nullptr);
   FLOAM_LAUNCH_CHECK();
 }
 
@@ -320,7 +319,7 @@ void radix_pass_payload_launch(RadixScratch& sc, const uint32_t* kin, uint32_t* 
   sc.reserve(n, st);
   const int tiles = (int)div_up((unsigned)n, (unsigned)kTile);
   hipLaunchKernelGGL(radix_pass<true>, dim3(tiles), dim3(kTB), 0, st, kin, nullptr, kout, vout, n, 0, sc.ctl.p,
-                     sc.status.p, nullptr, nullptr, stamps_on(), pin, pxyz, prec, nullptr);
+                     sc.status.p, nullptr, nullptr, stamps_on(), pin, pxyz, prec);
   FLOAM_LAUNCH_CHECK();
 }
 
@@ -334,19 +333,9 @@ void radix_sort_launch(RadixScratch& sc, uint32_t* k0, int* v0, uint32_t* k1, in
     hipLaunchKernelGGL(radix_pass<false>, dim3(tiles), dim3(kTB), 0, st, even ? k0 : k1, even ? v0 : v1,
                        even ? k1 : k0, even ? v1 : v0, n, p, sc.ctl.p,
                        sc.status.p + (size_t)p * sc.tiles_cap * kRadixDigits, gate, n_dev, stamps_on(), nullptr,
-                       nullptr, nullptr, nullptr);
+                       nullptr, nullptr);
     FLOAM_LAUNCH_CHECK();
   }
-}
-
-void radix_digit_pass_launch(RadixScratch& sc, const uint32_t* kin, const int* vin, uint32_t* kout, int* vout, int n,
-                             const uint8_t* digs, hipStream_t st, const int* gate, const int* n_dev) {
-  if (n <= 0) return;
-  sc.reserve(n, st);
-  const int tiles = (int)div_up((unsigned)n, (unsigned)kTile);
-  hipLaunchKernelGGL(radix_pass<false>, dim3(tiles), dim3(kTB), 0, st, kin, vin, kout, vout, n, 0, sc.ctl.p,
-                     sc.status.p, gate, n_dev, stamps_on(), nullptr, nullptr, nullptr, digs);
-  FLOAM_LAUNCH_CHECK();
 }
 
 }  // namespace floam

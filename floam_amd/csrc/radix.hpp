@@ -78,9 +78,4 @@ void radix_stamps_print();
 void radix_pass_launch(RadixScratch& sc, const uint32_t* kin, const int* vin, uint32_t* kout, int* vout, int n,
                        int pass, hipStream_t st);
 
-// One stable scatter pass whose digits are given per element (digs[i], e.g. a bucket: bucket.hip); the pass-0
-// histogram words of sc.ctl must hold the digits' counts
-void radix_digit_pass_launch(RadixScratch& sc, const uint32_t* kin, const int* vin, uint32_t* kout, int* vout, int n,
-                             const uint8_t* digs, hipStream_t st, const int* gate, const int* n_dev);
-
 }  // namespace floam

@@ -59,14 +59,15 @@ __global__ __launch_bounds__(kTB) void vox_keys(VoxelJobDev A, VoxelJobDev B, co
 #pragma unroll
   for (int u = 0; u < kMinMaxBlocks / 32; ++u)
     pv[u] = threadIdx.x < 6 * 32 ? partials[(job * kMinMaxBlocks + l + 32 * u) * 6 + c] : 0.f;
-  const int i0 = blockIdx.x * blockDim.x + threadIdx.x;
+  // the first element of this thread: a chunk of kTB x kAppendR per block with the bucket append, else a grid stride
+  const int i0 = blockIdx.x * blockDim.x * (bd.split ? kAppendR : 1) + threadIdx.x;
   PointRec p0;
   if (i0 < J.n0_ub) p0 = J.part0[i0];
   const unsigned long long sp_t = bucket_split_prefetch(bd.split);   // (the splitters, bucket_keys_lds)
   if (!gv) return;
   __shared__ float s_mm[6];
   __shared__ unsigned s_hist[kRadixHistWords];
-  // bd.split: the bucket sort (its bucket histogram in s_hist[0, 256)), else the four digit histograms
+  // bd.split: the bucket append's per-bucket words in s_hist (bucket_append), else the four digit histograms
   radix_hist_begin(s_hist);
   if (threadIdx.x < 6 * 32) {   // the partials' min / max per component: 32 lanes, then a 32-lane reduction
     const bool is_min = c < 3;
@@ -96,8 +97,7 @@ __global__ __launch_bounds__(kTB) void vox_keys(VoxelJobDev A, VoxelJobDev B, co
   if (job == 0 && blockIdx.x == 0 && threadIdx.x == 0) *n_dev = nA0 + nA1 + nB0 + nB1;
   __shared__ uint32_t s_spl[kBuckets];
   const bool bucket = vox_bucket_begin(bd, sp_t, job, g, mx[2], J.inv, s_spl);
-  for (int i = i0; i < n0 + n1; i += gridDim.x * blockDim.x) {
-    uint32_t key = 0xFFFFFFFFu;
+  auto key_of = [&](int i) {   // element i's sort key (0xFFFFFFFF: none / dropped)
     PointRec p;
     bool in;
     if (i == i0 && i < n0 && !J.pose) {   // the prefetched record (no transform, no crop: vox_fetch's first part)
@@ -106,26 +106,33 @@ __global__ __launch_bounds__(kTB) void vox_keys(VoxelJobDev A, VoxelJobDev B, co
     } else {
       in = vox_fetch(J, n0, n1, i, p);
     }
-    if (in) {
-      uint32_t idx;
-      if (g.overflow) {
-        idx = (uint32_t)i;   // output = input unchanged (Q9): identity order, one "voxel" per point
-      } else {
-        idx = voxel_idx(g, J.inv, p);
+    if (!in) return 0xFFFFFFFFu;
+    // index overflow: output = input unchanged (Q9): identity order, one "voxel" per point
+    const uint32_t idx = g.overflow ? (uint32_t)i : voxel_idx(g, J.inv, p);
+    return ((uint32_t)job << 31) | idx;
+  };
+  if (bucket) {   // appended to the buckets' regions: no keys array, no scatter pass
+    for (int c0 = blockIdx.x * blockDim.x * kAppendR; c0 < n0 + n1; c0 += gridDim.x * blockDim.x * kAppendR) {
+      uint32_t key[kAppendR];
+      int val[kAppendR];
+#pragma unroll
+      for (int r = 0; r < kAppendR; ++r) {
+        const int i = c0 + r * kTB + (int)threadIdx.x;
+        key[r] = i < n0 + n1 ? key_of(i) : 0xFFFFFFFFu;
+        val[r] = i;
       }
-      key = ((uint32_t)job << 31) | idx;
+      bucket_append<kAppendR>(bd, radix_ctl, s_spl, key, val, s_hist, reinterpret_cast<int*>(s_hist + kBuckets),
+                              reinterpret_cast<int*>(s_hist + 2 * kBuckets));
     }
+    return;
+  }
+  for (int i = i0; i < n0 + n1; i += gridDim.x * blockDim.x) {
+    const uint32_t key = key_of(i);
     keys[base + i] = key;
     vals[base + i] = i;
-    if (bucket) {
-      const unsigned b = bucket_of(s_spl, key);
-      bd.bkt[base + i] = (uint8_t)b;
-      atomicAdd(&s_hist[b], 1u);
-    } else {
-      radix_hist_add(s_hist, key);
-    }
+    radix_hist_add(s_hist, key);
   }
-  radix_hist_end(s_hist, radix_ctl);   // (the bucket counts are the words of digit pass 0)
+  radix_hist_end(s_hist, radix_ctl);
 }
 
 // Run heads of the sorted keys -> output slot per cloud (decoupled lookback over tiles) -> centroid of the run.
@@ -490,15 +497,14 @@ void voxel2_launch(VoxelScratch2& sc, const VoxelJob& a, const VoxelJob& b, hipS
     hipLaunchKernelGGL(vox_minmax, dim3(kMinMaxBlocks, 2), dim3(kTB), 0, st, A, B, sc.partials.p, sc.rs.ctl.p, gate);
     FLOAM_LAUNCH_CHECK();
   }
-  // few blocks: each folds its LDS digit histograms into the global ones with one atomic per non-zero bin
-  const unsigned kb = std::max(1u, std::min(div_up(std::max(umax, 1), kTB), 64u));
   // the bucket sort once its splitters are seeded; the first sort of the pipeline takes the digit passes and seeds them
   const bool use_bucket = bucket && sc.bs.seeded;
-  BucketDev bd{nullptr, nullptr, nullptr};
-  if (bucket) {
-    sc.bs.reserve(n, st);
-    bd = BucketDev{use_bucket ? sc.bs.split.p : nullptr, sc.bs.bkt.p, sc.bs.geo.p};
-  }
+  BucketDev bd{};
+  if (bucket) bd = bucket_dev(sc.bs, n, st);
+  // the digit histograms: few blocks (each folds its LDS histograms into the global ones with one atomic per non-zero
+  // bin); the bucket append: one chunk of kTB x kAppendR elements per block
+  const unsigned kb = use_bucket ? std::max(1u, std::min(div_up(std::max(umax, 1), kTB * kAppendR), 1024u))
+                                 : std::max(1u, std::min(div_up(std::max(umax, 1), kTB), 64u));
   hipLaunchKernelGGL(vox_keys, dim3(kb, 2), dim3(kTB), 0, st, A, B, sc.partials.p, sc.s.k0.p, sc.s.v0.p,
                      sc.overflow.p, sc.status.p, nstatus, sc.ticket.p, sc.rs.ctl.p, gate, sc.overflow.p + 2, bd);
   FLOAM_LAUNCH_CHECK();

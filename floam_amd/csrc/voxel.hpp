@@ -137,11 +137,14 @@ __device__ __forceinline__ VoxelGeom voxel_geom(const float (&mn)[3], const floa
 }
 
 // the voxel index of a point inside the grid's box (vox_keys; 32 bits with the cloud in bit 31)
-__device__ __forceinline__ uint32_t voxel_idx(const VoxelGeom& g, float inv, const PointRec& p) {
-  const int ijk0 = (int)(floorf(p.x * inv) - (float)g.min_b[0]);
-  const int ijk1 = (int)(floorf(p.y * inv) - (float)g.min_b[1]);
-  const int ijk2 = (int)(floorf(p.z * inv) - (float)g.min_b[2]);
+__device__ __forceinline__ uint32_t voxel_idx(const VoxelGeom& g, float inv, float x, float y, float z) {
+  const int ijk0 = (int)(floorf(x * inv) - (float)g.min_b[0]);
+  const int ijk1 = (int)(floorf(y * inv) - (float)g.min_b[1]);
+  const int ijk2 = (int)(floorf(z * inv) - (float)g.min_b[2]);
   return (uint32_t)(ijk0 * g.divb_mul[0] + ijk1 * g.divb_mul[1] + ijk2 * g.divb_mul[2]);
+}
+__device__ __forceinline__ uint32_t voxel_idx(const VoxelGeom& g, float inv, const PointRec& p) {
+  return voxel_idx(g, inv, p.x, p.y, p.z);
 }
 
 // The bounding-box stage for one cloud: min / max over the elements i = b * blockDim.x + threadIdx.x (+ k * nblocks *

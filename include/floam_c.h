@@ -350,9 +350,13 @@ floam_status floam_odom_set_shard_callback(floam_odom* o, int rank, int world, f
  *   opened) or as world device pointers; exactly one of the two.  world <= 8.  It starts a fresh exchange sequence
  *   (the rank's exchange counter reset, its buffer zeroed), so every rank calls it — also when re-peering — and the
  *   ranks then meet at a barrier before their next update; from there on all ranks issue the same sequence of
- *   updates concurrently (one process per rank: the handles of one process share a stream, so ranks in one process
- *   would wait on each other).  FLOAM_ERR_UNSUPPORTED when uncached device memory (which the cross-GPU polls need)
- *   cannot be allocated: use floam_odom_set_shard (RCCL) instead. */
+ *   updates concurrently.  The ranks call it together (one process per rank, or one host thread per rank on
+ *   different GPUs): it probes every peer mapping — each rank publishes a word in its own buffer and reads every
+ *   rank's — and returns FLOAM_ERR_COMM when a rank does not answer within 2 s (the xGMI mapping does not work: use
+ *   floam_odom_set_shard, RCCL, instead), so a bad node costs seconds, not the first solve's ~20-s timeout.  Handles
+ *   of one process on the SAME GPU cannot be peers: they share that GPU's library stream, so one rank's solve would
+ *   wait for a rank queued behind it.  FLOAM_ERR_UNSUPPORTED when uncached device memory (which the cross-GPU polls
+ *   need) cannot be allocated.  On any error the handle is left unsharded (world 1), never half-configured. */
 floam_status floam_odom_shard_exchange(floam_odom* o, void* ipc_handle_64, void** dev_ptr);
 floam_status floam_odom_set_shard_peers(floam_odom* o, int rank, int world, const void* ipc_handles,
                                         void* const* dev_ptrs);

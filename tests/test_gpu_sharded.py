@@ -345,3 +345,59 @@ def test_peer_five_ranks_match_unsharded(floam_gpu):
         dt = np.linalg.norm(res[0][0][k][4:] - ref[k][4:])
         dr = 2 * math.acos(min(1.0, abs(float(np.dot(res[0][0][k][:4], ref[k][:4])))))
         assert dt < 1e-9 and dr < 1e-9, (k, dt, dr)
+
+
+def test_peer_eight_ranks_match_unsharded(floam_gpu, oracle_lib, prefilled_map):
+    """world = kMaxShardRanks = 8, the world the driver's 8-GPU run uses, as eight processes on
+    the one GPU (IPC-mapped exchange buffers; every rank's set_shard_peers probes the seven others' mappings first).
+    C1 (5 scans): poses identical on all ranks and within 1e-9 of the unsharded run; C4 (128 rings, 500k prefill):
+    identical on all ranks, map sizes equal to the oracle's and poses within 1e-6 of it."""
+    ref = _run(0, 1, _free_port(), None)
+    res = _peer_ranks("c1", NSCAN, world=8)
+    for r in range(1, 8):
+        assert np.array_equal(res[0][0], res[r][0]), r
+    for k in range(NSCAN):
+        dt = np.linalg.norm(res[0][0][k][4:] - ref[k][4:])
+        dr = 2 * math.acos(min(1.0, abs(float(np.dot(res[0][0][k][:4], ref[k][:4])))))
+        assert dt < 1e-9 and dr < 1e-9, (k, dt, dr)
+    mapE, mapS = prefilled_map("c4")
+    oref, ref_sizes = _c4_oracle(oracle_lib, mapE, mapS)
+    res = _peer_ranks("c4", C4_SCANS, maps=(mapE, mapS), world=8)
+    for r in range(1, 8):
+        assert np.array_equal(res[0][0], res[r][0]), r
+        assert res[r][1] == ref_sizes, (r, res[r][1], ref_sizes)
+    _assert_close_to_oracle(res[0][0], oref, "8-rank peer shard")
+
+
+def _probe_lonely_rank(q):
+    """One rank of a two-rank peer group whose other rank never calls set_shard_peers (its mapping never answers)."""
+    import floam_amd
+    p = floam_amd.LidarParams(num_lines=16, scan_period=0.1, max_distance=90.0, min_distance=0.5)
+    odo = floam_amd.OdomEstimationClass(device=0)
+    odo.init(p, 0.1, "Cauchy")
+    other = floam_amd.OdomEstimationClass(device=0)   # a second handle: its buffer exists but never answers
+    other.init(p, 0.1, "Cauchy")
+    _, mine = odo.shard_exchange()
+    _, theirs = other.shard_exchange()
+    import time
+    t0 = time.time()
+    try:
+        odo.set_shard_peers(0, 2, ptrs=[mine, theirs])
+        q.put(("no error", time.time() - t0))
+    except floam_amd.FloamError as e:
+        q.put((str(e), time.time() - t0))
+
+
+def test_peer_probe_fails_fast(floam_gpu):
+    """a peer mapping that never answers fails floam_odom_set_shard_peers in seconds with
+    FLOAM_ERR_COMM (bench.py then takes the RCCL form), instead of the first solve's ~20-s hand-off timeout."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    pr = ctx.Process(target=_probe_lonely_rank, args=(q,))
+    pr.start()
+    msg, dt = q.get(timeout=120)
+    pr.join(timeout=60)
+    assert pr.exitcode == 0
+    assert "probe" in msg and "rank(s) 1" in msg, msg
+    assert 1.5 < dt < 10.0, dt

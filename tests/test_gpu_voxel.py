@@ -105,3 +105,22 @@ def test_voxel_run_lengths(floam_gpu, oracle_lib):
     first = _check(floam_gpu, oracle_lib, pts, 0.1)
     second = _check(floam_gpu, oracle_lib, pts, 0.1)
     assert first.shape[0] <= 12 * len(lens) and second.shape == first.shape
+
+
+def test_voxel_stale_splitters_overflow(floam_gpu, oracle_lib):
+    """bucket.hpp bucket_append: a bucket's region holds twice the mean bucket; appends past it go to the overflow
+    list, which the bucket's block gathers back (bucket.hip bucket_source).  Splitters seeded by a spread-out cloud,
+    then clouds whose points crowd into a few of those buckets: one bucket past its region but within the in-LDS
+    network (3000 points in a 0.3-m cube), one past the network too (20000 points of a thin slab: streamed, sorted by
+    (key, value) through global memory), then the spread-out cloud again with the crowded splitters."""
+    rng = np.random.default_rng(23)
+    spread = _cloud(rng.uniform(-30, 30, (40000, 3)).astype(np.float32))
+    _check(floam_gpu, oracle_lib, spread, 0.1)
+    _check(floam_gpu, oracle_lib, spread, 0.1)   # (sorted with its own splitters: balanced)
+    cube = np.concatenate([rng.uniform(2.0, 2.3, (3000, 3)), rng.uniform(-30, 30, (500, 3))])
+    _check(floam_gpu, oracle_lib, _cloud(cube[rng.permutation(len(cube))].astype(np.float32)), 0.1)
+    _check(floam_gpu, oracle_lib, spread, 0.1)
+    slab = np.stack([rng.uniform(4.0, 4.6, 20000), rng.uniform(4.0, 4.2, 20000), rng.uniform(4.0, 4.1, 20000)], 1)
+    slab = np.concatenate([slab, rng.uniform(-30, 30, (2000, 3))])
+    _check(floam_gpu, oracle_lib, _cloud(slab[rng.permutation(len(slab))].astype(np.float32)), 0.1)
+    _check(floam_gpu, oracle_lib, spread, 0.1)

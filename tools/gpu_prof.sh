@@ -1,12 +1,13 @@
 #!/bin/bash
 # Bench + rocprofv3 kernel-trace stats + separate FETCH_SIZE / WRITE_SIZE passes of the same bench command (no
-# tests).  Usage (GPU box, repo root): bash tools/gpu_prof.sh TAG [bench args...]; then on the host
-# python tools/prof_summary.py gpurun_out/TAG TAG --config <config>
+# tests; the device-code hash of the tree into code_hash.txt).  Usage (GPU box, repo root): bash tools/gpu_prof.sh TAG
+# [bench args...]; then on the host python tools/prof_summary.py gpurun_out/TAG TAG --config <config> --steps <steps>
 set -o pipefail
 TAG=${1:-prof}; shift || true
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+python -c "import bench; print(bench.code_hash())" > $OUT/code_hash.txt
 timeout -k 10 400 python bench.py "$@" > $OUT/bench.json 2> $OUT/bench.err || { tail -30 $OUT/bench.err; exit 1; }
 cut -c1-400 $OUT/bench.json
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_trace -o run -- \

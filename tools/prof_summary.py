@@ -16,7 +16,8 @@ Outputs:
   profiles/<tag>/kernel_stats.csv   per-kernel calls / total / avg / min / max over the timed region
   profiles/<tag>/kernel_stats_whole_run.csv   the rocprofv3 --stats summary, verbatim (prefill, replay included)
   profiles/<tag>/summary.md         per-kernel table (calls per scan, avg us, HBM bytes per launch) + bench line
-  profiles/<tag>/hbm_traffic.json   per-kernel PMC bytes per launch (timed region), read by bench.py's roofline
+  profiles/<tag>/hbm_traffic.json   per-kernel PMC bytes per launch (timed region), read by bench.py's roofline,
+                                    with the profiled tree's device-code hash (code_hash.txt), steps and a timestamp
 
 HBM bytes per launch follow /opt/skills/guides/MI355X_MICROARCH.md § HBM: FETCH_SIZE and WRITE_SIZE are KiB;
 on gfx950 FETCH_SIZE reports half the bytes of a wide (16 B/lane) coalesced read, so it is doubled; WRITE_SIZE
@@ -26,6 +27,7 @@ pass).
 import argparse
 import collections
 import csv
+import datetime
 import json
 import os
 import shutil
@@ -72,13 +74,19 @@ def main():
     ap.add_argument("run", help="gpurun_out/<tag> directory")
     ap.add_argument("tag")
     ap.add_argument("--config", default="c3", help="bench config the profiled run used (bench.py keys traffic by it)")
-    ap.add_argument("--steps", type=int, default=60, help="timed scans of the profiled bench run")
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed scans of the profiled bench run (default: the session's bench.json steps, else 60)")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles"))
     args = ap.parse_args()
     out = os.path.join(args.out, args.tag)
     os.makedirs(out, exist_ok=True)
     shutil.copy(os.path.join(args.run, "prof_trace", "run_kernel_stats.csv"),
                 os.path.join(out, "kernel_stats_whole_run.csv"))
+    bpath = os.path.join(args.run, "bench.json")
+    if args.steps is None:
+        args.steps = 60
+        if os.path.exists(bpath) and os.path.getsize(bpath):
+            args.steps = int(json.loads(open(bpath).read().strip().splitlines()[-1]).get("steps", 60))
     rows, marked, span = trace_region(os.path.join(args.run, "prof_trace", "run_kernel_trace.csv"))
     per = collections.defaultdict(list)
     for r in rows:
@@ -124,7 +132,12 @@ def main():
     if bench:
         lines += ["", "## bench line of the same session (un-profiled run)", "", "```json", json.dumps(bench), "```"]
     open(os.path.join(out, "summary.md"), "w").write("\n".join(lines) + "\n")
-    json.dump({"source": f"profiles/{args.tag}", "config": args.config,
+    chash = None
+    hpath = os.path.join(args.run, "code_hash.txt")
+    if os.path.exists(hpath):
+        chash = open(hpath).read().strip() or None
+    json.dump({"source": f"profiles/{args.tag}", "config": args.config, "steps": args.steps, "code_hash": chash,
+               "created": datetime.datetime.now(datetime.timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ"),
                "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate runs; FETCH_SIZE x2 (gfx950), KiB->B; "
                          "average over the dispatches of the timed region (between the bench's marker dispatches)",
                "kernels": traffic},
