@@ -19,11 +19,18 @@ from floam_amd import _ffi
 OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
 
 
-@pytest.mark.skipif(not os.path.exists(OBJDUMP), reason="llvm-objdump (ROCm) not installed")
+import re
+
+NARROW = re.compile(r"s_and_b64 exec, exec, (vcc|s\[)")   # exec narrowed without saving the mask
+HIPCC = "/opt/rocm/bin/hipcc"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
 @pytest.mark.parametrize("lib", [_ffi.PRODUCT_LIB_PATH, _ffi.DIAG_LIB_PATH], ids=["product", "diag"])
 def test_no_unsaved_exec_narrowing(tmp_path, lib):
-    if not os.path.exists(lib):
-        pytest.skip(f"{os.path.basename(lib)} not built")
+    # no skip: a library that cannot be checked (not built, no ROCm disassembler) fails the suite (VERDICT r05 Weak 9)
+    assert os.path.exists(OBJDUMP), "llvm-objdump (ROCm) is needed to check the code objects"
+    assert os.path.exists(lib), f"{os.path.basename(lib)} not built (floam_amd/csrc: make)"
     name = os.path.basename(lib)
     local = tmp_path / name
     shutil.copy(lib, local)
@@ -35,5 +42,22 @@ def test_no_unsaved_exec_narrowing(tmp_path, lib):
     for o in objs:
         dis = subprocess.run([OBJDUMP, "-d", "--mcpu=gfx950", o], check=True, capture_output=True, text=True).stdout
         assert "s_and_saveexec_b64" in dis or "v_" in dis   # (a real disassembly)
-        bad += [ln.strip() for ln in dis.splitlines() if "s_and_b64 exec, exec, s[" in ln]
+        bad += [ln.strip() for ln in dis.splitlines() if NARROW.search(ln)]
     assert not bad, f"{len(bad)} exec narrowings without a saved mask, e.g. {bad[:3]}"
+
+
+def test_endcf_reproducer(tmp_path):
+    """tools/micro/endcf_repro.hip: the nested-if shape of lm_solve's write-back.  The default LLVM pipeline narrows
+    exec without saving the mask there (the compiler's transformation: the source has no divergence hazard); the
+    Makefile's -amdgpu-remove-redundant-endcf=false keeps the inner if's own save / restore."""
+    assert os.path.exists(HIPCC)
+    src = os.path.join(ROOT, "tools", "micro", "endcf_repro.hip")
+    counts = {}
+    for name, extra in (("default", []), ("flag", ["-mllvm", "-amdgpu-remove-redundant-endcf=false"])):
+        out = tmp_path / f"{name}.s"
+        subprocess.run([HIPCC, "-O3", "--offload-arch=gfx950", "--offload-device-only", "-S", *extra, src, "-o",
+                        str(out)], check=True, capture_output=True)
+        asm = out.read_text()
+        counts[name] = (len(NARROW.findall(asm)), asm.count("s_and_saveexec_b64"))
+    assert counts["default"][0] >= 1, counts   # the unsaved narrowing appears without the flag
+    assert counts["flag"][0] == 0 and counts["flag"][1] >= 2, counts   # both ifs save and restore with it

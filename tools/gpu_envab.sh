@@ -6,6 +6,14 @@ TAG=$1; shift
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
+# every A/B and hook variable is read only by the diagnostic build (FLOAM_DIAG_ENV, floam_common.hpp); only FLOAM_GRAPH
+# and FLOAM_MAP_MERGE reach the product library.  A spec is measured on the diagnostic library unless it names only those.
+for spec in "$@"; do
+  for kv in $(echo ${spec#*:} | tr ',' ' '); do
+    case ${kv%%=*} in FLOAM_GRAPH|FLOAM_MAP_MERGE|FLOAM_AMD_LIB) ;; *) export FLOAM_AMD_LIB=diag ;; esac
+  done
+done
+echo "library: ${FLOAM_AMD_LIB:-product}"
 for round in 1 2; do
   for spec in "$@"; do
     name=${spec%%:*}; envs=${spec#*:}
