@@ -608,14 +608,19 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
   const bool peer = o->peer && o->world > 1;   // peer sharding: the resident solve exchanges the ranks' sums itself
   if (peer && !lm_resident(o, mode))
     throw Error(FLOAM_ERR_UNSUPPORTED, "peer sharding needs the resident solve (its grid does not fit the device)");
+  // (diagnostic, FLOAM_SHARD_SOLO=N on an unsharded handle: this GPU runs only rank 0's 1/N of the correspondence
+  // queries and solves on them alone, no exchange — the per-rank compute of an N-rank sharded run)
+  static const int solo = FLOAM_DIAG_ENV("FLOAM_SHARD_SOLO") ? std::atoi(FLOAM_DIAG_ENV("FLOAM_SHARD_SOLO")) : 0;
+  const int qrank = o->rank, qworld = (solo > 1 && o->world == 1) ? std::min(solo, kMaxShardRanks) : o->world;
   for (int it = 0; it < o->optimization_count; ++it) {
+    bool split = false;
     {
       ProfScope ps(ctx, "knn", FLOAM_PROF_KNN);   // the correspondence pass: search + geometry
       {
         static const bool stages = FLOAM_DIAG_ENV("FLOAM_KNN_STAGES") != nullptr;
         if (stages && (ctx.profile & FLOAM_PROF_KNN_BYTES))   // (replay only, before the timed scope)
           knn_stage_launch(o->lm.p, it == 0 ? x0_dev : nullptr, qe, o->gE, o->ce, qs, o->gS, o->cs, o->mapE.count.p,
-                           o->mapS.count.p, o->rank, o->world, o->knn_evict, st);
+                           o->mapS.count.p, qrank, qworld, o->knn_evict, st);
         ProfScope ps1(ctx, "knn_search_bracket", FLOAM_PROF_KNN_DETAIL);   // (events around the launch)
         // "knn_search": HIP events set by the launch itself to the kernel's start and end (rocprofv3's duration)
         hipEvent_t k0 = nullptr, k1 = nullptr;
@@ -624,16 +629,20 @@ void odom_issue(floam_odom* o, DeviceCtx& ctx, const floam_cloud* edge, const fl
           k1 = ctx.get_event();
         }
         // (also starts the solve: LM state reset, the first solve at the prediction)
-        knn_launch(o->lm.p, it == 0 ? x0_dev : nullptr, qe, o->gE, o->ce, qs, o->gS, o->cs, o->mapE.count.p,
-                   o->mapS.count.p, o->rank, o->world, st, k0, k1);
+        split = knn_geom_split_launch(o->lm.p, it == 0 ? x0_dev : nullptr, qe, o->gE, o->ce, qs, o->gS, o->cs,
+                                      o->mapE.count.p, o->mapS.count.p, qrank, qworld, gram, o->fp32_geom, o->lmb,
+                                      st, k0, k1);   // (diagnostic prototype; false in the product)
+        if (!split)
+          knn_launch(o->lm.p, it == 0 ? x0_dev : nullptr, qe, o->gE, o->ce, qs, o->gS, o->cs, o->mapE.count.p,
+                     o->mapS.count.p, qrank, qworld, st, k0, k1);
         if (k0) ctx.pending.push_back(PendingTiming{"knn_search", k0, k1, 0.0});
       }
       ProfScope ps2(ctx, "knn_geometry", FLOAM_PROF_KNN_DETAIL);
-      geom_launch(o->lm.p, qe, o->ce, qs, o->cs, gram, o->fp32_geom, o->lmb, st);
+      if (!split) geom_launch(o->lm.p, qe, o->ce, qs, o->cs, gram, o->fp32_geom, o->lmb, st);
     }
     if (ctx.profile & FLOAM_PROF_KNN_BYTES) {   // replay only: algorithmic bytes of the two launches above
-      knn_traffic_launch(o->lm.p, qe, o->gE, o->ce, o->rank, o->world, o->traffic_set, o->prof_bytes.p + 0, st);
-      knn_traffic_launch(o->lm.p, qs, o->gS, o->cs, o->rank, o->world, o->traffic_set, o->prof_bytes.p + 1, st);
+      knn_traffic_launch(o->lm.p, qe, o->gE, o->ce, qrank, qworld, o->traffic_set, o->prof_bytes.p + 0, st);
+      knn_traffic_launch(o->lm.p, qs, o->gS, o->cs, qrank, qworld, o->traffic_set, o->prof_bytes.p + 1, st);
     }
     // ceres::Solve: iteration zero + at most max_num_iterations = 4 candidates (odomEstimationClass.cpp:102)
     if ((!sharded || peer) && lm_resident(o, mode)) {

@@ -66,8 +66,14 @@ __global__ __launch_bounds__(kTB) void mm_keys(VoxelJobDev A, VoxelJobDev B, con
   const VoxelJobDev& J0 = job ? B : A;
   // this thread's first element: a chunk of kTB x kAppendR per block with the bucket append, else a grid stride
   const int e0 = blockIdx.x * blockDim.x * (bd.split ? kAppendR : 1) + threadIdx.x;
-  PointRec sp0;
-  if (e0 < J0.n1_ub) sp0 = J0.part1[e0];
+  // (the bucket append: all kAppendR scan records of this thread's first chunk, element e0 + r kTB)
+  float4 sp[kAppendR];
+#pragma unroll
+  for (int r = 0; r < kAppendR; ++r) {
+    const int e = e0 + r * kTB;
+    sp[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if ((r == 0 || bd.split) && e < J0.n1_ub) sp[r] = *reinterpret_cast<const float4*>(&J0.part1[e].x);
+  }
   double pose0[7];
 #pragma unroll
   for (int k = 0; k < 7; ++k) pose0[k] = J0.pose[k];
@@ -145,13 +151,14 @@ __global__ __launch_bounds__(kTB) void mm_keys(VoxelJobDev A, VoxelJobDev B, con
   __shared__ uint32_t s_spl[kBuckets];
   const bool bucket = vox_bucket_begin(bd, sp_t, job, G, job ? s_mm[1][5] : s_mm[0][5], J.inv, s_spl);
   int kept = 0;
-  auto key_of = [&](int e) {   // sort key of element e of the job's set (0xFFFFFFFF: cropped)
+  // sort key of element e of the job's set (0xFFFFFFFF: cropped); pre: its scan record prefetched (the merge path)
+  auto key_of = [&](int e, bool pre, float4 spr) {
     const int i = start + e;   // index into the job's [map ; scan] concatenation
     float4 q;   // (x, y, z, intensity: no PointRec temporary, which stays a private array in this kernel)
     bool in;
-    if (!full && e == e0) {   // the prefetched scan record: vox_fetch's transform and CropBox, on registers
+    if (!full && pre) {   // the prefetched scan record: vox_fetch's transform and CropBox, on registers
       float x, y, z;
-      associate_to_map(pose0, sp0.x, sp0.y, sp0.z, x, y, z);
+      associate_to_map(pose0, spr.x, spr.y, spr.z, x, y, z);
       q = make_float4(x, y, z, 0.f);
       const float mnx = (float)(pose0[4] - 100), mny = (float)(pose0[5] - 100), mnz = (float)(pose0[6] - 100);
       const float mxx = (float)(pose0[4] + 100), mxy = (float)(pose0[5] + 100), mxz = (float)(pose0[6] + 100);
@@ -170,7 +177,7 @@ __global__ __launch_bounds__(kTB) void mm_keys(VoxelJobDev A, VoxelJobDev B, con
 #pragma unroll
       for (int r = 0; r < kAppendR; ++r) {
         const int e = c0 + r * kTB + (int)threadIdx.x;
-        key[r] = e < count ? key_of(e) : 0xFFFFFFFFu;
+        key[r] = e < count ? key_of(e, e == e0 + r * kTB && e < J0.n1_ub, sp[r]) : 0xFFFFFFFFu;
         val[r] = start + e;
       }
       bucket_append<kAppendR>(bd, radix_ctl, s_spl, key, val, s_hist, reinterpret_cast<int*>(s_hist + kBuckets),
@@ -180,7 +187,7 @@ __global__ __launch_bounds__(kTB) void mm_keys(VoxelJobDev A, VoxelJobDev B, con
     __syncthreads();
   } else {
     for (int e = e0; e < count; e += gridDim.x * blockDim.x) {
-      const uint32_t key = key_of(e);
+      const uint32_t key = key_of(e, e == e0 && e < J0.n1_ub, sp[0]);
       keys[base + e] = key;
       vals[base + e] = start + e;
       radix_hist_add(s_hist, key);
@@ -753,7 +760,9 @@ void map_merge_launch(VoxelScratch2& vs, MapMergeScratch& ms, const VoxelJob& a,
   const VoxelJobDev A = to_dev(a, 0);
   const VoxelJobDev B = to_dev(b, a.n0_ub + a.n1_ub);
   const int nA = a.n0_ub + a.n1_ub, nB = b.n0_ub + b.n1_ub, n = std::max(nA + nB, 1);
-  const int tile = kTB * kMergePer;
+  // (diagnostic, FLOAM_MM_PER=2: 512-element tiles — twice the tile edges for the tests' runs to cross)
+  static const int per = FLOAM_DIAG_ENV("FLOAM_MM_PER") && std::atoi(FLOAM_DIAG_ENV("FLOAM_MM_PER")) == 2 ? 2 : kMergePer;
+  const int tile = kTB * per;
   const int tilesA = std::max(1, (int)div_up(std::max(nA, 1), tile));
   const int tilesB = std::max(1, (int)div_up(std::max(nB, 1), tile));
   ms.reserve(std::max(tilesA, tilesB), st);
@@ -784,6 +793,12 @@ void map_merge_launch(VoxelScratch2& vs, MapMergeScratch& ms, const VoxelJob& a,
   const bool wb = prof_wb_enabled();   // (diagnostic: the merge's own write bytes, profwb.hpp)
   static const int stamps = FLOAM_DIAG_ENV("FLOAM_MM_STAMPS") ? 1 : 0;
   if (wb) prof_l2_writeback(st);
+#ifdef FLOAM_DIAG
+  if (per == 2)
+    hipLaunchKernelGGL(mm_merge<2>, dim3(tilesA + tilesB), dim3(kTB), 0, st, A, B, ka, kb, vs.s.k0.p, vs.s.v0.p,
+                       ms.ctl.p, ms.status.p, ms.tiles_cap, tilesA, vs.rs.ctl.p, gate, seq, violate_mod, stamps);
+  else
+#endif
   hipLaunchKernelGGL(mm_merge<kMergePer>, dim3(tilesA + tilesB), dim3(kTB), 0, st, A, B, ka, kb, vs.s.k0.p, vs.s.v0.p,
                        ms.ctl.p, ms.status.p, ms.tiles_cap, tilesA, vs.rs.ctl.p, gate, seq, violate_mod,
                        stamps);

@@ -883,17 +883,298 @@ __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArg
 // Edge and surf kNN in one launch: blocks [0, nbE) run edge groups, the others surf groups.  The launch also starts
 // the solve (lm_init folded in): block 0 resets the LM state and, for the first solve of an update, stores the
 // prediction x0 that every block uses for its transforms (the others never read st->x in that case).
-template <int G, int U, int W, int NB, int STOP = 0>
-__global__ __launch_bounds__(kTB, W) void knn_kernel(LMState* __restrict__ st, const double* __restrict__ x0_dev,
-                                                  CorrArgs E, CorrArgs S, int nbE,
-                                                  const int* __restrict__ d_me, const int* __restrict__ d_ms,
-                                                  int rank, int world) {
+// (the search of logical block blk: knn_kernel's, and the search role of the role-split prototype below)
+template <int G, int U, int NB, int STOP = 0>
+__device__ __forceinline__ void knn_block(LMState* __restrict__ st, const double* __restrict__ x0_dev,
+                                          const CorrArgs& E, const CorrArgs& S, int nbE, int nblocks, int blk,
+                                          const int* __restrict__ d_me, const int* __restrict__ d_ms, int rank,
+                                          int world) {
   __shared__ int s_pre[kTB / G][kMaxStencil + 1];
   __shared__ int s_start[kTB / G][kMaxStencil];
   __shared__ int s_cc[kTB / G][8 * 9];
   const int lane = threadIdx.x & (G - 1);
   const int g = threadIdx.x / G;
   double pose[7];   // wave-uniform: kept in SGPRs (readfirstlane), not in 14 VGPRs of every lane
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    const long long b = __double_as_longlong(x0_dev ? x0_dev[k] : st->x[k]);
+    const int lo = __builtin_amdgcn_readfirstlane((int)b), hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+    pose[k] = __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+  }
+  if (blk == 0 && threadIdx.x == 0) {
+    X7 xs;
+    xs.set = x0_dev ? 1 : 0;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) xs.v[k] = pose[k];
+    lm_reset(st, xs);
+  }
+  const bool gate = *d_me > 10 && *d_ms > 50;   // map-size gate (odomEstimationClass.cpp:77)
+  // XCD-aware placement: the blocks that hold queries are renumbered so that the blocks sharing an XCD (physical
+  // index mod 8 under round-robin dispatch) take consecutive query ranges.  The queries are in voxel order, so each
+  // XCD then works on a compact slab of the scene and its L2 holds that slab's map cells instead of all of them.
+  const bool edge = blk < nbE;
+  const CorrArgs& A = edge ? E : S;
+  const int nb = edge ? nbE : nblocks - nbE;
+  int p = edge ? blk : blk - nbE;
+  const int nq = min(*A.d_n, A.n_ub);
+  const int nact = min(nb, (int)(((long long)nq * G + kTB - 1) / kTB));
+  if (p < nact) p = xcd_block(p, nact);
+  knn_group<G, U, NB, STOP>(pose, A, (p * kTB + (int)threadIdx.x) / G, nb * (kTB / G), lane, gate, rank, world,
+                            s_pre[g], s_start[g], s_cc[g]);
+}
+
+template <int G, int U, int W, int NB, int STOP = 0>
+__global__ __launch_bounds__(kTB, W) void knn_kernel(LMState* __restrict__ st, const double* __restrict__ x0_dev,
+                                                  CorrArgs E, CorrArgs S, int nbE,
+                                                  const int* __restrict__ d_me, const int* __restrict__ d_ms,
+                                                  int rank, int world) {
+  knn_block<G, U, NB, STOP>(st, x0_dev, E, S, nbE, (int)gridDim.x, (int)blockIdx.x, d_me, d_ms, rank, world);
+}
+
+// ----------------------------------------------------------------------------------- LDS-staged stage 1
+// The north star's "LDS-staged spatial-hash grid", re-measured against the search above (diagnostic build:
+// FLOAM_KNN_LDS=1).  A block's 16 queries (one per 16-lane group, as knn_kernel) are consecutive in voxel order, so
+// their 3 x 3 x 3 fine blocks overlap: the block takes the bounding box of the 16 fine blocks (fine cells, <= kLdsCells),
+// probes the coarse entries that cover it once (one thread per coarse cell, <= kLdsCoarse), lays the box's fine cells
+// out in LDS order (a block scan of their counts) and copies their points into LDS with one flattened, coalesced load
+// round (<= kLdsPts points); each group then scans its query's 27 fine cells from LDS — the same candidates, float
+// distances and (distance, map index) keys as the global scan, so the same top-5.  Stage 2 and the outputs are the
+// search's own.  A block whose box or points do not fit takes the global stage 1 (fine_block_ranges + stencil_scan).
+constexpr int kLdsCells = 512;
+constexpr int kLdsCoarse = 256;
+constexpr int kLdsPts = 1536;
+
+template <int G, int U>
+__device__ __forceinline__ void knn_group_lds(const double (&pose)[7], const CorrArgs& A, int gbase, int ngroups,
+                                              int lane, int g, bool gate, int rank, int world, int* __restrict__ s_pre,
+                                              int* __restrict__ s_start, int* __restrict__ s_cc) {
+  constexpr int NB = 3;
+  __shared__ int s_box[6];                 // fine-corner min x, y, z, max x, y, z of the active queries
+  __shared__ int s_cs[kLdsCoarse][9];      // coarse entries over the box: start, 8 sub-cell counts
+  __shared__ int s_fs[kLdsCells];          // fine cells of the box: start in the cell-grouped map
+  __shared__ int s_fo[kLdsCells + 1];      // ... and their offset in s_pts (exclusive scan of the counts)
+  __shared__ float4 s_pts[kLdsPts];
+  __shared__ int s_ws[kTB / 64];
+  const int t = (int)threadIdx.x;
+  const int n = min(*A.d_n, A.n_ub);
+  const int lo = (int)(((long long)n * rank) / world), hi = (int)(((long long)n * (rank + 1)) / world);
+  for (int i0 = 0; i0 < n; i0 += ngroups) {   // block-uniform trip count (every group of the block in each round)
+    const int i = i0 + gbase + g;
+    const bool act = i < n && i >= lo && i < hi && gate;
+    float wx = 0.f, wy = 0.f, wz = 0.f;
+    int lx = 0, ly = 0, lz = 0;
+    if (act) {
+      const float4 pq = *reinterpret_cast<const float4*>(&A.q[i].x);
+      associate_to_map(pose, pq.x, pq.y, pq.z, wx, wy, wz);   // pointAssociateToMap (:126-135)
+      int qx, qy, qz;
+      fine_cell(wx, wy, wz, qx, qy, qz);
+      knn_block_corner(NB, wx, wy, wz, qx, qy, qz, lx, ly, lz);
+    }
+    // the block's box of fine blocks
+    if (t < 6) s_box[t] = t < 3 ? INT_MAX : INT_MIN;
+    __syncthreads();
+    if (act && lane == 0) {
+      atomicMin(&s_box[0], lx); atomicMin(&s_box[1], ly); atomicMin(&s_box[2], lz);
+      atomicMax(&s_box[3], lx); atomicMax(&s_box[4], ly); atomicMax(&s_box[5], lz);
+    }
+    __syncthreads();
+    const int bx0 = s_box[0], by0 = s_box[1], bz0 = s_box[2];
+    const bool any = bx0 != INT_MAX;
+    const int DX = any ? s_box[3] - bx0 + NB : 0, DY = any ? s_box[4] - by0 + NB : 0, DZ = any ? s_box[5] - bz0 + NB : 0;
+    const long long nfc = (long long)DX * DY * DZ;
+    const int cx0 = bx0 >> 1, cy0 = by0 >> 1, cz0 = bz0 >> 1;   // coarse box (floor halves)
+    const int CX = any ? ((bx0 + DX - 1) >> 1) - cx0 + 1 : 0, CY = any ? ((by0 + DY - 1) >> 1) - cy0 + 1 : 0,
+              CZ = any ? ((bz0 + DZ - 1) >> 1) - cz0 + 1 : 0;
+    const long long ncc = (long long)CX * CY * CZ;
+    bool staged = any && nfc <= kLdsCells && ncc <= kLdsCoarse;   // (block-uniform)
+    if (staged) {
+      if (t < ncc) {   // one coarse probe per thread (head + sub counts: 48 B of the 64-B entry)
+        const int ax = t % CX, ay = (t / CX) % CY, az = t / (CX * CY);
+        const unsigned long long key = cell_key(cx0 + ax, cy0 + ay, cz0 + az);
+        unsigned slot = coarse_slot(key, A.bits);
+        const int4* e = reinterpret_cast<const int4*>(&A.coarse[slot]);
+        int4 h = e[0], s0 = e[1], s1 = e[2];
+        unsigned long long k = ((unsigned long long)(unsigned)h.y << 32) | (unsigned)h.x;
+        while (k != key && k != kEmptyKey) {   // collision chain (rare)
+          slot = (slot + 1) & A.mask;
+          e = reinterpret_cast<const int4*>(&A.coarse[slot]);
+          h = e[0]; s0 = e[1]; s1 = e[2];
+          k = ((unsigned long long)(unsigned)h.y << 32) | (unsigned)h.x;
+        }
+        const bool hit = k == key;
+        int* cc = s_cs[t];
+        cc[0] = hit ? h.z : 0;
+        cc[1] = hit ? s0.x : 0; cc[2] = hit ? s0.y : 0; cc[3] = hit ? s0.z : 0; cc[4] = hit ? s0.w : 0;
+        cc[5] = hit ? s1.x : 0; cc[6] = hit ? s1.y : 0; cc[7] = hit ? s1.z : 0; cc[8] = hit ? s1.w : 0;
+      }
+      __syncthreads();
+      // fine cells c = 2 t, 2 t + 1 (box order, x fastest): start and count, then the block's exclusive scan
+      int cnt2[2] = {0, 0};
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int c = 2 * t + u;
+        if (c < nfc) {
+          const int fx = bx0 + c % DX, fy = by0 + (c / DX) % DY, fz = bz0 + c / (DX * DY);
+          const int ci = ((fx >> 1) - cx0) + CX * (((fy >> 1) - cy0) + CY * ((fz >> 1) - cz0));
+          const int sub = (fx & 1) | ((fy & 1) << 1) | ((fz & 1) << 2);
+          const int* cc = s_cs[ci];
+          int start = cc[0];
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            if (k < sub) start += cc[1 + k];
+          s_fs[c] = start;
+          cnt2[u] = cc[1 + sub];
+        }
+      }
+      const int mine = cnt2[0] + cnt2[1];
+      const int incl = wave_incl_scan(mine);
+      if ((t & 63) == 63) s_ws[t >> 6] = incl;
+      __syncthreads();
+      int wb = 0, tot = 0;
+#pragma unroll
+      for (int k = 0; k < kTB / 64; ++k) {
+        if (k < (t >> 6)) wb += s_ws[k];
+        tot += s_ws[k];
+      }
+      const int ex = wb + incl - mine;
+      if (2 * t < nfc) s_fo[2 * t] = ex;
+      if (2 * t + 1 < nfc) s_fo[2 * t + 1] = ex + cnt2[0];
+      if (t == 0) s_fo[nfc] = tot;
+      staged = tot <= kLdsPts;   // (block-uniform)
+      __syncthreads();
+      if (staged) {   // the box's points into LDS: element q of the flattened list, cell by binary search
+        constexpr int kR = (kLdsPts + kTB - 1) / kTB;
+        int src[kR];   // every element's source first (LDS binary searches, fixed 9 steps), then all loads in flight
+#pragma unroll
+        for (int r = 0; r < kR; ++r) {
+          const int q = r * kTB + t;
+          int a = 0;   // last cell with s_fo[cell] <= q
+#pragma unroll
+          for (int step = kLdsCells / 2; step > 0; step >>= 1)
+            if (a + step < nfc && s_fo[a + step] <= q) a += step;
+          src[r] = q < tot ? s_fs[a] + (q - s_fo[a]) : -1;
+        }
+        float4 m[kR];
+#pragma unroll
+        for (int r = 0; r < kR; ++r) m[r] = src[r] >= 0 ? A.gpts[src[r]] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int r = 0; r < kR; ++r)
+          if (r * kTB + t < tot) s_pts[r * kTB + t] = m[r];
+        __syncthreads();
+      }
+    }
+    int flags = 0;
+    Top5 tp;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) tp.k[k] = ~0ull;
+    int cnt = 0;
+    if (act) {
+      if (staged) {   // the query's 27 fine cells from LDS: lane l takes cells 2 l, 2 l + 1 (a group scan of counts)
+        constexpr int NC = NB * NB * NB;
+        int lc[2], lo2[2], ln[2];
+        int local = 0;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int c = 2 * lane + u;
+          lc[u] = 0; lo2[u] = 0; ln[u] = 0;
+          if (c < NC) {
+            const int fx = lx + c % NB, fy = ly + (c / NB) % NB, fz = lz + c / (NB * NB);
+            const int bc = (fx - bx0) + DX * ((fy - by0) + DY * (fz - bz0));
+            lo2[u] = s_fo[bc];
+            ln[u] = s_fo[bc + 1] - lo2[u];
+            lc[u] = local;
+            local += ln[u];
+          }
+        }
+        const int inc = group_incl_scan<G>(local, lane);
+        const int ex = inc - local;
+        const int tot = __shfl(inc, G - 1, G);
+        int* pre = s_pre;   // this group's: [c] prefix, and s_start[c] its LDS offset
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+          if (2 * lane + u < NC) {
+            pre[2 * lane + u] = ex + lc[u];
+            s_start[2 * lane + u] = lo2[u];
+          }
+        if (lane == 0) pre[NC] = tot;
+        wave_lds_order();
+        int c = 0, c_lo = 0, c_hi = pre[1], c_start = s_start[0];
+        for (int tt = lane; tt < tot; tt += G) {
+          while (tt >= c_hi) {
+            ++c;
+            c_lo = c_hi;
+            c_hi = pre[c + 1];
+            c_start = s_start[c];
+          }
+          const float4 mm = s_pts[c_start + (tt - c_lo)];
+          float dd = 0.0f;   // flann::L2_Simple<float>: ((0 + dx*dx) + dy*dy) + dz*dz
+          float df = wx - mm.x;
+          dd += df * df;
+          df = wy - mm.y;
+          dd += df * df;
+          df = wz - mm.z;
+          dd += df * df;
+          if (dd < 1.0f) {
+            ++cnt;
+            top5_insert(tp, ((unsigned long long)__float_as_uint(dd) << 32) | (unsigned)__float_as_int(mm.w));
+          }
+        }
+        wave_lds_order();
+      } else {
+        stencil_scan<G, U, false, NB>(A, lx, lx + NB - 1, ly, ly + NB - 1, lz, lz + NB - 1, wx, wy, wz, lane, s_pre,
+                                      s_start, tp, cnt, s_cc);
+      }
+      group_merge<G>(tp, cnt);
+      const float b = fminf(fminf(fminf(wx - 0.5f * (float)lx, 0.5f * (float)(lx + NB) - wx),
+                                  fminf(wy - 0.5f * (float)ly, 0.5f * (float)(ly + NB) - wy)),
+                            fminf(wz - 0.5f * (float)lz, 0.5f * (float)(lz + NB) - wz));
+      const bool complete = cnt >= 5 && __uint_as_float((unsigned)(tp.k[4] >> 32)) < b * b;
+      if (!complete) {   // stage 2 exactly as knn_group
+        double r = 1.0;
+        if (cnt >= 5) r = fmin(1.0, sqrt((double)__uint_as_float((unsigned)(tp.k[4] >> 32))) * (1.0 + 1e-6));
+#pragma unroll
+        for (int k = 0; k < 5; ++k) tp.k[k] = ~0ull;
+        cnt = 0;
+        stencil_scan<G, U, true>(A, (int)floor((double)wx - r), (int)floor((double)wx + r),
+                                 (int)floor((double)wy - r), (int)floor((double)wy + r),
+                                 (int)floor((double)wz - r), (int)floor((double)wz + r), wx, wy, wz, lane, s_pre,
+                                 s_start, tp, cnt);
+        group_merge<G>(tp, cnt);
+        flags |= 2;
+      }
+      if (cnt >= 5) {   // sqd[4] < 1 (:154, :210)
+        flags |= 1;
+        if (lane < 5) {   // lane k writes the coordinates of neighbour k
+          unsigned long long kk = tp.k[0];
+#pragma unroll
+          for (int k = 1; k < 5; ++k)
+            if (lane == k) kk = tp.k[k];
+          const float4 mm = A.map[(int)(kk & 0xFFFFFFFFull)];
+          A.nnxyz[(3 * lane + 0) * A.cap + i] = mm.x;
+          A.nnxyz[(3 * lane + 1) * A.cap + i] = mm.y;
+          A.nnxyz[(3 * lane + 2) * A.cap + i] = mm.z;
+          if (A.nnidx) {
+            A.nnidx[lane * A.cap + i] = (int)(kk & 0xFFFFFFFFull);
+            A.nnsqd[lane * A.cap + i] = __uint_as_float((unsigned)(kk >> 32));
+          }
+        }
+      }
+    }
+    if (i < n && lane == 0) A.valid[i] = (uint8_t)flags;
+    __syncthreads();   // (the staging arrays are rewritten next round)
+  }
+}
+
+template <int G, int U>
+__global__ __launch_bounds__(kTB) void knn_kernel_lds(LMState* __restrict__ st, const double* __restrict__ x0_dev,
+                                                       CorrArgs E, CorrArgs S, int nbE, const int* __restrict__ d_me,
+                                                       const int* __restrict__ d_ms, int rank, int world) {
+  __shared__ int s_pre[kTB / G][kMaxStencil + 1];
+  __shared__ int s_start[kTB / G][kMaxStencil];
+  __shared__ int s_cc[kTB / G][8 * 9];
+  const int lane = threadIdx.x & (G - 1);
+  const int g = threadIdx.x / G;
+  double pose[7];
 #pragma unroll
   for (int k = 0; k < 7; ++k) {
     const long long b = __double_as_longlong(x0_dev ? x0_dev[k] : st->x[k]);
@@ -907,10 +1188,7 @@ __global__ __launch_bounds__(kTB, W) void knn_kernel(LMState* __restrict__ st, c
     for (int k = 0; k < 7; ++k) xs.v[k] = pose[k];
     lm_reset(st, xs);
   }
-  const bool gate = *d_me > 10 && *d_ms > 50;   // map-size gate (odomEstimationClass.cpp:77)
-  // XCD-aware placement: the blocks that hold queries are renumbered so that the blocks sharing an XCD (physical
-  // index mod 8 under round-robin dispatch) take consecutive query ranges.  The queries are in voxel order, so each
-  // XCD then works on a compact slab of the scene and its L2 holds that slab's map cells instead of all of them.
+  const bool gate = *d_me > 10 && *d_ms > 50;
   const bool edge = (int)blockIdx.x < nbE;
   const CorrArgs& A = edge ? E : S;
   const int nb = edge ? nbE : (int)gridDim.x - nbE;
@@ -918,8 +1196,8 @@ __global__ __launch_bounds__(kTB, W) void knn_kernel(LMState* __restrict__ st, c
   const int nq = min(*A.d_n, A.n_ub);
   const int nact = min(nb, (int)(((long long)nq * G + kTB - 1) / kTB));
   if (p < nact) p = xcd_block(p, nact);
-  knn_group<G, U, NB, STOP>(pose, A, (p * kTB + (int)threadIdx.x) / G, nb * (kTB / G), lane, gate, rank, world,
-                            s_pre[g], s_start[g], s_cc[g]);
+  knn_group_lds<G, U>(pose, A, p * (kTB / G), nb * (kTB / G), lane, g, gate, rank, world, s_pre[g], s_start[g],
+                      s_cc[g]);
 }
 
 // Pass 2: line / plane geometry, one query per lane (all 64 lanes busy), in R = double (the reference's precision)
@@ -1076,9 +1354,9 @@ __device__ __forceinline__ void gram_pair(int e, int& i, int& j) {   // upper-tr
 // partial Gram matrix of its accepted surf records (waves stage w in LDS, lane e sums entry e over the wave's 64
 // records in lane order, waves combined in order) into gpart[block][91].
 template <typename R>
-__global__ __launch_bounds__(kTB) void geom_kernel(LMState* __restrict__ st, CorrArgs E, CorrArgs S, int nbE,
-                                                   double* __restrict__ gpart, double* __restrict__ gmat,
-                                                   unsigned* __restrict__ gcnt) {
+__device__ __forceinline__ void geom_block(LMState* __restrict__ st, const CorrArgs& E, const CorrArgs& S, int nbE,
+                                           int blk, double* __restrict__ gpart, double* __restrict__ gmat,
+                                           unsigned* __restrict__ gcnt) {
 #ifdef FLOAM_GEOM_STAMPS
   GEOM_STAMP(t0, 0);
   unsigned long long tq[2] = {t0, t0};
@@ -1086,14 +1364,14 @@ __global__ __launch_bounds__(kTB) void geom_kernel(LMState* __restrict__ st, Cor
 #else
 #define GEOM_TQ
 #endif
-  if ((int)blockIdx.x < nbE) {
-    geom_query<true, R>(st, E, blockIdx.x * blockDim.x + threadIdx.x, nullptr, nullptr GEOM_TQ);
+  if (blk < nbE) {
+    geom_query<true, R>(st, E, blk * (int)blockDim.x + (int)threadIdx.x, nullptr, nullptr GEOM_TQ);
 #ifdef FLOAM_GEOM_STAMPS
     geom_row(t0, tq[0], tq[1], tq[1], tq[1], 0);
 #endif
     return;
   }
-  const int sb = (int)blockIdx.x - nbE;
+  const int sb = blk - nbE;
   const int ns = min(*S.d_n, S.n_ub);   // the device count bounds the grid-stride loops (block-uniform)
   if (!gpart) {
     for (int i0 = sb * kTB; i0 < ns; i0 += kSurfGeomBlocks * kTB) geom_query<false, R>(st, S, i0 + threadIdx.x);
@@ -1184,6 +1462,94 @@ __global__ __launch_bounds__(kTB) void geom_kernel(LMState* __restrict__ st, Cor
 #endif
 }
 #undef GEOM_TQ
+
+template <typename R>
+__global__ __launch_bounds__(kTB) void geom_kernel(LMState* __restrict__ st, CorrArgs E, CorrArgs S, int nbE,
+                                                   double* __restrict__ gpart, double* __restrict__ gmat,
+                                                   unsigned* __restrict__ gcnt) {
+  geom_block<R>(st, E, S, nbE, (int)blockIdx.x, gpart, gmat, gcnt);
+}
+
+#ifdef FLOAM_DIAG
+// ----------------------------------------------------------------------------------- role-split prototype (r05 item 2)
+// The search and the geometry fits in ONE launch (diagnostic build, FLOAM_KNN_SPLIT=1): every block takes a ticket
+// at its start; tickets [0, nbK) run the search blocks of knn_kernel, the later ones the geometry blocks of
+// geom_kernel, each after polling the completion count of the 256 queries it fits (sctl[1 + chunk]: edge chunks
+// first, then surf).  A geometry block only waits on search blocks with smaller tickets, which are already running,
+// so the launch cannot deadlock (the lookbacks' argument).  Hand-off (MI355X_MICROARCH.md, valid forms):
+// the search block's plain stores -> every wave's vmcnt(0) -> barrier -> one lane's agent release fence -> vmcnt(0) ->
+// relaxed agent adds to the chunk counters; the geometry block: relaxed polls -> agent acquire -> vmcnt(0) -> barrier.
+// The LM reset of ticket 0 is published the same way (sctl[kSplitResetWord] = epoch) before any geometry block counts
+// correspondences.  The kernel is allocated the geometry's registers, so the search runs at the occupancy those allow.
+constexpr int kSplitResetWord = 1;
+constexpr int kSplitChunk0 = 2;
+template <typename R>
+__global__ __launch_bounds__(kTB) void knn_geom_split(LMState* __restrict__ st, const double* __restrict__ x0_dev,
+                                                      CorrArgs E, CorrArgs S, int nbE, int nbK, int gE,
+                                                      const int* __restrict__ d_me, const int* __restrict__ d_ms,
+                                                      int rank, int world, double* __restrict__ gpart,
+                                                      double* __restrict__ gmat, unsigned* __restrict__ gcnt,
+                                                      unsigned* __restrict__ sctl, unsigned epoch) {
+  constexpr int G = kGroupDefault;
+  __shared__ int s_t;
+  if (threadIdx.x == 0) s_t = (int)atomicAdd(&sctl[0], 1u);
+  __syncthreads();
+  const int t = s_t;
+  if (t == (int)gridDim.x - 1 && threadIdx.x == 0) sctl[0] = 0u;   // every ticket taken: ready for the next launch
+  if (t < nbK) {
+    knn_block<G, kUnrollDefault, 3>(st, x0_dev, E, S, nbE, nbK, t, d_me, d_ms, rank, world);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (t == 0) __hip_atomic_store(&sctl[kSplitResetWord], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // the chunks this block's rounds covered (knn_block's query mapping)
+      const bool edge = t < nbE;
+      const CorrArgs& A = edge ? E : S;
+      const int nb = edge ? nbE : nbK - nbE;
+      int p = edge ? t : t - nbE;
+      const int nq = min(*A.d_n, A.n_ub);
+      const int nact = min(nb, (int)(((long long)nq * G + kTB - 1) / kTB));
+      if (p < nact) p = xcd_block(p, nact);
+      const int ngroups = nb * (kTB / G);
+      for (int i0 = 0; i0 < nq; i0 += ngroups) {
+        const int q = i0 + p * (kTB / G);
+        if (q >= nq) break;
+        atomicAdd(&sctl[kSplitChunk0 + (edge ? 0 : gE) + q / kTB], 1u);
+      }
+    }
+    return;
+  }
+  const int gb = t - nbK;   // geometry block
+  const bool edge = gb < gE;
+  const CorrArgs& A = edge ? E : S;
+  const int nq = min(*A.d_n, A.n_ub);
+  if (threadIdx.x == 0) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    bool ok = true;
+    while (__hip_atomic_load(&sctl[kSplitResetWord], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) { ok = false; break; }   // 1 s (never expected)
+      __builtin_amdgcn_s_sleep(2);
+    }
+    // the chunks of this block: edge chunk gb; surf chunks sb, sb + kSurfGeomBlocks, ...
+    const int c0 = edge ? gb : gb - gE, cstep = edge ? 1 << 30 : kSurfGeomBlocks;
+    for (int c = c0; ok && c * kTB < nq; c += cstep) {
+      const unsigned need = (unsigned)((min(nq, (c + 1) * kTB) - c * kTB + G - 1) / G);
+      unsigned* w = &sctl[kSplitChunk0 + (edge ? 0 : gE) + c];
+      while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) { ok = false; break; }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      *w = 0u;   // (the only consumer: zero for the next launch, ordered by the kernel boundary)
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  geom_block<R>(st, E, S, gE, gb, gpart, gmat, gcnt);
+}
+#endif
 
 // Algorithmic traffic of one launch of the search kernel (knn_kernel; SURVEY.md §8 d): every map
 // cell any query scans is streamed once (16 B per map point: the union over queries of the fine 3x3x3 block around
@@ -1562,13 +1928,55 @@ void knn_launch(LMState* d_st, const double* x0_dev, const QuerySet& qe, const G
   const int nS = qs.grid_hint > 0 ? std::min(qs.grid_hint, qs.n_ub) : qs.n_ub;
   const unsigned nbE = std::min(div_up((size_t)std::max(nE, 1) * G, kTB), 4096u);
   const unsigned nbS = std::min(div_up((size_t)std::max(nS, 1) * G, kTB), 8192u);
-  if (ev0 || ev1)
-    hipExtLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6, 3>), dim3(nbE + nbS), dim3(kTB), 0, st, ev0, ev1, 0,
+  // (diagnostic, FLOAM_KNN_LDS_PAD=bytes: dynamic LDS that caps the blocks per CU — the search at the occupancy a
+  // launch that also ran the geometry fits would have: 118 VGPRs -> 4 waves per SIMD = 40 KB of LDS a block)
+  static const unsigned pad = FLOAM_DIAG_ENV("FLOAM_KNN_LDS_PAD") ? (unsigned)std::atoi(FLOAM_DIAG_ENV("FLOAM_KNN_LDS_PAD")) : 0u;
+  static const bool lds = FLOAM_DIAG_ENV("FLOAM_KNN_LDS") != nullptr;   // (diagnostic: the LDS-staged stage 1)
+  if (lds)
+    hipExtLaunchKernelGGL((knn_kernel_lds<G, kUnrollDefault>), dim3(nbE + nbS), dim3(kTB), 0, st, ev0, ev1, 0,
+                          d_st, x0_dev, E, S, (int)nbE, d_me, d_ms, rank, world);
+  else if (ev0 || ev1)
+    hipExtLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6, 3>), dim3(nbE + nbS), dim3(kTB), pad, st, ev0, ev1, 0,
                           d_st, x0_dev, E, S, (int)nbE, d_me, d_ms, rank, world);
   else
-    hipLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6, 3>), dim3(nbE + nbS), dim3(kTB), 0, st, d_st, x0_dev, E, S,
+    hipLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6, 3>), dim3(nbE + nbS), dim3(kTB), pad, st, d_st, x0_dev, E, S,
                        (int)nbE, d_me, d_ms, rank, world);
   FLOAM_LAUNCH_CHECK();
+}
+
+bool knn_geom_split_launch(LMState* d_st, const double* x0_dev, const QuerySet& qe, const Grid& ge, CorrSet& ce,
+                           const QuerySet& qs, const Grid& gs, CorrSet& cs, const int* d_me, const int* d_ms,
+                           int rank, int world, bool gram, bool fp32, LMBuffers& b, hipStream_t st, hipEvent_t ev0,
+                           hipEvent_t ev1) {
+#ifdef FLOAM_DIAG
+  static const bool on = FLOAM_DIAG_ENV("FLOAM_KNN_SPLIT") != nullptr;
+  if (!on || fp32 || qe.n_ub <= 0 || qs.n_ub <= 0) return false;
+  constexpr int G = kGroupDefault;
+  CorrArgs E, S;
+  corr_args(qe, ge, ce, qs, gs, cs, E, S);
+  const int nE = qe.grid_hint > 0 ? std::min(qe.grid_hint, qe.n_ub) : qe.n_ub;
+  const int nS = qs.grid_hint > 0 ? std::min(qs.grid_hint, qs.n_ub) : qs.n_ub;
+  const unsigned nbE = std::min(div_up((size_t)std::max(nE, 1) * G, kTB), 4096u);
+  const unsigned nbS = std::min(div_up((size_t)std::max(nS, 1) * G, kTB), 8192u);
+  const unsigned gE = div_up(std::max(qe.n_ub, 1), kTB);
+  const int chunks = 2 + (int)gE + (int)div_up(std::max(qs.n_ub, 1), kTB);
+  static DevBuf<unsigned> sctl;   // (one prototype launch in flight per process: the diagnostic measurements)
+  static unsigned epoch = 0;
+  if ((size_t)chunks > sctl.cap) {
+    sctl.reserve((size_t)chunks);
+    FLOAM_HIP(hipMemsetAsync(sctl.p, 0, sizeof(unsigned) * sctl.cap, st));
+  }
+  if (gram) b.reserve(st);
+  hipExtLaunchKernelGGL(knn_geom_split<double>, dim3(nbE + nbS + gE + kSurfGeomBlocks), dim3(kTB), 0, st, ev0, ev1, 0,
+                        d_st, x0_dev, E, S, (int)nbE, (int)(nbE + nbS), (int)gE, d_me, d_ms, rank, world,
+                        gram ? b.gpart.p : nullptr, gram ? b.gmat.p : nullptr, b.gcnt.p, sctl.p, ++epoch);
+  FLOAM_LAUNCH_CHECK();
+  return true;
+#else
+  (void)d_st; (void)x0_dev; (void)qe; (void)ge; (void)ce; (void)qs; (void)gs; (void)cs; (void)d_me; (void)d_ms;
+  (void)rank; (void)world; (void)gram; (void)fp32; (void)b; (void)st; (void)ev0; (void)ev1;
+  return false;
+#endif
 }
 
 void geom_launch(LMState* d_st, const QuerySet& qe, CorrSet& ce, const QuerySet& qs, CorrSet& cs, bool gram,

@@ -288,6 +288,12 @@ void deskew_bridge_launch(const LMState* st, OdomDev* s, double scan_period, Poi
 void knn_launch(LMState* d_st, const double* x0_dev, const QuerySet& qe, const Grid& ge, CorrSet& ce,
                 const QuerySet& qs, const Grid& gs, CorrSet& cs, const int* d_me, const int* d_ms, int rank, int world,
                 hipStream_t st, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
+// (diagnostic build, FLOAM_KNN_SPLIT=1) the role-split prototype: knn_launch + geom_launch as ONE launch (search
+// blocks, then geometry blocks that wait for their queries' search); false (nothing launched) when off or fp32
+bool knn_geom_split_launch(LMState* d_st, const double* x0_dev, const QuerySet& qe, const Grid& ge, CorrSet& ce,
+                           const QuerySet& qs, const Grid& gs, CorrSet& cs, const int* d_me, const int* d_ms,
+                           int rank, int world, bool gram, bool fp32, LMBuffers& b, hipStream_t st,
+                           hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 // gram: the squared-loss solves' surf Gram matrix of the accepted surf records into b.gmat (b.gpart's partials)
 void geom_launch(LMState* d_st, const QuerySet& qe, CorrSet& ce, const QuerySet& qs, CorrSet& cs, bool gram,
                  bool fp32, LMBuffers& b, hipStream_t st);

@@ -61,8 +61,14 @@ __global__ __launch_bounds__(kTB) void vox_keys(VoxelJobDev A, VoxelJobDev B, co
     pv[u] = threadIdx.x < 6 * 32 ? partials[(job * kMinMaxBlocks + l + 32 * u) * 6 + c] : 0.f;
   // the first element of this thread: a chunk of kTB x kAppendR per block with the bucket append, else a grid stride
   const int i0 = blockIdx.x * blockDim.x * (bd.split ? kAppendR : 1) + threadIdx.x;
-  PointRec p0;
-  if (i0 < J.n0_ub) p0 = J.part0[i0];
+  // (the bucket append: the kAppendR first-part records of this thread's first chunk, element i0 + r kTB)
+  float4 p0[kAppendR];
+#pragma unroll
+  for (int r = 0; r < kAppendR; ++r) {
+    const int i = i0 + r * kTB;
+    p0[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if ((r == 0 || bd.split) && i < J.n0_ub) p0[r] = *reinterpret_cast<const float4*>(&J.part0[i].x);
+  }
   const unsigned long long sp_t = bucket_split_prefetch(bd.split);   // (the splitters, bucket_keys_lds)
   if (!gv) return;
   __shared__ float s_mm[6];
@@ -97,18 +103,19 @@ __global__ __launch_bounds__(kTB) void vox_keys(VoxelJobDev A, VoxelJobDev B, co
   if (job == 0 && blockIdx.x == 0 && threadIdx.x == 0) *n_dev = nA0 + nA1 + nB0 + nB1;
   __shared__ uint32_t s_spl[kBuckets];
   const bool bucket = vox_bucket_begin(bd, sp_t, job, g, mx[2], J.inv, s_spl);
-  auto key_of = [&](int i) {   // element i's sort key (0xFFFFFFFF: none / dropped)
-    PointRec p;
+  // element i's sort key (0xFFFFFFFF: none / dropped); pre: its first-part record prefetched
+  auto key_of = [&](int i, bool pre, float4 pr) {
+    float4 q;   // (x, y, z, intensity: no PointRec temporary)
     bool in;
-    if (i == i0 && i < n0 && !J.pose) {   // the prefetched record (no transform, no crop: vox_fetch's first part)
-      p = p0;
+    if (pre && i < n0 && !J.pose) {   // the prefetched record (no transform, no crop: vox_fetch's first part)
+      q = pr;
       in = true;
     } else {
-      in = vox_fetch(J, n0, n1, i, p);
+      in = vox_fetch4(J, n0, n1, i, q);
     }
     if (!in) return 0xFFFFFFFFu;
     // index overflow: output = input unchanged (Q9): identity order, one "voxel" per point
-    const uint32_t idx = g.overflow ? (uint32_t)i : voxel_idx(g, J.inv, p);
+    const uint32_t idx = g.overflow ? (uint32_t)i : voxel_idx(g, J.inv, q.x, q.y, q.z);
     return ((uint32_t)job << 31) | idx;
   };
   if (bucket) {   // appended to the buckets' regions: no keys array, no scatter pass
@@ -118,7 +125,7 @@ __global__ __launch_bounds__(kTB) void vox_keys(VoxelJobDev A, VoxelJobDev B, co
 #pragma unroll
       for (int r = 0; r < kAppendR; ++r) {
         const int i = c0 + r * kTB + (int)threadIdx.x;
-        key[r] = i < n0 + n1 ? key_of(i) : 0xFFFFFFFFu;
+        key[r] = i < n0 + n1 ? key_of(i, i == i0 + r * kTB, p0[r]) : 0xFFFFFFFFu;
         val[r] = i;
       }
       bucket_append<kAppendR>(bd, radix_ctl, s_spl, key, val, s_hist, reinterpret_cast<int*>(s_hist + kBuckets),
@@ -127,7 +134,7 @@ __global__ __launch_bounds__(kTB) void vox_keys(VoxelJobDev A, VoxelJobDev B, co
     return;
   }
   for (int i = i0; i < n0 + n1; i += gridDim.x * blockDim.x) {
-    const uint32_t key = key_of(i);
+    const uint32_t key = key_of(i, i == i0, p0[0]);
     keys[base + i] = key;
     vals[base + i] = i;
     radix_hist_add(s_hist, key);

@@ -14,8 +14,10 @@ VARIANTS = {"merge": {}, "voxelgrid": {"FLOAM_MAP_MERGE": "0"},
             # the merge pipeline forced onto its full-sort path
             "full": {"FLOAM_MAP_FULL": "1"},
             # every other merge reports its keys out of order: the next update takes the full sort, then merges again
-            "fallback": {"FLOAM_MM_VIOLATE": "2"}}
-DIAG_VARIANTS = ("full", "fallback")
+            "fallback": {"FLOAM_MM_VIOLATE": "2"},
+            # 512-element merge tiles (twice the tile edges for runs, cropped-point runs included, to cross)
+            "tiles512": {"FLOAM_MM_PER": "2"}}
+DIAG_VARIANTS = ("full", "fallback", "tiles512")
 
 
 def _params(R):
@@ -84,6 +86,7 @@ def test_merge_equals_full_voxelgrid(floam_gpu, monkeypatch, prefilled_map, conf
     _same(runs["merge"], runs["full"], f"{config} merge vs full")
     _same(runs["merge"], runs["voxelgrid"], f"{config} merge vs whole-map VoxelGrid")
     _same(runs["merge"], runs["fallback"], f"{config} merge vs merge with full-sort fallbacks")
+    _same(runs["merge"], runs["tiles512"], f"{config} merge vs merge with 512-element tiles")
 
 
 def test_merge_after_skipped_keyframe(floam_gpu, monkeypatch):
@@ -203,7 +206,7 @@ def test_merge_crops_map_points(floam_gpu, monkeypatch, prefilled_map):
     prefill, xslab, yslab = _c2_crop_prefill(prefilled_map)
     nscan = 20
     variant = "merge"
-    runs = {v: _run(floam_gpu, monkeypatch, v, "c2", nscan, prefill) for v in (variant, "voxelgrid")}
+    runs = {v: _run(floam_gpu, monkeypatch, v, "c2", nscan, prefill) for v in (variant, "voxelgrid", "tiles512")}
     assert sum(r[3] for r in runs[variant]) >= 10, "too few keyframes to exercise the merge"
     for (_, e, s, _) in runs[variant]:
         for m in (e, s):
@@ -213,3 +216,4 @@ def test_merge_crops_map_points(floam_gpu, monkeypatch, prefilled_map):
     assert np.count_nonzero(e_last["x"] < -97.8) < xslab.size // 4, "the x slab was not cropped"
     assert np.count_nonzero(e_last["y"] < -99.8) < yslab.size // 2, "the y slab was not cropped"
     _same(runs[variant], runs["voxelgrid"], f"c2 cropping slabs {variant} vs whole-map VoxelGrid")
+    _same(runs["tiles512"], runs["voxelgrid"], "c2 cropping slabs, 512-element merge tiles, vs whole-map VoxelGrid")

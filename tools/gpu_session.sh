@@ -4,6 +4,7 @@
 #   smoke          __graft_entry__.smoke()
 #   bench[=ARGS]   python bench.py ARGS (comma-separated), the JSON line to $OUT/bench.json
 #   prof[=ARGS]    tools/gpu_prof.sh: bench + rocprofv3 kernel-trace stats + FETCH_SIZE / WRITE_SIZE passes
+#   proj           tools/gpu_projection.sh: per-rank compute of the sharded mode at C4 / C5, N = 1, 2, 4, 8
 #   n2             tools/gpu_n2.sh: the N = 2 bench line rehearsed with two ranks on this one GPU
 #   stamps         tools/gpu_stamps.sh: the LM solve's segment stamps (diagnostic build)
 #   sweep=CONFIG   tools/precision_sweep.py: fp64 / fp32 / fp32-geometry poses against the oracle (8 scans)
@@ -34,6 +35,7 @@ for step in "$@"; do
       cut -c1-600 $OUT/bench.json ;;
     prof) bash tools/gpu_prof.sh ${TAG}/prof ${arg//,/ } || exit $? ;;
     n2) bash tools/gpu_n2.sh ${TAG}/n2 || exit $? ;;
+    proj) bash tools/gpu_projection.sh ${TAG}/proj || exit $? ;;
     stamps) bash tools/gpu_stamps.sh ${TAG}/stamps || exit $? ;;
     sweep)
       timeout -k 10 600 python tools/precision_sweep.py --config ${arg:-c5} --scans 8 --out $OUT/precision_${arg:-c5}.json \
