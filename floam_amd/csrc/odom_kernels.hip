@@ -5,6 +5,9 @@
 // Reference: src/odomEstimationClass.cpp:78-79 (kd-tree), :126-135 (pointAssociateToMap), :144-196
 // (addEdgeCostFactor), :198-251 (addSurfCostFactor), :57-124 (updatePointsToMap control), :320-343 (KeyFrameUpdate).
 #include <cfloat>
+#include <chrono>
+#include <cstring>
+#include <thread>
 #include <cstdlib>
 #include <climits>
 
@@ -1474,28 +1477,37 @@ __global__ __launch_bounds__(kTB) void geom_kernel(LMState* __restrict__ st, Cor
 // ----------------------------------------------------------------------------------- role-split prototype (r05 item 2)
 // The search and the geometry fits in ONE launch (diagnostic build, FLOAM_KNN_SPLIT=1): every block takes a ticket
 // at its start; tickets [0, nbK) run the search blocks of knn_kernel, the later ones the geometry blocks of
-// geom_kernel, each after polling the completion count of the 256 queries it fits (sctl[1 + chunk]: edge chunks
+// geom_kernel, each after polling the completion count of the 256 queries it fits (sctl[kSplitChunk0 + chunk]: edge chunks
 // first, then surf).  A geometry block only waits on search blocks with smaller tickets, which are already running,
 // so the launch cannot deadlock (the lookbacks' argument).  Hand-off (MI355X_MICROARCH.md, valid forms):
 // the search block's plain stores -> every wave's vmcnt(0) -> barrier -> one lane's agent release fence -> vmcnt(0) ->
 // relaxed agent adds to the chunk counters; the geometry block: relaxed polls -> agent acquire -> vmcnt(0) -> barrier.
 // The LM reset of ticket 0 is published the same way (sctl[kSplitResetWord] = epoch) before any geometry block counts
 // correspondences.  The kernel is allocated the geometry's registers, so the search runs at the occupancy those allow.
-constexpr int kSplitResetWord = 1;
-constexpr int kSplitChunk0 = 2;
+// sctl: [0] the ticket, [32] the reset word, [64 + chunk] the completion counts — each on lines of its own, and every
+// access atomic (agent scope: sc1).  A plain store or load of one of these lines leaves it in that XCD's L2, where the
+// sc1 polls of that XCD's blocks then keep reading the stale copy (the first form of this prototype did so, saw no
+// completion and went on with the fits of stale flags).
+constexpr int kSplitResetWord = 32;
+constexpr int kSplitChunk0 = 64;
 template <typename R>
 __global__ __launch_bounds__(kTB) void knn_geom_split(LMState* __restrict__ st, const double* __restrict__ x0_dev,
                                                       CorrArgs E, CorrArgs S, int nbE, int nbK, int gE,
                                                       const int* __restrict__ d_me, const int* __restrict__ d_ms,
                                                       int rank, int world, double* __restrict__ gpart,
                                                       double* __restrict__ gmat, unsigned* __restrict__ gcnt,
-                                                      unsigned* __restrict__ sctl, unsigned epoch) {
+                                                      unsigned* __restrict__ sctl, unsigned epoch,
+                                                      unsigned* __restrict__ watch) {
   constexpr int G = kGroupDefault;
+  auto wadd = [&](int k, unsigned v) {   // (watch: host-pinned progress counters, system scope)
+    if (watch) __hip_atomic_fetch_add(&watch[k], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  };
   __shared__ int s_t;
   if (threadIdx.x == 0) s_t = (int)atomicAdd(&sctl[0], 1u);
   __syncthreads();
   const int t = s_t;
-  if (t == (int)gridDim.x - 1 && threadIdx.x == 0) sctl[0] = 0u;   // every ticket taken: ready for the next launch
+  if (t == (int)gridDim.x - 1 && threadIdx.x == 0)   // every ticket taken: ready for the next launch
+    __hip_atomic_store(&sctl[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (t < nbK) {
     knn_block<G, kUnrollDefault, 3>(st, x0_dev, E, S, nbE, nbK, t, d_me, d_ms, rank, world);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1517,7 +1529,9 @@ __global__ __launch_bounds__(kTB) void knn_geom_split(LMState* __restrict__ st, 
         const int q = i0 + p * (kTB / G);
         if (q >= nq) break;
         atomicAdd(&sctl[kSplitChunk0 + (edge ? 0 : gE) + q / kTB], 1u);
+        wadd(1, 1u);
       }
+      wadd(0, 1u);
     }
     return;
   }
@@ -1525,7 +1539,9 @@ __global__ __launch_bounds__(kTB) void knn_geom_split(LMState* __restrict__ st, 
   const bool edge = gb < gE;
   const CorrArgs& A = edge ? E : S;
   const int nq = min(*A.d_n, A.n_ub);
+  __shared__ int s_ok;
   if (threadIdx.x == 0) {
+    wadd(2, 1u);
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     bool ok = true;
     while (__hip_atomic_load(&sctl[kSplitResetWord], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
@@ -1533,20 +1549,34 @@ __global__ __launch_bounds__(kTB) void knn_geom_split(LMState* __restrict__ st, 
       __builtin_amdgcn_s_sleep(2);
     }
     // the chunks of this block: edge chunk gb; surf chunks sb, sb + kSurfGeomBlocks, ...
-    const int c0 = edge ? gb : gb - gE, cstep = edge ? 1 << 30 : kSurfGeomBlocks;
-    for (int c = c0; ok && c * kTB < nq; c += cstep) {
+    const int c0 = edge ? gb : gb - gE;
+    for (int c = c0; ok && c < (nq + kTB - 1) / kTB; c += edge ? (nq + kTB - 1) / kTB : kSurfGeomBlocks) {
       const unsigned need = (unsigned)((min(nq, (c + 1) * kTB) - c * kTB + G - 1) / G);
       unsigned* w = &sctl[kSplitChunk0 + (edge ? 0 : gE) + c];
       while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
         if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) { ok = false; break; }
         __builtin_amdgcn_s_sleep(2);
       }
-      *w = 0u;   // (the only consumer: zero for the next launch, ordered by the kernel boundary)
+      // (the only consumer: zero for the next launch, ordered by the kernel boundary)
+      __hip_atomic_store(w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (!ok) atomicOr(&sctl[kSplitResetWord + 1], 1u);   // (a wait timed out: never expected; the fits are skipped)
+    wadd(ok ? 3 : 4, 1u);
+    if (!ok && watch) {
+      watch[5] = __hip_atomic_load(&sctl[kSplitResetWord], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      watch[6] = epoch;
+      watch[7] = (unsigned)gb;
+      const int c = edge ? gb : gb - gE;
+      if (c < (nq + kTB - 1) / kTB) watch[8] = __hip_atomic_load(&sctl[kSplitChunk0 + (edge ? 0 : gE) + c], __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+      watch[9] = (unsigned)nq;
+    }
+    s_ok = ok;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
+  if (!s_ok) return;   // (block-uniform; never on stale neighbours)
   geom_block<R>(st, E, S, gE, gb, gpart, gmat, gcnt);
 }
 #endif
@@ -1962,14 +1992,31 @@ bool knn_geom_split_launch(LMState* d_st, const double* x0_dev, const QuerySet& 
   const int chunks = 2 + (int)gE + (int)div_up(std::max(qs.n_ub, 1), kTB);
   static DevBuf<unsigned> sctl;   // (one prototype launch in flight per process: the diagnostic measurements)
   static unsigned epoch = 0;
-  if ((size_t)chunks > sctl.cap) {
-    sctl.reserve((size_t)chunks);
+  if ((size_t)(kSplitChunk0 + chunks) > sctl.cap) {
+    sctl.reserve((size_t)(kSplitChunk0 + chunks));
     FLOAM_HIP(hipMemsetAsync(sctl.p, 0, sizeof(unsigned) * sctl.cap, st));
   }
   if (gram) b.reserve(st);
+  // (FLOAM_SPLIT_WATCH=1: host-pinned progress counters, printed every 2 s by a watcher thread — kNN blocks published,
+  // chunk adds, geometry blocks started / passed / timed out, and the words a timed-out block saw)
+  static unsigned* watch = [] {
+    if (!FLOAM_DIAG_ENV("FLOAM_SPLIT_WATCH")) return (unsigned*)nullptr;
+    unsigned* w = nullptr;
+    FLOAM_HIP(hipHostMalloc(reinterpret_cast<void**>(&w), 64 * sizeof(unsigned), hipHostMallocCoherent));
+    std::memset(w, 0, 64 * sizeof(unsigned));
+    std::thread([w] {
+      for (;;) {
+        std::this_thread::sleep_for(std::chrono::seconds(2));
+        std::fprintf(stderr, "[split watch] knn published %u, chunk adds %u, geometry started %u passed %u timed out %u; "
+                     "last timeout: reset word %u epoch %u block %u count %u nq %u\n", w[0], w[1], w[2], w[3], w[4],
+                     w[5], w[6], w[7], w[8], w[9]);
+      }
+    }).detach();
+    return w;
+  }();
   hipExtLaunchKernelGGL(knn_geom_split<double>, dim3(nbE + nbS + gE + kSurfGeomBlocks), dim3(kTB), 0, st, ev0, ev1, 0,
                         d_st, x0_dev, E, S, (int)nbE, (int)(nbE + nbS), (int)gE, d_me, d_ms, rank, world,
-                        gram ? b.gpart.p : nullptr, gram ? b.gmat.p : nullptr, b.gcnt.p, sctl.p, ++epoch);
+                        gram ? b.gpart.p : nullptr, gram ? b.gmat.p : nullptr, b.gcnt.p, sctl.p, ++epoch, watch);
   FLOAM_LAUNCH_CHECK();
   return true;
 #else
