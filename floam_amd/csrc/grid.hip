@@ -145,7 +145,7 @@ __global__ __launch_bounds__(kTB) void grid_scatter(GridJob E, GridJob S) {
       if (k < sub) pos += c.sub[k];
     const float4 p = i == i_first ? p_first : *reinterpret_cast<const float4*>(&J.map[i].x);
     J.pts[pos] = make_float4(p.x, p.y, p.z, __int_as_float(i));
-    J.xyz[i] = make_float4(p.x, p.y, p.z, 0.0f);
+    if (J.xyz) J.xyz[i] = make_float4(p.x, p.y, p.z, 0.0f);
   }
 }
 
@@ -175,10 +175,16 @@ GridClearDev clear_job(const Grid& g) {
 GridJob make_job(Grid& g, const PointRec* map, const int* d_m, int m_ub, size_t map_cap = 0) {
   const int p = g.parity;
   const int spec = (int)std::min<size_t>({(size_t)m_ub, map_cap, g.where.cap});
-  return GridJob{map, d_m, m_ub, spec, g.pts.p, g.coarse.p, g.where.p, g.xyz.p, g.clist[p].p, g.clist[p ^ 1].p,
-                 g.counters.p, p, g.fresh ? 1 : 0, g.bits, g.mask};
+  g.src = map;
+  return GridJob{map, d_m, m_ub, spec, g.pts.p, g.coarse.p, g.where.p, grid_noxyz() ? nullptr : g.xyz.p,
+                 g.clist[p].p, g.clist[p ^ 1].p, g.counters.p, p, g.fresh ? 1 : 0, g.bits, g.mask};
 }
 }  // namespace
+
+bool grid_noxyz() {
+  static const bool on = FLOAM_DIAG_ENV("FLOAM_GRID_NOXYZ") != nullptr;
+  return on;
+}
 
 GridClearDev grid_clear_prepare(Grid& g, int ub, hipStream_t st) {
   reserve_grid(g, std::max(ub, 1));

@@ -529,6 +529,7 @@ struct CorrArgs {
   int bits;                // table size 1 << bits (both tables)
   unsigned mask;
   const float4* map;       // the map's coordinates in its own order (neighbour coordinates by map index)
+  int map_stride;          // float4s per map index: 1 (the grid's xyz copy) or 2 (FLOAM_GRID_NOXYZ: the records)
   double* rec;
   uint8_t* valid;
   float* nnxyz;
@@ -536,6 +537,15 @@ struct CorrArgs {
   float* nnsqd;            // ... and their float squared distances
   int cap;
 };
+
+// a neighbour's coordinates in A.map: the grid's xyz copy (product), or the map records (FLOAM_GRID_NOXYZ, diagnostic)
+__device__ __forceinline__ size_t knn_map_index(const CorrArgs& A, unsigned idx) {
+#ifdef FLOAM_DIAG
+  return (size_t)A.map_stride * idx;
+#else
+  return idx;
+#endif
+}
 
 __device__ __forceinline__ int fine_count(const CorrArgs& A, int fx, int fy, int fz) {
   const unsigned long long key = cell_key(fx >> 1, fy >> 1, fz >> 1);
@@ -868,7 +878,7 @@ __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArg
 #pragma unroll
           for (int k = 1; k < 5; ++k)
             if (lane == k) kk = t.k[k];
-          const float4 m = A.map[(int)(kk & 0xFFFFFFFFull)];
+          const float4 m = A.map[knn_map_index(A, (unsigned)(kk & 0xFFFFFFFFull))];
           A.nnxyz[(3 * lane + 0) * A.cap + i] = m.x;
           A.nnxyz[(3 * lane + 1) * A.cap + i] = m.y;
           A.nnxyz[(3 * lane + 2) * A.cap + i] = m.z;
@@ -1152,7 +1162,7 @@ __device__ __forceinline__ void knn_group_lds(const double (&pose)[7], const Cor
 #pragma unroll
           for (int k = 1; k < 5; ++k)
             if (lane == k) kk = tp.k[k];
-          const float4 mm = A.map[(int)(kk & 0xFFFFFFFFull)];
+          const float4 mm = A.map[knn_map_index(A, (unsigned)(kk & 0xFFFFFFFFull))];
           A.nnxyz[(3 * lane + 0) * A.cap + i] = mm.x;
           A.nnxyz[(3 * lane + 1) * A.cap + i] = mm.y;
           A.nnxyz[(3 * lane + 2) * A.cap + i] = mm.z;
@@ -1937,9 +1947,12 @@ static void corr_args(const QuerySet& qe, const Grid& ge, CorrSet& ce, const Que
                       CorrSet& cs, CorrArgs& E, CorrArgs& S) {
   ce.reserve(std::max(qe.n_ub, 1), EDGE_FIELDS);
   cs.reserve(std::max(qs.n_ub, 1), SURF_FIELDS);
-  E = CorrArgs{qe.pts, qe.d_n, qe.n_ub, ge.pts.p, ge.coarse.p, ge.bits, ge.mask, ge.xyz.p, ce.rec.p,
+  const bool rec = grid_noxyz();   // (diagnostic: neighbour coordinates from the map records, 2 float4s each)
+  E = CorrArgs{qe.pts, qe.d_n, qe.n_ub, ge.pts.p, ge.coarse.p, ge.bits, ge.mask,
+               rec ? reinterpret_cast<const float4*>(ge.src) : ge.xyz.p, rec ? 2 : 1, ce.rec.p,
                ce.valid.p, ce.nnxyz.p, ce.trace ? ce.nnidx.p : nullptr, ce.trace ? ce.nnsqd.p : nullptr, ce.cap};
-  S = CorrArgs{qs.pts, qs.d_n, qs.n_ub, gs.pts.p, gs.coarse.p, gs.bits, gs.mask, gs.xyz.p, cs.rec.p,
+  S = CorrArgs{qs.pts, qs.d_n, qs.n_ub, gs.pts.p, gs.coarse.p, gs.bits, gs.mask,
+               rec ? reinterpret_cast<const float4*>(gs.src) : gs.xyz.p, rec ? 2 : 1, cs.rec.p,
                cs.valid.p, cs.nnxyz.p, cs.trace ? cs.nnidx.p : nullptr, cs.trace ? cs.nnsqd.p : nullptr, cs.cap};
 }
 

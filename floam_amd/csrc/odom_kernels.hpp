@@ -30,7 +30,11 @@ struct Grid {
   int parity = 0;
   bool fresh = true;         // tables (re)allocated: the next clear is a full one
   bool precleared = false;   // the next build's clear was issued in advance (grid_clear_prepare)
+  const PointRec* src = nullptr;   // the map the last build read (FLOAM_GRID_NOXYZ: the neighbour gathers read it)
 };
+// (diagnostic, FLOAM_GRID_NOXYZ=1: the grid build writes no xyz copy and the search gathers the neighbours'
+// coordinates from the map records the grid was built from — VERDICT r05 item 1b's measurement)
+bool grid_noxyz();
 
 // The first step of a grid build — empty the table entries the previous build occupied (its slot list; the whole
 // table after a reallocation) and reset the cursors — as a device job, so that it can run inside an earlier launch
