@@ -944,6 +944,7 @@ __global__ __launch_bounds__(kTB, W) void knn_kernel(LMState* __restrict__ st, c
   knn_block<G, U, NB, STOP>(st, x0_dev, E, S, nbE, (int)gridDim.x, (int)blockIdx.x, d_me, d_ms, rank, world);
 }
 
+#ifdef FLOAM_DIAG
 // ----------------------------------------------------------------------------------- LDS-staged stage 1
 // The north star's "LDS-staged spatial-hash grid", re-measured against the search above (diagnostic build:
 // FLOAM_KNN_LDS=1).  A block's 16 queries (one per 16-lane group, as knn_kernel) are consecutive in voxel order, so
@@ -1212,6 +1213,7 @@ __global__ __launch_bounds__(kTB) void knn_kernel_lds(LMState* __restrict__ st, 
   knn_group_lds<G, U>(pose, A, p * (kTB / G), nb * (kTB / G), lane, g, gate, rank, world, s_pre[g], s_start[g],
                       s_cc[g]);
 }
+#endif
 
 // Pass 2: line / plane geometry, one query per lane (all 64 lanes busy), in R = double (the reference's precision)
 // or float (the C5 sweep's fp32 variant; records are stored as the doubles of the float results).
@@ -1974,11 +1976,14 @@ void knn_launch(LMState* d_st, const double* x0_dev, const QuerySet& qe, const G
   // (diagnostic, FLOAM_KNN_LDS_PAD=bytes: dynamic LDS that caps the blocks per CU — the search at the occupancy a
   // launch that also ran the geometry fits would have: 118 VGPRs -> 4 waves per SIMD = 40 KB of LDS a block)
   static const unsigned pad = FLOAM_DIAG_ENV("FLOAM_KNN_LDS_PAD") ? (unsigned)std::atoi(FLOAM_DIAG_ENV("FLOAM_KNN_LDS_PAD")) : 0u;
-  static const bool lds = FLOAM_DIAG_ENV("FLOAM_KNN_LDS") != nullptr;   // (diagnostic: the LDS-staged stage 1)
+#ifdef FLOAM_DIAG
+  static const bool lds = FLOAM_DIAG_ENV("FLOAM_KNN_LDS") != nullptr;   // (the LDS-staged stage 1, profiles/r06c)
   if (lds)
     hipExtLaunchKernelGGL((knn_kernel_lds<G, kUnrollDefault>), dim3(nbE + nbS), dim3(kTB), 0, st, ev0, ev1, 0,
                           d_st, x0_dev, E, S, (int)nbE, d_me, d_ms, rank, world);
-  else if (ev0 || ev1)
+  else
+#endif
+  if (ev0 || ev1)
     hipExtLaunchKernelGGL((knn_kernel<G, kUnrollDefault, 6, 3>), dim3(nbE + nbS), dim3(kTB), pad, st, ev0, ev1, 0,
                           d_st, x0_dev, E, S, (int)nbE, d_me, d_ms, rank, world);
   else
