@@ -515,7 +515,7 @@ __device__ __forceinline__ bool lm_step(const double (&H)[21], const double (&g)
 }
 
 // -DFLOAM_CTRL_STAMPS (diagnostic build): block 0's control-step segments, s_memrealtime (100 MHz), accumulated by
-// lane 0: [0] steps, [1] bookkeeping before the step, [2] solve_step, [3] se3_plus, [4] gradient test + candidate
+// lane 0: [0] steps, [1] bookkeeping before the step, [2] solve_step, [3] se3_plus, [4] the candidate hand-over
 // broadcast, [5] whole step; printed by lm_ctrl_stamps_print
 #ifdef FLOAM_CTRL_STAMPS
 __device__ unsigned long long g_ctrl_stamps[8];
@@ -587,6 +587,50 @@ __device__ __forceinline__ void pin(double (&v)[N]) {
   for (int k = 0; k < N; ++k) asm volatile("" : "+v"(v[k]));
 }
 
+// The tests of a candidate that read nothing of its evaluation — the gradient-norm test due with the step
+// (max_i |x_i - (x [+] -g)_i| <= 1e-10, the projection in S.proj) and ParameterToleranceReached (|x - cand| <= 1e-8
+// (|x| + 1e-8)) — and |cand|, run by one wave while the candidate is being evaluated instead of between the step and
+// the evaluation (resident solve: wave 0, between its publish and its polls; the per-evaluation launches: at the start
+// of the next control step).  When one ends the solve, the candidate's evaluation is discarded, as if it had not been
+// made (the sequential order skips it; nothing of it enters the state).  Same operands, same order, same bits as the
+// tests inline.
+__device__ __forceinline__ void deferred_tests(LMState& S, int lane) {
+  const int tp = S.tpend;   // (wave-uniform)
+  if (!tp) return;
+  double x[7], c[7], p[7];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    x[k] = S.x[k];
+    c[k] = S.cand[k];
+    p[k] = S.proj[k];
+  }
+  double gm = S.gmax;
+  const double x_norm = S.x_norm;
+  int verdict = 0;
+  if (tp & 2) {
+    double ml = 0.0;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) ml = fmax(ml, fabs(x[i] - p[i]));
+    gm = ml;
+    if (gm <= 1e-10) verdict = 2;
+  }
+  if (!verdict && (tp & 1)) {
+    double sn2 = 0.0;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) sn2 += (x[i] - c[i]) * (x[i] - c[i]);
+    const double ptol = 1e-8 * (x_norm + 1e-8);
+    if (sn2 <= ptol * ptol) verdict = 1;
+  }
+  const double cn = norm7(c);
+  if (lane == 0) {
+    S.gmax = gm;
+    S.cand_norm = cn;
+    S.tdone = verdict;
+    S.tpend = 0;
+  }
+  wave_lds_order();
+}
+
 // One Ceres control step after an evaluation (sums: cost, J^T J, J^T r, count at x in phase 0, else at cand), run by
 // the 64 lanes of one wave on the LM state in LDS.  Every lane reads the same words (LDS broadcast) and computes the
 // same values — but lane 1, which forms the gradient projection of the gradient-norm test beside lane 0's candidate —
@@ -596,8 +640,11 @@ __device__ __forceinline__ void pin(double (&v)[N]) {
 // of its instructions moving the state through the accumulation registers).  The next point is S.cand (every block's
 // evaluation reads it there); S.done ends the solve.  The step itself is NextStep: ComputeTrustRegionStep (lm_step)
 // with HandleInvalidStep's retries, the gradient-norm test folded in.
-__device__ __forceinline__ void control_step(LMState& S, const double* __restrict__ sums, int lane) {
+// tests: the candidate's deferred tests are still to run (the per-evaluation launches; the resident solve ran them
+// during the evaluation).
+__device__ __forceinline__ void control_step(LMState& S, const double* __restrict__ sums, int lane, bool tests) {
   CTRL_T(t0);
+  if (tests) deferred_tests(S, lane);
   // every word the decisions read, loaded together and pinned where they are loaded: one LDS round trip (the compiler
   // otherwise sinks each load into the branch that uses it, a round trip per branch)
   double x[7], c[7], sm[28], lo[6], hi[6];   // sm: cost, H[21], g[6]; lo, hi: the diagonal's clamp bounds
@@ -617,6 +664,7 @@ __device__ __forceinline__ void control_step(LMState& S, const double* __restric
   const double cand_norm = S.cand_norm;
   int iteration = S.iteration, reuse = S.reuse, invalid = S.invalid, successful = S.successful;
   int phase = S.phase;
+  const int tdone = S.tdone;
   pin(x);
   pin(c);
   pin(sm);
@@ -660,8 +708,10 @@ __device__ __forceinline__ void control_step(LMState& S, const double* __restric
       fresh = true;
       check_gmax = true;
     }
+  } else if (tdone) {   // a deferred test of the candidate ended the solve: its evaluation is discarded
+    done = 1;
+    if (tdone == 2) --iteration;   // (the gradient-norm test comes before the step: the step is not counted)
   } else {
-    // (ParameterToleranceReached was decided when the candidate was formed: it does not depend on the evaluation)
     const double cand_cost = isfinite(cost) ? cost : DBL_MAX;
     if (fabs(x_cost - cand_cost) <= 1e-6 * x_cost) {   // FunctionToleranceReached
       done = 1;
@@ -690,7 +740,8 @@ __device__ __forceinline__ void control_step(LMState& S, const double* __restric
   CTRL_T(t1);
   CTRL_ADD(1, t1 - t0);
   bool have_cand = false;
-  double out[7], cand_norm_new = 0.0;
+  int tp = 0;   // the candidate's deferred tests (LMState::tpend)
+  double out[7];
   if (!done) {
     double H[21], g[6], E[6];
     if (fresh) {
@@ -729,8 +780,23 @@ __device__ __forceinline__ void control_step(LMState& S, const double* __restric
       CTRL_T(tc);
       CTRL_ADD(2, tb - ta);
       CTRL_ADD(3, tc - tb);
-      // (wave-uniform) lane 1 computed the projection: it measures its own distance to x, which is read from it (one
-      // read-lane pair); lane 0 writes the candidate
+      if (valid) {   // the candidate goes to its evaluation now, its tests with it (deferred_tests)
+        if (check_gmax) {
+          if (far) gmax = HUGE_VAL;   // (the test fails: only the comparison with the tolerance is used)
+          else tp |= 2;               // lane 1's projection, written with the candidate
+          check_gmax = false;
+        }
+        tp |= 1;
+        iteration++;
+        mcc = m;
+        invalid = 0;
+        have_cand = true;
+        CTRL_T(td);
+        CTRL_ADD(4, td - tc);
+        break;   // candidate pending evaluation
+      }
+      // an invalid step: the gradient-norm test inline, then HandleInvalidStep.  (Wave-uniform) lane 1 computed the
+      // projection: it measures its own distance to x, which is read from it (one read-lane pair)
       if (check_gmax) {
         double gm = HUGE_VAL;   // (far: the test fails; only the comparison with the tolerance is used)
         if (!far) {
@@ -747,25 +813,6 @@ __device__ __forceinline__ void control_step(LMState& S, const double* __restric
         }
       }
       iteration++;
-      if (valid) {
-        mcc = m;
-        invalid = 0;
-        have_cand = true;
-        // ParameterToleranceReached (the candidate not applied): |x - cand| <= 1e-8 (|x| + 1e-8), compared squared
-        // (both sides non-negative).  Ceres tests it after evaluating the candidate, but nothing of the evaluation
-        // enters the test and the solve ends with x unchanged either way, so the evaluation is skipped.  Lane 0 holds
-        // the candidate (lane 1 may hold the projection): its distance and norm are read from it.
-        double sn2 = 0.0;
-#pragma unroll
-        for (int i = 0; i < 7; ++i) sn2 += (x[i] - out[i]) * (x[i] - out[i]);
-        sn2 = bcast(sn2, 0);
-        cand_norm_new = bcast(norm7(out), 0);
-        const double ptol = 1e-8 * (x_norm + 1e-8);
-        if (sn2 <= ptol * ptol) done = 1;
-        CTRL_T(td);
-        CTRL_ADD(4, td - tc);
-        break;   // candidate pending evaluation
-      }
       // HandleInvalidStep -> StepIsInvalid -> StepRejected(0)
       if (++invalid >= 5) {
         done = 1;
@@ -783,6 +830,10 @@ __device__ __forceinline__ void control_step(LMState& S, const double* __restric
       for (int k = 0; k < 6; ++k) S.diag[k] = E[k];
     }
   }
+  if (lane == 1 && (tp & 2)) {   // the projection x [+] -g (lane 1's se3_plus)
+#pragma unroll
+    for (int k = 0; k < 7; ++k) S.proj[k] = out[k];
+  }
   if (lane == 0) {
     if (moved) {
 #pragma unroll
@@ -791,8 +842,8 @@ __device__ __forceinline__ void control_step(LMState& S, const double* __restric
     if (have_cand) {
 #pragma unroll
       for (int k = 0; k < 7; ++k) S.cand[k] = out[k];
-      S.cand_norm = cand_norm_new;
     }
+    S.tpend = tp;
     S.x_cost = x_cost; S.radius = radius; S.dfac = dfac; S.mcc = mcc; S.x_norm = x_norm; S.gmax = gmax;
     S.iteration = iteration; S.reuse = reuse; S.invalid = invalid; S.successful = successful;
     S.phase = phase;
@@ -1105,6 +1156,9 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
         put_granule(&slot[blk * 2 * LM_NSUM + 2 * c + h], granule(tag, h ? (unsigned)(b >> 32) : (unsigned)b));
       }
       t1 = LM_NOW();
+      // the candidate's tests while the granules travel (wave 0, between its publish and its polls; the control step
+      // reads the verdict after the gather's barrier)
+      if (tid < 64) deferred_tests(sst, lane);
       // every active block's granules of this evaluation (this block's own included), summed in block order as they
       // are gathered
       bool bad = false;
@@ -1127,7 +1181,7 @@ __global__ __launch_bounds__(kTB) void lm_solve(LMArgs a) {
       ++nx;
     }
     const unsigned long long t3 = LM_NOW();
-    if (tid < 64) control_step(sst, s_sums, lane);   // the next point (if the solve goes on)
+    if (tid < 64) control_step(sst, s_sums, lane, false);   // the next point (if the solve goes on)
     if (a.dbg && blk == 0) {
       const unsigned long long t4 = LM_NOW();
       tm[0] += t1 - t0; tm[1] += t2 - t1; tm[2] += t3 - t2; tm[3] += t4 - t3;
@@ -1176,7 +1230,7 @@ __global__ __launch_bounds__(kTB) void lm_shard_eval(LMArgs a, int k) {
   if (k > 0 && tid < LM_NSUM) s_sums[tid] = a.sums[tid];   // all-reduced (kernel boundary)
   __syncthreads();
   if (tid < 64) {
-    if (k > 0 && !sst.done) control_step(sst, s_sums, lane);
+    if (k > 0 && !sst.done) control_step(sst, s_sums, lane, true);
     else if (tid < 7 && sst.phase == 0) sst.cand[tid] = sst.x[tid];   // iteration zero evaluates at x
   }
   __syncthreads();
@@ -1243,7 +1297,7 @@ __global__ __launch_bounds__(64) void lm_shard_final(LMState* __restrict__ st, c
   stage_state(st, sst);
   if (threadIdx.x < LM_NSUM) s_sums[threadIdx.x] = sums[threadIdx.x];
   __syncthreads();
-  if (!sst.done) control_step(sst, s_sums, threadIdx.x);
+  if (!sst.done) control_step(sst, s_sums, threadIdx.x, true);
   __syncthreads();
   publish_state(sst, st);
 }
@@ -1287,7 +1341,7 @@ void lm_ctrl_stamps_print() {
   FLOAM_HIP(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_ctrl_stamps), sizeof(h)));
   const double n = h[0] ? (double)h[0] : 1.0;
   std::fprintf(stderr, "[floam ctrl] %llu phase-1 control steps (block 0): bookkeeping %.3f us, solve_step %.3f us, "
-               "se3_plus %.3f us, gradient test + broadcast %.3f us; whole step %.3f us\n", h[0], h[1] / n / 100.0,
+               "se3_plus %.3f us, candidate hand-over %.3f us; whole step %.3f us\n", h[0], h[1] / n / 100.0,
                h[2] / n / 100.0, h[3] / n / 100.0, h[4] / n / 100.0, h[5] / n / 100.0);
 #endif
 }

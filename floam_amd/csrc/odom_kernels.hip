@@ -415,6 +415,8 @@ __device__ __forceinline__ void lm_reset(LMState* st, const X7& x0) {
   st->n_res = 0;
   st->corr_edge = 0;
   st->corr_surf = 0;
+  st->tpend = 0;
+  st->tdone = 0;
   st->radius = 1e4;
   st->dfac = 2.0;
   st->epoch += 8u;   // fresh hand-off tags for this solve's granules (lm.hip)

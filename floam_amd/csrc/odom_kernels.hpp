@@ -122,7 +122,8 @@ struct LMState {
                            // at iteration 0 (lm.hip lm_step)
   double diag[6];     // unscaled LM diagonal (reused after a rejected / invalid step)
   double radius, dfac, mcc, x_norm, gmax, initial_cost;
-  double cand_norm;   // |cand|, formed with the candidate (x_norm once it is accepted)
+  double cand_norm;   // |cand| (x_norm once it is accepted): formed by the candidate's deferred tests
+  double proj[7];     // x [+] -g, the gradient-norm test's projection (deferred tests, lm.hip)
   // the solve's iteration-zero quantities (stage inspection; oracle/odom.cpp SolveTrace): the starting point and the
   // unscaled J^T J and J^T r there
   double x_in[7];
@@ -136,6 +137,10 @@ struct LMState {
   int successful;
   int n_res;
   int corr_edge, corr_surf;   // accepted correspondences (this solve)
+  // the candidate's tests that do not depend on its evaluation, run off the control step's chain (lm.hip
+  // deferred_tests): tpend — pending (bit 0 parameter tolerance, bit 1 gradient norm against proj); tdone — their
+  // verdict (1: parameter tolerance, 2: gradient norm, which also takes back the step's iteration count)
+  int tpend, tdone;
   unsigned epoch;     // hand-off tag base of the resident solve (lm.hip): advanced by 8 per solve (lm_reset)
   // peer sharding: evaluations exchanged with the other ranks since floam_odom_set_shard_peers (continues across
   // solves; lm_reset keeps it): the exchange slot and tag of each evaluation (lm.hip peer_exchange)

@@ -1,6 +1,6 @@
 #!/bin/bash
 # One GPU session (run on the GPU box from the repo root), steps in the order given, stopping at the first failure:
-#   tests[=EXPR]   the -m gpu suite in one process (per-test timeouts; EXPR: a pytest -k expression)
+#   tests[=EXPR]   the -m gpu suite in one process (per-test timeouts; EXPR: a pytest -k expression, commas for spaces)
 #   smoke          __graft_entry__.smoke()
 #   bench[=ARGS]   python bench.py ARGS (comma-separated), the JSON line to $OUT/bench.json
 #   prof[=ARGS]    tools/gpu_prof.sh: bench + rocprofv3 kernel-trace stats + FETCH_SIZE / WRITE_SIZE passes
@@ -21,7 +21,7 @@ for step in "$@"; do
   echo "== $step"
   case $name in
     tests)
-      K=(); [ -n "$arg" ] && K=(-k "$arg")
+      K=(); [ -n "$arg" ] && K=(-k "${arg//,/ }")   # (commas for spaces: "a,or,b")
       timeout -k 10 1500 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${K[@]}" \
           > $OUT/pytest_gpu.log 2>&1; rc=$?
       grep -cE "PASSED" $OUT/pytest_gpu.log; tail -3 $OUT/pytest_gpu.log
