@@ -1503,6 +1503,7 @@ floam_status floam_odom_destroy(floam_odom* o) {
       bucket_stamps_print();
       mm_stamps_print();
       geom_stamps_print();
+      knn_waves_dump();
       lm_ctrl_stamps_print();
       if (o->dbg_stamps.p) {   // FLOAM_DEBUG_STAMPS: the resident solve's segments in block 0 (100 MHz ticks)
         unsigned long long h[10];

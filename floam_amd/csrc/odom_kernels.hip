@@ -895,6 +895,13 @@ __device__ __forceinline__ void knn_group(const double (&pose)[7], const CorrArg
   }
 }
 
+// -DFLOAM_KNN_WAVES (a scratch diagnostic build, tools/gpu_knn_waves.sh): every wave of the latest search launch
+// records its start and end (s_memrealtime, 100 MHz) and its block's role; dumped by knn_waves_dump at handle close
+#ifdef FLOAM_KNN_WAVES
+constexpr int kKnnWaveRows = 16384;
+__device__ unsigned long long g_knn_waves[kKnnWaveRows][2];
+#endif
+
 // Edge and surf kNN in one launch: blocks [0, nbE) run edge groups, the others surf groups.  The launch also starts
 // the solve (lm_init folded in): block 0 resets the LM state and, for the first solve of an update, stores the
 // prediction x0 that every block uses for its transforms (the others never read st->x in that case).
@@ -904,6 +911,9 @@ __device__ __forceinline__ void knn_block(LMState* __restrict__ st, const double
                                           const CorrArgs& E, const CorrArgs& S, int nbE, int nblocks, int blk,
                                           const int* __restrict__ d_me, const int* __restrict__ d_ms, int rank,
                                           int world) {
+#ifdef FLOAM_KNN_WAVES
+  const unsigned long long kw0 = __builtin_amdgcn_s_memrealtime();
+#endif
   __shared__ int s_pre[kTB / G][kMaxStencil + 1];
   __shared__ int s_start[kTB / G][kMaxStencil];
   __shared__ int s_cc[kTB / G][8 * 9];
@@ -936,6 +946,18 @@ __device__ __forceinline__ void knn_block(LMState* __restrict__ st, const double
   if (p < nact) p = xcd_block(p, nact);
   knn_group<G, U, NB, STOP>(pose, A, (p * kTB + (int)threadIdx.x) / G, nb * (kTB / G), lane, gate, rank, world,
                             s_pre[g], s_start[g], s_cc[g]);
+#ifdef FLOAM_KNN_WAVES
+  {   // start | edge << 62 | holds queries << 61 | XCC id << 56 (HW_REG_XCC_ID), end; vector stores by lane 0
+    const unsigned long long kw1 = __builtin_amdgcn_s_memrealtime();
+    const unsigned xcc = (unsigned)__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u;
+    const int w = blk * (kTB / 64) + (int)threadIdx.x / 64;
+    if ((threadIdx.x & 63) == 0 && w < kKnnWaveRows) {
+      g_knn_waves[w][0] = (kw0 & ((1ull << 56) - 1)) | ((unsigned long long)(edge ? 1 : 0) << 62) |
+                          ((unsigned long long)(p < nact ? 1 : 0) << 61) | ((unsigned long long)xcc << 56);
+      g_knn_waves[w][1] = kw1;
+    }
+  }
+#endif
 }
 
 template <int G, int U, int W, int NB, int STOP = 0>
@@ -2071,6 +2093,22 @@ __global__ __launch_bounds__(kTB) void l2_evict(const float4* __restrict__ buf, 
   float acc = 0.f;
   for (size_t i = (size_t)blockIdx.x * kTB + threadIdx.x; i < n; i += (size_t)gridDim.x * kTB) acc += buf[i].x;
   if (acc == 1234.5f) sink[0] = acc;   // (never: keeps the loads)
+}
+
+void knn_waves_dump() {
+#ifdef FLOAM_KNN_WAVES
+  const char* path = std::getenv("FLOAM_KNN_WAVES");
+  if (!path) return;
+  static unsigned long long h[kKnnWaveRows][2];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_knn_waves), sizeof(h)) != hipSuccess) {
+    (void)hipGetLastError();
+    return;
+  }
+  if (FILE* f = std::fopen(path, "wb")) {
+    std::fwrite(h, sizeof(h), 1, f);
+    std::fclose(f);
+  }
+#endif
 }
 
 void geom_stamps_print() {

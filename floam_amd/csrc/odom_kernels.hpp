@@ -75,6 +75,7 @@ struct OdomDev;
 // (nullable): the update's constant-velocity prediction (odom_predict_step) runs in the first of them instead of a
 // launch of its own.
 void geom_stamps_print();   // -DFLOAM_GEOM_STAMPS (diagnostic build)
+void knn_waves_dump();      // -DFLOAM_KNN_WAVES (diagnostic build): FLOAM_KNN_WAVES=path
 void grid_build_launch(Grid& gE, const PointRec* mapE, const int* d_mE, int mE_ub, Grid& gS, const PointRec* mapS,
                        const int* d_mS, int mS_ub, hipStream_t st, OdomDev* predict = nullptr, bool precleared = false,
                        size_t mE_cap = 0, size_t mS_cap = 0);   // caps: the maps' buffer sizes (speculative loads)
